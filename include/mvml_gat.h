@@ -1,0 +1,182 @@
+/*
+ * mvml_gat.h — C ABI of the MI355X-native molecular-graph (GAT) view of MVML-MPI.
+ *
+ * The reference's hot path is GNNModule (model.py:77-95): dgllife GAT (model.py:81,91)
+ * -> dgl Set2Set (model.py:82-84,92) -> PyG GraphNorm, batch=None (model.py:85,93) ->
+ * Linear+ReLU+Dropout (model.py:86-87,94), fed by dgl.batch (dataset.py:52-54) over
+ * mol_to_bigraph(add_self_loop=True) graphs (dataset.py:33-35).  The reference has no FFI of
+ * its own: its operator API is the PyTorch nn.Module API, and the native code it runs is
+ * DGL's C kernels (_CAPI_DGLKernelSpMM / SDDMM / EdgeSoftmax, dgl 0.9.1), torch_scatter
+ * (GraphNorm) and cuBLAS/MKL (Linear, LSTM).  Each entry point below names the reference
+ * operation it replaces; the Python package mvml_gat binds them with ctypes (see
+ * INTEGRATION.md) behind the reference's nn.Module signatures.
+ *
+ * Conventions (all entry points):
+ *  - every pointer is a DEVICE pointer owned by the caller (PyTorch caching allocator);
+ *    the library never allocates or frees device memory.  Scratch comes from a caller-sized
+ *    `workspace` (query the matching *_workspace_size function).
+ *  - `stream` is a hipStream_t passed as void* (NULL = legacy default stream); every call
+ *    only enqueues work on it: no host synchronisation, no allocation, graph-capturable.
+ *  - row-major fp32 tensors; `ld*` are leading dimensions in elements; indices int32 unless
+ *    stated (node/edge offsets int64, as dgl's batch_num_nodes/edges).
+ *  - return 0 on success, nonzero MVML_ERR_* on failure; mvml_last_error() then describes it.
+ *  - deterministic: no floating-point atomics anywhere, results are bitwise reproducible.
+ */
+#ifndef MVML_GAT_H
+#define MVML_GAT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVML_OK 0
+#define MVML_ERR_INVALID 1   /* bad argument / unsupported shape */
+#define MVML_ERR_LAUNCH 2    /* HIP launch or runtime error */
+#define MVML_ERR_WORKSPACE 3 /* workspace too small */
+
+/* Human-readable description of the last error on the calling thread ("" if none). */
+const char* mvml_last_error(void);
+/* Library version string, and the gfx target the kernels were built for. */
+const char* mvml_version(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Batching: dgl.batch (dataset.py:54) + DGL's COO->CSR conversion on first update_all.
+ * Inputs are the per-graph LOCAL edge lists of mol_to_bigraph (dataset.py:34-35) concatenated
+ * in graph order, plus batch_num_nodes/batch_num_edges (int64[B]).  Outputs are bit-exact with
+ * dgl.batch's global src/dst and with a stable counting sort by dst (in-CSR) and by src
+ * (out-CSR).  status_flags (int32[2]): [0] = number of nodes with zero in-degree (GATConv
+ * raises DGLError on those, dgl 0.9.1 GATConv.forward), [1] = number of out-of-range local ids.
+ * ------------------------------------------------------------------------------------- */
+size_t mvml_build_csr_workspace_size(int64_t num_graphs, int64_t num_nodes, int64_t num_edges);
+int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local,
+                   const int64_t* batch_num_nodes, const int64_t* batch_num_edges,
+                   int64_t num_graphs, int64_t num_nodes, int64_t num_edges,
+                   int64_t* node_offsets /* [B+1] */, int64_t* edge_offsets /* [B+1] */,
+                   int32_t* src /* [E] */, int32_t* dst /* [E] */, int32_t* node_graph /* [N] */,
+                   int32_t* in_rowptr /* [N+1] */, int32_t* in_src /* [E] */,
+                   int32_t* in_eid /* [E] */, int32_t* out_rowptr /* [N+1] */,
+                   int32_t* out_dst /* [E] */, int32_t* out_inslot /* [E] */,
+                   int32_t* status_flags /* [2] */, void* workspace, size_t workspace_bytes,
+                   void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Dense fp32 GEMM on CDNA4 MFMA (v_mfma_f32_32x32x2_f32, exact f32 fmaf chains).
+ * C[M,N] = act(A[M,K] * B[K,N] + bias[N] + beta * C)
+ *   a_kmajor = 0: A(m,k) = A[m*lda + k]      a_kmajor = 1: A(m,k) = A[k*lda + m]
+ *   b_kmajor = 0: B(k,n) = B[n*ldb + k]      b_kmajor = 1: B(k,n) = B[k*ldb + n]
+ *   act: 0 none, 1 ReLU.  Replaces nn.Linear / torch.matmul (cuBLAS / rocBLAS) used by
+ *   GATConv.fc/res_fc, Set2Set's nn.LSTM and GNNModule.fc (model.py:86-87).  K is split over
+ *   workgroups when M*N is small (deterministic slab reduction, needs workspace).
+ * ------------------------------------------------------------------------------------- */
+size_t mvml_gemm_workspace_size(int64_t M, int64_t N, int64_t K);
+int mvml_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                  const float* A, int64_t lda, const float* B, int64_t ldb,
+                  const float* bias, float beta, int act, float* C, int64_t ldc,
+                  void* workspace, size_t workspace_bytes, void* stream);
+/* Column sums: out[n] = beta*out[n] + sum_m X[m*ldx + n], deterministic two-stage tree.
+ * Replaces the bias gradients torch autograd computes for GATConv.bias / LSTM / Linear. */
+size_t mvml_colsum_workspace_size(int64_t M, int64_t N);
+int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx, float beta, float* out,
+                    void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * GATConv projection (dgl 0.9.1 GATConv.fc, res_fc, and the el/er reductions
+ * `(feat_src * attn_l).sum(-1)` / `(feat_dst * attn_r).sum(-1)`), folded into ONE GEMM:
+ *   Wcat[C, Fin], C = 2*H*F + 2*H, rows = [fc.weight ; res_fc.weight ; A_l ; A_r] with
+ *   A_l[h,k] = sum_f attn_l[h,f] * fc.weight[h*F+f, k]   (likewise A_r with attn_r)
+ *   Y[N, C] = X[N, Fin] * Wcat^T  =>  Y[:, 0:HF] = Z, Y[:, HF:2HF] = R, Y[:, 2HF:2HF+H] = el,
+ *                                     Y[:, 2HF+H:2HF+2H] = er.
+ * mvml_gat_unfold_grads maps dL/dWcat back onto the four parameters (exact chain rule).
+ * ------------------------------------------------------------------------------------- */
+int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_l,
+                          const float* attn_r, int H, int F, int Fin, float* Wcat, void* stream);
+int mvml_gat_unfold_grads(const float* gWcat, const float* fc_w, const float* attn_l,
+                          const float* attn_r, int H, int F, int Fin, float* g_fc_w,
+                          float* g_res_fc_w, float* g_attn_l, float* g_attn_r, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Fused GAT attention + aggregation, forward (one wavefront per destination atom):
+ *   apply_edges(u_add_v) -> LeakyReLU(slope) -> edge_softmax -> update_all(u_mul_e, sum)
+ *   -> + residual R -> + bias -> GATLayer agg (dgllife 0.3.0): mode 0 flatten+ELU,
+ *   mode 1 mean over heads, mode 2 flatten (no activation).
+ * Y is the projection output above (ldy >= 2*H*F + 2*H).  out is [N, H*F] (modes 0, 2) or
+ * [N, F] (mode 1).  attn (optional, may be NULL) receives edge_softmax output [E, H] in
+ * in-CSR slot order, for the backward.
+ * ------------------------------------------------------------------------------------- */
+int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
+                     const float* Y, int64_t ldy, int H, int F, const float* bias, float slope,
+                     int mode, float* out, float* attn, void* stream);
+/* Backward of mvml_gat_agg_fwd (DGL GSpMM / GSDDMM / EdgeSoftmax backward + torch autograd of
+ * the residual/bias/ELU/mean).  Atomic-free: the u_mul_e-sum transpose is a gather over the
+ * out-CSR.  Writes gY[N, ldgy] = [dZ | dR | d el | d er] (the GEMM backward's input).
+ * out is the forward output (mode 0 uses ELU'(x) = out + 1 for x <= 0).  gpre_ws: [E, H]. */
+size_t mvml_gat_agg_bwd_workspace_size(int64_t num_edges, int H);
+int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
+                     const int32_t* out_rowptr, const int32_t* out_dst,
+                     const int32_t* out_inslot, const float* Y, int64_t ldy, const float* attn,
+                     const float* out, const float* g_out, int H, int F, float slope, int mode,
+                     float* gY, int64_t ldgy, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Set2Set (dgl 0.9.1, model.py:82-84, 92) building blocks.
+ * LSTM cell (torch.nn.LSTM gate order i,f,g,o): gates_pre[B, 4D] = x W_ih^T + h W_hh^T (by
+ * mvml_gemm_f32), then
+ *   c = sigmoid(f)*c_prev + sigmoid(i)*tanh(g);  h = sigmoid(o)*tanh(c)
+ * act_out[B,4D] saves the activated gates for the backward.  c_prev may be NULL (zeros).
+ * h is written with leading dimension ldh (so the top layer can write straight into q*).
+ * ------------------------------------------------------------------------------------- */
+int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_ih,
+                       const float* b_hh, const float* c_prev, float* c_out, float* h_out,
+                       int64_t ldh, float* act_out, void* stream);
+/* g_h [B,D] (ld ldgh), g_c [B,D] (carry from t+1, may be NULL) -> g_gates [B,4D] (pre-act),
+ * g_c_prev [B,D] (may be NULL). */
+int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const float* c, const float* c_prev,
+                       const float* g_h, int64_t ldgh, const float* g_c, float* g_gates,
+                       float* g_c_prev, void* stream);
+/* Readout segment pass (one wavefront per molecule): e_n = <x_n, q_g>, alpha = softmax over
+ * the molecule's atoms (softmax_nodes), r_g = sum_n alpha_n x_n (sum_nodes).  Writes r into
+ * qstar[:, D:2D] (ld ldq, q itself already sits in qstar[:, 0:D]) and lse[g] for backward. */
+int mvml_set2set_seg_fwd(int64_t B, int D, const int64_t* node_offsets, const float* X,
+                         float* qstar, int64_t ldq, float* lse, void* stream);
+/* Backward of one segment pass: from g_qstar[:, D:2D] (= dL/dr) computes dL/dq into
+ * g_q (g_q = g_qstar[:, 0:D] + segment term; may alias g_qstar with ld ldgq), and saves
+ * alpha[N], g_e[N] for mvml_set2set_gx. */
+int mvml_set2set_seg_bwd(int64_t B, int D, const int64_t* node_offsets, const float* X,
+                         const float* qstar, int64_t ldq, const float* lse,
+                         const float* g_qstar, int64_t ldgq, float* g_q, int64_t ldgout,
+                         float* alpha, float* g_e, void* stream);
+/* dL/dX[n] = sum_t alpha_t[n] * g_r_t[g(n)] + g_e_t[n] * q_t[g(n)] over T iterations,
+ * g(n) = node_graph[n] (from mvml_build_csr).  qstars: T consecutive [B, ldq] buffers
+ * (stride qstar_stride), g_qstars likewise; alphas / g_es: T consecutive [N] buffers. */
+int mvml_set2set_gx(int64_t num_nodes, int D, int T, const int32_t* node_graph,
+                    const float* qstars, int64_t ldq, int64_t qstar_stride,
+                    const float* g_qstars, int64_t ldgq, int64_t g_qstar_stride,
+                    const float* alphas, const float* g_es, float* gX, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * GraphNorm (torch_geometric 2.2.0, eps, batch=None at model.py:93): independent statistics
+ * per normalisation group (group_offsets int64[G+1], in rows); the reference's group is its
+ * 64-molecule mini-batch (config.py:21).
+ * ------------------------------------------------------------------------------------- */
+int mvml_graphnorm_fwd(int64_t G, int D, const int64_t* group_offsets, const float* x,
+                       const float* weight, const float* bias, const float* mean_scale,
+                       float eps, float* y, void* stream);
+size_t mvml_graphnorm_bwd_workspace_size(int64_t G, int D);
+int mvml_graphnorm_bwd(int64_t G, int D, const int64_t* group_offsets, const float* x,
+                       const float* weight, const float* mean_scale, float eps,
+                       const float* g_y, float* g_x, float* g_weight, float* g_bias,
+                       float* g_mean_scale, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
+/* Small elementwise helpers.  ReLU backward (threshold_backward on the output):
+ * g_x = g_y * (y > 0). */
+int mvml_relu_bwd(int64_t n, const float* y, const float* g_y, float* g_x, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MVML_GAT_H */

@@ -1,0 +1,289 @@
+// Device-side graph batching: dgl.batch (dataset.py:52-54) + in/out CSR construction.
+//
+// Layout produced (all int32 unless noted), N = sum of nodes, E = sum of edges:
+//   node_offsets/edge_offsets int64[B+1]  exclusive cumsum of batch_num_nodes / _edges
+//   src/dst[E]        global ids, edge order = graph order then each graph's local order
+//   node_graph[N]     molecule id of every atom (Set2Set / readout segments)
+//   in_rowptr[N+1], in_src[E], in_eid[E]       rows = dst, stable in edge id
+//   out_rowptr[N+1], out_dst[E], out_inslot[E]  rows = src, stable in edge id; out_inslot
+//                                               is the in-CSR slot of the same edge
+// Molecules are independent and small, so the CSR is built by ONE workgroup per graph: the
+// per-graph degree histogram lives in LDS (graphs above kLdsNodes atoms fall back to a
+// workspace histogram) and the stable placement walks the edges in 256-edge chunks, ranking
+// equal keys inside a chunk by lane order.  Integer atomics are used only for histogram
+// counts (order-independent), so the output is deterministic and bit-exact with the oracle
+// (oracle/graph_ref.py: csr_ref).
+#include "common.h"
+
+namespace mvml {
+namespace {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 4;
+constexpr int kScanTile = kScanThreads * kScanItems;  // 1024 items per block
+constexpr int kCsrThreads = 256;
+constexpr int kLdsNodes = 4096;
+
+template <typename T>
+__device__ T block_exclusive_scan(T v, T* lds_waves /*[kWaves]*/, T* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  T x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds_waves[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T run = 0;
+    for (int w = 0; w < nw; ++w) {
+      T t = lds_waves[w];
+      lds_waves[w] = run;
+      run += t;
+    }
+    lds_waves[nw] = run;
+  }
+  __syncthreads();
+  T res = x - v + lds_waves[wid];
+  *total = lds_waves[nw];
+  __syncthreads();
+  return res;
+}
+
+__global__ void scan_tile_sums(const int64_t* __restrict__ in, int64_t n, int64_t* __restrict__ sums) {
+  __shared__ int64_t w[kScanThreads / 64 + 1];
+  int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+  int64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i)
+    if (base + i < n) s += in[base + i];
+  int64_t tot;
+  block_exclusive_scan<int64_t>(s, w, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// Single workgroup: exclusive scan of the tile sums in place.
+__global__ void scan_sums_single(int64_t* __restrict__ sums, int64_t nt) {
+  __shared__ int64_t w[kScanThreads / 64 + 1];
+  int64_t carry = 0;
+  for (int64_t b = 0; b < nt; b += kScanThreads) {
+    int64_t i = b + threadIdx.x;
+    int64_t v = i < nt ? sums[i] : 0;
+    int64_t tot;
+    int64_t ex = block_exclusive_scan<int64_t>(v, w, &tot);
+    if (i < nt) sums[i] = ex + carry;
+    carry += tot;
+  }
+}
+
+__global__ void scan_tile_apply(const int64_t* __restrict__ in, int64_t n,
+                                const int64_t* __restrict__ sums, int64_t* __restrict__ out) {
+  __shared__ int64_t w[kScanThreads / 64 + 1];
+  int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+  int64_t v[kScanItems];
+  int64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    v[i] = (base + i < n) ? in[base + i] : 0;
+    s += v[i];
+  }
+  int64_t tot;
+  int64_t ex = block_exclusive_scan<int64_t>(s, w, &tot) + sums[blockIdx.x];
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    if (base + i < n) out[base + i] = ex;
+    ex += v[i];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == blockDim.x - 1) out[n] = sums[blockIdx.x] + tot;
+}
+
+int exclusive_scan_i64(const int64_t* in, int64_t n, int64_t* out, int64_t* tmp, hipStream_t st) {
+  if (n == 0) {
+    hipMemsetAsync(out, 0, sizeof(int64_t), st);
+    return check_launch("scan(empty)");
+  }
+  int64_t nt = ceil_div(n, kScanTile);
+  scan_tile_sums<<<(unsigned)nt, kScanThreads, 0, st>>>(in, n, tmp);
+  scan_sums_single<<<1, kScanThreads, 0, st>>>(tmp, nt);
+  scan_tile_apply<<<(unsigned)nt, kScanThreads, 0, st>>>(in, n, tmp, out);
+  return check_launch("exclusive_scan_i64");
+}
+
+// Stable placement of one graph's edges into the CSR keyed by `key_local` (dst for the
+// in-CSR, src for the out-CSR).  cursor[] holds each row's next free local slot.
+// For the in-CSR pass (IN = true) it records every edge's in-slot in inslot_ws; the out
+// pass reads it back to fill out_inslot.
+template <bool IN>
+__device__ void place_edges(int ne, int64_t eoff, int64_t noff, const int32_t* __restrict__ key_local,
+                            const int32_t* __restrict__ val_local, int* cursor, int* chunk_key,
+                            int32_t* __restrict__ out_val, int32_t* __restrict__ out_aux,
+                            int32_t* __restrict__ inslot_ws, int n) {
+  for (int base = 0; base < ne; base += kCsrThreads) {
+    const int i = base + threadIdx.x;
+    int k = -1, v = 0;
+    if (i < ne) {
+      k = key_local[eoff + i];
+      v = val_local[eoff + i];
+      if (k < 0 || k >= n || v < 0 || v >= n) k = -1;  // invalid edges are skipped (flagged)
+    }
+    chunk_key[threadIdx.x] = k;
+    __syncthreads();
+    int rank = 0;
+    bool last = true;
+    if (k >= 0) {
+      for (int j = 0; j < (int)threadIdx.x; ++j) rank += (chunk_key[j] == k);
+      const int lim = min(kCsrThreads, ne - base);
+      for (int j = threadIdx.x + 1; j < lim; ++j)
+        if (chunk_key[j] == k) { last = false; break; }
+    }
+    int slot = 0;
+    if (k >= 0) slot = cursor[k] + rank;
+    __syncthreads();
+    if (k >= 0) {
+      if (last) cursor[k] = slot + 1;
+      const int64_t g = eoff + slot;
+      out_val[g] = v + (int32_t)noff;
+      if (IN) {
+        out_aux[g] = (int32_t)(eoff + i);     // in_eid
+        inslot_ws[eoff + i] = (int32_t)g;     // in-slot of edge eoff+i
+      } else {
+        out_aux[g] = inslot_ws[eoff + i];     // out_inslot
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Block-wide exclusive scan of cnt[0..n) in place; writes rowptr[noff + j] = eoff + excl[j].
+__device__ void rows_from_counts(int* cnt, int n, int64_t noff, int64_t eoff,
+                                 int32_t* __restrict__ rowptr, int* zero_rows) {
+  __shared__ int w[kCsrThreads / 64 + 1];
+  int carry = 0, zeros = 0;
+  for (int b = 0; b < n; b += kCsrThreads) {
+    const int j = b + threadIdx.x;
+    const int c = j < n ? cnt[j] : 0;
+    if (j < n && c == 0) ++zeros;
+    int tot;
+    const int ex = block_exclusive_scan<int>(c, w, &tot);
+    if (j < n) {
+      cnt[j] = carry + ex;
+      rowptr[noff + j] = (int32_t)(eoff + carry + ex);
+    }
+    carry += tot;
+  }
+  if (zero_rows && zeros) atomicAdd(zero_rows, zeros);
+}
+
+__global__ void __launch_bounds__(kCsrThreads)
+build_csr_kernel(const int32_t* __restrict__ src_local, const int32_t* __restrict__ dst_local,
+                 const int64_t* __restrict__ num_nodes, const int64_t* __restrict__ num_edges,
+                 const int64_t* __restrict__ node_off, const int64_t* __restrict__ edge_off,
+                 int64_t N, int64_t E, int32_t* __restrict__ src, int32_t* __restrict__ dst,
+                 int32_t* __restrict__ node_graph, int32_t* __restrict__ in_rowptr,
+                 int32_t* __restrict__ in_src, int32_t* __restrict__ in_eid,
+                 int32_t* __restrict__ out_rowptr, int32_t* __restrict__ out_dst,
+                 int32_t* __restrict__ out_inslot, int32_t* __restrict__ flags,
+                 int32_t* __restrict__ inslot_ws, int* __restrict__ big_cnt) {
+  __shared__ int cnt_in_l[kLdsNodes];
+  __shared__ int cnt_out_l[kLdsNodes];
+  __shared__ int chunk_key[kCsrThreads];
+  const int64_t g = blockIdx.x;
+  const int n = (int)num_nodes[g];
+  const int ne = (int)num_edges[g];
+  const int64_t noff = node_off[g], eoff = edge_off[g];
+  int* cnt_in = cnt_in_l;
+  int* cnt_out = cnt_out_l;
+  if (n > kLdsNodes) {  // large graph: histogram in the workspace slice of this graph
+    cnt_in = big_cnt + 2 * noff;
+    cnt_out = cnt_in + n;
+  }
+  for (int j = threadIdx.x; j < n; j += kCsrThreads) {
+    cnt_in[j] = 0;
+    cnt_out[j] = 0;
+    node_graph[noff + j] = (int32_t)g;
+  }
+  __syncthreads();
+  int bad = 0;
+  for (int i = threadIdx.x; i < ne; i += kCsrThreads) {
+    const int s = src_local[eoff + i], d = dst_local[eoff + i];
+    src[eoff + i] = s + (int32_t)noff;
+    dst[eoff + i] = d + (int32_t)noff;
+    if (s < 0 || s >= n || d < 0 || d >= n) {
+      ++bad;
+      continue;
+    }
+    atomicAdd(&cnt_in[d], 1);
+    atomicAdd(&cnt_out[s], 1);
+  }
+  if (bad) atomicAdd(&flags[1], bad);
+  __syncthreads();
+  rows_from_counts(cnt_in, n, noff, eoff, in_rowptr, &flags[0]);
+  __syncthreads();
+  rows_from_counts(cnt_out, n, noff, eoff, out_rowptr, nullptr);
+  if (threadIdx.x == 0) {  // row end of this graph == next graph's first row start
+    in_rowptr[noff + n] = (int32_t)(eoff + ne);
+    out_rowptr[noff + n] = (int32_t)(eoff + ne);
+  }
+  __syncthreads();
+  place_edges<true>(ne, eoff, noff, dst_local, src_local, cnt_in, chunk_key, in_src, in_eid,
+                    inslot_ws, n);
+  // inslot_ws written above by this workgroup; __syncthreads in place_edges orders it.
+  place_edges<false>(ne, eoff, noff, src_local, dst_local, cnt_out, chunk_key, out_dst,
+                     out_inslot, inslot_ws, n);
+}
+
+}  // namespace
+}  // namespace mvml
+
+using namespace mvml;
+
+extern "C" size_t mvml_build_csr_workspace_size(int64_t num_graphs, int64_t num_nodes,
+                                                int64_t num_edges) {
+  size_t nt = (size_t)ceil_div(num_graphs > 0 ? num_graphs : 1, kScanTile);
+  return carve_size(nt * sizeof(int64_t)) + carve_size((size_t)num_edges * sizeof(int32_t)) +
+         carve_size((size_t)2 * num_nodes * sizeof(int)) + 256;
+}
+
+extern "C" int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local,
+                              const int64_t* batch_num_nodes, const int64_t* batch_num_edges,
+                              int64_t num_graphs, int64_t num_nodes, int64_t num_edges,
+                              int64_t* node_offsets, int64_t* edge_offsets, int32_t* src,
+                              int32_t* dst, int32_t* node_graph, int32_t* in_rowptr,
+                              int32_t* in_src, int32_t* in_eid, int32_t* out_rowptr,
+                              int32_t* out_dst, int32_t* out_inslot, int32_t* status_flags,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  MVML_REQUIRE(num_graphs >= 0 && num_nodes >= 0 && num_edges >= 0, "build_csr: negative size");
+  MVML_REQUIRE(num_nodes < (int64_t(1) << 31) && num_edges < (int64_t(1) << 31),
+               "build_csr: int32 index overflow (N=%lld, E=%lld)", (long long)num_nodes,
+               (long long)num_edges);
+  MVML_REQUIRE(num_graphs < (int64_t(1) << 31), "build_csr: too many graphs");
+  if (workspace_bytes < mvml_build_csr_workspace_size(num_graphs, num_nodes, num_edges)) {
+    set_error("build_csr: workspace too small");
+    return MVML_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  Carver cv(workspace, workspace_bytes);
+  int64_t* tmp = cv.take<int64_t>((size_t)ceil_div(num_graphs > 0 ? num_graphs : 1, kScanTile));
+  int32_t* inslot = cv.take<int32_t>((size_t)num_edges);
+  int* big = cv.take<int>((size_t)2 * num_nodes);
+  hipMemsetAsync(status_flags, 0, 2 * sizeof(int32_t), st);
+  int rc = exclusive_scan_i64(batch_num_nodes, num_graphs, node_offsets, tmp, st);
+  if (rc) return rc;
+  rc = exclusive_scan_i64(batch_num_edges, num_graphs, edge_offsets, tmp, st);
+  if (rc) return rc;
+  if (num_nodes == 0) {
+    hipMemsetAsync(in_rowptr, 0, sizeof(int32_t), st);
+    hipMemsetAsync(out_rowptr, 0, sizeof(int32_t), st);
+    return check_launch("build_csr(empty)");
+  }
+  if (num_graphs > 0) {
+    build_csr_kernel<<<(unsigned)num_graphs, kCsrThreads, 0, st>>>(
+        src_local, dst_local, batch_num_nodes, batch_num_edges, node_offsets, edge_offsets,
+        num_nodes, num_edges, src, dst, node_graph, in_rowptr, in_src, in_eid, out_rowptr,
+        out_dst, out_inslot, status_flags, inslot, big);
+  }
+  return check_launch("build_csr_kernel");
+}

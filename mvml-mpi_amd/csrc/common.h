@@ -1,0 +1,63 @@
+// Shared helpers for the mvml_gat HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include <algorithm>
+
+#include "../../include/mvml_gat.h"
+
+namespace mvml {
+
+// Thread-local last-error string (mvml_last_error).
+void set_error(const char* fmt, ...);
+void clear_error();
+
+constexpr int kWave = 64;
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Check the launch we just enqueued; never synchronises.
+int check_launch(const char* what);
+
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Workspace carving: 256-byte aligned sub-buffers.
+struct Carver {
+  char* base;
+  size_t cap;
+  size_t used = 0;
+  Carver(void* b, size_t c) : base(static_cast<char*>(b)), cap(c) {}
+  template <typename T>
+  T* take(size_t count) {
+    size_t off = (used + 255) & ~size_t(255);
+    used = off + count * sizeof(T);
+    return reinterpret_cast<T*>(base + off);
+  }
+  bool ok() const { return used <= cap; }
+};
+inline size_t carve_size(size_t bytes) { return (bytes + 255) & ~size_t(255); }
+
+// ---- device helpers -------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+}  // namespace mvml
+
+#define MVML_REQUIRE(cond, ...)          \
+  do {                                   \
+    if (!(cond)) {                       \
+      ::mvml::set_error(__VA_ARGS__);    \
+      return MVML_ERR_INVALID;           \
+    }                                    \
+  } while (0)

@@ -1,0 +1,612 @@
+// Fused GAT attention + aggregation (dgl 0.9.1 GATConv.forward after the projection) and its
+// atomic-free backward.  One wavefront per destination atom.
+//
+// Forward, per destination v (rows of the in-CSR, in-edges in ascending edge id):
+//   s_e   = LeakyReLU(el[src_e] + er[v], slope)            apply_edges(u_add_v), leaky_relu
+//   a_e   = exp(s_e - max_v s) / sum_v exp(s - max_v s)   edge_softmax (norm_by = dst)
+//   rst_v = sum_e a_e * Z[src_e] + R[v] + bias            update_all(u_mul_e, sum), res_fc, bias
+//   out_v = ELU(rst_v.flatten) | mean_h(rst_v) | rst_v    dgllife GATLayer agg_mode/activation
+// Lanes take the in-edges (64 per chunk) for the logits/softmax, then the wave walks the
+// edges and every lane accumulates 4 consecutive feature columns per 256-column slice
+// (16-B loads of the gathered Z rows; neighbour rows of a molecule are L2 hits).
+//
+// Backward (two passes, no float atomics):
+//   A (per dst v):  g_a_e = <Z[src_e], g_rst[v]>_f per head; g_s = a*(g_a - sum_v a*g_a);
+//                   g_pre = g_s * leaky'(s_e); d er[v] = sum_e g_pre           -> gpre_ws, gY
+//   B (per src u):  dZ[u] = sum_{e: u->w} a_e * g_rst[w]; d el[u] = sum_{e: u->w} g_pre_e
+//                   (gather over the out-CSR, out_inslot -> in-CSR slot of the edge), and the
+//                   residual gradient dR[u] = g_rst[u]                            -> gY
+#include "common.h"
+
+namespace mvml {
+namespace {
+
+constexpr int kWavesPerBlock = 4;
+
+__device__ __forceinline__ float rl(float x, int j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j));
+}
+__device__ __forceinline__ int rl(int x, int j) { return __builtin_amdgcn_readlane(x, j); }
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float leaky(float x, float slope) { return x > 0.f ? x : x * slope; }
+__device__ __forceinline__ float elu(float x) { return x > 0.f ? x : expm1f(x); }
+
+__device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
+__device__ __forceinline__ float4 fma4(float a, float4 z, float4 c) {
+  return make_float4(fmaf(a, z.x, c.x), fmaf(a, z.y, c.y), fmaf(a, z.z, c.z), fmaf(a, z.w, c.w));
+}
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float dot4(float4 a, float4 b) {
+  return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+}
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+template <int H>
+__device__ __forceinline__ float pick(const float (&a)[H], int h) {
+  float r = a[0];
+#pragma unroll
+  for (int k = 1; k < H; ++k) r = (h == k) ? a[k] : r;
+  return r;
+}
+
+// g_rst[v, col..col+3] from the layer output gradient (undoing ELU / head-mean / identity).
+__device__ __forceinline__ float4 grst_of(const float* __restrict__ g_out, const float* __restrict__ out,
+                                          int64_t v, int col, int HF, int F, int H, int mode) {
+  if (mode == 1) {
+    const float4 g = ld4(g_out + v * F + (col % F));
+    const float inv = (float)H;
+    return make_float4(g.x / inv, g.y / inv, g.z / inv, g.w / inv);
+  }
+  float4 g = ld4(g_out + v * HF + col);
+  if (mode == 0) {  // ELU'(x) = 1 (x > 0) else exp(x) = out + 1 (torch elu_backward, is_result)
+    const float4 o = ld4(out + v * HF + col);
+    g.x *= o.x > 0.f ? 1.f : o.x + 1.f;
+    g.y *= o.y > 0.f ? 1.f : o.y + 1.f;
+    g.z *= o.z > 0.f ? 1.f : o.z + 1.f;
+    g.w *= o.w > 0.f ? 1.f : o.w + 1.f;
+  }
+  return g;
+}
+
+template <int H, int VPL>
+__global__ void __launch_bounds__(kWavesPerBlock * 64)
+gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
+                   const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ bias,
+                   float slope, int mode, float* __restrict__ out, float* __restrict__ attn) {
+  __shared__ __attribute__((aligned(16))) float red[kWavesPerBlock][VPL * 256];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t v = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  if (v >= N) return;
+  const int HF = H * F;
+  const int beg = rowptr[v], end = rowptr[v + 1];
+  const int deg = end - beg;
+  const float* yv = Y + v * ldy;
+  float er[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) er[h] = yv[2 * HF + H + h];
+
+  // ---- softmax statistics over the in-edges (exactly max -> exp -> sum -> divide) ----
+  float mx[H], sm[H], s_l[H];
+  int u_l = 0;
+#pragma unroll
+  for (int h = 0; h < H; ++h) { mx[h] = -INFINITY; sm[h] = 0.f; s_l[h] = -INFINITY; }
+  for (int base = 0; base < deg; base += 64) {
+    const bool valid = base + lane < deg;
+    if (valid) {
+      u_l = in_src[beg + base + lane];
+      const float* yu = Y + (int64_t)u_l * ldy + 2 * HF;
+#pragma unroll
+      for (int h = 0; h < H; ++h) s_l[h] = leaky(yu[h] + er[h], slope);
+    } else {
+#pragma unroll
+      for (int h = 0; h < H; ++h) s_l[h] = -INFINITY;
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) mx[h] = fmaxf(mx[h], wave_max(s_l[h]));
+  }
+  const bool one_chunk = deg <= 64;
+  if (one_chunk) {
+#pragma unroll
+    for (int h = 0; h < H; ++h) sm[h] = wave_sum(lane < deg ? expf(s_l[h] - mx[h]) : 0.f);
+  } else {
+    for (int base = 0; base < deg; base += 64) {
+      const bool valid = base + lane < deg;
+      float ex[H];
+      if (valid) {
+        const int u = in_src[beg + base + lane];
+        const float* yu = Y + (int64_t)u * ldy + 2 * HF;
+#pragma unroll
+        for (int h = 0; h < H; ++h) ex[h] = expf(leaky(yu[h] + er[h], slope) - mx[h]);
+      } else {
+#pragma unroll
+        for (int h = 0; h < H; ++h) ex[h] = 0.f;
+      }
+#pragma unroll
+      for (int h = 0; h < H; ++h) sm[h] += wave_sum(ex[h]);
+    }
+  }
+
+  // ---- aggregation ----
+  int hc[VPL];
+  bool okc[VPL];
+  float4 acc[VPL];
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    okc[c] = col < HF;
+    hc[c] = okc[c] ? col / F : 0;
+    acc[c] = f4(0.f);
+  }
+  for (int base = 0; base < deg; base += 64) {
+    const int cnt = min(64, deg - base);
+    float a_l[H];
+    if (!one_chunk) {
+      if (base + lane < deg) {
+        u_l = in_src[beg + base + lane];
+        const float* yu = Y + (int64_t)u_l * ldy + 2 * HF;
+#pragma unroll
+        for (int h = 0; h < H; ++h) s_l[h] = leaky(yu[h] + er[h], slope);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) a_l[h] = (base + lane < deg) ? expf(s_l[h] - mx[h]) / sm[h] : 0.f;
+    if (attn && base + lane < deg) {
+      float* ap = attn + (int64_t)(beg + base + lane) * H;
+      if (H == 4) st4(ap, make_float4(a_l[0], a_l[H > 1 ? 1 : 0], a_l[H > 2 ? 2 : 0], a_l[H > 3 ? 3 : 0]));
+      else {
+#pragma unroll
+        for (int h = 0; h < H; ++h) ap[h] = a_l[h];
+      }
+    }
+    int j = 0;
+    for (; j + 1 < cnt; j += 2) {
+      const int u0 = rl(u_l, j), u1 = rl(u_l, j + 1);
+      float a0[H], a1[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) { a0[h] = rl(a_l[h], j); a1[h] = rl(a_l[h], j + 1); }
+      const float* z0 = Y + (int64_t)u0 * ldy;
+      const float* z1 = Y + (int64_t)u1 * ldy;
+      float4 zv0[VPL], zv1[VPL];
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) {
+        const int col = 4 * (lane + 64 * c);
+        if (okc[c]) { zv0[c] = ld4(z0 + col); zv1[c] = ld4(z1 + col); }
+      }
+#pragma unroll
+      for (int c = 0; c < VPL; ++c)
+        if (okc[c]) {
+          acc[c] = fma4(pick<H>(a0, hc[c]), zv0[c], acc[c]);
+          acc[c] = fma4(pick<H>(a1, hc[c]), zv1[c], acc[c]);
+        }
+    }
+    if (j < cnt) {
+      const int u0 = rl(u_l, j);
+      float a0[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) a0[h] = rl(a_l[h], j);
+      const float* z0 = Y + (int64_t)u0 * ldy;
+#pragma unroll
+      for (int c = 0; c < VPL; ++c)
+        if (okc[c]) acc[c] = fma4(pick<H>(a0, hc[c]), ld4(z0 + 4 * (lane + 64 * c)), acc[c]);
+    }
+  }
+
+  // ---- epilogue: + residual + bias, then GATLayer aggregation ----
+#pragma unroll
+  for (int c = 0; c < VPL; ++c)
+    if (okc[c]) {
+      const int col = 4 * (lane + 64 * c);
+      acc[c] = add4(add4(acc[c], ld4(yv + HF + col)), ld4(bias + col));
+    }
+  if (mode == 1) {
+    float* r = red[wid];
+#pragma unroll
+    for (int c = 0; c < VPL; ++c)
+      if (okc[c]) st4(r + 4 * (lane + 64 * c), acc[c]);
+    wave_lds_sync();
+    const float invh = (float)H;
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) {
+      const int f = 4 * (lane + 64 * c);
+      if (f < F) {
+        float4 s = ld4(r + f);
+#pragma unroll
+        for (int h = 1; h < H; ++h) s = add4(s, ld4(r + h * F + f));
+        st4(out + v * F + f, make_float4(s.x / invh, s.y / invh, s.z / invh, s.w / invh));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < VPL; ++c)
+      if (okc[c]) {
+        float4 o = acc[c];
+        if (mode == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
+        st4(out + v * HF + 4 * (lane + 64 * c), o);
+      }
+  }
+}
+
+// Backward pass A: one wave per destination v.
+template <int H, int VPL>
+__global__ void __launch_bounds__(kWavesPerBlock * 64)
+gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
+                       const float* __restrict__ Y, int64_t ldy, const float* __restrict__ attn,
+                       const float* __restrict__ out, const float* __restrict__ g_out, int F,
+                       float slope, int mode, float* __restrict__ gpre, float* __restrict__ gY,
+                       int64_t ldgy) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t v = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  if (v >= N) return;
+  const int HF = H * F;
+  const int beg = rowptr[v], end = rowptr[v + 1];
+  const int deg = end - beg;
+  int hc[VPL];
+  bool okc[VPL];
+  float4 gr[VPL];
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    okc[c] = col < HF;
+    hc[c] = okc[c] ? col / F : 0;
+    gr[c] = okc[c] ? grst_of(g_out, out, v, col, HF, F, H, mode) : f4(0.f);
+  }
+  const float* yv = Y + v * ldy;
+  float er[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) er[h] = yv[2 * HF + H + h];
+
+  float dots[H];  // sum_e a_e * g_a_e per head
+#pragma unroll
+  for (int h = 0; h < H; ++h) dots[h] = 0.f;
+  float ga_l[H], a_l[H];
+  for (int base = 0; base < deg; base += 64) {
+    const int cnt = min(64, deg - base);
+    int u_l = 0;
+    if (base + lane < deg) u_l = in_src[beg + base + lane];
+#pragma unroll
+    for (int h = 0; h < H; ++h) ga_l[h] = 0.f;
+    for (int j = 0; j < cnt; ++j) {
+      const int u = rl(u_l, j);
+      const float* zu = Y + (int64_t)u * ldy;
+      float part[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) part[h] = 0.f;
+#pragma unroll
+      for (int c = 0; c < VPL; ++c)
+        if (okc[c]) {
+          const float d = dot4(ld4(zu + 4 * (lane + 64 * c)), gr[c]);
+#pragma unroll
+          for (int h = 0; h < H; ++h) part[h] += (hc[c] == h) ? d : 0.f;
+        }
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const float g = wave_sum(part[h]);
+        ga_l[h] = (lane == j) ? g : ga_l[h];
+      }
+    }
+    const bool valid = base + lane < deg;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      a_l[h] = valid ? attn[(int64_t)(beg + base + lane) * H + h] : 0.f;
+      dots[h] += wave_sum(a_l[h] * ga_l[h]);
+    }
+    if (deg > 64 && valid) {  // keep g_a for the second sweep
+#pragma unroll
+      for (int h = 0; h < H; ++h) gpre[(int64_t)(beg + base + lane) * H + h] = ga_l[h];
+    }
+  }
+  float ger[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) ger[h] = 0.f;
+  for (int base = 0; base < deg; base += 64) {
+    const bool valid = base + lane < deg;
+    const int64_t slot = beg + base + lane;
+    float gp[H];
+    if (valid) {
+      const int u = in_src[slot];
+      const float* yu = Y + (int64_t)u * ldy + 2 * HF;
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const float a = (deg > 64) ? attn[slot * H + h] : a_l[h];
+        const float ga = (deg > 64) ? gpre[slot * H + h] : ga_l[h];
+        const float gs = a * (ga - dots[h]);
+        const float spre = yu[h] + er[h];
+        gp[h] = spre > 0.f ? gs : gs * slope;
+        gpre[slot * H + h] = gp[h];
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < H; ++h) gp[h] = 0.f;
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) ger[h] += wave_sum(gp[h]);
+  }
+  if (lane < H) {
+    float g = ger[0];
+#pragma unroll
+    for (int h = 1; h < H; ++h) g = (lane == h) ? ger[h] : g;
+    gY[v * ldgy + 2 * HF + H + lane] = g;
+  }
+}
+
+// Backward pass B: one wave per source u (out-CSR gather).
+template <int H, int VPL>
+__global__ void __launch_bounds__(kWavesPerBlock * 64)
+gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
+                       const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
+                       const float* __restrict__ attn, const float* __restrict__ gpre,
+                       const float* __restrict__ out, const float* __restrict__ g_out, int F,
+                       int mode, float* __restrict__ gY, int64_t ldgy) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t u = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  if (u >= N) return;
+  const int HF = H * F;
+  const int beg = out_rowptr[u], end = out_rowptr[u + 1];
+  const int deg = end - beg;
+  int hc[VPL];
+  bool okc[VPL];
+  float4 gz[VPL];
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    okc[c] = col < HF;
+    hc[c] = okc[c] ? col / F : 0;
+    gz[c] = f4(0.f);
+  }
+  float gel[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) gel[h] = 0.f;
+  for (int base = 0; base < deg; base += 64) {
+    const int cnt = min(64, deg - base);
+    int w_l = 0;
+    float a_l[H], gp_l[H];
+    if (base + lane < deg) {
+      w_l = out_dst[beg + base + lane];
+      const int64_t js = out_inslot[beg + base + lane];
+#pragma unroll
+      for (int h = 0; h < H; ++h) { a_l[h] = attn[js * H + h]; gp_l[h] = gpre[js * H + h]; }
+    } else {
+#pragma unroll
+      for (int h = 0; h < H; ++h) { a_l[h] = 0.f; gp_l[h] = 0.f; }
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) gel[h] += wave_sum(gp_l[h]);
+    for (int j = 0; j < cnt; ++j) {
+      const int w = rl(w_l, j);
+      float a[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) a[h] = rl(a_l[h], j);
+#pragma unroll
+      for (int c = 0; c < VPL; ++c)
+        if (okc[c]) gz[c] = fma4(pick<H>(a, hc[c]), grst_of(g_out, out, w, 4 * (lane + 64 * c), HF, F, H, mode), gz[c]);
+    }
+  }
+  float* gyu = gY + u * ldgy;
+#pragma unroll
+  for (int c = 0; c < VPL; ++c)
+    if (okc[c]) {
+      const int col = 4 * (lane + 64 * c);
+      st4(gyu + col, gz[c]);
+      st4(gyu + HF + col, grst_of(g_out, out, u, col, HF, F, H, mode));
+    }
+  if (lane < H) {
+    float g = gel[0];
+#pragma unroll
+    for (int h = 1; h < H; ++h) g = (lane == h) ? gel[h] : g;
+    gyu[2 * HF + lane] = g;
+  }
+}
+
+template <int H, int VPL>
+int launch_fwd(int64_t N, const int32_t* rp, const int32_t* src, const float* Y, int64_t ldy, int F,
+               const float* bias, float slope, int mode, float* out, float* attn, hipStream_t st) {
+  const unsigned blocks = (unsigned)ceil_div(N, kWavesPerBlock);
+  gat_agg_fwd_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(N, rp, src, Y, ldy, F, bias,
+                                                                       slope, mode, out, attn);
+  return check_launch("gat_agg_fwd_kernel");
+}
+
+template <int H, int VPL>
+int launch_bwd(int64_t N, const int32_t* rp, const int32_t* src, const int32_t* orp,
+               const int32_t* odst, const int32_t* oslot, const float* Y, int64_t ldy,
+               const float* attn, const float* out, const float* g_out, int F, float slope,
+               int mode, float* gpre, float* gY, int64_t ldgy, hipStream_t st) {
+  const unsigned blocks = (unsigned)ceil_div(N, kWavesPerBlock);
+  gat_agg_bwd_dst_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
+      N, rp, src, Y, ldy, attn, out, g_out, F, slope, mode, gpre, gY, ldgy);
+  int rc = check_launch("gat_agg_bwd_dst_kernel");
+  if (rc) return rc;
+  gat_agg_bwd_src_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
+      N, orp, odst, oslot, attn, gpre, out, g_out, F, mode, gY, ldgy);
+  return check_launch("gat_agg_bwd_src_kernel");
+}
+
+#define MVML_VPL_CASES(FN, H, ...)                 \
+  switch (vpl) {                                   \
+    case 1: return FN<H, 1>(__VA_ARGS__);          \
+    case 2: return FN<H, 2>(__VA_ARGS__);          \
+    case 3: return FN<H, 3>(__VA_ARGS__);          \
+    case 4: return FN<H, 4>(__VA_ARGS__);          \
+    case 5: return FN<H, 5>(__VA_ARGS__);          \
+    case 6: return FN<H, 6>(__VA_ARGS__);          \
+    case 7: return FN<H, 7>(__VA_ARGS__);          \
+    case 8: return FN<H, 8>(__VA_ARGS__);          \
+    default: break;                                \
+  }
+
+int check_shapes(int H, int F, int64_t ldy, const void* Y, const char* who) {
+  MVML_REQUIRE(H == 1 || H == 2 || H == 4 || H == 8, "%s: num_heads must be 1, 2, 4 or 8 (got %d)", who, H);
+  MVML_REQUIRE(F > 0 && F % 4 == 0, "%s: out_feats must be a positive multiple of 4 (got %d)", who, F);
+  MVML_REQUIRE(H * F <= 2048, "%s: H*F must be <= 2048 (got %d)", who, H * F);
+  MVML_REQUIRE(ldy >= 2 * H * F + 2 * H && ldy % 4 == 0, "%s: bad leading dimension %lld", who, (long long)ldy);
+  MVML_REQUIRE(((uintptr_t)Y & 15) == 0, "%s: tensors must be 16-byte aligned", who);
+  return MVML_OK;
+}
+
+}  // namespace
+}  // namespace mvml
+
+using namespace mvml;
+
+extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
+                                const float* Y, int64_t ldy, int H, int F, const float* bias,
+                                float slope, int mode, float* out, float* attn, void* stream) {
+  clear_error();
+  int rc = check_shapes(H, F, ldy, Y, "gat_agg_fwd");
+  if (rc) return rc;
+  MVML_REQUIRE(mode >= 0 && mode <= 2, "gat_agg_fwd: bad mode %d", mode);
+  MVML_REQUIRE(((uintptr_t)out & 15) == 0 && ((uintptr_t)bias & 15) == 0, "gat_agg_fwd: unaligned out/bias");
+  if (num_nodes == 0) return MVML_OK;
+  hipStream_t st = as_stream(stream);
+  const int vpl = (int)ceil_div(H * F, 256);
+  switch (H) {
+    case 1: { MVML_VPL_CASES(launch_fwd, 1, num_nodes, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, st) break; }
+    case 2: { MVML_VPL_CASES(launch_fwd, 2, num_nodes, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, st) break; }
+    case 4: { MVML_VPL_CASES(launch_fwd, 4, num_nodes, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, st) break; }
+    case 8: { MVML_VPL_CASES(launch_fwd, 8, num_nodes, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, st) break; }
+  }
+  set_error("gat_agg_fwd: unsupported shape");
+  return MVML_ERR_INVALID;
+}
+
+extern "C" size_t mvml_gat_agg_bwd_workspace_size(int64_t num_edges, int H) {
+  return carve_size((size_t)num_edges * H * sizeof(float));
+}
+
+extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
+                                const int32_t* out_rowptr, const int32_t* out_dst,
+                                const int32_t* out_inslot, const float* Y, int64_t ldy,
+                                const float* attn, const float* out, const float* g_out, int H,
+                                int F, float slope, int mode, float* gY, int64_t ldgy,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  int rc = check_shapes(H, F, ldy, Y, "gat_agg_bwd");
+  if (rc) return rc;
+  MVML_REQUIRE(mode >= 0 && mode <= 2, "gat_agg_bwd: bad mode %d", mode);
+  MVML_REQUIRE(ldgy >= 2 * H * F + 2 * H && ldgy % 4 == 0, "gat_agg_bwd: bad ldgy");
+  MVML_REQUIRE(attn != nullptr, "gat_agg_bwd: attention from the forward is required");
+  MVML_REQUIRE(mode != 0 || out != nullptr, "gat_agg_bwd: mode 0 needs the forward output");
+  if (num_nodes == 0) return MVML_OK;
+  if (!workspace || workspace_bytes == 0) {
+    set_error("gat_agg_bwd: workspace of mvml_gat_agg_bwd_workspace_size(E, H) bytes required");
+    return MVML_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  float* gpre = static_cast<float*>(workspace);
+  const int vpl = (int)ceil_div(H * F, 256);
+  switch (H) {
+    case 1: { MVML_VPL_CASES(launch_bwd, 1, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, st) break; }
+    case 2: { MVML_VPL_CASES(launch_bwd, 2, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, st) break; }
+    case 4: { MVML_VPL_CASES(launch_bwd, 4, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, st) break; }
+    case 8: { MVML_VPL_CASES(launch_bwd, 8, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, st) break; }
+  }
+  set_error("gat_agg_bwd: unsupported shape");
+  return MVML_ERR_INVALID;
+}
+
+// ---- projection weight folding (attention vectors folded into the fc GEMM) ----------------
+
+namespace mvml {
+namespace {
+
+// Wcat rows: [0,HF) fc.weight, [HF,2HF) res_fc.weight, [2HF,2HF+H) A_l, [2HF+H,2HF+2H) A_r.
+__global__ void fold_weights_kernel(const float* __restrict__ fc_w, const float* __restrict__ res_w,
+                                    const float* __restrict__ attn_l, const float* __restrict__ attn_r,
+                                    int H, int F, int Fin, float* __restrict__ Wcat) {
+  const int HF = H * F;
+  const int64_t total = (int64_t)(2 * HF + 2 * H) * Fin;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(e / Fin), k = (int)(e % Fin);
+    float v;
+    if (row < HF) v = fc_w[(int64_t)row * Fin + k];
+    else if (row < 2 * HF) v = res_w[(int64_t)(row - HF) * Fin + k];
+    else {
+      const int r = row - 2 * HF;
+      const int h = r % H;
+      const float* at = (r < H) ? attn_l : attn_r;
+      float s = 0.f;
+      for (int f = 0; f < F; ++f) s = fmaf(at[h * F + f], fc_w[(int64_t)(h * F + f) * Fin + k], s);
+      v = s;
+    }
+    Wcat[e] = v;
+  }
+}
+
+// dL/dfc.weight[hF+f,k] = gWcat[hF+f,k] + attn_l[h,f]*gA_l[h,k] + attn_r[h,f]*gA_r[h,k]
+// dL/dres_fc.weight = gWcat[HF:2HF]
+__global__ void unfold_w_kernel(const float* __restrict__ gW, const float* __restrict__ attn_l,
+                                const float* __restrict__ attn_r, int H, int F, int Fin,
+                                float* __restrict__ g_fc, float* __restrict__ g_res) {
+  const int HF = H * F;
+  const int64_t total = (int64_t)HF * Fin;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(e / Fin), k = (int)(e % Fin);
+    const int h = row / F;
+    const float gl = gW[(int64_t)(2 * HF + h) * Fin + k];
+    const float gr = gW[(int64_t)(2 * HF + H + h) * Fin + k];
+    g_fc[e] = gW[e] + attn_l[row] * gl + attn_r[row] * gr;
+    g_res[e] = gW[(int64_t)HF * Fin + e];
+  }
+}
+
+// dL/dattn_l[h,f] = sum_k gA_l[h,k] * fc.weight[hF+f,k]  (one wave per (side, h, f))
+__global__ void unfold_attn_kernel(const float* __restrict__ gW, const float* __restrict__ fc_w,
+                                   int H, int F, int Fin, float* __restrict__ g_al,
+                                   float* __restrict__ g_ar) {
+  const int HF = H * F;
+  const int lane = threadIdx.x & 63;
+  const int64_t item = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (item >= 2 * HF) return;
+  const int side = (int)(item / HF), row = (int)(item % HF);
+  const int h = row / F;
+  const float* ga = gW + (int64_t)(2 * HF + side * H + h) * Fin;
+  const float* w = fc_w + (int64_t)row * Fin;
+  float s = 0.f;
+  for (int k = lane; k < Fin; k += 64) s = fmaf(ga[k], w[k], s);
+  s = wave_sum(s);
+  if (lane == 0) (side ? g_ar : g_al)[row] = s;
+}
+
+}  // namespace
+}  // namespace mvml
+
+extern "C" int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_l,
+                                     const float* attn_r, int H, int F, int Fin, float* Wcat,
+                                     void* stream) {
+  clear_error();
+  MVML_REQUIRE(H > 0 && F > 0 && Fin > 0, "gat_fold_weights: bad shape");
+  hipStream_t st = as_stream(stream);
+  const int64_t total = (int64_t)(2 * H * F + 2 * H) * Fin;
+  const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
+  fold_weights_kernel<<<blocks, 256, 0, st>>>(fc_w, res_fc_w, attn_l, attn_r, H, F, Fin, Wcat);
+  return check_launch("fold_weights_kernel");
+}
+
+extern "C" int mvml_gat_unfold_grads(const float* gWcat, const float* fc_w, const float* attn_l,
+                                     const float* attn_r, int H, int F, int Fin, float* g_fc_w,
+                                     float* g_res_fc_w, float* g_attn_l, float* g_attn_r,
+                                     void* stream) {
+  clear_error();
+  MVML_REQUIRE(H > 0 && F > 0 && Fin > 0, "gat_unfold_grads: bad shape");
+  hipStream_t st = as_stream(stream);
+  const int64_t total = (int64_t)H * F * Fin;
+  const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
+  unfold_w_kernel<<<blocks, 256, 0, st>>>(gWcat, attn_l, attn_r, H, F, Fin, g_fc_w, g_res_fc_w);
+  int rc = check_launch("unfold_w_kernel");
+  if (rc) return rc;
+  const int64_t items = 2 * (int64_t)H * F;
+  unfold_attn_kernel<<<(unsigned)ceil_div(items, 4), 256, 0, st>>>(gWcat, fc_w, H, F, Fin, g_attn_l,
+                                                                   g_attn_r);
+  return check_launch("unfold_attn_kernel");
+}

@@ -1,0 +1,311 @@
+// Set2Set readout (dgl 0.9.1 Set2Set, model.py:82-84 and 92): LSTM cell pointwise kernels and
+// the fused per-molecule segment pass (broadcast_nodes -> dot -> softmax_nodes -> sum_nodes).
+//
+// The LSTM gate GEMMs run on mvml_gemm_f32; these kernels apply the torch.nn.LSTM cell
+// (gate order i, f, g, o):  c = sig(f)*c_prev + sig(i)*tanh(g);  h = sig(o)*tanh(c).
+// The segment pass gives each molecule one wavefront that streams its atoms' 384-float rows
+// once (online max/sum softmax), so the six Set2Set iterations read the node features six
+// times in total, never materialising broadcast q or per-node products.
+#include "common.h"
+
+namespace mvml {
+namespace {
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float dot4(float4 a, float4 b) {
+  return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+}
+
+__global__ void lstm_cell_fwd_kernel(int64_t B, int D, const float* __restrict__ gp,
+                                     const float* __restrict__ b_ih, const float* __restrict__ b_hh,
+                                     const float* __restrict__ c_prev, float* __restrict__ c_out,
+                                     float* __restrict__ h_out, int64_t ldh, float* __restrict__ act) {
+  const int64_t total = B * D;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = e / D;
+    const int d = (int)(e - b * D);
+    const float* g = gp + b * 4 * D;
+    const float gi = g[d] + b_ih[d] + b_hh[d];
+    const float gf = g[D + d] + b_ih[D + d] + b_hh[D + d];
+    const float gg = g[2 * D + d] + b_ih[2 * D + d] + b_hh[2 * D + d];
+    const float go = g[3 * D + d] + b_ih[3 * D + d] + b_hh[3 * D + d];
+    const float i = sigm(gi), f = sigm(gf), gt = tanhf(gg), o = sigm(go);
+    const float cp = c_prev ? c_prev[e] : 0.f;
+    const float c = f * cp + i * gt;
+    c_out[e] = c;
+    h_out[b * ldh + d] = o * tanhf(c);
+    float* a = act + b * 4 * D;
+    a[d] = i;
+    a[D + d] = f;
+    a[2 * D + d] = gt;
+    a[3 * D + d] = o;
+  }
+}
+
+__global__ void lstm_cell_bwd_kernel(int64_t B, int D, const float* __restrict__ act,
+                                     const float* __restrict__ c, const float* __restrict__ c_prev,
+                                     const float* __restrict__ g_h, int64_t ldgh,
+                                     const float* __restrict__ g_c, float* __restrict__ g_gates,
+                                     float* __restrict__ g_c_prev) {
+  const int64_t total = B * D;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = e / D;
+    const int d = (int)(e - b * D);
+    const float* a = act + b * 4 * D;
+    const float i = a[d], f = a[D + d], gt = a[2 * D + d], o = a[3 * D + d];
+    const float gh = g_h[b * ldgh + d];
+    const float tc = tanhf(c[e]);
+    const float gc = (g_c ? g_c[e] : 0.f) + gh * o * (1.f - tc * tc);
+    const float cp = c_prev ? c_prev[e] : 0.f;
+    float* gg = g_gates + b * 4 * D;
+    gg[d] = gc * gt * i * (1.f - i);
+    gg[D + d] = gc * cp * f * (1.f - f);
+    gg[2 * D + d] = gc * i * (1.f - gt * gt);
+    gg[3 * D + d] = gh * tc * o * (1.f - o);
+    if (g_c_prev) g_c_prev[e] = gc * f;
+  }
+}
+
+// One wave per molecule; lane holds float4 column groups col = 4*(lane + 64*c).
+template <int NV>
+__global__ void __launch_bounds__(256)
+seg_fwd_kernel(int64_t B, int D, const int64_t* __restrict__ node_off, const float* __restrict__ X,
+               float* __restrict__ qstar, int64_t ldq, float* __restrict__ lse) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= B) return;
+  const int64_t n0 = node_off[g], n1 = node_off[g + 1];
+  float4 q[NV], r[NV];
+  bool ok[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    ok[c] = col < D;
+    q[c] = ok[c] ? ld4(qstar + g * ldq + col) : make_float4(0, 0, 0, 0);
+    r[c] = make_float4(0, 0, 0, 0);
+  }
+  float m = -INFINITY, s = 0.f;
+  for (int64_t n = n0; n < n1; ++n) {
+    float4 x[NV];
+    float part = 0.f;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      x[c] = ok[c] ? ld4(X + n * D + 4 * (lane + 64 * c)) : make_float4(0, 0, 0, 0);
+      part += dot4(x[c], q[c]);
+    }
+    const float e = wave_sum(part);
+    const float mn = fmaxf(m, e);
+    const float sc = expf(m - mn);
+    const float p = expf(e - mn);
+    s = s * sc + p;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      r[c].x = r[c].x * sc + p * x[c].x;
+      r[c].y = r[c].y * sc + p * x[c].y;
+      r[c].z = r[c].z * sc + p * x[c].z;
+      r[c].w = r[c].w * sc + p * x[c].w;
+    }
+    m = mn;
+  }
+  const float inv = (n1 > n0) ? 1.f / s : 0.f;
+#pragma unroll
+  for (int c = 0; c < NV; ++c)
+    if (ok[c])
+      st4(qstar + g * ldq + D + 4 * (lane + 64 * c),
+          make_float4(r[c].x * inv, r[c].y * inv, r[c].z * inv, r[c].w * inv));
+  if (lane == 0) lse[g] = (n1 > n0) ? m + logf(s) : -INFINITY;
+}
+
+template <int NV>
+__global__ void __launch_bounds__(256)
+seg_bwd_kernel(int64_t B, int D, const int64_t* __restrict__ node_off, const float* __restrict__ X,
+               const float* __restrict__ qstar, int64_t ldq, const float* __restrict__ lse,
+               const float* g_qstar, int64_t ldgq, float* g_q,
+               int64_t ldgout, float* __restrict__ alpha, float* __restrict__ g_e) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= B) return;
+  const int64_t n0 = node_off[g], n1 = node_off[g + 1];
+  float4 q[NV], gr[NV], gq[NV];
+  bool ok[NV];
+  float cpart = 0.f;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    ok[c] = col < D;
+    q[c] = ok[c] ? ld4(qstar + g * ldq + col) : make_float4(0, 0, 0, 0);
+    gr[c] = ok[c] ? ld4(g_qstar + g * ldgq + D + col) : make_float4(0, 0, 0, 0);
+    const float4 rr = ok[c] ? ld4(qstar + g * ldq + D + col) : make_float4(0, 0, 0, 0);
+    cpart += dot4(rr, gr[c]);
+    gq[c] = make_float4(0, 0, 0, 0);
+  }
+  const float cdot = wave_sum(cpart);  // sum_n alpha_n <x_n, g_r> = <r, g_r>
+  const float L = lse[g];
+  for (int64_t n = n0; n < n1; ++n) {
+    float4 x[NV];
+    float pe = 0.f, pa = 0.f;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      x[c] = ok[c] ? ld4(X + n * D + 4 * (lane + 64 * c)) : make_float4(0, 0, 0, 0);
+      pe += dot4(x[c], q[c]);
+      pa += dot4(x[c], gr[c]);
+    }
+    const float e = wave_sum(pe);
+    const float ga = wave_sum(pa);
+    const float al = expf(e - L);
+    const float ge = al * (ga - cdot);
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      gq[c].x += ge * x[c].x;
+      gq[c].y += ge * x[c].y;
+      gq[c].z += ge * x[c].z;
+      gq[c].w += ge * x[c].w;
+    }
+    if (lane == 0) {
+      alpha[n] = al;
+      g_e[n] = ge;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NV; ++c)
+    if (ok[c]) {
+      const int col = 4 * (lane + 64 * c);
+      const float4 gd = ld4(g_qstar + g * ldgq + col);
+      st4(g_q + g * ldgout + col,
+          make_float4(gd.x + gq[c].x, gd.y + gq[c].y, gd.z + gq[c].z, gd.w + gq[c].w));
+    }
+}
+
+// One wave per node: gX[n] = sum_t alpha_t[n] * g_r_t[g] + g_e_t[n] * q_t[g].
+template <int NV>
+__global__ void __launch_bounds__(256)
+seg_gx_kernel(int64_t N, int D, int T, const int32_t* __restrict__ node_graph,
+              const float* __restrict__ qstars, int64_t ldq, int64_t qs_stride,
+              const float* __restrict__ g_qstars, int64_t ldgq, int64_t gqs_stride,
+              const float* __restrict__ alphas, const float* __restrict__ g_es,
+              float* __restrict__ gX) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const int64_t g = node_graph[n];
+  float4 acc[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) acc[c] = make_float4(0, 0, 0, 0);
+  for (int t = 0; t < T; ++t) {
+    const float al = alphas[(int64_t)t * N + n];
+    const float ge = g_es[(int64_t)t * N + n];
+    const float* q = qstars + t * qs_stride + g * ldq;
+    const float* gr = g_qstars + t * gqs_stride + g * ldgq + D;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int col = 4 * (lane + 64 * c);
+      if (col < D) {
+        const float4 a = ld4(gr + col), b = ld4(q + col);
+        acc[c].x += al * a.x + ge * b.x;
+        acc[c].y += al * a.y + ge * b.y;
+        acc[c].z += al * a.z + ge * b.z;
+        acc[c].w += al * a.w + ge * b.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    if (col < D) st4(gX + n * D + col, acc[c]);
+  }
+}
+
+unsigned grid_for(int64_t total) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(total, 256), 16384));
+}
+
+int check_d(int D, const char* who) {
+  MVML_REQUIRE(D > 0 && D % 4 == 0 && D <= 1024, "%s: feature size must be a multiple of 4 <= 1024 (got %d)", who, D);
+  return MVML_OK;
+}
+
+}  // namespace
+}  // namespace mvml
+
+using namespace mvml;
+
+#define MVML_NV_SWITCH(KERNEL, GRID, ...)                                                   \
+  switch ((int)ceil_div(D, 256)) {                                                          \
+    case 1: KERNEL<1><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                            \
+    case 2: KERNEL<2><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                            \
+    case 3: KERNEL<3><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                            \
+    default: KERNEL<4><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                           \
+  }
+
+extern "C" int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_ih,
+                                  const float* b_hh, const float* c_prev, float* c_out,
+                                  float* h_out, int64_t ldh, float* act_out, void* stream) {
+  clear_error();
+  MVML_REQUIRE(B >= 0 && D > 0 && ldh >= D, "lstm_cell_fwd: bad shape");
+  if (B == 0) return MVML_OK;
+  hipStream_t st = as_stream(stream);
+  lstm_cell_fwd_kernel<<<grid_for(B * D), 256, 0, st>>>(B, D, gates_pre, b_ih, b_hh, c_prev, c_out,
+                                                        h_out, ldh, act_out);
+  return check_launch("lstm_cell_fwd_kernel");
+}
+
+extern "C" int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const float* c,
+                                  const float* c_prev, const float* g_h, int64_t ldgh,
+                                  const float* g_c, float* g_gates, float* g_c_prev, void* stream) {
+  clear_error();
+  MVML_REQUIRE(B >= 0 && D > 0 && ldgh >= D, "lstm_cell_bwd: bad shape");
+  if (B == 0) return MVML_OK;
+  hipStream_t st = as_stream(stream);
+  lstm_cell_bwd_kernel<<<grid_for(B * D), 256, 0, st>>>(B, D, act, c, c_prev, g_h, ldgh, g_c,
+                                                        g_gates, g_c_prev);
+  return check_launch("lstm_cell_bwd_kernel");
+}
+
+extern "C" int mvml_set2set_seg_fwd(int64_t B, int D, const int64_t* node_offsets, const float* X,
+                                    float* qstar, int64_t ldq, float* lse, void* stream) {
+  clear_error();
+  int rc = check_d(D, "set2set_seg_fwd");
+  if (rc) return rc;
+  MVML_REQUIRE(ldq >= 2 * D && ldq % 4 == 0, "set2set_seg_fwd: bad ldq");
+  if (B == 0) return MVML_OK;
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = (unsigned)ceil_div(B, 4);
+  MVML_NV_SWITCH(seg_fwd_kernel, grid, B, D, node_offsets, X, qstar, ldq, lse)
+  return check_launch("seg_fwd_kernel");
+}
+
+extern "C" int mvml_set2set_seg_bwd(int64_t B, int D, const int64_t* node_offsets, const float* X,
+                                    const float* qstar, int64_t ldq, const float* lse,
+                                    const float* g_qstar, int64_t ldgq, float* g_q,
+                                    int64_t ldgout, float* alpha, float* g_e, void* stream) {
+  clear_error();
+  int rc = check_d(D, "set2set_seg_bwd");
+  if (rc) return rc;
+  MVML_REQUIRE(ldq >= 2 * D && ldgq >= 2 * D && ldgout >= D, "set2set_seg_bwd: bad ld");
+  if (B == 0) return MVML_OK;
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = (unsigned)ceil_div(B, 4);
+  MVML_NV_SWITCH(seg_bwd_kernel, grid, B, D, node_offsets, X, qstar, ldq, lse, g_qstar, ldgq, g_q,
+                 ldgout, alpha, g_e)
+  return check_launch("seg_bwd_kernel");
+}
+
+extern "C" int mvml_set2set_gx(int64_t num_nodes, int D, int T, const int32_t* node_graph,
+                               const float* qstars, int64_t ldq, int64_t qstar_stride,
+                               const float* g_qstars, int64_t ldgq, int64_t g_qstar_stride,
+                               const float* alphas, const float* g_es, float* gX, void* stream) {
+  clear_error();
+  int rc = check_d(D, "set2set_gx");
+  if (rc) return rc;
+  MVML_REQUIRE(T >= 0 && ldq >= 2 * D && ldgq >= 2 * D, "set2set_gx: bad shape");
+  if (num_nodes == 0) return MVML_OK;
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = (unsigned)ceil_div(num_nodes, 4);
+  MVML_NV_SWITCH(seg_gx_kernel, grid, num_nodes, D, T, node_graph, qstars, ldq, qstar_stride,
+                 g_qstars, ldgq, g_qstar_stride, alphas, g_es, gX)
+  return check_launch("seg_gx_kernel");
+}

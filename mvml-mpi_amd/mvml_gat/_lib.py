@@ -1,0 +1,129 @@
+"""ctypes binding of libmvml_gat.so (the C ABI declared in include/mvml_gat.h).
+
+The argument types of every entry point are parsed from the header itself, so the binding
+cannot drift from the ABI.  There is deliberately no fallback: if the shared library is
+missing or fails to load, every op raises.
+"""
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  (import first: the library then binds torch's HIP runtime)
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MVML_GAT_LIB", os.path.join(_PKG, "libmvml_gat.so"))
+HEADER_PATH = os.path.normpath(os.path.join(_PKG, "..", "..", "include", "mvml_gat.h"))
+
+_CTYPE = {
+    "int64_t": ctypes.c_int64,
+    "int": ctypes.c_int,
+    "float": ctypes.c_float,
+    "size_t": ctypes.c_size_t,
+    "void": None,
+}
+
+
+def _strip_comments(text):
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    return re.sub(r"//[^\n]*", " ", text)
+
+
+def parse_header(path=HEADER_PATH):
+    """Return {name: (restype, [argtypes])} for every mvml_* prototype in the header."""
+    with open(path) as f:
+        text = _strip_comments(f.read())
+    protos = {}
+    for m in re.finditer(r"([A-Za-z_][\w\s\*]*?)\b(mvml_\w+)\s*\(([^)]*)\)\s*;", text):
+        ret, name, args = m.group(1).strip(), m.group(2), m.group(3).strip()
+        protos[name] = (_ctype_of(ret, is_ret=True), [_ctype_of(a) for a in _split_args(args)])
+    return protos
+
+
+def _split_args(args):
+    if args in ("", "void"):
+        return []
+    return [a.strip() for a in args.split(",")]
+
+
+def _ctype_of(decl, is_ret=False):
+    if "*" in decl:
+        if is_ret and "char" in decl:
+            return ctypes.c_char_p
+        return ctypes.c_void_p
+    toks = [t for t in decl.replace("const", " ").split() if t]
+    base = toks[0]
+    if base not in _CTYPE:
+        raise ValueError(f"unsupported type in header: {decl!r}")
+    return _CTYPE[base]
+
+
+class MvmlError(RuntimeError):
+    pass
+
+
+_lib = None
+_protos = None
+
+
+def lib():
+    """Load (once) and return the ctypes library with argtypes set from the header."""
+    global _lib, _protos
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MvmlError(
+            f"libmvml_gat.so not found at {LIB_PATH}: build it with "
+            "`python mvml-mpi_amd/build.py` (or __graft_entry__.build()); there is no CPU fallback")
+    handle = ctypes.CDLL(LIB_PATH)
+    protos = parse_header()
+    for name, (res, args) in protos.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib, _protos = handle, protos
+    return _lib
+
+
+def exported_symbols():
+    lib()
+    return sorted(_protos)
+
+
+def call(name, *args):
+    """Invoke an int-returning entry point; raise MvmlError with mvml_last_error() on failure."""
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if rc != 0:
+        msg = lib().mvml_last_error().decode(errors="replace")
+        raise MvmlError(f"{name} failed (status {rc}): {msg}")
+
+
+def ptr(t):
+    """Raw device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+_ws = {}
+
+
+def workspace(nbytes, device):
+    """Per-device scratch buffer (stream-ordered reuse through the caching allocator)."""
+    key = torch.device(device).index or 0
+    buf = _ws.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _ws[key] = buf
+    return buf
+
+
+def ws_ptr_size(nbytes, device):
+    if nbytes == 0:
+        return None, 0
+    buf = workspace(nbytes, device)
+    return ctypes.c_void_p(buf.data_ptr()), buf.numel()

@@ -1,0 +1,219 @@
+"""Molecule graphs and device-side batching (replaces dgl.graph / dgl.batch for this path).
+
+Reference call sites: ``mol_to_bigraph(mol, add_self_loop=True, ...)`` (dataset.py:34-35),
+``dgl.batch(graphs)`` in ``collate`` (dataset.py:52-54), ``batch_graph.to(device)`` and
+``batch_graph.ndata['h']`` (main.py:27-30), and the DGLGraph methods Set2Set / GATConv use
+(``batch_size``, ``batch_num_nodes()``, ``in_degrees()``).
+
+``BatchedMolGraph.to('cuda')`` uploads the per-graph LOCAL edge lists once and builds every
+index on the device with ``mvml_build_csr`` (global src/dst bit-identical to dgl.batch, in-CSR
+and out-CSR stable in edge id, atom -> molecule map).  GraphNorm groups (``group_offsets``)
+let one launch cover many reference mini-batches: by default the whole batch is one group,
+which is what model.py:93 does with ``batch=None``.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+
+
+class MolGraph:
+    """One molecule as a directed graph with local int32 ids (what mol_to_bigraph returns)."""
+
+    def __init__(self, num_nodes, src, dst, ndata=None):
+        self._num_nodes = int(num_nodes)
+        self.src = np.ascontiguousarray(src, dtype=np.int32)
+        self.dst = np.ascontiguousarray(dst, dtype=np.int32)
+        if self.src.shape != self.dst.shape:
+            raise ValueError("src and dst must have the same length")
+        self.ndata = dict(ndata or {})
+
+    def num_nodes(self):
+        return self._num_nodes
+
+    def num_edges(self):
+        return int(self.src.shape[0])
+
+    def edges(self):
+        return self.src, self.dst
+
+
+def graph(data, num_nodes=None, ndata=None):
+    """dgl.graph((src, dst), num_nodes=...) for one molecule."""
+    src, dst = data
+    src = np.asarray(src)
+    dst = np.asarray(dst)
+    if num_nodes is None:
+        num_nodes = int(max(src.max(initial=-1), dst.max(initial=-1)) + 1)
+    return MolGraph(num_nodes, src, dst, ndata)
+
+
+def bigraph_from_bonds(num_atoms, bonds, node_feats=None, add_self_loop=True):
+    """dgllife construct_bigraph_from_mol edge order (dataset.py:34): for bond i,
+    (u_i -> v_i), (v_i -> u_i); then one self-loop per atom when add_self_loop."""
+    bonds = np.asarray(bonds, dtype=np.int32).reshape(-1, 2)
+    nb = bonds.shape[0]
+    ns = num_atoms if add_self_loop else 0
+    src = np.empty(2 * nb + ns, dtype=np.int32)
+    dst = np.empty(2 * nb + ns, dtype=np.int32)
+    src[0:2 * nb:2], dst[0:2 * nb:2] = bonds[:, 0], bonds[:, 1]
+    src[1:2 * nb:2], dst[1:2 * nb:2] = bonds[:, 1], bonds[:, 0]
+    if add_self_loop:
+        src[2 * nb:] = np.arange(num_atoms, dtype=np.int32)
+        dst[2 * nb:] = np.arange(num_atoms, dtype=np.int32)
+    ndata = {} if node_feats is None else {"h": torch.as_tensor(node_feats, dtype=torch.float32)}
+    return MolGraph(num_atoms, src, dst, ndata)
+
+
+class BatchedMolGraph:
+    """A batch of molecule graphs (dgl.batch result) with device-built CSR indices.
+
+    Host-side state: per-graph counts and concatenated LOCAL edge lists (numpy).
+    After ``.to(cuda_device)``: ``src``, ``dst`` (global int32), ``node_offsets``,
+    ``edge_offsets`` (int64[B+1]), ``node_graph`` (int32[N]), ``in_rowptr``/``in_src``/
+    ``in_eid`` (in-CSR), ``out_rowptr``/``out_dst``/``out_inslot`` (out-CSR) and
+    ``group_offsets`` (int64[G+1], GraphNorm groups in molecules) are device tensors.
+    """
+
+    def __init__(self, batch_num_nodes, batch_num_edges, src_local, dst_local, ndata=None,
+                 group_size=None):
+        self._bnn = np.ascontiguousarray(batch_num_nodes, dtype=np.int64)
+        self._bne = np.ascontiguousarray(batch_num_edges, dtype=np.int64)
+        self.src_local = np.ascontiguousarray(src_local, dtype=np.int32)
+        self.dst_local = np.ascontiguousarray(dst_local, dtype=np.int32)
+        if self._bnn.shape != self._bne.shape:
+            raise ValueError("batch_num_nodes / batch_num_edges length mismatch")
+        if int(self._bne.sum()) != self.src_local.shape[0] or self.src_local.shape != self.dst_local.shape:
+            raise ValueError("edge lists do not match batch_num_edges")
+        self.ndata = dict(ndata or {})
+        self.device = torch.device("cpu")
+        self.group_size = group_size
+        self._dev = None
+        self.has_zero_in_degree = None
+
+    # ---- DGLGraph-like API used by the reference ----
+    @property
+    def batch_size(self):
+        return int(self._bnn.shape[0])
+
+    def batch_num_nodes(self):
+        return torch.as_tensor(self._bnn)
+
+    def batch_num_edges(self):
+        return torch.as_tensor(self._bne)
+
+    def num_nodes(self):
+        return int(self._bnn.sum())
+
+    def num_edges(self):
+        return int(self._bne.sum())
+
+    def edges(self):
+        if self._dev is not None:
+            return self._dev["src"], self._dev["dst"]
+        off = np.concatenate([[0], np.cumsum(self._bnn)])
+        shift = np.repeat(off[:-1], self._bne)
+        return (torch.as_tensor(self.src_local.astype(np.int64) + shift).int(),
+                torch.as_tensor(self.dst_local.astype(np.int64) + shift).int())
+
+    def in_degrees(self):
+        _, dst = self.edges()
+        return torch.bincount(dst.long().cpu(), minlength=self.num_nodes())
+
+    def group_offsets_host(self):
+        B = self.batch_size
+        gs = self.group_size or max(B, 1)
+        offs = list(range(0, B, gs)) + [B]
+        return np.asarray(offs if B > 0 else [0, 0], dtype=np.int64)
+
+    def set_group_size(self, group_size):
+        """GraphNorm groups of `group_size` consecutive molecules (None = whole batch)."""
+        self.group_size = group_size
+        if self._dev is not None:
+            self._dev["group_offsets"] = torch.as_tensor(self.group_offsets_host(), device=self.device)
+            self._dev["group_node_offsets"] = None
+        return self
+
+    def __getattr__(self, name):
+        dev = self.__dict__.get("_dev")
+        if dev is not None and name in dev:
+            return dev[name]
+        raise AttributeError(name)
+
+    # ---- device build ----
+    def to(self, device):
+        device = torch.device(device)
+        if device.type != "cuda":
+            self.device = device
+            self.ndata = {k: v.to(device) for k, v in self.ndata.items()}
+            return self
+        with torch.cuda.device(device):
+            self._build_device(device)
+        self.device = device
+        self.ndata = {k: v.to(device, non_blocking=True) for k, v in self.ndata.items()}
+        return self
+
+    def _build_device(self, device):
+        B, N, E = self.batch_size, self.num_nodes(), self.num_edges()
+        if N >= 2 ** 31 or E >= 2 ** 31:
+            raise ValueError("batch too large for int32 indices")
+        i32 = dict(dtype=torch.int32, device=device)
+        i64 = dict(dtype=torch.int64, device=device)
+        bnn = torch.as_tensor(self._bnn).to(device)
+        bne = torch.as_tensor(self._bne).to(device)
+        src_l = torch.as_tensor(self.src_local).to(device)
+        dst_l = torch.as_tensor(self.dst_local).to(device)
+        d = dict(
+            node_offsets=torch.empty(B + 1, **i64), edge_offsets=torch.empty(B + 1, **i64),
+            src=torch.empty(E, **i32), dst=torch.empty(E, **i32), node_graph=torch.empty(N, **i32),
+            in_rowptr=torch.empty(N + 1, **i32), in_src=torch.empty(E, **i32),
+            in_eid=torch.empty(E, **i32), out_rowptr=torch.empty(N + 1, **i32),
+            out_dst=torch.empty(E, **i32), out_inslot=torch.empty(E, **i32))
+        flags = torch.zeros(2, **i32)
+        L = _lib.lib()
+        wsz = L.mvml_build_csr_workspace_size(B, N, E)
+        wp, wn = _lib.ws_ptr_size(wsz, device)
+        P = _lib.ptr
+        _lib.call("mvml_build_csr", P(src_l), P(dst_l), P(bnn), P(bne), B, N, E,
+                  P(d["node_offsets"]), P(d["edge_offsets"]), P(d["src"]), P(d["dst"]),
+                  P(d["node_graph"]), P(d["in_rowptr"]), P(d["in_src"]), P(d["in_eid"]),
+                  P(d["out_rowptr"]), P(d["out_dst"]), P(d["out_inslot"]), P(flags), wp, wn,
+                  _lib.stream_ptr(device))
+        fl = flags.cpu().numpy()  # one sync per batch (DGL's GATConv also syncs on in_degrees)
+        if fl[1] != 0:
+            raise ValueError(f"{int(fl[1])} edges reference node ids outside their graph")
+        self.has_zero_in_degree = bool(fl[0] > 0)
+        d["group_offsets"] = torch.as_tensor(self.group_offsets_host()).to(device)
+        d["group_node_offsets"] = None
+        # keep the uploaded inputs alive until the stream has consumed them
+        d["_inputs"] = (bnn, bne, src_l, dst_l)
+        self._dev = d
+
+    def group_offsets_rows(self):
+        """GraphNorm group offsets in molecules (rows of the (B, 2D) readout)."""
+        if self._dev is None:
+            return torch.as_tensor(self.group_offsets_host())
+        return self._dev["group_offsets"]
+
+
+def batch(graphs, group_size=None):
+    """dgl.batch (dataset.py:54): concatenate graphs; node features under ndata['h'] are
+    concatenated too."""
+    graphs = list(graphs)
+    bnn = np.array([g.num_nodes() for g in graphs], dtype=np.int64)
+    bne = np.array([g.num_edges() for g in graphs], dtype=np.int64)
+    src = np.concatenate([g.src for g in graphs]) if graphs else np.zeros(0, np.int32)
+    dst = np.concatenate([g.dst for g in graphs]) if graphs else np.zeros(0, np.int32)
+    ndata = {}
+    keys = set.intersection(*[set(g.ndata) for g in graphs]) if graphs else set()
+    for k in keys:
+        ndata[k] = torch.cat([torch.as_tensor(g.ndata[k]) for g in graphs], 0)
+    return BatchedMolGraph(bnn, bne, src, dst, ndata, group_size=group_size)
+
+
+def from_arrays(batch_num_nodes, batch_num_edges, src_local, dst_local, node_feats=None,
+                group_size=None):
+    """Build a batch directly from concatenated local edge lists (the synthetic generators)."""
+    ndata = {} if node_feats is None else {"h": torch.as_tensor(node_feats)}
+    return BatchedMolGraph(batch_num_nodes, batch_num_edges, src_local, dst_local, ndata,
+                           group_size=group_size)

@@ -1,0 +1,298 @@
+"""torch.autograd.Functions over the HIP kernels of libmvml_gat.so.
+
+Each Function owns one stage of GNNModule (model.py:89-95) and calls only the C ABI; there is
+no PyTorch math on the hot path besides allocation (and nn.Dropout, which the reference
+applies with torch's own RNG, model.py:87).
+"""
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+
+MODE_FLATTEN_ELU, MODE_MEAN, MODE_FLATTEN = 0, 1, 2
+
+
+def _check_cuda_f32(t, name):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a CUDA (HIP) tensor: the mvml_gat path has no CPU fallback")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _stream(dev):
+    return _lib.stream_ptr(dev)
+
+
+def _round4(x):
+    return (x + 3) // 4 * 4
+
+
+def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0):
+    """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32)."""
+    L = _lib.lib()
+    dev = C.device
+    wsz = L.mvml_gemm_workspace_size(M, N, K)
+    wp, wn = _lib.ws_ptr_size(wsz, dev)
+    call("mvml_gemm_f32", int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda, ptr(B), ldb,
+         ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
+
+
+def colsum(X, M, N, ldx, out, beta=0.0, offset=0):
+    L = _lib.lib()
+    dev = out.device
+    wp, wn = _lib.ws_ptr_size(L.mvml_colsum_workspace_size(M, N), dev)
+    xp = ptr(X).value + 4 * offset
+    import ctypes
+    call("mvml_colsum_f32", M, N, ctypes.c_void_p(xp), ldx, float(beta), ptr(out), wp, wn, _stream(dev))
+
+
+class GATLayerFunction(torch.autograd.Function):
+    """dgllife GATLayer(GATConv) forward/backward: projection GEMM (fc, res_fc, el, er folded
+    into one MFMA GEMM) + fused attention/softmax/aggregation/residual/bias/agg kernel."""
+
+    @staticmethod
+    def forward(ctx, X, fc_w, res_w, attn_l, attn_r, bias, g, H, F, slope, mode):
+        for t, n in ((X, "feat"), (fc_w, "fc.weight"), (res_w, "res_fc.weight")):
+            _check_cuda_f32(t, n)
+        X = _c(X)
+        N, Fin = X.shape
+        dev = X.device
+        HF = H * F
+        C = 2 * HF + 2 * H
+        ldy = _round4(C)
+        st = _stream(dev)
+        Wcat = torch.empty((C, Fin), dtype=torch.float32, device=dev)
+        call("mvml_gat_fold_weights", ptr(_c(fc_w)), ptr(_c(res_w)), ptr(_c(attn_l)), ptr(_c(attn_r)),
+             H, F, Fin, ptr(Wcat), st)
+        Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
+        gemm(X, Wcat, N, C, Fin, 0, 0, Fin, Fin, Y, ldy)
+        out_cols = F if mode == MODE_MEAN else HF
+        out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
+        E = g.num_edges()
+        attn = torch.empty((E, H), dtype=torch.float32, device=dev)
+        call("mvml_gat_agg_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F, ptr(_c(bias)),
+             float(slope), int(mode), ptr(out), ptr(attn), st)
+        ctx.save_for_backward(X, Wcat, Y, attn, out, fc_w, attn_l, attn_r)
+        ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode, ctx.ldy = g, H, F, slope, mode, ldy
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        X, Wcat, Y, attn, out, fc_w, attn_l, attn_r = ctx.saved_tensors
+        g, H, F, mode, ldy = ctx.g, ctx.H, ctx.F, ctx.mode, ctx.ldy
+        g_out = _c(g_out)
+        N, Fin = X.shape
+        dev = X.device
+        HF = H * F
+        C = 2 * HF + 2 * H
+        st = _stream(dev)
+        L = _lib.lib()
+        gY = torch.empty((N, ldy), dtype=torch.float32, device=dev)
+        wp, wn = _lib.ws_ptr_size(L.mvml_gat_agg_bwd_workspace_size(g.num_edges(), H), dev)
+        call("mvml_gat_agg_bwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr),
+             ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(attn), ptr(out), ptr(g_out), H, F,
+             float(ctx.slope), int(mode), ptr(gY), ldy, wp, wn, st)
+        # dL/dWcat = gY^T X  (split-K over atoms)
+        gW = torch.empty((C, Fin), dtype=torch.float32, device=dev)
+        gemm(gY, X, C, Fin, N, 1, 1, ldy, Fin, gW, Fin)
+        g_fc = torch.empty_like(fc_w)
+        g_res = torch.empty_like(fc_w)
+        g_al = torch.empty_like(attn_l)
+        g_ar = torch.empty_like(attn_r)
+        call("mvml_gat_unfold_grads", ptr(gW), ptr(_c(fc_w)), ptr(_c(attn_l)), ptr(_c(attn_r)), H, F, Fin,
+             ptr(g_fc), ptr(g_res), ptr(g_al), ptr(g_ar), st)
+        g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
+        colsum(gY, N, HF, ldy, g_bias, offset=HF)
+        gX = None
+        if ctx.needs_input_grad[0]:
+            gX = torch.empty((N, Fin), dtype=torch.float32, device=dev)
+            gemm(gY, Wcat, N, Fin, C, 0, 1, ldy, Fin, gX, Fin)
+        return gX, g_fc, g_res, g_al, g_ar, g_bias, None, None, None, None, None
+
+
+class Set2SetFunction(torch.autograd.Function):
+    """dgl Set2Set.forward (model.py:92): n_iters x {n_layers LSTM cell steps, fused segment
+    softmax readout}.  LSTM gates: two MFMA GEMMs per cell + pointwise kernel."""
+
+    @staticmethod
+    def forward(ctx, X, g, n_iters, n_layers, *lstm_params):
+        _check_cuda_f32(X, "feat")
+        X = _c(X)
+        N, D = X.shape
+        B = g.batch_size
+        dev = X.device
+        st = _stream(dev)
+        T, Lr = n_iters, n_layers
+        W = [tuple(_c(p) for p in lstm_params[4 * l:4 * l + 4]) for l in range(Lr)]  # w_ih, w_hh, b_ih, b_hh
+        f32 = dict(dtype=torch.float32, device=dev)
+        qstars = torch.empty((T, B, 2 * D), **f32)
+        acts = torch.empty((T, Lr, B, 4 * D), **f32)
+        cs = torch.empty((T, Lr, B, D), **f32)
+        hs = torch.empty((T, max(Lr - 1, 1), B, D), **f32)  # non-top layer outputs
+        lse = torch.empty((T, B), **f32)
+        gates = torch.empty((B, 4 * D), **f32)
+        for t in range(T):
+            for l in range(Lr):
+                w_ih, w_hh, b_ih, b_hh = W[l]
+                kin = 2 * D if l == 0 else D
+                if l == 0:
+                    x, ldx, x_zero = (qstars[t - 1] if t > 0 else None), 2 * D, t == 0
+                else:
+                    x, ldx, x_zero = hs[t, l - 1], D, False
+                if t > 0:
+                    hp, ldhp = (qstars[t - 1] if l == Lr - 1 else hs[t - 1, l]), (2 * D if l == Lr - 1 else D)
+                else:
+                    hp = None
+                if x_zero:
+                    gates.zero_()
+                    beta = 1.0
+                else:
+                    gemm(x, w_ih, B, 4 * D, kin, 0, 0, ldx, kin, gates, 4 * D)
+                    beta = 1.0
+                if hp is not None:
+                    gemm(hp, w_hh, B, 4 * D, D, 0, 0, ldhp, D, gates, 4 * D, beta=beta)
+                if l == Lr - 1:
+                    h_out, ldh = qstars[t], 2 * D
+                else:
+                    h_out, ldh = hs[t, l], D
+                c_prev = cs[t - 1, l] if t > 0 else None
+                call("mvml_lstm_cell_fwd", B, D, ptr(gates), ptr(b_ih), ptr(b_hh), ptr(c_prev),
+                     ptr(cs[t, l]), ptr(h_out), ldh, ptr(acts[t, l]), st)
+            call("mvml_set2set_seg_fwd", B, D, ptr(g.node_offsets), ptr(X), ptr(qstars[t]), 2 * D,
+                 ptr(lse[t]), st)
+        ctx.save_for_backward(X, qstars, acts, cs, hs, lse, *[p for w in W for p in w])
+        ctx.g, ctx.T, ctx.Lr = g, T, Lr
+        return qstars[T - 1].clone()
+
+    @staticmethod
+    def backward(ctx, g_out):
+        X, qstars, acts, cs, hs, lse, *flat = ctx.saved_tensors
+        g, T, Lr = ctx.g, ctx.T, ctx.Lr
+        W = [tuple(flat[4 * l:4 * l + 4]) for l in range(Lr)]
+        N, D = X.shape
+        B = g.batch_size
+        dev = X.device
+        st = _stream(dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        g_qstars = torch.empty((T, B, 2 * D), **f32)
+        g_qstars[T - 1].copy_(g_out)
+        alphas = torch.empty((T, N), **f32)
+        g_es = torch.empty((T, N), **f32)
+        gW_ih = [torch.zeros_like(w[0]) for w in W]
+        gW_hh = [torch.zeros_like(w[1]) for w in W]
+        gb = [torch.zeros_like(w[2]) for w in W]
+        g_gates = torch.empty((B, 4 * D), **f32)
+        g_h = torch.empty((B, D), **f32)
+        g_hrec = [torch.zeros((B, D), **f32) for _ in range(Lr)]  # dL/dh_l(t-1) from step t
+        g_c = [torch.zeros((B, D), **f32) for _ in range(Lr)]
+        g_c_new = torch.empty((B, D), **f32)
+        g_below = torch.empty((B, D), **f32)  # dL/dh_{l-1}(t) from layer l's input
+        for t in range(T - 1, -1, -1):
+            # readout segment backward: dL/dq_t = g_qstar_t[:, :D] + segment term -> g_h
+            call("mvml_set2set_seg_bwd", B, D, ptr(g.node_offsets), ptr(X), ptr(qstars[t]), 2 * D,
+                 ptr(lse[t]), ptr(g_qstars[t]), 2 * D, ptr(g_h), D, ptr(alphas[t]), ptr(g_es[t]), st)
+            for l in range(Lr - 1, -1, -1):
+                w_ih, w_hh, b_ih, b_hh = W[l]
+                kin = 2 * D if l == 0 else D
+                gh = g_h if l == Lr - 1 else g_below
+                if t < T - 1:
+                    gh.add_(g_hrec[l])  # dL/dh_l(t) through the recurrence at step t+1
+                c_prev = cs[t - 1, l] if t > 0 else None
+                call("mvml_lstm_cell_bwd", B, D, ptr(acts[t, l]), ptr(cs[t, l]), ptr(c_prev), ptr(gh), D,
+                     ptr(g_c[l]) if t < T - 1 else None, ptr(g_gates), ptr(g_c_new), st)
+                g_c[l], g_c_new = g_c_new, g_c[l]
+                if l == 0:
+                    x, ldx = (qstars[t - 1], 2 * D) if t > 0 else (None, 0)  # q*_{-1} = 0
+                else:
+                    x, ldx = hs[t, l - 1], D
+                if x is not None:
+                    gemm(g_gates, x, 4 * D, kin, B, 1, 1, 4 * D, ldx, gW_ih[l], kin, beta=1.0)
+                if t > 0:
+                    hp, ldhp = (qstars[t - 1], 2 * D) if l == Lr - 1 else (hs[t - 1, l], D)
+                    gemm(g_gates, hp, 4 * D, D, B, 1, 1, 4 * D, ldhp, gW_hh[l], D, beta=1.0)
+                    gemm(g_gates, w_hh, B, D, 4 * D, 0, 1, 4 * D, D, g_hrec[l], D)
+                colsum(g_gates, B, 4 * D, 4 * D, gb[l], beta=1.0)
+                if l > 0:
+                    gemm(g_gates, w_ih, B, D, 4 * D, 0, 1, 4 * D, D, g_below, D)
+                elif t > 0:  # layer-0 input at step t is q*_{t-1}
+                    gemm(g_gates, w_ih, B, 2 * D, 4 * D, 0, 1, 4 * D, 2 * D, g_qstars[t - 1], 2 * D)
+        gX = torch.empty((N, D), **f32)
+        call("mvml_set2set_gx", N, D, T, ptr(g.node_graph), ptr(qstars), 2 * D, B * 2 * D,
+             ptr(g_qstars), 2 * D, B * 2 * D, ptr(alphas), ptr(g_es), ptr(gX), st)
+        grads = []
+        for l in range(Lr):
+            grads += [gW_ih[l], gW_hh[l], gb[l], gb[l].clone()]
+        return (gX, None, None, None, *grads)
+
+
+class GraphNormFunction(torch.autograd.Function):
+    """torch_geometric GraphNorm.forward(x, batch=None) (model.py:93), per group."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, mean_scale, group_offsets, eps):
+        _check_cuda_f32(x, "x")
+        x = _c(x)
+        G = group_offsets.numel() - 1
+        D = x.shape[1]
+        y = torch.empty_like(x)
+        call("mvml_graphnorm_fwd", G, D, ptr(group_offsets), ptr(x), ptr(_c(weight)), ptr(_c(bias)),
+             ptr(_c(mean_scale)), float(eps), ptr(y), _stream(x.device))
+        ctx.save_for_backward(x, weight, mean_scale, group_offsets)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    def backward(ctx, g_y):
+        x, weight, mean_scale, group_offsets = ctx.saved_tensors
+        g_y = _c(g_y)
+        G = group_offsets.numel() - 1
+        D = x.shape[1]
+        dev = x.device
+        L = _lib.lib()
+        gx = torch.empty_like(x)
+        gw = torch.empty_like(weight)
+        gb = torch.empty_like(weight)
+        gms = torch.empty_like(weight)
+        wp, wn = _lib.ws_ptr_size(L.mvml_graphnorm_bwd_workspace_size(G, D), dev)
+        call("mvml_graphnorm_bwd", G, D, ptr(group_offsets), ptr(x), ptr(_c(weight)), ptr(_c(mean_scale)),
+             float(ctx.eps), ptr(g_y), ptr(gx), ptr(gw), ptr(gb), ptr(gms), wp, wn, _stream(dev))
+        return gx, gw, gb, gms, None, None
+
+
+class LinearReLUFunction(torch.autograd.Function):
+    """nn.Linear + nn.ReLU of GNNModule.fc (model.py:86-87) as one MFMA GEMM with a bias+ReLU
+    epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        _check_cuda_f32(x, "x")
+        x = _c(x)
+        M, K = x.shape
+        Nout = weight.shape[0]
+        y = torch.empty((M, Nout), dtype=torch.float32, device=x.device)
+        gemm(x, _c(weight), M, Nout, K, 0, 0, K, K, y, Nout, bias=_c(bias), act=1)
+        ctx.save_for_backward(x, weight, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g_y):
+        x, weight, y = ctx.saved_tensors
+        g_y = _c(g_y)
+        M, K = x.shape
+        Nout = weight.shape[0]
+        dev = x.device
+        g_pre = torch.empty_like(y)
+        call("mvml_relu_bwd", y.numel(), ptr(y), ptr(g_y), ptr(g_pre), _stream(dev))
+        gw = torch.empty_like(weight)
+        gemm(g_pre, x, Nout, K, M, 1, 1, Nout, K, gw, K)
+        gb = torch.empty((Nout,), dtype=torch.float32, device=dev)
+        colsum(g_pre, M, Nout, Nout, gb)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            gemm(g_pre, _c(weight), M, K, Nout, 0, 1, Nout, K, gx, K)
+        return gx, gw, gb

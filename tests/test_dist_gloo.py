@@ -1,0 +1,88 @@
+"""world_size-2 gloo test of the data-parallel decomposition used by bench.py: each rank owns
+whole GraphNorm groups, runs forward/backward independently, then ONE flat all-reduce of the
+gradients reproduces the single-process gradient of the full batch."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mvml_gat.dist import FlatGradAllReduce, shard_groups
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup(seed=0):
+    from _util import batch_of_sizes, model_pair
+    sizes = [9, 12, 7, 15, 10, 8, 11, 6, 13, 5]  # 5 groups of 2 molecules
+    sb = batch_of_sizes(sizes, seed=seed)
+    _, ref = model_pair(hidden=(8, 12), seed=seed, n_iters=2, n_layers=2)
+    ref = ref.double().eval()
+    return sb, ref
+
+
+def _subbatch(sb, lo, hi):
+    from _util import graph_dict
+    from mvml_gat.synth import SynthBatch
+    e0, e1 = int(sb.num_edges[:lo].sum()), int(sb.num_edges[:hi].sum())
+    n0, n1 = int(sb.num_nodes[:lo].sum()), int(sb.num_nodes[:hi].sum())
+    s = SynthBatch(sb.num_nodes[lo:hi], sb.num_edges[lo:hi], sb.src_local[e0:e1],
+                   sb.dst_local[e0:e1], sb.feats[n0:n1])
+    return graph_dict(s, group_size=2), torch.as_tensor(s.feats, dtype=torch.float64)
+
+
+def _loss(model, gd, X, row0=0):
+    y = model(gd, X)
+    w = torch.arange(row0 * y.shape[1], row0 * y.shape[1] + y.numel(), dtype=y.dtype).view_as(y).sin()
+    return (y * w).sum()
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sb, ref = _setup()
+    costs = [int(sb.num_edges[2 * i:2 * i + 2].sum()) for i in range(5)]
+    g0, g1 = shard_groups(costs, world, rank)
+    gd, X = _subbatch(sb, 2 * g0, 2 * g1)
+    _loss(ref, gd, X, 2 * g0).backward()
+    FlatGradAllReduce(ref.parameters())()
+    if rank == 0:
+        out.put({n: p.grad.numpy().copy() for n, p in ref.named_parameters()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_flat_allreduce_matches_single_process():
+    sb, ref = _setup()
+    gd, X = _subbatch(sb, 0, 10)
+    _loss(ref, gd, X).backward()
+    want = {n: p.grad.clone() for n, p in ref.named_parameters()}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for n, g in want.items():
+        assert torch.allclose(torch.as_tensor(got[n]), g, rtol=1e-10, atol=1e-12), (n, (torch.as_tensor(got[n]) - g).abs().max().item(), g.abs().max().item())
+
+
+def test_shard_groups_balanced_and_covering():
+    costs = np.r_[np.full(10, 100), np.full(10, 1000)]
+    cuts = [shard_groups(costs, 4, r) for r in range(4)]
+    assert cuts[0][0] == 0 and cuts[-1][1] == 20
+    assert all(cuts[i][1] == cuts[i + 1][0] for i in range(3))
+    loads = [costs[a:b].sum() for a, b in cuts]
+    assert max(loads) <= 1.5 * (costs.sum() / 4)

@@ -1,0 +1,250 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on identical inputs.
+
+Bars (BASELINE.json north_star): bit-exact for batching/CSR indices; fp32 outputs and
+gradients within 1e-5 norm-wise relative error of the float64 oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from _util import batch_of_sizes, graph_dict, model_pair
+from conftest import rel_err
+from oracle import gnn_ref, graph_ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+TOL = 1e-5
+
+
+def _to_dev(sb, group_size=None):
+    return sb.to_graph(group_size=group_size).to(DEV)
+
+
+# ------------------------------------------------------------------ batching / CSR (bit-exact)
+@pytest.mark.parametrize("sizes,hubs", [
+    ([25] * 37, False),
+    ([11, 23, 80, 5, 1, 40, 23], False),
+    ([150, 300, 220], True),
+    ([1] * 5, False),
+])
+def test_build_csr_bit_exact(sizes, hubs):
+    sb = batch_of_sizes(sizes, seed=3, hubs=hubs)
+    g = _to_dev(sb)
+    ref = graph_ref.batch_ref(sb.num_nodes, sb.src_local, sb.dst_local, sb.num_edges)
+    csr = graph_ref.csr_ref(ref["src"], ref["dst"], ref["node_offsets"][-1])
+    for k in ("node_offsets", "edge_offsets", "src", "dst", "node_graph"):
+        np.testing.assert_array_equal(getattr(g, k).cpu().numpy(), ref[k], err_msg=k)
+    for k in ("in_rowptr", "in_src", "in_eid", "out_rowptr", "out_dst", "out_inslot"):
+        np.testing.assert_array_equal(getattr(g, k).cpu().numpy(), csr[k], err_msg=k)
+    assert g.has_zero_in_degree is False
+
+
+def test_build_csr_edge_cases():
+    from mvml_gat import batching as G
+    graphs = [
+        G.bigraph_from_bonds(3, [(0, 1), (1, 2)]),
+        G.MolGraph(0, [], []),                                      # empty molecule
+        G.graph(([0, 1, 2, 2], [1, 2, 0, 1]), num_nodes=4),         # node 3 has no in-edge
+        G.bigraph_from_bonds(5000, [(i, i + 1) for i in range(4999)]),  # > LDS histogram path
+    ]
+    bg = G.batch(graphs).to(DEV)
+    src, dst = bg.edges()
+    ref = graph_ref.batch_ref(bg._bnn, bg.src_local, bg.dst_local, bg._bne)
+    csr = graph_ref.csr_ref(ref["src"], ref["dst"], ref["node_offsets"][-1])
+    np.testing.assert_array_equal(src.cpu().numpy(), ref["src"])
+    for k in ("in_rowptr", "in_src", "in_eid", "out_rowptr", "out_dst", "out_inslot"):
+        np.testing.assert_array_equal(getattr(bg, k).cpu().numpy(), csr[k], err_msg=k)
+    assert bg.has_zero_in_degree is True and csr["zero_in_degree"] == 1
+
+
+def test_build_csr_rejects_bad_ids():
+    from mvml_gat import batching as G
+    bad = G.MolGraph(2, [0, 5], [1, 0])
+    with pytest.raises(ValueError):
+        G.batch([bad]).to(DEV)
+
+
+# ------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (130, 70, 74), (257, 300, 768), (96, 40, 20000)])
+def test_gemm_layouts(ak, bk, M, N, K):
+    from mvml_gat.functional import gemm
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(K, N, generator=g, dtype=torch.float64)
+    bias = torch.randn(N, generator=g, dtype=torch.float64)
+    C0 = torch.randn(M, N, generator=g, dtype=torch.float64)
+    Ad = (A.t() if ak else A).contiguous().float().to(DEV)
+    Bd = (B if bk else B.t()).contiguous().float().to(DEV)
+    C = C0.float().to(DEV)
+    gemm(Ad, Bd, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N, bias=bias.float().to(DEV),
+         beta=0.5, act=1)
+    ref = torch.relu(A @ B + bias + 0.5 * C0)
+    assert rel_err(C, ref) < TOL
+
+
+def test_colsum():
+    from mvml_gat.functional import colsum
+    X = torch.randn(5000, 37, dtype=torch.float64)
+    out = torch.ones(37, dtype=torch.float32, device=DEV)
+    colsum(X.float().to(DEV), 5000, 37, 37, out, beta=1.0)
+    assert rel_err(out, X.sum(0) + 1) < TOL
+
+
+# ------------------------------------------------------------------ GAT layers
+def _gat_case(layer, sb, seed=0):
+    torch.manual_seed(seed)
+    prod, ref = model_pair(seed=seed)
+    conv_p = prod.conv.gnn_layers[layer]
+    conv_r = ref.conv.gnn_layers[layer].gat_conv
+    Fin = 74 if layer == 0 else 768
+    X = torch.randn(int(sb.num_nodes.sum()), Fin, dtype=torch.float64)
+    if layer == 0:
+        X = torch.as_tensor(sb.feats, dtype=torch.float64) + 0.1 * X
+    gd = graph_dict(sb)
+    H, Fo = 4, (192 if layer == 0 else 384)
+    params = {"fc.weight": conv_r.fc.weight, "res_fc.weight": conv_r.res_fc.weight,
+              "attn_l": conv_r.attn_l, "attn_r": conv_r.attn_r, "bias": conv_r.bias}
+    params64 = {k: v.detach().double().requires_grad_() for k, v in params.items()}
+    Xr = X.clone().requires_grad_()
+    out_r = gnn_ref.gat_layer_ref(gd["src"], gd["dst"], Xr, params64, H, Fo,
+                                  "flatten" if layer == 0 else "mean",
+                                  torch.nn.functional.elu if layer == 0 else None)
+    gout = torch.randn_like(out_r)
+    out_r.backward(gout)
+
+    conv_p = conv_p.to(DEV)
+    g = _to_dev(sb)
+    Xp = X.float().to(DEV).requires_grad_()
+    out_p = conv_p(g, Xp)
+    out_p.backward(gout.float().to(DEV))
+    assert rel_err(out_p, out_r) < TOL, "forward"
+    assert rel_err(Xp.grad, Xr.grad) < TOL, "dX"
+    c = conv_p.gat_conv
+    for name, pp in (("fc.weight", c.fc.weight), ("res_fc.weight", c.res_fc.weight),
+                     ("attn_l", c.attn_l), ("attn_r", c.attn_r), ("bias", c.bias)):
+        assert rel_err(pp.grad, params64[name].grad) < TOL, name
+
+
+@pytest.mark.parametrize("layer", [0, 1])
+def test_gat_layer_parity(layer):
+    _gat_case(layer, batch_of_sizes([25, 11, 40, 23, 17, 3, 1], seed=5))
+
+
+def test_gat_layer_hubs_parity():
+    # in-degree > 64 exercises the multi-chunk softmax / backward paths
+    _gat_case(1, batch_of_sizes([150, 90], seed=7, hubs=True))
+
+
+# ------------------------------------------------------------------ readout / norm
+def test_set2set_parity():
+    from mvml_gat.nn import Set2Set
+    sb = batch_of_sizes([25, 1, 40, 7, 23], seed=9)
+    gd = graph_dict(sb)
+    torch.manual_seed(0)
+    s2s = Set2Set(384, 6, 3)
+    X = torch.randn(int(sb.num_nodes.sum()), 384, dtype=torch.float64)
+    lstm64 = torch.nn.LSTM(768, 384, 3).double()
+    lstm64.load_state_dict({k: v.double() for k, v in s2s.lstm.state_dict().items()})
+    Xr = X.clone().requires_grad_()
+    out_r = gnn_ref.set2set_ref(gd["node_offsets"], Xr, lstm64, 6)
+    gout = torch.randn_like(out_r)
+    out_r.backward(gout)
+    s2s = s2s.to(DEV)
+    Xp = X.float().to(DEV).requires_grad_()
+    out_p = s2s(_to_dev(sb), Xp)
+    out_p.backward(gout.float().to(DEV))
+    assert rel_err(out_p, out_r) < TOL
+    assert rel_err(Xp.grad, Xr.grad) < TOL
+    for (n, p), (n2, p2) in zip(s2s.lstm.named_parameters(), lstm64.named_parameters()):
+        assert rel_err(p.grad, p2.grad) < TOL, n
+
+
+def test_graphnorm_parity():
+    from mvml_gat.nn import GraphNorm
+    x = torch.randn(164, 768, dtype=torch.float64) * 3 + 1
+    gn = GraphNorm(768)
+    with torch.no_grad():
+        gn.weight.add_(torch.randn(768) * 0.1)
+        gn.bias.add_(torch.randn(768) * 0.1)
+        gn.mean_scale.add_(torch.randn(768) * 0.1)
+    offs = [0, 64, 128, 164]
+    w, b, ms = (p.detach().double().requires_grad_() for p in (gn.weight, gn.bias, gn.mean_scale))
+    xr = x.clone().requires_grad_()
+    yr = gnn_ref.graphnorm_ref(xr, w, b, ms, 1e-5, offs)
+    gy = torch.randn_like(yr)
+    yr.backward(gy)
+    gn = gn.to(DEV)
+    xp = x.float().to(DEV).requires_grad_()
+    yp = gn(xp, group_offsets=torch.tensor(offs, device=DEV))
+    yp.backward(gy.float().to(DEV))
+    assert rel_err(yp, yr) < TOL
+    assert rel_err(xp.grad, xr.grad) < TOL
+    for a, r in ((gn.weight, w), (gn.bias, b), (gn.mean_scale, ms)):
+        assert rel_err(a.grad, r.grad) < TOL
+
+
+# ------------------------------------------------------------------ full GNNModule
+def test_gnn_module_parity_eval_and_grads():
+    sb = batch_of_sizes([25, 11, 40, 23, 17, 3, 1, 60, 33], seed=11)
+    prod, ref = model_pair(seed=3)
+    prod.eval()
+    ref.eval()
+    ref64 = ref.double()
+    gd = graph_dict(sb)
+    X = torch.as_tensor(sb.feats, dtype=torch.float64)
+    out_r = ref64(gd, X)
+    gout = torch.randn_like(out_r)
+    out_r.backward(gout)
+    prod = prod.to(DEV)
+    g = _to_dev(sb)
+    out_p = prod(g, g.ndata["h"])
+    out_p.backward(gout.float().to(DEV))
+    assert rel_err(out_p, out_r) < TOL
+    pr = dict(ref64.named_parameters())
+    for n, p in prod.named_parameters():
+        assert rel_err(p.grad, pr[n].grad) < TOL, n
+
+
+def test_gnn_module_groups_equal_separate_batches():
+    """GraphNorm groups in one launch == the reference run batch by batch."""
+    sb = batch_of_sizes([20] * 5 + [30] * 4, seed=2)
+    prod, _ = model_pair(seed=4)
+    prod = prod.to(DEV).eval()
+    with torch.no_grad():
+        g = _to_dev(sb, group_size=5)
+        y_all = prod(g, g.ndata["h"])
+        from mvml_gat import from_arrays
+        ys = []
+        for lo, hi in ((0, 5), (5, 9)):
+            e0, e1 = int(sb.num_edges[:lo].sum()), int(sb.num_edges[:hi].sum())
+            n0, n1 = int(sb.num_nodes[:lo].sum()), int(sb.num_nodes[:hi].sum())
+            gi = from_arrays(sb.num_nodes[lo:hi], sb.num_edges[lo:hi], sb.src_local[e0:e1],
+                             sb.dst_local[e0:e1], sb.feats[n0:n1]).to(DEV)
+            ys.append(prod(gi, gi.ndata["h"]))
+    assert rel_err(y_all, torch.cat(ys)) < TOL
+
+
+def test_deterministic_bitwise():
+    sb = batch_of_sizes([25, 11, 40, 23], seed=1)
+    prod, _ = model_pair(seed=5)
+    prod = prod.to(DEV).eval()
+    res = []
+    for _ in range(2):
+        prod.zero_grad()
+        g = _to_dev(sb)
+        y = prod(g, g.ndata["h"])
+        y.sum().backward()
+        res.append([y.detach().clone()] + [p.grad.clone() for p in prod.parameters()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_zero_in_degree_raises():
+    from mvml_gat import batching as G
+    prod, _ = model_pair(seed=0)
+    prod = prod.to(DEV)
+    g = G.graph(([0], [1]), num_nodes=2, ndata={"h": torch.randn(2, 74)})
+    bg = G.batch([g]).to(DEV)
+    with pytest.raises(RuntimeError, match="0-in-degree"):
+        prod(bg, bg.ndata["h"])

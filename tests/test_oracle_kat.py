@@ -1,0 +1,184 @@
+"""Known-answer tests pinning the CPU oracle (oracle/) — hand-derivable cases from SURVEY.md
+§8c plus float64 gradchecks.  These are the only pins available: the reference ships no tests
+or fixtures and its third-party kernels (dgl/dgllife/PyG) are absent (parity unpinned)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_err
+from oracle import gnn_ref, graph_ref
+
+D64 = dict(dtype=torch.float64)
+
+
+def _params(Fin, H, Fo, seed=0, zero_attn=False):
+    g = torch.Generator().manual_seed(seed)
+    p = {"fc.weight": torch.randn(H * Fo, Fin, generator=g, **D64) * 0.3,
+         "res_fc.weight": torch.randn(H * Fo, Fin, generator=g, **D64) * 0.3,
+         "attn_l": torch.randn(1, H, Fo, generator=g, **D64) * 0.3,
+         "attn_r": torch.randn(1, H, Fo, generator=g, **D64) * 0.3,
+         "bias": torch.randn(H * Fo, generator=g, **D64) * 0.1}
+    if zero_attn:
+        p["attn_l"].zero_()
+        p["attn_r"].zero_()
+    return p
+
+
+def _conv(src, dst, X, p, H, Fo):
+    return gnn_ref.gatconv_ref(src, dst, X, p["fc.weight"], p["res_fc.weight"], p["attn_l"],
+                               p["attn_r"], p["bias"], H, Fo)
+
+
+def _mol(n, bonds):
+    return graph_ref.bigraph_edges(n, bonds)
+
+
+def test_zero_attention_is_mean_aggregation():
+    src, dst = _mol(4, [(0, 1), (1, 2), (2, 3), (3, 0)])
+    H, Fo, Fin = 2, 3, 5
+    p = _params(Fin, H, Fo, zero_attn=True)
+    X = torch.randn(4, Fin, **D64)
+    rst = _conv(src, dst, X, p, H, Fo)
+    Z = (X @ p["fc.weight"].t()).view(4, H, Fo)
+    R = (X @ p["res_fc.weight"].t()).view(4, H, Fo)
+    for v in range(4):
+        ins = [int(s) for s, d in zip(src, dst) if d == v]
+        exp = sum(Z[u] for u in ins) / len(ins) + R[v] + p["bias"].view(H, Fo)
+        assert torch.allclose(rst[v], exp, atol=1e-12)
+
+
+def test_isolated_atom_self_loop_only():
+    src, dst = _mol(1, [])
+    H, Fo, Fin = 4, 2, 3
+    p = _params(Fin, H, Fo, seed=1)
+    X = torch.randn(1, Fin, **D64)
+    rst, a = gnn_ref.gatconv_ref(src, dst, X, p["fc.weight"], p["res_fc.weight"], p["attn_l"],
+                                 p["attn_r"], p["bias"], H, Fo, return_attention=True)
+    assert torch.allclose(a, torch.ones_like(a))
+    exp = (X @ p["fc.weight"].t() + X @ p["res_fc.weight"].t()).view(1, H, Fo) + p["bias"].view(H, Fo)
+    assert torch.allclose(rst, exp, atol=1e-12)
+
+
+def test_two_atom_closed_form_softmax():
+    src, dst = _mol(2, [(0, 1)])  # edges: 0->1, 1->0, 0->0, 1->1
+    assert list(src) == [0, 1, 0, 1] and list(dst) == [1, 0, 0, 1]
+    H, Fo, Fin = 1, 3, 4
+    p = _params(Fin, H, Fo, seed=2)
+    X = torch.randn(2, Fin, **D64)
+    rst = _conv(src, dst, X, p, H, Fo)
+    Z = X @ p["fc.weight"].t()
+    el = Z @ p["attn_l"].view(-1)
+    er = Z @ p["attn_r"].view(-1)
+    lr = lambda x: x if x > 0 else 0.2 * x
+    s_10 = lr(float(el[1] + er[0]))  # 1 -> 0
+    s_00 = lr(float(el[0] + er[0]))  # 0 -> 0
+    a10 = 1.0 / (1.0 + math.exp(s_00 - s_10))
+    exp0 = a10 * Z[1] + (1 - a10) * Z[0] + X[0] @ p["res_fc.weight"].t() + p["bias"]
+    assert torch.allclose(rst[0, 0], exp0, atol=1e-12)
+
+
+def _lstm(D, layers=3, seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.LSTM(2 * D, D, layers).double()
+
+
+def test_permutation_equivariance_and_readout_invariance():
+    n = 6
+    bonds = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 0), (1, 4)]
+    perm = np.array([3, 0, 5, 1, 4, 2])  # new id of old atom i is perm[i]
+    src, dst = _mol(n, bonds)
+    src2, dst2 = _mol(n, [(perm[a], perm[b]) for a, b in bonds])
+    Fin = 7
+    X = torch.randn(n, Fin, **D64)
+    X2 = torch.empty_like(X)
+    X2[torch.as_tensor(perm)] = X
+    layers = [_params(Fin, 4, 3, seed=3), _params(12, 4, 5, seed=4)]
+    out = gnn_ref.gat_ref(src, dst, X, layers, [3, 5])
+    out2 = gnn_ref.gat_ref(src2, dst2, X2, layers, [3, 5])
+    assert torch.allclose(out2[torch.as_tensor(perm)], out, atol=1e-10)
+    lstm = _lstm(5)
+    r = gnn_ref.set2set_ref([0, n], out, lstm, 6)
+    r2 = gnn_ref.set2set_ref([0, n], out2, lstm, 6)
+    assert torch.allclose(r, r2, atol=1e-10)
+
+
+def test_single_atom_set2set_readout_is_the_atom():
+    D = 4
+    X = torch.randn(3, D, **D64)
+    lstm = _lstm(D, layers=1)
+    q = gnn_ref.set2set_ref([0, 1, 2, 3], X, lstm, 1)
+    assert torch.allclose(q[:, D:], X, atol=1e-12)
+
+
+def test_graphnorm_single_molecule_gives_bias():
+    x = torch.randn(1, 6, **D64)
+    w, b, ms = torch.rand(6, **D64) + 0.5, torch.randn(6, **D64), torch.ones(6, **D64)
+    y = gnn_ref.graphnorm_ref(x, w, b, ms, 1e-5)
+    assert torch.allclose(y, b.view(1, -1), atol=1e-12)
+
+
+def test_graphnorm_formula():
+    x = torch.randn(10, 3, **D64)
+    w, b, ms = torch.rand(3, **D64) + 0.5, torch.randn(3, **D64), torch.rand(3, **D64)
+    y = gnn_ref.graphnorm_ref(x, w, b, ms, 1e-5)
+    o = x - x.mean(0) * ms
+    exp = w * o / torch.sqrt((o ** 2).mean(0) + 1e-5) + b
+    assert torch.allclose(y, exp, atol=1e-12)
+
+
+def test_bigraph_reverse_edge_property():
+    n, bonds = 5, [(0, 1), (1, 2), (2, 3), (1, 4)]
+    src, dst = _mol(n, bonds)
+    nb = len(bonds)
+    for e in range(2 * nb):
+        assert src[e ^ 1] == dst[e] and dst[e ^ 1] == src[e]
+    for e in range(2 * nb, 2 * nb + n):
+        assert src[e] == dst[e] == e - 2 * nb
+
+
+def test_batch_equals_concatenation_for_gat():
+    mols = [(3, [(0, 1), (1, 2)]), (1, []), (4, [(0, 1), (1, 2), (2, 3), (3, 1)])]
+    Fin = 5
+    layers = [_params(Fin, 4, 2, seed=5), _params(8, 4, 3, seed=6)]
+    feats = [torch.randn(n, Fin, **D64) for n, _ in mols]
+    per = [gnn_ref.gat_ref(*_mol(n, b), f, layers, [2, 3]) for (n, b), f in zip(mols, feats)]
+    edges = [_mol(n, b) for n, b in mols]
+    bt = graph_ref.batch_ref([n for n, _ in mols], np.concatenate([e[0] for e in edges]),
+                             np.concatenate([e[1] for e in edges]), [len(e[0]) for e in edges])
+    out = gnn_ref.gat_ref(bt["src"], bt["dst"], torch.cat(feats), layers, [2, 3])
+    assert torch.allclose(out, torch.cat(per), atol=1e-12)
+
+
+def test_gradcheck_gatconv_set2set_graphnorm():
+    src, dst = _mol(4, [(0, 1), (1, 2), (2, 3)])
+    H, Fo, Fin = 2, 2, 3
+    p = {k: v.clone().requires_grad_() for k, v in _params(Fin, H, Fo, seed=7).items()}
+    X = torch.randn(4, Fin, requires_grad=True, **D64)
+    fn = lambda X, a, b, c, d, e: gnn_ref.gatconv_ref(src, dst, X, a, b, c, d, e, H, Fo)
+    assert torch.autograd.gradcheck(fn, (X, p["fc.weight"], p["res_fc.weight"], p["attn_l"],
+                                         p["attn_r"], p["bias"]))
+    lstm = _lstm(2, layers=2)
+    Xs = torch.randn(5, 2, requires_grad=True, **D64)
+    assert torch.autograd.gradcheck(lambda x: gnn_ref.set2set_ref([0, 2, 5], x, lstm, 3), (Xs,))
+    xg = torch.randn(5, 3, requires_grad=True, **D64)
+    w, b, ms = (torch.rand(3, requires_grad=True, **D64) for _ in range(3))
+    assert torch.autograd.gradcheck(lambda x, w, b, m: gnn_ref.graphnorm_ref(x, w, b, m, 1e-5, [0, 2, 5]),
+                                    (xg, w, b, ms))
+
+
+def test_fp32_reference_error_budget():
+    """The reference computes in fp32; its distance to the float64 restatement on a realistic
+    batch sits well inside the 1e-5 bar the HIP path is held to."""
+    from _util import batch_of_sizes, graph_dict, model_pair
+    sb = batch_of_sizes([25, 11, 40, 23], seed=4)
+    _, ref = model_pair(seed=1)
+    ref.eval()
+    gd = graph_dict(sb)
+    X = torch.as_tensor(sb.feats)
+    with torch.no_grad():
+        y32 = ref.float()(gd, X.float())
+        y64 = ref.double()(gd, X.double())
+    assert rel_err(y32, y64) < 1e-5
