@@ -76,34 +76,39 @@ int mvml_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                   const float* A, int64_t lda, const float* B, int64_t ldb,
                   const float* bias, float beta, int act, float* C, int64_t ldc,
                   void* workspace, size_t workspace_bytes, void* stream);
-/* Column sums: out[n] = beta*out[n] + sum_m X[m*ldx + n], deterministic two-stage tree.
- * Replaces the bias gradients torch autograd computes for GATConv.bias / LSTM / Linear. */
+/* Column sums: out[n] = beta*out[n] + alpha * sum_m X[m*ldx + n], deterministic two-stage
+ * tree.  Replaces the bias gradients torch autograd computes for GATConv.bias / LSTM / Linear. */
 size_t mvml_colsum_workspace_size(int64_t M, int64_t N);
-int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx, float beta, float* out,
-                    void* workspace, size_t workspace_bytes, void* stream);
+int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx, float alpha, float beta,
+                    float* out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * GATConv projection (dgl 0.9.1 GATConv.fc, res_fc, and the el/er reductions
  * `(feat_src * attn_l).sum(-1)` / `(feat_dst * attn_r).sum(-1)`), folded into ONE GEMM:
- *   Wcat[C, Fin], C = 2*H*F + 2*H, rows = [fc.weight ; res_fc.weight ; A_l ; A_r] with
+ *   Y[N, C] = X[N, Fin] * Wcat^T,  Wcat[C, Fin] rows = [fc.weight ; Wr ; A_l ; A_r]
  *   A_l[h,k] = sum_f attn_l[h,f] * fc.weight[h*F+f, k]   (likewise A_r with attn_r)
- *   Y[N, C] = X[N, Fin] * Wcat^T  =>  Y[:, 0:HF] = Z, Y[:, HF:2HF] = R, Y[:, 2HF:2HF+H] = el,
- *                                     Y[:, 2HF+H:2HF+2H] = er.
+ *   Wr = res_fc.weight (H*F rows), or with mean_residual = 1 its head mean
+ *        (1/H) sum_h res_fc.weight[h*F+f, :] (F rows): a 'mean' GATLayer only ever uses the
+ *        head-mean of the residual, so that layer's GEMM is 37 % smaller.
+ *   Y row = [ Z (H*F) | R (H*F or F) | el (H) | er (H) ];  C = mvml_gat_proj_cols(H,F,mean).
  * mvml_gat_unfold_grads maps dL/dWcat back onto the four parameters (exact chain rule).
  * ------------------------------------------------------------------------------------- */
+int mvml_gat_proj_cols(int H, int F, int mean_residual);
 int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_l,
-                          const float* attn_r, int H, int F, int Fin, float* Wcat, void* stream);
+                          const float* attn_r, int H, int F, int Fin, int mean_residual,
+                          float* Wcat, void* stream);
 int mvml_gat_unfold_grads(const float* gWcat, const float* fc_w, const float* attn_l,
-                          const float* attn_r, int H, int F, int Fin, float* g_fc_w,
-                          float* g_res_fc_w, float* g_attn_l, float* g_attn_r, void* stream);
+                          const float* attn_r, int H, int F, int Fin, int mean_residual,
+                          float* g_fc_w, float* g_res_fc_w, float* g_attn_l, float* g_attn_r,
+                          void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Fused GAT attention + aggregation, forward (one wavefront per destination atom):
  *   apply_edges(u_add_v) -> LeakyReLU(slope) -> edge_softmax -> update_all(u_mul_e, sum)
  *   -> + residual R -> + bias -> GATLayer agg (dgllife 0.3.0): mode 0 flatten+ELU,
  *   mode 1 mean over heads, mode 2 flatten (no activation).
- * Y is the projection output above (ldy >= 2*H*F + 2*H).  out is [N, H*F] (modes 0, 2) or
- * [N, F] (mode 1).  attn (optional, may be NULL) receives edge_softmax output [E, H] in
+ * Y is the projection output above (mean_residual layout iff mode 1; ldy >= its C, multiple of
+ * 4).  out is [N, H*F] (modes 0, 2) or [N, F] (mode 1).  attn (optional, may be NULL) receives edge_softmax output [E, H] in
  * in-CSR slot order, for the backward.
  * ------------------------------------------------------------------------------------- */
 int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
@@ -111,7 +116,8 @@ int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t*
                      int mode, float* out, float* attn, void* stream);
 /* Backward of mvml_gat_agg_fwd (DGL GSpMM / GSDDMM / EdgeSoftmax backward + torch autograd of
  * the residual/bias/ELU/mean).  Atomic-free: the u_mul_e-sum transpose is a gather over the
- * out-CSR.  Writes gY[N, ldgy] = [dZ | dR | d el | d er] (the GEMM backward's input).
+ * out-CSR.  Writes gY[N, ldgy] = [dZ | dR | d el | d er] (the GEMM backward's input, same
+ * column layout as Y).
  * out is the forward output (mode 0 uses ELU'(x) = out + 1 for x <= 0).  gpre_ws: [E, H]. */
 size_t mvml_gat_agg_bwd_workspace_size(int64_t num_edges, int H);
 int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,

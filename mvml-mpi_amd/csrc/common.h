@@ -52,6 +52,15 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// XCD-aware workgroup remap (bijective for any grid size).  The dispatcher deals workgroups
+// round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch); this returns a logical
+// block index such that each XCD walks ONE contiguous range, so neighbouring atoms / molecules
+// share an XCD's L2.  Speed only: correctness never depends on the placement.
+__device__ __forceinline__ int64_t xcd_block(unsigned b, unsigned nb) {
+  const unsigned q = nb / 8, r = nb % 8, x = b % 8, i = b / 8;
+  return (int64_t)((x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 }  // namespace mvml
 
 #define MVML_REQUIRE(cond, ...)          \

@@ -1,6 +1,12 @@
 // Fused GAT attention + aggregation (dgl 0.9.1 GATConv.forward after the projection) and its
 // atomic-free backward.  One wavefront per destination atom.
 //
+// Projection row layout (written by the folded GEMM, see mvml_gat_fold_weights):
+//   Y[n] = [ Z (H*F) | R (RW) | el (H) | er (H) ]     RW = H*F (flatten modes) or F (mean)
+// In mean mode (dgllife's last GATLayer, agg 'mean') only the head-mean of the residual is
+// ever used, so the GEMM produces R_mean = X * mean_h(W_res_h)^T directly (F columns instead
+// of H*F: 37 % fewer FLOPs and bytes for the 768 -> 4x384 layer).
+//
 // Forward, per destination v (rows of the in-CSR, in-edges in ascending edge id):
 //   s_e   = LeakyReLU(el[src_e] + er[v], slope)            apply_edges(u_add_v), leaky_relu
 //   a_e   = exp(s_e - max_v s) / sum_v exp(s - max_v s)   edge_softmax (norm_by = dst)
@@ -8,14 +14,18 @@
 //   out_v = ELU(rst_v.flatten) | mean_h(rst_v) | rst_v    dgllife GATLayer agg_mode/activation
 // Lanes take the in-edges (64 per chunk) for the logits/softmax, then the wave walks the
 // edges and every lane accumulates 4 consecutive feature columns per 256-column slice
-// (16-B loads of the gathered Z rows; neighbour rows of a molecule are L2 hits).
+// (16-B loads of the gathered Z rows).
 //
 // Backward (two passes, no float atomics):
 //   A (per dst v):  g_a_e = <Z[src_e], g_rst[v]>_f per head; g_s = a*(g_a - sum_v a*g_a);
 //                   g_pre = g_s * leaky'(s_e); d er[v] = sum_e g_pre           -> gpre_ws, gY
 //   B (per src u):  dZ[u] = sum_{e: u->w} a_e * g_rst[w]; d el[u] = sum_{e: u->w} g_pre_e
 //                   (gather over the out-CSR, out_inslot -> in-CSR slot of the edge), and the
-//                   residual gradient dR[u] = g_rst[u]                            -> gY
+//                   residual gradient dR[u]                                          -> gY
+//
+// Workgroup -> node mapping is XCD-aware: the dispatcher deals workgroups round-robin over the
+// 8 XCDs, so logical block = remap(blockIdx) gives each XCD one contiguous range of atoms; a
+// molecule's neighbour rows are then gathered from ONE XCD's L2 instead of up to eight.
 #include "common.h"
 
 namespace mvml {
@@ -44,6 +54,9 @@ __device__ __forceinline__ float4 fma4(float a, float4 z, float4 c) {
 __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
+__device__ __forceinline__ float4 scale4(float4 a, float s) {
+  return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
+}
 __device__ __forceinline__ float dot4(float4 a, float4 b) {
   return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
 }
@@ -58,10 +71,10 @@ __device__ __forceinline__ float pick(const float (&a)[H], int h) {
   return r;
 }
 
-// g_rst[v, col..col+3] from the layer output gradient (undoing ELU / head-mean / identity).
+// g_rst[v, col..col+3] (per-head gradient of rst) from the layer-output gradient.
 __device__ __forceinline__ float4 grst_of(const float* __restrict__ g_out, const float* __restrict__ out,
                                           int64_t v, int col, int HF, int F, int H, int mode) {
-  if (mode == 1) {
+  if (mode == 1) {  // mean over heads: torch mean backward = grad / H
     const float4 g = ld4(g_out + v * F + (col % F));
     const float inv = (float)H;
     return make_float4(g.x / inv, g.y / inv, g.z / inv, g.w / inv);
@@ -84,15 +97,17 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
                    float slope, int mode, float* __restrict__ out, float* __restrict__ attn) {
   __shared__ __attribute__((aligned(16))) float red[kWavesPerBlock][VPL * 256];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t v = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t v = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
   if (v >= N) return;
   const int HF = H * F;
+  const int RW = (mode == 1) ? F : HF;
+  const int EA = HF + RW;  // el column; er at EA + H
   const int beg = rowptr[v], end = rowptr[v + 1];
   const int deg = end - beg;
   const float* yv = Y + v * ldy;
   float er[H];
 #pragma unroll
-  for (int h = 0; h < H; ++h) er[h] = yv[2 * HF + H + h];
+  for (int h = 0; h < H; ++h) er[h] = yv[EA + H + h];
 
   // ---- softmax statistics over the in-edges (exactly max -> exp -> sum -> divide) ----
   float mx[H], sm[H], s_l[H];
@@ -103,7 +118,7 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
     const bool valid = base + lane < deg;
     if (valid) {
       u_l = in_src[beg + base + lane];
-      const float* yu = Y + (int64_t)u_l * ldy + 2 * HF;
+      const float* yu = Y + (int64_t)u_l * ldy + EA;
 #pragma unroll
       for (int h = 0; h < H; ++h) s_l[h] = leaky(yu[h] + er[h], slope);
     } else {
@@ -123,7 +138,7 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
       float ex[H];
       if (valid) {
         const int u = in_src[beg + base + lane];
-        const float* yu = Y + (int64_t)u * ldy + 2 * HF;
+        const float* yu = Y + (int64_t)u * ldy + EA;
 #pragma unroll
         for (int h = 0; h < H; ++h) ex[h] = expf(leaky(yu[h] + er[h], slope) - mx[h]);
       } else {
@@ -152,7 +167,7 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
     if (!one_chunk) {
       if (base + lane < deg) {
         u_l = in_src[beg + base + lane];
-        const float* yu = Y + (int64_t)u_l * ldy + 2 * HF;
+        const float* yu = Y + (int64_t)u_l * ldy + EA;
 #pragma unroll
         for (int h = 0; h < H; ++h) s_l[h] = leaky(yu[h] + er[h], slope);
       }
@@ -201,17 +216,14 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
   }
 
   // ---- epilogue: + residual + bias, then GATLayer aggregation ----
-#pragma unroll
-  for (int c = 0; c < VPL; ++c)
-    if (okc[c]) {
-      const int col = 4 * (lane + 64 * c);
-      acc[c] = add4(add4(acc[c], ld4(yv + HF + col)), ld4(bias + col));
-    }
   if (mode == 1) {
     float* r = red[wid];
 #pragma unroll
     for (int c = 0; c < VPL; ++c)
-      if (okc[c]) st4(r + 4 * (lane + 64 * c), acc[c]);
+      if (okc[c]) {
+        const int col = 4 * (lane + 64 * c);
+        st4(r + col, add4(acc[c], ld4(bias + col)));
+      }
     wave_lds_sync();
     const float invh = (float)H;
 #pragma unroll
@@ -221,16 +233,19 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
         float4 s = ld4(r + f);
 #pragma unroll
         for (int h = 1; h < H; ++h) s = add4(s, ld4(r + h * F + f));
-        st4(out + v * F + f, make_float4(s.x / invh, s.y / invh, s.z / invh, s.w / invh));
+        const float4 rm = ld4(yv + HF + f);  // head-mean residual
+        st4(out + v * F + f, make_float4(s.x / invh + rm.x, s.y / invh + rm.y, s.z / invh + rm.z,
+                                         s.w / invh + rm.w));
       }
     }
   } else {
 #pragma unroll
     for (int c = 0; c < VPL; ++c)
       if (okc[c]) {
-        float4 o = acc[c];
+        const int col = 4 * (lane + 64 * c);
+        float4 o = add4(add4(acc[c], ld4(yv + HF + col)), ld4(bias + col));
         if (mode == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
-        st4(out + v * HF + 4 * (lane + 64 * c), o);
+        st4(out + v * HF + col, o);
       }
   }
 }
@@ -244,9 +259,10 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
                        float slope, int mode, float* __restrict__ gpre, float* __restrict__ gY,
                        int64_t ldgy) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t v = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t v = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
   if (v >= N) return;
   const int HF = H * F;
+  const int EA = HF + ((mode == 1) ? F : HF);
   const int beg = rowptr[v], end = rowptr[v + 1];
   const int deg = end - beg;
   int hc[VPL];
@@ -262,7 +278,7 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
   const float* yv = Y + v * ldy;
   float er[H];
 #pragma unroll
-  for (int h = 0; h < H; ++h) er[h] = yv[2 * HF + H + h];
+  for (int h = 0; h < H; ++h) er[h] = yv[EA + H + h];
 
   float dots[H];  // sum_e a_e * g_a_e per head
 #pragma unroll
@@ -313,7 +329,7 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
     float gp[H];
     if (valid) {
       const int u = in_src[slot];
-      const float* yu = Y + (int64_t)u * ldy + 2 * HF;
+      const float* yu = Y + (int64_t)u * ldy + EA;
 #pragma unroll
       for (int h = 0; h < H; ++h) {
         const float a = (deg > 64) ? attn[slot * H + h] : a_l[h];
@@ -334,7 +350,7 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
     float g = ger[0];
 #pragma unroll
     for (int h = 1; h < H; ++h) g = (lane == h) ? ger[h] : g;
-    gY[v * ldgy + 2 * HF + H + lane] = g;
+    gY[v * ldgy + EA + H + lane] = g;
   }
 }
 
@@ -347,9 +363,11 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
                        const float* __restrict__ out, const float* __restrict__ g_out, int F,
                        int mode, float* __restrict__ gY, int64_t ldgy) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t u = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t u = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
   if (u >= N) return;
   const int HF = H * F;
+  const int RW = (mode == 1) ? F : HF;
+  const int EA = HF + RW;
   const int beg = out_rowptr[u], end = out_rowptr[u + 1];
   const int deg = end - beg;
   int hc[VPL];
@@ -392,17 +410,17 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
   }
   float* gyu = gY + u * ldgy;
 #pragma unroll
-  for (int c = 0; c < VPL; ++c)
-    if (okc[c]) {
-      const int col = 4 * (lane + 64 * c);
-      st4(gyu + col, gz[c]);
-      st4(gyu + HF + col, grst_of(g_out, out, u, col, HF, F, H, mode));
-    }
+  for (int c = 0; c < VPL; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    if (okc[c]) st4(gyu + col, gz[c]);
+    if (col < RW)  // dR: per-head g_rst (flatten) or the head-mean residual's g_out (mean)
+      st4(gyu + HF + col, mode == 1 ? ld4(g_out + u * F + col) : grst_of(g_out, out, u, col, HF, F, H, mode));
+  }
   if (lane < H) {
     float g = gel[0];
 #pragma unroll
     for (int h = 1; h < H; ++h) g = (lane == h) ? gel[h] : g;
-    gyu[2 * HF + lane] = g;
+    gyu[EA + lane] = g;
   }
 }
 
@@ -443,11 +461,14 @@ int launch_bwd(int64_t N, const int32_t* rp, const int32_t* src, const int32_t* 
     default: break;                                \
   }
 
-int check_shapes(int H, int F, int64_t ldy, const void* Y, const char* who) {
+int check_shapes(int H, int F, int mode, int64_t ldy, const void* Y, const char* who) {
   MVML_REQUIRE(H == 1 || H == 2 || H == 4 || H == 8, "%s: num_heads must be 1, 2, 4 or 8 (got %d)", who, H);
   MVML_REQUIRE(F > 0 && F % 4 == 0, "%s: out_feats must be a positive multiple of 4 (got %d)", who, F);
   MVML_REQUIRE(H * F <= 2048, "%s: H*F must be <= 2048 (got %d)", who, H * F);
-  MVML_REQUIRE(ldy >= 2 * H * F + 2 * H && ldy % 4 == 0, "%s: bad leading dimension %lld", who, (long long)ldy);
+  MVML_REQUIRE(mode >= 0 && mode <= 2, "%s: bad mode %d", who, mode);
+  const int64_t need = (int64_t)mvml_gat_proj_cols(H, F, mode == 1);
+  MVML_REQUIRE(ldy >= need && ldy % 4 == 0, "%s: leading dimension %lld < %lld or not a multiple of 4",
+               who, (long long)ldy, (long long)need);
   MVML_REQUIRE(((uintptr_t)Y & 15) == 0, "%s: tensors must be 16-byte aligned", who);
   return MVML_OK;
 }
@@ -457,13 +478,16 @@ int check_shapes(int H, int F, int64_t ldy, const void* Y, const char* who) {
 
 using namespace mvml;
 
+extern "C" int mvml_gat_proj_cols(int H, int F, int mean_residual) {
+  return H * F + (mean_residual ? F : H * F) + 2 * H;
+}
+
 extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
                                 const float* Y, int64_t ldy, int H, int F, const float* bias,
                                 float slope, int mode, float* out, float* attn, void* stream) {
   clear_error();
-  int rc = check_shapes(H, F, ldy, Y, "gat_agg_fwd");
+  int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_fwd");
   if (rc) return rc;
-  MVML_REQUIRE(mode >= 0 && mode <= 2, "gat_agg_fwd: bad mode %d", mode);
   MVML_REQUIRE(((uintptr_t)out & 15) == 0 && ((uintptr_t)bias & 15) == 0, "gat_agg_fwd: unaligned out/bias");
   if (num_nodes == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
@@ -489,10 +513,9 @@ extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* in_rowptr, con
                                 int F, float slope, int mode, float* gY, int64_t ldgy,
                                 void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
-  int rc = check_shapes(H, F, ldy, Y, "gat_agg_bwd");
+  int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_bwd");
   if (rc) return rc;
-  MVML_REQUIRE(mode >= 0 && mode <= 2, "gat_agg_bwd: bad mode %d", mode);
-  MVML_REQUIRE(ldgy >= 2 * H * F + 2 * H && ldgy % 4 == 0, "gat_agg_bwd: bad ldgy");
+  MVML_REQUIRE(ldgy >= mvml_gat_proj_cols(H, F, mode == 1) && ldgy % 4 == 0, "gat_agg_bwd: bad ldgy");
   MVML_REQUIRE(attn != nullptr, "gat_agg_bwd: attention from the forward is required");
   MVML_REQUIRE(mode != 0 || out != nullptr, "gat_agg_bwd: mode 0 needs the forward output");
   if (num_nodes == 0) return MVML_OK;
@@ -518,20 +541,31 @@ extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* in_rowptr, con
 namespace mvml {
 namespace {
 
-// Wcat rows: [0,HF) fc.weight, [HF,2HF) res_fc.weight, [2HF,2HF+H) A_l, [2HF+H,2HF+2H) A_r.
+// Wcat rows: [0,HF) fc.weight | [HF,HF+RW) res_fc.weight (RW = HF) or its head mean (RW = F) |
+//            [HF+RW, +H) A_l | [+H, +2H) A_r,   A_l[h,k] = sum_f attn_l[h,f] fc.weight[hF+f,k].
 __global__ void fold_weights_kernel(const float* __restrict__ fc_w, const float* __restrict__ res_w,
                                     const float* __restrict__ attn_l, const float* __restrict__ attn_r,
-                                    int H, int F, int Fin, float* __restrict__ Wcat) {
+                                    int H, int F, int Fin, int mean_res, float* __restrict__ Wcat) {
   const int HF = H * F;
-  const int64_t total = (int64_t)(2 * HF + 2 * H) * Fin;
+  const int RW = mean_res ? F : HF;
+  const int64_t total = (int64_t)(HF + RW + 2 * H) * Fin;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int row = (int)(e / Fin), k = (int)(e % Fin);
     float v;
-    if (row < HF) v = fc_w[(int64_t)row * Fin + k];
-    else if (row < 2 * HF) v = res_w[(int64_t)(row - HF) * Fin + k];
-    else {
-      const int r = row - 2 * HF;
+    if (row < HF) {
+      v = fc_w[(int64_t)row * Fin + k];
+    } else if (row < HF + RW) {
+      const int r = row - HF;
+      if (mean_res) {
+        float s = 0.f;
+        for (int h = 0; h < H; ++h) s += res_w[(int64_t)(h * F + r) * Fin + k];
+        v = s / (float)H;
+      } else {
+        v = res_w[(int64_t)r * Fin + k];
+      }
+    } else {
+      const int r = row - HF - RW;
       const int h = r % H;
       const float* at = (r < H) ? attn_l : attn_r;
       float s = 0.f;
@@ -543,34 +577,36 @@ __global__ void fold_weights_kernel(const float* __restrict__ fc_w, const float*
 }
 
 // dL/dfc.weight[hF+f,k] = gWcat[hF+f,k] + attn_l[h,f]*gA_l[h,k] + attn_r[h,f]*gA_r[h,k]
-// dL/dres_fc.weight = gWcat[HF:2HF]
+// dL/dres_fc.weight[hF+f,k] = gWcat[HF+hF+f,k]  or  gWcat[HF+f,k] / H  (head-mean residual)
 __global__ void unfold_w_kernel(const float* __restrict__ gW, const float* __restrict__ attn_l,
-                                const float* __restrict__ attn_r, int H, int F, int Fin,
+                                const float* __restrict__ attn_r, int H, int F, int Fin, int mean_res,
                                 float* __restrict__ g_fc, float* __restrict__ g_res) {
   const int HF = H * F;
+  const int RW = mean_res ? F : HF;
   const int64_t total = (int64_t)HF * Fin;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int row = (int)(e / Fin), k = (int)(e % Fin);
     const int h = row / F;
-    const float gl = gW[(int64_t)(2 * HF + h) * Fin + k];
-    const float gr = gW[(int64_t)(2 * HF + H + h) * Fin + k];
+    const float gl = gW[(int64_t)(HF + RW + h) * Fin + k];
+    const float gr = gW[(int64_t)(HF + RW + H + h) * Fin + k];
     g_fc[e] = gW[e] + attn_l[row] * gl + attn_r[row] * gr;
-    g_res[e] = gW[(int64_t)HF * Fin + e];
+    g_res[e] = mean_res ? gW[(int64_t)(HF + row % F) * Fin + k] / (float)H : gW[(int64_t)HF * Fin + e];
   }
 }
 
 // dL/dattn_l[h,f] = sum_k gA_l[h,k] * fc.weight[hF+f,k]  (one wave per (side, h, f))
 __global__ void unfold_attn_kernel(const float* __restrict__ gW, const float* __restrict__ fc_w,
-                                   int H, int F, int Fin, float* __restrict__ g_al,
+                                   int H, int F, int Fin, int mean_res, float* __restrict__ g_al,
                                    float* __restrict__ g_ar) {
   const int HF = H * F;
+  const int RW = mean_res ? F : HF;
   const int lane = threadIdx.x & 63;
   const int64_t item = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (item >= 2 * HF) return;
   const int side = (int)(item / HF), row = (int)(item % HF);
   const int h = row / F;
-  const float* ga = gW + (int64_t)(2 * HF + side * H + h) * Fin;
+  const float* ga = gW + (int64_t)(HF + RW + side * H + h) * Fin;
   const float* w = fc_w + (int64_t)row * Fin;
   float s = 0.f;
   for (int k = lane; k < Fin; k += 64) s = fmaf(ga[k], w[k], s);
@@ -582,31 +618,33 @@ __global__ void unfold_attn_kernel(const float* __restrict__ gW, const float* __
 }  // namespace mvml
 
 extern "C" int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_l,
-                                     const float* attn_r, int H, int F, int Fin, float* Wcat,
-                                     void* stream) {
+                                     const float* attn_r, int H, int F, int Fin, int mean_residual,
+                                     float* Wcat, void* stream) {
   clear_error();
   MVML_REQUIRE(H > 0 && F > 0 && Fin > 0, "gat_fold_weights: bad shape");
   hipStream_t st = as_stream(stream);
-  const int64_t total = (int64_t)(2 * H * F + 2 * H) * Fin;
+  const int64_t total = (int64_t)mvml_gat_proj_cols(H, F, mean_residual) * Fin;
   const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
-  fold_weights_kernel<<<blocks, 256, 0, st>>>(fc_w, res_fc_w, attn_l, attn_r, H, F, Fin, Wcat);
+  fold_weights_kernel<<<blocks, 256, 0, st>>>(fc_w, res_fc_w, attn_l, attn_r, H, F, Fin,
+                                              mean_residual, Wcat);
   return check_launch("fold_weights_kernel");
 }
 
 extern "C" int mvml_gat_unfold_grads(const float* gWcat, const float* fc_w, const float* attn_l,
-                                     const float* attn_r, int H, int F, int Fin, float* g_fc_w,
-                                     float* g_res_fc_w, float* g_attn_l, float* g_attn_r,
-                                     void* stream) {
+                                     const float* attn_r, int H, int F, int Fin, int mean_residual,
+                                     float* g_fc_w, float* g_res_fc_w, float* g_attn_l,
+                                     float* g_attn_r, void* stream) {
   clear_error();
   MVML_REQUIRE(H > 0 && F > 0 && Fin > 0, "gat_unfold_grads: bad shape");
   hipStream_t st = as_stream(stream);
   const int64_t total = (int64_t)H * F * Fin;
   const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
-  unfold_w_kernel<<<blocks, 256, 0, st>>>(gWcat, attn_l, attn_r, H, F, Fin, g_fc_w, g_res_fc_w);
+  unfold_w_kernel<<<blocks, 256, 0, st>>>(gWcat, attn_l, attn_r, H, F, Fin, mean_residual, g_fc_w,
+                                          g_res_fc_w);
   int rc = check_launch("unfold_w_kernel");
   if (rc) return rc;
   const int64_t items = 2 * (int64_t)H * F;
-  unfold_attn_kernel<<<(unsigned)ceil_div(items, 4), 256, 0, st>>>(gWcat, fc_w, H, F, Fin, g_attn_l,
-                                                                   g_attn_r);
+  unfold_attn_kernel<<<(unsigned)ceil_div(items, 4), 256, 0, st>>>(gWcat, fc_w, H, F, Fin,
+                                                                   mean_residual, g_attn_l, g_attn_r);
   return check_launch("unfold_attn_kernel");
 }

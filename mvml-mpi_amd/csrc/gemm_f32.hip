@@ -202,30 +202,37 @@ int choose_splits(int64_t M, int64_t N, int64_t K) {
 
 int64_t k_chunk(int64_t K, int S) { return ceil_div(ceil_div(K, S), BKT) * BKT; }
 
+// Column sums, stage 1: each thread owns one column of a row chunk; eight independent partial
+// sums keep eight loads in flight per lane (the loop is otherwise latency-bound).
 __global__ void colsum_partial_kernel(int64_t M, int64_t N, const float* __restrict__ X,
                                       int64_t ldx, int64_t rows_per, float* __restrict__ part) {
   const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (col >= N) return;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
-  float s = 0.f;
-  for (int64_t r = r0; r < r1; ++r) s += X[r * ldx + col];
-  part[(int64_t)blockIdx.y * N + col] = s;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int64_t r = r0;
+  for (; r + 8 <= r1; r += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += X[(r + j) * ldx + col];
+  }
+  for (; r < r1; ++r) s[0] += X[r * ldx + col];
+  part[(int64_t)blockIdx.y * N + col] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
-__global__ void colsum_final_kernel(int64_t N, int S, const float* __restrict__ part, float beta,
-                                    float* __restrict__ out) {
+__global__ void colsum_final_kernel(int64_t N, int S, const float* __restrict__ part, float alpha,
+                                    float beta, float* __restrict__ out) {
   const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (col >= N) return;
   float s = 0.f;
   for (int z = 0; z < S; ++z) s += part[(int64_t)z * N + col];
-  out[col] = (beta != 0.f ? beta * out[col] : 0.f) + s;
+  out[col] = (beta != 0.f ? beta * out[col] : 0.f) + alpha * s;
 }
 
 int colsum_splits(int64_t M, int64_t N) {
   const int64_t colblocks = ceil_div(N, 256);
-  int64_t s = ceil_div(1024, colblocks);
+  int64_t s = ceil_div(2048, colblocks);
   s = std::min<int64_t>(s, ceil_div(M, 64));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 1024));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 4096));
 }
 
 }  // namespace
@@ -288,8 +295,8 @@ extern "C" size_t mvml_colsum_workspace_size(int64_t M, int64_t N) {
   return carve_size((size_t)colsum_splits(M, N) * N * sizeof(float));
 }
 
-extern "C" int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx, float beta,
-                               float* out, void* workspace, size_t workspace_bytes,
+extern "C" int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx, float alpha,
+                               float beta, float* out, void* workspace, size_t workspace_bytes,
                                void* stream) {
   clear_error();
   MVML_REQUIRE(M >= 0 && N >= 0 && ldx >= N, "colsum: bad shape");
@@ -304,6 +311,6 @@ extern "C" int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx
   float* part = static_cast<float*>(workspace);
   dim3 g1((unsigned)ceil_div(N, 256), (unsigned)S);
   colsum_partial_kernel<<<g1, 256, 0, st>>>(M, N, X, ldx, rows_per, part);
-  colsum_final_kernel<<<(unsigned)ceil_div(N, 256), 256, 0, st>>>(N, S, part, beta, out);
+  colsum_final_kernel<<<(unsigned)ceil_div(N, 256), 256, 0, st>>>(N, S, part, alpha, beta, out);
   return check_launch("colsum");
 }

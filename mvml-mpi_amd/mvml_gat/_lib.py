@@ -89,10 +89,48 @@ def exported_symbols():
     return sorted(_protos)
 
 
+class KernelTimer:
+    """Optional HIP-event bracketing of selected entry points on the launching stream (torch's
+    current stream, which is where every call enqueues).  bench.py enables it over its timed
+    region to measure per-kernel average durations live; disabled it costs one dict lookup."""
+
+    def __init__(self):
+        self.names = set()
+        self.events = {}
+        self.tags = {}
+
+    def enable(self, names):
+        self.names = set(names)
+        self.events = {n: [] for n in names}
+
+    def disable(self):
+        self.names = set()
+
+    def record(self, name, start, end, tag):
+        self.events[name].append((start, end, tag))
+
+    def summary(self):
+        """{name: [(ms, tag), ...]} — synchronises."""
+        torch.cuda.synchronize()
+        return {n: [(s.elapsed_time(e), tag) for s, e, tag in ev] for n, ev in self.events.items()}
+
+
+timer = KernelTimer()
+call_tag = [None]  # set by callers to attach per-call metadata (e.g. bytes moved) to a timing
+
+
 def call(name, *args):
     """Invoke an int-returning entry point; raise MvmlError with mvml_last_error() on failure."""
     fn = getattr(lib(), name)
-    rc = fn(*args)
+    tag, call_tag[0] = call_tag[0], None
+    if name in timer.names:
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        rc = fn(*args)
+        e.record()
+        timer.record(name, s, e, tag)
+    else:
+        rc = fn(*args)
     if rc != 0:
         msg = lib().mvml_last_error().decode(errors="replace")
         raise MvmlError(f"{name} failed (status {rc}): {msg}")

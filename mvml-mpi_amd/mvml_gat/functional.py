@@ -4,6 +4,8 @@ Each Function owns one stage of GNNModule (model.py:89-95) and calls only the C 
 no PyTorch math on the hot path besides allocation (and nn.Dropout, which the reference
 applies with torch's own RNG, model.py:87).
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -31,8 +33,27 @@ def _round4(x):
     return (x + 3) // 4 * 4
 
 
+def agg_fwd_bytes(N, E, H, F, out_cols, res_cols):
+    """Algorithmic HBM bytes of one mvml_gat_agg_fwd: read Z and R once,
+    el/er, rowptr, src ids; write the layer output and the saved attention.  R is the
+    head-mean residual (F columns) in mean mode."""
+    return 4 * (N * H * F + N * res_cols + 2 * N * H + (N + 1) + E + N * out_cols + E * H)
+
+
+def agg_bwd_bytes(N, E, H, F, gout_cols, mode):
+    """Algorithmic bytes of mvml_gat_agg_bwd: read Z, el/er, g_out (+ out for ELU'), saved
+    attention, both CSRs; write gY = [dZ | dR | d el | d er]; the [E,H] g_pre round trip
+    between its two passes is counted once each way."""
+    rw = F if mode == MODE_MEAN else H * F
+    reads = N * H * F + 2 * N * H + N * gout_cols + (N * H * F if mode == 0 else 0) + E * H
+    idx = 2 * (N + 1) + 3 * E
+    writes = N * (H * F + rw + 2 * H) + 2 * E * H
+    return 4 * (reads + idx + writes)
+
+
 def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0):
     """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32)."""
+    _lib.call_tag[0] = {"flops": 2 * M * N * K}
     L = _lib.lib()
     dev = C.device
     wsz = L.mvml_gemm_workspace_size(M, N, K)
@@ -41,13 +62,13 @@ def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.
          ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
 
 
-def colsum(X, M, N, ldx, out, beta=0.0, offset=0):
+def colsum(X, M, N, ldx, out, beta=0.0, offset=0, alpha=1.0):
+    """out = beta*out + alpha * column sums of X[:, offset:offset+N] (deterministic)."""
     L = _lib.lib()
     dev = out.device
     wp, wn = _lib.ws_ptr_size(L.mvml_colsum_workspace_size(M, N), dev)
-    xp = ptr(X).value + 4 * offset
-    import ctypes
-    call("mvml_colsum_f32", M, N, ctypes.c_void_p(xp), ldx, float(beta), ptr(out), wp, wn, _stream(dev))
+    xp = ctypes.c_void_p(ptr(X).value + 4 * offset)
+    call("mvml_colsum_f32", M, N, xp, ldx, float(alpha), float(beta), ptr(out), wp, wn, _stream(dev))
 
 
 class GATLayerFunction(torch.autograd.Function):
@@ -62,18 +83,20 @@ class GATLayerFunction(torch.autograd.Function):
         N, Fin = X.shape
         dev = X.device
         HF = H * F
-        C = 2 * HF + 2 * H
+        mean_res = int(mode == MODE_MEAN)
+        C = _lib.lib().mvml_gat_proj_cols(H, F, mean_res)
         ldy = _round4(C)
         st = _stream(dev)
         Wcat = torch.empty((C, Fin), dtype=torch.float32, device=dev)
         call("mvml_gat_fold_weights", ptr(_c(fc_w)), ptr(_c(res_w)), ptr(_c(attn_l)), ptr(_c(attn_r)),
-             H, F, Fin, ptr(Wcat), st)
+             H, F, Fin, mean_res, ptr(Wcat), st)
         Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
         gemm(X, Wcat, N, C, Fin, 0, 0, Fin, Fin, Y, ldy)
         out_cols = F if mode == MODE_MEAN else HF
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()
         attn = torch.empty((E, H), dtype=torch.float32, device=dev)
+        _lib.call_tag[0] = {"layer": f"H{H}xF{F}", "bytes": agg_fwd_bytes(N, E, H, F, out_cols, C - HF - 2 * H)}
         call("mvml_gat_agg_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F, ptr(_c(bias)),
              float(slope), int(mode), ptr(out), ptr(attn), st)
         ctx.save_for_backward(X, Wcat, Y, attn, out, fc_w, attn_l, attn_r)
@@ -88,25 +111,34 @@ class GATLayerFunction(torch.autograd.Function):
         N, Fin = X.shape
         dev = X.device
         HF = H * F
-        C = 2 * HF + 2 * H
+        mean_res = int(mode == MODE_MEAN)
+        C = _lib.lib().mvml_gat_proj_cols(H, F, mean_res)
+        RW = C - HF - 2 * H
         st = _stream(dev)
         L = _lib.lib()
         gY = torch.empty((N, ldy), dtype=torch.float32, device=dev)
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_agg_bwd_workspace_size(g.num_edges(), H), dev)
+        _lib.call_tag[0] = {"layer": f"H{H}xF{F}",
+                            "bytes": agg_bwd_bytes(N, g.num_edges(), H, F, g_out.shape[1], mode)}
         call("mvml_gat_agg_bwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr),
              ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(attn), ptr(out), ptr(g_out), H, F,
              float(ctx.slope), int(mode), ptr(gY), ldy, wp, wn, st)
         # dL/dWcat = gY^T X  (split-K over atoms)
         gW = torch.empty((C, Fin), dtype=torch.float32, device=dev)
+        assert RW in (F, HF)
         gemm(gY, X, C, Fin, N, 1, 1, ldy, Fin, gW, Fin)
         g_fc = torch.empty_like(fc_w)
         g_res = torch.empty_like(fc_w)
         g_al = torch.empty_like(attn_l)
         g_ar = torch.empty_like(attn_r)
         call("mvml_gat_unfold_grads", ptr(gW), ptr(_c(fc_w)), ptr(_c(attn_l)), ptr(_c(attn_r)), H, F, Fin,
-             ptr(g_fc), ptr(g_res), ptr(g_al), ptr(g_ar), st)
+             mean_res, ptr(g_fc), ptr(g_res), ptr(g_al), ptr(g_ar), st)
         g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
-        colsum(gY, N, HF, ldy, g_bias, offset=HF)
+        if mean_res:  # every head's bias sees g_out / H: one column sum, replicated over heads
+            colsum(gY, N, F, ldy, g_bias, offset=HF, alpha=1.0 / H)
+            g_bias.view(H, F)[1:].copy_(g_bias[:F].expand(H - 1, F))
+        else:
+            colsum(gY, N, HF, ldy, g_bias, offset=HF)
         gX = None
         if ctx.needs_input_grad[0]:
             gX = torch.empty((N, Fin), dtype=torch.float32, device=dev)
