@@ -91,14 +91,16 @@ int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx, float alp
  *        (1/H) sum_h res_fc.weight[h*F+f, :] (F rows): a 'mean' GATLayer only ever uses the
  *        head-mean of the residual, so that layer's GEMM is 37 % smaller.
  *   Y row = [ Z (H*F) | R (H*F or F) | el (H) | er (H) ];  C = mvml_gat_proj_cols(H,F,mean).
+ *   Wcat has row stride ldw >= Fin; columns Fin..ldw-1 are written as zeros, so a caller can
+ *   pad X to a multiple of 4 columns and keep every GEMM operand 16-B aligned.
  * mvml_gat_unfold_grads maps dL/dWcat back onto the four parameters (exact chain rule).
  * ------------------------------------------------------------------------------------- */
 int mvml_gat_proj_cols(int H, int F, int mean_residual);
 int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_l,
-                          const float* attn_r, int H, int F, int Fin, int mean_residual,
+                          const float* attn_r, int H, int F, int Fin, int ldw, int mean_residual,
                           float* Wcat, void* stream);
 int mvml_gat_unfold_grads(const float* gWcat, const float* fc_w, const float* attn_l,
-                          const float* attn_r, int H, int F, int Fin, int mean_residual,
+                          const float* attn_r, int H, int F, int Fin, int ldg, int mean_residual,
                           float* g_fc_w, float* g_res_fc_w, float* g_attn_l, float* g_attn_r,
                           void* stream);
 

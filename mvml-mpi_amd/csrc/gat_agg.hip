@@ -545,15 +545,18 @@ namespace {
 //            [HF+RW, +H) A_l | [+H, +2H) A_r,   A_l[h,k] = sum_f attn_l[h,f] fc.weight[hF+f,k].
 __global__ void fold_weights_kernel(const float* __restrict__ fc_w, const float* __restrict__ res_w,
                                     const float* __restrict__ attn_l, const float* __restrict__ attn_r,
-                                    int H, int F, int Fin, int mean_res, float* __restrict__ Wcat) {
+                                    int H, int F, int Fin, int ldw, int mean_res,
+                                    float* __restrict__ Wcat) {
   const int HF = H * F;
   const int RW = mean_res ? F : HF;
-  const int64_t total = (int64_t)(HF + RW + 2 * H) * Fin;
+  const int64_t total = (int64_t)(HF + RW + 2 * H) * ldw;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
-    const int row = (int)(e / Fin), k = (int)(e % Fin);
+    const int row = (int)(e / ldw), k = (int)(e % ldw);
     float v;
-    if (row < HF) {
+    if (k >= Fin) {
+      v = 0.f;  // zero pad columns (aligned K for the LDS-DMA GEMM path)
+    } else if (row < HF) {
       v = fc_w[(int64_t)row * Fin + k];
     } else if (row < HF + RW) {
       const int r = row - HF;
@@ -579,8 +582,8 @@ __global__ void fold_weights_kernel(const float* __restrict__ fc_w, const float*
 // dL/dfc.weight[hF+f,k] = gWcat[hF+f,k] + attn_l[h,f]*gA_l[h,k] + attn_r[h,f]*gA_r[h,k]
 // dL/dres_fc.weight[hF+f,k] = gWcat[HF+hF+f,k]  or  gWcat[HF+f,k] / H  (head-mean residual)
 __global__ void unfold_w_kernel(const float* __restrict__ gW, const float* __restrict__ attn_l,
-                                const float* __restrict__ attn_r, int H, int F, int Fin, int mean_res,
-                                float* __restrict__ g_fc, float* __restrict__ g_res) {
+                                const float* __restrict__ attn_r, int H, int F, int Fin, int ldg,
+                                int mean_res, float* __restrict__ g_fc, float* __restrict__ g_res) {
   const int HF = H * F;
   const int RW = mean_res ? F : HF;
   const int64_t total = (int64_t)HF * Fin;
@@ -588,16 +591,17 @@ __global__ void unfold_w_kernel(const float* __restrict__ gW, const float* __res
        e += (int64_t)gridDim.x * blockDim.x) {
     const int row = (int)(e / Fin), k = (int)(e % Fin);
     const int h = row / F;
-    const float gl = gW[(int64_t)(HF + RW + h) * Fin + k];
-    const float gr = gW[(int64_t)(HF + RW + H + h) * Fin + k];
-    g_fc[e] = gW[e] + attn_l[row] * gl + attn_r[row] * gr;
-    g_res[e] = mean_res ? gW[(int64_t)(HF + row % F) * Fin + k] / (float)H : gW[(int64_t)HF * Fin + e];
+    const float gl = gW[(int64_t)(HF + RW + h) * ldg + k];
+    const float gr = gW[(int64_t)(HF + RW + H + h) * ldg + k];
+    g_fc[e] = gW[(int64_t)row * ldg + k] + attn_l[row] * gl + attn_r[row] * gr;
+    g_res[e] = mean_res ? gW[(int64_t)(HF + row % F) * ldg + k] / (float)H
+                        : gW[(int64_t)(HF + row) * ldg + k];
   }
 }
 
 // dL/dattn_l[h,f] = sum_k gA_l[h,k] * fc.weight[hF+f,k]  (one wave per (side, h, f))
 __global__ void unfold_attn_kernel(const float* __restrict__ gW, const float* __restrict__ fc_w,
-                                   int H, int F, int Fin, int mean_res, float* __restrict__ g_al,
+                                   int H, int F, int Fin, int ldg, int mean_res, float* __restrict__ g_al,
                                    float* __restrict__ g_ar) {
   const int HF = H * F;
   const int RW = mean_res ? F : HF;
@@ -606,7 +610,7 @@ __global__ void unfold_attn_kernel(const float* __restrict__ gW, const float* __
   if (item >= 2 * HF) return;
   const int side = (int)(item / HF), row = (int)(item % HF);
   const int h = row / F;
-  const float* ga = gW + (int64_t)(HF + RW + side * H + h) * Fin;
+  const float* ga = gW + (int64_t)(HF + RW + side * H + h) * ldg;
   const float* w = fc_w + (int64_t)row * Fin;
   float s = 0.f;
   for (int k = lane; k < Fin; k += 64) s = fmaf(ga[k], w[k], s);
@@ -618,33 +622,33 @@ __global__ void unfold_attn_kernel(const float* __restrict__ gW, const float* __
 }  // namespace mvml
 
 extern "C" int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_l,
-                                     const float* attn_r, int H, int F, int Fin, int mean_residual,
-                                     float* Wcat, void* stream) {
+                                     const float* attn_r, int H, int F, int Fin, int ldw,
+                                     int mean_residual, float* Wcat, void* stream) {
   clear_error();
-  MVML_REQUIRE(H > 0 && F > 0 && Fin > 0, "gat_fold_weights: bad shape");
+  MVML_REQUIRE(H > 0 && F > 0 && Fin > 0 && ldw >= Fin, "gat_fold_weights: bad shape");
   hipStream_t st = as_stream(stream);
-  const int64_t total = (int64_t)mvml_gat_proj_cols(H, F, mean_residual) * Fin;
+  const int64_t total = (int64_t)mvml_gat_proj_cols(H, F, mean_residual) * ldw;
   const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
-  fold_weights_kernel<<<blocks, 256, 0, st>>>(fc_w, res_fc_w, attn_l, attn_r, H, F, Fin,
+  fold_weights_kernel<<<blocks, 256, 0, st>>>(fc_w, res_fc_w, attn_l, attn_r, H, F, Fin, ldw,
                                               mean_residual, Wcat);
   return check_launch("fold_weights_kernel");
 }
 
 extern "C" int mvml_gat_unfold_grads(const float* gWcat, const float* fc_w, const float* attn_l,
-                                     const float* attn_r, int H, int F, int Fin, int mean_residual,
-                                     float* g_fc_w, float* g_res_fc_w, float* g_attn_l,
-                                     float* g_attn_r, void* stream) {
+                                     const float* attn_r, int H, int F, int Fin, int ldg,
+                                     int mean_residual, float* g_fc_w, float* g_res_fc_w,
+                                     float* g_attn_l, float* g_attn_r, void* stream) {
   clear_error();
-  MVML_REQUIRE(H > 0 && F > 0 && Fin > 0, "gat_unfold_grads: bad shape");
+  MVML_REQUIRE(H > 0 && F > 0 && Fin > 0 && ldg >= Fin, "gat_unfold_grads: bad shape");
   hipStream_t st = as_stream(stream);
   const int64_t total = (int64_t)H * F * Fin;
   const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
-  unfold_w_kernel<<<blocks, 256, 0, st>>>(gWcat, attn_l, attn_r, H, F, Fin, mean_residual, g_fc_w,
-                                          g_res_fc_w);
+  unfold_w_kernel<<<blocks, 256, 0, st>>>(gWcat, attn_l, attn_r, H, F, Fin, ldg, mean_residual,
+                                          g_fc_w, g_res_fc_w);
   int rc = check_launch("unfold_w_kernel");
   if (rc) return rc;
   const int64_t items = 2 * (int64_t)H * F;
-  unfold_attn_kernel<<<(unsigned)ceil_div(items, 4), 256, 0, st>>>(gWcat, fc_w, H, F, Fin,
+  unfold_attn_kernel<<<(unsigned)ceil_div(items, 4), 256, 0, st>>>(gWcat, fc_w, H, F, Fin, ldg,
                                                                    mean_residual, g_attn_l, g_attn_r);
   return check_launch("unfold_attn_kernel");
 }

@@ -6,10 +6,11 @@
 // results match a CPU fp32 GEMM to rounding.
 //
 // Tiling: 128x128 output tile per 256-thread workgroup (4 waves as 2x2, 64x64 per wave =
-// 2x2 MFMA 32x32 tiles), K staged through LDS 32 deep with register prefetch of the next
-// stage.  LDS images are k-major ([k][m], [k][n]) so that an MFMA operand fragment
-// (lane l -> row l&31, k = l>>5) is one conflict-free ds_read_b32.  Operands may be stored
-// k-major or not (a_kmajor / b_kmajor); rows that allow it are loaded 16 B per lane.
+// 2x2 MFMA 32x32 tiles), K staged 32 deep through a 2-stage LDS ring filled by LDS-DMA
+// (global_load_lds_dwordx4) one stage ahead, one raw s_barrier per stage, two workgroups/CU.
+// The K order inside a 32-deep stage is permuted so that one ds_read_b128 yields a lane's
+// operand for four consecutive MFMA steps: step s of k-group g pairs k = 8g+s (lanes 0-31) with
+// k = 8g+4+s (lanes 32-63) for BOTH operands, so the sum is unchanged.
 // Small-output / long-K products (the weight gradients, K = atoms in the batch) split K over
 // workgroups into fp32 slabs that a second kernel sums in fixed order — deterministic, no
 // float atomics.
@@ -21,86 +22,157 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int BM = 128, BN = 128, BKT = 32, kThreads = 256;
+constexpr int kTileFloats = 128 * BKT;  // one operand tile in LDS (16 KB)
 
+// ---- operand staging ---------------------------------------------------------------------
+// An operand tile is 128 rows (M for A, N for B) x 32 k.
+//  * K-contiguous operands (A stored [M][K], B stored [N][K]) live in LDS as [row][32 k] with
+//    the 16-B chunk index XOR-swizzled by (row >> 1) & 7, so that the ds_read_b128 fragment
+//    reads below are bank-conflict free.
+//  * K-major operands (stored [K][rows]) live in LDS as [k][128], read by ds_read_b32.
+// Each wave-instruction fills 1 KB (64 lanes x 16 B) of LDS; a 16 KB tile is 16 instructions,
+// 4 per wave.  The same lane -> (row, chunk) map serves the LDS-DMA path (global_load_lds, the
+// per-lane SOURCE carries the swizzle) and the guarded register path (tails / unaligned).
 template <bool KMAJ>
-struct TileLoader {
-  // Loads a (rows=128) x (k=32) operand tile. KMAJ: element(r,k) = P[k*ld + r], else P[r*ld + k].
-  static constexpr int PAD = KMAJ ? 4 : 1;
-  static constexpr int LDS_LD = 128 + PAD;
-  float4 reg[4];
+struct Stager {
+  __device__ static __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
-  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int64_t r0,
-                                       int64_t rows, int64_t k0, int64_t kend, bool vec) {
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int idx = threadIdx.x + it * kThreads;
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (!KMAJ) {
-        const int r = idx >> 3, k4 = idx & 7;
-        const int64_t gr = r0 + r, gk = k0 + 4 * k4;
-        if (gr < rows) {
-          const float* p = P + gr * ld + gk;
-          if (vec && gk + 3 < kend) {
-            float4 t = *reinterpret_cast<const float4*>(p);
-            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (gk + j < kend) v[j] = p[j];
-          }
-        }
-      } else {
-        const int k = idx >> 5, r4 = idx & 31;
-        const int64_t gk = k0 + k, gr = r0 + 4 * r4;
-        if (gk < kend) {
-          const float* p = P + gk * ld + gr;
-          if (vec && gr + 3 < rows) {
-            float4 t = *reinterpret_cast<const float4*>(p);
-            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (gr + j < rows) v[j] = p[j];
-          }
-        }
-      }
-      reg[it] = make_float4(v[0], v[1], v[2], v[3]);
+  // Global element offset (row, k) of this lane's 16-B piece for wave-instruction `inst`,
+  // and the LDS float offset it lands at.
+  __device__ static __forceinline__ void piece(int inst, int lane, int& row, int& kk) {
+    if (!KMAJ) {
+      row = inst * 8 + (lane >> 3);
+      kk = 4 * ((lane & 7) ^ swz(row));
+    } else {
+      kk = inst * 2 + (lane >> 5);
+      row = 4 * (lane & 31);
     }
   }
 
-  __device__ __forceinline__ void store(float* lds) const {
+  __device__ static __forceinline__ void issue_lds_dma(const float* __restrict__ P, int64_t ld,
+                                                       int64_t r0, int64_t rows, int64_t k0,
+                                                       float* lds_tile, int wid, int lane) {
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
-      const int idx = threadIdx.x + it * kThreads;
+      const int inst = wid * 4 + it;
+      int row, kk;
+      piece(inst, lane, row, kk);
+      const float* src;
       if (!KMAJ) {
-        const int r = idx >> 3, k4 = idx & 7;
-        lds[(4 * k4 + 0) * LDS_LD + r] = reg[it].x;
-        lds[(4 * k4 + 1) * LDS_LD + r] = reg[it].y;
-        lds[(4 * k4 + 2) * LDS_LD + r] = reg[it].z;
-        lds[(4 * k4 + 3) * LDS_LD + r] = reg[it].w;
-      } else {
-        const int k = idx >> 5, r4 = idx & 31;
-        *reinterpret_cast<float4*>(&lds[k * LDS_LD + 4 * r4]) = reg[it];
+        const int64_t gr = min(r0 + row, rows - 1);  // rows past the edge are never stored
+        src = P + gr * ld + k0 + kk;
+      } else {  // rows % 4 == 0 here: a piece past the edge re-reads the last in-range piece
+        src = P + (k0 + kk) * ld + min(r0 + row, rows - 4);
       }
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(lds_tile + inst * 256),
+                                       16, 0, 0);
+    }
+  }
+
+  // Guarded register path: zero-fills k >= kend and rows >= rows; same LDS image.  Split into
+  // a load (issued before the MFMAs) and a store (after them) so the latency overlaps compute.
+  __device__ static __forceinline__ void load_guarded(const float* __restrict__ P, int64_t ld,
+                                                      int64_t r0, int64_t rows, int64_t k0,
+                                                      int64_t kend, bool vec, int wid, int lane,
+                                                      float4 (&v)[4]) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int inst = wid * 4 + it;
+      int row, kk;
+      piece(inst, lane, row, kk);
+      float e[4] = {0.f, 0.f, 0.f, 0.f};
+      if (!KMAJ) {
+        const int64_t gr = r0 + row, gk = k0 + kk;
+        if (gr < rows) {
+          const float* p = P + gr * ld + gk;
+          if (vec && gk + 3 < kend) {
+            const float4 t = *reinterpret_cast<const float4*>(p);
+            e[0] = t.x; e[1] = t.y; e[2] = t.z; e[3] = t.w;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (gk + j < kend) e[j] = p[j];
+          }
+        }
+      } else {
+        const int64_t gk = k0 + kk, gr = r0 + row;
+        if (gk < kend) {
+          const float* p = P + gk * ld + gr;
+          if (vec && gr + 3 < rows) {
+            const float4 t = *reinterpret_cast<const float4*>(p);
+            e[0] = t.x; e[1] = t.y; e[2] = t.z; e[3] = t.w;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (gr + j < rows) e[j] = p[j];
+          }
+        }
+      }
+      v[it] = make_float4(e[0], e[1], e[2], e[3]);
+    }
+  }
+
+  __device__ static __forceinline__ void store_guarded(float* lds_tile, int wid, int lane,
+                                                       const float4 (&v)[4]) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+      *reinterpret_cast<float4*>(lds_tile + (wid * 4 + it) * 256 + lane * 4) = v[it];
+  }
+
+  // Inline-asm fragment read (the compiler does not see it, so it cannot insert a vmcnt(0)
+  // that would drain the LDS-DMA prefetch in flight).  The caller waits lgkmcnt and places a
+  // sched_barrier before using the result.  tile_b = LDS byte address of the operand tile.
+  template <int G>
+  __device__ static __forceinline__ void frag_asm(uint32_t tile_b, int row, int h, float4& out) {
+    if (!KMAJ) {
+      const uint32_t addr = tile_b + row * (BKT * 4) + 16 * ((2 * G + h) ^ swz(row));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(out) : "v"(addr) : "memory");
+    } else {
+      const uint32_t addr = tile_b + ((8 * G + 4 * h) * 128 + row) * 4;
+      asm volatile(
+          "ds_read_b32 %0, %4\n\t"
+          "ds_read_b32 %1, %4 offset:512\n\t"
+          "ds_read_b32 %2, %4 offset:1024\n\t"
+          "ds_read_b32 %3, %4 offset:1536"
+          : "=v"(out.x), "=v"(out.y), "=v"(out.z), "=v"(out.w)
+          : "v"(addr)
+          : "memory");
+    }
+  }
+
+  // Fragment of k-group g (8 k values): element s of the result is the operand value at
+  // row `row`, k = 8g + 4h + s, where h = lane >> 5 — the k order both operands share.
+  __device__ static __forceinline__ float4 frag(const float* lds_tile, int row, int g, int h) {
+    if (!KMAJ) {
+      const int slot = (2 * g + h) ^ swz(row);
+      return *reinterpret_cast<const float4*>(lds_tile + row * BKT + slot * 4);
+    } else {
+      const float* p = lds_tile + (8 * g + 4 * h) * 128 + row;
+      return make_float4(p[0], p[128], p[256], p[384]);
     }
   }
 };
 
+__device__ __forceinline__ float comp(const float4& v, int s) {
+  return s == 0 ? v.x : (s == 1 ? v.y : (s == 2 ? v.z : v.w));
+}
+
 template <bool AK, bool BKM>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, 2)
 gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
                 float* __restrict__ slab, int a_vec, int b_vec) {
-  using LA = TileLoader<AK>;
-  using LB = TileLoader<BKM>;
-  __shared__ __attribute__((aligned(16))) float lds[BKT * LA::LDS_LD + BKT * LB::LDS_LD];
-  float* As = lds;
-  float* Bs = lds + BKT * LA::LDS_LD;
+  using SA = Stager<AK>;
+  using SB = Stager<BKM>;
+  // [stage][A tile | B tile], one __shared__ object (a second one can de-pipeline glds waits).
+  __shared__ __attribute__((aligned(16))) float lds[2 * 2 * kTileFloats];
 
-  // Tile order: consecutive workgroups walk N first so an A row-panel is reused from L2.
+  // XCD-aware tile order: each XCD walks a contiguous range of tiles, N fastest, so the
+  // workgroups sharing an A row-panel share one L2.
   const int64_t tiles_n = ceil_div(N, BN);
-  const int64_t tile = blockIdx.x;
+  const int64_t tile = xcd_block(blockIdx.x, gridDim.x);
   const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
   const int64_t kbeg = (int64_t)blockIdx.y * k_split;
   const int64_t kend = min(K, kbeg + k_split);
@@ -117,32 +189,85 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  LA la;
-  LB lb;
-  if (kbeg < kend) {
-    la.load(A, lda, m0, M, kbeg, kend, a_vec);
-    lb.load(B, ldb, n0, N, kbeg, kend, b_vec);
+  // LDS-DMA needs 16-B aligned pieces; a k-major operand's edge tile also needs rows % 4 == 0
+  // (no piece straddles the edge), otherwise the guarded register path fills the stage.
+  const bool dma = a_vec && b_vec && (!AK || M % 4 == 0 || m0 + BM <= M) &&
+                   (!BKM || N % 4 == 0 || n0 + BN <= N);
+  const int64_t nfull = (kend > kbeg) ? (kend - kbeg) / BKT : 0;       // whole 32-deep tiles
+  const int64_t ntiles = (kend > kbeg) ? ceil_div(kend - kbeg, BKT) : 0;
+
+  auto stage_ptr = [&](int st) { return lds + st * 2 * kTileFloats; };
+
+  // Single-barrier pipeline.  Iteration t: wait for tile t (vmcnt(0) / lgkmcnt(0)) and barrier
+  // (which also proves every wave finished reading the other stage), immediately start
+  // filling the other stage with tile t+1 (LDS-DMA; a synchronous guarded fill for tails), then
+  // run the 4 k-groups x 16 MFMAs with the next group's fragments read (inline-asm ds_read,
+  // double-buffered registers) under the current group's MFMAs.
+  const uint32_t lds_b = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
+  const int ra0 = wm * 64 + li, ra1 = ra0 + 32, rb0 = wn * 64 + li, rb1 = rb0 + 32;
+  if (ntiles > 0) {
+    float* sa = stage_ptr(0);
+    if (dma && nfull > 0) {
+      SA::issue_lds_dma(A, lda, m0, M, kbeg, sa, wid, lane);
+      SB::issue_lds_dma(B, ldb, n0, N, kbeg, sa + kTileFloats, wid, lane);
+    } else {
+      float4 ra[4], rb[4];
+      SA::load_guarded(A, lda, m0, M, kbeg, kend, a_vec, wid, lane, ra);
+      SB::load_guarded(B, ldb, n0, N, kbeg, kend, b_vec, wid, lane, rb);
+      SA::store_guarded(sa, wid, lane, ra);
+      SB::store_guarded(sa + kTileFloats, wid, lane, rb);
+    }
   }
-  for (int64_t kt = kbeg; kt < kend; kt += BKT) {
-    la.store(As);
-    lb.store(Bs);
-    __syncthreads();
-    if (kt + BKT < kend) {
-      la.load(A, lda, m0, M, kt + BKT, kend, a_vec);
-      lb.load(B, ldb, n0, N, kt + BKT, kend, b_vec);
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int cur = (int)(t & 1);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const bool next = t + 1 < ntiles;
+    const int64_t k1 = kbeg + (t + 1) * BKT;
+    float* na = stage_ptr(cur ^ 1);
+    if (next && dma && t + 1 < nfull) {
+      SA::issue_lds_dma(A, lda, m0, M, k1, na, wid, lane);
+      SB::issue_lds_dma(B, ldb, n0, N, k1, na + kTileFloats, wid, lane);
+    } else if (next) {  // tails / unaligned operands: synchronous guarded fill
+      float4 ra[4], rb[4];
+      SA::load_guarded(A, lda, m0, M, k1, kend, a_vec, wid, lane, ra);
+      SB::load_guarded(B, ldb, n0, N, k1, kend, b_vec, wid, lane, rb);
+      SA::store_guarded(na, wid, lane, ra);
+      SB::store_guarded(na + kTileFloats, wid, lane, rb);
     }
-#pragma unroll
-    for (int kk = 0; kk < BKT; kk += 2) {
-      const float a0 = As[(kk + lk) * LA::LDS_LD + wm * 64 + li];
-      const float a1 = As[(kk + lk) * LA::LDS_LD + wm * 64 + 32 + li];
-      const float b0 = Bs[(kk + lk) * LB::LDS_LD + wn * 64 + li];
-      const float b1 = Bs[(kk + lk) * LB::LDS_LD + wn * 64 + 32 + li];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    const uint32_t sa_b = lds_b + (uint32_t)(cur * 2 * kTileFloats * 4);
+    const uint32_t sb_b = sa_b + kTileFloats * 4;
+    float4 fa0[2], fa1[2], fb0[2], fb1[2];  // [register set] x (sub-tile 0 / 1)
+#define MVML_FRAGS(G, SET)                                  \
+    SA::template frag_asm<G>(sa_b, ra0, lk, fa0[SET]);      \
+    SA::template frag_asm<G>(sa_b, ra1, lk, fa1[SET]);      \
+    SB::template frag_asm<G>(sb_b, rb0, lk, fb0[SET]);      \
+    SB::template frag_asm<G>(sb_b, rb1, lk, fb1[SET]);
+#define MVML_MFMAS(SET)                                                                                      \
+    _Pragma("unroll") for (int s = 0; s < 4; ++s) {                                                          \
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(fa0[SET], s), comp(fb0[SET], s), acc[0][0], 0, 0, 0); \
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(fa0[SET], s), comp(fb1[SET], s), acc[0][1], 0, 0, 0); \
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(fa1[SET], s), comp(fb0[SET], s), acc[1][0], 0, 0, 0); \
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(fa1[SET], s), comp(fb1[SET], s), acc[1][1], 0, 0, 0); \
     }
-    __syncthreads();
+#define MVML_WAIT_LDS()                                  \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
+    __builtin_amdgcn_sched_barrier(0);
+    MVML_FRAGS(0, 0)
+    MVML_WAIT_LDS()
+    MVML_FRAGS(1, 1)
+    MVML_MFMAS(0)
+    MVML_WAIT_LDS()
+    MVML_FRAGS(2, 0)
+    MVML_MFMAS(1)
+    MVML_WAIT_LDS()
+    MVML_FRAGS(3, 1)
+    MVML_MFMAS(0)
+    MVML_WAIT_LDS()
+    MVML_MFMAS(1)
+    __builtin_amdgcn_sched_barrier(0);
+#undef MVML_FRAGS
+#undef MVML_MFMAS
+#undef MVML_WAIT_LDS
   }
 
   // Epilogue. C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
@@ -189,15 +314,22 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int S, const float* _
   }
 }
 
-// Split policy: enough workgroups to cover the chip (~2 per CU) for small-output, long-K
-// products; K chunks are multiples of the 32-deep stage.
+// Split-K policy for small-output / long-K products (the weight gradients): pick the split
+// count that fills whole rounds of resident workgroups (256 CUs x 2) best, keeping >= 1024 K
+// per split so the slab reduction stays negligible.
 int choose_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
-  if (tiles >= 512 || K < 1024) return 1;
-  int64_t s = ceil_div(512, tiles);
-  s = std::min<int64_t>(s, ceil_div(K, 512));  // keep >= 512 K per split
-  s = std::min<int64_t>(s, 64);
-  return (int)std::max<int64_t>(s, 1);
+  const int64_t slots = 512;
+  if (tiles >= 2 * slots || K < 2048) return 1;
+  int best = 1;
+  double best_eff = (double)tiles / (double)(ceil_div(tiles, slots) * slots);
+  for (int s = 2; s <= 64; ++s) {
+    if (K / s < 1024) break;
+    const int64_t tot = tiles * s;
+    const double eff = (double)tot / (double)(ceil_div(tot, slots) * slots);
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
+  }
+  return best;
 }
 
 int64_t k_chunk(int64_t K, int S) { return ceil_div(ceil_div(K, S), BKT) * BKT; }

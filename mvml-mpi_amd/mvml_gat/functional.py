@@ -87,11 +87,15 @@ class GATLayerFunction(torch.autograd.Function):
         C = _lib.lib().mvml_gat_proj_cols(H, F, mean_res)
         ldy = _round4(C)
         st = _stream(dev)
-        Wcat = torch.empty((C, Fin), dtype=torch.float32, device=dev)
+        # Pad the feature dimension to a multiple of 4 (e.g. 74 atom features -> 76) so every
+        # GEMM operand row is 16-B aligned and the LDS-DMA path applies; pad columns are zero.
+        Fp = _round4(Fin)
+        Xp = X if Fp == Fin else torch.nn.functional.pad(X, (0, Fp - Fin))
+        Wcat = torch.empty((C, Fp), dtype=torch.float32, device=dev)
         call("mvml_gat_fold_weights", ptr(_c(fc_w)), ptr(_c(res_w)), ptr(_c(attn_l)), ptr(_c(attn_r)),
-             H, F, Fin, mean_res, ptr(Wcat), st)
+             H, F, Fin, Fp, mean_res, ptr(Wcat), st)
         Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
-        gemm(X, Wcat, N, C, Fin, 0, 0, Fin, Fin, Y, ldy)
+        gemm(Xp, Wcat, N, C, Fp, 0, 0, Fp, Fp, Y, ldy)
         out_cols = F if mode == MODE_MEAN else HF
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()
@@ -99,16 +103,18 @@ class GATLayerFunction(torch.autograd.Function):
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}", "bytes": agg_fwd_bytes(N, E, H, F, out_cols, C - HF - 2 * H)}
         call("mvml_gat_agg_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F, ptr(_c(bias)),
              float(slope), int(mode), ptr(out), ptr(attn), st)
-        ctx.save_for_backward(X, Wcat, Y, attn, out, fc_w, attn_l, attn_r)
+        ctx.save_for_backward(Xp, Wcat, Y, attn, out, fc_w, attn_l, attn_r)
+        ctx.Fin = Fin
         ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode, ctx.ldy = g, H, F, slope, mode, ldy
         return out
 
     @staticmethod
     def backward(ctx, g_out):
-        X, Wcat, Y, attn, out, fc_w, attn_l, attn_r = ctx.saved_tensors
+        Xp, Wcat, Y, attn, out, fc_w, attn_l, attn_r = ctx.saved_tensors
         g, H, F, mode, ldy = ctx.g, ctx.H, ctx.F, ctx.mode, ctx.ldy
         g_out = _c(g_out)
-        N, Fin = X.shape
+        N, Fp = Xp.shape
+        Fin = ctx.Fin
         dev = X.device
         HF = H * F
         mean_res = int(mode == MODE_MEAN)
@@ -124,15 +130,15 @@ class GATLayerFunction(torch.autograd.Function):
              ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(attn), ptr(out), ptr(g_out), H, F,
              float(ctx.slope), int(mode), ptr(gY), ldy, wp, wn, st)
         # dL/dWcat = gY^T X  (split-K over atoms)
-        gW = torch.empty((C, Fin), dtype=torch.float32, device=dev)
+        gW = torch.empty((C, Fp), dtype=torch.float32, device=dev)
         assert RW in (F, HF)
-        gemm(gY, X, C, Fin, N, 1, 1, ldy, Fin, gW, Fin)
+        gemm(gY, Xp, C, Fp, N, 1, 1, ldy, Fp, gW, Fp)
         g_fc = torch.empty_like(fc_w)
         g_res = torch.empty_like(fc_w)
         g_al = torch.empty_like(attn_l)
         g_ar = torch.empty_like(attn_r)
         call("mvml_gat_unfold_grads", ptr(gW), ptr(_c(fc_w)), ptr(_c(attn_l)), ptr(_c(attn_r)), H, F, Fin,
-             mean_res, ptr(g_fc), ptr(g_res), ptr(g_al), ptr(g_ar), st)
+             Fp, mean_res, ptr(g_fc), ptr(g_res), ptr(g_al), ptr(g_ar), st)
         g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
         if mean_res:  # every head's bias sees g_out / H: one column sum, replicated over heads
             colsum(gY, N, F, ldy, g_bias, offset=HF, alpha=1.0 / H)
@@ -142,7 +148,7 @@ class GATLayerFunction(torch.autograd.Function):
         gX = None
         if ctx.needs_input_grad[0]:
             gX = torch.empty((N, Fin), dtype=torch.float32, device=dev)
-            gemm(gY, Wcat, N, Fin, C, 0, 1, ldy, Fin, gX, Fin)
+            gemm(gY, Wcat, N, Fin, C, 0, 1, ldy, Fp, gX, Fin)
         return gX, g_fc, g_res, g_al, g_ar, g_bias, None, None, None, None, None
 
 

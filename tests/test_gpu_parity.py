@@ -66,7 +66,8 @@ def test_build_csr_rejects_bad_ids():
 
 # ------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (130, 70, 74), (257, 300, 768), (96, 40, 20000)])
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (130, 70, 74), (257, 300, 768), (96, 40, 20000),
+                                   (256, 384, 1000), (640, 512, 4000), (1000, 1928, 768)])
 def test_gemm_layouts(ak, bk, M, N, K):
     from mvml_gat.functional import gemm
     g = torch.Generator().manual_seed(M * 7 + N + K)

@@ -1,0 +1,54 @@
+"""Microbenchmark of mvml_gemm_f32 on the GEMM shapes of one GNNModule training step, with
+torch.matmul (hipBLASLt / rocBLAS fp32) on the same shapes as a yardstick.  Prints TF/s."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "mvml-mpi_amd"), ROOT]
+import torch  # noqa: E402
+from mvml_gat.functional import gemm  # noqa: E402
+
+N_ATOMS, B = 1754373, 65536
+SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor
+    ("L2 fwd  X*Wcat^T", N_ATOMS, 1928, 768, 0, 0),
+    ("L2 dX   gY*Wcat", N_ATOMS, 768, 1928, 0, 1),
+    ("L2 dW   gY^T*X", 1928, 768, N_ATOMS, 1, 1),
+    ("L1 fwd  K=74", N_ATOMS, 1544, 74, 0, 0),
+    ("LSTM gates x*Wih^T", B, 1536, 768, 0, 0),
+    ("LSTM dx g*Wih", B, 768, 1536, 0, 1),
+    ("LSTM dW g^T*x", 1536, 768, B, 1, 1),
+]
+
+
+def tf(fn, flops, it=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / it
+    return ms, flops / (ms * 1e-3) / 1e12
+
+
+def main():
+    dev = "cuda"
+    torch.manual_seed(0)
+    for name, M, N, K, ak, bk in SHAPES:
+        A = torch.randn((K, M) if ak else (M, K), device=dev)
+        Bm = torch.randn((K, N) if bk else (N, K), device=dev)
+        C = torch.empty((M, N), device=dev)
+        flops = 2 * M * N * K
+        ms, t = tf(lambda: gemm(A, Bm, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N), flops)
+        At = A.t() if ak else A
+        Bt = Bm if bk else Bm.t()
+        ms2, t2 = tf(lambda: torch.matmul(At, Bt, out=C), flops)
+        print(f"{name:22s} M={M:8d} N={N:5d} K={K:8d}  mvml {ms:8.3f} ms {t:6.1f} TF/s | torch {ms2:8.3f} ms {t2:6.1f} TF/s", flush=True)
+        del A, Bm, C
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
