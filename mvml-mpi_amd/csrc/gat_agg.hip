@@ -71,6 +71,41 @@ __device__ __forceinline__ float pick(const float (&a)[H], int h) {
   return r;
 }
 
+// All-reduce of H per-lane values over the 64 lanes in (H - 1) + (6 - log2 H) shuffles instead
+// of 6 H: a butterfly that halves the value count per step (lanes with the mask bit set keep
+// the upper half) and then finishes the single remaining value inside 64/H-lane groups.  After
+// it, lane l holds the total of head ((l >> (6 - log2 H)) & (H - 1)); readlane broadcasts them.
+template <int H>
+struct HeadReduce {
+  static constexpr int LOG = H == 1 ? 0 : H == 2 ? 1 : H == 4 ? 2 : 3;
+  template <bool MAX>
+  __device__ static __forceinline__ float op(float a, float b) { return MAX ? fmaxf(a, b) : a + b; }
+  template <bool MAX>
+  __device__ static __forceinline__ void all(float (&v)[H], int lane) {
+    float w[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) w[h] = v[h];
+    if constexpr (H >= 8) step<MAX, 8>(w, lane, 32);
+    if constexpr (H >= 4) step<MAX, 4>(w, lane, 32 >> (LOG - 2));
+    if constexpr (H >= 2) step<MAX, 2>(w, lane, 32 >> (LOG - 1));
+#pragma unroll
+    for (int m = 32 >> LOG; m >= 1; m >>= 1) w[0] = op<MAX>(w[0], __shfl_xor(w[0], m, 64));
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+      v[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w[0]), h << (6 - LOG)));
+  }
+  template <bool MAX, int N>
+  __device__ static __forceinline__ void step(float (&w)[H], int lane, int mask) {
+    const bool hi = (lane & mask) != 0;
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) {
+      const float keep = hi ? w[i + N / 2] : w[i];
+      const float send = hi ? w[i] : w[i + N / 2];
+      w[i] = op<MAX>(keep, __shfl_xor(send, mask, 64));
+    }
+  }
+};
+
 // g_rst[v, col..col+3] (per-head gradient of rst) from the layer-output gradient.
 __device__ __forceinline__ float4 grst_of(const float* __restrict__ g_out, const float* __restrict__ out,
                                           int64_t v, int col, int HF, int F, int H, int mode) {
@@ -125,13 +160,18 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
 #pragma unroll
       for (int h = 0; h < H; ++h) s_l[h] = -INFINITY;
     }
+    float cm[H];
 #pragma unroll
-    for (int h = 0; h < H; ++h) mx[h] = fmaxf(mx[h], wave_max(s_l[h]));
+    for (int h = 0; h < H; ++h) cm[h] = s_l[h];
+    HeadReduce<H>::template all<true>(cm, lane);
+#pragma unroll
+    for (int h = 0; h < H; ++h) mx[h] = fmaxf(mx[h], cm[h]);
   }
   const bool one_chunk = deg <= 64;
   if (one_chunk) {
 #pragma unroll
-    for (int h = 0; h < H; ++h) sm[h] = wave_sum(lane < deg ? expf(s_l[h] - mx[h]) : 0.f);
+    for (int h = 0; h < H; ++h) sm[h] = lane < deg ? expf(s_l[h] - mx[h]) : 0.f;
+    HeadReduce<H>::template all<false>(sm, lane);
   } else {
     for (int base = 0; base < deg; base += 64) {
       const bool valid = base + lane < deg;
@@ -145,8 +185,9 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
 #pragma unroll
         for (int h = 0; h < H; ++h) ex[h] = 0.f;
       }
+      HeadReduce<H>::template all<false>(ex, lane);
 #pragma unroll
-      for (int h = 0; h < H; ++h) sm[h] += wave_sum(ex[h]);
+      for (int h = 0; h < H; ++h) sm[h] += ex[h];
     }
   }
 
@@ -303,18 +344,20 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
 #pragma unroll
           for (int h = 0; h < H; ++h) part[h] += (hc[c] == h) ? d : 0.f;
         }
+      HeadReduce<H>::template all<false>(part, lane);
 #pragma unroll
-      for (int h = 0; h < H; ++h) {
-        const float g = wave_sum(part[h]);
-        ga_l[h] = (lane == j) ? g : ga_l[h];
-      }
+      for (int h = 0; h < H; ++h) ga_l[h] = (lane == j) ? part[h] : ga_l[h];
     }
     const bool valid = base + lane < deg;
+    float ag[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       a_l[h] = valid ? attn[(int64_t)(beg + base + lane) * H + h] : 0.f;
-      dots[h] += wave_sum(a_l[h] * ga_l[h]);
+      ag[h] = a_l[h] * ga_l[h];
     }
+    HeadReduce<H>::template all<false>(ag, lane);
+#pragma unroll
+    for (int h = 0; h < H; ++h) dots[h] += ag[h];
     if (deg > 64 && valid) {  // keep g_a for the second sweep
 #pragma unroll
       for (int h = 0; h < H; ++h) gpre[(int64_t)(beg + base + lane) * H + h] = ga_l[h];
@@ -343,8 +386,9 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
 #pragma unroll
       for (int h = 0; h < H; ++h) gp[h] = 0.f;
     }
+    HeadReduce<H>::template all<false>(gp, lane);
 #pragma unroll
-    for (int h = 0; h < H; ++h) ger[h] += wave_sum(gp[h]);
+    for (int h = 0; h < H; ++h) ger[h] += gp[h];
   }
   if (lane < H) {
     float g = ger[0];
@@ -396,8 +440,12 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
 #pragma unroll
       for (int h = 0; h < H; ++h) { a_l[h] = 0.f; gp_l[h] = 0.f; }
     }
+    float gsum[H];
 #pragma unroll
-    for (int h = 0; h < H; ++h) gel[h] += wave_sum(gp_l[h]);
+    for (int h = 0; h < H; ++h) gsum[h] = gp_l[h];
+    HeadReduce<H>::template all<false>(gsum, lane);
+#pragma unroll
+    for (int h = 0; h < H; ++h) gel[h] += gsum[h];
     for (int j = 0; j < cnt; ++j) {
       const int w = rl(w_l, j);
       float a[H];
