@@ -93,7 +93,10 @@ int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx, float alp
  *   Y row = [ Z (H*F) | R (H*F or F) | el (H) | er (H) ];  C = mvml_gat_proj_cols(H,F,mean).
  *   Wcat has row stride ldw >= Fin; columns Fin..ldw-1 are written as zeros, so a caller can
  *   pad X to a multiple of 4 columns and keep every GEMM operand 16-B aligned.
- * mvml_gat_unfold_grads maps dL/dWcat back onto the four parameters (exact chain rule).
+ * mvml_gat_unfold_grads maps dL/dWcat back onto fc.weight and res_fc.weight (and, if the
+ * g_attn pointers are non-NULL, onto attn_l/attn_r through the fold; the library's own path
+ * instead uses mvml_gat_attn_grad, which sums d el * Z over atoms directly like autograd does,
+ * because chaining through the fold loses ~sqrt(Fin) of fp32 accuracy when Z cancels).
  * ------------------------------------------------------------------------------------- */
 int mvml_gat_proj_cols(int H, int F, int mean_residual);
 int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_l,
@@ -103,6 +106,13 @@ int mvml_gat_unfold_grads(const float* gWcat, const float* fc_w, const float* at
                           const float* attn_r, int H, int F, int Fin, int ldg, int mean_residual,
                           float* g_fc_w, float* g_res_fc_w, float* g_attn_l, float* g_attn_r,
                           void* stream);
+
+/* dL/dattn_l[h,f] = sum_n gY[n, el+h] * Z[n, h*F+f] and likewise attn_r (the autograd of
+ * `(feat * attn_l).sum(-1)` in GATConv.forward); deterministic two-stage column reduction. */
+size_t mvml_gat_attn_grad_workspace_size(int64_t num_nodes, int H, int F);
+int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, int mean_residual, const float* Y,
+                       int64_t ldy, const float* gY, int64_t ldgy, float* g_attn_l,
+                       float* g_attn_r, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Fused GAT attention + aggregation, forward (one wavefront per destination atom):

@@ -19,9 +19,10 @@
 // Backward (two passes, no float atomics):
 //   A (per dst v):  g_a_e = <Z[src_e], g_rst[v]>_f per head; g_s = a*(g_a - sum_v a*g_a);
 //                   g_pre = g_s * leaky'(s_e); d er[v] = sum_e g_pre           -> gpre_ws, gY
+//                   and the residual gradient dR[v] (= g_rst[v], or g_out[v] in mean mode)
 //   B (per src u):  dZ[u] = sum_{e: u->w} a_e * g_rst[w]; d el[u] = sum_{e: u->w} g_pre_e
-//                   (gather over the out-CSR, out_inslot -> in-CSR slot of the edge), and the
-//                   residual gradient dR[u]                                          -> gY
+//                   (gather over the out-CSR, out_inslot -> in-CSR slot of the edge; g_rst[w]
+//                   rows come back from gY's dR block)                              -> gY
 //
 // Workgroup -> node mapping is XCD-aware: the dispatcher deals workgroups round-robin over the
 // 8 XCDs, so logical block = remap(blockIdx) gives each XCD one contiguous range of atoms; a
@@ -125,165 +126,183 @@ __device__ __forceinline__ float4 grst_of(const float* __restrict__ g_out, const
   return g;
 }
 
-template <int H, int VPL>
+// Forward.  CS waves share one destination atom, each owning HW = H / CS heads (HF / CS
+// columns): the wide 768 -> 4x384 layer runs with CS = 2 so every wave keeps only 3 float4
+// column slices per gathered row (half the VGPRs -> twice the waves in flight to hide the
+// dependent el-gather -> softmax -> Z-gather chain).  Block = 4 waves = 4 / CS atoms.
+template <int H, int VPL, int CS>
 __global__ void __launch_bounds__(kWavesPerBlock * 64)
 gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
                    const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ bias,
                    float slope, int mode, float* __restrict__ out, float* __restrict__ attn) {
+  constexpr int HW = H / CS;
   __shared__ __attribute__((aligned(16))) float red[kWavesPerBlock][VPL * 256];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t v = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
-  if (v >= N) return;
+  const int part = wid % CS;
+  const int64_t v = xcd_block(blockIdx.x, gridDim.x) * (kWavesPerBlock / CS) + wid / CS;
+  const bool live = v < N;  // (CS > 1: every wave must reach the block barrier)
+  if (CS == 1 && !live) return;
   const int HF = H * F;
+  const int HFW = HF / CS;           // columns of this wave
+  const int c0 = part * HFW;         // first column (global) of this wave
+  const int h0 = part * HW;          // first head of this wave
   const int RW = (mode == 1) ? F : HF;
-  const int EA = HF + RW;  // el column; er at EA + H
-  const int beg = rowptr[v], end = rowptr[v + 1];
+  const int EA = HF + RW;            // el column; er at EA + H
+  const int beg = live ? rowptr[v] : 0, end = live ? rowptr[v + 1] : 0;
   const int deg = end - beg;
-  const float* yv = Y + v * ldy;
-  float er[H];
+  const float* yv = Y + (live ? v : 0) * ldy;
+  float er[HW];
 #pragma unroll
-  for (int h = 0; h < H; ++h) er[h] = yv[EA + H + h];
+  for (int h = 0; h < HW; ++h) er[h] = live ? yv[EA + H + h0 + h] : 0.f;
 
   // ---- softmax statistics over the in-edges (exactly max -> exp -> sum -> divide) ----
-  float mx[H], sm[H], s_l[H];
+  float mx[HW], sm[HW], s_l[HW];
   int u_l = 0;
 #pragma unroll
-  for (int h = 0; h < H; ++h) { mx[h] = -INFINITY; sm[h] = 0.f; s_l[h] = -INFINITY; }
+  for (int h = 0; h < HW; ++h) { mx[h] = -INFINITY; sm[h] = 0.f; s_l[h] = -INFINITY; }
   for (int base = 0; base < deg; base += 64) {
     const bool valid = base + lane < deg;
     if (valid) {
       u_l = in_src[beg + base + lane];
-      const float* yu = Y + (int64_t)u_l * ldy + EA;
+      const float* yu = Y + (int64_t)u_l * ldy + EA + h0;
 #pragma unroll
-      for (int h = 0; h < H; ++h) s_l[h] = leaky(yu[h] + er[h], slope);
+      for (int h = 0; h < HW; ++h) s_l[h] = leaky(yu[h] + er[h], slope);
     } else {
 #pragma unroll
-      for (int h = 0; h < H; ++h) s_l[h] = -INFINITY;
+      for (int h = 0; h < HW; ++h) s_l[h] = -INFINITY;
     }
-    float cm[H];
+    float cm[HW];
 #pragma unroll
-    for (int h = 0; h < H; ++h) cm[h] = s_l[h];
-    HeadReduce<H>::template all<true>(cm, lane);
+    for (int h = 0; h < HW; ++h) cm[h] = s_l[h];
+    HeadReduce<HW>::template all<true>(cm, lane);
 #pragma unroll
-    for (int h = 0; h < H; ++h) mx[h] = fmaxf(mx[h], cm[h]);
+    for (int h = 0; h < HW; ++h) mx[h] = fmaxf(mx[h], cm[h]);
   }
   const bool one_chunk = deg <= 64;
   if (one_chunk) {
 #pragma unroll
-    for (int h = 0; h < H; ++h) sm[h] = lane < deg ? expf(s_l[h] - mx[h]) : 0.f;
-    HeadReduce<H>::template all<false>(sm, lane);
+    for (int h = 0; h < HW; ++h) sm[h] = lane < deg ? expf(s_l[h] - mx[h]) : 0.f;
+    HeadReduce<HW>::template all<false>(sm, lane);
   } else {
     for (int base = 0; base < deg; base += 64) {
       const bool valid = base + lane < deg;
-      float ex[H];
+      float ex[HW];
       if (valid) {
         const int u = in_src[beg + base + lane];
-        const float* yu = Y + (int64_t)u * ldy + EA;
+        const float* yu = Y + (int64_t)u * ldy + EA + h0;
 #pragma unroll
-        for (int h = 0; h < H; ++h) ex[h] = expf(leaky(yu[h] + er[h], slope) - mx[h]);
+        for (int h = 0; h < HW; ++h) ex[h] = expf(leaky(yu[h] + er[h], slope) - mx[h]);
       } else {
 #pragma unroll
-        for (int h = 0; h < H; ++h) ex[h] = 0.f;
+        for (int h = 0; h < HW; ++h) ex[h] = 0.f;
       }
-      HeadReduce<H>::template all<false>(ex, lane);
+      HeadReduce<HW>::template all<false>(ex, lane);
 #pragma unroll
-      for (int h = 0; h < H; ++h) sm[h] += ex[h];
+      for (int h = 0; h < HW; ++h) sm[h] += ex[h];
     }
   }
 
-  // ---- aggregation ----
+  // ---- aggregation over this wave's columns ----
   int hc[VPL];
   bool okc[VPL];
   float4 acc[VPL];
 #pragma unroll
   for (int c = 0; c < VPL; ++c) {
-    const int col = 4 * (lane + 64 * c);
-    okc[c] = col < HF;
-    hc[c] = okc[c] ? col / F : 0;
+    const int lc = 4 * (lane + 64 * c);  // column within this wave's range
+    okc[c] = lc < HFW;
+    hc[c] = okc[c] ? (c0 + lc) / F - h0 : 0;
     acc[c] = f4(0.f);
   }
   for (int base = 0; base < deg; base += 64) {
     const int cnt = min(64, deg - base);
-    float a_l[H];
+    float a_l[HW];
     if (!one_chunk) {
       if (base + lane < deg) {
         u_l = in_src[beg + base + lane];
-        const float* yu = Y + (int64_t)u_l * ldy + EA;
+        const float* yu = Y + (int64_t)u_l * ldy + EA + h0;
 #pragma unroll
-        for (int h = 0; h < H; ++h) s_l[h] = leaky(yu[h] + er[h], slope);
+        for (int h = 0; h < HW; ++h) s_l[h] = leaky(yu[h] + er[h], slope);
       }
     }
 #pragma unroll
-    for (int h = 0; h < H; ++h) a_l[h] = (base + lane < deg) ? expf(s_l[h] - mx[h]) / sm[h] : 0.f;
+    for (int h = 0; h < HW; ++h) a_l[h] = (base + lane < deg) ? expf(s_l[h] - mx[h]) / sm[h] : 0.f;
     if (attn && base + lane < deg) {
-      float* ap = attn + (int64_t)(beg + base + lane) * H;
-      if (H == 4) st4(ap, make_float4(a_l[0], a_l[H > 1 ? 1 : 0], a_l[H > 2 ? 2 : 0], a_l[H > 3 ? 3 : 0]));
+      float* ap = attn + (int64_t)(beg + base + lane) * H + h0;
+      if (HW == 4) st4(ap, make_float4(a_l[0], a_l[HW > 1 ? 1 : 0], a_l[HW > 2 ? 2 : 0], a_l[HW > 3 ? 3 : 0]));
       else {
 #pragma unroll
-        for (int h = 0; h < H; ++h) ap[h] = a_l[h];
+        for (int h = 0; h < HW; ++h) ap[h] = a_l[h];
       }
     }
     int j = 0;
     for (; j + 1 < cnt; j += 2) {
       const int u0 = rl(u_l, j), u1 = rl(u_l, j + 1);
-      float a0[H], a1[H];
+      float a0[HW], a1[HW];
 #pragma unroll
-      for (int h = 0; h < H; ++h) { a0[h] = rl(a_l[h], j); a1[h] = rl(a_l[h], j + 1); }
-      const float* z0 = Y + (int64_t)u0 * ldy;
-      const float* z1 = Y + (int64_t)u1 * ldy;
+      for (int h = 0; h < HW; ++h) { a0[h] = rl(a_l[h], j); a1[h] = rl(a_l[h], j + 1); }
+      const float* z0 = Y + (int64_t)u0 * ldy + c0;
+      const float* z1 = Y + (int64_t)u1 * ldy + c0;
       float4 zv0[VPL], zv1[VPL];
 #pragma unroll
       for (int c = 0; c < VPL; ++c) {
-        const int col = 4 * (lane + 64 * c);
-        if (okc[c]) { zv0[c] = ld4(z0 + col); zv1[c] = ld4(z1 + col); }
+        const int lc = 4 * (lane + 64 * c);
+        if (okc[c]) { zv0[c] = ld4(z0 + lc); zv1[c] = ld4(z1 + lc); }
       }
 #pragma unroll
       for (int c = 0; c < VPL; ++c)
         if (okc[c]) {
-          acc[c] = fma4(pick<H>(a0, hc[c]), zv0[c], acc[c]);
-          acc[c] = fma4(pick<H>(a1, hc[c]), zv1[c], acc[c]);
+          acc[c] = fma4(pick<HW>(a0, hc[c]), zv0[c], acc[c]);
+          acc[c] = fma4(pick<HW>(a1, hc[c]), zv1[c], acc[c]);
         }
     }
     if (j < cnt) {
       const int u0 = rl(u_l, j);
-      float a0[H];
+      float a0[HW];
 #pragma unroll
-      for (int h = 0; h < H; ++h) a0[h] = rl(a_l[h], j);
-      const float* z0 = Y + (int64_t)u0 * ldy;
+      for (int h = 0; h < HW; ++h) a0[h] = rl(a_l[h], j);
+      const float* z0 = Y + (int64_t)u0 * ldy + c0;
 #pragma unroll
       for (int c = 0; c < VPL; ++c)
-        if (okc[c]) acc[c] = fma4(pick<H>(a0, hc[c]), ld4(z0 + 4 * (lane + 64 * c)), acc[c]);
+        if (okc[c]) acc[c] = fma4(pick<HW>(a0, hc[c]), ld4(z0 + 4 * (lane + 64 * c)), acc[c]);
     }
   }
 
   // ---- epilogue: + residual + bias, then GATLayer aggregation ----
   if (mode == 1) {
+    // rst + bias of this wave's heads -> LDS; the part-0 wave of the atom sums the heads in
+    // order h = 0..H-1, divides by H and adds the head-mean residual.
     float* r = red[wid];
 #pragma unroll
     for (int c = 0; c < VPL; ++c)
       if (okc[c]) {
-        const int col = 4 * (lane + 64 * c);
-        st4(r + col, add4(acc[c], ld4(bias + col)));
+        const int lc = 4 * (lane + 64 * c);
+        st4(r + lc, add4(acc[c], ld4(bias + c0 + lc)));
       }
-    wave_lds_sync();
-    const float invh = (float)H;
+    if (CS > 1) __syncthreads();
+    else wave_lds_sync();
+    if (live && part == 0) {
+      const float invh = (float)H;
 #pragma unroll
-    for (int c = 0; c < VPL; ++c) {
-      const int f = 4 * (lane + 64 * c);
-      if (f < F) {
-        float4 s = ld4(r + f);
+      for (int c = 0; c < VPL; ++c) {
+        const int f = 4 * (lane + 64 * c);
+        if (f < F) {
+          float4 sacc = ld4(red[wid] + f);
 #pragma unroll
-        for (int h = 1; h < H; ++h) s = add4(s, ld4(r + h * F + f));
-        const float4 rm = ld4(yv + HF + f);  // head-mean residual
-        st4(out + v * F + f, make_float4(s.x / invh + rm.x, s.y / invh + rm.y, s.z / invh + rm.z,
-                                         s.w / invh + rm.w));
+          for (int h = 1; h < H; ++h) {
+            const int p = h / HW, hl = h % HW;
+            sacc = add4(sacc, ld4(red[wid + p] + hl * F + f));
+          }
+          const float4 rm = ld4(yv + HF + f);  // head-mean residual
+          st4(out + v * F + f, make_float4(sacc.x / invh + rm.x, sacc.y / invh + rm.y,
+                                           sacc.z / invh + rm.z, sacc.w / invh + rm.w));
+        }
       }
     }
-  } else {
+  } else if (live) {
 #pragma unroll
     for (int c = 0; c < VPL; ++c)
       if (okc[c]) {
-        const int col = 4 * (lane + 64 * c);
+        const int col = c0 + 4 * (lane + 64 * c);
         float4 o = add4(add4(acc[c], ld4(yv + HF + col)), ld4(bias + col));
         if (mode == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
         st4(out + v * HF + col, o);
@@ -315,6 +334,18 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
     okc[c] = col < HF;
     hc[c] = okc[c] ? col / F : 0;
     gr[c] = okc[c] ? grst_of(g_out, out, v, col, HF, F, H, mode) : f4(0.f);
+  }
+  // dR[v]: per-head g_rst (flatten modes) or g_out (head-mean residual).  Written here so the
+  // source pass can gather finished g_rst rows from gY instead of re-deriving them per edge.
+  float* gyv = gY + v * ldgy;
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    if (mode != 1) {
+      if (okc[c]) st4(gyv + HF + col, gr[c]);
+    } else if (col < F) {
+      st4(gyv + HF + col, ld4(g_out + v * F + col));
+    }
   }
   const float* yv = Y + v * ldy;
   float er[H];
@@ -451,19 +482,20 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
       float a[H];
 #pragma unroll
       for (int h = 0; h < H; ++h) a[h] = rl(a_l[h], j);
+      const float* gw = gY + (int64_t)w * ldgy + HF;  // g_rst row written by the dst pass
 #pragma unroll
       for (int c = 0; c < VPL; ++c)
-        if (okc[c]) gz[c] = fma4(pick<H>(a, hc[c]), grst_of(g_out, out, w, 4 * (lane + 64 * c), HF, F, H, mode), gz[c]);
+        if (okc[c]) {
+          const int col = 4 * (lane + 64 * c);
+          const float4 g = (mode == 1) ? grst_of(g_out, out, w, col, HF, F, H, mode) : ld4(gw + col);
+          gz[c] = fma4(pick<H>(a, hc[c]), g, gz[c]);
+        }
     }
   }
   float* gyu = gY + u * ldgy;
 #pragma unroll
-  for (int c = 0; c < VPL; ++c) {
-    const int col = 4 * (lane + 64 * c);
-    if (okc[c]) st4(gyu + col, gz[c]);
-    if (col < RW)  // dR: per-head g_rst (flatten) or the head-mean residual's g_out (mean)
-      st4(gyu + HF + col, mode == 1 ? ld4(g_out + u * F + col) : grst_of(g_out, out, u, col, HF, F, H, mode));
-  }
+  for (int c = 0; c < VPL; ++c)
+    if (okc[c]) st4(gyu + 4 * (lane + 64 * c), gz[c]);
   if (lane < H) {
     float g = gel[0];
 #pragma unroll
@@ -475,9 +507,17 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
 template <int H, int VPL>
 int launch_fwd(int64_t N, const int32_t* rp, const int32_t* src, const float* Y, int64_t ldy, int F,
                const float* bias, float slope, int mode, float* out, float* attn, hipStream_t st) {
-  const unsigned blocks = (unsigned)ceil_div(N, kWavesPerBlock);
-  gat_agg_fwd_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(N, rp, src, Y, ldy, F, bias,
-                                                                       slope, mode, out, attn);
+  // Wide layers (more than 4 float4 slices per lane) split the columns over 2 waves.
+  if constexpr (VPL > 4 && H % 2 == 0) {
+    constexpr int CS = 2, V2 = (VPL + 1) / 2;
+    const unsigned blocks = (unsigned)ceil_div(N, kWavesPerBlock / CS);
+    gat_agg_fwd_kernel<H, V2, CS><<<blocks, kWavesPerBlock * 64, 0, st>>>(N, rp, src, Y, ldy, F, bias,
+                                                                          slope, mode, out, attn);
+  } else {
+    const unsigned blocks = (unsigned)ceil_div(N, kWavesPerBlock);
+    gat_agg_fwd_kernel<H, VPL, 1><<<blocks, kWavesPerBlock * 64, 0, st>>>(N, rp, src, Y, ldy, F, bias,
+                                                                          slope, mode, out, attn);
+  }
   return check_launch("gat_agg_fwd_kernel");
 }
 
@@ -666,8 +706,86 @@ __global__ void unfold_attn_kernel(const float* __restrict__ gW, const float* __
   if (lane == 0) (side ? g_ar : g_al)[row] = s;
 }
 
+// dL/dattn_l[h,f] = sum_n d el[n,h] * Z[n,h,f] (likewise attn_r with d er), summed directly over
+// atoms as DGL/autograd does.  (Chaining through the folded GEMM, sum_k gA_l[h,k] W[hF+f,k],
+// is algebraically equal but loses ~sqrt(Fin) in fp32 accuracy when Z cancels.)  Stage 1:
+// each thread owns one Z column over a chunk of atoms, 4 independent partial sums per side.
+__global__ void attn_grad_partial_kernel(int64_t N, int H, int F, const float* __restrict__ Y,
+                                         int64_t ldy, const float* __restrict__ gY, int64_t ldgy,
+                                         int ea, int64_t rows_per, float* __restrict__ part) {
+  const int HF = H * F;
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= HF) return;
+  const int h = col / F;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  float sl[4] = {0.f, 0.f, 0.f, 0.f}, sr[4] = {0.f, 0.f, 0.f, 0.f};
+  int64_t r = r0;
+  for (; r + 4 <= r1; r += 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float z = Y[(r + j) * ldy + col];
+      const float* g = gY + (r + j) * ldgy + ea;
+      sl[j] = fmaf(g[h], z, sl[j]);
+      sr[j] = fmaf(g[H + h], z, sr[j]);
+    }
+  }
+  for (; r < r1; ++r) {
+    const float z = Y[r * ldy + col];
+    const float* g = gY + r * ldgy + ea;
+    sl[0] = fmaf(g[h], z, sl[0]);
+    sr[0] = fmaf(g[H + h], z, sr[0]);
+  }
+  part[((int64_t)blockIdx.y * 2 + 0) * HF + col] = (sl[0] + sl[1]) + (sl[2] + sl[3]);
+  part[((int64_t)blockIdx.y * 2 + 1) * HF + col] = (sr[0] + sr[1]) + (sr[2] + sr[3]);
+}
+
+__global__ void attn_grad_final_kernel(int HF, int S, const float* __restrict__ part,
+                                       float* __restrict__ g_al, float* __restrict__ g_ar) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over 2*HF
+  if (i >= 2 * HF) return;
+  const int side = i / HF, col = i % HF;
+  float s = 0.f;
+  for (int z = 0; z < S; ++z) s += part[((int64_t)z * 2 + side) * HF + col];
+  (side ? g_ar : g_al)[col] = s;
+}
+
+int attn_grad_splits(int64_t N, int HF) {
+  const int64_t colblocks = ceil_div(HF, 256);
+  int64_t s = ceil_div(2048, colblocks);
+  s = std::min<int64_t>(s, ceil_div(N, 256));
+  return (int)std::max<int64_t>(1, s);
+}
+
 }  // namespace
 }  // namespace mvml
+
+extern "C" size_t mvml_gat_attn_grad_workspace_size(int64_t num_nodes, int H, int F) {
+  return carve_size((size_t)attn_grad_splits(num_nodes, H * F) * 2 * H * F * sizeof(float));
+}
+
+extern "C" int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, int mean_residual, const float* Y,
+                                  int64_t ldy, const float* gY, int64_t ldgy, float* g_attn_l,
+                                  float* g_attn_r, void* workspace, size_t workspace_bytes,
+                                  void* stream) {
+  clear_error();
+  MVML_REQUIRE(H > 0 && F > 0 && num_nodes >= 0, "gat_attn_grad: bad shape");
+  const int C = mvml_gat_proj_cols(H, F, mean_residual);
+  MVML_REQUIRE(ldy >= C && ldgy >= C, "gat_attn_grad: bad leading dimension");
+  if (!workspace || workspace_bytes < mvml_gat_attn_grad_workspace_size(num_nodes, H, F)) {
+    set_error("gat_attn_grad: workspace too small");
+    return MVML_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  const int HF = H * F;
+  const int S = attn_grad_splits(num_nodes, HF);
+  const int64_t rows_per = ceil_div(num_nodes > 0 ? num_nodes : 1, S);
+  const int ea = C - 2 * H;
+  float* part = static_cast<float*>(workspace);
+  dim3 g1((unsigned)ceil_div(HF, 256), (unsigned)S);
+  attn_grad_partial_kernel<<<g1, 256, 0, st>>>(num_nodes, H, F, Y, ldy, gY, ldgy, ea, rows_per, part);
+  attn_grad_final_kernel<<<(unsigned)ceil_div(2 * HF, 256), 256, 0, st>>>(HF, S, part, g_attn_l, g_attn_r);
+  return check_launch("attn_grad");
+}
 
 extern "C" int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_l,
                                      const float* attn_r, int H, int F, int Fin, int ldw,
@@ -694,7 +812,7 @@ extern "C" int mvml_gat_unfold_grads(const float* gWcat, const float* fc_w, cons
   unfold_w_kernel<<<blocks, 256, 0, st>>>(gWcat, attn_l, attn_r, H, F, Fin, ldg, mean_residual,
                                           g_fc_w, g_res_fc_w);
   int rc = check_launch("unfold_w_kernel");
-  if (rc) return rc;
+  if (rc || !g_attn_l || !g_attn_r) return rc;  // attention grads: mvml_gat_attn_grad (exact path)
   const int64_t items = 2 * (int64_t)H * F;
   unfold_attn_kernel<<<(unsigned)ceil_div(items, 4), 256, 0, st>>>(gWcat, fc_w, H, F, Fin, ldg,
                                                                    mean_residual, g_attn_l, g_attn_r);

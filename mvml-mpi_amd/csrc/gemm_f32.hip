@@ -135,7 +135,7 @@ struct Stager {
           "ds_read_b32 %1, %4 offset:512\n\t"
           "ds_read_b32 %2, %4 offset:1024\n\t"
           "ds_read_b32 %3, %4 offset:1536"
-          : "=v"(out.x), "=v"(out.y), "=v"(out.z), "=v"(out.w)
+          : "=&v"(out.x), "=&v"(out.y), "=&v"(out.z), "=&v"(out.w)
           : "v"(addr)
           : "memory");
     }
@@ -355,9 +355,15 @@ __global__ void colsum_final_kernel(int64_t N, int S, const float* __restrict__ 
                                     float beta, float* __restrict__ out) {
   const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (col >= N) return;
-  float s = 0.f;
-  for (int z = 0; z < S; ++z) s += part[(int64_t)z * N + col];
-  out[col] = (beta != 0.f ? beta * out[col] : 0.f) + alpha * s;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 loads in flight, fixed order
+  int z = 0;
+  for (; z + 8 <= S; z += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += part[(int64_t)(z + j) * N + col];
+  }
+  for (; z < S; ++z) s[0] += part[(int64_t)z * N + col];
+  const float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  out[col] = (beta != 0.f ? beta * out[col] : 0.f) + alpha * t;
 }
 
 int colsum_splits(int64_t M, int64_t N) {

@@ -115,7 +115,7 @@ class GATLayerFunction(torch.autograd.Function):
         g_out = _c(g_out)
         N, Fp = Xp.shape
         Fin = ctx.Fin
-        dev = X.device
+        dev = Xp.device
         HF = H * F
         mean_res = int(mode == MODE_MEAN)
         C = _lib.lib().mvml_gat_proj_cols(H, F, mean_res)
@@ -138,7 +138,10 @@ class GATLayerFunction(torch.autograd.Function):
         g_al = torch.empty_like(attn_l)
         g_ar = torch.empty_like(attn_r)
         call("mvml_gat_unfold_grads", ptr(gW), ptr(_c(fc_w)), ptr(_c(attn_l)), ptr(_c(attn_r)), H, F, Fin,
-             Fp, mean_res, ptr(g_fc), ptr(g_res), ptr(g_al), ptr(g_ar), st)
+             Fp, mean_res, ptr(g_fc), ptr(g_res), None, None, st)
+        wp2, wn2 = _lib.ws_ptr_size(L.mvml_gat_attn_grad_workspace_size(N, H, F), dev)
+        call("mvml_gat_attn_grad", N, H, F, mean_res, ptr(Y), ldy, ptr(gY), ldy, ptr(g_al), ptr(g_ar),
+             wp2, wn2, st)
         g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
         if mean_res:  # every head's bias sees g_out / H: one column sum, replicated over heads
             colsum(gY, N, F, ldy, g_bias, offset=HF, alpha=1.0 / H)

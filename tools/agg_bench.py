@@ -1,0 +1,76 @@
+"""Microbenchmark of the fused GAT aggregation kernels, per layer, on the bench workload
+(65,536 KEGG-like molecules): time per launch and algorithmic GB/s (formulas in
+mvml_gat.functional.agg_fwd_bytes / agg_bwd_bytes), plus the Set2Set segment pass."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "mvml-mpi_amd"), ROOT]
+import torch  # noqa: E402
+
+from mvml_gat import _lib, synth  # noqa: E402
+from mvml_gat._lib import call, ptr  # noqa: E402
+from mvml_gat.functional import agg_bwd_bytes, agg_fwd_bytes  # noqa: E402
+
+
+def timeit(fn, it=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mols", type=int, default=65536)
+    ap.add_argument("--config", default="3")
+    a = ap.parse_args()
+    sb = getattr(synth, f"config{a.config}")(a.mols)
+    g = sb.to_graph().to("cuda")
+    N, E = g.num_nodes(), g.num_edges()
+    L = _lib.lib()
+    st = _lib.stream_ptr()
+    print(f"config{a.config}: {a.mols} molecules, N={N}, E={E}")
+    for (H, F, mode, name) in ((4, 192, 0, "L1 flatten+ELU"), (4, 384, 1, "L2 mean")):
+        C = L.mvml_gat_proj_cols(H, F, int(mode == 1))
+        ldy = (C + 3) // 4 * 4
+        Y = torch.randn((N, ldy), device="cuda") * 0.3
+        bias = torch.randn(H * F, device="cuda") * 0.1
+        oc = F if mode == 1 else H * F
+        out = torch.empty((N, oc), device="cuda")
+        attn = torch.empty((E, H), device="cuda")
+        f = lambda: call("mvml_gat_agg_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F,
+                         ptr(bias), 0.2, mode, ptr(out), ptr(attn), st)
+        ms = timeit(f)
+        by = agg_fwd_bytes(N, E, H, F, oc, C - H * F - 2 * H)
+        print(f"  agg_fwd {name:16s} {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
+        g_out = torch.randn_like(out)
+        gY = torch.empty((N, ldy), device="cuda")
+        wsz = L.mvml_gat_agg_bwd_workspace_size(E, H)
+        ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
+        b = lambda: call("mvml_gat_agg_bwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr),
+                         ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(attn), ptr(out), ptr(g_out),
+                         H, F, 0.2, mode, ptr(gY), ldy, ptr(ws), wsz, st)
+        ms = timeit(b)
+        by = agg_bwd_bytes(N, E, H, F, oc, mode)
+        print(f"  agg_bwd {name:16s} {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
+        del Y, gY, out, attn, ws
+    D = 384
+    X = torch.randn((N, D), device="cuda")
+    B = g.batch_size
+    qs = torch.randn((B, 2 * D), device="cuda")
+    lse = torch.empty(B, device="cuda")
+    f = lambda: call("mvml_set2set_seg_fwd", B, D, ptr(g.node_offsets), ptr(X), ptr(qs), 2 * D, ptr(lse), st)
+    ms = timeit(f)
+    by = 4 * (N * D + B * 3 * D)
+    print(f"  set2set seg_fwd        {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
+
+
+if __name__ == "__main__":
+    main()
