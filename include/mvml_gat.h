@@ -83,61 +83,62 @@ int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx, float alp
                     float* out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
- * GATConv projection (dgl 0.9.1 GATConv.fc, res_fc, and the el/er reductions
- * `(feat_src * attn_l).sum(-1)` / `(feat_dst * attn_r).sum(-1)`), folded into ONE GEMM:
- *   Y[N, C] = X[N, Fin] * Wcat^T,  Wcat[C, Fin] rows = [fc.weight ; Wr ; A_l ; A_r]
- *   A_l[h,k] = sum_f attn_l[h,f] * fc.weight[h*F+f, k]   (likewise A_r with attn_r)
+ * GATConv projection (dgl 0.9.1 GATConv.fc and res_fc, gatconv.py forward, homogeneous-graph
+ * branch; called from dgllife GATLayer.forward, model.py:79-81) as ONE GEMM:
+ *   Y[N, C] = X[N, Fin] * Wcat^T,  Wcat[C, Fin] rows = [fc.weight ; Wr]
  *   Wr = res_fc.weight (H*F rows), or with mean_residual = 1 its head mean
  *        (1/H) sum_h res_fc.weight[h*F+f, :] (F rows): a 'mean' GATLayer only ever uses the
  *        head-mean of the residual, so that layer's GEMM is 37 % smaller.
- *   Y row = [ Z (H*F) | R (H*F or F) | el (H) | er (H) ];  C = mvml_gat_proj_cols(H,F,mean).
+ *   Y row = [ Z (H*F) | R (H*F or F) ];  C = mvml_gat_proj_cols(H,F,mean).
  *   Wcat has row stride ldw >= Fin; columns Fin..ldw-1 are written as zeros, so a caller can
  *   pad X to a multiple of 4 columns and keep every GEMM operand 16-B aligned.
- * mvml_gat_unfold_grads maps dL/dWcat back onto fc.weight and res_fc.weight (and, if the
- * g_attn pointers are non-NULL, onto attn_l/attn_r through the fold; the library's own path
- * instead uses mvml_gat_attn_grad, which sums d el * Z over atoms directly like autograd does,
- * because chaining through the fold loses ~sqrt(Fin) of fp32 accuracy when Z cancels).
+ * The attention reductions el/er are NOT folded into the GEMM: they are computed from Z inside
+ * mvml_gat_agg_fwd exactly like `(feat * attn_l).sum(-1)`, which keeps fp32 logits as accurate
+ * as the reference's.  mvml_gat_unfold_grads maps dL/dWcat back onto fc.weight and
+ * res_fc.weight (the mean residual's gradient is replicated / H over the heads).
  * ------------------------------------------------------------------------------------- */
 int mvml_gat_proj_cols(int H, int F, int mean_residual);
-int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_l,
-                          const float* attn_r, int H, int F, int Fin, int ldw, int mean_residual,
-                          float* Wcat, void* stream);
-int mvml_gat_unfold_grads(const float* gWcat, const float* fc_w, const float* attn_l,
-                          const float* attn_r, int H, int F, int Fin, int ldg, int mean_residual,
-                          float* g_fc_w, float* g_res_fc_w, float* g_attn_l, float* g_attn_r,
-                          void* stream);
+int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, int H, int F, int Fin,
+                          int ldw, int mean_residual, float* Wcat, void* stream);
+int mvml_gat_unfold_grads(const float* gWcat, int H, int F, int Fin, int ldg, int mean_residual,
+                          float* g_fc_w, float* g_res_fc_w, void* stream);
 
-/* dL/dattn_l[h,f] = sum_n gY[n, el+h] * Z[n, h*F+f] and likewise attn_r (the autograd of
- * `(feat * attn_l).sum(-1)` in GATConv.forward); deterministic two-stage column reduction. */
+/* dL/dattn_l[h,f] = sum_n gelr[n, h] * Z[n, h*F+f] and dL/dattn_r with gelr[n, H+h] (autograd
+ * of `(feat * attn_l).sum(-1)` in GATConv.forward); deterministic two-stage reduction. */
 size_t mvml_gat_attn_grad_workspace_size(int64_t num_nodes, int H, int F);
-int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, int mean_residual, const float* Y,
-                       int64_t ldy, const float* gY, int64_t ldgy, float* g_attn_l,
-                       float* g_attn_r, void* workspace, size_t workspace_bytes, void* stream);
+int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, const float* Y, int64_t ldy,
+                       const float* gelr, float* g_attn_l, float* g_attn_r, void* workspace,
+                       size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
- * Fused GAT attention + aggregation, forward (one wavefront per destination atom):
- *   apply_edges(u_add_v) -> LeakyReLU(slope) -> edge_softmax -> update_all(u_mul_e, sum)
- *   -> + residual R -> + bias -> GATLayer agg (dgllife 0.3.0): mode 0 flatten+ELU,
- *   mode 1 mean over heads, mode 2 flatten (no activation).
+ * Fused GAT attention + aggregation, forward (one wavefront per destination atom; replaces
+ * dgl GATConv.forward from `el = ...` to the residual/bias, plus dgllife GATLayer's
+ * flatten/ELU or head-mean, model.py:77-81):
+ *   el/er = <Z, attn_l/attn_r> -> apply_edges(u_add_v) -> LeakyReLU(slope) -> edge_softmax
+ *   -> update_all(u_mul_e, sum) -> + residual R -> + bias -> GATLayer agg (dgllife 0.3.0):
+ *   mode 0 flatten+ELU, mode 1 mean over heads, mode 2 flatten (no activation).
  * Y is the projection output above (mean_residual layout iff mode 1; ldy >= its C, multiple of
- * 4).  out is [N, H*F] (modes 0, 2) or [N, F] (mode 1).  attn (optional, may be NULL) receives edge_softmax output [E, H] in
- * in-CSR slot order, for the backward.
+ * 4).  attn_l/attn_r: [H*F] (GATConv.attn_l / attn_r).  out is [N, H*F] (modes 0, 2) or [N, F]
+ * (mode 1).  attn [E, H] receives the edge_softmax output in in-CSR slot order and elr [N, 2H]
+ * the logit halves [el | er]; both are required by the backward.
  * ------------------------------------------------------------------------------------- */
 int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
-                     const float* Y, int64_t ldy, int H, int F, const float* bias, float slope,
-                     int mode, float* out, float* attn, void* stream);
+                     const float* Y, int64_t ldy, int H, int F, const float* attn_l,
+                     const float* attn_r, const float* bias, float slope, int mode, float* out,
+                     float* attn, float* elr, void* stream);
 /* Backward of mvml_gat_agg_fwd (DGL GSpMM / GSDDMM / EdgeSoftmax backward + torch autograd of
- * the residual/bias/ELU/mean).  Atomic-free: the u_mul_e-sum transpose is a gather over the
- * out-CSR.  Writes gY[N, ldgy] = [dZ | dR | d el | d er] (the GEMM backward's input, same
- * column layout as Y).
- * out is the forward output (mode 0 uses ELU'(x) = out + 1 for x <= 0).  gpre_ws: [E, H]. */
+ * el/er, residual, bias, ELU, mean).  Atomic-free: the u_mul_e-sum transpose is a gather over
+ * the out-CSR.  Writes gY[N, ldgy] = [dZ | dR] (the GEMM backward's input, same column layout
+ * as Y) and gelr[N, 2H] = [d el | d er] (input of mvml_gat_attn_grad).
+ * out is the forward output (mode 0 uses ELU'(x) = out + 1 for x <= 0).  workspace: [E, H]. */
 size_t mvml_gat_agg_bwd_workspace_size(int64_t num_edges, int H);
 int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
                      const int32_t* out_rowptr, const int32_t* out_dst,
-                     const int32_t* out_inslot, const float* Y, int64_t ldy, const float* attn,
+                     const int32_t* out_inslot, const float* Y, int64_t ldy, const float* elr,
+                     const float* attn, const float* attn_l, const float* attn_r,
                      const float* out, const float* g_out, int H, int F, float slope, int mode,
-                     float* gY, int64_t ldgy, void* workspace, size_t workspace_bytes,
-                     void* stream);
+                     float* gY, int64_t ldgy, float* gelr, void* workspace,
+                     size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Set2Set (dgl 0.9.1, model.py:82-84, 92) building blocks.

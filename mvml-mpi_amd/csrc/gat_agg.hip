@@ -1,32 +1,34 @@
-// Fused GAT attention + aggregation (dgl 0.9.1 GATConv.forward after the projection) and its
-// atomic-free backward.  One wavefront per destination atom.
+// Fused GAT attention + aggregation (dgl 0.9.1 GATConv.forward after fc/res_fc) and its
+// atomic-free backward.  One wavefront per destination atom (two for wide layers).
 //
-// Projection row layout (written by the folded GEMM, see mvml_gat_fold_weights):
-//   Y[n] = [ Z (H*F) | R (RW) | el (H) | er (H) ]     RW = H*F (flatten modes) or F (mean)
-// In mean mode (dgllife's last GATLayer, agg 'mean') only the head-mean of the residual is
-// ever used, so the GEMM produces R_mean = X * mean_h(W_res_h)^T directly (F columns instead
-// of H*F: 37 % fewer FLOPs and bytes for the 768 -> 4x384 layer).
+// Projection row layout (the plain fc / res_fc GEMM, see mvml_gat_fold_weights):
+//   Y[n] = [ Z (H*F) | R (RW) ]            RW = H*F (flatten modes) or F (mean mode)
+// In mean mode (dgllife's last GATLayer, agg 'mean') only the head-mean of the residual is ever
+// used, so the GEMM produces R_mean = X * mean_h(W_res_h)^T directly (F columns instead of H*F).
 //
 // Forward, per destination v (rows of the in-CSR, in-edges in ascending edge id):
-//   s_e   = LeakyReLU(el[src_e] + er[v], slope)            apply_edges(u_add_v), leaky_relu
-//   a_e   = exp(s_e - max_v s) / sum_v exp(s - max_v s)   edge_softmax (norm_by = dst)
-//   rst_v = sum_e a_e * Z[src_e] + R[v] + bias            update_all(u_mul_e, sum), res_fc, bias
-//   out_v = ELU(rst_v.flatten) | mean_h(rst_v) | rst_v    dgllife GATLayer agg_mode/activation
-// Lanes take the in-edges (64 per chunk) for the logits/softmax, then the wave walks the
-// edges and every lane accumulates 4 consecutive feature columns per 256-column slice
-// (16-B loads of the gathered Z rows).
+//   el[n,h] = <Z[n,h,:], attn_l[h,:]>, er[n,h] = <Z[n,h,:], attn_r[h,:]>   GATConv el / er, from
+//             Z exactly like `(feat_src * attn_l).sum(-1)`; saved to elr[n] = [el | er]
+//   s_e   = LeakyReLU(el[src_e] + er[v], slope)                apply_edges(u_add_v), leaky_relu
+//   a_e   = exp(s_e - max_v s) / sum_v exp(s - max_v s)       edge_softmax (norm_by = dst)
+//   rst_v = sum_e a_e * Z[src_e] + R[v] + bias                update_all(u_mul_e, sum), res, bias
+//   out_v = ELU(rst_v.flatten) | mean_h(rst_v) | rst_v        dgllife GATLayer agg / activation
+// Two launches: gat_logits_kernel streams Z once into the compact elr array, then the
+// aggregation kernel gathers 16-B logits per in-edge for the softmax and the Z rows for the sum.
+// (A single-pass variant that reduces el[u] from each gathered Z row with an online softmax was
+// measured 2x slower: its per-edge shuffle -> exp -> rescale chain is latency-bound.)
 //
 // Backward (two passes, no float atomics):
 //   A (per dst v):  g_a_e = <Z[src_e], g_rst[v]>_f per head; g_s = a*(g_a - sum_v a*g_a);
-//                   g_pre = g_s * leaky'(s_e); d er[v] = sum_e g_pre           -> gpre_ws, gY
-//                   and the residual gradient dR[v] (= g_rst[v], or g_out[v] in mean mode)
-//   B (per src u):  dZ[u] = sum_{e: u->w} a_e * g_rst[w]; d el[u] = sum_{e: u->w} g_pre_e
-//                   (gather over the out-CSR, out_inslot -> in-CSR slot of the edge; g_rst[w]
-//                   rows come back from gY's dR block)                              -> gY
+//                   g_pre = g_s * leaky'(s_e); d er[v] = sum_e g_pre; dR[v] = g_rst[v] (or
+//                   g_out[v] for the head-mean residual)                 -> gpre_ws, gelr, gY
+//   B (per src u):  dZ[u] = sum_{e: u->w} a_e * g_rst[w] + d el[u] attn_l + d er[u] attn_r,
+//                   d el[u] = sum_{e: u->w} g_pre_e (gather over the out-CSR; out_inslot maps an
+//                   out-edge to its in-CSR slot; g_rst[w] rows come back from gY's dR block)
+//   dL/dattn_{l,r} = sum_n d{el,er}[n,h] Z[n,h,:]   (mvml_gat_attn_grad, directly over atoms)
 //
-// Workgroup -> node mapping is XCD-aware: the dispatcher deals workgroups round-robin over the
-// 8 XCDs, so logical block = remap(blockIdx) gives each XCD one contiguous range of atoms; a
-// molecule's neighbour rows are then gathered from ONE XCD's L2 instead of up to eight.
+// Workgroup -> atom mapping is XCD-aware (xcd_block): each XCD walks one contiguous range of
+// atoms, so a molecule's neighbour rows are gathered from ONE XCD's L2.
 #include "common.h"
 
 namespace mvml {
@@ -55,9 +57,6 @@ __device__ __forceinline__ float4 fma4(float a, float4 z, float4 c) {
 __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
-__device__ __forceinline__ float4 scale4(float4 a, float s) {
-  return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
-}
 __device__ __forceinline__ float dot4(float4 a, float4 b) {
   return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
 }
@@ -70,6 +69,16 @@ __device__ __forceinline__ float pick(const float (&a)[H], int h) {
 #pragma unroll
   for (int k = 1; k < H; ++k) r = (h == k) ? a[k] : r;
   return r;
+}
+template <int H>
+__device__ __forceinline__ void add_at(float (&a)[H], int h, float v) {
+#pragma unroll
+  for (int k = 0; k < H; ++k) a[k] += (h == k) ? v : 0.f;
+}
+// wave-uniform per-head values -> p[0..H): lane h stores a[h]
+template <int H>
+__device__ __forceinline__ void store_heads(float* p, const float (&a)[H], int lane) {
+  if (lane < H) p[lane] = pick<H>(a, lane);
 }
 
 // All-reduce of H per-lane values over the 64 lanes in (H - 1) + (6 - log2 H) shuffles instead
@@ -126,15 +135,53 @@ __device__ __forceinline__ float4 grst_of(const float* __restrict__ g_out, const
   return g;
 }
 
-// Forward.  CS waves share one destination atom, each owning HW = H / CS heads (HF / CS
+// ---------------------------------------------------------------------------------- forward
+// Logits: el[n,h] = <Z[n,h,:], attn_l[h,:]>, er likewise, one wave per atom (a streaming read of
+// Z, 16-B slices per lane, butterfly head reduction).  elr[n] = [el | er] is a compact [N, 2H]
+// array, so the aggregation gathers a neighbour's logits as one 16-B load instead of reaching
+// into Y's wide rows.
+template <int H, int VPL>
+__global__ void __launch_bounds__(kWavesPerBlock * 64)
+gat_logits_kernel(int64_t N, const float* __restrict__ Y, int64_t ldy, int F,
+                  const float* __restrict__ attn_l, const float* __restrict__ attn_r,
+                  float* __restrict__ elr) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t v = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  if (v >= N) return;
+  const int HF = H * F;
+  const float* yv = Y + v * ldy;
+  float el[H], er[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) { el[h] = 0.f; er[h] = 0.f; }
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    if (col < HF) {
+      const float4 z = ld4(yv + col);
+      const int h = col / F;
+      add_at<H>(el, h, dot4(z, ld4(attn_l + col)));
+      add_at<H>(er, h, dot4(z, ld4(attn_r + col)));
+    }
+  }
+  HeadReduce<H>::template all<false>(el, lane);
+  HeadReduce<H>::template all<false>(er, lane);
+  store_heads<H>(elr + v * 2 * H, el, lane);
+  store_heads<H>(elr + v * 2 * H + H, er, lane);
+}
+
+// Aggregation.  CS waves share one destination atom, each owning HW = H / CS heads (HF / CS
 // columns): the wide 768 -> 4x384 layer runs with CS = 2 so every wave keeps only 3 float4
 // column slices per gathered row (half the VGPRs -> twice the waves in flight to hide the
-// dependent el-gather -> softmax -> Z-gather chain).  Block = 4 waves = 4 / CS atoms.
+// dependent logit-gather -> softmax -> Z-gather chain).  Block = 4 waves = 4 / CS atoms.
+// Lanes take the in-edges (64 per chunk) for the softmax (max -> exp -> sum -> divide, as
+// dgl's edge_softmax), then the wave walks the edges two at a time, every lane accumulating 4
+// consecutive columns per 256-column slice of the gathered Z rows.
 template <int H, int VPL, int CS>
 __global__ void __launch_bounds__(kWavesPerBlock * 64)
 gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
-                   const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ bias,
-                   float slope, int mode, float* __restrict__ out, float* __restrict__ attn) {
+                   const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ elr,
+                   const float* __restrict__ bias, float slope, int mode, float* __restrict__ out,
+                   float* __restrict__ attn) {
   constexpr int HW = H / CS;
   __shared__ __attribute__((aligned(16))) float red[kWavesPerBlock][VPL * 256];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -143,19 +190,17 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
   const bool live = v < N;  // (CS > 1: every wave must reach the block barrier)
   if (CS == 1 && !live) return;
   const int HF = H * F;
-  const int HFW = HF / CS;           // columns of this wave
-  const int c0 = part * HFW;         // first column (global) of this wave
-  const int h0 = part * HW;          // first head of this wave
-  const int RW = (mode == 1) ? F : HF;
-  const int EA = HF + RW;            // el column; er at EA + H
+  const int HFW = HF / CS;    // columns of this wave
+  const int c0 = part * HFW;  // first column (global) of this wave
+  const int h0 = part * HW;   // first head of this wave
   const int beg = live ? rowptr[v] : 0, end = live ? rowptr[v + 1] : 0;
   const int deg = end - beg;
   const float* yv = Y + (live ? v : 0) * ldy;
   float er[HW];
 #pragma unroll
-  for (int h = 0; h < HW; ++h) er[h] = live ? yv[EA + H + h0 + h] : 0.f;
+  for (int h = 0; h < HW; ++h) er[h] = live ? elr[v * 2 * H + H + h0 + h] : 0.f;
 
-  // ---- softmax statistics over the in-edges (exactly max -> exp -> sum -> divide) ----
+  // ---- softmax statistics over the in-edges ----
   float mx[HW], sm[HW], s_l[HW];
   int u_l = 0;
 #pragma unroll
@@ -164,9 +209,9 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
     const bool valid = base + lane < deg;
     if (valid) {
       u_l = in_src[beg + base + lane];
-      const float* yu = Y + (int64_t)u_l * ldy + EA + h0;
+      const float* eu = elr + (int64_t)u_l * 2 * H + h0;
 #pragma unroll
-      for (int h = 0; h < HW; ++h) s_l[h] = leaky(yu[h] + er[h], slope);
+      for (int h = 0; h < HW; ++h) s_l[h] = leaky(eu[h] + er[h], slope);
     } else {
 #pragma unroll
       for (int h = 0; h < HW; ++h) s_l[h] = -INFINITY;
@@ -189,9 +234,9 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
       float ex[HW];
       if (valid) {
         const int u = in_src[beg + base + lane];
-        const float* yu = Y + (int64_t)u * ldy + EA + h0;
+        const float* eu = elr + (int64_t)u * 2 * H + h0;
 #pragma unroll
-        for (int h = 0; h < HW; ++h) ex[h] = expf(leaky(yu[h] + er[h], slope) - mx[h]);
+        for (int h = 0; h < HW; ++h) ex[h] = expf(leaky(eu[h] + er[h], slope) - mx[h]);
       } else {
 #pragma unroll
         for (int h = 0; h < HW; ++h) ex[h] = 0.f;
@@ -219,20 +264,17 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
     if (!one_chunk) {
       if (base + lane < deg) {
         u_l = in_src[beg + base + lane];
-        const float* yu = Y + (int64_t)u_l * ldy + EA + h0;
+        const float* eu = elr + (int64_t)u_l * 2 * H + h0;
 #pragma unroll
-        for (int h = 0; h < HW; ++h) s_l[h] = leaky(yu[h] + er[h], slope);
+        for (int h = 0; h < HW; ++h) s_l[h] = leaky(eu[h] + er[h], slope);
       }
     }
 #pragma unroll
     for (int h = 0; h < HW; ++h) a_l[h] = (base + lane < deg) ? expf(s_l[h] - mx[h]) / sm[h] : 0.f;
-    if (attn && base + lane < deg) {
+    if (base + lane < deg) {
       float* ap = attn + (int64_t)(beg + base + lane) * H + h0;
-      if (HW == 4) st4(ap, make_float4(a_l[0], a_l[HW > 1 ? 1 : 0], a_l[HW > 2 ? 2 : 0], a_l[HW > 3 ? 3 : 0]));
-      else {
 #pragma unroll
-        for (int h = 0; h < HW; ++h) ap[h] = a_l[h];
-      }
+      for (int h = 0; h < HW; ++h) ap[h] = a_l[h];
     }
     int j = 0;
     for (; j + 1 < cnt; j += 2) {
@@ -267,7 +309,7 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
     }
   }
 
-  // ---- epilogue: + residual + bias, then GATLayer aggregation ----
+  // ---- epilogue: + residual + bias, then the GATLayer aggregation ----
   if (mode == 1) {
     // rst + bias of this wave's heads -> LDS; the part-0 wave of the atom sums the heads in
     // order h = 0..H-1, divides by H and adds the head-mean residual.
@@ -310,19 +352,20 @@ gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
   }
 }
 
-// Backward pass A: one wave per destination v.
+// --------------------------------------------------------------------------------- backward
+// Pass A: one wave per destination v.
 template <int H, int VPL>
 __global__ void __launch_bounds__(kWavesPerBlock * 64)
 gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
-                       const float* __restrict__ Y, int64_t ldy, const float* __restrict__ attn,
-                       const float* __restrict__ out, const float* __restrict__ g_out, int F,
-                       float slope, int mode, float* __restrict__ gpre, float* __restrict__ gY,
-                       int64_t ldgy) {
+                       const float* __restrict__ Y, int64_t ldy, const float* __restrict__ elr,
+                       const float* __restrict__ attn, const float* __restrict__ out,
+                       const float* __restrict__ g_out, int F, float slope, int mode,
+                       float* __restrict__ gpre, float* __restrict__ gY, int64_t ldgy,
+                       float* __restrict__ gelr) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t v = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
   if (v >= N) return;
   const int HF = H * F;
-  const int EA = HF + ((mode == 1) ? F : HF);
   const int beg = rowptr[v], end = rowptr[v + 1];
   const int deg = end - beg;
   int hc[VPL];
@@ -347,10 +390,9 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
       st4(gyv + HF + col, ld4(g_out + v * F + col));
     }
   }
-  const float* yv = Y + v * ldy;
   float er[H];
 #pragma unroll
-  for (int h = 0; h < H; ++h) er[h] = yv[EA + H + h];
+  for (int h = 0; h < H; ++h) er[h] = elr[v * 2 * H + H + h];
 
   float dots[H];  // sum_e a_e * g_a_e per head
 #pragma unroll
@@ -358,23 +400,17 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
   float ga_l[H], a_l[H];
   for (int base = 0; base < deg; base += 64) {
     const int cnt = min(64, deg - base);
-    int u_l = 0;
-    if (base + lane < deg) u_l = in_src[beg + base + lane];
+    const int u_l = (base + lane < deg) ? in_src[beg + base + lane] : 0;
 #pragma unroll
     for (int h = 0; h < H; ++h) ga_l[h] = 0.f;
     for (int j = 0; j < cnt; ++j) {
-      const int u = rl(u_l, j);
-      const float* zu = Y + (int64_t)u * ldy;
+      const float* zu = Y + (int64_t)rl(u_l, j) * ldy;
       float part[H];
 #pragma unroll
       for (int h = 0; h < H; ++h) part[h] = 0.f;
 #pragma unroll
       for (int c = 0; c < VPL; ++c)
-        if (okc[c]) {
-          const float d = dot4(ld4(zu + 4 * (lane + 64 * c)), gr[c]);
-#pragma unroll
-          for (int h = 0; h < H; ++h) part[h] += (hc[c] == h) ? d : 0.f;
-        }
+        if (okc[c]) add_at<H>(part, hc[c], dot4(ld4(zu + 4 * (lane + 64 * c)), gr[c]));
       HeadReduce<H>::template all<false>(part, lane);
 #pragma unroll
       for (int h = 0; h < H; ++h) ga_l[h] = (lane == j) ? part[h] : ga_l[h];
@@ -402,15 +438,13 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
     const int64_t slot = beg + base + lane;
     float gp[H];
     if (valid) {
-      const int u = in_src[slot];
-      const float* yu = Y + (int64_t)u * ldy + EA;
+      const float* el_u = elr + (int64_t)in_src[slot] * 2 * H;
 #pragma unroll
       for (int h = 0; h < H; ++h) {
         const float a = (deg > 64) ? attn[slot * H + h] : a_l[h];
         const float ga = (deg > 64) ? gpre[slot * H + h] : ga_l[h];
         const float gs = a * (ga - dots[h]);
-        const float spre = yu[h] + er[h];
-        gp[h] = spre > 0.f ? gs : gs * slope;
+        gp[h] = (el_u[h] + er[h]) > 0.f ? gs : gs * slope;
         gpre[slot * H + h] = gp[h];
       }
     } else {
@@ -421,28 +455,22 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
 #pragma unroll
     for (int h = 0; h < H; ++h) ger[h] += gp[h];
   }
-  if (lane < H) {
-    float g = ger[0];
-#pragma unroll
-    for (int h = 1; h < H; ++h) g = (lane == h) ? ger[h] : g;
-    gY[v * ldgy + EA + H + lane] = g;
-  }
+  store_heads<H>(gelr + v * 2 * H + H, ger, lane);
 }
 
-// Backward pass B: one wave per source u (out-CSR gather).
+// Pass B: one wave per source u (out-CSR gather).
 template <int H, int VPL>
 __global__ void __launch_bounds__(kWavesPerBlock * 64)
 gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
                        const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
                        const float* __restrict__ attn, const float* __restrict__ gpre,
+                       const float* __restrict__ attn_l, const float* __restrict__ attn_r,
                        const float* __restrict__ out, const float* __restrict__ g_out, int F,
-                       int mode, float* __restrict__ gY, int64_t ldgy) {
+                       int mode, float* __restrict__ gY, int64_t ldgy, float* __restrict__ gelr) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t u = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
   if (u >= N) return;
   const int HF = H * F;
-  const int RW = (mode == 1) ? F : HF;
-  const int EA = HF + RW;
   const int beg = out_rowptr[u], end = out_rowptr[u + 1];
   const int deg = end - beg;
   int hc[VPL];
@@ -471,12 +499,9 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
 #pragma unroll
       for (int h = 0; h < H; ++h) { a_l[h] = 0.f; gp_l[h] = 0.f; }
     }
-    float gsum[H];
+    HeadReduce<H>::template all<false>(gp_l, lane);
 #pragma unroll
-    for (int h = 0; h < H; ++h) gsum[h] = gp_l[h];
-    HeadReduce<H>::template all<false>(gsum, lane);
-#pragma unroll
-    for (int h = 0; h < H; ++h) gel[h] += gsum[h];
+    for (int h = 0; h < H; ++h) gel[h] += gp_l[h];
     for (int j = 0; j < cnt; ++j) {
       const int w = rl(w_l, j);
       float a[H];
@@ -492,31 +517,40 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
         }
     }
   }
+  // + the el / er paths: Z also feeds el = <Z, attn_l> and er = <Z, attn_r>
+  float ger[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) ger[h] = gelr[u * 2 * H + H + h];
   float* gyu = gY + u * ldgy;
 #pragma unroll
   for (int c = 0; c < VPL; ++c)
-    if (okc[c]) st4(gyu + 4 * (lane + 64 * c), gz[c]);
-  if (lane < H) {
-    float g = gel[0];
-#pragma unroll
-    for (int h = 1; h < H; ++h) g = (lane == h) ? gel[h] : g;
-    gyu[EA + lane] = g;
-  }
+    if (okc[c]) {
+      const int col = 4 * (lane + 64 * c);
+      float4 g = fma4(pick<H>(gel, hc[c]), ld4(attn_l + col), gz[c]);
+      g = fma4(pick<H>(ger, hc[c]), ld4(attn_r + col), g);
+      st4(gyu + col, g);
+    }
+  store_heads<H>(gelr + u * 2 * H, gel, lane);
 }
 
 template <int H, int VPL>
 int launch_fwd(int64_t N, const int32_t* rp, const int32_t* src, const float* Y, int64_t ldy, int F,
-               const float* bias, float slope, int mode, float* out, float* attn, hipStream_t st) {
+               const float* al, const float* ar, const float* bias, float slope, int mode, float* out,
+               float* attn, float* elr, hipStream_t st) {
+  gat_logits_kernel<H, VPL><<<(unsigned)ceil_div(N, kWavesPerBlock), kWavesPerBlock * 64, 0, st>>>(
+      N, Y, ldy, F, al, ar, elr);
+  int rc = check_launch("gat_logits_kernel");
+  if (rc) return rc;
   // Wide layers (more than 4 float4 slices per lane) split the columns over 2 waves.
   if constexpr (VPL > 4 && H % 2 == 0) {
     constexpr int CS = 2, V2 = (VPL + 1) / 2;
     const unsigned blocks = (unsigned)ceil_div(N, kWavesPerBlock / CS);
-    gat_agg_fwd_kernel<H, V2, CS><<<blocks, kWavesPerBlock * 64, 0, st>>>(N, rp, src, Y, ldy, F, bias,
-                                                                          slope, mode, out, attn);
+    gat_agg_fwd_kernel<H, V2, CS><<<blocks, kWavesPerBlock * 64, 0, st>>>(
+        N, rp, src, Y, ldy, F, elr, bias, slope, mode, out, attn);
   } else {
     const unsigned blocks = (unsigned)ceil_div(N, kWavesPerBlock);
-    gat_agg_fwd_kernel<H, VPL, 1><<<blocks, kWavesPerBlock * 64, 0, st>>>(N, rp, src, Y, ldy, F, bias,
-                                                                          slope, mode, out, attn);
+    gat_agg_fwd_kernel<H, VPL, 1><<<blocks, kWavesPerBlock * 64, 0, st>>>(
+        N, rp, src, Y, ldy, F, elr, bias, slope, mode, out, attn);
   }
   return check_launch("gat_agg_fwd_kernel");
 }
@@ -524,15 +558,16 @@ int launch_fwd(int64_t N, const int32_t* rp, const int32_t* src, const float* Y,
 template <int H, int VPL>
 int launch_bwd(int64_t N, const int32_t* rp, const int32_t* src, const int32_t* orp,
                const int32_t* odst, const int32_t* oslot, const float* Y, int64_t ldy,
-               const float* attn, const float* out, const float* g_out, int F, float slope,
-               int mode, float* gpre, float* gY, int64_t ldgy, hipStream_t st) {
+               const float* elr, const float* attn, const float* al, const float* ar,
+               const float* out, const float* g_out, int F, float slope, int mode, float* gpre,
+               float* gY, int64_t ldgy, float* gelr, hipStream_t st) {
   const unsigned blocks = (unsigned)ceil_div(N, kWavesPerBlock);
   gat_agg_bwd_dst_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
-      N, rp, src, Y, ldy, attn, out, g_out, F, slope, mode, gpre, gY, ldgy);
+      N, rp, src, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, gelr);
   int rc = check_launch("gat_agg_bwd_dst_kernel");
   if (rc) return rc;
   gat_agg_bwd_src_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
-      N, orp, odst, oslot, attn, gpre, out, g_out, F, mode, gY, ldgy);
+      N, orp, odst, oslot, attn, gpre, al, ar, out, g_out, F, mode, gY, ldgy, gelr);
   return check_launch("gat_agg_bwd_src_kernel");
 }
 
@@ -561,158 +596,12 @@ int check_shapes(int H, int F, int mode, int64_t ldy, const void* Y, const char*
   return MVML_OK;
 }
 
-}  // namespace
-}  // namespace mvml
-
-using namespace mvml;
-
-extern "C" int mvml_gat_proj_cols(int H, int F, int mean_residual) {
-  return H * F + (mean_residual ? F : H * F) + 2 * H;
-}
-
-extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
-                                const float* Y, int64_t ldy, int H, int F, const float* bias,
-                                float slope, int mode, float* out, float* attn, void* stream) {
-  clear_error();
-  int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_fwd");
-  if (rc) return rc;
-  MVML_REQUIRE(((uintptr_t)out & 15) == 0 && ((uintptr_t)bias & 15) == 0, "gat_agg_fwd: unaligned out/bias");
-  if (num_nodes == 0) return MVML_OK;
-  hipStream_t st = as_stream(stream);
-  const int vpl = (int)ceil_div(H * F, 256);
-  switch (H) {
-    case 1: { MVML_VPL_CASES(launch_fwd, 1, num_nodes, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, st) break; }
-    case 2: { MVML_VPL_CASES(launch_fwd, 2, num_nodes, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, st) break; }
-    case 4: { MVML_VPL_CASES(launch_fwd, 4, num_nodes, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, st) break; }
-    case 8: { MVML_VPL_CASES(launch_fwd, 8, num_nodes, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, st) break; }
-  }
-  set_error("gat_agg_fwd: unsupported shape");
-  return MVML_ERR_INVALID;
-}
-
-extern "C" size_t mvml_gat_agg_bwd_workspace_size(int64_t num_edges, int H) {
-  return carve_size((size_t)num_edges * H * sizeof(float));
-}
-
-extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
-                                const int32_t* out_rowptr, const int32_t* out_dst,
-                                const int32_t* out_inslot, const float* Y, int64_t ldy,
-                                const float* attn, const float* out, const float* g_out, int H,
-                                int F, float slope, int mode, float* gY, int64_t ldgy,
-                                void* workspace, size_t workspace_bytes, void* stream) {
-  clear_error();
-  int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_bwd");
-  if (rc) return rc;
-  MVML_REQUIRE(ldgy >= mvml_gat_proj_cols(H, F, mode == 1) && ldgy % 4 == 0, "gat_agg_bwd: bad ldgy");
-  MVML_REQUIRE(attn != nullptr, "gat_agg_bwd: attention from the forward is required");
-  MVML_REQUIRE(mode != 0 || out != nullptr, "gat_agg_bwd: mode 0 needs the forward output");
-  if (num_nodes == 0) return MVML_OK;
-  if (!workspace || workspace_bytes == 0) {
-    set_error("gat_agg_bwd: workspace of mvml_gat_agg_bwd_workspace_size(E, H) bytes required");
-    return MVML_ERR_WORKSPACE;
-  }
-  hipStream_t st = as_stream(stream);
-  float* gpre = static_cast<float*>(workspace);
-  const int vpl = (int)ceil_div(H * F, 256);
-  switch (H) {
-    case 1: { MVML_VPL_CASES(launch_bwd, 1, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, st) break; }
-    case 2: { MVML_VPL_CASES(launch_bwd, 2, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, st) break; }
-    case 4: { MVML_VPL_CASES(launch_bwd, 4, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, st) break; }
-    case 8: { MVML_VPL_CASES(launch_bwd, 8, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, st) break; }
-  }
-  set_error("gat_agg_bwd: unsupported shape");
-  return MVML_ERR_INVALID;
-}
-
-// ---- projection weight folding (attention vectors folded into the fc GEMM) ----------------
-
-namespace mvml {
-namespace {
-
-// Wcat rows: [0,HF) fc.weight | [HF,HF+RW) res_fc.weight (RW = HF) or its head mean (RW = F) |
-//            [HF+RW, +H) A_l | [+H, +2H) A_r,   A_l[h,k] = sum_f attn_l[h,f] fc.weight[hF+f,k].
-__global__ void fold_weights_kernel(const float* __restrict__ fc_w, const float* __restrict__ res_w,
-                                    const float* __restrict__ attn_l, const float* __restrict__ attn_r,
-                                    int H, int F, int Fin, int ldw, int mean_res,
-                                    float* __restrict__ Wcat) {
-  const int HF = H * F;
-  const int RW = mean_res ? F : HF;
-  const int64_t total = (int64_t)(HF + RW + 2 * H) * ldw;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int row = (int)(e / ldw), k = (int)(e % ldw);
-    float v;
-    if (k >= Fin) {
-      v = 0.f;  // zero pad columns (aligned K for the LDS-DMA GEMM path)
-    } else if (row < HF) {
-      v = fc_w[(int64_t)row * Fin + k];
-    } else if (row < HF + RW) {
-      const int r = row - HF;
-      if (mean_res) {
-        float s = 0.f;
-        for (int h = 0; h < H; ++h) s += res_w[(int64_t)(h * F + r) * Fin + k];
-        v = s / (float)H;
-      } else {
-        v = res_w[(int64_t)r * Fin + k];
-      }
-    } else {
-      const int r = row - HF - RW;
-      const int h = r % H;
-      const float* at = (r < H) ? attn_l : attn_r;
-      float s = 0.f;
-      for (int f = 0; f < F; ++f) s = fmaf(at[h * F + f], fc_w[(int64_t)(h * F + f) * Fin + k], s);
-      v = s;
-    }
-    Wcat[e] = v;
-  }
-}
-
-// dL/dfc.weight[hF+f,k] = gWcat[hF+f,k] + attn_l[h,f]*gA_l[h,k] + attn_r[h,f]*gA_r[h,k]
-// dL/dres_fc.weight[hF+f,k] = gWcat[HF+hF+f,k]  or  gWcat[HF+f,k] / H  (head-mean residual)
-__global__ void unfold_w_kernel(const float* __restrict__ gW, const float* __restrict__ attn_l,
-                                const float* __restrict__ attn_r, int H, int F, int Fin, int ldg,
-                                int mean_res, float* __restrict__ g_fc, float* __restrict__ g_res) {
-  const int HF = H * F;
-  const int RW = mean_res ? F : HF;
-  const int64_t total = (int64_t)HF * Fin;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int row = (int)(e / Fin), k = (int)(e % Fin);
-    const int h = row / F;
-    const float gl = gW[(int64_t)(HF + RW + h) * ldg + k];
-    const float gr = gW[(int64_t)(HF + RW + H + h) * ldg + k];
-    g_fc[e] = gW[(int64_t)row * ldg + k] + attn_l[row] * gl + attn_r[row] * gr;
-    g_res[e] = mean_res ? gW[(int64_t)(HF + row % F) * ldg + k] / (float)H
-                        : gW[(int64_t)(HF + row) * ldg + k];
-  }
-}
-
-// dL/dattn_l[h,f] = sum_k gA_l[h,k] * fc.weight[hF+f,k]  (one wave per (side, h, f))
-__global__ void unfold_attn_kernel(const float* __restrict__ gW, const float* __restrict__ fc_w,
-                                   int H, int F, int Fin, int ldg, int mean_res, float* __restrict__ g_al,
-                                   float* __restrict__ g_ar) {
-  const int HF = H * F;
-  const int RW = mean_res ? F : HF;
-  const int lane = threadIdx.x & 63;
-  const int64_t item = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (item >= 2 * HF) return;
-  const int side = (int)(item / HF), row = (int)(item % HF);
-  const int h = row / F;
-  const float* ga = gW + (int64_t)(HF + RW + side * H + h) * ldg;
-  const float* w = fc_w + (int64_t)row * Fin;
-  float s = 0.f;
-  for (int k = lane; k < Fin; k += 64) s = fmaf(ga[k], w[k], s);
-  s = wave_sum(s);
-  if (lane == 0) (side ? g_ar : g_al)[row] = s;
-}
-
+// ------------------------------------------------------------------ parameter-side helpers
 // dL/dattn_l[h,f] = sum_n d el[n,h] * Z[n,h,f] (likewise attn_r with d er), summed directly over
-// atoms as DGL/autograd does.  (Chaining through the folded GEMM, sum_k gA_l[h,k] W[hF+f,k],
-// is algebraically equal but loses ~sqrt(Fin) in fp32 accuracy when Z cancels.)  Stage 1:
-// each thread owns one Z column over a chunk of atoms, 4 independent partial sums per side.
+// atoms as autograd does.  Stage 1: each thread owns one Z column over a chunk of atoms.
 __global__ void attn_grad_partial_kernel(int64_t N, int H, int F, const float* __restrict__ Y,
-                                         int64_t ldy, const float* __restrict__ gY, int64_t ldgy,
-                                         int ea, int64_t rows_per, float* __restrict__ part) {
+                                         int64_t ldy, const float* __restrict__ gelr,
+                                         int64_t rows_per, float* __restrict__ part) {
   const int HF = H * F;
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   if (col >= HF) return;
@@ -724,14 +613,14 @@ __global__ void attn_grad_partial_kernel(int64_t N, int H, int F, const float* _
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float z = Y[(r + j) * ldy + col];
-      const float* g = gY + (r + j) * ldgy + ea;
+      const float* g = gelr + (r + j) * 2 * H;
       sl[j] = fmaf(g[h], z, sl[j]);
       sr[j] = fmaf(g[H + h], z, sr[j]);
     }
   }
   for (; r < r1; ++r) {
     const float z = Y[r * ldy + col];
-    const float* g = gY + r * ldgy + ea;
+    const float* g = gelr + r * 2 * H;
     sl[0] = fmaf(g[h], z, sl[0]);
     sr[0] = fmaf(g[H + h], z, sr[0]);
   }
@@ -756,21 +645,128 @@ int attn_grad_splits(int64_t N, int HF) {
   return (int)std::max<int64_t>(1, s);
 }
 
+// Wcat rows: [0,HF) fc.weight | [HF,HF+RW) res_fc.weight (RW = HF) or its head mean (RW = F);
+// columns Fin..ldw-1 are zero.
+__global__ void fold_weights_kernel(const float* __restrict__ fc_w, const float* __restrict__ res_w,
+                                    int H, int F, int Fin, int ldw, int mean_res,
+                                    float* __restrict__ Wcat) {
+  const int HF = H * F;
+  const int RW = mean_res ? F : HF;
+  const int64_t total = (int64_t)(HF + RW) * ldw;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(e / ldw), k = (int)(e % ldw);
+    float v;
+    if (k >= Fin) {
+      v = 0.f;
+    } else if (row < HF) {
+      v = fc_w[(int64_t)row * Fin + k];
+    } else {
+      const int r = row - HF;
+      if (mean_res) {
+        float s = 0.f;
+        for (int h = 0; h < H; ++h) s += res_w[(int64_t)(h * F + r) * Fin + k];
+        v = s / (float)H;
+      } else {
+        v = res_w[(int64_t)r * Fin + k];
+      }
+    }
+    Wcat[e] = v;
+  }
+}
+
+// dL/dfc.weight = gWcat[0:HF];  dL/dres_fc.weight[hF+f] = gWcat[HF+hF+f] or gWcat[HF+f] / H.
+__global__ void unfold_w_kernel(const float* __restrict__ gW, int H, int F, int Fin, int ldg,
+                                int mean_res, float* __restrict__ g_fc, float* __restrict__ g_res) {
+  const int HF = H * F;
+  const int64_t total = (int64_t)HF * Fin;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(e / Fin), k = (int)(e % Fin);
+    g_fc[e] = gW[(int64_t)row * ldg + k];
+    g_res[e] = mean_res ? gW[(int64_t)(HF + row % F) * ldg + k] / (float)H
+                        : gW[(int64_t)(HF + row) * ldg + k];
+  }
+}
+
 }  // namespace
 }  // namespace mvml
+
+using namespace mvml;
+
+extern "C" int mvml_gat_proj_cols(int H, int F, int mean_residual) {
+  return H * F + (mean_residual ? F : H * F);
+}
+
+extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
+                                const float* Y, int64_t ldy, int H, int F, const float* attn_l,
+                                const float* attn_r, const float* bias, float slope, int mode,
+                                float* out, float* attn, float* elr, void* stream) {
+  clear_error();
+  int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_fwd");
+  if (rc) return rc;
+  MVML_REQUIRE(((uintptr_t)out & 15) == 0 && ((uintptr_t)bias & 15) == 0 &&
+               ((uintptr_t)attn_l & 15) == 0 && ((uintptr_t)attn_r & 15) == 0,
+               "gat_agg_fwd: out / bias / attention vectors must be 16-byte aligned");
+  MVML_REQUIRE(attn != nullptr && elr != nullptr, "gat_agg_fwd: attn and elr outputs are required");
+  if (num_nodes == 0) return MVML_OK;
+  hipStream_t st = as_stream(stream);
+  const int vpl = (int)ceil_div(H * F, 256);
+  switch (H) {
+    case 1: { MVML_VPL_CASES(launch_fwd, 1, num_nodes, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
+    case 2: { MVML_VPL_CASES(launch_fwd, 2, num_nodes, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
+    case 4: { MVML_VPL_CASES(launch_fwd, 4, num_nodes, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
+    case 8: { MVML_VPL_CASES(launch_fwd, 8, num_nodes, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
+  }
+  set_error("gat_agg_fwd: unsupported shape");
+  return MVML_ERR_INVALID;
+}
+
+extern "C" size_t mvml_gat_agg_bwd_workspace_size(int64_t num_edges, int H) {
+  return carve_size((size_t)num_edges * H * sizeof(float));
+}
+
+extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
+                                const int32_t* out_rowptr, const int32_t* out_dst,
+                                const int32_t* out_inslot, const float* Y, int64_t ldy,
+                                const float* elr, const float* attn, const float* attn_l,
+                                const float* attn_r, const float* out, const float* g_out, int H,
+                                int F, float slope, int mode, float* gY, int64_t ldgy, float* gelr,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_bwd");
+  if (rc) return rc;
+  MVML_REQUIRE(ldgy >= mvml_gat_proj_cols(H, F, mode == 1) && ldgy % 4 == 0, "gat_agg_bwd: bad ldgy");
+  MVML_REQUIRE(attn != nullptr && elr != nullptr && gelr != nullptr,
+               "gat_agg_bwd: attn / elr from the forward and the gelr output are required");
+  MVML_REQUIRE(mode != 0 || out != nullptr, "gat_agg_bwd: mode 0 needs the forward output");
+  if (num_nodes == 0) return MVML_OK;
+  if (!workspace || workspace_bytes == 0) {
+    set_error("gat_agg_bwd: workspace of mvml_gat_agg_bwd_workspace_size(E, H) bytes required");
+    return MVML_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  float* gpre = static_cast<float*>(workspace);
+  const int vpl = (int)ceil_div(H * F, 256);
+  switch (H) {
+    case 1: { MVML_VPL_CASES(launch_bwd, 1, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, attn_l, attn_r, out, g_out, F, slope, mode, gpre, gY, ldgy, gelr, st) break; }
+    case 2: { MVML_VPL_CASES(launch_bwd, 2, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, attn_l, attn_r, out, g_out, F, slope, mode, gpre, gY, ldgy, gelr, st) break; }
+    case 4: { MVML_VPL_CASES(launch_bwd, 4, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, attn_l, attn_r, out, g_out, F, slope, mode, gpre, gY, ldgy, gelr, st) break; }
+    case 8: { MVML_VPL_CASES(launch_bwd, 8, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, attn_l, attn_r, out, g_out, F, slope, mode, gpre, gY, ldgy, gelr, st) break; }
+  }
+  set_error("gat_agg_bwd: unsupported shape");
+  return MVML_ERR_INVALID;
+}
 
 extern "C" size_t mvml_gat_attn_grad_workspace_size(int64_t num_nodes, int H, int F) {
   return carve_size((size_t)attn_grad_splits(num_nodes, H * F) * 2 * H * F * sizeof(float));
 }
 
-extern "C" int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, int mean_residual, const float* Y,
-                                  int64_t ldy, const float* gY, int64_t ldgy, float* g_attn_l,
-                                  float* g_attn_r, void* workspace, size_t workspace_bytes,
-                                  void* stream) {
+extern "C" int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, const float* Y, int64_t ldy,
+                                  const float* gelr, float* g_attn_l, float* g_attn_r,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
-  MVML_REQUIRE(H > 0 && F > 0 && num_nodes >= 0, "gat_attn_grad: bad shape");
-  const int C = mvml_gat_proj_cols(H, F, mean_residual);
-  MVML_REQUIRE(ldy >= C && ldgy >= C, "gat_attn_grad: bad leading dimension");
+  MVML_REQUIRE(H > 0 && F > 0 && num_nodes >= 0 && ldy >= (int64_t)H * F, "gat_attn_grad: bad shape");
   if (!workspace || workspace_bytes < mvml_gat_attn_grad_workspace_size(num_nodes, H, F)) {
     set_error("gat_attn_grad: workspace too small");
     return MVML_ERR_WORKSPACE;
@@ -779,42 +775,32 @@ extern "C" int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, int mean_resi
   const int HF = H * F;
   const int S = attn_grad_splits(num_nodes, HF);
   const int64_t rows_per = ceil_div(num_nodes > 0 ? num_nodes : 1, S);
-  const int ea = C - 2 * H;
   float* part = static_cast<float*>(workspace);
   dim3 g1((unsigned)ceil_div(HF, 256), (unsigned)S);
-  attn_grad_partial_kernel<<<g1, 256, 0, st>>>(num_nodes, H, F, Y, ldy, gY, ldgy, ea, rows_per, part);
+  attn_grad_partial_kernel<<<g1, 256, 0, st>>>(num_nodes, H, F, Y, ldy, gelr, rows_per, part);
   attn_grad_final_kernel<<<(unsigned)ceil_div(2 * HF, 256), 256, 0, st>>>(HF, S, part, g_attn_l, g_attn_r);
   return check_launch("attn_grad");
 }
 
-extern "C" int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_l,
-                                     const float* attn_r, int H, int F, int Fin, int ldw,
-                                     int mean_residual, float* Wcat, void* stream) {
+extern "C" int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, int H, int F, int Fin,
+                                     int ldw, int mean_residual, float* Wcat, void* stream) {
   clear_error();
   MVML_REQUIRE(H > 0 && F > 0 && Fin > 0 && ldw >= Fin, "gat_fold_weights: bad shape");
   hipStream_t st = as_stream(stream);
   const int64_t total = (int64_t)mvml_gat_proj_cols(H, F, mean_residual) * ldw;
   const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
-  fold_weights_kernel<<<blocks, 256, 0, st>>>(fc_w, res_fc_w, attn_l, attn_r, H, F, Fin, ldw,
-                                              mean_residual, Wcat);
+  fold_weights_kernel<<<blocks, 256, 0, st>>>(fc_w, res_fc_w, H, F, Fin, ldw, mean_residual, Wcat);
   return check_launch("fold_weights_kernel");
 }
 
-extern "C" int mvml_gat_unfold_grads(const float* gWcat, const float* fc_w, const float* attn_l,
-                                     const float* attn_r, int H, int F, int Fin, int ldg,
+extern "C" int mvml_gat_unfold_grads(const float* gWcat, int H, int F, int Fin, int ldg,
                                      int mean_residual, float* g_fc_w, float* g_res_fc_w,
-                                     float* g_attn_l, float* g_attn_r, void* stream) {
+                                     void* stream) {
   clear_error();
   MVML_REQUIRE(H > 0 && F > 0 && Fin > 0 && ldg >= Fin, "gat_unfold_grads: bad shape");
   hipStream_t st = as_stream(stream);
   const int64_t total = (int64_t)H * F * Fin;
   const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
-  unfold_w_kernel<<<blocks, 256, 0, st>>>(gWcat, attn_l, attn_r, H, F, Fin, ldg, mean_residual,
-                                          g_fc_w, g_res_fc_w);
-  int rc = check_launch("unfold_w_kernel");
-  if (rc || !g_attn_l || !g_attn_r) return rc;  // attention grads: mvml_gat_attn_grad (exact path)
-  const int64_t items = 2 * (int64_t)H * F;
-  unfold_attn_kernel<<<(unsigned)ceil_div(items, 4), 256, 0, st>>>(gWcat, fc_w, H, F, Fin, ldg,
-                                                                   mean_residual, g_attn_l, g_attn_r);
-  return check_launch("unfold_attn_kernel");
+  unfold_w_kernel<<<blocks, 256, 0, st>>>(gWcat, H, F, Fin, ldg, mean_residual, g_fc_w, g_res_fc_w);
+  return check_launch("unfold_w_kernel");
 }

@@ -7,6 +7,9 @@
 //   y = weight*o/std + bias
 // One thread per (group, column): column reads of a 768-wide row are coalesced across the
 // workgroup.  Parameter gradients are reduced over groups in fixed order (no atomics).
+// Statistics and per-element arithmetic run in fp64 (inputs/outputs fp32): GraphNorm over a
+// small group is ill-conditioned (x - mean cancels), the layer is tiny ((B, 768) per step, no
+// measurable cost), and fp64 keeps its own rounding out of the gradients it sends upstream.
 #include "common.h"
 
 namespace mvml {
@@ -20,21 +23,21 @@ __global__ void graphnorm_fwd_kernel(int D, const int64_t* __restrict__ off, con
   const int64_t g = blockIdx.x;
   const int64_t r0 = off[g], r1 = off[g + 1];
   if (r1 <= r0) return;
-  const float n = (float)(r1 - r0);
-  float s = 0.f;
+  const double n = (double)(r1 - r0);
+  double s = 0.0;
   for (int64_t r = r0; r < r1; ++r) s += x[r * D + col];
-  const float mean = s / n;
-  const float msc = ms[col];
-  float v = 0.f;
+  const double mean = s / n;
+  const double msc = ms[col];
+  double v = 0.0;
   for (int64_t r = r0; r < r1; ++r) {
-    const float o = x[r * D + col] - mean * msc;
+    const double o = x[r * D + col] - mean * msc;
     v += o * o;
   }
-  const float stdv = sqrtf(v / n + eps);
-  const float wc = w[col], bc = b[col];
+  const double k = (double)w[col] / sqrt(v / n + (double)eps);
+  const double bc = b[col];
   for (int64_t r = r0; r < r1; ++r) {
-    const float o = x[r * D + col] - mean * msc;
-    y[r * D + col] = wc * o / stdv + bc;
+    const double o = x[r * D + col] - mean * msc;
+    y[r * D + col] = (float)(k * o + bc);
   }
 }
 
@@ -42,37 +45,37 @@ __global__ void graphnorm_fwd_kernel(int D, const int64_t* __restrict__ off, con
 __global__ void graphnorm_bwd_kernel(int D, const int64_t* __restrict__ off, const float* __restrict__ x,
                                      const float* __restrict__ w, const float* __restrict__ ms, float eps,
                                      const float* __restrict__ gy, float* __restrict__ gx,
-                                     float* __restrict__ part /* [3][G][D] */, int64_t G) {
+                                     double* __restrict__ part /* [3][G][D] */, int64_t G) {
   const int col = blockIdx.y * blockDim.x + threadIdx.x;
   if (col >= D) return;
   const int64_t g = blockIdx.x;
   const int64_t r0 = off[g], r1 = off[g + 1];
-  float pw = 0.f, pb = 0.f, pms = 0.f;
+  double pw = 0.0, pb = 0.0, pms = 0.0;
   if (r1 > r0) {
-    const float n = (float)(r1 - r0);
-    float s = 0.f;
+    const double n = (double)(r1 - r0);
+    double s = 0.0;
     for (int64_t r = r0; r < r1; ++r) s += x[r * D + col];
-    const float mean = s / n;
-    const float msc = ms[col], wc = w[col];
-    float v = 0.f, so = 0.f, sgy = 0.f, sgyo = 0.f;
+    const double mean = s / n;
+    const double msc = ms[col], wc = w[col];
+    double v = 0.0, so = 0.0, sgy = 0.0, sgyo = 0.0;
     for (int64_t r = r0; r < r1; ++r) {
-      const float o = x[r * D + col] - mean * msc;
-      const float gyr = gy[r * D + col];
+      const double o = x[r * D + col] - mean * msc;
+      const double gyr = gy[r * D + col];
       v += o * o;
       so += o;
       sgy += gyr;
       sgyo += gyr * o;
     }
-    const float stdv = sqrtf(v / n + eps);
-    const float inv = 1.f / stdv;
+    const double var = v / n + (double)eps;
+    const double inv = 1.0 / sqrt(var);
     // g_o_j = w/std * (g_y_j - S1 * o_j / (n std^2)),  S1 = sum g_y o
-    const float k1 = wc * inv;
-    const float k2 = sgyo / (n * stdv * stdv);
-    const float sum_go = k1 * (sgy - k2 * so);
+    const double k1 = wc * inv;
+    const double k2 = sgyo / (n * var);
+    const double sum_go = k1 * (sgy - k2 * so);
     for (int64_t r = r0; r < r1; ++r) {
-      const float o = x[r * D + col] - mean * msc;
-      const float go = k1 * (gy[r * D + col] - k2 * o);
-      gx[r * D + col] = go - msc * sum_go / n;
+      const double o = x[r * D + col] - mean * msc;
+      const double go = k1 * (gy[r * D + col] - k2 * o);
+      gx[r * D + col] = (float)(go - msc * sum_go / n);
     }
     pw = sgyo * inv;
     pb = sgy;
@@ -83,16 +86,16 @@ __global__ void graphnorm_bwd_kernel(int D, const int64_t* __restrict__ off, con
   part[(2 * G + g) * D + col] = pms;
 }
 
-__global__ void graphnorm_param_reduce(int D, int64_t G, const float* __restrict__ part,
+__global__ void graphnorm_param_reduce(int D, int64_t G, const double* __restrict__ part,
                                        float* __restrict__ gw, float* __restrict__ gb,
                                        float* __restrict__ gms) {
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   const int which = blockIdx.y;
   if (col >= D) return;
-  float s = 0.f;
+  double s = 0.0;
   for (int64_t g = 0; g < G; ++g) s += part[((int64_t)which * G + g) * D + col];
   float* dst = which == 0 ? gw : (which == 1 ? gb : gms);
-  if (dst) dst[col] = s;
+  if (dst) dst[col] = (float)s;
 }
 
 __global__ void relu_bwd_kernel(int64_t n, const float* __restrict__ y, const float* __restrict__ gy,
@@ -120,7 +123,7 @@ extern "C" int mvml_graphnorm_fwd(int64_t G, int D, const int64_t* group_offsets
 }
 
 extern "C" size_t mvml_graphnorm_bwd_workspace_size(int64_t G, int D) {
-  return carve_size((size_t)3 * G * D * sizeof(float));
+  return carve_size((size_t)3 * G * D * sizeof(double));
 }
 
 extern "C" int mvml_graphnorm_bwd(int64_t G, int D, const int64_t* group_offsets, const float* x,
@@ -136,7 +139,7 @@ extern "C" int mvml_graphnorm_bwd(int64_t G, int D, const int64_t* group_offsets
     return MVML_ERR_WORKSPACE;
   }
   hipStream_t st = as_stream(stream);
-  float* part = static_cast<float*>(workspace);
+  double* part = static_cast<double*>(workspace);
   dim3 grid((unsigned)G, (unsigned)ceil_div(D, 256));
   graphnorm_bwd_kernel<<<grid, 256, 0, st>>>(D, group_offsets, x, weight, mean_scale, eps, g_y, g_x,
                                              part, G);

@@ -29,20 +29,25 @@ def _stream(dev):
     return _lib.stream_ptr(dev)
 
 
+# Diagnostics hook (tools/diag_golden.py): when a dict, GATLayerFunction.backward stores its
+# saved el/er, attention and el/er gradients into it.  None in normal use.
+DEBUG_CAPTURE = None
+
+
 def _round4(x):
     return (x + 3) // 4 * 4
 
 
 def agg_fwd_bytes(N, E, H, F, out_cols, res_cols):
     """Algorithmic HBM bytes of one mvml_gat_agg_fwd: read Z and R once,
-    el/er, rowptr, src ids; write the layer output and the saved attention.  R is the
+    rowptr, src ids; write the layer output, the saved attention and el/er.  R is the
     head-mean residual (F columns) in mean mode."""
     return 4 * (N * H * F + N * res_cols + 2 * N * H + (N + 1) + E + N * out_cols + E * H)
 
 
 def agg_bwd_bytes(N, E, H, F, gout_cols, mode):
     """Algorithmic bytes of mvml_gat_agg_bwd: read Z, el/er, g_out (+ out for ELU'), saved
-    attention, both CSRs; write gY = [dZ | dR | d el | d er]; the [E,H] g_pre round trip
+    attention, both CSRs; write gY = [dZ | dR] and [d el | d er]; the [E,H] g_pre round trip
     between its two passes is counted once each way."""
     rw = F if mode == MODE_MEAN else H * F
     reads = N * H * F + 2 * N * H + N * gout_cols + (N * H * F if mode == 0 else 0) + E * H
@@ -72,8 +77,9 @@ def colsum(X, M, N, ldx, out, beta=0.0, offset=0, alpha=1.0):
 
 
 class GATLayerFunction(torch.autograd.Function):
-    """dgllife GATLayer(GATConv) forward/backward: projection GEMM (fc, res_fc, el, er folded
-    into one MFMA GEMM) + fused attention/softmax/aggregation/residual/bias/agg kernel."""
+    """dgllife GATLayer(GATConv) forward/backward (model.py:79-81): projection GEMM (fc and
+    res_fc as one MFMA GEMM) + fused el/er, edge-softmax, aggregation, residual, bias and
+    flatten/ELU or head-mean kernel."""
 
     @staticmethod
     def forward(ctx, X, fc_w, res_w, attn_l, attn_r, bias, g, H, F, slope, mode):
@@ -92,25 +98,27 @@ class GATLayerFunction(torch.autograd.Function):
         Fp = _round4(Fin)
         Xp = X if Fp == Fin else torch.nn.functional.pad(X, (0, Fp - Fin))
         Wcat = torch.empty((C, Fp), dtype=torch.float32, device=dev)
-        call("mvml_gat_fold_weights", ptr(_c(fc_w)), ptr(_c(res_w)), ptr(_c(attn_l)), ptr(_c(attn_r)),
-             H, F, Fin, Fp, mean_res, ptr(Wcat), st)
+        call("mvml_gat_fold_weights", ptr(_c(fc_w)), ptr(_c(res_w)), H, F, Fin, Fp, mean_res,
+             ptr(Wcat), st)
         Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
         gemm(Xp, Wcat, N, C, Fp, 0, 0, Fp, Fp, Y, ldy)
         out_cols = F if mode == MODE_MEAN else HF
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()
         attn = torch.empty((E, H), dtype=torch.float32, device=dev)
-        _lib.call_tag[0] = {"layer": f"H{H}xF{F}", "bytes": agg_fwd_bytes(N, E, H, F, out_cols, C - HF - 2 * H)}
-        call("mvml_gat_agg_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F, ptr(_c(bias)),
-             float(slope), int(mode), ptr(out), ptr(attn), st)
-        ctx.save_for_backward(Xp, Wcat, Y, attn, out, fc_w, attn_l, attn_r)
+        elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
+        attn_l, attn_r = _c(attn_l), _c(attn_r)
+        _lib.call_tag[0] = {"layer": f"H{H}xF{F}", "bytes": agg_fwd_bytes(N, E, H, F, out_cols, C - HF)}
+        call("mvml_gat_agg_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F, ptr(attn_l),
+             ptr(attn_r), ptr(_c(bias)), float(slope), int(mode), ptr(out), ptr(attn), ptr(elr), st)
+        ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r)
         ctx.Fin = Fin
         ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode, ctx.ldy = g, H, F, slope, mode, ldy
         return out
 
     @staticmethod
     def backward(ctx, g_out):
-        Xp, Wcat, Y, attn, out, fc_w, attn_l, attn_r = ctx.saved_tensors
+        Xp, Wcat, Y, attn, elr, out, attn_l, attn_r = ctx.saved_tensors
         g, H, F, mode, ldy = ctx.g, ctx.H, ctx.F, ctx.mode, ctx.ldy
         g_out = _c(g_out)
         N, Fp = Xp.shape
@@ -119,29 +127,31 @@ class GATLayerFunction(torch.autograd.Function):
         HF = H * F
         mean_res = int(mode == MODE_MEAN)
         C = _lib.lib().mvml_gat_proj_cols(H, F, mean_res)
-        RW = C - HF - 2 * H
+        RW = C - HF
         st = _stream(dev)
         L = _lib.lib()
         gY = torch.empty((N, ldy), dtype=torch.float32, device=dev)
+        gelr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_agg_bwd_workspace_size(g.num_edges(), H), dev)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}",
                             "bytes": agg_bwd_bytes(N, g.num_edges(), H, F, g_out.shape[1], mode)}
         call("mvml_gat_agg_bwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr),
-             ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(attn), ptr(out), ptr(g_out), H, F,
-             float(ctx.slope), int(mode), ptr(gY), ldy, wp, wn, st)
+             ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr), ptr(attn), ptr(attn_l),
+             ptr(attn_r), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldy,
+             ptr(gelr), wp, wn, st)
         # dL/dWcat = gY^T X  (split-K over atoms)
         gW = torch.empty((C, Fp), dtype=torch.float32, device=dev)
         assert RW in (F, HF)
         gemm(gY, Xp, C, Fp, N, 1, 1, ldy, Fp, gW, Fp)
-        g_fc = torch.empty_like(fc_w)
-        g_res = torch.empty_like(fc_w)
+        g_fc = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
+        g_res = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_al = torch.empty_like(attn_l)
         g_ar = torch.empty_like(attn_r)
-        call("mvml_gat_unfold_grads", ptr(gW), ptr(_c(fc_w)), ptr(_c(attn_l)), ptr(_c(attn_r)), H, F, Fin,
-             Fp, mean_res, ptr(g_fc), ptr(g_res), None, None, st)
+        call("mvml_gat_unfold_grads", ptr(gW), H, F, Fin, Fp, mean_res, ptr(g_fc), ptr(g_res), st)
         wp2, wn2 = _lib.ws_ptr_size(L.mvml_gat_attn_grad_workspace_size(N, H, F), dev)
-        call("mvml_gat_attn_grad", N, H, F, mean_res, ptr(Y), ldy, ptr(gY), ldy, ptr(g_al), ptr(g_ar),
-             wp2, wn2, st)
+        call("mvml_gat_attn_grad", N, H, F, ptr(Y), ldy, ptr(gelr), ptr(g_al), ptr(g_ar), wp2, wn2, st)
+        if DEBUG_CAPTURE is not None:
+            DEBUG_CAPTURE.update(elr=elr, gelr=gelr, attn=attn)
         g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
         if mean_res:  # every head's bias sees g_out / H: one column sum, replicated over heads
             colsum(gY, N, F, ldy, g_bias, offset=HF, alpha=1.0 / H)

@@ -29,6 +29,13 @@ MOLS = [  # (num_atoms, bonds) — small hand-made molecules incl. a ring, a bra
 ]
 
 
+# (file, GraphNorm group size).  gnn_small: ONE group over the whole 5-molecule batch, exactly
+# model.py:93 (GraphNorm with batch=None normalises over the mini-batch).  gnn_small_groups:
+# groups of 3 + 2 molecules, the multi-group batching of mvml_gat; a 2-molecule group makes
+# GraphNorm ill-conditioned (x - mean cancels), so fp32 errors are amplified ~10x there.
+FIXTURES = (("gnn_small.npz", 5), ("gnn_small_groups.npz", 3))
+
+
 def build(group_size=3, seed=7):
     n = [m[0] for m in MOLS]
     edges = [bigraph_edges(a, b) for a, b in MOLS]
@@ -67,7 +74,8 @@ def build(group_size=3, seed=7):
 
 
 if __name__ == "__main__":
-    d = build()
-    path = os.path.join(HERE, "gnn_small.npz")
-    np.savez_compressed(path, **d)
-    print(f"wrote {path} ({os.path.getsize(path)} bytes, {len(d)} arrays)")
+    for name, gs in FIXTURES:
+        d = build(group_size=gs)
+        path = os.path.join(HERE, name)
+        np.savez_compressed(path, **d)
+        print(f"wrote {path} ({os.path.getsize(path)} bytes, {len(d)} arrays)")

@@ -42,21 +42,26 @@ def main():
         ldy = (C + 3) // 4 * 4
         Y = torch.randn((N, ldy), device="cuda") * 0.3
         bias = torch.randn(H * F, device="cuda") * 0.1
+        al = torch.randn(H * F, device="cuda") * 0.1
+        ar = torch.randn(H * F, device="cuda") * 0.1
+        elr = torch.empty((N, 2 * H), device="cuda")
+        gelr = torch.empty((N, 2 * H), device="cuda")
         oc = F if mode == 1 else H * F
         out = torch.empty((N, oc), device="cuda")
         attn = torch.empty((E, H), device="cuda")
         f = lambda: call("mvml_gat_agg_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F,
-                         ptr(bias), 0.2, mode, ptr(out), ptr(attn), st)
+                         ptr(al), ptr(ar), ptr(bias), 0.2, mode, ptr(out), ptr(attn), ptr(elr), st)
         ms = timeit(f)
-        by = agg_fwd_bytes(N, E, H, F, oc, C - H * F - 2 * H)
+        by = agg_fwd_bytes(N, E, H, F, oc, C - H * F)
         print(f"  agg_fwd {name:16s} {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
         g_out = torch.randn_like(out)
         gY = torch.empty((N, ldy), device="cuda")
         wsz = L.mvml_gat_agg_bwd_workspace_size(E, H)
         ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
         b = lambda: call("mvml_gat_agg_bwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr),
-                         ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(attn), ptr(out), ptr(g_out),
-                         H, F, 0.2, mode, ptr(gY), ldy, ptr(ws), wsz, st)
+                         ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr), ptr(attn), ptr(al),
+                         ptr(ar), ptr(out), ptr(g_out), H, F, 0.2, mode, ptr(gY), ldy, ptr(gelr),
+                         ptr(ws), wsz, st)
         ms = timeit(b)
         by = agg_bwd_bytes(N, E, H, F, oc, mode)
         print(f"  agg_bwd {name:16s} {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
