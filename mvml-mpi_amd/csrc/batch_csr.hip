@@ -101,7 +101,7 @@ __global__ void scan_tile_apply(const int64_t* __restrict__ in, int64_t n,
 
 int exclusive_scan_i64(const int64_t* in, int64_t n, int64_t* out, int64_t* tmp, hipStream_t st) {
   if (n == 0) {
-    hipMemsetAsync(out, 0, sizeof(int64_t), st);
+    (void)hipMemsetAsync(out, 0, sizeof(int64_t), st);
     return check_launch("scan(empty)");
   }
   int64_t nt = ceil_div(n, kScanTile);
@@ -269,14 +269,14 @@ extern "C" int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local
   int64_t* tmp = cv.take<int64_t>((size_t)ceil_div(num_graphs > 0 ? num_graphs : 1, kScanTile));
   int32_t* inslot = cv.take<int32_t>((size_t)num_edges);
   int* big = cv.take<int>((size_t)2 * num_nodes);
-  hipMemsetAsync(status_flags, 0, 2 * sizeof(int32_t), st);
+  (void)hipMemsetAsync(status_flags, 0, 2 * sizeof(int32_t), st);
   int rc = exclusive_scan_i64(batch_num_nodes, num_graphs, node_offsets, tmp, st);
   if (rc) return rc;
   rc = exclusive_scan_i64(batch_num_edges, num_graphs, edge_offsets, tmp, st);
   if (rc) return rc;
   if (num_nodes == 0) {
-    hipMemsetAsync(in_rowptr, 0, sizeof(int32_t), st);
-    hipMemsetAsync(out_rowptr, 0, sizeof(int32_t), st);
+    (void)hipMemsetAsync(in_rowptr, 0, sizeof(int32_t), st);
+    (void)hipMemsetAsync(out_rowptr, 0, sizeof(int32_t), st);
     return check_launch("build_csr(empty)");
   }
   if (num_graphs > 0) {

@@ -35,6 +35,9 @@ namespace mvml {
 namespace {
 
 constexpr int kWavesPerBlock = 4;
+#ifndef MVML_FWD_UNR
+#define MVML_FWD_UNR 2  // neighbour rows in flight per gather step (forward)
+#endif
 
 __device__ __forceinline__ float rl(float x, int j) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j));
@@ -169,186 +172,190 @@ gat_logits_kernel(int64_t N, const float* __restrict__ Y, int64_t ldy, int F,
   store_heads<H>(elr + v * 2 * H + H, er, lane);
 }
 
-// Aggregation.  CS waves share one destination atom, each owning HW = H / CS heads (HF / CS
-// columns): the wide 768 -> 4x384 layer runs with CS = 2 so every wave keeps only 3 float4
-// column slices per gathered row (half the VGPRs -> twice the waves in flight to hide the
-// dependent logit-gather -> softmax -> Z-gather chain).  Block = 4 waves = 4 / CS atoms.
-// Lanes take the in-edges (64 per chunk) for the softmax (max -> exp -> sum -> divide, as
-// dgl's edge_softmax), then the wave walks the edges two at a time, every lane accumulating 4
-// consecutive columns per 256-column slice of the gathered Z rows.
-template <int H, int VPL, int CS>
+// Aggregation.  A wave owns a GROUP of 64 consecutive destination atoms (CS waves share a
+// group, each owning F / CS columns of EVERY head, so a wave never needs another wave's data).
+//  1. Prologue, lane i <-> atom v0 + i: the softmax statistics of the atom's in-edges (max,
+//     then sum of exp, exactly dgl's edge_softmax) from the gathered logits, the first DC
+//     logits cached in registers; the attention a_e is written (part-0 wave).  The dependent
+//     rowptr -> in_src -> elr chains of 64 atoms are in flight together.
+//  2. Edge stream: the group's in-edges are contiguous in the in-CSR, so the wave walks them
+//     UNR at a time regardless of atom boundaries (source ids from a 64-edge register chunk via
+//     readlane, no per-atom index round trip): UNR neighbour rows Z[u] (16-B column slices per
+//     lane) and their logits are loaded together, a_e is recomputed bit-identically from the
+//     atom's statistics, and an atom is finished (residual prefetched when it starts) as soon
+//     as the stream passes its last edge.
+//  3. Epilogue per atom: + residual + bias, then flatten+ELU / flatten, or the head mean
+//     through a wave-private LDS transpose.
+template <int H, int VPL, int CS, int UNR>
 __global__ void __launch_bounds__(kWavesPerBlock * 64)
 gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
                    const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ elr,
                    const float* __restrict__ bias, float slope, int mode, float* __restrict__ out,
                    float* __restrict__ attn) {
-  constexpr int HW = H / CS;
+  constexpr int DC = 4;  // logits cached per atom in the prologue
   __shared__ __attribute__((aligned(16))) float red[kWavesPerBlock][VPL * 256];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int part = wid % CS;
-  const int64_t v = xcd_block(blockIdx.x, gridDim.x) * (kWavesPerBlock / CS) + wid / CS;
-  const bool live = v < N;  // (CS > 1: every wave must reach the block barrier)
-  if (CS == 1 && !live) return;
-  const int HF = H * F;
-  const int HFW = HF / CS;    // columns of this wave
-  const int c0 = part * HFW;  // first column (global) of this wave
-  const int h0 = part * HW;   // first head of this wave
-  const int beg = live ? rowptr[v] : 0, end = live ? rowptr[v + 1] : 0;
-  const int deg = end - beg;
-  const float* yv = Y + (live ? v : 0) * ldy;
-  float er[HW];
-#pragma unroll
-  for (int h = 0; h < HW; ++h) er[h] = live ? elr[v * 2 * H + H + h0 + h] : 0.f;
+  const int64_t wave = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
+  const int part = (int)(wave % CS);
+  const int64_t v0 = (wave / CS) * 64;
+  if (v0 >= N) return;
+  const int HF = H * F, FW = F / CS, HFW = HF / CS;
 
-  // ---- softmax statistics over the in-edges ----
-  float mx[HW], sm[HW], s_l[HW];
-  int u_l = 0;
+  // ---- 1. prologue: softmax statistics, lane per atom ----
+  const int64_t vl = v0 + lane;
+  const bool lv = vl < N;
+  int beg_l = 0, end_l = 0;
+  if (lv) { beg_l = rowptr[vl]; end_l = rowptr[vl + 1]; }
+  float er_l[H], m_l[H], s_l[H], sc[DC][H];
 #pragma unroll
-  for (int h = 0; h < HW; ++h) { mx[h] = -INFINITY; sm[h] = 0.f; s_l[h] = -INFINITY; }
-  for (int base = 0; base < deg; base += 64) {
-    const bool valid = base + lane < deg;
-    if (valid) {
-      u_l = in_src[beg + base + lane];
-      const float* eu = elr + (int64_t)u_l * 2 * H + h0;
-#pragma unroll
-      for (int h = 0; h < HW; ++h) s_l[h] = leaky(eu[h] + er[h], slope);
-    } else {
-#pragma unroll
-      for (int h = 0; h < HW; ++h) s_l[h] = -INFINITY;
-    }
-    float cm[HW];
-#pragma unroll
-    for (int h = 0; h < HW; ++h) cm[h] = s_l[h];
-    HeadReduce<HW>::template all<true>(cm, lane);
-#pragma unroll
-    for (int h = 0; h < HW; ++h) mx[h] = fmaxf(mx[h], cm[h]);
+  for (int h = 0; h < H; ++h) {
+    er_l[h] = lv ? elr[vl * 2 * H + H + h] : 0.f;
+    m_l[h] = -INFINITY;
+    s_l[h] = 0.f;
   }
-  const bool one_chunk = deg <= 64;
-  if (one_chunk) {
 #pragma unroll
-    for (int h = 0; h < HW; ++h) sm[h] = lane < deg ? expf(s_l[h] - mx[h]) : 0.f;
-    HeadReduce<HW>::template all<false>(sm, lane);
-  } else {
-    for (int base = 0; base < deg; base += 64) {
-      const bool valid = base + lane < deg;
-      float ex[HW];
-      if (valid) {
-        const int u = in_src[beg + base + lane];
-        const float* eu = elr + (int64_t)u * 2 * H + h0;
+  for (int t = 0; t < DC; ++t) {
+    const int j = beg_l + t;
+    const float* eu = elr + (int64_t)(j < end_l ? in_src[j] : 0) * 2 * H;
 #pragma unroll
-        for (int h = 0; h < HW; ++h) ex[h] = expf(leaky(eu[h] + er[h], slope) - mx[h]);
-      } else {
+    for (int h = 0; h < H; ++h) {
+      sc[t][h] = leaky(eu[h] + er_l[h], slope);
+      if (j < end_l) m_l[h] = fmaxf(m_l[h], sc[t][h]);
+    }
+  }
+  for (int j = beg_l + DC; j < end_l; ++j) {
+    const float* eu = elr + (int64_t)in_src[j] * 2 * H;
 #pragma unroll
-        for (int h = 0; h < HW; ++h) ex[h] = 0.f;
+    for (int h = 0; h < H; ++h) m_l[h] = fmaxf(m_l[h], leaky(eu[h] + er_l[h], slope));
+  }
+#pragma unroll
+  for (int t = 0; t < DC; ++t)
+    if (beg_l + t < end_l) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) s_l[h] += expf(sc[t][h] - m_l[h]);
+    }
+  for (int j = beg_l + DC; j < end_l; ++j) {
+    const float* eu = elr + (int64_t)in_src[j] * 2 * H;
+#pragma unroll
+    for (int h = 0; h < H; ++h) s_l[h] += expf(leaky(eu[h] + er_l[h], slope) - m_l[h]);
+  }
+  if (part == 0) {
+#pragma unroll
+    for (int t = 0; t < DC; ++t)
+      if (beg_l + t < end_l) {
+#pragma unroll
+        for (int h = 0; h < H; ++h)
+          attn[(int64_t)(beg_l + t) * H + h] = expf(sc[t][h] - m_l[h]) / s_l[h];
       }
-      HeadReduce<HW>::template all<false>(ex, lane);
+    for (int j = beg_l + DC; j < end_l; ++j) {
+      const float* eu = elr + (int64_t)in_src[j] * 2 * H;
 #pragma unroll
-      for (int h = 0; h < HW; ++h) sm[h] += ex[h];
+      for (int h = 0; h < H; ++h)
+        attn[(int64_t)j * H + h] = expf(leaky(eu[h] + er_l[h], slope) - m_l[h]) / s_l[h];
     }
   }
 
-  // ---- aggregation over this wave's columns ----
-  int hc[VPL];
+  // ---- column map of this lane: wave column j -> (head, f) -> global column ----
+  int hc[VPL], gcol[VPL];
   bool okc[VPL];
-  float4 acc[VPL];
+  float4 bc[VPL];
 #pragma unroll
   for (int c = 0; c < VPL; ++c) {
-    const int lc = 4 * (lane + 64 * c);  // column within this wave's range
-    okc[c] = lc < HFW;
-    hc[c] = okc[c] ? (c0 + lc) / F - h0 : 0;
-    acc[c] = f4(0.f);
+    const int j = 4 * (lane + 64 * c);
+    okc[c] = j < HFW;
+    hc[c] = okc[c] ? j / FW : 0;
+    gcol[c] = okc[c] ? hc[c] * F + part * FW + j % FW : 0;
+    bc[c] = okc[c] ? ld4(bias + gcol[c]) : f4(0.f);
   }
-  for (int base = 0; base < deg; base += 64) {
-    const int cnt = min(64, deg - base);
-    float a_l[HW];
-    if (!one_chunk) {
-      if (base + lane < deg) {
-        u_l = in_src[beg + base + lane];
-        const float* eu = elr + (int64_t)u_l * 2 * H + h0;
+
+  // ---- 2./3. edge stream + per-atom epilogue ----
+  const int nv = (int)min<int64_t>(64, N - v0);
+  int k = 0, kend = 0;
+  float M[H], S[H], ER[H];
+  float4 r[VPL], acc[VPL];
+  auto start_atom = [&](int kk) {
+    kend = rl(end_l, kk);
 #pragma unroll
-        for (int h = 0; h < HW; ++h) s_l[h] = leaky(eu[h] + er[h], slope);
-      }
+    for (int h = 0; h < H; ++h) { M[h] = rl(m_l[h], kk); S[h] = rl(s_l[h], kk); ER[h] = rl(er_l[h], kk); }
+    if (mode != 1) {
+      const float* rv = Y + (v0 + kk) * ldy + HF;
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) r[c] = okc[c] ? ld4(rv + gcol[c]) : f4(0.f);
     }
 #pragma unroll
-    for (int h = 0; h < HW; ++h) a_l[h] = (base + lane < deg) ? expf(s_l[h] - mx[h]) / sm[h] : 0.f;
-    if (base + lane < deg) {
-      float* ap = attn + (int64_t)(beg + base + lane) * H + h0;
+    for (int c = 0; c < VPL; ++c) acc[c] = f4(0.f);
+  };
+  auto finish_atom = [&](int kk) {
+    const int64_t v = v0 + kk;
+    if (mode == 1) {
+      // head mean: rst + bias of every head -> LDS, then sum heads h = 0..H-1 per column
+      float* rr = red[wid];
 #pragma unroll
-      for (int h = 0; h < HW; ++h) ap[h] = a_l[h];
-    }
-    int j = 0;
-    for (; j + 1 < cnt; j += 2) {
-      const int u0 = rl(u_l, j), u1 = rl(u_l, j + 1);
-      float a0[HW], a1[HW];
+      for (int c = 0; c < VPL; ++c)
+        if (okc[c]) st4(rr + 4 * (lane + 64 * c), add4(acc[c], bc[c]));
+      wave_lds_sync();
+      const float invh = (float)H;
+      const float* rm_row = Y + v * ldy + HF + part * FW;  // head-mean residual
+      for (int f = 4 * lane; f < FW; f += 256) {
+        float4 s = ld4(rr + f);
 #pragma unroll
-      for (int h = 0; h < HW; ++h) { a0[h] = rl(a_l[h], j); a1[h] = rl(a_l[h], j + 1); }
-      const float* z0 = Y + (int64_t)u0 * ldy + c0;
-      const float* z1 = Y + (int64_t)u1 * ldy + c0;
-      float4 zv0[VPL], zv1[VPL];
-#pragma unroll
-      for (int c = 0; c < VPL; ++c) {
-        const int lc = 4 * (lane + 64 * c);
-        if (okc[c]) { zv0[c] = ld4(z0 + lc); zv1[c] = ld4(z1 + lc); }
+        for (int h = 1; h < H; ++h) s = add4(s, ld4(rr + h * FW + f));
+        const float4 rm = ld4(rm_row + f);
+        st4(out + v * F + part * FW + f, make_float4(s.x / invh + rm.x, s.y / invh + rm.y,
+                                                     s.z / invh + rm.z, s.w / invh + rm.w));
       }
+      wave_lds_sync();
+    } else {
 #pragma unroll
       for (int c = 0; c < VPL; ++c)
         if (okc[c]) {
-          acc[c] = fma4(pick<HW>(a0, hc[c]), zv0[c], acc[c]);
-          acc[c] = fma4(pick<HW>(a1, hc[c]), zv1[c], acc[c]);
+          float4 o = add4(add4(acc[c], r[c]), bc[c]);
+          if (mode == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
+          st4(out + v * HF + gcol[c], o);
         }
     }
-    if (j < cnt) {
-      const int u0 = rl(u_l, j);
-      float a0[HW];
+  };
+
+  start_atom(0);
+  const int E0 = rl(beg_l, 0), E1 = rl(end_l, nv - 1);
+  for (int cb = E0; cb < E1; cb += 64) {
+    const int cnt = min(64, E1 - cb);
+    const int u_c = (lane < cnt) ? in_src[cb + lane] : 0;
+    for (int i = 0; i < cnt; i += UNR) {
+      float4 z[UNR][VPL];
+      float el[UNR][H];
 #pragma unroll
-      for (int h = 0; h < HW; ++h) a0[h] = rl(a_l[h], j);
-      const float* z0 = Y + (int64_t)u0 * ldy + c0;
+      for (int t = 0; t < UNR; ++t) {
+        const int u = rl(u_c, min(i + t, cnt - 1));
+        const float* zu = Y + (int64_t)u * ldy;
 #pragma unroll
-      for (int c = 0; c < VPL; ++c)
-        if (okc[c]) acc[c] = fma4(pick<HW>(a0, hc[c]), ld4(z0 + 4 * (lane + 64 * c)), acc[c]);
+        for (int c = 0; c < VPL; ++c) z[t][c] = okc[c] ? ld4(zu + gcol[c]) : f4(0.f);
+        const float* eu = elr + (int64_t)u * 2 * H;
+#pragma unroll
+        for (int h = 0; h < H; ++h) el[t][h] = eu[h];
+      }
+#pragma unroll
+      for (int t = 0; t < UNR; ++t) {
+        if (i + t < cnt) {
+          while (cb + i + t >= kend) {  // the stream passed atom k's last edge
+            finish_atom(k);
+            start_atom(++k);
+          }
+          float a[H];
+#pragma unroll
+          for (int h = 0; h < H; ++h) a[h] = expf(leaky(el[t][h] + ER[h], slope) - M[h]) / S[h];
+#pragma unroll
+          for (int c = 0; c < VPL; ++c)
+            if (okc[c]) acc[c] = fma4(pick<H>(a, hc[c]), z[t][c], acc[c]);
+        }
+      }
     }
   }
-
-  // ---- epilogue: + residual + bias, then the GATLayer aggregation ----
-  if (mode == 1) {
-    // rst + bias of this wave's heads -> LDS; the part-0 wave of the atom sums the heads in
-    // order h = 0..H-1, divides by H and adds the head-mean residual.
-    float* r = red[wid];
-#pragma unroll
-    for (int c = 0; c < VPL; ++c)
-      if (okc[c]) {
-        const int lc = 4 * (lane + 64 * c);
-        st4(r + lc, add4(acc[c], ld4(bias + c0 + lc)));
-      }
-    if (CS > 1) __syncthreads();
-    else wave_lds_sync();
-    if (live && part == 0) {
-      const float invh = (float)H;
-#pragma unroll
-      for (int c = 0; c < VPL; ++c) {
-        const int f = 4 * (lane + 64 * c);
-        if (f < F) {
-          float4 sacc = ld4(red[wid] + f);
-#pragma unroll
-          for (int h = 1; h < H; ++h) {
-            const int p = h / HW, hl = h % HW;
-            sacc = add4(sacc, ld4(red[wid + p] + hl * F + f));
-          }
-          const float4 rm = ld4(yv + HF + f);  // head-mean residual
-          st4(out + v * F + f, make_float4(sacc.x / invh + rm.x, sacc.y / invh + rm.y,
-                                           sacc.z / invh + rm.z, sacc.w / invh + rm.w));
-        }
-      }
-    }
-  } else if (live) {
-#pragma unroll
-    for (int c = 0; c < VPL; ++c)
-      if (okc[c]) {
-        const int col = c0 + 4 * (lane + 64 * c);
-        float4 o = add4(add4(acc[c], ld4(yv + HF + col)), ld4(bias + col));
-        if (mode == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
-        st4(out + v * HF + col, o);
-      }
+  // the last atom with edges and any trailing atoms without
+  for (;;) {
+    finish_atom(k);
+    if (++k >= nv) break;
+    start_atom(k);
   }
 }
 
@@ -541,15 +548,19 @@ int launch_fwd(int64_t N, const int32_t* rp, const int32_t* src, const float* Y,
       N, Y, ldy, F, al, ar, elr);
   int rc = check_launch("gat_logits_kernel");
   if (rc) return rc;
-  // Wide layers (more than 4 float4 slices per lane) split the columns over 2 waves.
-  if constexpr (VPL > 4 && H % 2 == 0) {
+  // Wide layers (more than 4 float4 slices per lane) split every head's columns over 2 waves.
+  if constexpr (VPL > 4) {
     constexpr int CS = 2, V2 = (VPL + 1) / 2;
-    const unsigned blocks = (unsigned)ceil_div(N, kWavesPerBlock / CS);
-    gat_agg_fwd_kernel<H, V2, CS><<<blocks, kWavesPerBlock * 64, 0, st>>>(
+    if (F % 8 != 0) {
+      set_error("gat_agg_fwd: H*F > 1024 needs out_feats divisible by 8");
+      return MVML_ERR_INVALID;
+    }
+    const unsigned blocks = (unsigned)ceil_div(ceil_div(N, 64) * CS, kWavesPerBlock);
+    gat_agg_fwd_kernel<H, V2, CS, (V2 <= 3 ? MVML_FWD_UNR : 2)><<<blocks, kWavesPerBlock * 64, 0, st>>>(
         N, rp, src, Y, ldy, F, elr, bias, slope, mode, out, attn);
   } else {
-    const unsigned blocks = (unsigned)ceil_div(N, kWavesPerBlock);
-    gat_agg_fwd_kernel<H, VPL, 1><<<blocks, kWavesPerBlock * 64, 0, st>>>(
+    const unsigned blocks = (unsigned)ceil_div(ceil_div(N, 64), kWavesPerBlock);
+    gat_agg_fwd_kernel<H, VPL, 1, (VPL <= 3 ? MVML_FWD_UNR : 2)><<<blocks, kWavesPerBlock * 64, 0, st>>>(
         N, rp, src, Y, ldy, F, elr, bias, slope, mode, out, attn);
   }
   return check_launch("gat_agg_fwd_kernel");
