@@ -62,6 +62,16 @@ int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local,
                    int32_t* status_flags /* [2] */, void* workspace, size_t workspace_bytes,
                    void* stream);
 
+/* Node groups (no reference counterpart: the launch geometry of the aggregation kernels).
+ * Group g = the contiguous range of WHOLE molecules [group_start[g], group_start[g+1]) that
+ * begins with the molecule containing atom 64*g; G = mvml_node_group_count(N) groups, some
+ * possibly empty.  Every in-edge of a group's atoms starts inside the group, so one workgroup
+ * can stage a group's projection rows in LDS and read each of them from HBM once.
+ * node_offsets: int64[B+1] from mvml_build_csr; group_start: int32[G+1]. */
+int64_t mvml_node_group_count(int64_t num_nodes);
+int mvml_build_node_groups(int64_t num_graphs, int64_t num_nodes, const int64_t* node_offsets,
+                           int32_t* group_start, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Dense fp32 GEMM on CDNA4 MFMA (v_mfma_f32_32x32x2_f32, exact f32 fmaf chains).
  * C[M,N] = act(A[M,K] * B[K,N] + bias[N] + beta * C)
@@ -111,7 +121,7 @@ int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, const float* Y, int64_t 
                        size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
- * Fused GAT attention + aggregation, forward (one wavefront per destination atom; replaces
+ * Fused GAT attention + aggregation, forward (one workgroup per node group; replaces
  * dgl GATConv.forward from `el = ...` to the residual/bias, plus dgllife GATLayer's
  * flatten/ELU or head-mean, model.py:77-81):
  *   el/er = <Z, attn_l/attn_r> -> apply_edges(u_add_v) -> LeakyReLU(slope) -> edge_softmax
@@ -122,9 +132,10 @@ int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, const float* Y, int64_t 
  * (mode 1).  attn [E, H] receives the edge_softmax output in in-CSR slot order and elr [N, 2H]
  * the logit halves [el | er]; both are required by the backward.
  * ------------------------------------------------------------------------------------- */
-int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
-                     const float* Y, int64_t ldy, int H, int F, const float* attn_l,
-                     const float* attn_r, const float* bias, float slope, int mode, float* out,
+int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
+                     const int32_t* in_rowptr, const int32_t* in_src, const float* Y, int64_t ldy,
+                     int H, int F, const float* attn_l, const float* attn_r, const float* bias,
+                     float slope, int mode, float* out,
                      float* attn, float* elr, void* stream);
 /* Backward of mvml_gat_agg_fwd (DGL GSpMM / GSDDMM / EdgeSoftmax backward + torch autograd of
  * el/er, residual, bias, ELU, mean).  Atomic-free: the u_mul_e-sum transpose is a gather over

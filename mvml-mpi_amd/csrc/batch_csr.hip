@@ -234,6 +234,26 @@ build_csr_kernel(const int32_t* __restrict__ src_local, const int32_t* __restric
                      out_inslot, inslot_ws, n);
 }
 
+// Node groups: group g starts at the first atom of the molecule that contains atom
+// g * kNodeGroupAtoms (binary search of node_offsets), so every group is a range of whole
+// molecules (possibly empty when a molecule spans several multiples).  group_start[G] = N.
+__global__ void node_groups_kernel(int64_t B, int64_t N, const int64_t* __restrict__ node_offsets,
+                                   int64_t G, int32_t* __restrict__ group_start) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g > G) return;
+  const int64_t a = g * kNodeGroupAtoms;
+  if (g == G || a >= N) {
+    group_start[g] = (int32_t)N;
+    return;
+  }
+  int64_t lo = 0, hi = B;  // last m with node_offsets[m] <= a
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) / 2;
+    if (node_offsets[mid] <= a) lo = mid; else hi = mid;
+  }
+  group_start[g] = (int32_t)node_offsets[lo];
+}
+
 }  // namespace
 }  // namespace mvml
 
@@ -286,4 +306,22 @@ extern "C" int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local
         out_dst, out_inslot, status_flags, inslot, big);
   }
   return check_launch("build_csr_kernel");
+}
+
+extern "C" int64_t mvml_node_group_count(int64_t num_nodes) {
+  return num_nodes > 0 ? ceil_div(num_nodes, kNodeGroupAtoms) : 0;
+}
+
+extern "C" int mvml_build_node_groups(int64_t num_graphs, int64_t num_nodes,
+                                      const int64_t* node_offsets, int32_t* group_start,
+                                      void* stream) {
+  clear_error();
+  MVML_REQUIRE(num_graphs >= 0 && num_nodes >= 0 && num_nodes < (int64_t(1) << 31),
+               "build_node_groups: bad sizes");
+  const int64_t G = mvml_node_group_count(num_nodes);
+  if (G == 0) return MVML_OK;
+  MVML_REQUIRE(num_graphs > 0 && node_offsets && group_start, "build_node_groups: null input");
+  node_groups_kernel<<<(unsigned)ceil_div(G + 1, 256), 256, 0, as_stream(stream)>>>(
+      num_graphs, num_nodes, node_offsets, G, group_start);
+  return check_launch("node_groups_kernel");
 }

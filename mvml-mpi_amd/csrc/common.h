@@ -15,6 +15,8 @@ void set_error(const char* fmt, ...);
 void clear_error();
 
 constexpr int kWave = 64;
+// Target size of a node group (mvml_build_node_groups): whole molecules, ~this many atoms.
+constexpr int kNodeGroupAtoms = 64;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -51,6 +53,20 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Raw buffer addressing: a wave-uniform base in a 128-bit SGPR resource + a 32-bit per-lane
+// byte offset (one VGPR per address instead of a 64-bit pointer pair).  Out-of-range offsets
+// (>= bytes) read 0 and drop stores.  Resource word 3 = 0x00020000 for gfx9 (32-bit data).
+typedef unsigned int mvml_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+__device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(mvml_u32x4, v), r, byte_off, 0, 0);
+}
 
 // XCD-aware workgroup remap (bijective for any grid size).  The dispatcher deals workgroups
 // round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch); this returns a logical

@@ -172,190 +172,321 @@ gat_logits_kernel(int64_t N, const float* __restrict__ Y, int64_t ldy, int F,
   store_heads<H>(elr + v * 2 * H + H, er, lane);
 }
 
-// Aggregation.  A wave owns a GROUP of 64 consecutive destination atoms (CS waves share a
-// group, each owning F / CS columns of EVERY head, so a wave never needs another wave's data).
-//  1. Prologue, lane i <-> atom v0 + i: the softmax statistics of the atom's in-edges (max,
-//     then sum of exp, exactly dgl's edge_softmax) from the gathered logits, the first DC
-//     logits cached in registers; the attention a_e is written (part-0 wave).  The dependent
-//     rowptr -> in_src -> elr chains of 64 atoms are in flight together.
-//  2. Edge stream: the group's in-edges are contiguous in the in-CSR, so the wave walks them
-//     UNR at a time regardless of atom boundaries (source ids from a 64-edge register chunk via
-//     readlane, no per-atom index round trip): UNR neighbour rows Z[u] (16-B column slices per
-//     lane) and their logits are loaded together, a_e is recomputed bit-identically from the
-//     atom's statistics, and an atom is finished (residual prefetched when it starts) as soon
-//     as the stream passes its last edge.
-//  3. Epilogue per atom: + residual + bias, then flatten+ELU / flatten, or the head mean
-//     through a wave-private LDS transpose.
-template <int H, int VPL, int CS, int UNR>
-__global__ void __launch_bounds__(kWavesPerBlock * 64)
-gat_agg_fwd_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
-                   const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ elr,
-                   const float* __restrict__ bias, float slope, int mode, float* __restrict__ out,
-                   float* __restrict__ attn) {
-  constexpr int DC = 4;  // logits cached per atom in the prologue
-  __shared__ __attribute__((aligned(16))) float red[kWavesPerBlock][VPL * 256];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t wave = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
-  const int part = (int)(wave % CS);
-  const int64_t v0 = (wave / CS) * 64;
-  if (v0 >= N) return;
-  const int HF = H * F, FW = F / CS, HFW = HF / CS;
-
-  // ---- 1. prologue: softmax statistics, lane per atom ----
-  const int64_t vl = v0 + lane;
-  const bool lv = vl < N;
-  int beg_l = 0, end_l = 0;
-  if (lv) { beg_l = rowptr[vl]; end_l = rowptr[vl + 1]; }
-  float er_l[H], m_l[H], s_l[H], sc[DC][H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-    er_l[h] = lv ? elr[vl * 2 * H + H + h] : 0.f;
-    m_l[h] = -INFINITY;
-    s_l[h] = 0.f;
-  }
+// edge_softmax (dgl 0.9.1, norm_by='dst'): one thread per (destination, head) pair:
+//   s_e = LeakyReLU(el[src_e] + er[v]),  a_e = exp(s_e - max_v s) / sum_v exp(s - max_v s)
+// written to attn[E, H] in in-CSR slot order (the aggregation's and the backward's input).
+template <int H>
+__global__ void __launch_bounds__(256)
+gat_softmax_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
+                   const float* __restrict__ elr, float slope, float* __restrict__ attn) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * H) return;
+  const int64_t v = i / H;
+  const int h = (int)(i % H);
+  const float er = elr[v * 2 * H + H + h];
+  const int eb = rowptr[v], ee = rowptr[v + 1];
+  constexpr int DC = 6;  // logits of the first DC in-edges stay in registers
+  float sc[DC];
+  float m = -INFINITY, sum = 0.f;
 #pragma unroll
   for (int t = 0; t < DC; ++t) {
-    const int j = beg_l + t;
-    const float* eu = elr + (int64_t)(j < end_l ? in_src[j] : 0) * 2 * H;
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      sc[t][h] = leaky(eu[h] + er_l[h], slope);
-      if (j < end_l) m_l[h] = fmaxf(m_l[h], sc[t][h]);
-    }
+    sc[t] = (eb + t < ee) ? leaky(elr[(int64_t)in_src[eb + t] * 2 * H + h] + er, slope) : -INFINITY;
+    m = fmaxf(m, sc[t]);
   }
-  for (int j = beg_l + DC; j < end_l; ++j) {
-    const float* eu = elr + (int64_t)in_src[j] * 2 * H;
-#pragma unroll
-    for (int h = 0; h < H; ++h) m_l[h] = fmaxf(m_l[h], leaky(eu[h] + er_l[h], slope));
-  }
+  for (int e = eb + DC; e < ee; ++e) m = fmaxf(m, leaky(elr[(int64_t)in_src[e] * 2 * H + h] + er, slope));
 #pragma unroll
   for (int t = 0; t < DC; ++t)
-    if (beg_l + t < end_l) {
+    if (eb + t < ee) sum += expf(sc[t] - m);
+  for (int e = eb + DC; e < ee; ++e) sum += expf(leaky(elr[(int64_t)in_src[e] * 2 * H + h] + er, slope) - m);
 #pragma unroll
-      for (int h = 0; h < H; ++h) s_l[h] += expf(sc[t][h] - m_l[h]);
-    }
-  for (int j = beg_l + DC; j < end_l; ++j) {
-    const float* eu = elr + (int64_t)in_src[j] * 2 * H;
-#pragma unroll
-    for (int h = 0; h < H; ++h) s_l[h] += expf(leaky(eu[h] + er_l[h], slope) - m_l[h]);
-  }
-  if (part == 0) {
-#pragma unroll
-    for (int t = 0; t < DC; ++t)
-      if (beg_l + t < end_l) {
-#pragma unroll
-        for (int h = 0; h < H; ++h)
-          attn[(int64_t)(beg_l + t) * H + h] = expf(sc[t][h] - m_l[h]) / s_l[h];
-      }
-    for (int j = beg_l + DC; j < end_l; ++j) {
-      const float* eu = elr + (int64_t)in_src[j] * 2 * H;
-#pragma unroll
-      for (int h = 0; h < H; ++h)
-        attn[(int64_t)j * H + h] = expf(leaky(eu[h] + er_l[h], slope) - m_l[h]) / s_l[h];
-    }
-  }
+  for (int t = 0; t < DC; ++t)
+    if (eb + t < ee) attn[(int64_t)(eb + t) * H + h] = expf(sc[t] - m) / sum;
+  for (int e = eb + DC; e < ee; ++e)
+    attn[(int64_t)e * H + h] = expf(leaky(elr[(int64_t)in_src[e] * 2 * H + h] + er, slope) - m) / sum;
+}
 
-  // ---- column map of this lane: wave column j -> (head, f) -> global column ----
-  int hc[VPL], gcol[VPL];
-  bool okc[VPL];
-  float4 bc[VPL];
-#pragma unroll
-  for (int c = 0; c < VPL; ++c) {
-    const int j = 4 * (lane + 64 * c);
-    okc[c] = j < HFW;
-    hc[c] = okc[c] ? j / FW : 0;
-    gcol[c] = okc[c] ? hc[c] * F + part * FW + j % FW : 0;
-    bc[c] = okc[c] ? ld4(bias + gcol[c]) : f4(0.f);
-  }
+// Aggregation over NODE GROUPS.  A node group is a contiguous range of whole molecules of about
+// kNodeGroupAtoms atoms (mvml_build_node_groups); edges never leave a molecule, so every in-edge
+// of a group's atoms has its source inside the group, and one workgroup per group can read each
+// projection row from HBM once.  The attention comes from gat_softmax_kernel.  The projection
+// columns are swept CW at a time; CW/4 lanes own one destination atom (16-B column slices).
+// Flatten modes walk the chunks head-major; the mean mode walks them f-chunk-major, head-minor,
+// summing the heads in registers (+ bias per head, / H, + head-mean residual).
+//
+// Two kernels share the groups (each block decides with the same block-wide predicate):
+//  * gat_agg_fwd_lds_kernel — the molecule case: a group of <= kWinL atoms, <= kECap in-edges,
+//    in-degree <= kEC everywhere (organic atoms: 4 bonds + self-loop).  The group's rows are
+//    streamed ONCE into an LDS double buffer through a register ring two chunks deep (chunks
+//    k+1, k+2 and the next residual in flight while chunk k is aggregated, one barrier per
+//    chunk); the kEC source-row LDS offsets of every destination are cached in registers, so a
+//    chunk's gathers are kEC x NP independent ds_read_b128 (branch-free: a missing edge reads
+//    the destination's own row and is discarded by a select) — one LDS round trip per chunk.
+//  * gat_agg_fwd_gather_kernel — everything else (large molecules, hubs): no staging; the
+//    gathers go straight to global memory, where the chunk-synchronous sweep keeps the group's
+//    chunk rows in the XCD's L2.  Correct for any graph.
+constexpr int kWinL = 128;    // LDS kernel: atoms per group
+constexpr int kECap = 512;    // LDS kernel: in-edges per group (attention staged in LDS)
+constexpr int kWin = 64;      // gather kernel: destination atoms per pass set
+constexpr int kEC = 5;        // in-edges per destination with cached offsets
+constexpr int kAggThreads = 512;
 
-  // ---- 2./3. edge stream + per-atom epilogue ----
-  const int nv = (int)min<int64_t>(64, N - v0);
-  int k = 0, kend = 0;
-  float M[H], S[H], ER[H];
-  float4 r[VPL], acc[VPL];
-  auto start_atom = [&](int kk) {
-    kend = rl(end_l, kk);
+// Block-wide: does group [a0, a1) take the LDS kernel?  (All threads must call it.)
+__device__ __forceinline__ bool lds_group(int a0, int a1, const int32_t* __restrict__ rowptr) {
+  if (a1 - a0 > kWinL || rowptr[a1] - rowptr[a0] > kECap) return false;  // block-uniform
+  bool hub = false;
+  for (int v = a0 + (int)threadIdx.x; v < a1; v += kAggThreads) hub |= rowptr[v + 1] - rowptr[v] > kEC;
+  return !__syncthreads_or(hub);
+}
+
+template <int H, int CW, int MODE>
+__global__ void __launch_bounds__(kAggThreads, 4)  // 2 workgroups (16 waves) per CU
+gat_agg_fwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __restrict__ rowptr,
+                       const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
+                       int F, const float* __restrict__ bias, const float* __restrict__ attn,
+                       float* __restrict__ out) {
+  constexpr int LPD = CW / 4;                        // lanes per destination atom
+  constexpr int DPP = kAggThreads / LPD;             // destinations per pass
+  constexpr int NP = (kWinL + DPP - 1) / DPP;        // passes
+  __shared__ float4 zbuf[2][kWinL * LPD];
+  __shared__ float s_att[(kECap + 1) * H];  // + H zeros: the attention of a missing edge
+  const int tid = threadIdx.x;
+  const int ds = tid / LPD, q = tid % LPD;
+  const int HF = H * F;
+  const int a0 = groups[blockIdx.x], a1 = groups[blockIdx.x + 1];
+  if (a1 <= a0 || !lds_group(a0, a1, rowptr)) return;
+  const int nr = a1 - a0;
+  const int nfc = F / CW;     // column chunks per head
+  const int nch = H * nfc;
+  const int ocols = MODE == 1 ? F : HF;
+  const int e0 = rowptr[a0];
+  const int ne = rowptr[a1] - e0;
+  for (int i = tid; i < ne * H; i += kAggThreads) s_att[i] = attn[(int64_t)e0 * H + i];
+  if (tid < H) s_att[kECap * H + tid] = 0.f;
+  const uint32_t rowb = (uint32_t)ldy * 4u;
+  const __amdgpu_buffer_rsrc_t rY = make_rsrc(Y + (int64_t)a0 * ldy, (uint32_t)nr * rowb);
+  const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)a0 * ocols, (uint32_t)(nr * ocols) * 4u);
+  // this thread's destinations: the LDS slots of their first kEC source rows and attention
+  // values; a missing edge (i >= in-degree) points at the destination's own row and at a zero
+  // attention, so the edge loop is branch- and mask-free (fma(0, z, acc) == acc)
+  int so[NP][kEC], ao[NP][kEC];
 #pragma unroll
-    for (int h = 0; h < H; ++h) { M[h] = rl(m_l[h], kk); S[h] = rl(s_l[h], kk); ER[h] = rl(er_l[h], kk); }
-    if (mode != 1) {
-      const float* rv = Y + (v0 + kk) * ldy + HF;
-#pragma unroll
-      for (int c = 0; c < VPL; ++c) r[c] = okc[c] ? ld4(rv + gcol[c]) : f4(0.f);
+  for (int p = 0; p < NP; ++p) {
+    const int d = ds + DPP * p;
+    int eb = 0, deg = 0;
+    if (d < nr) {
+      eb = rowptr[a0 + d] - e0;
+      deg = rowptr[a0 + d + 1] - e0 - eb;
     }
 #pragma unroll
-    for (int c = 0; c < VPL; ++c) acc[c] = f4(0.f);
+    for (int i = 0; i < kEC; ++i) {
+      so[p][i] = ((i < deg) ? in_src[e0 + eb + i] - a0 : (d < nr ? d : 0)) * LPD + q;
+      ao[p][i] = ((i < deg) ? eb + i : kECap) * H;
+    }
+  }
+  // chunk k -> global column of this lane
+  auto col_of = [&](int k) {
+    return (MODE == 1 ? (k % H) * F + (k / H) * CW : (k / nfc) * F + (k % nfc) * CW) + 4 * q;
   };
-  auto finish_atom = [&](int kk) {
-    const int64_t v = v0 + kk;
-    if (mode == 1) {
-      // head mean: rst + bias of every head -> LDS, then sum heads h = 0..H-1 per column
-      float* rr = red[wid];
+  float4 zA[NP], zB[NP], rres[NP], rnx[NP], tot[NP];
+  auto load_rows = [&](int k, float4 (&dst)[NP]) {
+    if (k >= nch) return;
+    const uint32_t cb = 4u * (uint32_t)col_of(k);
 #pragma unroll
-      for (int c = 0; c < VPL; ++c)
-        if (okc[c]) st4(rr + 4 * (lane + 64 * c), add4(acc[c], bc[c]));
-      wave_lds_sync();
-      const float invh = (float)H;
-      const float* rm_row = Y + v * ldy + HF + part * FW;  // head-mean residual
-      for (int f = 4 * lane; f < FW; f += 256) {
-        float4 s = ld4(rr + f);
-#pragma unroll
-        for (int h = 1; h < H; ++h) s = add4(s, ld4(rr + h * FW + f));
-        const float4 rm = ld4(rm_row + f);
-        st4(out + v * F + part * FW + f, make_float4(s.x / invh + rm.x, s.y / invh + rm.y,
-                                                     s.z / invh + rm.z, s.w / invh + rm.w));
-      }
-      wave_lds_sync();
-    } else {
-#pragma unroll
-      for (int c = 0; c < VPL; ++c)
-        if (okc[c]) {
-          float4 o = add4(add4(acc[c], r[c]), bc[c]);
-          if (mode == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
-          st4(out + v * HF + gcol[c], o);
-        }
+    for (int j = 0; j < NP; ++j) {
+      const int r = ds + DPP * j;
+      if (r < nr) dst[j] = buf_ld4(rY, (uint32_t)r * rowb + cb);
     }
   };
-
-  start_atom(0);
-  const int E0 = rl(beg_l, 0), E1 = rl(end_l, nv - 1);
-  for (int cb = E0; cb < E1; cb += 64) {
-    const int cnt = min(64, E1 - cb);
-    const int u_c = (lane < cnt) ? in_src[cb + lane] : 0;
-    for (int i = 0; i < cnt; i += UNR) {
-      float4 z[UNR][VPL];
-      float el[UNR][H];
+  auto load_res = [&](int k, float4 (&dst)[NP]) {
+    const uint32_t cb = 4u * (uint32_t)(HF + (MODE == 1 ? (k / H) * CW + 4 * q : col_of(k)));
 #pragma unroll
-      for (int t = 0; t < UNR; ++t) {
-        const int u = rl(u_c, min(i + t, cnt - 1));
-        const float* zu = Y + (int64_t)u * ldy;
+    for (int j = 0; j < NP; ++j) {
+      const int r = ds + DPP * j;
+      if (r < nr) dst[j] = buf_ld4(rY, (uint32_t)r * rowb + cb);
+    }
+  };
+  auto store_rows = [&](int buf, const float4 (&src)[NP]) {
 #pragma unroll
-        for (int c = 0; c < VPL; ++c) z[t][c] = okc[c] ? ld4(zu + gcol[c]) : f4(0.f);
-        const float* eu = elr + (int64_t)u * 2 * H;
+    for (int j = 0; j < NP; ++j) {
+      const int r = ds + DPP * j;
+      if (r < nr) zbuf[buf][r * LPD + q] = src[j];
+    }
+  };
+  // one chunk: aggregate k from zbuf[k & 1] while k+1 (in `nxt`) and k+2 (the other register
+  // slot) are in flight; then stage k+1 and refill its slot with k+3
+  auto step = [&](int k, float4 (&nxt)[NP]) {
+    const int h = MODE == 1 ? k % H : k / nfc;
+    const int col = col_of(k);
+    if (MODE != 1) { if (k + 1 < nch) load_res(k + 1, rnx); }
+    else if (h == 0) load_res(k, rres);  // consumed at head H-1, three chunks later
+    const float4 b4 = ld4(bias + col);
+    const float4* zl = zbuf[k & 1];
+    float4 acc[NP];
 #pragma unroll
-        for (int h = 0; h < H; ++h) el[t][h] = eu[h];
-      }
+    for (int p = 0; p < NP; ++p) acc[p] = f4(0.f);
+#ifndef MVML_AGG_NOEDGE
 #pragma unroll
-      for (int t = 0; t < UNR; ++t) {
-        if (i + t < cnt) {
-          while (cb + i + t >= kend) {  // the stream passed atom k's last edge
-            finish_atom(k);
-            start_atom(++k);
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int i = 0; i < kEC; ++i) acc[p] = fma4(s_att[ao[p][i] + h], zl[so[p][i]], acc[p]);
+#endif
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int d = ds + DPP * p;
+      if (d < nr) {
+        if (MODE == 1) {
+          const float4 t = add4(acc[p], b4);
+          tot[p] = (h == 0) ? t : add4(tot[p], t);
+          if (h == H - 1) {
+            const float invh = (float)H;
+            buf_st4(rO, 4u * (uint32_t)(d * F + (k / H) * CW + 4 * q),
+                    make_float4(tot[p].x / invh + rres[p].x, tot[p].y / invh + rres[p].y,
+                                tot[p].z / invh + rres[p].z, tot[p].w / invh + rres[p].w));
           }
-          float a[H];
-#pragma unroll
-          for (int h = 0; h < H; ++h) a[h] = expf(leaky(el[t][h] + ER[h], slope) - M[h]) / S[h];
-#pragma unroll
-          for (int c = 0; c < VPL; ++c)
-            if (okc[c]) acc[c] = fma4(pick<H>(a, hc[c]), z[t][c], acc[c]);
+        } else {
+          float4 o = add4(add4(acc[p], rres[p]), b4);
+          if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
+          buf_st4(rO, 4u * (uint32_t)(d * HF + col), o);
         }
       }
     }
+    if (k + 1 < nch) {
+      store_rows((k + 1) & 1, nxt);
+      load_rows(k + 3, nxt);
+    }
+    if (MODE != 1) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) rres[j] = rnx[j];
+    }
+    __syncthreads();
+  };
+  load_rows(0, zA);
+  load_rows(1, zB);
+  if (MODE != 1) load_res(0, rres);
+  store_rows(0, zA);
+  load_rows(2, zA);
+  __syncthreads();  // chunk 0 and s_att staged
+  for (int k = 0; k < nch; k += 2) {
+    step(k, zB);                       // zB holds chunk k+1, zA chunk k+2
+    if (k + 1 < nch) step(k + 1, zA);  // zA holds chunk k+2, zB chunk k+3
   }
-  // the last atom with edges and any trailing atoms without
-  for (;;) {
-    finish_atom(k);
-    if (++k >= nv) break;
-    start_atom(k);
+}
+
+template <int H, int CW, int MODE>
+__global__ void __launch_bounds__(kAggThreads, 4)  // 2 workgroups (16 waves) per CU
+gat_agg_fwd_gather_kernel(const int32_t* __restrict__ groups, const int32_t* __restrict__ rowptr,
+                   const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
+                   int F, const float* __restrict__ bias, const float* __restrict__ attn,
+                   float* __restrict__ out) {
+  constexpr int LPD = CW / 4;                        // lanes per destination atom
+  constexpr int DPP = kAggThreads / LPD;             // destinations per pass
+  constexpr int NP = (kWin + DPP - 1) / DPP;         // passes over a full window
+  const int tid = threadIdx.x;
+  const int ds = tid / LPD, q = tid % LPD;
+  const int HF = H * F;
+  const int a0 = groups[blockIdx.x], a1 = groups[blockIdx.x + 1];
+  if (a1 <= a0 || lds_group(a0, a1, rowptr)) return;
+  const int nfc = F / CW;     // column chunks per head
+  const int nch = H * nfc;
+  const int ocols = MODE == 1 ? F : HF;
+  // group-relative 32-bit byte offsets from a wave-uniform base (< 2^31: a group spans at most
+  // kNodeGroupAtoms + one molecule's atoms, rows of <= 2^20 floats are checked by the host)
+  const float* Yg = Y + (int64_t)a0 * ldy;
+  const uint32_t rowb = (uint32_t)ldy * 4u;
+  const __amdgpu_buffer_rsrc_t rY = make_rsrc(Yg, (uint32_t)(a1 - a0) * rowb);
+  constexpr uint32_t kNone = 0xFFFFFFF0u;  // out of range: the load returns 0, moves no data
+
+  for (int w0 = a0; w0 < a1; w0 += kWin) {
+    const int nr = min(kWin, a1 - w0);
+    const int e0 = rowptr[w0];
+    const float* __restrict__ attw = attn + (int64_t)e0 * H;
+    const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)w0 * ocols, (uint32_t)(nr * ocols) * 4u);
+    // this thread's destinations: in-CSR ranges and the cached source-row offsets
+    int eb[NP], deg[NP];
+    uint32_t so[NP][kEC];
+    int dmax = 0;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int d = ds + DPP * p;
+      eb[p] = 0;
+      deg[p] = 0;
+      if (d < nr) {
+        eb[p] = rowptr[w0 + d] - e0;
+        deg[p] = rowptr[w0 + d + 1] - e0 - eb[p];
+      }
+#pragma unroll
+      for (int i = 0; i < kEC; ++i)
+        so[p][i] = (i < deg[p]) ? (uint32_t)(in_src[e0 + eb[p] + i] - a0) * rowb : kNone;
+      dmax = max(dmax, deg[p]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dmax = max(dmax, __shfl_xor(dmax, o, 64));  // wave-uniform
+    auto att = [&](int e, int h) -> float { return attw[e * H + h]; };
+
+    float4 tot[NP], rm[NP];
+    for (int k = 0; k < nch; ++k) {
+      const int h = MODE == 1 ? k % H : k / nfc;
+      const int fc = MODE == 1 ? k / H : k % nfc;
+      const int col = h * F + fc * CW + 4 * q;
+      const uint32_t colb = 4u * (uint32_t)col;
+      float4 acc[NP], res[NP];
+      // residual (flatten: this chunk's columns; mean: the f-chunk's head-mean columns)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int d = ds + DPP * p;
+        const uint32_t rb = (d < nr) ? (uint32_t)(w0 + d - a0) * rowb : kNone;
+        if (MODE != 1) res[p] = buf_ld4(rY, rb == kNone ? kNone : rb + 4u * (uint32_t)(HF + col));
+        else if (h == 0) rm[p] = buf_ld4(rY, rb == kNone ? kNone : rb + 4u * (uint32_t)(HF + fc * CW + 4 * q));
+      }
+      // cached edges: one batch of independent loads (one memory round trip per chunk)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) acc[p] = f4(0.f);
+      {
+        float4 z[NP][kEC];
+        float a[NP][kEC];
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+          for (int i = 0; i < kEC; ++i) {
+            z[p][i] = buf_ld4(rY, so[p][i] == kNone ? kNone : so[p][i] + colb);
+            a[p][i] = (i < deg[p]) ? att(eb[p] + i, h) : 0.f;
+          }
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+          for (int i = 0; i < kEC; ++i)
+            if (i < deg[p]) acc[p] = fma4(a[p][i], z[p][i], acc[p]);
+      }
+      if (dmax > kEC) {  // hubs
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          for (int i = kEC; i < deg[p]; ++i) {
+            const int e = eb[p] + i;
+            const uint32_t ob = (uint32_t)(in_src[e0 + e] - a0) * rowb + colb;
+            acc[p] = fma4(att(e, h), buf_ld4(rY, ob), acc[p]);
+          }
+      }
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int d = ds + DPP * p;
+        if (d < nr) {
+          if (MODE == 1) {
+            const float4 t = add4(acc[p], ld4(bias + col));
+            tot[p] = (h == 0) ? t : add4(tot[p], t);
+            if (h == H - 1) {
+              const float invh = (float)H;
+              buf_st4(rO, 4u * (uint32_t)(d * F + fc * CW + 4 * q),
+                      make_float4(tot[p].x / invh + rm[p].x, tot[p].y / invh + rm[p].y,
+                                  tot[p].z / invh + rm[p].z, tot[p].w / invh + rm[p].w));
+            }
+          } else {
+            float4 o = add4(add4(acc[p], res[p]), ld4(bias + col));
+            if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
+            buf_st4(rO, 4u * (uint32_t)(d * HF + col), o);
+          }
+        }
+      }
+    }
   }
 }
 
@@ -541,28 +672,37 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
 }
 
 template <int H, int VPL>
-int launch_fwd(int64_t N, const int32_t* rp, const int32_t* src, const float* Y, int64_t ldy, int F,
-               const float* al, const float* ar, const float* bias, float slope, int mode, float* out,
-               float* attn, float* elr, hipStream_t st) {
+int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, const int32_t* src,
+               const float* Y, int64_t ldy, int F, const float* al, const float* ar,
+               const float* bias, float slope, int mode, float* out, float* attn, float* elr,
+               hipStream_t st) {
   gat_logits_kernel<H, VPL><<<(unsigned)ceil_div(N, kWavesPerBlock), kWavesPerBlock * 64, 0, st>>>(
       N, Y, ldy, F, al, ar, elr);
   int rc = check_launch("gat_logits_kernel");
   if (rc) return rc;
-  // Wide layers (more than 4 float4 slices per lane) split every head's columns over 2 waves.
-  if constexpr (VPL > 4) {
-    constexpr int CS = 2, V2 = (VPL + 1) / 2;
-    if (F % 8 != 0) {
-      set_error("gat_agg_fwd: H*F > 1024 needs out_feats divisible by 8");
-      return MVML_ERR_INVALID;
-    }
-    const unsigned blocks = (unsigned)ceil_div(ceil_div(N, 64) * CS, kWavesPerBlock);
-    gat_agg_fwd_kernel<H, V2, CS, (V2 <= 3 ? MVML_FWD_UNR : 2)><<<blocks, kWavesPerBlock * 64, 0, st>>>(
-        N, rp, src, Y, ldy, F, elr, bias, slope, mode, out, attn);
-  } else {
-    const unsigned blocks = (unsigned)ceil_div(ceil_div(N, 64), kWavesPerBlock);
-    gat_agg_fwd_kernel<H, VPL, 1, (VPL <= 3 ? MVML_FWD_UNR : 2)><<<blocks, kWavesPerBlock * 64, 0, st>>>(
-        N, rp, src, Y, ldy, F, elr, bias, slope, mode, out, attn);
-  }
+  gat_softmax_kernel<H><<<(unsigned)ceil_div(N * H, 256), 256, 0, st>>>(N, rp, src, elr, slope, attn);
+  rc = check_launch("gat_softmax_kernel");
+  if (rc) return rc;
+  if (G == 0) return MVML_OK;
+#define MVML_AGG_FWD_M(CW, M)                                                                       \
+  do {                                                                                              \
+    gat_agg_fwd_lds_kernel<H, CW, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, rp, src, Y, ldy, F, \
+                                                                         bias, attn, out);          \
+    gat_agg_fwd_gather_kernel<H, CW, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, rp, src, Y, ldy,  \
+                                                                            F, bias, attn, out);    \
+  } while (0)
+#define MVML_AGG_FWD(CW)                                  \
+  do {                                                    \
+    if (mode == 0) MVML_AGG_FWD_M(CW, 0);                 \
+    else if (mode == 1) MVML_AGG_FWD_M(CW, 1);            \
+    else MVML_AGG_FWD_M(CW, 2);                           \
+  } while (0)
+  if (F % 32 == 0) MVML_AGG_FWD(32);
+  else if (F % 16 == 0) MVML_AGG_FWD(16);
+  else if (F % 8 == 0) MVML_AGG_FWD(8);
+  else MVML_AGG_FWD(4);
+#undef MVML_AGG_FWD
+#undef MVML_AGG_FWD_M
   return check_launch("gat_agg_fwd_kernel");
 }
 
@@ -599,6 +739,7 @@ int check_shapes(int H, int F, int mode, int64_t ldy, const void* Y, const char*
   MVML_REQUIRE(H == 1 || H == 2 || H == 4 || H == 8, "%s: num_heads must be 1, 2, 4 or 8 (got %d)", who, H);
   MVML_REQUIRE(F > 0 && F % 4 == 0, "%s: out_feats must be a positive multiple of 4 (got %d)", who, F);
   MVML_REQUIRE(H * F <= 2048, "%s: H*F must be <= 2048 (got %d)", who, H * F);
+  MVML_REQUIRE(ldy < (1 << 20), "%s: leading dimension too large", who);
   MVML_REQUIRE(mode >= 0 && mode <= 2, "%s: bad mode %d", who, mode);
   const int64_t need = (int64_t)mvml_gat_proj_cols(H, F, mode == 1);
   MVML_REQUIRE(ldy >= need && ldy % 4 == 0, "%s: leading dimension %lld < %lld or not a multiple of 4",
@@ -709,8 +850,8 @@ extern "C" int mvml_gat_proj_cols(int H, int F, int mean_residual) {
   return H * F + (mean_residual ? F : H * F);
 }
 
-extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
-                                const float* Y, int64_t ldy, int H, int F, const float* attn_l,
+extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
+                                const int32_t* in_rowptr, const int32_t* in_src, const float* Y, int64_t ldy, int H, int F, const float* attn_l,
                                 const float* attn_r, const float* bias, float slope, int mode,
                                 float* out, float* attn, float* elr, void* stream) {
   clear_error();
@@ -720,14 +861,17 @@ extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* in_rowptr, con
                ((uintptr_t)attn_l & 15) == 0 && ((uintptr_t)attn_r & 15) == 0,
                "gat_agg_fwd: out / bias / attention vectors must be 16-byte aligned");
   MVML_REQUIRE(attn != nullptr && elr != nullptr, "gat_agg_fwd: attn and elr outputs are required");
+  MVML_REQUIRE(num_groups == mvml_node_group_count(num_nodes) && (num_groups == 0 || node_groups),
+               "gat_agg_fwd: node_groups must come from mvml_build_node_groups (%lld groups expected)",
+               (long long)mvml_node_group_count(num_nodes));
   if (num_nodes == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
   const int vpl = (int)ceil_div(H * F, 256);
   switch (H) {
-    case 1: { MVML_VPL_CASES(launch_fwd, 1, num_nodes, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
-    case 2: { MVML_VPL_CASES(launch_fwd, 2, num_nodes, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
-    case 4: { MVML_VPL_CASES(launch_fwd, 4, num_nodes, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
-    case 8: { MVML_VPL_CASES(launch_fwd, 8, num_nodes, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
+    case 1: { MVML_VPL_CASES(launch_fwd, 1, num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
+    case 2: { MVML_VPL_CASES(launch_fwd, 2, num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
+    case 4: { MVML_VPL_CASES(launch_fwd, 4, num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
+    case 8: { MVML_VPL_CASES(launch_fwd, 8, num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
   }
   set_error("gat_agg_fwd: unsupported shape");
   return MVML_ERR_INVALID;

@@ -109,8 +109,9 @@ class GATLayerFunction(torch.autograd.Function):
         elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
         attn_l, attn_r = _c(attn_l), _c(attn_r)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}", "bytes": agg_fwd_bytes(N, E, H, F, out_cols, C - HF)}
-        call("mvml_gat_agg_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F, ptr(attn_l),
-             ptr(attn_r), ptr(_c(bias)), float(slope), int(mode), ptr(out), ptr(attn), ptr(elr), st)
+        call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.node_groups.numel() - 1, ptr(g.in_rowptr),
+             ptr(g.in_src), ptr(Y), ldy, H, F, ptr(attn_l), ptr(attn_r), ptr(_c(bias)), float(slope),
+             int(mode), ptr(out), ptr(attn), ptr(elr), st)
         ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r)
         ctx.Fin = Fin
         ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode, ctx.ldy = g, H, F, slope, mode, ldy

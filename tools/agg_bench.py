@@ -49,7 +49,7 @@ def main():
         oc = F if mode == 1 else H * F
         out = torch.empty((N, oc), device="cuda")
         attn = torch.empty((E, H), device="cuda")
-        f = lambda: call("mvml_gat_agg_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F,
+        f = lambda: call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.node_groups.numel() - 1, ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F,
                          ptr(al), ptr(ar), ptr(bias), 0.2, mode, ptr(out), ptr(attn), ptr(elr), st)
         ms = timeit(f)
         by = agg_fwd_bytes(N, E, H, F, oc, C - H * F)
