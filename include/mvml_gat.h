@@ -102,41 +102,47 @@ int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx, float alp
  *   Y row = [ Z (H*F) | R (H*F or F) ];  C = mvml_gat_proj_cols(H,F,mean).
  *   Wcat has row stride ldw >= Fin; columns Fin..ldw-1 are written as zeros, so a caller can
  *   pad X to a multiple of 4 columns and keep every GEMM operand 16-B aligned.
- * The attention reductions el/er are NOT folded into the GEMM: they are computed from Z inside
- * mvml_gat_agg_fwd exactly like `(feat * attn_l).sum(-1)`, which keeps fp32 logits as accurate
- * as the reference's.  mvml_gat_unfold_grads maps dL/dWcat back onto fc.weight and
- * res_fc.weight (the mean residual's gradient is replicated / H over the heads).
+ * mvml_gat_unfold_grads maps dL/dWcat back onto fc.weight and res_fc.weight (the mean
+ * residual's gradient is replicated / H over the heads).
  * ------------------------------------------------------------------------------------- */
 int mvml_gat_proj_cols(int H, int F, int mean_residual);
 int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, int H, int F, int Fin,
                           int ldw, int mean_residual, float* Wcat, void* stream);
 int mvml_gat_unfold_grads(const float* gWcat, int H, int F, int Fin, int ldg, int mean_residual,
                           float* g_fc_w, float* g_res_fc_w, void* stream);
-
+/* The projection GEMM (X [N, K] with row stride ldx, Wcat [C, K] with row stride ldw, K = the
+ * padded feature count) + GATConv's attention logits from the result:
+ *   el[n,h] = <Z[n,h,:], attn_l[h,:]>,  er[n,h] = <Z[n,h,:], attn_r[h,:]>
+ * (`(feat_src * attn_l).sum(-1)`), computed in the GEMM epilogue as per-32-column partial dots
+ * of the fp32 Z tile and summed per head in fixed order — no second pass over Z.
+ * attn_lr: [2, H*F] = [attn_l | attn_r]; elr: [N, 2H] = [el | er].  F % 32 == 0.
+ * workspace: mvml_gat_proj_fwd_workspace_size(N, H, F) bytes (the partials). */
+size_t mvml_gat_proj_fwd_workspace_size(int64_t num_nodes, int H, int F);
+int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx, int64_t K,
+                      const float* Wcat, int64_t ldw, const float* attn_lr, int H, int F,
+                      int mean_residual, float* Y, int64_t ldy, float* elr, void* workspace,
+                      size_t workspace_bytes, void* stream);
 /* dL/dattn_l[h,f] = sum_n gelr[n, h] * Z[n, h*F+f] and dL/dattn_r with gelr[n, H+h] (autograd
  * of `(feat * attn_l).sum(-1)` in GATConv.forward); deterministic two-stage reduction. */
 size_t mvml_gat_attn_grad_workspace_size(int64_t num_nodes, int H, int F);
 int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, const float* Y, int64_t ldy,
                        const float* gelr, float* g_attn_l, float* g_attn_r, void* workspace,
                        size_t workspace_bytes, void* stream);
-
 /* ---------------------------------------------------------------------------------------
- * Fused GAT attention + aggregation, forward (one workgroup per node group; replaces
- * dgl GATConv.forward from `el = ...` to the residual/bias, plus dgllife GATLayer's
- * flatten/ELU or head-mean, model.py:77-81):
- *   el/er = <Z, attn_l/attn_r> -> apply_edges(u_add_v) -> LeakyReLU(slope) -> edge_softmax
- *   -> update_all(u_mul_e, sum) -> + residual R -> + bias -> GATLayer agg (dgllife 0.3.0):
- *   mode 0 flatten+ELU, mode 1 mean over heads, mode 2 flatten (no activation).
- * Y is the projection output above (mean_residual layout iff mode 1; ldy >= its C, multiple of
- * 4).  attn_l/attn_r: [H*F] (GATConv.attn_l / attn_r).  out is [N, H*F] (modes 0, 2) or [N, F]
- * (mode 1).  attn [E, H] receives the edge_softmax output in in-CSR slot order and elr [N, 2H]
- * the logit halves [el | er]; both are required by the backward.
+ * Fused GAT attention + aggregation, forward (one workgroup per node group; replaces dgl
+ * GATConv.forward from apply_edges to the residual/bias, plus dgllife GATLayer's flatten/ELU
+ * or head-mean, model.py:77-81):
+ *   apply_edges(u_add_v) on elr -> LeakyReLU(slope) -> edge_softmax -> update_all(u_mul_e,
+ *   sum) -> + residual R -> + bias -> GATLayer agg (dgllife 0.3.0): mode 0 flatten+ELU,
+ *   mode 1 mean over heads, mode 2 flatten (no activation).
+ * Y is the projection output (mean_residual layout iff mode 1; ldy >= its C, multiple of 4),
+ * elr its logits (mvml_gat_proj_fwd).  out is [N, H*F] (modes 0, 2) or [N, F] (mode 1).
+ * attn [E, H] receives the edge_softmax output in in-CSR slot order (needed by the backward).
  * ------------------------------------------------------------------------------------- */
 int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
                      const int32_t* in_rowptr, const int32_t* in_src, const float* Y, int64_t ldy,
-                     int H, int F, const float* attn_l, const float* attn_r, const float* bias,
-                     float slope, int mode, float* out,
-                     float* attn, float* elr, void* stream);
+                     int H, int F, const float* elr, const float* bias, float slope, int mode,
+                     float* out, float* attn, void* stream);
 /* Backward of mvml_gat_agg_fwd (DGL GSpMM / GSDDMM / EdgeSoftmax backward + torch autograd of
  * el/er, residual, bias, ELU, mean).  Atomic-free: the u_mul_e-sum transpose is a gather over
  * the out-CSR.  Writes gY[N, ldgy] = [dZ | dR] (the GEMM backward's input, same column layout

@@ -139,37 +139,23 @@ __device__ __forceinline__ float4 grst_of(const float* __restrict__ g_out, const
 }
 
 // ---------------------------------------------------------------------------------- forward
-// Logits: el[n,h] = <Z[n,h,:], attn_l[h,:]>, er likewise, one wave per atom (a streaming read of
-// Z, 16-B slices per lane, butterfly head reduction).  elr[n] = [el | er] is a compact [N, 2H]
-// array, so the aggregation gathers a neighbour's logits as one 16-B load instead of reaching
-// into Y's wide rows.
-template <int H, int VPL>
-__global__ void __launch_bounds__(kWavesPerBlock * 64)
-gat_logits_kernel(int64_t N, const float* __restrict__ Y, int64_t ldy, int F,
-                  const float* __restrict__ attn_l, const float* __restrict__ attn_r,
-                  float* __restrict__ elr) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t v = (int64_t)blockIdx.x * kWavesPerBlock + wid;
-  if (v >= N) return;
-  const int HF = H * F;
-  const float* yv = Y + v * ldy;
-  float el[H], er[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) { el[h] = 0.f; er[h] = 0.f; }
-#pragma unroll
-  for (int c = 0; c < VPL; ++c) {
-    const int col = 4 * (lane + 64 * c);
-    if (col < HF) {
-      const float4 z = ld4(yv + col);
-      const int h = col / F;
-      add_at<H>(el, h, dot4(z, ld4(attn_l + col)));
-      add_at<H>(er, h, dot4(z, ld4(attn_r + col)));
-    }
-  }
-  HeadReduce<H>::template all<false>(el, lane);
-  HeadReduce<H>::template all<false>(er, lane);
-  store_heads<H>(elr + v * 2 * H, el, lane);
-  store_heads<H>(elr + v * 2 * H + H, er, lane);
+// Logits: el[n,h] = <Z[n,h,:], attn_l[h,:]>, er likewise.  The projection GEMM's epilogue leaves
+// per-W-column partial dots part[g][side][n]; this sums a head's F/32 blocks in order and
+// writes the compact elr[n] = [el | er] (the softmax's gathers and the backward read it).
+template <int H>
+__global__ void __launch_bounds__(256)
+gat_logits_finalize_kernel(int64_t N, int F, int W, const float* __restrict__ part,
+                           float* __restrict__ elr) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over N * 2H
+  if (i >= N * 2 * H) return;
+  const int64_t v = i % N;           // node-fastest: coalesced partial reads
+  const int sh = (int)(i / N);        // side * H + h
+  const int side = sh / H, h = sh % H;
+  const int nbh = F / W;
+  const float* p = part + ((int64_t)(h * nbh) * 2 + side) * N + v;  // [group][side][node]
+  float acc = p[0];
+  for (int b = 1; b < nbh; ++b) acc += p[(int64_t)b * 2 * N];
+  elr[v * 2 * H + sh] = acc;
 }
 
 // edge_softmax (dgl 0.9.1, norm_by='dst'): one thread per (destination, head) pair:
@@ -671,15 +657,11 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
   store_heads<H>(gelr + u * 2 * H, gel, lane);
 }
 
-template <int H, int VPL>
+template <int H>
 int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, const int32_t* src,
-               const float* Y, int64_t ldy, int F, const float* al, const float* ar,
-               const float* bias, float slope, int mode, float* out, float* attn, float* elr,
-               hipStream_t st) {
-  gat_logits_kernel<H, VPL><<<(unsigned)ceil_div(N, kWavesPerBlock), kWavesPerBlock * 64, 0, st>>>(
-      N, Y, ldy, F, al, ar, elr);
-  int rc = check_launch("gat_logits_kernel");
-  if (rc) return rc;
+               const float* Y, int64_t ldy, int F, const float* bias, float slope, int mode,
+               float* out, float* attn, const float* elr, hipStream_t st) {
+  int rc;
   gat_softmax_kernel<H><<<(unsigned)ceil_div(N * H, 256), 256, 0, st>>>(N, rp, src, elr, slope, attn);
   rc = check_launch("gat_softmax_kernel");
   if (rc) return rc;
@@ -850,28 +832,62 @@ extern "C" int mvml_gat_proj_cols(int H, int F, int mean_residual) {
   return H * F + (mean_residual ? F : H * F);
 }
 
+extern "C" size_t mvml_gat_proj_fwd_workspace_size(int64_t num_nodes, int H, int F) {
+  return carve_size((size_t)num_nodes * 2 * (H * F / (1 << proj_logw(F))) * sizeof(float));
+}
+
+extern "C" int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx, int64_t K,
+                                 const float* Wcat, int64_t ldw, const float* attn_lr, int H,
+                                 int F, int mean_residual, float* Y,
+                                 int64_t ldy, float* elr, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+  clear_error();
+  MVML_REQUIRE(H == 1 || H == 2 || H == 4 || H == 8, "gat_proj_fwd: num_heads must be 1, 2, 4 or 8 (got %d)", H);
+  MVML_REQUIRE(F > 0 && F % 4 == 0, "gat_proj_fwd: out_feats must be a positive multiple of 4 (got %d)", F);
+  MVML_REQUIRE(num_nodes >= 0 && K > 0 && ldx >= K && ldw >= K, "gat_proj_fwd: bad shape");
+  const int C = mvml_gat_proj_cols(H, F, mean_residual);
+  MVML_REQUIRE(ldy >= C, "gat_proj_fwd: ldy < %d", C);
+  if (num_nodes == 0) return MVML_OK;
+  if (!workspace || workspace_bytes < mvml_gat_proj_fwd_workspace_size(num_nodes, H, F)) {
+    set_error("gat_proj_fwd: workspace of mvml_gat_proj_fwd_workspace_size bytes required");
+    return MVML_ERR_WORKSPACE;
+  }
+  MVML_REQUIRE(attn_lr != nullptr && elr != nullptr, "gat_proj_fwd: attn_lr and elr are required");
+  hipStream_t st = as_stream(stream);
+  float* part = static_cast<float*>(workspace);
+  int rc = gemm_proj_epi(num_nodes, C, K, X, ldx, Wcat, ldw, Y, ldy, attn_lr, H * F, proj_logw(F), part, st);
+  if (rc) return rc;
+  const int W = 1 << proj_logw(F);
+  const unsigned blocks = (unsigned)ceil_div(num_nodes * 2 * H, 256);
+  switch (H) {
+    case 1: gat_logits_finalize_kernel<1><<<blocks, 256, 0, st>>>(num_nodes, F, W, part, elr); break;
+    case 2: gat_logits_finalize_kernel<2><<<blocks, 256, 0, st>>>(num_nodes, F, W, part, elr); break;
+    case 4: gat_logits_finalize_kernel<4><<<blocks, 256, 0, st>>>(num_nodes, F, W, part, elr); break;
+    case 8: gat_logits_finalize_kernel<8><<<blocks, 256, 0, st>>>(num_nodes, F, W, part, elr); break;
+  }
+  return check_launch("gat_logits_finalize_kernel");
+}
+
 extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
-                                const int32_t* in_rowptr, const int32_t* in_src, const float* Y, int64_t ldy, int H, int F, const float* attn_l,
-                                const float* attn_r, const float* bias, float slope, int mode,
-                                float* out, float* attn, float* elr, void* stream) {
+                                const int32_t* in_rowptr, const int32_t* in_src, const float* Y,
+                                int64_t ldy, int H, int F, const float* elr, const float* bias,
+                                float slope, int mode, float* out, float* attn, void* stream) {
   clear_error();
   int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_fwd");
   if (rc) return rc;
-  MVML_REQUIRE(((uintptr_t)out & 15) == 0 && ((uintptr_t)bias & 15) == 0 &&
-               ((uintptr_t)attn_l & 15) == 0 && ((uintptr_t)attn_r & 15) == 0,
-               "gat_agg_fwd: out / bias / attention vectors must be 16-byte aligned");
-  MVML_REQUIRE(attn != nullptr && elr != nullptr, "gat_agg_fwd: attn and elr outputs are required");
+  MVML_REQUIRE(((uintptr_t)out & 15) == 0 && ((uintptr_t)bias & 15) == 0,
+               "gat_agg_fwd: out / bias must be 16-byte aligned");
+  MVML_REQUIRE(attn != nullptr && elr != nullptr, "gat_agg_fwd: elr input and attn output are required");
   MVML_REQUIRE(num_groups == mvml_node_group_count(num_nodes) && (num_groups == 0 || node_groups),
                "gat_agg_fwd: node_groups must come from mvml_build_node_groups (%lld groups expected)",
                (long long)mvml_node_group_count(num_nodes));
   if (num_nodes == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
-  const int vpl = (int)ceil_div(H * F, 256);
   switch (H) {
-    case 1: { MVML_VPL_CASES(launch_fwd, 1, num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
-    case 2: { MVML_VPL_CASES(launch_fwd, 2, num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
-    case 4: { MVML_VPL_CASES(launch_fwd, 4, num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
-    case 8: { MVML_VPL_CASES(launch_fwd, 8, num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, attn_l, attn_r, bias, slope, mode, out, attn, elr, st) break; }
+    case 1: return launch_fwd<1>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, st);
+    case 2: return launch_fwd<2>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, st);
+    case 4: return launch_fwd<4>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, st);
+    case 8: return launch_fwd<8>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, st);
   }
   set_error("gat_agg_fwd: unsupported shape");
   return MVML_ERR_INVALID;

@@ -158,12 +158,28 @@ __device__ __forceinline__ float comp(const float4& v, int s) {
   return s == 0 ? v.x : (s == 1 ? v.y : (s == 2 ? v.z : v.w));
 }
 
-template <bool AK, bool BKM>
+// Optional GAT-projection epilogue (EPI_LOGW >= 0, W = 1 << EPI_LOGW columns per partial):
+// for every W-column group g of the first ep_cols output columns (Z = X fc^T), the per-row
+// partial logits
+//   part[g][0][row] = sum_{c in g} C[row][c] * attn_l[c],  part[g][1][row] = ... attn_r[c]
+// (attn_l / attn_r = ep_vec[0 : ep_cols] / ep_vec[ep_cols : 2 ep_cols]; W divides F so a group
+// never straddles two heads), so GATConv's el = (feat * attn_l).sum(-1) needs no second pass
+// over Z: mvml_gat_proj_fwd sums a head's groups in fixed order.  In a 32x32 accumulator tile
+// the lane holds a column and 16 rows: a halving butterfly over the W lanes of a group
+// (values 32 -> 32/W, masks W/2 .. 1) leaves lane li with the values of index
+// ((li & (W-1)) << (5 - EPI_LOGW)) | t, index = side * 16 + row register.
+struct ProjEpi {
+  const float* vec;  // [2][cols]
+  int cols;          // H*F
+  float* part;       // [cols / W][2][M]: a wave's stores for one (group, side) are 32 rows, contiguous
+};
+
+template <bool AK, bool BKM, int EPI_LOGW = -1>
 __global__ void __launch_bounds__(kThreads, 2)
 gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
-                float* __restrict__ slab, int a_vec, int b_vec) {
+                float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{}) {
   using SA = Stager<AK>;
   using SB = Stager<BKM>;
   // [stage][A tile | B tile], one __shared__ object (a second one can de-pipeline glds waits).
@@ -271,6 +287,47 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   }
 
   // Epilogue. C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  if constexpr (EPI_LOGW >= 0) {
+    constexpr int W = 1 << EPI_LOGW, NV = 32 >> EPI_LOGW;
+  #pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t cb0 = n0 + wn * 64 + j * 32;  // first column of this 32-column block
+        if (cb0 >= epi.cols) continue;             // wave-uniform
+        const int64_t c = cb0 + li;
+        const float al = c < epi.cols ? epi.vec[c] : 0.f;
+        const float ar = c < epi.cols ? epi.vec[epi.cols + c] : 0.f;
+        float v[32];  // [side][row register]
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { v[r] = acc[i][j][r] * al; v[16 + r] = acc[i][j][r] * ar; }
+#pragma unroll
+        for (int st = 0; st < EPI_LOGW; ++st) {
+          const int half = 16 >> st, mask = (W / 2) >> st;
+          const bool hi = (lane & mask) != 0;
+#pragma unroll
+          for (int t = 0; t < half; ++t) {
+            // the empty asm pins both values in registers first: otherwise the selects fold
+            // into a dynamically indexed v[], lowered as a 32-way compare chain
+            float lo = v[t], up = v[t + half];
+            asm volatile("" : "+v"(lo), "+v"(up));
+            const float keep = hi ? up : lo;
+            const float send = hi ? lo : up;
+            v[t] = keep + __shfl_xor(send, mask, 64);
+          }
+        }
+        const int64_t gc = cb0 + (li & ~(W - 1));  // first column of the lane's group
+        if (gc < epi.cols) {
+#pragma unroll
+          for (int t = 0; t < NV; ++t) {
+            const int idx = ((li & (W - 1)) << (5 - EPI_LOGW)) | t;
+            const int side = idx >> 4, r = idx & 15;
+            const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+            if (row < M) epi.part[((gc / W) * 2 + side) * M + row] = v[t];
+          }
+        }
+      }
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -428,6 +485,33 @@ extern "C" int mvml_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, i
   }
   return rc;
 }
+
+namespace mvml {
+// Projection GEMM with the logits-partial epilogue: C[M,N] = A[M,K] B[N,K]^T (both
+// K-contiguous, no split-K: K is the small feature dimension), part as in ProjEpi.
+int gemm_proj_epi(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
+                  int64_t ldb, float* C, int64_t ldc, const float* vec, int cols, int logw,
+                  float* part, hipStream_t st) {
+  const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
+  MVML_REQUIRE(tiles < (int64_t(1) << 31), "gat_proj_fwd: too many tiles");
+  MVML_REQUIRE(cols <= N && (logw >= 2 && logw <= 5), "gat_proj_fwd: bad partial width");
+  const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0);
+  const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0);
+  dim3 grid((unsigned)tiles, 1);
+#define MVML_PROJ(LW)                                                                          \
+  gemm_f32_kernel<false, false, LW><<<grid, kThreads, 0, st>>>(                                \
+      M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,        \
+      ProjEpi{vec, cols, part})
+  switch (logw) {
+    case 5: MVML_PROJ(5); break;
+    case 4: MVML_PROJ(4); break;
+    case 3: MVML_PROJ(3); break;
+    default: MVML_PROJ(2); break;
+  }
+#undef MVML_PROJ
+  return check_launch("gemm_f32_kernel(proj)");
+}
+}  // namespace mvml
 
 extern "C" size_t mvml_colsum_workspace_size(int64_t M, int64_t N) {
   return carve_size((size_t)colsum_splits(M, N) * N * sizeof(float));

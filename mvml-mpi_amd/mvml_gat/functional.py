@@ -40,7 +40,7 @@ def _round4(x):
 
 def agg_fwd_bytes(N, E, H, F, out_cols, res_cols):
     """Algorithmic HBM bytes of one mvml_gat_agg_fwd: read Z and R once,
-    rowptr, src ids; write the layer output, the saved attention and el/er.  R is the
+    rowptr, src ids, el/er; write the layer output and the saved attention.  R is the
     head-mean residual (F columns) in mean mode."""
     return 4 * (N * H * F + N * res_cols + 2 * N * H + (N + 1) + E + N * out_cols + E * H)
 
@@ -101,17 +101,22 @@ class GATLayerFunction(torch.autograd.Function):
         call("mvml_gat_fold_weights", ptr(_c(fc_w)), ptr(_c(res_w)), H, F, Fin, Fp, mean_res,
              ptr(Wcat), st)
         Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
-        gemm(Xp, Wcat, N, C, Fp, 0, 0, Fp, Fp, Y, ldy)
+        elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
+        attn_l, attn_r = _c(attn_l), _c(attn_r)
+        attn_lr = torch.cat([attn_l.reshape(-1), attn_r.reshape(-1)])
+        L = _lib.lib()
+        wp, wn = _lib.ws_ptr_size(L.mvml_gat_proj_fwd_workspace_size(N, H, F), dev)
+        _lib.call_tag[0] = {"flops": 2 * N * C * Fp}
+        call("mvml_gat_proj_fwd", N, ptr(Xp), Fp, Fp, ptr(Wcat), Fp, ptr(attn_lr), H, F, mean_res,
+             ptr(Y), ldy, ptr(elr), wp, wn, st)
         out_cols = F if mode == MODE_MEAN else HF
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()
         attn = torch.empty((E, H), dtype=torch.float32, device=dev)
-        elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
-        attn_l, attn_r = _c(attn_l), _c(attn_r)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}", "bytes": agg_fwd_bytes(N, E, H, F, out_cols, C - HF)}
         call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.node_groups.numel() - 1, ptr(g.in_rowptr),
-             ptr(g.in_src), ptr(Y), ldy, H, F, ptr(attn_l), ptr(attn_r), ptr(_c(bias)), float(slope),
-             int(mode), ptr(out), ptr(attn), ptr(elr), st)
+             ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(_c(bias)), float(slope), int(mode),
+             ptr(out), ptr(attn), st)
         ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r)
         ctx.Fin = Fin
         ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode, ctx.ldy = g, H, F, slope, mode, ldy

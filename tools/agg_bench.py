@@ -49,8 +49,10 @@ def main():
         oc = F if mode == 1 else H * F
         out = torch.empty((N, oc), device="cuda")
         attn = torch.empty((E, H), device="cuda")
-        f = lambda: call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.node_groups.numel() - 1, ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F,
-                         ptr(al), ptr(ar), ptr(bias), 0.2, mode, ptr(out), ptr(attn), ptr(elr), st)
+        elr.normal_()
+        f = lambda: call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.node_groups.numel() - 1,
+                         ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(bias), 0.2,
+                         mode, ptr(out), ptr(attn), st)
         ms = timeit(f)
         by = agg_fwd_bytes(N, E, H, F, oc, C - H * F)
         print(f"  agg_fwd {name:16s} {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
