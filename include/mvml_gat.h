@@ -86,6 +86,17 @@ int mvml_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                   const float* A, int64_t lda, const float* B, int64_t ldb,
                   const float* bias, float beta, int act, float* C, int64_t ldc,
                   void* workspace, size_t workspace_bytes, void* stream);
+/* Same contract, computed on bf16 MFMA (v_mfma_f32_32x32x16_bf16) at fp32 accuracy: each fp32
+ * operand is split exactly into three bf16 terms (x = x0 + x1 + x2, 24 significant bits) and
+ * the six cross products with relative weight >= 2^-16 are accumulated in fp32; the dropped
+ * ones are < 2^-25 relative.  Errors against fp64 are those of an fp32 GEMM (verified in
+ * tests/test_gpu_parity.py); results are deterministic but not bitwise equal to mvml_gemm_f32. */
+int mvml_gemm_f32x3(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                    const float* A, int64_t lda, const float* B, int64_t ldb,
+                    const float* bias, float beta, int act, float* C, int64_t ldc,
+                    void* workspace, size_t workspace_bytes, void* stream);
+#define MVML_GEMM_F32 0   /* algo: v_mfma_f32_32x32x2_f32 */
+#define MVML_GEMM_F32X3 1 /* algo: split-bf16 x3 */
 /* Column sums: out[n] = beta*out[n] + alpha * sum_m X[m*ldx + n], deterministic two-stage
  * tree.  Replaces the bias gradients torch autograd computes for GATConv.bias / LSTM / Linear. */
 size_t mvml_colsum_workspace_size(int64_t M, int64_t N);
@@ -120,8 +131,8 @@ int mvml_gat_unfold_grads(const float* gWcat, int H, int F, int Fin, int ldg, in
 size_t mvml_gat_proj_fwd_workspace_size(int64_t num_nodes, int H, int F);
 int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx, int64_t K,
                       const float* Wcat, int64_t ldw, const float* attn_lr, int H, int F,
-                      int mean_residual, float* Y, int64_t ldy, float* elr, void* workspace,
-                      size_t workspace_bytes, void* stream);
+                      int mean_residual, int algo /* MVML_GEMM_* */, float* Y, int64_t ldy,
+                      float* elr, void* workspace, size_t workspace_bytes, void* stream);
 /* dL/dattn_l[h,f] = sum_n gelr[n, h] * Z[n, h*F+f] and dL/dattn_r with gelr[n, H+h] (autograd
  * of `(feat * attn_l).sum(-1)` in GATConv.forward); deterministic two-stage reduction. */
 size_t mvml_gat_attn_grad_workspace_size(int64_t num_nodes, int H, int F);

@@ -224,8 +224,11 @@ __device__ __forceinline__ bool lds_group(int a0, int a1, const int32_t* __restr
   return !__syncthreads_or(hub);
 }
 
+#ifndef MVML_LDS_WAVES
+#define MVML_LDS_WAVES 4
+#endif
 template <int H, int CW, int MODE>
-__global__ void __launch_bounds__(kAggThreads, 4)  // 2 workgroups (16 waves) per CU
+__global__ void __launch_bounds__(kAggThreads, MVML_LDS_WAVES)  // 2 workgroups (16 waves) per CU
 gat_agg_fwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __restrict__ rowptr,
                        const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
                        int F, const float* __restrict__ bias, const float* __restrict__ attn,
@@ -254,7 +257,7 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __rest
   // this thread's destinations: the LDS slots of their first kEC source rows and attention
   // values; a missing edge (i >= in-degree) points at the destination's own row and at a zero
   // attention, so the edge loop is branch- and mask-free (fma(0, z, acc) == acc)
-  int so[NP][kEC], ao[NP][kEC];
+  int so[NP][kEC], ab[NP], ad[NP];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     const int d = ds + DPP * p;
@@ -263,10 +266,11 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __rest
       eb = rowptr[a0 + d] - e0;
       deg = rowptr[a0 + d + 1] - e0 - eb;
     }
+    ab[p] = eb * H;
+    ad[p] = deg;
 #pragma unroll
     for (int i = 0; i < kEC; ++i) {
       so[p][i] = ((i < deg) ? in_src[e0 + eb + i] - a0 : (d < nr ? d : 0)) * LPD + q;
-      ao[p][i] = ((i < deg) ? eb + i : kECap) * H;
     }
   }
   // chunk k -> global column of this lane
@@ -314,7 +318,8 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __rest
 #pragma unroll
     for (int p = 0; p < NP; ++p)
 #pragma unroll
-      for (int i = 0; i < kEC; ++i) acc[p] = fma4(s_att[ao[p][i] + h], zl[so[p][i]], acc[p]);
+      for (int i = 0; i < kEC; ++i)
+        acc[p] = fma4(s_att[(i < ad[p] ? ab[p] + i * H : kECap * H) + h], zl[so[p][i]], acc[p]);
 #endif
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
@@ -838,8 +843,8 @@ extern "C" size_t mvml_gat_proj_fwd_workspace_size(int64_t num_nodes, int H, int
 
 extern "C" int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx, int64_t K,
                                  const float* Wcat, int64_t ldw, const float* attn_lr, int H,
-                                 int F, int mean_residual, float* Y,
-                                 int64_t ldy, float* elr, void* workspace, size_t workspace_bytes,
+                                 int F, int mean_residual, int algo, float* Y, int64_t ldy,
+                                 float* elr, void* workspace, size_t workspace_bytes,
                                  void* stream) {
   clear_error();
   MVML_REQUIRE(H == 1 || H == 2 || H == 4 || H == 8, "gat_proj_fwd: num_heads must be 1, 2, 4 or 8 (got %d)", H);
@@ -855,7 +860,9 @@ extern "C" int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx,
   MVML_REQUIRE(attn_lr != nullptr && elr != nullptr, "gat_proj_fwd: attn_lr and elr are required");
   hipStream_t st = as_stream(stream);
   float* part = static_cast<float*>(workspace);
-  int rc = gemm_proj_epi(num_nodes, C, K, X, ldx, Wcat, ldw, Y, ldy, attn_lr, H * F, proj_logw(F), part, st);
+  MVML_REQUIRE(algo == MVML_GEMM_F32 || algo == MVML_GEMM_F32X3, "gat_proj_fwd: bad algo %d", algo);
+  int rc = gemm_proj_epi(algo == MVML_GEMM_F32X3, num_nodes, C, K, X, ldx, Wcat, ldw, Y, ldy,
+                         attn_lr, H * F, proj_logw(F), part, st);
   if (rc) return rc;
   const int W = 1 << proj_logw(F);
   const unsigned blocks = (unsigned)ceil_div(num_nodes * 2 * H, 256);

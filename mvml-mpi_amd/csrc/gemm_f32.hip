@@ -14,12 +14,45 @@
 // Small-output / long-K products (the weight gradients, K = atoms in the batch) split K over
 // workgroups into fp32 slabs that a second kernel sums in fixed order — deterministic, no
 // float atomics.
+//
+// Split-bf16 variant (X3): the same tiles and LDS pipeline, but every fp32 operand fragment is
+// split in registers into three bf16 terms, x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0),
+// x2 = bf16(x - x0 - x1): 3 x 8 significant bits = fp32's 24, exact for normal values), and
+// the product is the six bf16 MFMAs (v_mfma_f32_32x32x16_bf16, fp32 accumulate)
+//   a0b0 + a0b1 + a1b0 + a0b2 + a1b1 + a2b0,
+// dropping only a1b2 + a2b1 + a2b2 (< 2^-25 relative per product).  Products of bf16 are exact
+// in fp32, so the result carries fp32 GEMM accuracy (tests/test_gpu_parity.py compares both
+// variants against fp64) at 6 bf16 MFMAs per 16 k instead of 8 f32 MFMAs at 1/16 the rate.
 #include "common.h"
 
 namespace mvml {
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// fp32 x 8 -> three bf16 x 8 terms (round-to-nearest each; the residuals are exact in fp32).
+__device__ __forceinline__ void split3(const float4& lo, const float4& hi, bf16x8& p0, bf16x8& p1,
+                                       bf16x8& p2) {
+  const f32x8 x = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  p0 = __builtin_convertvector(x, bf16x8);
+  const f32x8 r = x - __builtin_convertvector(p0, f32x8);
+  p1 = __builtin_convertvector(r, bf16x8);
+  const f32x8 r2 = r - __builtin_convertvector(p1, f32x8);
+  p2 = __builtin_convertvector(r2, bf16x8);
+}
+
+// acc += (a0 + a1 + a2)(b0 + b1 + b2) to fp32 accuracy: the six significant cross terms.
+__device__ __forceinline__ f32x16 mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
 
 constexpr int BM = 128, BN = 128, BKT = 32, kThreads = 256;
 constexpr int kTileFloats = 128 * BKT;  // one operand tile in LDS (16 KB)
@@ -141,6 +174,34 @@ struct Stager {
     }
   }
 
+  // Split-bf16 operand fragment of one 32x32x16 MFMA: the lane's 8 consecutive k values
+  // k = 8g .. 8g+7 of k-group g (g = 2 t + (lane >> 5) for 16-k step t), as two float4.
+  // Inline asm for the same reason as frag_asm; the caller waits lgkmcnt.
+  __device__ static __forceinline__ void frag8_asm(uint32_t tile_b, int row, int g, float4& lo,
+                                                   float4& hi) {
+    if (!KMAJ) {
+      const uint32_t base = tile_b + row * (BKT * 4);
+      const uint32_t a0 = base + 16 * ((2 * g) ^ swz(row)), a1 = base + 16 * ((2 * g + 1) ^ swz(row));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(a0) : "memory");
+      asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(a1) : "memory");
+    } else {
+      const uint32_t addr = tile_b + ((8 * g) * 128 + row) * 4;
+      asm volatile(
+          "ds_read_b32 %0, %8\n\t"
+          "ds_read_b32 %1, %8 offset:512\n\t"
+          "ds_read_b32 %2, %8 offset:1024\n\t"
+          "ds_read_b32 %3, %8 offset:1536\n\t"
+          "ds_read_b32 %4, %8 offset:2048\n\t"
+          "ds_read_b32 %5, %8 offset:2560\n\t"
+          "ds_read_b32 %6, %8 offset:3072\n\t"
+          "ds_read_b32 %7, %8 offset:3584"
+          : "=&v"(lo.x), "=&v"(lo.y), "=&v"(lo.z), "=&v"(lo.w), "=&v"(hi.x), "=&v"(hi.y),
+            "=&v"(hi.z), "=&v"(hi.w)
+          : "v"(addr)
+          : "memory");
+    }
+  }
+
   // Fragment of k-group g (8 k values): element s of the result is the operand value at
   // row `row`, k = 8g + 4h + s, where h = lane >> 5 — the k order both operands share.
   __device__ static __forceinline__ float4 frag(const float* lds_tile, int row, int g, int h) {
@@ -174,7 +235,7 @@ struct ProjEpi {
   float* part;       // [cols / W][2][M]: a wave's stores for one (group, side) are 32 rows, contiguous
 };
 
-template <bool AK, bool BKM, int EPI_LOGW = -1>
+template <bool AK, bool BKM, int EPI_LOGW = -1, bool X3 = false>
 __global__ void __launch_bounds__(kThreads, 2)
 gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
@@ -252,6 +313,39 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     }
     const uint32_t sa_b = lds_b + (uint32_t)(cur * 2 * kTileFloats * 4);
     const uint32_t sb_b = sa_b + kTileFloats * 4;
+    if constexpr (X3) {
+      // two 16-k steps; the fp32 fragments of step 1 are read under step 0's MFMAs and split
+      // there (VALU beside the matrix pipe); 4 sub-tiles x 6 bf16 MFMAs per step
+      float4 f[2][4][2];  // [step][a0, a1, b0, b1][lo, hi]
+      bf16x8 pa[2][3], pb[2][3];
+#define MVML_FRAGS8(T)                                                          \
+      SA::frag8_asm(sa_b, ra0, 2 * (T) + lk, f[T][0][0], f[T][0][1]);           \
+      SA::frag8_asm(sa_b, ra1, 2 * (T) + lk, f[T][1][0], f[T][1][1]);           \
+      SB::frag8_asm(sb_b, rb0, 2 * (T) + lk, f[T][2][0], f[T][2][1]);           \
+      SB::frag8_asm(sb_b, rb1, 2 * (T) + lk, f[T][3][0], f[T][3][1]);
+#define MVML_SPLIT(T)                                                           \
+      split3(f[T][0][0], f[T][0][1], pa[0][0], pa[0][1], pa[0][2]);             \
+      split3(f[T][1][0], f[T][1][1], pa[1][0], pa[1][1], pa[1][2]);             \
+      split3(f[T][2][0], f[T][2][1], pb[0][0], pb[0][1], pb[0][2]);             \
+      split3(f[T][3][0], f[T][3][1], pb[1][0], pb[1][1], pb[1][2]);
+#define MVML_MFMAS3()                                                           \
+      acc[0][0] = mfma_x3(pa[0], pb[0], acc[0][0]);                             \
+      acc[0][1] = mfma_x3(pa[0], pb[1], acc[0][1]);                             \
+      acc[1][0] = mfma_x3(pa[1], pb[0], acc[1][0]);                             \
+      acc[1][1] = mfma_x3(pa[1], pb[1], acc[1][1]);
+      MVML_FRAGS8(0)
+      MVML_FRAGS8(1)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      MVML_SPLIT(0)
+      MVML_MFMAS3()
+      MVML_SPLIT(1)
+      MVML_MFMAS3()
+      __builtin_amdgcn_sched_barrier(0);
+#undef MVML_FRAGS8
+#undef MVML_SPLIT
+#undef MVML_MFMAS3
+    } else {
     float4 fa0[2], fa1[2], fb0[2], fb1[2];  // [register set] x (sub-tile 0 / 1)
 #define MVML_FRAGS(G, SET)                                  \
     SA::template frag_asm<G>(sa_b, ra0, lk, fa0[SET]);      \
@@ -284,6 +378,7 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #undef MVML_FRAGS
 #undef MVML_MFMAS
 #undef MVML_WAIT_LDS
+    }
   }
 
   // Epilogue. C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
@@ -440,10 +535,34 @@ extern "C" size_t mvml_gemm_workspace_size(int64_t M, int64_t N, int64_t K) {
   return S > 1 ? carve_size((size_t)S * M * N * sizeof(float)) : 0;
 }
 
+namespace {
+int gemm_launch(bool x3, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
+                float beta, int act, float* C, int64_t ldc, void* workspace,
+                size_t workspace_bytes, void* stream);
+}
+
 extern "C" int mvml_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                              const float* A, int64_t lda, const float* B, int64_t ldb,
                              const float* bias, float beta, int act, float* C, int64_t ldc,
                              void* workspace, size_t workspace_bytes, void* stream) {
+  return gemm_launch(false, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
+                     workspace, workspace_bytes, stream);
+}
+
+extern "C" int mvml_gemm_f32x3(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                               const float* A, int64_t lda, const float* B, int64_t ldb,
+                               const float* bias, float beta, int act, float* C, int64_t ldc,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+  return gemm_launch(true, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
+                     workspace, workspace_bytes, stream);
+}
+
+namespace {
+int gemm_launch(bool x3, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
+                float beta, int act, float* C, int64_t ldc, void* workspace,
+                size_t workspace_bytes, void* stream) {
   clear_error();
   MVML_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
   if (M == 0 || N == 0) return MVML_OK;
@@ -467,9 +586,15 @@ extern "C" int mvml_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, i
   const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0);
   const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0);
   dim3 grid((unsigned)tiles, (unsigned)S);
-#define MVML_GEMM_LAUNCH(AKV, BKV)                                                         \
-  gemm_f32_kernel<AKV, BKV><<<grid, kThreads, 0, st>>>(M, N, K, A, lda, B, ldb, bias, beta, \
-                                                       act, C, ldc, kc, slab, av, bv)
+#define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
+  do {                                                                                          \
+    if (x3)                                                                                     \
+      gemm_f32_kernel<AKV, BKV, -1, true><<<grid, kThreads, 0, st>>>(                           \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+    else                                                                                        \
+      gemm_f32_kernel<AKV, BKV><<<grid, kThreads, 0, st>>>(M, N, K, A, lda, B, ldb, bias, beta, \
+                                                           act, C, ldc, kc, slab, av, bv);      \
+  } while (0)
   if (!a_kmajor && !b_kmajor) MVML_GEMM_LAUNCH(false, false);
   else if (!a_kmajor && b_kmajor) MVML_GEMM_LAUNCH(false, true);
   else if (a_kmajor && !b_kmajor) MVML_GEMM_LAUNCH(true, false);
@@ -485,13 +610,14 @@ extern "C" int mvml_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, i
   }
   return rc;
 }
+}  // namespace
 
 namespace mvml {
 // Projection GEMM with the logits-partial epilogue: C[M,N] = A[M,K] B[N,K]^T (both
 // K-contiguous, no split-K: K is the small feature dimension), part as in ProjEpi.
-int gemm_proj_epi(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
-                  int64_t ldb, float* C, int64_t ldc, const float* vec, int cols, int logw,
-                  float* part, hipStream_t st) {
+int gemm_proj_epi(bool x3, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                  const float* B, int64_t ldb, float* C, int64_t ldc, const float* vec, int cols,
+                  int logw, float* part, hipStream_t st) {
   const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
   MVML_REQUIRE(tiles < (int64_t(1) << 31), "gat_proj_fwd: too many tiles");
   MVML_REQUIRE(cols <= N && (logw >= 2 && logw <= 5), "gat_proj_fwd: bad partial width");
@@ -499,9 +625,16 @@ int gemm_proj_epi(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, 
   const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0);
   dim3 grid((unsigned)tiles, 1);
 #define MVML_PROJ(LW)                                                                          \
-  gemm_f32_kernel<false, false, LW><<<grid, kThreads, 0, st>>>(                                \
-      M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,        \
-      ProjEpi{vec, cols, part})
+  do {                                                                                         \
+    if (x3)                                                                                    \
+      gemm_f32_kernel<false, false, LW, true><<<grid, kThreads, 0, st>>>(                      \
+          M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
+          ProjEpi{vec, cols, part});                                                           \
+    else                                                                                       \
+      gemm_f32_kernel<false, false, LW><<<grid, kThreads, 0, st>>>(                            \
+          M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
+          ProjEpi{vec, cols, part});                                                           \
+  } while (0)
   switch (logw) {
     case 5: MVML_PROJ(5); break;
     case 4: MVML_PROJ(4); break;

@@ -25,7 +25,8 @@ _CTYPE = {
 
 def _strip_comments(text):
     text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
-    return re.sub(r"//[^\n]*", " ", text)
+    text = re.sub(r"//[^\n]*", " ", text)
+    return re.sub(r"^\s*#[^\n]*", " ", text, flags=re.M)  # preprocessor lines
 
 
 def parse_header(path=HEADER_PATH):

@@ -5,6 +5,7 @@ no PyTorch math on the hot path besides allocation (and nn.Dropout, which the re
 applies with torch's own RNG, model.py:87).
 """
 import ctypes
+import os
 
 import torch
 
@@ -56,15 +57,22 @@ def agg_bwd_bytes(N, E, H, F, gout_cols, mode):
     return 4 * (reads + idx + writes)
 
 
-def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0):
-    """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32)."""
+# GEMM algorithm for every dense product of the view: "x3" = split-bf16 MFMA at fp32 accuracy
+# (mvml_gemm_f32x3, the default), "f32" = f32-input MFMA (mvml_gemm_f32).  Both are parity-
+# tested against fp64 at the fp32 bar; override with MVML_GEMM_ALGO=f32.
+GEMM_ALGO = os.environ.get("MVML_GEMM_ALGO", "x3")
+_GEMM_ENTRY = {"f32": ("mvml_gemm_f32", 0), "x3": ("mvml_gemm_f32x3", 1)}
+
+
+def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0, algo=None):
+    """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32 / mvml_gemm_f32x3)."""
     _lib.call_tag[0] = {"flops": 2 * M * N * K}
     L = _lib.lib()
     dev = C.device
     wsz = L.mvml_gemm_workspace_size(M, N, K)
     wp, wn = _lib.ws_ptr_size(wsz, dev)
-    call("mvml_gemm_f32", int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda, ptr(B), ldb,
-         ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
+    call(_GEMM_ENTRY[algo or GEMM_ALGO][0], int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda,
+         ptr(B), ldb, ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
 
 
 def colsum(X, M, N, ldx, out, beta=0.0, offset=0, alpha=1.0):
@@ -108,7 +116,7 @@ class GATLayerFunction(torch.autograd.Function):
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_proj_fwd_workspace_size(N, H, F), dev)
         _lib.call_tag[0] = {"flops": 2 * N * C * Fp}
         call("mvml_gat_proj_fwd", N, ptr(Xp), Fp, Fp, ptr(Wcat), Fp, ptr(attn_lr), H, F, mean_res,
-             ptr(Y), ldy, ptr(elr), wp, wn, st)
+             _GEMM_ENTRY[GEMM_ALGO][1], ptr(Y), ldy, ptr(elr), wp, wn, st)
         out_cols = F if mode == MODE_MEAN else HF
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()

@@ -41,11 +41,13 @@ def main():
         Bm = torch.randn((K, N) if bk else (N, K), device=dev)
         C = torch.empty((M, N), device=dev)
         flops = 2 * M * N * K
-        ms, t = tf(lambda: gemm(A, Bm, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N), flops)
+        ms, t = tf(lambda: gemm(A, Bm, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N, algo="f32"), flops)
+        ms3, t3 = tf(lambda: gemm(A, Bm, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N, algo="x3"), flops)
         At = A.t() if ak else A
         Bt = Bm if bk else Bm.t()
         ms2, t2 = tf(lambda: torch.matmul(At, Bt, out=C), flops)
-        print(f"{name:22s} M={M:8d} N={N:5d} K={K:8d}  mvml {ms:8.3f} ms {t:6.1f} TF/s | torch {ms2:8.3f} ms {t2:6.1f} TF/s", flush=True)
+        print(f"{name:22s} M={M:8d} N={N:5d} K={K:8d}  f32 {ms:8.3f} ms {t:6.1f} TF/s | x3 {ms3:8.3f} ms "
+              f"{t3:6.1f} TF/s | torch {ms2:8.3f} ms {t2:6.1f} TF/s", flush=True)
         del A, Bm, C
         torch.cuda.empty_cache()
 

@@ -9,7 +9,7 @@ import torch  # noqa: E402
 
 from mvml_gat import _lib  # noqa: E402
 from mvml_gat._lib import call, ptr  # noqa: E402
-from mvml_gat.functional import gemm  # noqa: E402
+from mvml_gat.functional import _GEMM_ENTRY, gemm  # noqa: E402
 
 
 def timeit(fn, it=5):
@@ -39,11 +39,12 @@ def main():
         wsz = L.mvml_gat_proj_fwd_workspace_size(N, H, F)
         ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
         fl = 2 * N * C * K
-        t0 = timeit(lambda: gemm(X, W, N, C, K, 0, 0, K, K, Y, ldy))
-        t1 = timeit(lambda: call("mvml_gat_proj_fwd", N, ptr(X), K, K, ptr(W), K, ptr(attn), H, F, mean,
-                                 ptr(Y), ldy, ptr(elr), ptr(ws), wsz, st))
-        print(f"H{H} F{F} K{K}: gemm {t0:8.3f} ms ({fl / t0 / 1e9:6.1f} TF/s)   proj_fwd {t1:8.3f} ms "
-              f"({fl / t1 / 1e9:6.1f} TF/s)")
+        for algo in ("f32", "x3"):
+            t0 = timeit(lambda: gemm(X, W, N, C, K, 0, 0, K, K, Y, ldy, algo=algo))
+            t1 = timeit(lambda: call("mvml_gat_proj_fwd", N, ptr(X), K, K, ptr(W), K, ptr(attn), H, F,
+                                     mean, _GEMM_ENTRY[algo][1], ptr(Y), ldy, ptr(elr), ptr(ws), wsz, st))
+            print(f"H{H} F{F} K{K} {algo}: gemm {t0:8.3f} ms ({fl / t0 / 1e9:6.1f} TF/s)   proj_fwd "
+                  f"{t1:8.3f} ms ({fl / t1 / 1e9:6.1f} TF/s)")
 
 
 if __name__ == "__main__":
