@@ -32,15 +32,38 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// fp32 x 8 -> three bf16 x 8 terms (round-to-nearest each; the residuals are exact in fp32).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Two fp32 -> packed bf16 pair (v_cvt_pk_bf16_f32, round-to-nearest-even) and the two exact
+// fp32 residuals x - bf16(x), unpacked with one shift / one mask: 5 VALU per pair.
+__device__ __forceinline__ uint32_t split_pair(float& a, float& b) {
+  const f32x2 v = {a, b};
+  const uint32_t p = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+  a -= __builtin_bit_cast(float, p << 16);
+  b -= __builtin_bit_cast(float, p & 0xffff0000u);
+  return p;
+}
+
+// fp32 x 8 -> three bf16 x 8 terms (round-to-nearest each; the residuals are exact in fp32):
+// 11 VALU per pair of values.
 __device__ __forceinline__ void split3(const float4& lo, const float4& hi, bf16x8& p0, bf16x8& p1,
                                        bf16x8& p2) {
-  const f32x8 x = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-  p0 = __builtin_convertvector(x, bf16x8);
-  const f32x8 r = x - __builtin_convertvector(p0, f32x8);
-  p1 = __builtin_convertvector(r, bf16x8);
-  const f32x8 r2 = r - __builtin_convertvector(p1, f32x8);
-  p2 = __builtin_convertvector(r2, bf16x8);
+  float x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  u32x4 q0, q1, q2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q0[i] = split_pair(x[2 * i], x[2 * i + 1]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q1[i] = split_pair(x[2 * i], x[2 * i + 1]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 v = {x[2 * i], x[2 * i + 1]};
+    q2[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+  }
+  p0 = __builtin_bit_cast(bf16x8, q0);
+  p1 = __builtin_bit_cast(bf16x8, q1);
+  p2 = __builtin_bit_cast(bf16x8, q2);
 }
 
 // acc += (a0 + a1 + a2)(b0 + b1 + b2) to fp32 accuracy: the six significant cross terms.
@@ -235,6 +258,83 @@ struct ProjEpi {
   float* part;       // [cols / W][2][M]: a wave's stores for one (group, side) are 32 rows, contiguous
 };
 
+// Epilogue of a 128x128 tile held as 2x2 32x32 accumulators per wave (wave (wm, wn) owns rows
+// m0 + 64 wm .., columns n0 + 64 wn ..): optional GAT logit partials, then bias / beta*C /
+// ReLU, or the raw split-K slab.
+template <int EPI_LOGW>
+__device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[2][2], int64_t M, int64_t N,
+                                              int64_t m0, int64_t n0, int wm, int wn, int lane,
+                                              const float* __restrict__ bias, float beta, int act,
+                                              float* __restrict__ C, int64_t ldc,
+                                              float* __restrict__ slab, const ProjEpi& epi) {
+  const int li = lane & 31, lk = lane >> 5;
+  // Epilogue. C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  if constexpr (EPI_LOGW >= 0) {
+    constexpr int W = 1 << EPI_LOGW, NV = 32 >> EPI_LOGW;
+  #pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t cb0 = n0 + wn * 64 + j * 32;  // first column of this 32-column block
+        if (cb0 >= epi.cols) continue;             // wave-uniform
+        const int64_t c = cb0 + li;
+        const float al = c < epi.cols ? epi.vec[c] : 0.f;
+        const float ar = c < epi.cols ? epi.vec[epi.cols + c] : 0.f;
+        float v[32];  // [side][row register]
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { v[r] = acc[i][j][r] * al; v[16 + r] = acc[i][j][r] * ar; }
+#pragma unroll
+        for (int st = 0; st < EPI_LOGW; ++st) {
+          const int half = 16 >> st, mask = (W / 2) >> st;
+          const bool hi = (lane & mask) != 0;
+#pragma unroll
+          for (int t = 0; t < half; ++t) {
+            // the empty asm pins both values in registers first: otherwise the selects fold
+            // into a dynamically indexed v[], lowered as a 32-way compare chain
+            float lo = v[t], up = v[t + half];
+            asm volatile("" : "+v"(lo), "+v"(up));
+            const float keep = hi ? up : lo;
+            const float send = hi ? lo : up;
+            v[t] = keep + __shfl_xor(send, mask, 64);
+          }
+        }
+        const int64_t gc = cb0 + (li & ~(W - 1));  // first column of the lane's group
+        if (gc < epi.cols) {
+#pragma unroll
+          for (int t = 0; t < NV; ++t) {
+            const int idx = ((li & (W - 1)) << (5 - EPI_LOGW)) | t;
+            const int side = idx >> 4, r = idx & 15;
+            const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+            if (row < M) epi.part[((gc / W) * 2 + side) * M + row] = v[t];
+          }
+        }
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wn * 64 + j * 32 + li;
+      if (col >= N) continue;
+      const float bcol = (bias && !slab) ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (row >= M) continue;
+        float v = acc[i][j][r];
+        if (slab) {
+          slab[((int64_t)blockIdx.y * M + row) * N + col] = v;
+        } else {
+          v += bcol;
+          float* cp = C + row * ldc + col;
+          if (beta != 0.f) v += beta * (*cp);
+          if (act == 1) v = fmaxf(v, 0.f);
+          *cp = v;
+        }
+      }
+    }
+}
+
 template <bool AK, bool BKM, int EPI_LOGW = -1, bool X3 = false>
 __global__ void __launch_bounds__(kThreads, 2)
 gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
@@ -381,71 +481,176 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     }
   }
 
-  // Epilogue. C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-  if constexpr (EPI_LOGW >= 0) {
-    constexpr int W = 1 << EPI_LOGW, NV = 32 >> EPI_LOGW;
-  #pragma unroll
-    for (int i = 0; i < 2; ++i)
+  tile_epilogue<EPI_LOGW>(acc, M, N, m0, n0, wm, wn, lane, bias, beta, act, C, ldc, slab, epi);
+}
+
+// ---- split-bf16 GEMM with the split done once per workgroup, at staging -------------------
+// The fp32 tile is loaded into registers (one tile ahead), split into its three bf16 terms and
+// written to LDS as three bf16 planes per operand; the waves then read ready-made MFMA operand
+// fragments (ds_read_b128), so an element is split once per workgroup instead of once per wave
+// that reads it (half the VALU of splitting fragments).
+// LDS image per operand: 3 planes x 128 rows x 32 k bf16 (64-B rows); the 16-B chunk (8 k) is
+// XOR-swizzled by (row >> 2) & 3, so 8 consecutive rows read at one chunk hit 8 distinct 16-B
+// bank groups.  48 KB per workgroup, two workgroups per CU.
+constexpr int kPlaneBytes = 128 * 64;
+constexpr int kOpBytes = 3 * kPlaneBytes;
+
+__device__ __forceinline__ uint32_t plane_off(int plane, int row, int chunk) {
+  return (uint32_t)(plane * kPlaneBytes + row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4));
+}
+
+// 4 fp32 -> three bf16 x 4 terms (two dwords each).
+__device__ __forceinline__ void split4(float a, float b, float c, float d, uint2& p0, uint2& p1,
+                                       uint2& p2) {
+  p0.x = split_pair(a, b);
+  p0.y = split_pair(c, d);
+  p1.x = split_pair(a, b);
+  p1.y = split_pair(c, d);
+  const f32x2 u = {a, b}, w = {c, d};
+  p2.x = __builtin_bit_cast(uint32_t, __builtin_convertvector(u, bf16x2));
+  p2.y = __builtin_bit_cast(uint32_t, __builtin_convertvector(w, bf16x2));
+}
+
+// A thread's 16 values of a 128 x 32 operand tile.
+//  * K-contiguous ([rows][K]): row = tid >> 1, k = 16 (tid & 1) + 4 i + [0, 4) in v[i].
+//  * K-major ([K][rows]): rows 4 (tid & 31) + [0, 4) in v[i].{x,y,z,w}, k = 4 (tid >> 5) + i.
+template <bool KMAJ>
+struct SplitStager {
+  __device__ static __forceinline__ void load(const float* __restrict__ P, int64_t ld, int64_t r0,
+                                              int64_t rows, int64_t k0, int64_t kend, bool fast,
+                                              int tid, float4 (&v)[4]) {
+    if (!KMAJ) {
+      const int64_t row = r0 + (tid >> 1), kb = k0 + 16 * (tid & 1);
+      if (fast) {
+        const float* p = P + row * ld + kb;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int64_t cb0 = n0 + wn * 64 + j * 32;  // first column of this 32-column block
-        if (cb0 >= epi.cols) continue;             // wave-uniform
-        const int64_t c = cb0 + li;
-        const float al = c < epi.cols ? epi.vec[c] : 0.f;
-        const float ar = c < epi.cols ? epi.vec[epi.cols + c] : 0.f;
-        float v[32];  // [side][row register]
+        for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const float4*>(p + 4 * i);
+      } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { v[r] = acc[i][j][r] * al; v[16 + r] = acc[i][j][r] * ar; }
+        for (int i = 0; i < 4; ++i) {
+          float e[4];
 #pragma unroll
-        for (int st = 0; st < EPI_LOGW; ++st) {
-          const int half = 16 >> st, mask = (W / 2) >> st;
-          const bool hi = (lane & mask) != 0;
-#pragma unroll
-          for (int t = 0; t < half; ++t) {
-            // the empty asm pins both values in registers first: otherwise the selects fold
-            // into a dynamically indexed v[], lowered as a 32-way compare chain
-            float lo = v[t], up = v[t + half];
-            asm volatile("" : "+v"(lo), "+v"(up));
-            const float keep = hi ? up : lo;
-            const float send = hi ? lo : up;
-            v[t] = keep + __shfl_xor(send, mask, 64);
+          for (int j = 0; j < 4; ++j) {
+            const int64_t k = kb + 4 * i + j;
+            e[j] = (row < rows && k < kend) ? P[row * ld + k] : 0.f;
           }
-        }
-        const int64_t gc = cb0 + (li & ~(W - 1));  // first column of the lane's group
-        if (gc < epi.cols) {
-#pragma unroll
-          for (int t = 0; t < NV; ++t) {
-            const int idx = ((li & (W - 1)) << (5 - EPI_LOGW)) | t;
-            const int side = idx >> 4, r = idx & 15;
-            const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-            if (row < M) epi.part[((gc / W) * 2 + side) * M + row] = v[t];
-          }
+          v[i] = make_float4(e[0], e[1], e[2], e[3]);
         }
       }
-  }
+    } else {
+      const int64_t rb = r0 + 4 * (tid & 31), kb = k0 + 4 * (tid >> 5);
+      if (fast) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const float4*>(P + (kb + i) * ld + rb);
+      } else {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t col = n0 + wn * 64 + j * 32 + li;
-      if (col >= N) continue;
-      const float bcol = (bias && !slab) ? bias[col] : 0.f;
+        for (int i = 0; i < 4; ++i) {
+          float e[4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (row >= M) continue;
-        float v = acc[i][j][r];
-        if (slab) {
-          slab[((int64_t)blockIdx.y * M + row) * N + col] = v;
-        } else {
-          v += bcol;
-          float* cp = C + row * ldc + col;
-          if (beta != 0.f) v += beta * (*cp);
-          if (act == 1) v = fmaxf(v, 0.f);
-          *cp = v;
+          for (int j = 0; j < 4; ++j) {
+            const int64_t k = kb + i, r = rb + j;
+            e[j] = (r < rows && k < kend) ? P[k * ld + r] : 0.f;
+          }
+          v[i] = make_float4(e[0], e[1], e[2], e[3]);
         }
       }
     }
+  }
+
+  __device__ static __forceinline__ void split_store(uint8_t* op, int tid, const float4 (&v)[4]) {
+    if (!KMAJ) {
+      const int row = tid >> 1;
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        bf16x8 p0, p1, p2;
+        split3(v[2 * g], v[2 * g + 1], p0, p1, p2);
+        const int chunk = 2 * (tid & 1) + g;
+        *reinterpret_cast<bf16x8*>(op + plane_off(0, row, chunk)) = p0;
+        *reinterpret_cast<bf16x8*>(op + plane_off(1, row, chunk)) = p1;
+        *reinterpret_cast<bf16x8*>(op + plane_off(2, row, chunk)) = p2;
+      }
+    } else {
+      const int rb = 4 * (tid & 31), kk = 4 * (tid >> 5);
+      const int chunk = kk >> 3, half = (kk >> 2) & 1;
+      const float* f = reinterpret_cast<const float*>(v);  // f[4 i + j]: k = kk + i, row rb + j
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint2 p0, p1, p2;
+        split4(f[j], f[4 + j], f[8 + j], f[12 + j], p0, p1, p2);
+        const int row = rb + j;
+        *reinterpret_cast<uint2*>(op + plane_off(0, row, chunk) + 8 * half) = p0;
+        *reinterpret_cast<uint2*>(op + plane_off(1, row, chunk) + 8 * half) = p1;
+        *reinterpret_cast<uint2*>(op + plane_off(2, row, chunk) + 8 * half) = p2;
+      }
+    }
+  }
+};
+
+#ifndef MVML_X3S_WAVES
+#define MVML_X3S_WAVES 2
+#endif
+template <bool AK, bool BKM, int EPI_LOGW = -1>
+__global__ void __launch_bounds__(kThreads, MVML_X3S_WAVES)  // 2 workgroups per CU
+gemm_x3s_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
+                const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
+                float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
+                float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{}) {
+  using SA = SplitStager<AK>;
+  using SB = SplitStager<BKM>;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kOpBytes];
+  const int64_t tiles_n = ceil_div(N, BN);
+  const int64_t tile = xcd_block(blockIdx.x, gridDim.x);
+  const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  const int64_t kbeg = (int64_t)blockIdx.y * k_split;
+  const int64_t kend = min(K, kbeg + k_split);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int li = lane & 31, lk = lane >> 5;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int64_t ntiles = (kend > kbeg) ? ceil_div(kend - kbeg, BKT) : 0;
+  // unguarded 16-B loads when the whole tile is in range and rows are 16-B aligned
+  const bool a_in = a_vec && (AK ? m0 + BM <= M : m0 + BM <= M);
+  const bool b_in = b_vec && (BKM ? n0 + BN <= N : n0 + BN <= N);
+  float4 va[4], vb[4];
+  auto load_tile = [&](int64_t k0) {
+    const bool kin = k0 + BKT <= kend;
+    SA::load(A, lda, m0, M, k0, kend, a_in && kin, tid, va);
+    SB::load(B, ldb, n0, N, k0, kend, b_in && kin, tid, vb);
+  };
+  if (ntiles > 0) load_tile(kbeg);
+  const int ra0 = wm * 64 + li, ra1 = ra0 + 32, rb0 = wn * 64 + li, rb1 = rb0 + 32;
+  for (int64_t t = 0; t < ntiles; ++t) {
+    if (t > 0) __syncthreads();  // every wave is done reading the previous tile
+    SA::split_store(lds, tid, va);
+    SB::split_store(lds + kOpBytes, tid, vb);
+    __syncthreads();
+    if (t + 1 < ntiles) load_tile(kbeg + (t + 1) * BKT);  // in flight under the MFMAs
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int chunk = 2 * st + lk;
+      bf16x8 pa[2][3], pb[2][3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        pa[0][p] = *reinterpret_cast<const bf16x8*>(lds + plane_off(p, ra0, chunk));
+        pa[1][p] = *reinterpret_cast<const bf16x8*>(lds + plane_off(p, ra1, chunk));
+        pb[0][p] = *reinterpret_cast<const bf16x8*>(lds + kOpBytes + plane_off(p, rb0, chunk));
+        pb[1][p] = *reinterpret_cast<const bf16x8*>(lds + kOpBytes + plane_off(p, rb1, chunk));
+      }
+      acc[0][0] = mfma_x3(pa[0], pb[0], acc[0][0]);
+      acc[0][1] = mfma_x3(pa[0], pb[1], acc[0][1]);
+      acc[1][0] = mfma_x3(pa[1], pb[0], acc[1][0]);
+      acc[1][1] = mfma_x3(pa[1], pb[1], acc[1][1]);
+    }
+  }
+  tile_epilogue<EPI_LOGW>(acc, M, N, m0, n0, wm, wn, lane, bias, beta, act, C, ldc, slab, epi);
 }
 
 // Sum S split-K slabs in fixed order: C = act(sum_z slab[z] + bias + beta*C).
@@ -588,8 +793,11 @@ int gemm_launch(bool x3, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
   dim3 grid((unsigned)tiles, (unsigned)S);
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
   do {                                                                                          \
-    if (x3)                                                                                     \
+    if (x3 && AKV && BKV) /* both k-major (weight gradients): fragment split measured faster */ \
       gemm_f32_kernel<AKV, BKV, -1, true><<<grid, kThreads, 0, st>>>(                           \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+    else if (x3)                                                                                \
+      gemm_x3s_kernel<AKV, BKV><<<grid, kThreads, 0, st>>>(                                     \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
     else                                                                                        \
       gemm_f32_kernel<AKV, BKV><<<grid, kThreads, 0, st>>>(M, N, K, A, lda, B, ldb, bias, beta, \
@@ -627,7 +835,7 @@ int gemm_proj_epi(bool x3, int64_t M, int64_t N, int64_t K, const float* A, int6
 #define MVML_PROJ(LW)                                                                          \
   do {                                                                                         \
     if (x3)                                                                                    \
-      gemm_f32_kernel<false, false, LW, true><<<grid, kThreads, 0, st>>>(                      \
+      gemm_x3s_kernel<false, false, LW><<<grid, kThreads, 0, st>>>(                            \
           M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
           ProjEpi{vec, cols, part});                                                           \
     else                                                                                       \
