@@ -1,10 +1,12 @@
 """Turn rocprofv3 PMC counter CSVs (FETCH_SIZE pass + WRITE_SIZE pass) into HBM traffic per
-launch for the kernels bench.py reports, written to profiles/pmc_traffic.json.
+launch of the C-ABI entry points bench.py reports, written to profiles/pmc_traffic.json.
 
 Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE (KB) reports exactly half
 of the bytes of wide (16 B/lane) coalesced reads, so hbm_read = 2 * FETCH_SIZE * 1024;
-WRITE_SIZE (KB) is exact for 16-B stores.  Narrower accesses are uncalibrated, so the result
-is an upper-bound-ish estimate for kernels that mix 4-B gathers in (documented in DESIGN.md).
+WRITE_SIZE (KB) is exact for 16-B stores.  The aggregation kernels read their streams with
+16-B buffer loads; their small 4-B index / logit reads are uncalibrated (documented in
+DESIGN.md).  One entry-point launch = one launch of each of its kernels, so its traffic is the
+sum of the per-kernel averages.
 
     python tools/pmc_traffic.py FETCH_DIR WRITE_DIR [--out profiles/pmc_traffic.json]
 """
@@ -15,9 +17,11 @@ import json
 import os
 from collections import defaultdict
 
-KERNELS = {"gat_agg_fwd": "gat_agg_fwd_kernel", "gat_agg_bwd_dst": "gat_agg_bwd_dst_kernel",
-           "gat_agg_bwd_src": "gat_agg_bwd_src_kernel", "gemm": "gemm_f32_kernel",
-           "set2set_seg_fwd": "seg_fwd_kernel"}
+ENTRIES = {  # C-ABI entry point -> its kernels (name substrings)
+    "gat_agg_fwd": ["gat_softmax_kernel", "gat_agg_fwd_lds_kernel", "gat_agg_fwd_gather_kernel"],
+    "gat_agg_bwd": ["gat_agg_bwd_dst_kernel", "gat_agg_bwd_src_kernel"],
+    "set2set_seg_fwd": ["seg_fwd_kernel"],
+}
 
 
 def read_counter(d, counter):
@@ -28,9 +32,10 @@ def read_counter(d, counter):
                 if row.get("Counter_Name") != counter:
                     continue
                 name = row.get("Kernel_Name", "")
-                for key, pat in KERNELS.items():
-                    if pat in name:
-                        per[key].append(float(row["Counter_Value"]))
+                for entry, pats in ENTRIES.items():
+                    for pat in pats:
+                        if pat in name:
+                            per[(entry, pat)].append(float(row["Counter_Value"]))
     return per
 
 
@@ -43,15 +48,19 @@ def main():
     fetch = read_counter(a.fetch_dir, "FETCH_SIZE")
     write = read_counter(a.write_dir, "WRITE_SIZE")
     out = {}
-    for key in KERNELS:
-        if not fetch.get(key) or not write.get(key):
+    for entry, pats in ENTRIES.items():
+        f_kb = sum(sum(fetch[(entry, p)]) / len(fetch[(entry, p)]) for p in pats if fetch.get((entry, p)))
+        w_kb = sum(sum(write[(entry, p)]) / len(write[(entry, p)]) for p in pats if write.get((entry, p)))
+        if not f_kb:
             continue
-        f_kb = sum(fetch[key]) / len(fetch[key])
-        w_kb = sum(write[key]) / len(write[key])
-        out[key] = {"launches": len(fetch[key]), "fetch_size_kb": round(f_kb, 1),
-                    "write_size_kb": round(w_kb, 1),
-                    "hbm_bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024),
-                    "correction": "read = 2 x FETCH_SIZE (gfx950 16-B/lane reads), write = WRITE_SIZE"}
+        out[entry] = {"kernels": {p: {"launches": len(fetch.get((entry, p), [])),
+                                      "fetch_size_kb": round(sum(fetch[(entry, p)]) / len(fetch[(entry, p)]), 1)
+                                      if fetch.get((entry, p)) else None,
+                                      "write_size_kb": round(sum(write[(entry, p)]) / len(write[(entry, p)]), 1)
+                                      if write.get((entry, p)) else None} for p in pats},
+                      "hbm_bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024),
+                      "correction": "read = 2 x FETCH_SIZE (gfx950 16-B/lane reads), write = WRITE_SIZE; "
+                                    "averaged over both GAT layers"}
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
