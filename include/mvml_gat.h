@@ -113,14 +113,21 @@ int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx, float alp
  *   Y row = [ Z (H*F) | R (H*F or F) ];  C = mvml_gat_proj_cols(H,F,mean).
  *   Wcat has row stride ldw >= Fin; columns Fin..ldw-1 are written as zeros, so a caller can
  *   pad X to a multiple of 4 columns and keep every GEMM operand 16-B aligned.
+ * With attn_lr = [attn_l | attn_r] ([2, H*F], may be NULL) mvml_gat_fold_weights also writes
+ * 2H rows after the C projection rows, A_l[h,:] = sum_f attn_l[h,f] fc.weight[h*F+f,:] and
+ * A_r likewise: the backward multiplies mvml_gat_agg_bwd's [d el | d er] columns by them, which
+ * is exactly the el / er path of dL/dX (el = Z . attn_l = X . A_l^T).
  * mvml_gat_unfold_grads maps dL/dWcat back onto fc.weight and res_fc.weight (the mean
- * residual's gradient is replicated / H over the heads).
+ * residual's gradient is replicated / H over the heads); with attn_lr it adds the el / er
+ * path of dL/dfc.weight from dL/dWcat's extra rows: attn_l[h,f] * G_l[h,:] + attn_r[h,f] *
+ * G_r[h,:], G = [d el | d er]^T X.
  * ------------------------------------------------------------------------------------- */
 int mvml_gat_proj_cols(int H, int F, int mean_residual);
-int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, int H, int F, int Fin,
-                          int ldw, int mean_residual, float* Wcat, void* stream);
-int mvml_gat_unfold_grads(const float* gWcat, int H, int F, int Fin, int ldg, int mean_residual,
-                          float* g_fc_w, float* g_res_fc_w, void* stream);
+int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_lr, int H,
+                          int F, int Fin, int ldw, int mean_residual, float* Wcat, void* stream);
+int mvml_gat_unfold_grads(const float* gWcat, const float* attn_lr, int H, int F, int Fin,
+                          int ldg, int mean_residual, float* g_fc_w, float* g_res_fc_w,
+                          void* stream);
 /* The projection GEMM (X [N, K] with row stride ldx, Wcat [C, K] with row stride ldw, K = the
  * padded feature count) + GATConv's attention logits from the result:
  *   el[n,h] = <Z[n,h,:], attn_l[h,:]>,  er[n,h] = <Z[n,h,:], attn_r[h,:]>
@@ -134,11 +141,12 @@ int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx, int64_t K,
                       int mean_residual, int algo /* MVML_GEMM_* */, float* Y, int64_t ldy,
                       float* elr, void* workspace, size_t workspace_bytes, void* stream);
 /* dL/dattn_l[h,f] = sum_n gelr[n, h] * Z[n, h*F+f] and dL/dattn_r with gelr[n, H+h] (autograd
- * of `(feat * attn_l).sum(-1)` in GATConv.forward); deterministic two-stage reduction. */
+ * of `(feat * attn_l).sum(-1)` in GATConv.forward); gelr rows [d el | d er] have stride ldgl
+ * (the backward's gY + C, ldgy); deterministic two-stage reduction. */
 size_t mvml_gat_attn_grad_workspace_size(int64_t num_nodes, int H, int F);
 int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, const float* Y, int64_t ldy,
-                       const float* gelr, float* g_attn_l, float* g_attn_r, void* workspace,
-                       size_t workspace_bytes, void* stream);
+                       const float* gelr, int64_t ldgl, float* g_attn_l, float* g_attn_r,
+                       void* workspace, size_t workspace_bytes, void* stream);
 /* ---------------------------------------------------------------------------------------
  * Fused GAT attention + aggregation, forward (one workgroup per node group; replaces dgl
  * GATConv.forward from apply_edges to the residual/bias, plus dgllife GATLayer's flatten/ELU
@@ -155,18 +163,22 @@ int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_
                      int H, int F, const float* elr, const float* bias, float slope, int mode,
                      float* out, float* attn, void* stream);
 /* Backward of mvml_gat_agg_fwd (DGL GSpMM / GSDDMM / EdgeSoftmax backward + torch autograd of
- * el/er, residual, bias, ELU, mean).  Atomic-free: the u_mul_e-sum transpose is a gather over
- * the out-CSR.  Writes gY[N, ldgy] = [dZ | dR] (the GEMM backward's input, same column layout
- * as Y) and gelr[N, 2H] = [d el | d er] (input of mvml_gat_attn_grad).
+ * residual, bias, ELU, mean).  Atomic-free: the u_mul_e-sum transpose is a gather over the
+ * out-CSR; one workgroup per node group reads Z, g_out and writes dZ once (molecule groups).
+ * Writes gY[N, ldgy] (ldgy >= C + 2H, C = mvml_gat_proj_cols) =
+ *   [ dZ_agg (H*F) | dR (H*F or F) | d el (H) | d er (H) ]
+ * where dZ_agg is dL/dZ through update_all(u_mul_e, sum) only: the el / er paths of dL/dZ
+ * (d el x attn_l + d er x attn_r) reach dL/dX and dL/dfc.weight through the 2H extra columns
+ * (GEMM against mvml_gat_fold_weights' A rows; mvml_gat_unfold_grads), and dL/dattn through
+ * mvml_gat_attn_grad(gelr = gY + C, ldgl = ldgy).
  * out is the forward output (mode 0 uses ELU'(x) = out + 1 for x <= 0).  workspace: [E, H]. */
 size_t mvml_gat_agg_bwd_workspace_size(int64_t num_edges, int H);
-int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
-                     const int32_t* out_rowptr, const int32_t* out_dst,
-                     const int32_t* out_inslot, const float* Y, int64_t ldy, const float* elr,
-                     const float* attn, const float* attn_l, const float* attn_r,
-                     const float* out, const float* g_out, int H, int F, float slope, int mode,
-                     float* gY, int64_t ldgy, float* gelr, void* workspace,
-                     size_t workspace_bytes, void* stream);
+int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
+                     const int32_t* in_rowptr, const int32_t* in_src, const int32_t* out_rowptr,
+                     const int32_t* out_dst, const int32_t* out_inslot, const float* Y,
+                     int64_t ldy, const float* elr, const float* attn, const float* out,
+                     const float* g_out, int H, int F, float slope, int mode, float* gY,
+                     int64_t ldgy, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Set2Set (dgl 0.9.1, model.py:82-84, 92) building blocks.

@@ -482,18 +482,224 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ groups, const int32_t* __r
 }
 
 // --------------------------------------------------------------------------------- backward
+// Backward contract (mvml_gat_agg_bwd): gY[n] = [dZ_agg | dR | d el | d er] where dZ_agg is
+// dL/dZ through update_all(u_mul_e, sum) only; the el / er paths of dL/dZ (d el x attn_l +
+// d er x attn_r) are NOT added to it: the projection backward takes them exactly through two
+// extra GEMM rows / columns (A_l = attn_l . W_fc, see mvml_gat_fold_attn_rows), which keeps
+// the backward to ONE pass over Z and dZ.
+//
+// The molecule case (group of <= kWinL atoms and <= kECap in-edges) is one workgroup per node
+// group: the group's CSR, out-CSR and attention are staged in LDS, then the columns are swept
+// CW at a time with Z and g_rst (= dL/d rst from g_out, ELU' or 1/H) staged in LDS:
+//   * thread per in-edge e: g_a[e,h] += <Z[src_e], g_rst[dst_e]> over the chunk's columns;
+//   * CW/4 lanes per source atom u: dZ_agg[u] = sum over u's out-edges of a_e g_rst[dst_e];
+//   * dR (g_rst, or g_out for the head-mean residual) is written from the staged rows;
+// then the softmax backward runs in LDS (g_s = a (g_a - sum a g_a), g_pre = g_s leaky') and
+// d er / d el are its per-destination / per-source sums.  Z, g_out and dZ cross HBM once.
+// Every other group (large molecules, edge-heavy hubs) takes the per-atom dst / src pair.
+__device__ __forceinline__ bool bwd_lds_group(int a0, int a1, const int32_t* __restrict__ rowptr) {
+  return a1 > a0 && a1 - a0 <= kWinL && rowptr[a1] - rowptr[a0] <= kECap;
+}
+
+template <int H, int MODE>
+__global__ void __launch_bounds__(kAggThreads, 4)  // 2 workgroups (16 waves) per CU
+gat_agg_bwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __restrict__ rowptr,
+                       const int32_t* __restrict__ in_src, const int32_t* __restrict__ out_rowptr,
+                       const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
+                       const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ elr,
+                       const float* __restrict__ attn, const float* __restrict__ out,
+                       const float* __restrict__ g_out, float slope, float* __restrict__ gY,
+                       int64_t ldgy, int C) {
+  constexpr int CW = 32, LPD = CW / 4, DPP = kAggThreads / LPD, NP = (kWinL + DPP - 1) / DPP;
+  __shared__ float4 zs[kWinL * LPD];  // Z chunk of the group's rows
+  __shared__ float4 gs[kWinL * LPD];  // g_rst chunk
+  __shared__ float s_att[(kECap + 1) * H];  // + H zeros: the attention of a missing edge
+  __shared__ float s_ga[kECap * H];
+  __shared__ int s_src[kECap], s_dst[kECap], s_odst[kECap], s_oslot[kECap];
+  __shared__ int s_rp[kWinL + 1], s_orp[kWinL + 1];
+  __shared__ float s_elr[kWinL * 2 * H];
+  const int a0 = groups[blockIdx.x], a1 = groups[blockIdx.x + 1];
+  if (!bwd_lds_group(a0, a1, rowptr)) return;
+  const int tid = threadIdx.x, ds = tid / LPD, q = tid % LPD;
+  const int nr = a1 - a0, HF = H * F, nfc = F / CW, nch = H * nfc;
+  const int ocols = MODE == 1 ? F : HF;
+  const int e0 = rowptr[a0], ne = rowptr[a1] - e0;  // = the group's out-edge range too
+  for (int i = tid; i <= nr; i += kAggThreads) {
+    s_rp[i] = rowptr[a0 + i] - e0;
+    s_orp[i] = out_rowptr[a0 + i] - e0;
+  }
+  for (int i = tid; i < ne; i += kAggThreads) {
+    s_src[i] = in_src[e0 + i] - a0;
+    s_odst[i] = out_dst[e0 + i] - a0;
+    s_oslot[i] = out_inslot[e0 + i] - e0;
+  }
+  for (int i = tid; i < ne * H; i += kAggThreads) s_att[i] = attn[(int64_t)e0 * H + i];
+  if (tid < H) s_att[kECap * H + tid] = 0.f;
+  for (int i = tid; i < nr * 2 * H; i += kAggThreads) s_elr[i] = elr[(int64_t)a0 * 2 * H + i];
+  __syncthreads();
+  for (int d = tid; d < nr; d += kAggThreads)
+    for (int e = s_rp[d]; e < s_rp[d + 1]; ++e) s_dst[e] = d;
+  const int ldyi = (int)ldy, ldgi = (int)ldgy;
+  const __amdgpu_buffer_rsrc_t rY = make_rsrc(Y + (int64_t)a0 * ldy, (uint32_t)(nr * ldyi) * 4u);
+  const __amdgpu_buffer_rsrc_t rG = make_rsrc(gY + (int64_t)a0 * ldgy, (uint32_t)(nr * ldgi) * 4u);
+  const __amdgpu_buffer_rsrc_t rGo = make_rsrc(g_out + (int64_t)a0 * ocols, (uint32_t)(nr * ocols) * 4u);
+  const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)a0 * HF, MODE == 0 ? (uint32_t)(nr * HF) * 4u : 0u);
+
+  auto head_of = [&](int k) { return MODE == 1 ? k % H : k / nfc; };
+  auto fch_of = [&](int k) { return MODE == 1 ? k / H : k % nfc; };
+  // chunk k's rows of this thread: Z and g_out (and out for ELU')
+  float4 zr[NP], gr[NP], orr[NP];
+  auto load = [&](int k) {
+    const int col = head_of(k) * F + fch_of(k) * CW + 4 * q;
+    const int gcol = MODE == 1 ? fch_of(k) * CW + 4 * q : col;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int r = ds + DPP * j;
+      if (r < nr) {
+        zr[j] = buf_ld4(rY, 4u * (uint32_t)(r * ldyi + col));
+        gr[j] = buf_ld4(rGo, 4u * (uint32_t)(r * ocols + gcol));
+        if (MODE == 0) orr[j] = buf_ld4(rO, 4u * (uint32_t)(r * HF + col));
+      }
+    }
+  };
+  // stage chunk k: g_rst = g_out * ELU'(x) (ELU' = out + 1 for x <= 0, torch elu_backward on
+  // the result) | g_out / H (head mean) | g_out; dR = g_rst, or g_out once per f-chunk (mean)
+  auto stage = [&](int k) {
+    const int h = head_of(k), fc = fch_of(k);
+    const int col = h * F + fc * CW + 4 * q;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int r = ds + DPP * j;
+      if (r < nr) {
+        float4 g = gr[j];
+        if (MODE == 0) {
+          const float4 o = orr[j];
+          g.x *= o.x > 0.f ? 1.f : o.x + 1.f;
+          g.y *= o.y > 0.f ? 1.f : o.y + 1.f;
+          g.z *= o.z > 0.f ? 1.f : o.z + 1.f;
+          g.w *= o.w > 0.f ? 1.f : o.w + 1.f;
+        } else if (MODE == 1) {
+          const float hh = (float)H;
+          g = make_float4(g.x / hh, g.y / hh, g.z / hh, g.w / hh);
+        }
+        zs[r * LPD + q] = zr[j];
+        gs[r * LPD + q] = g;
+        if (MODE != 1) buf_st4(rG, 4u * (uint32_t)(r * ldgi + HF + col), g);
+        else if (h == 0) buf_st4(rG, 4u * (uint32_t)(r * ldgi + HF + fc * CW + 4 * q), gr[j]);
+      }
+    }
+  };
+  const bool has_e = tid < ne;
+  const int es = has_e ? s_src[tid] : 0;
+  // node role: this thread's source atoms (NP), their first kEC out-edges' g_rst row slots and
+  // attention slots in registers (a missing edge reads the atom's own row with a zero
+  // attention), so a chunk's gathers are independent LDS reads; more out-edges (hubs) loop.
+  int go[NP][kEC], ga_[NP][kEC], oend[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int u = ds + DPP * p;
+    const int ob = u < nr ? s_orp[u] : 0;
+    oend[p] = u < nr ? s_orp[u + 1] : 0;
+#pragma unroll
+    for (int i = 0; i < kEC; ++i) {
+      const bool ok = ob + i < oend[p];
+      go[p][i] = (ok ? s_odst[ob + i] : (u < nr ? u : 0)) * LPD + q;
+      ga_[p][i] = ok ? s_oslot[ob + i] * H : kECap * H;
+    }
+  }
+  float ga[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) ga[h] = 0.f;
+  load(0);
+  __syncthreads();  // s_dst
+  stage(0);
+  int ed = 0;
+  if (has_e) ed = s_dst[tid];
+  __syncthreads();
+  for (int k = 0; k < nch; ++k) {
+    const int h = head_of(k);
+    const int col = h * F + fch_of(k) * CW + 4 * q;
+    if (k + 1 < nch) load(k + 1);
+    if (has_e) {  // g_a partial of this thread's in-edge
+      float sacc = 0.f;
+#pragma unroll
+      for (int c = 0; c < LPD; ++c) sacc += dot4(zs[es * LPD + c], gs[ed * LPD + c]);
+      add_at<H>(ga, h, sacc);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {  // dZ_agg of source atom u over its out-edges
+      const int u = ds + DPP * p;
+      float4 acc = f4(0.f);
+#pragma unroll
+      for (int i = 0; i < kEC; ++i) acc = fma4(s_att[ga_[p][i] + h], gs[go[p][i]], acc);
+      if (u < nr) {
+        for (int o = s_orp[u] + kEC; o < oend[p]; ++o)
+          acc = fma4(s_att[s_oslot[o] * H + h], gs[s_odst[o] * LPD + q], acc);
+        buf_st4(rG, 4u * (uint32_t)(u * ldgi + col), acc);
+      }
+    }
+    __syncthreads();
+    if (k + 1 < nch) {
+      stage(k + 1);
+      __syncthreads();
+    }
+  }
+  if (has_e) {
+#pragma unroll
+    for (int h = 0; h < H; ++h) s_ga[tid * H + h] = ga[h];
+  }
+  __syncthreads();
+  // edge_softmax backward per (destination, head); g_pre replaces g_a in LDS
+  for (int i = tid; i < nr * H; i += kAggThreads) {
+    const int d = i / H, h = i % H;
+    const int eb = s_rp[d], ee = s_rp[d + 1];
+    const float er = s_elr[d * 2 * H + H + h];
+    float dots = 0.f;
+    for (int e = eb; e < ee; ++e) dots += s_att[e * H + h] * s_ga[e * H + h];
+    float der = 0.f;
+    for (int e = eb; e < ee; ++e) {
+      const float g_s = s_att[e * H + h] * (s_ga[e * H + h] - dots);
+      const float gp = (s_elr[s_src[e] * 2 * H + h] + er) > 0.f ? g_s : g_s * slope;
+      s_ga[e * H + h] = gp;
+      der += gp;
+    }
+    gY[(int64_t)(a0 + d) * ldgy + C + H + h] = der;
+  }
+  __syncthreads();
+  for (int i = tid; i < nr * H; i += kAggThreads) {  // d el: sums over out-edges
+    const int u = i / H, h = i % H;
+    float del = 0.f;
+    for (int o = s_orp[u]; o < s_orp[u + 1]; ++o) del += s_ga[s_oslot[o] * H + h];
+    gY[(int64_t)(a0 + u) * ldgy + C + h] = del;
+  }
+}
+
 // Pass A: one wave per destination v.
 template <int H, int VPL>
 __global__ void __launch_bounds__(kWavesPerBlock * 64)
-gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
+gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
+                       const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
                        const float* __restrict__ Y, int64_t ldy, const float* __restrict__ elr,
                        const float* __restrict__ attn, const float* __restrict__ out,
                        const float* __restrict__ g_out, int F, float slope, int mode,
                        float* __restrict__ gpre, float* __restrict__ gY, int64_t ldgy,
-                       float* __restrict__ gelr) {
+                       float* __restrict__ gelr, int64_t ldgl) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t v = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
-  if (v >= N) return;
+  // G > 0: one block per node group, skipping the groups the LDS kernel handles; G == 0: one
+  // wave per atom over all atoms
+  int64_t v, vend, vstep;
+  if (G > 0) {
+    const int a0 = groups[blockIdx.x], a1 = groups[blockIdx.x + 1];
+    if (a1 <= a0 || bwd_lds_group(a0, a1, rowptr)) return;
+    v = a0 + wid;
+    vend = a1;
+    vstep = kWavesPerBlock;
+  } else {
+    v = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
+    vend = min<int64_t>(v + 1, N);
+    vstep = 1;
+  }
+  for (; v < vend; v += vstep) {
   const int HF = H * F;
   const int beg = rowptr[v], end = rowptr[v + 1];
   const int deg = end - beg;
@@ -584,21 +790,36 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
 #pragma unroll
     for (int h = 0; h < H; ++h) ger[h] += gp[h];
   }
-  store_heads<H>(gelr + v * 2 * H + H, ger, lane);
+  store_heads<H>(gelr + v * ldgl + H, ger, lane);
+  }
 }
 
 // Pass B: one wave per source u (out-CSR gather).
 template <int H, int VPL>
 __global__ void __launch_bounds__(kWavesPerBlock * 64)
-gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
+gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
+                       const int32_t* __restrict__ rowptr, const int32_t* __restrict__ out_rowptr,
                        const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
                        const float* __restrict__ attn, const float* __restrict__ gpre,
-                       const float* __restrict__ attn_l, const float* __restrict__ attn_r,
                        const float* __restrict__ out, const float* __restrict__ g_out, int F,
-                       int mode, float* __restrict__ gY, int64_t ldgy, float* __restrict__ gelr) {
+                       int mode, float* __restrict__ gY, int64_t ldgy, float* __restrict__ gelr,
+                       int64_t ldgl) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t u = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
-  if (u >= N) return;
+  // G > 0: one block per node group, skipping the groups the LDS kernel handles; G == 0: one
+  // wave per atom over all atoms
+  int64_t u, vend, vstep;
+  if (G > 0) {
+    const int a0 = groups[blockIdx.x], a1 = groups[blockIdx.x + 1];
+    if (a1 <= a0 || bwd_lds_group(a0, a1, rowptr)) return;
+    u = a0 + wid;
+    vend = a1;
+    vstep = kWavesPerBlock;
+  } else {
+    u = xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + wid;
+    vend = min<int64_t>(u + 1, N);
+    vstep = 1;
+  }
+  for (; u < vend; u += vstep) {
   const int HF = H * F;
   const int beg = out_rowptr[u], end = out_rowptr[u + 1];
   const int deg = end - beg;
@@ -646,20 +867,14 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
         }
     }
   }
-  // + the el / er paths: Z also feeds el = <Z, attn_l> and er = <Z, attn_r>
-  float ger[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) ger[h] = gelr[u * 2 * H + H + h];
+  // dZ through the aggregation only; the el / er paths (d el x attn_l + d er x attn_r) reach
+  // the projection's gradients through the [d el | d er] columns (mvml_gat_agg_bwd contract)
   float* gyu = gY + u * ldgy;
 #pragma unroll
   for (int c = 0; c < VPL; ++c)
-    if (okc[c]) {
-      const int col = 4 * (lane + 64 * c);
-      float4 g = fma4(pick<H>(gel, hc[c]), ld4(attn_l + col), gz[c]);
-      g = fma4(pick<H>(ger, hc[c]), ld4(attn_r + col), g);
-      st4(gyu + col, g);
-    }
-  store_heads<H>(gelr + u * 2 * H, gel, lane);
+    if (okc[c]) st4(gyu + 4 * (lane + 64 * c), gz[c]);
+  store_heads<H>(gelr + u * ldgl, gel, lane);
+  }
 }
 
 template <int H>
@@ -694,18 +909,32 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
 }
 
 template <int H, int VPL>
-int launch_bwd(int64_t N, const int32_t* rp, const int32_t* src, const int32_t* orp,
-               const int32_t* odst, const int32_t* oslot, const float* Y, int64_t ldy,
-               const float* elr, const float* attn, const float* al, const float* ar,
-               const float* out, const float* g_out, int F, float slope, int mode, float* gpre,
-               float* gY, int64_t ldgy, float* gelr, hipStream_t st) {
-  const unsigned blocks = (unsigned)ceil_div(N, kWavesPerBlock);
+int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, const int32_t* src,
+               const int32_t* orp, const int32_t* odst, const int32_t* oslot, const float* Y,
+               int64_t ldy, const float* elr, const float* attn, const float* out,
+               const float* g_out, int F, float slope, int mode, float* gpre, float* gY,
+               int64_t ldgy, int C, hipStream_t st) {
+  if (F % 32 == 0 && G > 0) {  // molecule groups: one pass over Z / g_out / dZ per group
+#define MVML_BWD_LDS(M)                                                                          \
+    gat_agg_bwd_lds_kernel<H, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, rp, src, orp, odst, \
+                                                                     oslot, Y, ldy, F, elr, attn, \
+                                                                     out, g_out, slope, gY, ldgy, C)
+    if (mode == 0) MVML_BWD_LDS(0);
+    else if (mode == 1) MVML_BWD_LDS(1);
+    else MVML_BWD_LDS(2);
+#undef MVML_BWD_LDS
+    int rc = check_launch("gat_agg_bwd_lds_kernel");
+    if (rc) return rc;
+  } else {
+    G = 0;  // no LDS groups: the per-atom pair covers every atom
+  }
+  const unsigned blocks = G > 0 ? (unsigned)G : (unsigned)ceil_div(N, kWavesPerBlock);
   gat_agg_bwd_dst_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
-      N, rp, src, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, gelr);
+      N, groups, G, rp, src, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, gY + C, ldgy);
   int rc = check_launch("gat_agg_bwd_dst_kernel");
   if (rc) return rc;
   gat_agg_bwd_src_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
-      N, orp, odst, oslot, attn, gpre, al, ar, out, g_out, F, mode, gY, ldgy, gelr);
+      N, groups, G, rp, orp, odst, oslot, attn, gpre, out, g_out, F, mode, gY, ldgy, gY + C, ldgy);
   return check_launch("gat_agg_bwd_src_kernel");
 }
 
@@ -739,7 +968,7 @@ int check_shapes(int H, int F, int mode, int64_t ldy, const void* Y, const char*
 // dL/dattn_l[h,f] = sum_n d el[n,h] * Z[n,h,f] (likewise attn_r with d er), summed directly over
 // atoms as autograd does.  Stage 1: each thread owns one Z column over a chunk of atoms.
 __global__ void attn_grad_partial_kernel(int64_t N, int H, int F, const float* __restrict__ Y,
-                                         int64_t ldy, const float* __restrict__ gelr,
+                                         int64_t ldy, const float* __restrict__ gelr, int64_t ldgl,
                                          int64_t rows_per, float* __restrict__ part) {
   const int HF = H * F;
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
@@ -752,14 +981,14 @@ __global__ void attn_grad_partial_kernel(int64_t N, int H, int F, const float* _
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float z = Y[(r + j) * ldy + col];
-      const float* g = gelr + (r + j) * 2 * H;
+      const float* g = gelr + (r + j) * ldgl;
       sl[j] = fmaf(g[h], z, sl[j]);
       sr[j] = fmaf(g[H + h], z, sr[j]);
     }
   }
   for (; r < r1; ++r) {
     const float z = Y[r * ldy + col];
-    const float* g = gelr + r * 2 * H;
+    const float* g = gelr + r * ldgl;
     sl[0] = fmaf(g[h], z, sl[0]);
     sr[0] = fmaf(g[H + h], z, sr[0]);
   }
@@ -787,11 +1016,11 @@ int attn_grad_splits(int64_t N, int HF) {
 // Wcat rows: [0,HF) fc.weight | [HF,HF+RW) res_fc.weight (RW = HF) or its head mean (RW = F);
 // columns Fin..ldw-1 are zero.
 __global__ void fold_weights_kernel(const float* __restrict__ fc_w, const float* __restrict__ res_w,
-                                    int H, int F, int Fin, int ldw, int mean_res,
-                                    float* __restrict__ Wcat) {
+                                    const float* __restrict__ attn_lr, int H, int F, int Fin,
+                                    int ldw, int mean_res, float* __restrict__ Wcat) {
   const int HF = H * F;
   const int RW = mean_res ? F : HF;
-  const int64_t total = (int64_t)(HF + RW) * ldw;
+  const int64_t total = (int64_t)(HF + RW + (attn_lr ? 2 * H : 0)) * ldw;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int row = (int)(e / ldw), k = (int)(e % ldw);
@@ -800,6 +1029,12 @@ __global__ void fold_weights_kernel(const float* __restrict__ fc_w, const float*
       v = 0.f;
     } else if (row < HF) {
       v = fc_w[(int64_t)row * Fin + k];
+    } else if (row >= HF + RW) {  // A_l / A_r rows: sum_f attn[h, f] fc.weight[h F + f, k]
+      const int side = (row - HF - RW) / H, h = (row - HF - RW) % H;
+      const float* a = attn_lr + side * HF + h * F;
+      float acc = 0.f;
+      for (int f = 0; f < F; ++f) acc = fmaf(a[f], fc_w[(int64_t)(h * F + f) * Fin + k], acc);
+      v = acc;
     } else {
       const int r = row - HF;
       if (mean_res) {
@@ -814,15 +1049,25 @@ __global__ void fold_weights_kernel(const float* __restrict__ fc_w, const float*
   }
 }
 
-// dL/dfc.weight = gWcat[0:HF];  dL/dres_fc.weight[hF+f] = gWcat[HF+hF+f] or gWcat[HF+f] / H.
-__global__ void unfold_w_kernel(const float* __restrict__ gW, int H, int F, int Fin, int ldg,
-                                int mean_res, float* __restrict__ g_fc, float* __restrict__ g_res) {
+// dL/dfc.weight = gWcat[0:HF] (+ attn_l[h,f] gWcat[C+h] + attn_r[h,f] gWcat[C+H+h]: the el / er
+// paths, when the backward folded them into the GEMM);  dL/dres_fc.weight[hF+f] =
+// gWcat[HF+hF+f] or gWcat[HF+f] / H.
+__global__ void unfold_w_kernel(const float* __restrict__ gW, const float* __restrict__ attn_lr,
+                                int H, int F, int Fin, int ldg, int mean_res,
+                                float* __restrict__ g_fc, float* __restrict__ g_res) {
   const int HF = H * F;
+  const int C = HF + (mean_res ? F : HF);
   const int64_t total = (int64_t)HF * Fin;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int row = (int)(e / Fin), k = (int)(e % Fin);
-    g_fc[e] = gW[(int64_t)row * ldg + k];
+    float gf = gW[(int64_t)row * ldg + k];
+    if (attn_lr) {
+      const int h = row / F;
+      gf = fmaf(attn_lr[row], gW[(int64_t)(C + h) * ldg + k], gf);
+      gf = fmaf(attn_lr[HF + row], gW[(int64_t)(C + H + h) * ldg + k], gf);
+    }
+    g_fc[e] = gf;
     g_res[e] = mean_res ? gW[(int64_t)(HF + row % F) * ldg + k] / (float)H
                         : gW[(int64_t)(HF + row) * ldg + k];
   }
@@ -904,20 +1149,24 @@ extern "C" size_t mvml_gat_agg_bwd_workspace_size(int64_t num_edges, int H) {
   return carve_size((size_t)num_edges * H * sizeof(float));
 }
 
-extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
+extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
+                                const int32_t* in_rowptr, const int32_t* in_src,
                                 const int32_t* out_rowptr, const int32_t* out_dst,
                                 const int32_t* out_inslot, const float* Y, int64_t ldy,
-                                const float* elr, const float* attn, const float* attn_l,
-                                const float* attn_r, const float* out, const float* g_out, int H,
-                                int F, float slope, int mode, float* gY, int64_t ldgy, float* gelr,
-                                void* workspace, size_t workspace_bytes, void* stream) {
+                                const float* elr, const float* attn, const float* out,
+                                const float* g_out, int H, int F, float slope, int mode, float* gY,
+                                int64_t ldgy, void* workspace, size_t workspace_bytes,
+                                void* stream) {
   clear_error();
   int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_bwd");
   if (rc) return rc;
-  MVML_REQUIRE(ldgy >= mvml_gat_proj_cols(H, F, mode == 1) && ldgy % 4 == 0, "gat_agg_bwd: bad ldgy");
-  MVML_REQUIRE(attn != nullptr && elr != nullptr && gelr != nullptr,
-               "gat_agg_bwd: attn / elr from the forward and the gelr output are required");
+  const int C = mvml_gat_proj_cols(H, F, mode == 1);
+  MVML_REQUIRE(ldgy >= C + 2 * H && ldgy % 4 == 0 && ldgy < (1 << 20),
+               "gat_agg_bwd: ldgy must be >= proj_cols + 2H = %d and a multiple of 4", C + 2 * H);
+  MVML_REQUIRE(attn != nullptr && elr != nullptr, "gat_agg_bwd: attn / elr from the forward are required");
   MVML_REQUIRE(mode != 0 || out != nullptr, "gat_agg_bwd: mode 0 needs the forward output");
+  MVML_REQUIRE(num_groups == mvml_node_group_count(num_nodes) && (num_groups == 0 || node_groups),
+               "gat_agg_bwd: node_groups must come from mvml_build_node_groups");
   if (num_nodes == 0) return MVML_OK;
   if (!workspace || workspace_bytes == 0) {
     set_error("gat_agg_bwd: workspace of mvml_gat_agg_bwd_workspace_size(E, H) bytes required");
@@ -927,10 +1176,10 @@ extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* in_rowptr, con
   float* gpre = static_cast<float*>(workspace);
   const int vpl = (int)ceil_div(H * F, 256);
   switch (H) {
-    case 1: { MVML_VPL_CASES(launch_bwd, 1, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, attn_l, attn_r, out, g_out, F, slope, mode, gpre, gY, ldgy, gelr, st) break; }
-    case 2: { MVML_VPL_CASES(launch_bwd, 2, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, attn_l, attn_r, out, g_out, F, slope, mode, gpre, gY, ldgy, gelr, st) break; }
-    case 4: { MVML_VPL_CASES(launch_bwd, 4, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, attn_l, attn_r, out, g_out, F, slope, mode, gpre, gY, ldgy, gelr, st) break; }
-    case 8: { MVML_VPL_CASES(launch_bwd, 8, num_nodes, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, attn_l, attn_r, out, g_out, F, slope, mode, gpre, gY, ldgy, gelr, st) break; }
+    case 1: { MVML_VPL_CASES(launch_bwd, 1, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, st) break; }
+    case 2: { MVML_VPL_CASES(launch_bwd, 2, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, st) break; }
+    case 4: { MVML_VPL_CASES(launch_bwd, 4, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, st) break; }
+    case 8: { MVML_VPL_CASES(launch_bwd, 8, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, st) break; }
   }
   set_error("gat_agg_bwd: unsupported shape");
   return MVML_ERR_INVALID;
@@ -941,10 +1190,11 @@ extern "C" size_t mvml_gat_attn_grad_workspace_size(int64_t num_nodes, int H, in
 }
 
 extern "C" int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, const float* Y, int64_t ldy,
-                                  const float* gelr, float* g_attn_l, float* g_attn_r,
+                                  const float* gelr, int64_t ldgl, float* g_attn_l, float* g_attn_r,
                                   void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
-  MVML_REQUIRE(H > 0 && F > 0 && num_nodes >= 0 && ldy >= (int64_t)H * F, "gat_attn_grad: bad shape");
+  MVML_REQUIRE(H > 0 && F > 0 && num_nodes >= 0 && ldy >= (int64_t)H * F && ldgl >= 2 * H,
+               "gat_attn_grad: bad shape");
   if (!workspace || workspace_bytes < mvml_gat_attn_grad_workspace_size(num_nodes, H, F)) {
     set_error("gat_attn_grad: workspace too small");
     return MVML_ERR_WORKSPACE;
@@ -955,30 +1205,31 @@ extern "C" int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, const float* 
   const int64_t rows_per = ceil_div(num_nodes > 0 ? num_nodes : 1, S);
   float* part = static_cast<float*>(workspace);
   dim3 g1((unsigned)ceil_div(HF, 256), (unsigned)S);
-  attn_grad_partial_kernel<<<g1, 256, 0, st>>>(num_nodes, H, F, Y, ldy, gelr, rows_per, part);
+  attn_grad_partial_kernel<<<g1, 256, 0, st>>>(num_nodes, H, F, Y, ldy, gelr, ldgl, rows_per, part);
   attn_grad_final_kernel<<<(unsigned)ceil_div(2 * HF, 256), 256, 0, st>>>(HF, S, part, g_attn_l, g_attn_r);
   return check_launch("attn_grad");
 }
 
-extern "C" int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, int H, int F, int Fin,
-                                     int ldw, int mean_residual, float* Wcat, void* stream) {
+extern "C" int mvml_gat_fold_weights(const float* fc_w, const float* res_fc_w, const float* attn_lr,
+                                     int H, int F, int Fin, int ldw, int mean_residual, float* Wcat,
+                                     void* stream) {
   clear_error();
   MVML_REQUIRE(H > 0 && F > 0 && Fin > 0 && ldw >= Fin, "gat_fold_weights: bad shape");
   hipStream_t st = as_stream(stream);
-  const int64_t total = (int64_t)mvml_gat_proj_cols(H, F, mean_residual) * ldw;
+  const int64_t total = (int64_t)(mvml_gat_proj_cols(H, F, mean_residual) + (attn_lr ? 2 * H : 0)) * ldw;
   const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
-  fold_weights_kernel<<<blocks, 256, 0, st>>>(fc_w, res_fc_w, H, F, Fin, ldw, mean_residual, Wcat);
+  fold_weights_kernel<<<blocks, 256, 0, st>>>(fc_w, res_fc_w, attn_lr, H, F, Fin, ldw, mean_residual, Wcat);
   return check_launch("fold_weights_kernel");
 }
 
-extern "C" int mvml_gat_unfold_grads(const float* gWcat, int H, int F, int Fin, int ldg,
-                                     int mean_residual, float* g_fc_w, float* g_res_fc_w,
-                                     void* stream) {
+extern "C" int mvml_gat_unfold_grads(const float* gWcat, const float* attn_lr, int H, int F,
+                                     int Fin, int ldg, int mean_residual, float* g_fc_w,
+                                     float* g_res_fc_w, void* stream) {
   clear_error();
   MVML_REQUIRE(H > 0 && F > 0 && Fin > 0 && ldg >= Fin, "gat_unfold_grads: bad shape");
   hipStream_t st = as_stream(stream);
   const int64_t total = (int64_t)H * F * Fin;
   const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
-  unfold_w_kernel<<<blocks, 256, 0, st>>>(gWcat, H, F, Fin, ldg, mean_residual, g_fc_w, g_res_fc_w);
+  unfold_w_kernel<<<blocks, 256, 0, st>>>(gWcat, attn_lr, H, F, Fin, ldg, mean_residual, g_fc_w, g_res_fc_w);
   return check_launch("unfold_w_kernel");
 }

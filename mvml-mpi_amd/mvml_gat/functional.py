@@ -47,13 +47,12 @@ def agg_fwd_bytes(N, E, H, F, out_cols, res_cols):
 
 
 def agg_bwd_bytes(N, E, H, F, gout_cols, mode):
-    """Algorithmic bytes of mvml_gat_agg_bwd: read Z, el/er, g_out (+ out for ELU'), saved
-    attention, both CSRs; write gY = [dZ | dR] and [d el | d er]; the [E,H] g_pre round trip
-    between its two passes is counted once each way."""
+    """Algorithmic bytes of mvml_gat_agg_bwd: read Z, el/er, g_out (+ out for ELU'), the saved
+    attention, both CSRs; write gY = [dZ_agg | dR | d el | d er]."""
     rw = F if mode == MODE_MEAN else H * F
     reads = N * H * F + 2 * N * H + N * gout_cols + (N * H * F if mode == 0 else 0) + E * H
     idx = 2 * (N + 1) + 3 * E
-    writes = N * (H * F + rw + 2 * H) + 2 * E * H
+    writes = N * (H * F + rw + 2 * H)
     return 4 * (reads + idx + writes)
 
 
@@ -105,13 +104,15 @@ class GATLayerFunction(torch.autograd.Function):
         # GEMM operand row is 16-B aligned and the LDS-DMA path applies; pad columns are zero.
         Fp = _round4(Fin)
         Xp = X if Fp == Fin else torch.nn.functional.pad(X, (0, Fp - Fin))
-        Wcat = torch.empty((C, Fp), dtype=torch.float32, device=dev)
-        call("mvml_gat_fold_weights", ptr(_c(fc_w)), ptr(_c(res_w)), H, F, Fin, Fp, mean_res,
-             ptr(Wcat), st)
-        Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
-        elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
         attn_l, attn_r = _c(attn_l), _c(attn_r)
         attn_lr = torch.cat([attn_l.reshape(-1), attn_r.reshape(-1)])
+        # [fc.weight ; res_fc.weight (or its head mean) ; A_l ; A_r]: the projection GEMM uses
+        # the first C rows, the backward all C + 2H (the el / er paths, see mvml_gat_agg_bwd)
+        Wcat = torch.empty((C + 2 * H, Fp), dtype=torch.float32, device=dev)
+        call("mvml_gat_fold_weights", ptr(_c(fc_w)), ptr(_c(res_w)), ptr(attn_lr), H, F, Fin, Fp,
+             mean_res, ptr(Wcat), st)
+        Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
+        elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
         L = _lib.lib()
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_proj_fwd_workspace_size(N, H, F), dev)
         _lib.call_tag[0] = {"flops": 2 * N * C * Fp}
@@ -125,14 +126,14 @@ class GATLayerFunction(torch.autograd.Function):
         call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.node_groups.numel() - 1, ptr(g.in_rowptr),
              ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(_c(bias)), float(slope), int(mode),
              ptr(out), ptr(attn), st)
-        ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r)
+        ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr)
         ctx.Fin = Fin
         ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode, ctx.ldy = g, H, F, slope, mode, ldy
         return out
 
     @staticmethod
     def backward(ctx, g_out):
-        Xp, Wcat, Y, attn, elr, out, attn_l, attn_r = ctx.saved_tensors
+        Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr = ctx.saved_tensors
         g, H, F, mode, ldy = ctx.g, ctx.H, ctx.F, ctx.mode, ctx.ldy
         g_out = _c(g_out)
         N, Fp = Xp.shape
@@ -140,42 +141,43 @@ class GATLayerFunction(torch.autograd.Function):
         dev = Xp.device
         HF = H * F
         mean_res = int(mode == MODE_MEAN)
-        C = _lib.lib().mvml_gat_proj_cols(H, F, mean_res)
-        RW = C - HF
-        st = _stream(dev)
         L = _lib.lib()
-        gY = torch.empty((N, ldy), dtype=torch.float32, device=dev)
-        gelr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
+        C = L.mvml_gat_proj_cols(H, F, mean_res)
+        CE = C + 2 * H  # + [d el | d er]
+        ldg = _round4(CE)
+        st = _stream(dev)
+        gY = torch.empty((N, ldg), dtype=torch.float32, device=dev)
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_agg_bwd_workspace_size(g.num_edges(), H), dev)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}",
                             "bytes": agg_bwd_bytes(N, g.num_edges(), H, F, g_out.shape[1], mode)}
-        call("mvml_gat_agg_bwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr),
-             ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr), ptr(attn), ptr(attn_l),
-             ptr(attn_r), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldy,
-             ptr(gelr), wp, wn, st)
-        # dL/dWcat = gY^T X  (split-K over atoms)
-        gW = torch.empty((C, Fp), dtype=torch.float32, device=dev)
-        assert RW in (F, HF)
-        gemm(gY, Xp, C, Fp, N, 1, 1, ldy, Fp, gW, Fp)
+        call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.node_groups.numel() - 1, ptr(g.in_rowptr),
+             ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr),
+             ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldg, wp, wn, st)
+        # dL/d[Wcat ; A_l ; A_r] = gY^T X  (split-K over atoms)
+        gW = torch.empty((CE, Fp), dtype=torch.float32, device=dev)
+        gemm(gY, Xp, CE, Fp, N, 1, 1, ldg, Fp, gW, Fp)
         g_fc = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_res = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_al = torch.empty_like(attn_l)
         g_ar = torch.empty_like(attn_r)
-        call("mvml_gat_unfold_grads", ptr(gW), H, F, Fin, Fp, mean_res, ptr(g_fc), ptr(g_res), st)
+        call("mvml_gat_unfold_grads", ptr(gW), ptr(attn_lr), H, F, Fin, Fp, mean_res, ptr(g_fc),
+             ptr(g_res), st)
+        gelr = gY[:, C:CE]
         wp2, wn2 = _lib.ws_ptr_size(L.mvml_gat_attn_grad_workspace_size(N, H, F), dev)
-        call("mvml_gat_attn_grad", N, H, F, ptr(Y), ldy, ptr(gelr), ptr(g_al), ptr(g_ar), wp2, wn2, st)
+        call("mvml_gat_attn_grad", N, H, F, ptr(Y), ldy, ctypes.c_void_p(ptr(gY).value + 4 * C), ldg,
+             ptr(g_al), ptr(g_ar), wp2, wn2, st)
         if DEBUG_CAPTURE is not None:
             DEBUG_CAPTURE.update(elr=elr, gelr=gelr, attn=attn)
         g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
         if mean_res:  # every head's bias sees g_out / H: one column sum, replicated over heads
-            colsum(gY, N, F, ldy, g_bias, offset=HF, alpha=1.0 / H)
+            colsum(gY, N, F, ldg, g_bias, offset=HF, alpha=1.0 / H)
             g_bias.view(H, F)[1:].copy_(g_bias[:F].expand(H - 1, F))
         else:
-            colsum(gY, N, HF, ldy, g_bias, offset=HF)
+            colsum(gY, N, HF, ldg, g_bias, offset=HF)
         gX = None
         if ctx.needs_input_grad[0]:
             gX = torch.empty((N, Fin), dtype=torch.float32, device=dev)
-            gemm(gY, Wcat, N, Fin, C, 0, 1, ldy, Fp, gX, Fin)
+            gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin)
         return gX, g_fc, g_res, g_al, g_ar, g_bias, None, None, None, None, None
 
 

@@ -57,13 +57,14 @@ def main():
         by = agg_fwd_bytes(N, E, H, F, oc, C - H * F)
         print(f"  agg_fwd {name:16s} {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
         g_out = torch.randn_like(out)
-        gY = torch.empty((N, ldy), device="cuda")
+        ldg = (C + 2 * H + 3) // 4 * 4
+        gY = torch.empty((N, ldg), device="cuda")
         wsz = L.mvml_gat_agg_bwd_workspace_size(E, H)
         ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
-        b = lambda: call("mvml_gat_agg_bwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr),
-                         ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr), ptr(attn), ptr(al),
-                         ptr(ar), ptr(out), ptr(g_out), H, F, 0.2, mode, ptr(gY), ldy, ptr(gelr),
-                         ptr(ws), wsz, st)
+        b = lambda: call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.node_groups.numel() - 1,
+                         ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst),
+                         ptr(g.out_inslot), ptr(Y), ldy, ptr(elr), ptr(attn), ptr(out), ptr(g_out), H, F,
+                         0.2, mode, ptr(gY), ldg, ptr(ws), wsz, st)
         ms = timeit(b)
         by = agg_bwd_bytes(N, E, H, F, oc, mode)
         print(f"  agg_bwd {name:16s} {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
