@@ -220,21 +220,24 @@ constexpr int kAggThreads = 512;
 __device__ __forceinline__ bool lds_group(int a0, int a1, const int32_t* __restrict__ rowptr) {
   if (a1 - a0 > kWinL || rowptr[a1] - rowptr[a0] > kECap) return false;  // block-uniform
   bool hub = false;
-  for (int v = a0 + (int)threadIdx.x; v < a1; v += kAggThreads) hub |= rowptr[v + 1] - rowptr[v] > kEC;
+  for (int v = a0 + (int)threadIdx.x; v < a1; v += (int)blockDim.x) hub |= rowptr[v + 1] - rowptr[v] > kEC;
   return !__syncthreads_or(hub);
 }
 
 #ifndef MVML_LDS_WAVES
 #define MVML_LDS_WAVES 4
 #endif
-template <int H, int CW, int MODE>
-__global__ void __launch_bounds__(kAggThreads, MVML_LDS_WAVES)  // 2 workgroups (16 waves) per CU
+// NT = 16 * CW threads: 64 destinations per pass, two passes cover kWinL = 128 atoms; 16 waves
+// per CU either way (2 x 512 threads for CW = 32, 1 x 1024 for CW = 64: half the barriers per
+// byte streamed).
+template <int H, int CW, int MODE, int NT>
+__global__ void __launch_bounds__(NT, MVML_LDS_WAVES)
 gat_agg_fwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __restrict__ rowptr,
                        const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
                        int F, const float* __restrict__ bias, const float* __restrict__ attn,
                        float* __restrict__ out) {
   constexpr int LPD = CW / 4;                        // lanes per destination atom
-  constexpr int DPP = kAggThreads / LPD;             // destinations per pass
+  constexpr int DPP = NT / LPD;                      // destinations per pass
   constexpr int NP = (kWinL + DPP - 1) / DPP;        // passes
   __shared__ float4 zbuf[2][kWinL * LPD];
   __shared__ float s_att[(kECap + 1) * H];  // + H zeros: the attention of a missing edge
@@ -249,7 +252,7 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __rest
   const int ocols = MODE == 1 ? F : HF;
   const int e0 = rowptr[a0];
   const int ne = rowptr[a1] - e0;
-  for (int i = tid; i < ne * H; i += kAggThreads) s_att[i] = attn[(int64_t)e0 * H + i];
+  for (int i = tid; i < ne * H; i += NT) s_att[i] = attn[(int64_t)e0 * H + i];
   if (tid < H) s_att[kECap * H + tid] = 0.f;
   const uint32_t rowb = (uint32_t)ldy * 4u;
   const __amdgpu_buffer_rsrc_t rY = make_rsrc(Y + (int64_t)a0 * ldy, (uint32_t)nr * rowb);
@@ -888,7 +891,7 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
   if (G == 0) return MVML_OK;
 #define MVML_AGG_FWD_M(CW, M)                                                                       \
   do {                                                                                              \
-    gat_agg_fwd_lds_kernel<H, CW, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, rp, src, Y, ldy, F, \
+    gat_agg_fwd_lds_kernel<H, CW, M, CW * 16><<<(unsigned)G, CW * 16, 0, st>>>(groups, rp, src, Y, ldy, F, \
                                                                          bias, attn, out);          \
     gat_agg_fwd_gather_kernel<H, CW, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, rp, src, Y, ldy,  \
                                                                             F, bias, attn, out);    \
@@ -899,7 +902,8 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
     else if (mode == 1) MVML_AGG_FWD_M(CW, 1);            \
     else MVML_AGG_FWD_M(CW, 2);                           \
   } while (0)
-  if (F % 32 == 0) MVML_AGG_FWD(32);
+  if (F % 64 == 0) MVML_AGG_FWD(64);
+  else if (F % 32 == 0) MVML_AGG_FWD(32);
   else if (F % 16 == 0) MVML_AGG_FWD(16);
   else if (F % 8 == 0) MVML_AGG_FWD(8);
   else MVML_AGG_FWD(4);
