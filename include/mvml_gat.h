@@ -67,10 +67,19 @@ int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local,
  * begins with the molecule containing atom 64*g; G = mvml_node_group_count(N) groups, some
  * possibly empty.  Every in-edge of a group's atoms starts inside the group, so one workgroup
  * can stage a group's projection rows in LDS and read each of them from HBM once.
- * node_offsets: int64[B+1] from mvml_build_csr; group_start: int32[G+1]. */
+ * The PLAN (int32[mvml_node_group_plan_size(N)]) holds, for G groups:
+ *   [0, G]          group_start (group_start[G] = N)
+ *   [G+1, 2G+1)     kind: bit 0 = forward LDS kernel (<= 128 atoms, <= 512 in-edges, every
+ *                   in-degree <= 5), bit 1 = backward LDS kernel (<= 128 atoms, <= 512 edges)
+ *   2G+1, 2G+2      number of non-empty groups without bit 0 / bit 1
+ *   [2G+3, 3G+3)    those groups for the forward fallback kernel (any order)
+ *   [3G+3, 4G+3)    those groups for the backward fallback kernels
+ * so the aggregation launches never scan the CSR to route groups.  node_offsets: int64[B+1]
+ * and in_rowptr: int32[N+1] from mvml_build_csr. */
 int64_t mvml_node_group_count(int64_t num_nodes);
+int64_t mvml_node_group_plan_size(int64_t num_nodes);
 int mvml_build_node_groups(int64_t num_graphs, int64_t num_nodes, const int64_t* node_offsets,
-                           int32_t* group_start, void* stream);
+                           const int32_t* in_rowptr, int32_t* plan, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Dense fp32 GEMM on CDNA4 MFMA (v_mfma_f32_32x32x2_f32, exact f32 fmaf chains).
@@ -157,6 +166,8 @@ int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, const float* Y, int64_t 
  * Y is the projection output (mean_residual layout iff mode 1; ldy >= its C, multiple of 4),
  * elr its logits (mvml_gat_proj_fwd).  out is [N, H*F] (modes 0, 2) or [N, F] (mode 1).
  * attn [E, H] receives the edge_softmax output in in-CSR slot order (needed by the backward).
+ * node_groups is the plan mvml_build_node_groups built from the same in_rowptr (a plan of
+ * another graph is undefined behaviour); num_groups = mvml_node_group_count(num_nodes).
  * ------------------------------------------------------------------------------------- */
 int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
                      const int32_t* in_rowptr, const int32_t* in_src, const float* Y, int64_t ldy,

@@ -254,6 +254,33 @@ __global__ void node_groups_kernel(int64_t B, int64_t N, const int64_t* __restri
   group_start[g] = (int32_t)node_offsets[lo];
 }
 
+// Group kinds (one wave per group): bit 0 = the forward LDS kernel takes the group (<=
+// kPlanWinAtoms atoms, <= kPlanEdgeCap in-edges, in-degree <= kPlanDegCap everywhere), bit 1 =
+// the backward LDS kernel does (atom and edge caps only).  Non-empty groups without a bit are
+// appended to that direction's fallback list (order irrelevant: groups are independent).
+__global__ void node_group_kind_kernel(int64_t G, const int32_t* __restrict__ rowptr,
+                                       int32_t* __restrict__ plan) {
+  const int64_t g = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const int lane = threadIdx.x & 63;
+  if (g >= G) return;
+  int32_t* kind = plan + G + 1;
+  int32_t* count = plan + 2 * G + 1;
+  const int a0 = plan[g], a1 = plan[g + 1];
+  int dmax = 0;
+  for (int v = a0 + lane; v < a1; v += 64) dmax = max(dmax, rowptr[v + 1] - rowptr[v]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) dmax = max(dmax, __shfl_xor(dmax, o, 64));
+  if (lane != 0) return;
+  int k = 0;
+  if (a1 > a0) {
+    const bool fits = a1 - a0 <= kPlanWinAtoms && rowptr[a1] - rowptr[a0] <= kPlanEdgeCap;
+    k = (fits && dmax <= kPlanDegCap ? 1 : 0) | (fits ? 2 : 0);
+    if (!(k & 1)) plan[2 * G + 3 + atomicAdd(&count[0], 1)] = (int32_t)g;
+    if (!(k & 2)) plan[3 * G + 3 + atomicAdd(&count[1], 1)] = (int32_t)g;
+  }
+  kind[g] = k;
+}
+
 }  // namespace
 }  // namespace mvml
 
@@ -312,16 +339,26 @@ extern "C" int64_t mvml_node_group_count(int64_t num_nodes) {
   return num_nodes > 0 ? ceil_div(num_nodes, kNodeGroupAtoms) : 0;
 }
 
+extern "C" int64_t mvml_node_group_plan_size(int64_t num_nodes) {
+  const int64_t G = mvml_node_group_count(num_nodes);
+  return G > 0 ? 4 * G + 3 : 1;
+}
+
 extern "C" int mvml_build_node_groups(int64_t num_graphs, int64_t num_nodes,
-                                      const int64_t* node_offsets, int32_t* group_start,
-                                      void* stream) {
+                                      const int64_t* node_offsets, const int32_t* in_rowptr,
+                                      int32_t* plan, void* stream) {
   clear_error();
   MVML_REQUIRE(num_graphs >= 0 && num_nodes >= 0 && num_nodes < (int64_t(1) << 31),
                "build_node_groups: bad sizes");
   const int64_t G = mvml_node_group_count(num_nodes);
   if (G == 0) return MVML_OK;
-  MVML_REQUIRE(num_graphs > 0 && node_offsets && group_start, "build_node_groups: null input");
-  node_groups_kernel<<<(unsigned)ceil_div(G + 1, 256), 256, 0, as_stream(stream)>>>(
-      num_graphs, num_nodes, node_offsets, G, group_start);
-  return check_launch("node_groups_kernel");
+  MVML_REQUIRE(num_graphs > 0 && node_offsets && in_rowptr && plan, "build_node_groups: null input");
+  hipStream_t st = as_stream(stream);
+  (void)hipMemsetAsync(plan + 2 * G + 1, 0, 2 * sizeof(int32_t), st);
+  node_groups_kernel<<<(unsigned)ceil_div(G + 1, 256), 256, 0, st>>>(num_graphs, num_nodes,
+                                                                    node_offsets, G, plan);
+  int rc = check_launch("node_groups_kernel");
+  if (rc) return rc;
+  node_group_kind_kernel<<<(unsigned)ceil_div(G, 4), 256, 0, st>>>(G, in_rowptr, plan);
+  return check_launch("node_group_kind_kernel");
 }

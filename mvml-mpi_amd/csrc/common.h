@@ -17,6 +17,23 @@ void clear_error();
 constexpr int kWave = 64;
 // Target size of a node group (mvml_build_node_groups): whole molecules, ~this many atoms.
 constexpr int kNodeGroupAtoms = 64;
+// Node-group plan caps (mvml_build_node_groups): the LDS aggregation kernels' limits.
+constexpr int kPlanWinAtoms = 128;  // atoms per group
+constexpr int kPlanEdgeCap = 512;   // in-edges per group
+constexpr int kPlanDegCap = 5;      // forward: in-degree of every atom
+// Plan layout (int32, G = mvml_node_group_count(N)): [0, G] group starts | [G+1, 2G+1) kinds |
+// 2G+1, 2G+2: forward / backward fallback counts | [2G+3, 3G+3) forward fallback groups |
+// [3G+3, 4G+3) backward fallback groups.
+struct GroupPlan {
+  const int32_t* start;
+  const int32_t* kind;
+  const int32_t* count;
+  const int32_t* fwd_list;
+  const int32_t* bwd_list;
+  __host__ __device__ GroupPlan(const int32_t* p, int64_t G)
+      : start(p), kind(p + G + 1), count(p + 2 * G + 1), fwd_list(p + 2 * G + 3),
+        bwd_list(p + 3 * G + 3) {}
+};
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -210,19 +210,13 @@ gat_softmax_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
 //  * gat_agg_fwd_gather_kernel — everything else (large molecules, hubs): no staging; the
 //    gathers go straight to global memory, where the chunk-synchronous sweep keeps the group's
 //    chunk rows in the XCD's L2.  Correct for any graph.
-constexpr int kWinL = 128;    // LDS kernel: atoms per group
-constexpr int kECap = 512;    // LDS kernel: in-edges per group (attention staged in LDS)
-constexpr int kWin = 64;      // gather kernel: destination atoms per pass set
-constexpr int kEC = 5;        // in-edges per destination with cached offsets
+// Which kernel takes a group is decided once per batch by mvml_build_node_groups (the group
+// plan: kind bits + fallback lists), so no launch scans the CSR to find its groups.
+constexpr int kWinL = kPlanWinAtoms;  // LDS kernel: atoms per group
+constexpr int kECap = kPlanEdgeCap;   // LDS kernel: in-edges per group (attention staged in LDS)
+constexpr int kWin = 64;              // gather kernel: destination atoms per pass set
+constexpr int kEC = kPlanDegCap;      // in-edges per destination with cached offsets
 constexpr int kAggThreads = 512;
-
-// Block-wide: does group [a0, a1) take the LDS kernel?  (All threads must call it.)
-__device__ __forceinline__ bool lds_group(int a0, int a1, const int32_t* __restrict__ rowptr) {
-  if (a1 - a0 > kWinL || rowptr[a1] - rowptr[a0] > kECap) return false;  // block-uniform
-  bool hub = false;
-  for (int v = a0 + (int)threadIdx.x; v < a1; v += (int)blockDim.x) hub |= rowptr[v + 1] - rowptr[v] > kEC;
-  return !__syncthreads_or(hub);
-}
 
 #ifndef MVML_LDS_WAVES
 #define MVML_LDS_WAVES 4
@@ -232,7 +226,7 @@ __device__ __forceinline__ bool lds_group(int a0, int a1, const int32_t* __restr
 // byte streamed).
 template <int H, int CW, int MODE, int NT>
 __global__ void __launch_bounds__(NT, MVML_LDS_WAVES)
-gat_agg_fwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __restrict__ rowptr,
+gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                        const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
                        int F, const float* __restrict__ bias, const float* __restrict__ attn,
                        float* __restrict__ out) {
@@ -244,8 +238,9 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __rest
   const int tid = threadIdx.x;
   const int ds = tid / LPD, q = tid % LPD;
   const int HF = H * F;
-  const int a0 = groups[blockIdx.x], a1 = groups[blockIdx.x + 1];
-  if (a1 <= a0 || !lds_group(a0, a1, rowptr)) return;
+  const GroupPlan gp(plan, G);
+  if (!(gp.kind[blockIdx.x] & 1)) return;
+  const int a0 = gp.start[blockIdx.x], a1 = gp.start[blockIdx.x + 1];
   const int nr = a1 - a0;
   const int nfc = F / CW;     // column chunks per head
   const int nch = H * nfc;
@@ -368,7 +363,7 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __rest
 
 template <int H, int CW, int MODE>
 __global__ void __launch_bounds__(kAggThreads, 4)  // 2 workgroups (16 waves) per CU
-gat_agg_fwd_gather_kernel(const int32_t* __restrict__ groups, const int32_t* __restrict__ rowptr,
+gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                    const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
                    int F, const float* __restrict__ bias, const float* __restrict__ attn,
                    float* __restrict__ out) {
@@ -378,8 +373,10 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ groups, const int32_t* __r
   const int tid = threadIdx.x;
   const int ds = tid / LPD, q = tid % LPD;
   const int HF = H * F;
-  const int a0 = groups[blockIdx.x], a1 = groups[blockIdx.x + 1];
-  if (a1 <= a0 || lds_group(a0, a1, rowptr)) return;
+  const GroupPlan gp(plan, G);
+  if ((int)blockIdx.x >= gp.count[0]) return;
+  const int g = gp.fwd_list[blockIdx.x];
+  const int a0 = gp.start[g], a1 = gp.start[g + 1];
   const int nfc = F / CW;     // column chunks per head
   const int nch = H * nfc;
   const int ocols = MODE == 1 ? F : HF;
@@ -500,13 +497,9 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ groups, const int32_t* __r
 // then the softmax backward runs in LDS (g_s = a (g_a - sum a g_a), g_pre = g_s leaky') and
 // d er / d el are its per-destination / per-source sums.  Z, g_out and dZ cross HBM once.
 // Every other group (large molecules, edge-heavy hubs) takes the per-atom dst / src pair.
-__device__ __forceinline__ bool bwd_lds_group(int a0, int a1, const int32_t* __restrict__ rowptr) {
-  return a1 > a0 && a1 - a0 <= kWinL && rowptr[a1] - rowptr[a0] <= kECap;
-}
-
 template <int H, int MODE>
 __global__ void __launch_bounds__(kAggThreads, 4)  // 2 workgroups (16 waves) per CU
-gat_agg_bwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __restrict__ rowptr,
+gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                        const int32_t* __restrict__ in_src, const int32_t* __restrict__ out_rowptr,
                        const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
                        const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ elr,
@@ -514,15 +507,21 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __rest
                        const float* __restrict__ g_out, float slope, float* __restrict__ gY,
                        int64_t ldgy, int C) {
   constexpr int CW = 32, LPD = CW / 4, DPP = kAggThreads / LPD, NP = (kWinL + DPP - 1) / DPP;
-  __shared__ float4 zs[kWinL * LPD];  // Z chunk of the group's rows
-  __shared__ float4 gs[kWinL * LPD];  // g_rst chunk
+  // Z and g_rst chunks of the group's rows, 16-B slot c of row r at r*LPD + (c ^ sw(r)): the
+  // edge role reads whole rows of 16 different atoms per quarter-wave, which unswizzled would
+  // all map onto the same two 128-B bank windows
+  static_assert(LPD == 8, "swizzle assumes 8 slots per row");
+  __shared__ float4 zs[kWinL * LPD];
+  __shared__ float4 gs[kWinL * LPD];
+  auto sw = [](int r) { return (r >> 1) & 7; };
   __shared__ float s_att[(kECap + 1) * H];  // + H zeros: the attention of a missing edge
   __shared__ float s_ga[kECap * H];
   __shared__ int s_src[kECap], s_dst[kECap], s_odst[kECap], s_oslot[kECap];
   __shared__ int s_rp[kWinL + 1], s_orp[kWinL + 1];
   __shared__ float s_elr[kWinL * 2 * H];
-  const int a0 = groups[blockIdx.x], a1 = groups[blockIdx.x + 1];
-  if (!bwd_lds_group(a0, a1, rowptr)) return;
+  const GroupPlan gp(plan, G);
+  if (!(gp.kind[blockIdx.x] & 2)) return;
+  const int a0 = gp.start[blockIdx.x], a1 = gp.start[blockIdx.x + 1];
   const int tid = threadIdx.x, ds = tid / LPD, q = tid % LPD;
   const int nr = a1 - a0, HF = H * F, nfc = F / CW, nch = H * nfc;
   const int ocols = MODE == 1 ? F : HF;
@@ -585,8 +584,8 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __rest
           const float hh = (float)H;
           g = make_float4(g.x / hh, g.y / hh, g.z / hh, g.w / hh);
         }
-        zs[r * LPD + q] = zr[j];
-        gs[r * LPD + q] = g;
+        zs[r * LPD + (q ^ sw(r))] = zr[j];
+        gs[r * LPD + (q ^ sw(r))] = g;
         if (MODE != 1) buf_st4(rG, 4u * (uint32_t)(r * ldgi + HF + col), g);
         else if (h == 0) buf_st4(rG, 4u * (uint32_t)(r * ldgi + HF + fc * CW + 4 * q), gr[j]);
       }
@@ -606,7 +605,8 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __rest
 #pragma unroll
     for (int i = 0; i < kEC; ++i) {
       const bool ok = ob + i < oend[p];
-      go[p][i] = (ok ? s_odst[ob + i] : (u < nr ? u : 0)) * LPD + q;
+      const int r = ok ? s_odst[ob + i] : (u < nr ? u : 0);
+      go[p][i] = r * LPD + (q ^ sw(r));
       ga_[p][i] = ok ? s_oslot[ob + i] * H : kECap * H;
     }
   }
@@ -626,7 +626,8 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __rest
     if (has_e) {  // g_a partial of this thread's in-edge
       float sacc = 0.f;
 #pragma unroll
-      for (int c = 0; c < LPD; ++c) sacc += dot4(zs[es * LPD + c], gs[ed * LPD + c]);
+      for (int c = 0; c < LPD; ++c)
+        sacc += dot4(zs[es * LPD + (c ^ sw(es))], gs[ed * LPD + (c ^ sw(ed))]);
       add_at<H>(ga, h, sacc);
     }
 #pragma unroll
@@ -637,7 +638,7 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ groups, const int32_t* __rest
       for (int i = 0; i < kEC; ++i) acc = fma4(s_att[ga_[p][i] + h], gs[go[p][i]], acc);
       if (u < nr) {
         for (int o = s_orp[u] + kEC; o < oend[p]; ++o)
-          acc = fma4(s_att[s_oslot[o] * H + h], gs[s_odst[o] * LPD + q], acc);
+          acc = fma4(s_att[s_oslot[o] * H + h], gs[s_odst[o] * LPD + (q ^ sw(s_odst[o]))], acc);
         buf_st4(rG, 4u * (uint32_t)(u * ldgi + col), acc);
       }
     }
@@ -688,12 +689,14 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
                        float* __restrict__ gpre, float* __restrict__ gY, int64_t ldgy,
                        float* __restrict__ gelr, int64_t ldgl) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  // G > 0: one block per node group, skipping the groups the LDS kernel handles; G == 0: one
-  // wave per atom over all atoms
+  // G > 0: one block per backward fallback group of the plan; G == 0: one wave per atom over
+  // all atoms
   int64_t v, vend, vstep;
   if (G > 0) {
-    const int a0 = groups[blockIdx.x], a1 = groups[blockIdx.x + 1];
-    if (a1 <= a0 || bwd_lds_group(a0, a1, rowptr)) return;
+    const GroupPlan gp(groups, G);
+    if ((int)blockIdx.x >= gp.count[1]) return;
+    const int g = gp.bwd_list[blockIdx.x];
+    const int a0 = gp.start[g], a1 = gp.start[g + 1];
     v = a0 + wid;
     vend = a1;
     vstep = kWavesPerBlock;
@@ -808,12 +811,14 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
                        int mode, float* __restrict__ gY, int64_t ldgy, float* __restrict__ gelr,
                        int64_t ldgl) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  // G > 0: one block per node group, skipping the groups the LDS kernel handles; G == 0: one
-  // wave per atom over all atoms
+  // G > 0: one block per backward fallback group of the plan; G == 0: one wave per atom over
+  // all atoms
   int64_t u, vend, vstep;
   if (G > 0) {
-    const int a0 = groups[blockIdx.x], a1 = groups[blockIdx.x + 1];
-    if (a1 <= a0 || bwd_lds_group(a0, a1, rowptr)) return;
+    const GroupPlan gp(groups, G);
+    if ((int)blockIdx.x >= gp.count[1]) return;
+    const int g = gp.bwd_list[blockIdx.x];
+    const int a0 = gp.start[g], a1 = gp.start[g + 1];
     u = a0 + wid;
     vend = a1;
     vstep = kWavesPerBlock;
@@ -891,9 +896,9 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
   if (G == 0) return MVML_OK;
 #define MVML_AGG_FWD_M(CW, M)                                                                       \
   do {                                                                                              \
-    gat_agg_fwd_lds_kernel<H, CW, M, CW * 16><<<(unsigned)G, CW * 16, 0, st>>>(groups, rp, src, Y, ldy, F, \
+    gat_agg_fwd_lds_kernel<H, CW, M, CW * 16><<<(unsigned)G, CW * 16, 0, st>>>(groups, G, rp, src, Y, ldy, F, \
                                                                          bias, attn, out);          \
-    gat_agg_fwd_gather_kernel<H, CW, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, rp, src, Y, ldy,  \
+    gat_agg_fwd_gather_kernel<H, CW, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, G, rp, src, Y, ldy, \
                                                                             F, bias, attn, out);    \
   } while (0)
 #define MVML_AGG_FWD(CW)                                  \
@@ -920,7 +925,7 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
                int64_t ldgy, int C, hipStream_t st) {
   if (F % 32 == 0 && G > 0) {  // molecule groups: one pass over Z / g_out / dZ per group
 #define MVML_BWD_LDS(M)                                                                          \
-    gat_agg_bwd_lds_kernel<H, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, rp, src, orp, odst, \
+    gat_agg_bwd_lds_kernel<H, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, G, rp, src, orp, odst, \
                                                                      oslot, Y, ldy, F, elr, attn, \
                                                                      out, g_out, slope, gY, ldgy, C)
     if (mode == 0) MVML_BWD_LDS(0);

@@ -183,9 +183,11 @@ class BatchedMolGraph:
         if fl[1] != 0:
             raise ValueError(f"{int(fl[1])} edges reference node ids outside their graph")
         self.has_zero_in_degree = bool(fl[0] > 0)
-        d["node_groups"] = torch.empty(L.mvml_node_group_count(N) + 1, **i32)
-        _lib.call("mvml_build_node_groups", B, N, P(d["node_offsets"]), P(d["node_groups"]),
-                  _lib.stream_ptr(device))
+        # node-group plan: group starts, LDS-kernel eligibility and the fallback group lists
+        d["num_node_groups"] = L.mvml_node_group_count(N)
+        d["node_groups"] = torch.empty(L.mvml_node_group_plan_size(N), **i32)
+        _lib.call("mvml_build_node_groups", B, N, P(d["node_offsets"]), P(d["in_rowptr"]),
+                  P(d["node_groups"]), _lib.stream_ptr(device))
         d["group_offsets"] = torch.as_tensor(self.group_offsets_host()).to(device)
         d["group_node_offsets"] = None
         # keep the uploaded inputs alive until the stream has consumed them

@@ -123,7 +123,7 @@ class GATLayerFunction(torch.autograd.Function):
         E = g.num_edges()
         attn = torch.empty((E, H), dtype=torch.float32, device=dev)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}", "bytes": agg_fwd_bytes(N, E, H, F, out_cols, C - HF)}
-        call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.node_groups.numel() - 1, ptr(g.in_rowptr),
+        call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
              ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(_c(bias)), float(slope), int(mode),
              ptr(out), ptr(attn), st)
         ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr)
@@ -150,7 +150,7 @@ class GATLayerFunction(torch.autograd.Function):
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_agg_bwd_workspace_size(g.num_edges(), H), dev)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}",
                             "bytes": agg_bwd_bytes(N, g.num_edges(), H, F, g_out.shape[1], mode)}
-        call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.node_groups.numel() - 1, ptr(g.in_rowptr),
+        call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
              ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr),
              ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldg, wp, wn, st)
         # dL/d[Wcat ; A_l ; A_r] = gY^T X  (split-K over atoms)

@@ -80,3 +80,34 @@ def csr_ref(src, dst, num_nodes_total):
     return dict(in_rowptr=i32(in_rowptr), in_src=i32(in_src), in_eid=i32(in_eid),
                 out_rowptr=i32(out_rowptr), out_dst=i32(out_dst), out_inslot=i32(out_inslot),
                 zero_in_degree=zero_in)
+
+
+def node_group_plan_ref(node_offsets, in_rowptr, group_atoms=64, win_atoms=128, edge_cap=512,
+                        deg_cap=5):
+    """Node-group plan of mvml_build_node_groups (launch geometry; no reference counterpart):
+    group g starts at the first atom of the molecule containing atom group_atoms*g; kind bit 0
+    = forward LDS kernel (atom, edge and in-degree caps), bit 1 = backward LDS kernel (atom and
+    edge caps).  Returns (starts [G+1], kinds [G], fwd fallback set, bwd fallback set)."""
+    node_offsets = np.asarray(node_offsets, dtype=np.int64)
+    rp = np.asarray(in_rowptr, dtype=np.int64)
+    N = int(node_offsets[-1])
+    G = -(-N // group_atoms) if N > 0 else 0
+    starts = np.empty(G + 1, dtype=np.int32)
+    for g in range(G):
+        m = np.searchsorted(node_offsets, g * group_atoms, side="right") - 1
+        starts[g] = node_offsets[m]
+    starts[G] = N
+    kinds = np.zeros(G, dtype=np.int32)
+    fwd, bwd = set(), set()
+    for g in range(G):
+        a0, a1 = int(starts[g]), int(starts[g + 1])
+        if a1 <= a0:
+            continue
+        fits = a1 - a0 <= win_atoms and rp[a1] - rp[a0] <= edge_cap
+        dmax = int(np.max(rp[a0 + 1:a1 + 1] - rp[a0:a1]))
+        kinds[g] = (1 if fits and dmax <= deg_cap else 0) | (2 if fits else 0)
+        if not kinds[g] & 1:
+            fwd.add(g)
+        if not kinds[g] & 2:
+            bwd.add(g)
+    return starts, kinds, fwd, bwd

@@ -39,6 +39,27 @@ def test_build_csr_bit_exact(sizes, hubs):
     assert g.has_zero_in_degree is False
 
 
+@pytest.mark.parametrize("sizes,hubs", [
+    ([25] * 37, False),
+    ([11, 23, 80, 5, 1, 40, 23, 130, 64, 64, 2], False),
+    ([150, 300, 220, 7, 9], True),
+    ([1] * 5, False),
+])
+def test_node_group_plan_bit_exact(sizes, hubs):
+    sb = batch_of_sizes(sizes, seed=5, hubs=hubs)
+    g = _to_dev(sb)
+    G = g.num_node_groups
+    plan = g.node_groups.cpu().numpy()
+    starts, kinds, fwd, bwd = graph_ref.node_group_plan_ref(g.node_offsets.cpu().numpy(),
+                                                            g.in_rowptr.cpu().numpy())
+    assert G == len(kinds) and plan.size == 4 * G + 3
+    np.testing.assert_array_equal(plan[:G + 1], starts)
+    np.testing.assert_array_equal(plan[G + 1:2 * G + 1], kinds)
+    nf, nb = int(plan[2 * G + 1]), int(plan[2 * G + 2])
+    assert sorted(plan[2 * G + 3:2 * G + 3 + nf].tolist()) == sorted(fwd)
+    assert sorted(plan[3 * G + 3:3 * G + 3 + nb].tolist()) == sorted(bwd)
+
+
 def test_build_csr_edge_cases():
     from mvml_gat import batching as G
     graphs = [

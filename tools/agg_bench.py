@@ -50,7 +50,7 @@ def main():
         out = torch.empty((N, oc), device="cuda")
         attn = torch.empty((E, H), device="cuda")
         elr.normal_()
-        f = lambda: call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.node_groups.numel() - 1,
+        f = lambda: call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.num_node_groups,
                          ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(bias), 0.2,
                          mode, ptr(out), ptr(attn), st)
         ms = timeit(f)
@@ -61,7 +61,7 @@ def main():
         gY = torch.empty((N, ldg), device="cuda")
         wsz = L.mvml_gat_agg_bwd_workspace_size(E, H)
         ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
-        b = lambda: call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.node_groups.numel() - 1,
+        b = lambda: call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups,
                          ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst),
                          ptr(g.out_inslot), ptr(Y), ldy, ptr(elr), ptr(attn), ptr(out), ptr(g_out), H, F,
                          0.2, mode, ptr(gY), ldg, ptr(ws), wsz, st)
