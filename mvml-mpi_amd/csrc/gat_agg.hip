@@ -221,46 +221,44 @@ constexpr int kAggThreads = 512;
 #ifndef MVML_LDS_WAVES
 #define MVML_LDS_WAVES 4
 #endif
-// NT = 16 * CW threads: 64 destinations per pass, two passes cover kWinL = 128 atoms; 16 waves
-// per CU either way (2 x 512 threads for CW = 32, 1 x 1024 for CW = 64: half the barriers per
-// byte streamed).
-template <int H, int CW, int MODE, int NT>
-__global__ void __launch_bounds__(NT, MVML_LDS_WAVES)
-gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
-                       const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
-                       int F, const float* __restrict__ bias, const float* __restrict__ attn,
-                       float* __restrict__ out) {
+#ifndef MVML_FWD_RING
+#define MVML_FWD_RING 2
+#endif
+// Chunk loop of the forward LDS kernel for a group of at most NPA * DPP atoms (NPA passes of
+// DPP destinations).  Chunks k+1 .. k+RING are in flight in a register ring while chunk k is
+// aggregated from LDS.  Loads are unconditional (rows past the group read 0 through the buffer
+// resource's range check; chunks past the end use an out-of-range offset), so the loop is
+// straight-line and the compiler's vmcnt waits are exact; stores of rows past the group are
+// skipped (an out-of-range store is not free).
+template <int H, int CW, int MODE, int NT, int NPA>
+__device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)], const float* s_att,
+                                               const int32_t* __restrict__ rowptr,
+                                               const int32_t* __restrict__ in_src,
+                                               __amdgpu_buffer_rsrc_t rY, uint32_t rowb,
+                                               __amdgpu_buffer_rsrc_t rO, int a0, int nr, int e0,
+                                               int F, const float* __restrict__ bias) {
   constexpr int LPD = CW / 4;                        // lanes per destination atom
   constexpr int DPP = NT / LPD;                      // destinations per pass
-  constexpr int NP = (kWinL + DPP - 1) / DPP;        // passes
-  __shared__ float4 zbuf[2][kWinL * LPD];
-  __shared__ float s_att[(kECap + 1) * H];  // + H zeros: the attention of a missing edge
+  constexpr int RING = MVML_FWD_RING;
+  constexpr uint32_t kNone = 0xFFFFFFF0u;            // out of range: reads 0
   const int tid = threadIdx.x;
   const int ds = tid / LPD, q = tid % LPD;
   const int HF = H * F;
-  const GroupPlan gp(plan, G);
-  if (!(gp.kind[blockIdx.x] & 1)) return;
-  const int a0 = gp.start[blockIdx.x], a1 = gp.start[blockIdx.x + 1];
-  const int nr = a1 - a0;
   const int nfc = F / CW;     // column chunks per head
   const int nch = H * nfc;
   const int ocols = MODE == 1 ? F : HF;
-  const int e0 = rowptr[a0];
-  const int ne = rowptr[a1] - e0;
-  for (int i = tid; i < ne * H; i += NT) s_att[i] = attn[(int64_t)e0 * H + i];
-  if (tid < H) s_att[kECap * H + tid] = 0.f;
-  const uint32_t rowb = (uint32_t)ldy * 4u;
-  const __amdgpu_buffer_rsrc_t rY = make_rsrc(Y + (int64_t)a0 * ldy, (uint32_t)nr * rowb);
-  const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)a0 * ocols, (uint32_t)(nr * ocols) * 4u);
   // this thread's destinations: the LDS slots of their first kEC source rows and attention
   // values; a missing edge (i >= in-degree) points at the destination's own row and at a zero
   // attention, so the edge loop is branch- and mask-free (fma(0, z, acc) == acc)
-  int so[NP][kEC], ab[NP], ad[NP];
+  int so[NPA][kEC], ab[NPA], ad[NPA];
+  uint32_t rb[NPA], ob[NPA];  // byte offsets of this thread's rows in Y and in out
+  bool live[NPA];
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
+  for (int p = 0; p < NPA; ++p) {
     const int d = ds + DPP * p;
+    live[p] = d < nr;
     int eb = 0, deg = 0;
-    if (d < nr) {
+    if (live[p]) {
       eb = rowptr[a0 + d] - e0;
       deg = rowptr[a0 + d + 1] - e0 - eb;
     }
@@ -268,97 +266,118 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
     ad[p] = deg;
 #pragma unroll
     for (int i = 0; i < kEC; ++i) {
-      so[p][i] = ((i < deg) ? in_src[e0 + eb + i] - a0 : (d < nr ? d : 0)) * LPD + q;
+      so[p][i] = ((i < deg) ? in_src[e0 + eb + i] - a0 : (live[p] ? d : 0)) * LPD + q;
     }
+    rb[p] = (uint32_t)d * rowb;            // d >= nr: past the resource, reads 0
+    ob[p] = 4u * (uint32_t)(d * ocols);
   }
   // chunk k -> global column of this lane
   auto col_of = [&](int k) {
     return (MODE == 1 ? (k % H) * F + (k / H) * CW : (k / nfc) * F + (k % nfc) * CW) + 4 * q;
   };
-  float4 zA[NP], zB[NP], rres[NP], rnx[NP], tot[NP];
-  auto load_rows = [&](int k, float4 (&dst)[NP]) {
-    if (k >= nch) return;
+  auto load_rows = [&](int k, float4 (&dst)[NPA]) {
+    const bool ok = k < nch;
     const uint32_t cb = 4u * (uint32_t)col_of(k);
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int r = ds + DPP * j;
-      if (r < nr) dst[j] = buf_ld4(rY, (uint32_t)r * rowb + cb);
-    }
+    for (int j = 0; j < NPA; ++j) dst[j] = buf_ld4(rY, ok ? rb[j] + cb : kNone);
   };
-  auto load_res = [&](int k, float4 (&dst)[NP]) {
+  // residual of chunk k (mean mode: of its f-chunk, re-read per head from L2 so that the loop
+  // stays branch-free)
+  auto load_res = [&](int k, float4 (&dst)[NPA]) {
+    const bool ok = k < nch;
     const uint32_t cb = 4u * (uint32_t)(HF + (MODE == 1 ? (k / H) * CW + 4 * q : col_of(k)));
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int r = ds + DPP * j;
-      if (r < nr) dst[j] = buf_ld4(rY, (uint32_t)r * rowb + cb);
-    }
+    for (int j = 0; j < NPA; ++j) dst[j] = buf_ld4(rY, ok ? rb[j] + cb : kNone);
   };
-  auto store_rows = [&](int buf, const float4 (&src)[NP]) {
+  auto store_rows = [&](int buf, const float4 (&src)[NPA]) {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int r = ds + DPP * j;
-      if (r < nr) zbuf[buf][r * LPD + q] = src[j];
-    }
+    for (int j = 0; j < NPA; ++j) zbuf[buf][(ds + DPP * j) * LPD + q] = src[j];
   };
-  // one chunk: aggregate k from zbuf[k & 1] while k+1 (in `nxt`) and k+2 (the other register
-  // slot) are in flight; then stage k+1 and refill its slot with k+3
-  auto step = [&](int k, float4 (&nxt)[NP]) {
+  float4 ring[RING][NPA], rres[NPA], rnx[NPA], tot[NPA];
+  {
+    float4 z0[NPA];
+    load_rows(0, z0);
+#pragma unroll
+    for (int i = 0; i < RING; ++i) load_rows(1 + i, ring[i]);
+    load_res(0, rres);
+    store_rows(0, z0);
+  }
+  __syncthreads();  // chunk 0 and s_att staged
+  for (int k = 0; k < nch; ++k) {
     const int h = MODE == 1 ? k % H : k / nfc;
     const int col = col_of(k);
-    if (MODE != 1) { if (k + 1 < nch) load_res(k + 1, rnx); }
-    else if (h == 0) load_res(k, rres);  // consumed at head H-1, three chunks later
+    load_res(k + 1, rnx);
     const float4 b4 = ld4(bias + col);
     const float4* zl = zbuf[k & 1];
-    float4 acc[NP];
+    float4 acc[NPA];
 #pragma unroll
-    for (int p = 0; p < NP; ++p) acc[p] = f4(0.f);
-#ifndef MVML_AGG_NOEDGE
+    for (int p = 0; p < NPA; ++p) acc[p] = f4(0.f);
 #pragma unroll
-    for (int p = 0; p < NP; ++p)
+    for (int p = 0; p < NPA; ++p)
 #pragma unroll
       for (int i = 0; i < kEC; ++i)
         acc[p] = fma4(s_att[(i < ad[p] ? ab[p] + i * H : kECap * H) + h], zl[so[p][i]], acc[p]);
-#endif
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int d = ds + DPP * p;
-      if (d < nr) {
-        if (MODE == 1) {
-          const float4 t = add4(acc[p], b4);
-          tot[p] = (h == 0) ? t : add4(tot[p], t);
-          if (h == H - 1) {
-            const float invh = (float)H;
-            buf_st4(rO, 4u * (uint32_t)(d * F + (k / H) * CW + 4 * q),
-                    make_float4(tot[p].x / invh + rres[p].x, tot[p].y / invh + rres[p].y,
-                                tot[p].z / invh + rres[p].z, tot[p].w / invh + rres[p].w));
-          }
-        } else {
-          float4 o = add4(add4(acc[p], rres[p]), b4);
-          if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
-          buf_st4(rO, 4u * (uint32_t)(d * HF + col), o);
+    for (int p = 0; p < NPA; ++p) {
+      if (MODE == 1) {
+        const float4 t = add4(acc[p], b4);
+        tot[p] = (h == 0) ? t : add4(tot[p], t);
+        if (h == H - 1 && live[p]) {
+          const float invh = (float)H;
+          buf_st4(rO, ob[p] + 4u * (uint32_t)((k / H) * CW + 4 * q),
+                  make_float4(tot[p].x / invh + rres[p].x, tot[p].y / invh + rres[p].y,
+                              tot[p].z / invh + rres[p].z, tot[p].w / invh + rres[p].w));
         }
+      } else {
+        float4 o = add4(add4(acc[p], rres[p]), b4);
+        if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
+        if (live[p]) buf_st4(rO, ob[p] + 4u * (uint32_t)col, o);
       }
     }
-    if (k + 1 < nch) {
-      store_rows((k + 1) & 1, nxt);
-      load_rows(k + 3, nxt);
-    }
-    if (MODE != 1) {
+    // stage chunk k+1 into the other buffer (read by nobody until the barrier) and rotate
+    store_rows((k + 1) & 1, ring[0]);
 #pragma unroll
-      for (int j = 0; j < NP; ++j) rres[j] = rnx[j];
-    }
+    for (int i = 0; i + 1 < RING; ++i)
+#pragma unroll
+      for (int j = 0; j < NPA; ++j) ring[i][j] = ring[i + 1][j];
+    load_rows(k + 1 + RING, ring[RING - 1]);
+#pragma unroll
+    for (int j = 0; j < NPA; ++j) rres[j] = rnx[j];
     __syncthreads();
-  };
-  load_rows(0, zA);
-  load_rows(1, zB);
-  if (MODE != 1) load_res(0, rres);
-  store_rows(0, zA);
-  load_rows(2, zA);
-  __syncthreads();  // chunk 0 and s_att staged
-  for (int k = 0; k < nch; k += 2) {
-    step(k, zB);                       // zB holds chunk k+1, zA chunk k+2
-    if (k + 1 < nch) step(k + 1, zA);  // zA holds chunk k+2, zB chunk k+3
   }
+}
+
+// NT = 16 * CW threads: 64 destinations per pass; groups of <= 64 atoms (most of them: the
+// target is kNodeGroupAtoms) run one pass, larger ones two (kWinL = 128 atoms).  16 waves per
+// CU either way (2 x 512 threads for CW = 32, 1 x 1024 for CW = 64).
+template <int H, int CW, int MODE, int NT>
+__global__ void __launch_bounds__(NT, MVML_LDS_WAVES)
+gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
+                       const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
+                       int F, const float* __restrict__ bias, const float* __restrict__ attn,
+                       float* __restrict__ out) {
+  constexpr int LPD = CW / 4;
+  constexpr int DPP = NT / LPD;
+  static_assert(2 * DPP == kWinL, "two passes must tile the LDS rows exactly");
+  __shared__ float4 zbuf[2][kWinL * LPD];
+  __shared__ float s_att[(kECap + 1) * H];  // + H zeros: the attention of a missing edge
+  const int tid = threadIdx.x;
+  const GroupPlan gp(plan, G);
+  if (!(gp.kind[blockIdx.x] & 1)) return;
+  const int a0 = gp.start[blockIdx.x], a1 = gp.start[blockIdx.x + 1];
+  const int nr = a1 - a0;
+  const int ocols = MODE == 1 ? F : H * F;
+  const int e0 = rowptr[a0];
+  const int ne = rowptr[a1] - e0;
+  for (int i = tid; i < ne * H; i += NT) s_att[i] = attn[(int64_t)e0 * H + i];
+  if (tid < H) s_att[kECap * H + tid] = 0.f;
+  const uint32_t rowb = (uint32_t)ldy * 4u;
+  const __amdgpu_buffer_rsrc_t rY = make_rsrc(Y + (int64_t)a0 * ldy, (uint32_t)nr * rowb);
+  const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)a0 * ocols, (uint32_t)(nr * ocols) * 4u);
+  if (nr <= DPP)
+    fwd_lds_chunks<H, CW, MODE, NT, 1>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias);
+  else
+    fwd_lds_chunks<H, CW, MODE, NT, 2>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias);
 }
 
 template <int H, int CW, int MODE>
@@ -497,8 +516,141 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
 // then the softmax backward runs in LDS (g_s = a (g_a - sum a g_a), g_pre = g_s leaky') and
 // d er / d el are its per-destination / per-source sums.  Z, g_out and dZ cross HBM once.
 // Every other group (large molecules, edge-heavy hubs) takes the per-atom dst / src pair.
+#ifndef MVML_BWD_WAVES
+#define MVML_BWD_WAVES 4
+#endif
+// Backward LDS layout: Z and g_rst chunks of the group's rows, 16-B slot c of row r at
+// r*8 + (c ^ bwd_sw(r)): the edge role reads whole rows of 16 different atoms per quarter-wave,
+// which unswizzled would all map onto the same two 128-B bank windows.
+__device__ __forceinline__ int bwd_sw(int r) { return (r >> 1) & 7; }
+
+// Chunk loop of the backward LDS kernel for a group of at most NPA * 64 atoms: 8 lanes per row
+// (CW = 32 columns), NPA rows per lane octet.  The chunk rows (Z, g_out, and for ELU' the
+// forward output) stream through a register ring two chunks deep (k+1 and k+2 in flight while
+// chunk k is processed from LDS).  Loads are unconditional (rows past the group read 0 through
+// the buffer resource's range check; chunks past the end use an out-of-range offset), so the
+// loop is straight-line and the vmcnt waits are exact; stores of rows past the group are
+// skipped.  Returns this thread's in-edge g_a partials in ga.
+template <int H, int MODE, int NPA>
+__device__ __forceinline__ void bwd_lds_chunks(
+    float4* zs, float4* gs, const float* s_att, const int* s_odst, const int* s_oslot,
+    const int* s_orp, int es, int ed, bool has_e, __amdgpu_buffer_rsrc_t rY, int ldyi,
+    __amdgpu_buffer_rsrc_t rGo, __amdgpu_buffer_rsrc_t rO, __amdgpu_buffer_rsrc_t rG, int ldgi,
+    int nr, int F, float (&ga)[H]) {
+  constexpr int CW = 32, LPD = CW / 4, DPP = kAggThreads / LPD;
+  constexpr uint32_t kNone = 0xFFFFFFF0u;
+  const int tid = threadIdx.x, ds = tid / LPD, q = tid % LPD;
+  const int HF = H * F, nfc = F / CW, nch = H * nfc;
+  const int ocols = MODE == 1 ? F : HF;
+  uint32_t yrow[NPA], grow[NPA], gorow[NPA], orow[NPA];
+  bool live[NPA];
+  // node role: the g_rst row slots and attention slots of the first kEC out-edges of this
+  // octet's source atoms in registers (a missing edge reads the atom's own row with a zero
+  // attention), so a chunk's gathers are independent LDS reads; more out-edges (hubs) loop.
+  int go[NPA][kEC], ga_[NPA][kEC], ob[NPA], oend[NPA];
+#pragma unroll
+  for (int p = 0; p < NPA; ++p) {
+    const int r = ds + DPP * p;
+    live[p] = r < nr;
+    yrow[p] = 4u * (uint32_t)(r * ldyi);
+    grow[p] = 4u * (uint32_t)(r * ldgi);
+    gorow[p] = 4u * (uint32_t)(r * ocols);
+    orow[p] = 4u * (uint32_t)(r * HF);
+    ob[p] = live[p] ? s_orp[r] : 0;
+    oend[p] = live[p] ? s_orp[r + 1] : 0;
+#pragma unroll
+    for (int i = 0; i < kEC; ++i) {
+      const bool ok = ob[p] + i < oend[p];
+      const int rr = ok ? s_odst[ob[p] + i] : r;
+      go[p][i] = rr * LPD + (q ^ bwd_sw(rr));
+      ga_[p][i] = ok ? s_oslot[ob[p] + i] * H : kECap * H;
+    }
+  }
+  auto head_of = [&](int k) { return MODE == 1 ? k % H : k / nfc; };
+  auto fch_of = [&](int k) { return MODE == 1 ? k / H : k % nfc; };
+  auto col_of = [&](int k) { return head_of(k) * F + fch_of(k) * CW + 4 * q; };
+  struct Rows { float4 z[NPA], g[NPA], o[NPA]; };
+  auto load = [&](int k, Rows& R) {
+    const bool ok = k < nch;
+    const int col = col_of(k);
+    const int gcol = MODE == 1 ? fch_of(k) * CW + 4 * q : col;
+#pragma unroll
+    for (int p = 0; p < NPA; ++p) {
+      R.z[p] = buf_ld4(rY, ok ? yrow[p] + 4u * (uint32_t)col : kNone);
+      R.g[p] = buf_ld4(rGo, ok ? gorow[p] + 4u * (uint32_t)gcol : kNone);
+      if (MODE == 0) R.o[p] = buf_ld4(rO, ok ? orow[p] + 4u * (uint32_t)col : kNone);
+    }
+  };
+  // stage chunk k: g_rst = g_out * ELU'(x) (ELU' = out + 1 for x <= 0, torch elu_backward on
+  // the result) | g_out / H (head mean) | g_out; dR = g_rst, or g_out once per f-chunk (mean)
+  auto stage = [&](int k, const Rows& R) {
+    const bool ok = k < nch;
+    const int h = head_of(k), fc = fch_of(k);
+#pragma unroll
+    for (int p = 0; p < NPA; ++p) {
+      const int r = ds + DPP * p;
+      float4 g = R.g[p];
+      if (MODE == 0) {
+        const float4 o = R.o[p];
+        g.x *= o.x > 0.f ? 1.f : o.x + 1.f;
+        g.y *= o.y > 0.f ? 1.f : o.y + 1.f;
+        g.z *= o.z > 0.f ? 1.f : o.z + 1.f;
+        g.w *= o.w > 0.f ? 1.f : o.w + 1.f;
+      } else if (MODE == 1) {
+        const float hh = (float)H;
+        g = make_float4(g.x / hh, g.y / hh, g.z / hh, g.w / hh);
+      }
+      zs[r * LPD + (q ^ bwd_sw(r))] = R.z[p];
+      gs[r * LPD + (q ^ bwd_sw(r))] = g;
+      if (ok && live[p]) {
+        if (MODE != 1) buf_st4(rG, grow[p] + 4u * (uint32_t)(HF + col_of(k)), g);
+        else if (h == 0) buf_st4(rG, grow[p] + 4u * (uint32_t)(HF + fc * CW + 4 * q), R.g[p]);
+      }
+    }
+  };
+  Rows R1, R2;  // chunks k+1 and k+2
+  {
+    Rows R0;
+    load(0, R0);
+    load(1, R1);
+    load(2, R2);
+    stage(0, R0);
+  }
+  __syncthreads();  // chunk 0
+  for (int k = 0; k < nch; ++k) {
+    const int h = head_of(k);
+    if (has_e) {  // g_a partial of this thread's in-edge
+      float sacc = 0.f;
+#pragma unroll
+      for (int c = 0; c < LPD; ++c)
+        sacc += dot4(zs[es * LPD + (c ^ bwd_sw(es))], gs[ed * LPD + (c ^ bwd_sw(ed))]);
+      add_at<H>(ga, h, sacc);
+    }
+    float4 acc[NPA];  // dZ_agg of the source atoms over their out-edges
+#pragma unroll
+    for (int p = 0; p < NPA; ++p) {
+      acc[p] = f4(0.f);
+#pragma unroll
+      for (int i = 0; i < kEC; ++i) acc[p] = fma4(s_att[ga_[p][i] + h], gs[go[p][i]], acc[p]);
+      for (int o = ob[p] + kEC; o < oend[p]; ++o)
+        acc[p] = fma4(s_att[s_oslot[o] * H + h], gs[s_odst[o] * LPD + (q ^ bwd_sw(s_odst[o]))], acc[p]);
+    }
+    __syncthreads();
+    stage(k + 1, R1);
+    R1 = R2;
+    load(k + 3, R2);
+#pragma unroll
+    for (int p = 0; p < NPA; ++p)
+      if (live[p]) buf_st4(rG, grow[p] + 4u * (uint32_t)col_of(k), acc[p]);
+    __syncthreads();
+  }
+}
+
+// One workgroup of 512 threads per node group (2 per CU): the group's CSR, out-CSR and
+// attention are staged in LDS, the column chunks stream through bwd_lds_chunks (one pass for
+// groups of <= 64 atoms, two up to kWinL), then the softmax backward runs in LDS.
 template <int H, int MODE>
-__global__ void __launch_bounds__(kAggThreads, 4)  // 2 workgroups (16 waves) per CU
+__global__ void __launch_bounds__(kAggThreads, MVML_BWD_WAVES)
 gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                        const int32_t* __restrict__ in_src, const int32_t* __restrict__ out_rowptr,
                        const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
@@ -506,14 +658,10 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
                        const float* __restrict__ attn, const float* __restrict__ out,
                        const float* __restrict__ g_out, float slope, float* __restrict__ gY,
                        int64_t ldgy, int C) {
-  constexpr int CW = 32, LPD = CW / 4, DPP = kAggThreads / LPD, NP = (kWinL + DPP - 1) / DPP;
-  // Z and g_rst chunks of the group's rows, 16-B slot c of row r at r*LPD + (c ^ sw(r)): the
-  // edge role reads whole rows of 16 different atoms per quarter-wave, which unswizzled would
-  // all map onto the same two 128-B bank windows
-  static_assert(LPD == 8, "swizzle assumes 8 slots per row");
+  constexpr int NT = kAggThreads, LPD = 8;
+  static_assert(NT / LPD * 2 == kWinL && NT == kECap, "two passes of 64 rows; one edge per thread");
   __shared__ float4 zs[kWinL * LPD];
   __shared__ float4 gs[kWinL * LPD];
-  auto sw = [](int r) { return (r >> 1) & 7; };
   __shared__ float s_att[(kECap + 1) * H];  // + H zeros: the attention of a missing edge
   __shared__ float s_ga[kECap * H];
   __shared__ int s_src[kECap], s_dst[kECap], s_odst[kECap], s_oslot[kECap];
@@ -522,139 +670,50 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   const GroupPlan gp(plan, G);
   if (!(gp.kind[blockIdx.x] & 2)) return;
   const int a0 = gp.start[blockIdx.x], a1 = gp.start[blockIdx.x + 1];
-  const int tid = threadIdx.x, ds = tid / LPD, q = tid % LPD;
-  const int nr = a1 - a0, HF = H * F, nfc = F / CW, nch = H * nfc;
+  const int tid = threadIdx.x;
+  const int nr = a1 - a0, HF = H * F;
   const int ocols = MODE == 1 ? F : HF;
   const int e0 = rowptr[a0], ne = rowptr[a1] - e0;  // = the group's out-edge range too
-  for (int i = tid; i <= nr; i += kAggThreads) {
+  for (int i = tid; i <= nr; i += NT) {
     s_rp[i] = rowptr[a0 + i] - e0;
     s_orp[i] = out_rowptr[a0 + i] - e0;
   }
-  for (int i = tid; i < ne; i += kAggThreads) {
+  for (int i = tid; i < ne; i += NT) {
     s_src[i] = in_src[e0 + i] - a0;
     s_odst[i] = out_dst[e0 + i] - a0;
     s_oslot[i] = out_inslot[e0 + i] - e0;
   }
-  for (int i = tid; i < ne * H; i += kAggThreads) s_att[i] = attn[(int64_t)e0 * H + i];
+  for (int i = tid; i < ne * H; i += NT) s_att[i] = attn[(int64_t)e0 * H + i];
   if (tid < H) s_att[kECap * H + tid] = 0.f;
-  for (int i = tid; i < nr * 2 * H; i += kAggThreads) s_elr[i] = elr[(int64_t)a0 * 2 * H + i];
-  __syncthreads();
-  for (int d = tid; d < nr; d += kAggThreads)
-    for (int e = s_rp[d]; e < s_rp[d + 1]; ++e) s_dst[e] = d;
+  for (int i = tid; i < nr * 2 * H; i += NT) s_elr[i] = elr[(int64_t)a0 * 2 * H + i];
   const int ldyi = (int)ldy, ldgi = (int)ldgy;
   const __amdgpu_buffer_rsrc_t rY = make_rsrc(Y + (int64_t)a0 * ldy, (uint32_t)(nr * ldyi) * 4u);
   const __amdgpu_buffer_rsrc_t rG = make_rsrc(gY + (int64_t)a0 * ldgy, (uint32_t)(nr * ldgi) * 4u);
   const __amdgpu_buffer_rsrc_t rGo = make_rsrc(g_out + (int64_t)a0 * ocols, (uint32_t)(nr * ocols) * 4u);
   const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)a0 * HF, MODE == 0 ? (uint32_t)(nr * HF) * 4u : 0u);
-
-  auto head_of = [&](int k) { return MODE == 1 ? k % H : k / nfc; };
-  auto fch_of = [&](int k) { return MODE == 1 ? k / H : k % nfc; };
-  // chunk k's rows of this thread: Z and g_out (and out for ELU')
-  float4 zr[NP], gr[NP], orr[NP];
-  auto load = [&](int k) {
-    const int col = head_of(k) * F + fch_of(k) * CW + 4 * q;
-    const int gcol = MODE == 1 ? fch_of(k) * CW + 4 * q : col;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int r = ds + DPP * j;
-      if (r < nr) {
-        zr[j] = buf_ld4(rY, 4u * (uint32_t)(r * ldyi + col));
-        gr[j] = buf_ld4(rGo, 4u * (uint32_t)(r * ocols + gcol));
-        if (MODE == 0) orr[j] = buf_ld4(rO, 4u * (uint32_t)(r * HF + col));
-      }
-    }
-  };
-  // stage chunk k: g_rst = g_out * ELU'(x) (ELU' = out + 1 for x <= 0, torch elu_backward on
-  // the result) | g_out / H (head mean) | g_out; dR = g_rst, or g_out once per f-chunk (mean)
-  auto stage = [&](int k) {
-    const int h = head_of(k), fc = fch_of(k);
-    const int col = h * F + fc * CW + 4 * q;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int r = ds + DPP * j;
-      if (r < nr) {
-        float4 g = gr[j];
-        if (MODE == 0) {
-          const float4 o = orr[j];
-          g.x *= o.x > 0.f ? 1.f : o.x + 1.f;
-          g.y *= o.y > 0.f ? 1.f : o.y + 1.f;
-          g.z *= o.z > 0.f ? 1.f : o.z + 1.f;
-          g.w *= o.w > 0.f ? 1.f : o.w + 1.f;
-        } else if (MODE == 1) {
-          const float hh = (float)H;
-          g = make_float4(g.x / hh, g.y / hh, g.z / hh, g.w / hh);
-        }
-        zs[r * LPD + (q ^ sw(r))] = zr[j];
-        gs[r * LPD + (q ^ sw(r))] = g;
-        if (MODE != 1) buf_st4(rG, 4u * (uint32_t)(r * ldgi + HF + col), g);
-        else if (h == 0) buf_st4(rG, 4u * (uint32_t)(r * ldgi + HF + fc * CW + 4 * q), gr[j]);
-      }
-    }
-  };
+  __syncthreads();  // CSR / attention staged
+  for (int d = tid; d < nr; d += NT)
+    for (int e = s_rp[d]; e < s_rp[d + 1]; ++e) s_dst[e] = d;
+  __syncthreads();
   const bool has_e = tid < ne;
   const int es = has_e ? s_src[tid] : 0;
-  // node role: this thread's source atoms (NP), their first kEC out-edges' g_rst row slots and
-  // attention slots in registers (a missing edge reads the atom's own row with a zero
-  // attention), so a chunk's gathers are independent LDS reads; more out-edges (hubs) loop.
-  int go[NP][kEC], ga_[NP][kEC], oend[NP];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int u = ds + DPP * p;
-    const int ob = u < nr ? s_orp[u] : 0;
-    oend[p] = u < nr ? s_orp[u + 1] : 0;
-#pragma unroll
-    for (int i = 0; i < kEC; ++i) {
-      const bool ok = ob + i < oend[p];
-      const int r = ok ? s_odst[ob + i] : (u < nr ? u : 0);
-      go[p][i] = r * LPD + (q ^ sw(r));
-      ga_[p][i] = ok ? s_oslot[ob + i] * H : kECap * H;
-    }
-  }
+  const int ed = has_e ? s_dst[tid] : 0;
   float ga[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) ga[h] = 0.f;
-  load(0);
-  __syncthreads();  // s_dst
-  stage(0);
-  int ed = 0;
-  if (has_e) ed = s_dst[tid];
-  __syncthreads();
-  for (int k = 0; k < nch; ++k) {
-    const int h = head_of(k);
-    const int col = h * F + fch_of(k) * CW + 4 * q;
-    if (k + 1 < nch) load(k + 1);
-    if (has_e) {  // g_a partial of this thread's in-edge
-      float sacc = 0.f;
-#pragma unroll
-      for (int c = 0; c < LPD; ++c)
-        sacc += dot4(zs[es * LPD + (c ^ sw(es))], gs[ed * LPD + (c ^ sw(ed))]);
-      add_at<H>(ga, h, sacc);
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {  // dZ_agg of source atom u over its out-edges
-      const int u = ds + DPP * p;
-      float4 acc = f4(0.f);
-#pragma unroll
-      for (int i = 0; i < kEC; ++i) acc = fma4(s_att[ga_[p][i] + h], gs[go[p][i]], acc);
-      if (u < nr) {
-        for (int o = s_orp[u] + kEC; o < oend[p]; ++o)
-          acc = fma4(s_att[s_oslot[o] * H + h], gs[s_odst[o] * LPD + (q ^ sw(s_odst[o]))], acc);
-        buf_st4(rG, 4u * (uint32_t)(u * ldgi + col), acc);
-      }
-    }
-    __syncthreads();
-    if (k + 1 < nch) {
-      stage(k + 1);
-      __syncthreads();
-    }
-  }
+  if (nr <= NT / LPD)
+    bwd_lds_chunks<H, MODE, 1>(zs, gs, s_att, s_odst, s_oslot, s_orp, es, ed, has_e, rY, ldyi,
+                               rGo, rO, rG, ldgi, nr, F, ga);
+  else
+    bwd_lds_chunks<H, MODE, 2>(zs, gs, s_att, s_odst, s_oslot, s_orp, es, ed, has_e, rY, ldyi,
+                               rGo, rO, rG, ldgi, nr, F, ga);
   if (has_e) {
 #pragma unroll
     for (int h = 0; h < H; ++h) s_ga[tid * H + h] = ga[h];
   }
   __syncthreads();
   // edge_softmax backward per (destination, head); g_pre replaces g_a in LDS
-  for (int i = tid; i < nr * H; i += kAggThreads) {
+  for (int i = tid; i < nr * H; i += NT) {
     const int d = i / H, h = i % H;
     const int eb = s_rp[d], ee = s_rp[d + 1];
     const float er = s_elr[d * 2 * H + H + h];
@@ -670,7 +729,7 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
     gY[(int64_t)(a0 + d) * ldgy + C + H + h] = der;
   }
   __syncthreads();
-  for (int i = tid; i < nr * H; i += kAggThreads) {  // d el: sums over out-edges
+  for (int i = tid; i < nr * H; i += NT) {  // d el: sums over out-edges
     const int u = i / H, h = i % H;
     float del = 0.f;
     for (int o = s_orp[u]; o < s_orp[u + 1]; ++o) del += s_ga[s_oslot[o] * H + h];

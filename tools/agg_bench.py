@@ -30,6 +30,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mols", type=int, default=65536)
     ap.add_argument("--config", default="3")
+    ap.add_argument("--layers", default="01", help="which layers: 0 = L1 flatten+ELU, 1 = L2 mean")
+    ap.add_argument("--no-bwd", action="store_true")
     a = ap.parse_args()
     sb = getattr(synth, f"config{a.config}")(a.mols)
     g = sb.to_graph().to("cuda")
@@ -37,7 +39,8 @@ def main():
     L = _lib.lib()
     st = _lib.stream_ptr()
     print(f"config{a.config}: {a.mols} molecules, N={N}, E={E}")
-    for (H, F, mode, name) in ((4, 192, 0, "L1 flatten+ELU"), (4, 384, 1, "L2 mean")):
+    layers = ((4, 192, 0, "L1 flatten+ELU"), (4, 384, 1, "L2 mean"))
+    for (H, F, mode, name) in [layers[int(i)] for i in a.layers]:
         C = L.mvml_gat_proj_cols(H, F, int(mode == 1))
         ldy = (C + 3) // 4 * 4
         Y = torch.randn((N, ldy), device="cuda") * 0.3
@@ -56,6 +59,8 @@ def main():
         ms = timeit(f)
         by = agg_fwd_bytes(N, E, H, F, oc, C - H * F)
         print(f"  agg_fwd {name:16s} {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
+        if a.no_bwd:
+            continue
         g_out = torch.randn_like(out)
         ldg = (C + 2 * H + 3) // 4 * 4
         gY = torch.empty((N, ldg), device="cuda")
