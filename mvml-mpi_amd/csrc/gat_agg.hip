@@ -240,7 +240,6 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)],
   constexpr int LPD = CW / 4;                        // lanes per destination atom
   constexpr int DPP = NT / LPD;                      // destinations per pass
   constexpr int RING = MVML_FWD_RING;
-  constexpr uint32_t kNone = 0xFFFFFFF0u;            // out of range: reads 0
   const int tid = threadIdx.x;
   const int ds = tid / LPD, q = tid % LPD;
   const int HF = H * F;
@@ -252,6 +251,10 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)],
   // attention, so the edge loop is branch- and mask-free (fma(0, z, acc) == acc)
   int so[NPA][kEC], ab[NPA], ad[NPA];
   uint32_t rb[NPA], ob[NPA];  // byte offsets of this thread's rows in Y and in out
+  // "no access" offsets: just past the resource's range (reads 0, drops stores) yet next to
+  // the group's own rows, so the address still translates through a warm TLB entry (a wild
+  // out-of-range offset costs a page walk per access)
+  const uint32_t noY = (uint32_t)nr * rowb;
   bool live[NPA];
 #pragma unroll
   for (int p = 0; p < NPA; ++p) {
@@ -279,7 +282,7 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)],
     const bool ok = k < nch;
     const uint32_t cb = 4u * (uint32_t)col_of(k);
 #pragma unroll
-    for (int j = 0; j < NPA; ++j) dst[j] = buf_ld4(rY, ok ? rb[j] + cb : kNone);
+    for (int j = 0; j < NPA; ++j) dst[j] = buf_ld4(rY, ok ? rb[j] + cb : noY);
   };
   // residual of chunk k (mean mode: of its f-chunk, re-read per head from L2 so that the loop
   // stays branch-free)
@@ -287,7 +290,7 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)],
     const bool ok = k < nch;
     const uint32_t cb = 4u * (uint32_t)(HF + (MODE == 1 ? (k / H) * CW + 4 * q : col_of(k)));
 #pragma unroll
-    for (int j = 0; j < NPA; ++j) dst[j] = buf_ld4(rY, ok ? rb[j] + cb : kNone);
+    for (int j = 0; j < NPA; ++j) dst[j] = buf_ld4(rY, ok ? rb[j] + cb : noY);
   };
   auto store_rows = [&](int buf, const float4 (&src)[NPA]) {
 #pragma unroll
@@ -322,7 +325,8 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)],
       if (MODE == 1) {
         const float4 t = add4(acc[p], b4);
         tot[p] = (h == 0) ? t : add4(tot[p], t);
-        if (h == H - 1 && live[p]) {
+        // a store whose lanes are ALL out of range still costs a real one: branch (uniform)
+        if (h == H - 1) {
           const float invh = (float)H;
           buf_st4(rO, ob[p] + 4u * (uint32_t)((k / H) * CW + 4 * q),
                   make_float4(tot[p].x / invh + rres[p].x, tot[p].y / invh + rres[p].y,
@@ -331,7 +335,7 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)],
       } else {
         float4 o = add4(add4(acc[p], rres[p]), b4);
         if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
-        if (live[p]) buf_st4(rO, ob[p] + 4u * (uint32_t)col, o);
+        buf_st4(rO, ob[p] + 4u * (uint32_t)col, o);  // rows past the group: dropped
       }
     }
     // stage chunk k+1 into the other buffer (read by nobody until the barrier) and rotate
@@ -520,50 +524,88 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
 #define MVML_BWD_WAVES 4
 #endif
 // Backward LDS layout: Z and g_rst chunks of the group's rows, 16-B slot c of row r at
-// r*8 + (c ^ bwd_sw(r)): the edge role reads whole rows of 16 different atoms per quarter-wave,
-// which unswizzled would all map onto the same two 128-B bank windows.
+// r*8 + (c ^ bwd_sw(r)) (spreads whole-row reads of different atoms over the banks).
 __device__ __forceinline__ int bwd_sw(int r) { return (r >> 1) & 7; }
+
+// DPP move within a row of 16 lanes (bound_ctrl: sources outside the row read 0).
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// Sum over each aligned octet of lanes; the result is valid in the octet's lanes 4..7.
+__device__ __forceinline__ float octet_sum_hi(float v) {
+  v += dppf<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dppf<0x4E>(v);   // quad_perm [2,3,0,1]
+  return v + dppf<0x114>(v);  // row_shr:4
+}
 
 // Chunk loop of the backward LDS kernel for a group of at most NPA * 64 atoms: 8 lanes per row
 // (CW = 32 columns), NPA rows per lane octet.  The chunk rows (Z, g_out, and for ELU' the
-// forward output) stream through a register ring two chunks deep (k+1 and k+2 in flight while
-// chunk k is processed from LDS).  Loads are unconditional (rows past the group read 0 through
+// forward output) stream through a register ring (k+1 and k+2 in flight while chunk k is
+// processed from LDS; k+1 only for two-pass groups).  Loads are unconditional (rows past the group read 0 through
 // the buffer resource's range check; chunks past the end use an out-of-range offset), so the
 // loop is straight-line and the vmcnt waits are exact; stores of rows past the group are
-// skipped.  Returns this thread's in-edge g_a partials in ga.
+// skipped.
+// Per chunk, the octet of destination atom d also forms g_a[e, h] += <Z[src_e], g_rst[d]> over
+// the chunk's columns for d's in-edges: lane q dots its 16-B slice of the source row (LDS) with
+// its slice of g_rst[d], a DPP octet sum finishes the dot, and one lane per edge adds it to
+// s_ga (zeroed by the caller; every (edge, head) has exactly one writer).  That reads each
+// source row slice once per in-edge: half the LDS bytes of an edge-per-thread dot.
 template <int H, int MODE, int NPA>
 __device__ __forceinline__ void bwd_lds_chunks(
     float4* zs, float4* gs, const float* s_att, const int* s_odst, const int* s_oslot,
-    const int* s_orp, int es, int ed, bool has_e, __amdgpu_buffer_rsrc_t rY, int ldyi,
-    __amdgpu_buffer_rsrc_t rGo, __amdgpu_buffer_rsrc_t rO, __amdgpu_buffer_rsrc_t rG, int ldgi,
-    int nr, int F, float (&ga)[H]) {
+    const int* s_orp, const int* s_rp, const int* s_src, float* s_ga,
+    __amdgpu_buffer_rsrc_t rY, int ldyi, __amdgpu_buffer_rsrc_t rGo, __amdgpu_buffer_rsrc_t rO,
+    __amdgpu_buffer_rsrc_t rG, int ldgi, int nr, int F) {
+  static_assert(kEC == 5, "in-edge writer lanes assume 5 cached in-edges");
   constexpr int CW = 32, LPD = CW / 4, DPP = kAggThreads / LPD;
-  constexpr uint32_t kNone = 0xFFFFFFF0u;
   const int tid = threadIdx.x, ds = tid / LPD, q = tid % LPD;
   const int HF = H * F, nfc = F / CW, nch = H * nfc;
   const int ocols = MODE == 1 ? F : HF;
-  uint32_t yrow[NPA], grow[NPA], gorow[NPA], orow[NPA];
+  // row byte offsets (recomputed where used: registers are the constraint at NPA = 2)
+  auto yrow = [&](int p) { return 4u * (uint32_t)((ds + DPP * p) * ldyi); };
+  auto grow = [&](int p) { return 4u * (uint32_t)((ds + DPP * p) * ldgi); };
+  auto gorow = [&](int p) { return 4u * (uint32_t)((ds + DPP * p) * ocols); };
+  auto orow = [&](int p) { return 4u * (uint32_t)((ds + DPP * p) * HF); };
+  // "no access" offsets just past each resource (see fwd_lds_chunks): every load and store is
+  // unconditional, so the compiler's vmcnt counts are exact
+  const uint32_t noY = 4u * (uint32_t)(nr * ldyi), noGo = 4u * (uint32_t)(nr * ocols);
+  const uint32_t noO = 4u * (uint32_t)(nr * HF), noG = 4u * (uint32_t)(nr * ldgi);
   bool live[NPA];
-  // node role: the g_rst row slots and attention slots of the first kEC out-edges of this
-  // octet's source atoms in registers (a missing edge reads the atom's own row with a zero
-  // attention), so a chunk's gathers are independent LDS reads; more out-edges (hubs) loop.
-  int go[NPA][kEC], ga_[NPA][kEC], ob[NPA], oend[NPA];
+  // node role: the g_rst row slot (low 16 bits) and attention slot (high 16 bits) of the
+  // first kEC out-edges of this octet's source atoms in registers (a missing edge reads the
+  // atom's own row with a zero attention), so a chunk's gathers are independent LDS reads;
+  // more out-edges (hubs) loop.
+  static_assert(kWinL * LPD <= 65536 && (kECap + 1) * H <= 65536, "16-bit slots");
+  uint32_t gsl[NPA][kEC];
+  int ob[NPA], oend[NPA];
 #pragma unroll
   for (int p = 0; p < NPA; ++p) {
     const int r = ds + DPP * p;
     live[p] = r < nr;
-    yrow[p] = 4u * (uint32_t)(r * ldyi);
-    grow[p] = 4u * (uint32_t)(r * ldgi);
-    gorow[p] = 4u * (uint32_t)(r * ocols);
-    orow[p] = 4u * (uint32_t)(r * HF);
     ob[p] = live[p] ? s_orp[r] : 0;
     oend[p] = live[p] ? s_orp[r + 1] : 0;
 #pragma unroll
     for (int i = 0; i < kEC; ++i) {
       const bool ok = ob[p] + i < oend[p];
       const int rr = ok ? s_odst[ob[p] + i] : r;
-      go[p][i] = rr * LPD + (q ^ bwd_sw(rr));
-      ga_[p][i] = ok ? s_oslot[ob[p] + i] * H : kECap * H;
+      gsl[p][i] = (uint32_t)(rr * LPD + (q ^ bwd_sw(rr))) |
+                  ((uint32_t)(ok ? s_oslot[ob[p] + i] * H : kECap * H) << 16);
+    }
+  }
+  // destination role: Z row slots of the first kEC in-edges (own row when missing; the dot is
+  // then discarded), the in-edge base and in-degree
+  uint32_t zsl[NPA][kEC];
+  int ieb[NPA], ideg[NPA];
+#pragma unroll
+  for (int p = 0; p < NPA; ++p) {
+    const int d = ds + DPP * p;
+    ieb[p] = live[p] ? s_rp[d] : 0;
+    ideg[p] = live[p] ? s_rp[d + 1] - ieb[p] : 0;
+#pragma unroll
+    for (int i = 0; i < kEC; ++i) {
+      const int sr = i < ideg[p] ? s_src[ieb[p] + i] : d;
+      zsl[p][i] = (uint32_t)(sr * LPD + (q ^ bwd_sw(sr)));
     }
   }
   auto head_of = [&](int k) { return MODE == 1 ? k % H : k / nfc; };
@@ -576,9 +618,9 @@ __device__ __forceinline__ void bwd_lds_chunks(
     const int gcol = MODE == 1 ? fch_of(k) * CW + 4 * q : col;
 #pragma unroll
     for (int p = 0; p < NPA; ++p) {
-      R.z[p] = buf_ld4(rY, ok ? yrow[p] + 4u * (uint32_t)col : kNone);
-      R.g[p] = buf_ld4(rGo, ok ? gorow[p] + 4u * (uint32_t)gcol : kNone);
-      if (MODE == 0) R.o[p] = buf_ld4(rO, ok ? orow[p] + 4u * (uint32_t)col : kNone);
+      R.z[p] = buf_ld4(rY, ok ? yrow(p) + 4u * (uint32_t)col : noY);
+      R.g[p] = buf_ld4(rGo, ok ? gorow(p) + 4u * (uint32_t)gcol : noGo);
+      if (MODE == 0) R.o[p] = buf_ld4(rO, ok ? orow(p) + 4u * (uint32_t)col : noO);
     }
   };
   // stage chunk k: g_rst = g_out * ELU'(x) (ELU' = out + 1 for x <= 0, torch elu_backward on
@@ -602,46 +644,65 @@ __device__ __forceinline__ void bwd_lds_chunks(
       }
       zs[r * LPD + (q ^ bwd_sw(r))] = R.z[p];
       gs[r * LPD + (q ^ bwd_sw(r))] = g;
-      if (ok && live[p]) {
-        if (MODE != 1) buf_st4(rG, grow[p] + 4u * (uint32_t)(HF + col_of(k)), g);
-        else if (h == 0) buf_st4(rG, grow[p] + 4u * (uint32_t)(HF + fc * CW + 4 * q), R.g[p]);
-      }
+      if (MODE != 1) buf_st4(rG, ok ? grow(p) + 4u * (uint32_t)(HF + col_of(k)) : noG, g);
+      else if (h == 0)  // uniform branch: an all-out-of-range store is not free
+        buf_st4(rG, ok ? grow(p) + 4u * (uint32_t)(HF + fc * CW + 4 * q) : noG, R.g[p]);
     }
   };
-  Rows R1, R2;  // chunks k+1 and k+2
+  // chunks k+1 .. k+RB in flight (two-pass groups already move twice the bytes per chunk)
+  constexpr int RB = NPA == 1 ? 2 : 1;
+  Rows ring[RB];
   {
     Rows R0;
     load(0, R0);
-    load(1, R1);
-    load(2, R2);
+#pragma unroll
+    for (int i = 0; i < RB; ++i) load(1 + i, ring[i]);
     stage(0, R0);
   }
   __syncthreads();  // chunk 0
   for (int k = 0; k < nch; ++k) {
     const int h = head_of(k);
-    if (has_e) {  // g_a partial of this thread's in-edge
-      float sacc = 0.f;
+#ifndef MVML_BWD_NOEDGE
 #pragma unroll
-      for (int c = 0; c < LPD; ++c)
-        sacc += dot4(zs[es * LPD + (c ^ bwd_sw(es))], gs[ed * LPD + (c ^ bwd_sw(ed))]);
-      add_at<H>(ga, h, sacc);
+    for (int p = 0; p < NPA; ++p) {  // g_a partials of the in-edges of destination d
+      const int d = ds + DPP * p;
+      const float4 gd = gs[d * LPD + (q ^ bwd_sw(d))];
+      float t[kEC];
+#pragma unroll
+      for (int i = 0; i < kEC; ++i) t[i] = octet_sum_hi(dot4(zs[zsl[p][i]], gd));
+      if (q >= 4) {  // lanes 4..7 write in-edges 0..3, lane 4 also in-edge 4
+        const int i0 = q - 4;
+        const float v = i0 == 0 ? t[0] : i0 == 1 ? t[1] : i0 == 2 ? t[2] : t[3];
+        if (i0 < ideg[p]) s_ga[(ieb[p] + i0) * H + h] += v;
+        if (i0 == 0 && ideg[p] > 4) s_ga[(ieb[p] + 4) * H + h] += t[4];
+      }
+      for (int i = kEC; i < ideg[p]; ++i) {  // hubs (octet-uniform trip count)
+        const int sr = s_src[ieb[p] + i];
+        const float v = octet_sum_hi(dot4(zs[sr * LPD + (q ^ bwd_sw(sr))], gd));
+        if (q == 4) s_ga[(ieb[p] + i) * H + h] += v;
+      }
     }
+#endif
     float4 acc[NPA];  // dZ_agg of the source atoms over their out-edges
 #pragma unroll
     for (int p = 0; p < NPA; ++p) {
       acc[p] = f4(0.f);
+#ifndef MVML_BWD_NONODE
 #pragma unroll
-      for (int i = 0; i < kEC; ++i) acc[p] = fma4(s_att[ga_[p][i] + h], gs[go[p][i]], acc[p]);
+      for (int i = 0; i < kEC; ++i)
+        acc[p] = fma4(s_att[(gsl[p][i] >> 16) + h], gs[gsl[p][i] & 0xFFFFu], acc[p]);
       for (int o = ob[p] + kEC; o < oend[p]; ++o)
         acc[p] = fma4(s_att[s_oslot[o] * H + h], gs[s_odst[o] * LPD + (q ^ bwd_sw(s_odst[o]))], acc[p]);
+#endif
     }
     __syncthreads();
-    stage(k + 1, R1);
-    R1 = R2;
-    load(k + 3, R2);
+    stage(k + 1, ring[0]);
+#pragma unroll
+    for (int i = 0; i + 1 < RB; ++i) ring[i] = ring[i + 1];
+    load(k + 1 + RB, ring[RB - 1]);
 #pragma unroll
     for (int p = 0; p < NPA; ++p)
-      if (live[p]) buf_st4(rG, grow[p] + 4u * (uint32_t)col_of(k), acc[p]);
+      buf_st4(rG, grow(p) + 4u * (uint32_t)col_of(k), acc[p]);  // rows past the group: dropped
     __syncthreads();
   }
 }
@@ -659,12 +720,12 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
                        const float* __restrict__ g_out, float slope, float* __restrict__ gY,
                        int64_t ldgy, int C) {
   constexpr int NT = kAggThreads, LPD = 8;
-  static_assert(NT / LPD * 2 == kWinL && NT == kECap, "two passes of 64 rows; one edge per thread");
+  static_assert(NT / LPD * 2 == kWinL, "two passes of 64 rows");
   __shared__ float4 zs[kWinL * LPD];
   __shared__ float4 gs[kWinL * LPD];
   __shared__ float s_att[(kECap + 1) * H];  // + H zeros: the attention of a missing edge
   __shared__ float s_ga[kECap * H];
-  __shared__ int s_src[kECap], s_dst[kECap], s_odst[kECap], s_oslot[kECap];
+  __shared__ int s_src[kECap], s_odst[kECap], s_oslot[kECap];
   __shared__ int s_rp[kWinL + 1], s_orp[kWinL + 1];
   __shared__ float s_elr[kWinL * 2 * H];
   const GroupPlan gp(plan, G);
@@ -691,26 +752,14 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   const __amdgpu_buffer_rsrc_t rG = make_rsrc(gY + (int64_t)a0 * ldgy, (uint32_t)(nr * ldgi) * 4u);
   const __amdgpu_buffer_rsrc_t rGo = make_rsrc(g_out + (int64_t)a0 * ocols, (uint32_t)(nr * ocols) * 4u);
   const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)a0 * HF, MODE == 0 ? (uint32_t)(nr * HF) * 4u : 0u);
+  for (int i = tid; i < ne * H; i += NT) s_ga[i] = 0.f;
   __syncthreads();  // CSR / attention staged
-  for (int d = tid; d < nr; d += NT)
-    for (int e = s_rp[d]; e < s_rp[d + 1]; ++e) s_dst[e] = d;
-  __syncthreads();
-  const bool has_e = tid < ne;
-  const int es = has_e ? s_src[tid] : 0;
-  const int ed = has_e ? s_dst[tid] : 0;
-  float ga[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) ga[h] = 0.f;
   if (nr <= NT / LPD)
-    bwd_lds_chunks<H, MODE, 1>(zs, gs, s_att, s_odst, s_oslot, s_orp, es, ed, has_e, rY, ldyi,
-                               rGo, rO, rG, ldgi, nr, F, ga);
+    bwd_lds_chunks<H, MODE, 1>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp, s_src, s_ga, rY,
+                               ldyi, rGo, rO, rG, ldgi, nr, F);
   else
-    bwd_lds_chunks<H, MODE, 2>(zs, gs, s_att, s_odst, s_oslot, s_orp, es, ed, has_e, rY, ldyi,
-                               rGo, rO, rG, ldgi, nr, F, ga);
-  if (has_e) {
-#pragma unroll
-    for (int h = 0; h < H; ++h) s_ga[tid * H + h] = ga[h];
-  }
+    bwd_lds_chunks<H, MODE, 2>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp, s_src, s_ga, rY,
+                               ldyi, rGo, rO, rG, ldgi, nr, F);
   __syncthreads();
   // edge_softmax backward per (destination, head); g_pre replaces g_a in LDS
   for (int i = tid; i < nr * H; i += NT) {

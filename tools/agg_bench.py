@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--config", default="3")
     ap.add_argument("--layers", default="01", help="which layers: 0 = L1 flatten+ELU, 1 = L2 mean")
     ap.add_argument("--no-bwd", action="store_true")
+    ap.add_argument("--no-fwd", action="store_true", help="time only the backward (forward runs once)")
     a = ap.parse_args()
     sb = getattr(synth, f"config{a.config}")(a.mols)
     g = sb.to_graph().to("cuda")
@@ -56,7 +57,11 @@ def main():
         f = lambda: call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.num_node_groups,
                          ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(bias), 0.2,
                          mode, ptr(out), ptr(attn), st)
-        ms = timeit(f)
+        if a.no_fwd:
+            f()
+            ms = float("nan")
+        else:
+            ms = timeit(f)
         by = agg_fwd_bytes(N, E, H, F, oc, C - H * F)
         print(f"  agg_fwd {name:16s} {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
         if a.no_bwd:
