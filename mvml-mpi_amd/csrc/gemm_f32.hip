@@ -23,6 +23,8 @@
 // dropping only a1b2 + a2b1 + a2b2 (< 2^-25 relative per product).  Products of bf16 are exact
 // in fp32, so the result carries fp32 GEMM accuracy (tests/test_gpu_parity.py compares both
 // variants against fp64) at 6 bf16 MFMAs per 16 k instead of 8 f32 MFMAs at 1/16 the rate.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mvml {
@@ -258,12 +260,11 @@ struct ProjEpi {
   float* part;       // [cols / W][2][M]: a wave's stores for one (group, side) are 32 rows, contiguous
 };
 
-// Epilogue of a 128x128 tile held as 2x2 32x32 accumulators per wave (wave (wm, wn) owns rows
-// m0 + 64 wm .., columns n0 + 64 wn ..): optional GAT logit partials, then bias / beta*C /
-// ReLU, or the raw split-K slab.
-template <int EPI_LOGW>
-__device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[2][2], int64_t M, int64_t N,
-                                              int64_t m0, int64_t n0, int wm, int wn, int lane,
+// Epilogue of a wave's FM x FN 32x32 accumulators (rows r0 + 32 i .., columns c0 + 32 j ..):
+// optional GAT logit partials, then bias / beta*C / ReLU, or the raw split-K slab.
+template <int EPI_LOGW, int FM = 2, int FN = 2>
+__device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[FM][FN], int64_t M, int64_t N,
+                                              int64_t r0, int64_t c0, int lane,
                                               const float* __restrict__ bias, float beta, int act,
                                               float* __restrict__ C, int64_t ldc,
                                               float* __restrict__ slab, const ProjEpi& epi) {
@@ -272,10 +273,10 @@ __device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[2][2], int64_t
   if constexpr (EPI_LOGW >= 0) {
     constexpr int W = 1 << EPI_LOGW, NV = 32 >> EPI_LOGW;
   #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int64_t cb0 = n0 + wn * 64 + j * 32;  // first column of this 32-column block
+      for (int j = 0; j < FN; ++j) {
+        const int64_t cb0 = c0 + j * 32;  // first column of this 32-column block
         if (cb0 >= epi.cols) continue;             // wave-uniform
         const int64_t c = cb0 + li;
         const float al = c < epi.cols ? epi.vec[c] : 0.f;
@@ -304,22 +305,22 @@ __device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[2][2], int64_t
           for (int t = 0; t < NV; ++t) {
             const int idx = ((li & (W - 1)) << (5 - EPI_LOGW)) | t;
             const int side = idx >> 4, r = idx & 15;
-            const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+            const int64_t row = r0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
             if (row < M) epi.part[((gc / W) * 2 + side) * M + row] = v[t];
           }
         }
       }
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t col = n0 + wn * 64 + j * 32 + li;
+    for (int j = 0; j < FN; ++j) {
+      const int64_t col = c0 + j * 32 + li;
       if (col >= N) continue;
       const float bcol = (bias && !slab) ? bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        const int64_t row = r0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
         if (row >= M) continue;
         float v = acc[i][j][r];
         if (slab) {
@@ -481,7 +482,8 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     }
   }
 
-  tile_epilogue<EPI_LOGW>(acc, M, N, m0, n0, wm, wn, lane, bias, beta, act, C, ldc, slab, epi);
+  tile_epilogue<EPI_LOGW>(acc, M, N, m0 + wm * 64, n0 + wn * 64, lane, bias, beta, act, C, ldc,
+                          slab, epi);
 }
 
 // ---- split-bf16 GEMM with the split done once per workgroup, at staging -------------------
@@ -650,7 +652,225 @@ gemm_x3s_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       acc[1][1] = mfma_x3(pa[1], pb[1], acc[1][1]);
     }
   }
-  tile_epilogue<EPI_LOGW>(acc, M, N, m0, n0, wm, wn, lane, bias, beta, act, C, ldc, slab, epi);
+  tile_epilogue<EPI_LOGW>(acc, M, N, m0 + wm * 64, n0 + wn * 64, lane, bias, beta, act, C, ldc,
+                          slab, epi);
+}
+
+// ---- 256x256 split-bf16 GEMM, one workgroup per CU ---------------------------------------
+// 512 threads = 8 waves as 2 (M) x 4 (N); a wave owns 128 x 64 outputs = 4 x 2 accumulators of
+// 32x32 (48 MFMAs per 16-deep k step: 4x the MFMAs per staged element of the 128x128 kernels,
+// so the per-element split and LDS writes are a quarter of the cost).  K is staged 16 deep: the
+// next fp32 tile (8 values per thread per operand) is loaded into registers one stage ahead,
+// split into three bf16 terms and written into the free half of a double-buffered LDS image
+// while the current stage's MFMAs run; one barrier per stage.
+//  * K-contiguous operands ([rows][K]) live as [row][16 k] bf16 planes (32-B rows; the 16-B
+//    chunk XOR-ed with row bit 3), read as 32x32x16 fragments by one ds_read_b128 per plane
+//    (conflict-free over the instruction's 16-lane groups).
+//  * K-major operands ([K][rows]) live as [k][256 rows] bf16 planes (k-row pitch 576 B: the four
+//    k rows of a transposed read land on four different bank quarters) and are read by two
+//    ds_read_b64_tr_b16 per plane — the hardware transpose delivers a lane its row's 8
+//    consecutive k — so both layouts are staged with contiguous, conflict-free writes.
+constexpr int XBM = 256, XBN = 256, XBK = 16, kXThreads = 512;
+constexpr int kXKmajPitch = 576;
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+template <bool KMAJ>
+struct XOp {
+  static constexpr int kPlane = KMAJ ? XBK * kXKmajPitch : 256 * 32;
+  static constexpr int kBytes = 3 * kPlane;
+
+  // This thread's 8 values of a 256 x 16 operand tile (rows r0.., k0..):
+  //  K-contiguous: rows (tid >> 2) + 128 i, k = 4 (tid & 3) + [0, 4) in v[i] (16 rows x 64 B per
+  //  wave-instruction); K-major: k = 2 (tid >> 6) + i, rows 4 (tid & 63) + [0, 4) in v[i] (1 KB
+  //  contiguous per wave-instruction).  Guarded path zero-fills rows >= rows, k >= kend.
+  __device__ static __forceinline__ void load(const float* __restrict__ P, int64_t ld, int64_t r0,
+                                              int64_t rows, int64_t k0, int64_t kend, bool fast,
+                                              int tid, float4 (&v)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (!KMAJ) {
+        const int64_t row = r0 + (tid >> 2) + 128 * i, k = k0 + 4 * (tid & 3);
+        if (fast) {
+          v[i] = *reinterpret_cast<const float4*>(P + row * ld + k);
+        } else {
+          float e[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) e[j] = (row < rows && k + j < kend) ? P[row * ld + k + j] : 0.f;
+          v[i] = make_float4(e[0], e[1], e[2], e[3]);
+        }
+      } else {
+        const int64_t k = k0 + 2 * (tid >> 6) + i, row = r0 + 4 * (tid & 63);
+        if (fast) {
+          v[i] = *reinterpret_cast<const float4*>(P + k * ld + row);
+        } else {
+          float e[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) e[j] = (k < kend && row + j < rows) ? P[k * ld + row + j] : 0.f;
+          v[i] = make_float4(e[0], e[1], e[2], e[3]);
+        }
+      }
+    }
+  }
+
+  // Fast path: this thread's two source pointers, rows clamped into range (a clamped row only
+  // feeds output rows / columns that are never stored; K-major needs rows % 4 == 0 or a full
+  // tile so that no float4 straddles the edge), advanced by kStep floats per stage.
+  __device__ static __forceinline__ void ptrs(const float* __restrict__ P, int64_t ld, int64_t r0,
+                                              int64_t rows, int64_t k0, int tid,
+                                              const float* (&p)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (!KMAJ) {
+        const int64_t row = min(r0 + (tid >> 2) + 128 * i, rows - 1);
+        p[i] = P + row * ld + k0 + 4 * (tid & 3);
+      } else {
+        const int64_t row = min(r0 + 4 * (tid & 63), rows - 4);
+        p[i] = P + (k0 + 2 * (tid >> 6) + i) * ld + row;
+      }
+    }
+  }
+  __device__ static __forceinline__ int64_t kstep(int64_t ld) { return KMAJ ? XBK * ld : XBK; }
+  __device__ static __forceinline__ bool fast_ok(bool vec, int64_t r0, int64_t rows) {
+    return vec && (!KMAJ || (rows % 4 == 0 && rows >= 4) || r0 + 256 <= rows);
+  }
+
+  __device__ static __forceinline__ void split_store(uint8_t* op, int tid, const float4 (&v)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint2 p0, p1, p2;
+      split4(v[i].x, v[i].y, v[i].z, v[i].w, p0, p1, p2);
+      uint32_t off;
+      if (!KMAJ) {
+        const int row = (tid >> 2) + 128 * i, q = tid & 3;
+        off = row * 32 + (((q >> 1) ^ ((row >> 3) & 1)) << 4) + 8 * (q & 1);
+      } else {
+        off = (2 * (tid >> 6) + i) * kXKmajPitch + 8 * (tid & 63);
+      }
+      *reinterpret_cast<uint2*>(op + off) = p0;
+      *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
+      *reinterpret_cast<uint2*>(op + 2 * kPlane + off) = p2;
+    }
+  }
+
+  // 32x32x16 operand fragment of tile rows R0 .. R0+31, plane p: lane l holds row R0 + (l & 31),
+  // k = 8 (l >> 5) + [0, 8).
+  __device__ static __forceinline__ bf16x8 frag(const uint8_t* op, int p, int R0, int lane) {
+    const uint8_t* pl = op + p * kPlane;
+    if (!KMAJ) {
+      const int row = R0 + (lane & 31);
+      return *reinterpret_cast<const bf16x8*>(pl + row * 32 + (((lane >> 5) ^ ((row >> 3) & 1)) << 4));
+    } else {
+      // ds_read_b64_tr_b16: 16-lane group g reads k rows k0 .. k0+3, columns mb .. mb+15; lane
+      // 4q+p of the group addresses row q, columns 4p .. 4p+3 and receives column (lane & 15)
+      const int g = lane >> 4, i = lane & 15;
+      const int mb = R0 + 16 * (g & 1), k0 = 8 * (g >> 1);
+      const uint8_t* a = pl + (k0 + (i >> 2)) * kXKmajPitch + 2 * (mb + 4 * (i & 3));
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 4 * kXKmajPitch));
+      const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8, r);
+    }
+  }
+};
+
+#ifndef MVML_X3W_WAVES
+#define MVML_X3W_WAVES 2
+#endif
+template <bool AK, bool BKM, int EPI_LOGW = -1>
+__global__ void __launch_bounds__(kXThreads, MVML_X3W_WAVES)  // one workgroup per CU
+gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
+                const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
+                float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
+                float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{}) {
+  using OA = XOp<AK>;
+  using OB = XOp<BKM>;
+  constexpr int kStage = OA::kBytes + OB::kBytes;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kStage];
+  const int64_t tiles_n = ceil_div(N, XBN);
+  const int64_t tile = xcd_block(blockIdx.x, gridDim.x);
+  const int64_t m0 = (tile / tiles_n) * XBM, n0 = (tile % tiles_n) * XBN;
+  const int64_t kbeg = (int64_t)blockIdx.y * k_split;
+  const int64_t kend = min(K, kbeg + k_split);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int64_t ntiles = (kend > kbeg) ? ceil_div(kend - kbeg, XBK) : 0;
+  // fast: unguarded float4 loads from clamped rows for every full 16-deep stage; the guarded
+  // path covers the K tail and operands that are unaligned / K-major with a ragged edge
+  const bool fast = OA::fast_ok(a_vec, m0, M) && OB::fast_ok(b_vec, n0, N);
+  const float* pa[2];
+  const float* pb[2];
+  OA::ptrs(A, lda, m0, M, kbeg, tid, pa);
+  OB::ptrs(B, ldb, n0, N, kbeg, tid, pb);
+  const int64_t sa_step = OA::kstep(lda), sb_step = OB::kstep(ldb);
+  float4 va[2], vb[2];
+  auto load_tile = [&](int64_t k0) {
+    if (fast && k0 + XBK <= kend) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        va[i] = *reinterpret_cast<const float4*>(pa[i]);
+        vb[i] = *reinterpret_cast<const float4*>(pb[i]);
+        pa[i] += sa_step;
+        pb[i] += sb_step;
+      }
+    } else {
+      const bool kin = k0 + XBK <= kend;
+      OA::load(A, lda, m0, M, k0, kend, a_vec && m0 + XBM <= M && kin, tid, va);
+      OB::load(B, ldb, n0, N, k0, kend, b_vec && n0 + XBN <= N && kin, tid, vb);
+    }
+  };
+  auto stage = [&](int buf) {
+    OA::split_store(lds + buf * kStage, tid, va);
+    OB::split_store(lds + buf * kStage + OA::kBytes, tid, vb);
+  };
+  if (ntiles > 0) {
+    load_tile(kbeg);
+    stage(0);
+    if (ntiles > 1) load_tile(kbeg + XBK);
+  }
+  __syncthreads();
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const uint8_t* sa = lds + (t & 1) * kStage;
+    const uint8_t* sb = sa + OA::kBytes;
+    bf16x8 fb[2][3];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fb[j][p] = OB::frag(sb, p, wn * 64 + 32 * j, lane);
+    // stage tile t+1 into the other buffer (its readers finished before the last barrier) and
+    // re-issue the loads for t+2 behind the MFMAs
+    if (t + 1 < ntiles) {
+      stage((t + 1) & 1);
+      if (t + 2 < ntiles) load_tile(kbeg + (t + 2) * XBK);
+    }
+#ifndef MVML_X3W_PRIO
+#define MVML_X3W_PRIO 1
+#endif
+    if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8 fa[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fa[p] = OA::frag(sa, p, wm * 128 + 32 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x3(fa, fb[j], acc[i][j]);
+    }
+    if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(0);
+    __syncthreads();
+  }
+  tile_epilogue<EPI_LOGW, 4, 2>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta, act, C,
+                                ldc, slab, epi);
 }
 
 // Sum S split-K slabs in fixed order: C = act(sum_z slab[z] + bias + beta*C).
@@ -674,9 +894,9 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int S, const float* _
 // Split-K policy for small-output / long-K products (the weight gradients): pick the split
 // count that fills whole rounds of resident workgroups (256 CUs x 2) best, keeping >= 1024 K
 // per split so the slab reduction stays negligible.
-int choose_splits(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
-  const int64_t slots = 512;
+// Split-K count for `tiles` output tiles over `slots` concurrent workgroups: the count that
+// best fills whole waves of workgroups, keeping >= 1024 k per split.
+int choose_splits_t(int64_t tiles, int64_t K, int64_t slots) {
   if (tiles >= 2 * slots || K < 2048) return 1;
   int best = 1;
   double best_eff = (double)tiles / (double)(ceil_div(tiles, slots) * slots);
@@ -687,6 +907,28 @@ int choose_splits(int64_t M, int64_t N, int64_t K) {
     if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
   }
   return best;
+}
+
+// Kernel plan of a product: the 256x256 split-bf16 kernel (one workgroup per CU) whenever its
+// tiles x splits fill the chip, the 128x128 kernels (two per CU) otherwise.  MVML_X3_TILE=128 /
+// 256 forces a tile size (tests).
+struct GemmPlan {
+  bool wide;
+  int S;
+};
+GemmPlan plan_gemm(bool x3, int64_t M, int64_t N, int64_t K) {
+  const char* env = getenv("MVML_X3_TILE");
+  const int force = env ? atoi(env) : 0;
+  if (x3) {
+    const int64_t tw = ceil_div(M, XBM) * ceil_div(N, XBN);
+    const int Sw = choose_splits_t(tw, K, 256);
+    if (force == 256 || (force != 128 && tw * Sw >= 192)) return {true, Sw};
+  }
+  return {false, choose_splits_t(ceil_div(M, BM) * ceil_div(N, BN), K, 512)};
+}
+int choose_splits(int64_t M, int64_t N, int64_t K) {  // the larger of the two plans' counts
+  return std::max(choose_splits_t(ceil_div(M, XBM) * ceil_div(N, XBN), K, 256),
+                  choose_splits_t(ceil_div(M, BM) * ceil_div(N, BN), K, 512));
 }
 
 int64_t k_chunk(int64_t K, int S) { return ceil_div(ceil_div(K, S), BKT) * BKT; }
@@ -776,7 +1018,8 @@ int gemm_launch(bool x3, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
   MVML_REQUIRE(b_kmajor ? ldb >= N : ldb >= K, "gemm: bad ldb");
   MVML_REQUIRE(act == 0 || act == 1, "gemm: bad act");
   hipStream_t st = as_stream(stream);
-  const int S = choose_splits(M, N, K);
+  const GemmPlan plan = plan_gemm(x3, M, N, K);
+  const int S = plan.S;
   float* slab = nullptr;
   if (S > 1) {
     if (workspace_bytes < mvml_gemm_workspace_size(M, N, K) || !workspace) {
@@ -786,14 +1029,17 @@ int gemm_launch(bool x3, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
     slab = static_cast<float*>(workspace);
   }
   const int64_t kc = S > 1 ? k_chunk(K, S) : (K > 0 ? K : 1);
-  const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
+  const int64_t tiles = plan.wide ? ceil_div(M, XBM) * ceil_div(N, XBN) : ceil_div(M, BM) * ceil_div(N, BN);
   MVML_REQUIRE(tiles < (int64_t(1) << 31), "gemm: too many tiles");
   const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0);
   const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0);
   dim3 grid((unsigned)tiles, (unsigned)S);
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
   do {                                                                                          \
-    if (x3 && AKV && BKV) /* both k-major (weight gradients): fragment split measured faster */ \
+    if (plan.wide)                                                                              \
+      gemm_x3w_kernel<AKV, BKV><<<grid, kXThreads, 0, st>>>(                                    \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+    else if (x3 && AKV && BKV) /* both k-major: fragment split measured faster at 128x128 */    \
       gemm_f32_kernel<AKV, BKV, -1, true><<<grid, kThreads, 0, st>>>(                           \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
     else if (x3)                                                                                \
@@ -826,7 +1072,8 @@ namespace mvml {
 int gemm_proj_epi(bool x3, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                   const float* B, int64_t ldb, float* C, int64_t ldc, const float* vec, int cols,
                   int logw, float* part, hipStream_t st) {
-  const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
+  const bool wide = x3 && plan_gemm(true, M, N, K).wide;
+  const int64_t tiles = wide ? ceil_div(M, XBM) * ceil_div(N, XBN) : ceil_div(M, BM) * ceil_div(N, BN);
   MVML_REQUIRE(tiles < (int64_t(1) << 31), "gat_proj_fwd: too many tiles");
   MVML_REQUIRE(cols <= N && (logw >= 2 && logw <= 5), "gat_proj_fwd: bad partial width");
   const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0);
@@ -834,7 +1081,11 @@ int gemm_proj_epi(bool x3, int64_t M, int64_t N, int64_t K, const float* A, int6
   dim3 grid((unsigned)tiles, 1);
 #define MVML_PROJ(LW)                                                                          \
   do {                                                                                         \
-    if (x3)                                                                                    \
+    if (wide)                                                                                  \
+      gemm_x3w_kernel<false, false, LW><<<grid, kXThreads, 0, st>>>(                           \
+          M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
+          ProjEpi{vec, cols, part});                                                           \
+    else if (x3)                                                                               \
       gemm_x3s_kernel<false, false, LW><<<grid, kThreads, 0, st>>>(                            \
           M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
           ProjEpi{vec, cols, part});                                                           \

@@ -86,12 +86,33 @@ def test_build_csr_rejects_bad_ids():
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.mark.parametrize("algo", ["f32", "x3"])
+import contextlib  # noqa: E402
+import os  # noqa: E402
+
+
+@contextlib.contextmanager
+def _x3_tile(algo):
+    """'x3-128' / 'x3-256' force the split-bf16 tile size (MVML_X3_TILE, read per call)."""
+    old = os.environ.pop("MVML_X3_TILE", None)
+    if algo.startswith("x3-"):
+        os.environ["MVML_X3_TILE"] = algo[3:]
+    try:
+        yield algo.split("-")[0]
+    finally:
+        os.environ.pop("MVML_X3_TILE", None)
+        if old is not None:
+            os.environ["MVML_X3_TILE"] = old
+
+
+@pytest.mark.parametrize("algo", ["f32", "x3", "x3-128", "x3-256"])
 @pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (130, 70, 74), (257, 300, 768), (96, 40, 20000),
-                                   (256, 384, 1000), (640, 512, 4000), (1000, 1928, 768)])
+                                   (256, 384, 1000), (640, 512, 4000), (1000, 1928, 768),
+                                   (512, 384, 65536 + 17)])
 def test_gemm_layouts(ak, bk, M, N, K, algo):
     from mvml_gat.functional import gemm
+    if K > 50000 and algo in ("f32", "x3-128"):
+        pytest.skip("long-K case targets the 256x256 split-K path")
     g = torch.Generator().manual_seed(M * 7 + N + K)
     A = torch.randn(M, K, generator=g, dtype=torch.float64)
     B = torch.randn(K, N, generator=g, dtype=torch.float64)
@@ -100,8 +121,9 @@ def test_gemm_layouts(ak, bk, M, N, K, algo):
     Ad = (A.t() if ak else A).contiguous().float().to(DEV)
     Bd = (B if bk else B.t()).contiguous().float().to(DEV)
     C = C0.float().to(DEV)
-    gemm(Ad, Bd, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N, bias=bias.float().to(DEV),
-         beta=0.5, act=1, algo=algo)
+    with _x3_tile(algo) as a:
+        gemm(Ad, Bd, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N,
+             bias=bias.float().to(DEV), beta=0.5, act=1, algo=a)
     ref = torch.relu(A @ B + bias + 0.5 * C0)
     assert rel_err(C, ref) < TOL
 
@@ -118,15 +140,17 @@ def test_gemm_x3_error_matches_fp32(K):
     B = torch.randn(K, N, generator=g, dtype=torch.float64)
     ref = A @ B
     errs = {}
-    for algo in ("f32", "x3"):
+    for algo in ("f32", "x3", "x3-256"):
         C = torch.zeros(M, N, device=DEV)
-        gemm(A.float().to(DEV), B.t().contiguous().float().to(DEV), M, N, K, 0, 0, K, K, C, N, algo=algo)
+        with _x3_tile(algo) as a:
+            gemm(A.float().to(DEV), B.t().contiguous().float().to(DEV), M, N, K, 0, 0, K, K, C, N, algo=a)
         d = (C.double().cpu() - ref)
         errs[algo] = (d.abs().max().item(), d.pow(2).mean().sqrt().item())
     cpu = (A.float() @ B.float()).double() - ref
     errs["cpu"] = (cpu.abs().max().item(), cpu.pow(2).mean().sqrt().item())
     base = max(errs["f32"][0], errs["cpu"][0]), max(errs["f32"][1], errs["cpu"][1])
-    assert errs["x3"][0] <= 2 * base[0] and errs["x3"][1] <= 2 * base[1], errs
+    for algo in ("x3", "x3-256"):
+        assert errs[algo][0] <= 2 * base[0] and errs[algo][1] <= 2 * base[1], errs
 
 
 def test_colsum():

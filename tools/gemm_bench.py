@@ -36,18 +36,29 @@ def tf(fn, flops, it=10):
 def main():
     dev = "cuda"
     torch.manual_seed(0)
-    for name, M, N, K, ak, bk in SHAPES:
+    algos = sys.argv[1].split(",") if len(sys.argv) > 1 else ["x3-128", "x3-256"]
+    shapes = SHAPES
+    if len(sys.argv) > 2:  # e.g. "0,4": indices into SHAPES
+        shapes = [SHAPES[int(i)] for i in sys.argv[2].split(",")]
+    for name, M, N, K, ak, bk in shapes:
         A = torch.randn((K, M) if ak else (M, K), device=dev)
         Bm = torch.randn((K, N) if bk else (N, K), device=dev)
         C = torch.empty((M, N), device=dev)
         flops = 2 * M * N * K
-        ms, t = tf(lambda: gemm(A, Bm, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N, algo="f32"), flops)
-        ms3, t3 = tf(lambda: gemm(A, Bm, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N, algo="x3"), flops)
-        At = A.t() if ak else A
-        Bt = Bm if bk else Bm.t()
-        ms2, t2 = tf(lambda: torch.matmul(At, Bt, out=C), flops)
-        print(f"{name:22s} M={M:8d} N={N:5d} K={K:8d}  f32 {ms:8.3f} ms {t:6.1f} TF/s | x3 {ms3:8.3f} ms "
-              f"{t3:6.1f} TF/s | torch {ms2:8.3f} ms {t2:6.1f} TF/s", flush=True)
+        cols = []
+        for algo in algos:
+            if algo == "torch":
+                At = A.t() if ak else A
+                Bt = Bm if bk else Bm.t()
+                ms, t = tf(lambda: torch.matmul(At, Bt, out=C), flops)
+            else:
+                os.environ.pop("MVML_X3_TILE", None)
+                if algo.startswith("x3-"):
+                    os.environ["MVML_X3_TILE"] = algo[3:]
+                a = algo.split("-")[0]
+                ms, t = tf(lambda: gemm(A, Bm, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N, algo=a), flops)
+            cols.append(f"{algo} {ms:8.3f} ms {t:6.1f} TF/s")
+        print(f"{name:22s} M={M:8d} N={N:5d} K={K:8d}  " + " | ".join(cols), flush=True)
         del A, Bm, C
         torch.cuda.empty_cache()
 
