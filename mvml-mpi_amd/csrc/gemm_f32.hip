@@ -24,6 +24,7 @@
 // in fp32, so the result carries fp32 GEMM accuracy (tests/test_gpu_parity.py compares both
 // variants against fp64) at 6 bf16 MFMAs per 16 k instead of 8 f32 MFMAs at 1/16 the rate.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -733,9 +734,7 @@ struct XOp {
     }
   }
   __device__ static __forceinline__ int64_t kstep(int64_t ld) { return KMAJ ? XBK * ld : XBK; }
-  __device__ static __forceinline__ bool fast_ok(bool vec, int64_t r0, int64_t rows) {
-    return vec && (!KMAJ || (rows % 4 == 0 && rows >= 4) || r0 + 256 <= rows);
-  }
+
 
   __device__ static __forceinline__ void split_store(uint8_t* op, int tid, const float4 (&v)[2]) {
 #pragma unroll
@@ -779,7 +778,10 @@ struct XOp {
 #ifndef MVML_X3W_WAVES
 #define MVML_X3W_WAVES 2
 #endif
-template <bool AK, bool BKM, int EPI_LOGW = -1>
+// FAST (host-checked: both operands 16-B aligned rows, K-major row counts % 4 == 0): whole
+// stages by unguarded loads from clamped rows, the K tail as one guarded stage; !FAST: every
+// stage guarded.
+template <bool AK, bool BKM, int EPI_LOGW = -1, bool FAST = true>
 __global__ void __launch_bounds__(kXThreads, MVML_X3W_WAVES)  // one workgroup per CU
 gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
@@ -806,41 +808,69 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int64_t ntiles = (kend > kbeg) ? ceil_div(kend - kbeg, XBK) : 0;
-  // fast: unguarded float4 loads from clamped rows for every full 16-deep stage; the guarded
-  // path covers the K tail and operands that are unaligned / K-major with a ragged edge
-  const bool fast = OA::fast_ok(a_vec, m0, M) && OB::fast_ok(b_vec, n0, N);
+  const int64_t nfull = (kend > kbeg) ? (kend - kbeg) / XBK : 0;  // whole 16-deep stages
   const float* pa[2];
   const float* pb[2];
   OA::ptrs(A, lda, m0, M, kbeg, tid, pa);
   OB::ptrs(B, ldb, n0, N, kbeg, tid, pb);
   const int64_t sa_step = OA::kstep(lda), sb_step = OB::kstep(ldb);
   float4 va[2], vb[2];
-  auto load_tile = [&](int64_t k0) {
-    if (fast && k0 + XBK <= kend) {
+  auto load_fast = [&]() {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        va[i] = *reinterpret_cast<const float4*>(pa[i]);
-        vb[i] = *reinterpret_cast<const float4*>(pb[i]);
-        pa[i] += sa_step;
-        pb[i] += sb_step;
-      }
-    } else {
-      const bool kin = k0 + XBK <= kend;
-      OA::load(A, lda, m0, M, k0, kend, a_vec && m0 + XBM <= M && kin, tid, va);
-      OB::load(B, ldb, n0, N, k0, kend, b_vec && n0 + XBN <= N && kin, tid, vb);
+    for (int i = 0; i < 2; ++i) {
+      va[i] = *reinterpret_cast<const float4*>(pa[i]);
+      vb[i] = *reinterpret_cast<const float4*>(pb[i]);
+      pa[i] += sa_step;
+      pb[i] += sb_step;
     }
+  };
+  // fast load of a stage that may be the K tail: addresses clamped to k < kend (host: kend %
+  // 4 == 0), A's values at k >= kend zeroed, so B's clamped (finite) values add nothing
+  auto load_masked = [&](int64_t t) {
+    const int64_t k0 = kbeg + t * XBK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int64_t ka, kb_;  // this thread's k for operand A / B piece i
+      const float* qa;
+      const float* qb;
+      if (!AK) {
+        ka = k0 + 4 * (tid & 3);
+        qa = pa[i] + (min(ka, kend - 4) - ka);
+      } else {
+        ka = k0 + 2 * (tid >> 6) + i;
+        qa = pa[i] + (min(ka, kend - 1) - ka) * lda;
+      }
+      if (!BKM) {
+        kb_ = k0 + 4 * (tid & 3);
+        qb = pb[i] + (min(kb_, kend - 4) - kb_);
+      } else {
+        kb_ = k0 + 2 * (tid >> 6) + i;
+        qb = pb[i] + (min(kb_, kend - 1) - kb_) * ldb;
+      }
+      const float4 a = *reinterpret_cast<const float4*>(qa);
+      va[i] = ka < kend ? a : make_float4(0.f, 0.f, 0.f, 0.f);
+      vb[i] = *reinterpret_cast<const float4*>(qb);
+      pa[i] += sa_step;
+      pb[i] += sb_step;
+    }
+  };
+  auto load_guarded = [&](int64_t t) {
+    const int64_t k0 = kbeg + t * XBK;
+    const bool kin = k0 + XBK <= kend;
+    OA::load(A, lda, m0, M, k0, kend, a_vec && m0 + XBM <= M && kin, tid, va);
+    OB::load(B, ldb, n0, N, k0, kend, b_vec && n0 + XBN <= N && kin, tid, vb);
   };
   auto stage = [&](int buf) {
     OA::split_store(lds + buf * kStage, tid, va);
     OB::split_store(lds + buf * kStage + OA::kBytes, tid, vb);
   };
-  if (ntiles > 0) {
-    load_tile(kbeg);
-    stage(0);
-    if (ntiles > 1) load_tile(kbeg + XBK);
-  }
-  __syncthreads();
-  for (int64_t t = 0; t < ntiles; ++t) {
+#ifndef MVML_X3W_PRIO
+#define MVML_X3W_PRIO 1
+#endif
+  // One 16-deep stage: fragments of stage t from LDS buffer t & 1; with STAGE, split + store
+  // stage t+1 (in va / vb) into the other buffer; LOAD: 0 none, 1 fast, 2 guarded load of t+2.
+  // Each (STAGE, LOAD) is its own straight-line body: no control flow around the accumulators.
+  auto body = [&](int64_t t, auto STAGE, auto LOAD) {
     const uint8_t* sa = lds + (t & 1) * kStage;
     const uint8_t* sb = sa + OA::kBytes;
     bf16x8 fb[2][3];
@@ -848,15 +878,10 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int p = 0; p < 3; ++p) fb[j][p] = OB::frag(sb, p, wn * 64 + 32 * j, lane);
-    // stage tile t+1 into the other buffer (its readers finished before the last barrier) and
-    // re-issue the loads for t+2 behind the MFMAs
-    if (t + 1 < ntiles) {
-      stage((t + 1) & 1);
-      if (t + 2 < ntiles) load_tile(kbeg + (t + 2) * XBK);
-    }
-#ifndef MVML_X3W_PRIO
-#define MVML_X3W_PRIO 1
-#endif
+    if constexpr (decltype(STAGE)::value) stage((t + 1) & 1);
+    if constexpr (decltype(LOAD)::value == 1) load_fast();
+    if constexpr (decltype(LOAD)::value == 2) load_guarded(t + 2);
+    if constexpr (decltype(LOAD)::value == 3) load_masked(t + 2);
     if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -868,9 +893,59 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     }
     if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  using L0 = std::integral_constant<int, 0>;
+  using L1 = std::integral_constant<int, 1>;
+  using L2 = std::integral_constant<int, 2>;
+  if constexpr (FAST) {
+    using LM = std::integral_constant<int, 3>;
+    if (ntiles >= 3) {
+      load_fast();
+      stage(0);
+      load_fast();
+      __syncthreads();
+      int64_t t = 0;
+      for (; t + 3 < ntiles; ++t) body(t, T_{}, L1{});  // loads stages t+2 < ntiles-1: whole
+      body(t, T_{}, LM{});                             // loads the last stage (maybe the tail)
+      body(t + 1, T_{}, L0{});
+      body(t + 2, F_{}, L0{});
+    } else if (ntiles == 2) {
+      load_masked(0);
+      stage(0);
+      load_masked(1);
+      __syncthreads();
+      body(0, T_{}, L0{});
+      body(1, F_{}, L0{});
+    } else if (ntiles == 1) {
+      load_masked(0);
+      stage(0);
+      __syncthreads();
+      body(0, F_{}, L0{});
+    }
+  } else if (ntiles > 0) {  // generic guarded pipeline (unaligned / ragged K-major operands)
+    load_guarded(0);
+    stage(0);
+    __syncthreads();
+    for (int64_t t = 0; t < ntiles; ++t) {
+      if (t + 1 < ntiles) load_guarded(t + 1);
+      body(t, F_{}, L0{});
+      if (t + 1 < ntiles) {
+        stage((t + 1) & 1);
+        __syncthreads();
+      }
+    }
   }
   tile_epilogue<EPI_LOGW, 4, 2>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta, act, C,
                                 ldc, slab, epi);
+}
+
+// Host check for gemm_x3w_kernel<FAST = true>: aligned rows; a K-major operand's row count
+// % 4 == 0 (its clamped float4 never straddles the edge); K % 4 == 0 when an operand is
+// K-contiguous (the K tail's clamped float4 stays inside the row).
+bool x3w_fast(bool ak, bool bk, int64_t M, int64_t N, int64_t K, int av, int bv) {
+  return av && bv && ((ak && bk) || K % 4 == 0) && (!ak || M % 4 == 0) && (!bk || N % 4 == 0);
 }
 
 // Sum S split-K slabs in fixed order: C = act(sum_z slab[z] + bias + beta*C).
@@ -1036,8 +1111,11 @@ int gemm_launch(bool x3, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
   dim3 grid((unsigned)tiles, (unsigned)S);
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
   do {                                                                                          \
-    if (plan.wide)                                                                              \
-      gemm_x3w_kernel<AKV, BKV><<<grid, kXThreads, 0, st>>>(                                    \
+    if (plan.wide && x3w_fast(AKV, BKV, M, N, K, av, bv))                                          \
+      gemm_x3w_kernel<AKV, BKV, -1, true><<<grid, kXThreads, 0, st>>>(                          \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+    else if (plan.wide)                                                                         \
+      gemm_x3w_kernel<AKV, BKV, -1, false><<<grid, kXThreads, 0, st>>>(                         \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
     else if (x3 && AKV && BKV) /* both k-major: fragment split measured faster at 128x128 */    \
       gemm_f32_kernel<AKV, BKV, -1, true><<<grid, kThreads, 0, st>>>(                           \
@@ -1081,8 +1159,12 @@ int gemm_proj_epi(bool x3, int64_t M, int64_t N, int64_t K, const float* A, int6
   dim3 grid((unsigned)tiles, 1);
 #define MVML_PROJ(LW)                                                                          \
   do {                                                                                         \
-    if (wide)                                                                                  \
-      gemm_x3w_kernel<false, false, LW><<<grid, kXThreads, 0, st>>>(                           \
+    if (wide && x3w_fast(false, false, M, N, K, av, bv))                                          \
+      gemm_x3w_kernel<false, false, LW, true><<<grid, kXThreads, 0, st>>>(                     \
+          M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
+          ProjEpi{vec, cols, part});                                                           \
+    else if (wide)                                                                             \
+      gemm_x3w_kernel<false, false, LW, false><<<grid, kXThreads, 0, st>>>(                    \
           M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
           ProjEpi{vec, cols, part});                                                           \
     else if (x3)                                                                               \
