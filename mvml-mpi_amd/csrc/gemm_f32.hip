@@ -937,6 +937,20 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       }
     }
   }
+#ifdef MVML_X3W_NOEPI
+  if (M < 0) {  // ablation: keep the accumulators live, store nothing
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[i][j]));
+  return;
+#endif
   tile_epilogue<EPI_LOGW, 4, 2>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta, act, C,
                                 ldc, slab, epi);
 }

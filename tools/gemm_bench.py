@@ -17,6 +17,9 @@ SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor
     ("LSTM gates x*Wih^T", B, 1536, 768, 0, 0),
     ("LSTM dx g*Wih", B, 768, 1536, 0, 1),
     ("LSTM dW g^T*x", 1536, 768, B, 1, 1),
+    ("LSTM dW batched l0", 1536, 768, 5 * B, 1, 1),
+    ("LSTM dW batched hh", 1536, 384, 5 * B, 1, 1),
+    ("LSTM dW batched l1", 1536, 384, 6 * B, 1, 1),
 ]
 
 
