@@ -246,6 +246,40 @@ int mvml_graphnorm_bwd(int64_t G, int D, const int64_t* group_offsets, const flo
  * g_x = g_y * (y > 0). */
 int mvml_relu_bwd(int64_t n, const float* y, const float* g_y, float* g_x, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Multi-view attention fusion head (MVP, model.py:28-48, 57-71), the consumer
+ * of the graph view.  GEMMs (Q/K/V, MLP) use mvml_gemm_f32x3; the rest:
+ *   mvml_layernorm_fwd/_bwd: torch.nn.LayerNorm over rows of D <= 512 (model.py:23, 54-56);
+ *     fwd saves per-row mean / rstd; bwd writes g_x and g_y_xhat[rows, D] = g_y * xhat, whose
+ *     column sums (mvml_colsum_f32) are dL/dgamma (dL/dbeta = column sums of g_y).
+ *   mvml_token_attn_fwd/_bwd: the 3-token attention of model.py:62-68 per (molecule, head);
+ *     qkv rows 3b+t = [q (H*dk) | k (H*dk) | v (H*dk)] (ld >= 3 H dk), dk = 384; att [B, H, 3,
+ *     dk] (the Conv2d input layout), P [B, H, 3, 3] saved softmax; scale = 1/sqrt(dk).
+ *   mvml_conv3_fwd/_bwd: Conv2d(12, 12, kernel 3) + ReLU on att (model.py:27, 69):
+ *     in [B, 12, 3, W] -> out [B, 12, W-2] (post-ReLU); bwd gives g_in, g_weight [12,12,3,3],
+ *     g_bias [12] (deterministic partial sums; workspace mvml_conv3_bwd_workspace_size(B)).
+ *   mvml_bce_logits: BCEWithLogitsLoss (mean, main.py:91) element terms and dL/dz.
+ * ------------------------------------------------------------------------------------- */
+int mvml_layernorm_fwd(int64_t rows, int D, const float* x, int64_t ldx, const float* gamma,
+                       const float* beta, float eps, float* y, int64_t ldy, float* mean,
+                       float* rstd, void* stream);
+int mvml_layernorm_bwd(int64_t rows, int D, const float* x, int64_t ldx, const float* gamma,
+                       const float* mean, const float* rstd, const float* g_y, int64_t ldgy,
+                       float* g_x, int64_t ldgx, float* g_y_xhat, void* stream);
+int mvml_token_attn_fwd(int64_t B, int H, int dk, const float* qkv, int64_t ld, float scale,
+                        float* att, float* P, void* stream);
+int mvml_token_attn_bwd(int64_t B, int H, int dk, const float* qkv, int64_t ld, float scale,
+                        const float* P, const float* g_att, float* g_qkv, int64_t ldg,
+                        void* stream);
+int mvml_conv3_fwd(int64_t B, int C, int O, int W, const float* in, const float* weight,
+                   const float* bias, float* out, void* stream);
+size_t mvml_conv3_bwd_workspace_size(int64_t B);
+int mvml_conv3_bwd(int64_t B, int C, int O, int W, const float* in, const float* weight,
+                   const float* out, const float* g_out, float* g_in, float* g_weight,
+                   float* g_bias, void* workspace, size_t workspace_bytes, void* stream);
+int mvml_bce_logits(int64_t n, const float* z, const float* y, float* loss_terms, float* g_z,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

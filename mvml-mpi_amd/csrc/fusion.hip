@@ -1,0 +1,498 @@
+// Multi-view attention fusion head of MVP (model.py:28-48, 57-71), the consumer of the graph
+// view: shared LayerNorm(384) on the three view embeddings, Q/K/V projection
+// (three bias-free Linear(384 -> 12 x 384), one GEMM), attention over the 3 view tokens per head,
+// Conv2d(12, 12, 3) + ReLU over the (head, token, feature) cube, MLP 4584 -> 1024 -> 11, and
+// BCEWithLogitsLoss (main.py:91).  The GEMMs go through mvml_gemm_f32x3; this file holds the
+// non-GEMM kernels and their backward:
+//   * LayerNorm rows: one wave per row, two-pass statistics in registers.
+//   * token attention: one wave per (molecule, head); the 3x3 scores are nine wave dot
+//     products, the softmax is lane-local, the 384-wide rows stream once (HBM bound).
+//   * 3x3 convolution: one workgroup per molecule stages the (12, 3, 384) cube in LDS; a thread
+//     per output column computes all 12 output channels (weights as uniform LDS broadcasts).
+//     Weight gradients: per-workgroup partials over a run of molecules, summed in fixed order
+//     by a second kernel (deterministic, no atomics).
+#include "common.h"
+
+namespace mvml {
+namespace {
+
+constexpr int kFuseMaxVpl = 8;  // LayerNorm rows up to 512 wide
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// LayerNorm (torch.nn.LayerNorm, biased variance, eps inside the sqrt), one wave per row.
+__global__ void __launch_bounds__(256)
+layernorm_fwd_kernel(int64_t rows, int D, const float* __restrict__ x, int64_t ldx,
+                     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                     float* __restrict__ y, int64_t ldy, float* __restrict__ mean_out,
+                     float* __restrict__ rstd_out) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  float v[kFuseMaxVpl];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < kFuseMaxVpl; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < D ? x[r * ldx + c] : 0.f;
+    s += v[i];
+  }
+  const float mean = wsum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < kFuseMaxVpl; ++i) {
+    const int c = lane + 64 * i;
+    const float d = c < D ? v[i] - mean : 0.f;
+    q += d * d;
+  }
+  const float rstd = 1.f / sqrtf(wsum(q) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < kFuseMaxVpl; ++i) {
+    const int c = lane + 64 * i;
+    if (c < D) y[r * ldy + c] = (v[i] - mean) * rstd * gamma[c] + beta[c];
+  }
+  if (lane == 0) {
+    mean_out[r] = mean;
+    rstd_out[r] = rstd;
+  }
+}
+
+// g_x = rstd * (g_xh - mean(g_xh) - xh * mean(g_xh * xh)), g_xh = g_y * gamma;
+// gxh_out = g_y * xh (its column sums are dL/dgamma; column sums of g_y are dL/dbeta).
+__global__ void __launch_bounds__(256)
+layernorm_bwd_kernel(int64_t rows, int D, const float* __restrict__ x, int64_t ldx,
+                     const float* __restrict__ gamma, const float* __restrict__ mean_in,
+                     const float* __restrict__ rstd_in, const float* __restrict__ gy,
+                     int64_t ldgy, float* __restrict__ gx, int64_t ldgx,
+                     float* __restrict__ gyxh) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float mean = mean_in[r], rstd = rstd_in[r];
+  float xh[kFuseMaxVpl], g[kFuseMaxVpl];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < kFuseMaxVpl; ++i) {
+    const int c = lane + 64 * i;
+    xh[i] = c < D ? (x[r * ldx + c] - mean) * rstd : 0.f;
+    const float gyv = c < D ? gy[r * ldgy + c] : 0.f;
+    g[i] = c < D ? gyv * gamma[c] : 0.f;
+    if (c < D) gyxh[r * D + c] = gyv * xh[i];
+    s1 += g[i];
+    s2 += g[i] * xh[i];
+  }
+  const float m1 = wsum(s1) / (float)D, m2 = wsum(s2) / (float)D;
+#pragma unroll
+  for (int i = 0; i < kFuseMaxVpl; ++i) {
+    const int c = lane + 64 * i;
+    if (c < D) gx[r * ldgx + c] = rstd * (g[i] - m1 - xh[i] * m2);
+  }
+}
+
+// Attention over the NT = 3 view tokens of one molecule, per head (model.py:62-68):
+//   q/k/v of token t = QKV row 3b+t, columns [h*dk | HD + h*dk | 2HD + h*dk] (dk wide)
+//   s_ij = <q_i, k_j> * scale;  p = softmax_j(s);  att[b][h][i] = sum_j p_ij v_j
+constexpr int NT = 3;
+constexpr int kDkVpl = 6;  // dk = 384 = 6 x 64
+
+__global__ void __launch_bounds__(256)
+token_attn_fwd_kernel(int64_t B, int H, int dk, const float* __restrict__ qkv, int64_t ld,
+                      float scale, float* __restrict__ att, float* __restrict__ P) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= B * H) return;
+  const int64_t b = w / H;
+  const int h = (int)(w % H);
+  const int64_t HD = (int64_t)H * dk;
+  float q[NT][kDkVpl], k[NT][kDkVpl], v[NT][kDkVpl];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const float* row = qkv + (b * NT + t) * ld + (int64_t)h * dk;
+#pragma unroll
+    for (int i = 0; i < kDkVpl; ++i) {
+      const int c = lane + 64 * i;
+      q[t][i] = row[c];
+      k[t][i] = row[HD + c];
+      v[t][i] = row[2 * HD + c];
+    }
+  }
+  float p[NT][NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < kDkVpl; ++i) s = fmaf(q[a][i], k[c][i], s);
+      p[a][c] = wsum(s) * scale;
+    }
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+    const float m = fmaxf(p[a][0], fmaxf(p[a][1], p[a][2]));
+    float z = 0.f;
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      p[a][c] = expf(p[a][c] - m);
+      z += p[a][c];
+    }
+#pragma unroll
+    for (int c = 0; c < NT; ++c) p[a][c] /= z;
+  }
+  float* out = att + w * NT * dk;
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int i = 0; i < kDkVpl; ++i) {
+      float o = 0.f;
+#pragma unroll
+      for (int c = 0; c < NT; ++c) o = fmaf(p[a][c], v[c][i], o);
+      out[a * dk + lane + 64 * i] = o;
+    }
+  if (lane < NT * NT) {
+    float pv = p[0][0];
+#pragma unroll
+    for (int e = 1; e < NT * NT; ++e) pv = lane == e ? p[e / NT][e % NT] : pv;
+    P[w * NT * NT + lane] = pv;
+  }
+}
+
+// Backward of token_attn_fwd: g_v_j = sum_i p_ij g_i;  g_p_ij = <g_i, v_j>;
+// g_s_ij = p_ij (g_p_ij - sum_j' p_ij' g_p_ij');  g_q_i = scale sum_j g_s_ij k_j;
+// g_k_j = scale sum_i g_s_ij q_i.  gqkv has the layout of qkv.
+__global__ void __launch_bounds__(256)
+token_attn_bwd_kernel(int64_t B, int H, int dk, const float* __restrict__ qkv, int64_t ld,
+                      float scale, const float* __restrict__ P, const float* __restrict__ g_att,
+                      float* __restrict__ gqkv, int64_t ldg) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= B * H) return;
+  const int64_t b = w / H;
+  const int h = (int)(w % H);
+  const int64_t HD = (int64_t)H * dk;
+  float p[NT][NT];
+#pragma unroll
+  for (int e = 0; e < NT * NT; ++e) p[e / NT][e % NT] = P[w * NT * NT + e];
+  float g[NT][kDkVpl], v[NT][kDkVpl];
+  const float* ga = g_att + w * NT * dk;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const float* row = qkv + (b * NT + t) * ld + (int64_t)h * dk;
+#pragma unroll
+    for (int i = 0; i < kDkVpl; ++i) {
+      const int c = lane + 64 * i;
+      g[t][i] = ga[t * dk + c];
+      v[t][i] = row[2 * HD + c];
+    }
+  }
+  float gs[NT][NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+    float gp[NT];
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < kDkVpl; ++i) s = fmaf(g[a][i], v[c][i], s);
+      gp[c] = wsum(s);
+    }
+    const float dot = p[a][0] * gp[0] + p[a][1] * gp[1] + p[a][2] * gp[2];
+#pragma unroll
+    for (int c = 0; c < NT; ++c) gs[a][c] = p[a][c] * (gp[c] - dot) * scale;
+  }
+  // g_v (reuses v registers), then g_q, g_k from q, k
+#pragma unroll
+  for (int c = 0; c < NT; ++c) {
+    float* grow = gqkv + (b * NT + c) * ldg + (int64_t)h * dk;
+#pragma unroll
+    for (int i = 0; i < kDkVpl; ++i) {
+      float o = 0.f;
+#pragma unroll
+      for (int a = 0; a < NT; ++a) o = fmaf(p[a][c], g[a][i], o);
+      grow[2 * HD + lane + 64 * i] = o;
+    }
+  }
+  float q[NT][kDkVpl], k[NT][kDkVpl];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const float* row = qkv + (b * NT + t) * ld + (int64_t)h * dk;
+#pragma unroll
+    for (int i = 0; i < kDkVpl; ++i) {
+      q[t][i] = row[lane + 64 * i];
+      k[t][i] = row[HD + lane + 64 * i];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    float* grow = gqkv + (b * NT + t) * ldg + (int64_t)h * dk;
+#pragma unroll
+    for (int i = 0; i < kDkVpl; ++i) {
+      float oq = 0.f, ok = 0.f;
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        oq = fmaf(gs[t][c], k[c][i], oq);
+        ok = fmaf(gs[c][t], q[c][i], ok);
+      }
+      grow[lane + 64 * i] = oq;
+      grow[HD + lane + 64 * i] = ok;
+    }
+  }
+}
+
+// Conv2d(C, O, 3) over the (C, 3, W) cube of one molecule (model.py:27, 69): the kernel height
+// equals the token count, so the output is (O, 1, W - 2); + bias, ReLU (model.py:27-28).
+constexpr int kConvC = 12, kConvO = 12, kConvH = 3;
+constexpr int kConvThreads = 384;
+constexpr int kConvLd = 385;  // LDS row stride (W <= 384): rows land on different banks
+
+__global__ void __launch_bounds__(kConvThreads)
+conv3_fwd_kernel(int64_t B, int W, const float* __restrict__ in, const float* __restrict__ wgt,
+                 const float* __restrict__ bias, float* __restrict__ out) {
+  __shared__ float s_in[kConvC * kConvH * kConvLd];
+  __shared__ float s_w[kConvO * kConvC * 9];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int Wo = W - 2;
+  const float* src = in + b * (int64_t)(kConvC * kConvH * W);
+  for (int i = tid; i < kConvC * kConvH * W; i += kConvThreads) s_in[(i / W) * kConvLd + i % W] = src[i];
+  for (int i = tid; i < kConvO * kConvC * 9; i += kConvThreads) s_w[i] = wgt[i];
+  __syncthreads();
+  const int x = tid;
+  if (x >= Wo) return;
+  float acc[kConvO];
+#pragma unroll
+  for (int o = 0; o < kConvO; ++o) acc[o] = bias[o];
+  for (int c = 0; c < kConvC; ++c)
+#pragma unroll
+    for (int dy = 0; dy < kConvH; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const float a = s_in[(c * kConvH + dy) * kConvLd + x + dx];
+#pragma unroll
+        for (int o = 0; o < kConvO; ++o) acc[o] = fmaf(s_w[((o * kConvC + c) * 3 + dy) * 3 + dx], a, acc[o]);
+      }
+  float* dst = out + b * (int64_t)(kConvO * Wo);
+#pragma unroll
+  for (int o = 0; o < kConvO; ++o) dst[o * Wo + x] = fmaxf(acc[o], 0.f);
+}
+
+// Input gradient of conv3 (through the ReLU: g_pre = g_out * (out > 0)):
+//   g_in[c][dy][x'] = sum_o sum_dx w[o][c][dy][dx] g_pre[o][x' - dx]   (0 <= x' - dx < W - 2)
+// and per-workgroup weight / bias gradient partials over molecules [b0, b1):
+//   part[blk][(o, c, dy, dx)] = sum_b sum_x g_pre[o][x] in[c][dy][x + dx], part[blk][1296 + o].
+constexpr int kConvWg = kConvO * kConvC * kConvH * 3;  // 1296 weights
+
+__global__ void __launch_bounds__(kConvThreads)
+conv3_bwd_kernel(int64_t B, int W, int64_t per_block, const float* __restrict__ in,
+                 const float* __restrict__ wgt, const float* __restrict__ out,
+                 const float* __restrict__ g_out, float* __restrict__ g_in,
+                 float* __restrict__ part) {
+  __shared__ float s_in[kConvC * kConvH * kConvLd];
+  __shared__ float s_g[kConvO * kConvLd];
+  __shared__ float s_w[kConvWg];
+  const int tid = threadIdx.x;
+  const int Wo = W - 2;
+  for (int i = tid; i < kConvWg; i += kConvThreads) s_w[i] = wgt[i];
+  // weight-gradient role: thread t < 432 would own (o, c, dy); 384 threads own 384 of the 432
+  // (o, c, dy) triples in a first sweep and the remaining 48 in a second (dx = 0..2 each), plus
+  // thread o < 12 the bias of channel o
+  float pw[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+  float pb = 0.f;
+  const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(B, b0 + per_block);
+  for (int64_t b = b0; b < b1; ++b) {
+    __syncthreads();  // previous molecule's LDS reads done
+    const float* src = in + b * (int64_t)(kConvC * kConvH * W);
+    for (int i = tid; i < kConvC * kConvH * W; i += kConvThreads) s_in[(i / W) * kConvLd + i % W] = src[i];
+    const float* go = g_out + b * (int64_t)(kConvO * Wo);
+    const float* oo = out + b * (int64_t)(kConvO * Wo);
+    for (int i = tid; i < kConvO * 384; i += kConvThreads) {
+      const int o = i / 384, x = i % 384;
+      s_g[o * kConvLd + x] = (x < Wo && oo[o * Wo + x] > 0.f) ? go[o * Wo + x] : 0.f;  // zero-padded
+    }
+    __syncthreads();
+    // input gradient: thread per column x' (< W), all (c, dy)
+    if (tid < W) {
+      const int xp = tid;
+      float* dst = g_in + b * (int64_t)(kConvC * kConvH * W);
+      for (int c = 0; c < kConvC; ++c)
+#pragma unroll
+        for (int dy = 0; dy < kConvH; ++dy) {
+          float acc = 0.f;
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx) {
+            const int x = xp - dx;
+            if (x < 0) continue;  // x >= Wo reads the zero padding
+#pragma unroll
+            for (int o = 0; o < kConvO; ++o) acc = fmaf(s_w[((o * kConvC + c) * 3 + dy) * 3 + dx], s_g[o * kConvLd + x], acc);
+          }
+          dst[(c * kConvH + dy) * W + xp] = acc;
+        }
+    }
+    // weight / bias gradient partials
+#pragma unroll
+    for (int sweep = 0; sweep < 2; ++sweep) {
+      const int t = tid + sweep * kConvThreads;
+      if (t < kConvO * kConvC * kConvH) {
+        const int o = t / (kConvC * kConvH), c = (t / kConvH) % kConvC, dy = t % kConvH;
+        const float* gi = s_g + o * kConvLd;
+        const float* ai = s_in + (c * kConvH + dy) * kConvLd;
+        float a0 = ai[0], a1 = ai[1];
+        for (int x = 0; x < Wo; ++x) {
+          const float a2 = ai[x + 2];
+          const float gv = gi[x];
+          pw[sweep][0] = fmaf(gv, a0, pw[sweep][0]);
+          pw[sweep][1] = fmaf(gv, a1, pw[sweep][1]);
+          pw[sweep][2] = fmaf(gv, a2, pw[sweep][2]);
+          a0 = a1;
+          a1 = a2;
+        }
+      }
+    }
+    if (tid < kConvO) {
+      float s = 0.f;
+      for (int x = 0; x < Wo; ++x) s += s_g[tid * kConvLd + x];
+      pb += s;
+    }
+  }
+  float* dst = part + (int64_t)blockIdx.x * (kConvWg + kConvO);
+#pragma unroll
+  for (int sweep = 0; sweep < 2; ++sweep) {
+    const int t = tid + sweep * kConvThreads;
+    if (t < kConvO * kConvC * kConvH) {
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) dst[t * 3 + dx] = pw[sweep][dx];
+    }
+  }
+  if (tid < kConvO) dst[kConvWg + tid] = pb;
+}
+
+// Fixed-order sum of the per-workgroup partials: out[i] = sum_blk part[blk * stride + i].
+__global__ void partial_sum_kernel(int nblk, int count, int stride, const float* __restrict__ part,
+                                   float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  float s = 0.f;
+  for (int k = 0; k < nblk; ++k) s += part[(int64_t)k * stride + i];
+  out[i] = s;
+}
+
+// BCEWithLogitsLoss (mean over all B x C logits, main.py:91): per-element loss terms (summed by
+// the caller) and dL/dz = (sigmoid(z) - y) / (B C).
+__global__ void bce_logits_kernel(int64_t n, const float* __restrict__ z, const float* __restrict__ y,
+                                  float* __restrict__ loss_terms, float* __restrict__ gz) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float zi = z[i], yi = y[i];
+  // max(z, 0) - z y + log(1 + exp(-|z|)): torch's stable form
+  loss_terms[i] = fmaxf(zi, 0.f) - zi * yi + log1pf(expf(-fabsf(zi)));
+  gz[i] = (1.f / (1.f + expf(-zi)) - yi) / (float)n;
+}
+
+}  // namespace
+}  // namespace mvml
+
+using namespace mvml;
+
+extern "C" int mvml_layernorm_fwd(int64_t rows, int D, const float* x, int64_t ldx,
+                                  const float* gamma, const float* beta, float eps, float* y,
+                                  int64_t ldy, float* mean, float* rstd, void* stream) {
+  clear_error();
+  MVML_REQUIRE(rows >= 0 && D > 0 && D <= 64 * kFuseMaxVpl && ldx >= D && ldy >= D,
+               "layernorm_fwd: bad shape (D must be <= %d)", 64 * kFuseMaxVpl);
+  if (rows == 0) return MVML_OK;
+  layernorm_fwd_kernel<<<(unsigned)ceil_div(rows, 4), 256, 0, as_stream(stream)>>>(
+      rows, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd);
+  return check_launch("layernorm_fwd_kernel");
+}
+
+extern "C" int mvml_layernorm_bwd(int64_t rows, int D, const float* x, int64_t ldx,
+                                  const float* gamma, const float* mean, const float* rstd,
+                                  const float* g_y, int64_t ldgy, float* g_x, int64_t ldgx,
+                                  float* g_y_xhat, void* stream) {
+  clear_error();
+  MVML_REQUIRE(rows >= 0 && D > 0 && D <= 64 * kFuseMaxVpl && ldx >= D && ldgy >= D && ldgx >= D,
+               "layernorm_bwd: bad shape");
+  if (rows == 0) return MVML_OK;
+  layernorm_bwd_kernel<<<(unsigned)ceil_div(rows, 4), 256, 0, as_stream(stream)>>>(
+      rows, D, x, ldx, gamma, mean, rstd, g_y, ldgy, g_x, ldgx, g_y_xhat);
+  return check_launch("layernorm_bwd_kernel");
+}
+
+extern "C" int mvml_token_attn_fwd(int64_t B, int H, int dk, const float* qkv, int64_t ld,
+                                   float scale, float* att, float* P, void* stream) {
+  clear_error();
+  MVML_REQUIRE(B >= 0 && H > 0 && dk == 64 * kDkVpl && ld >= 3 * (int64_t)H * dk,
+               "token_attn_fwd: dk must be %d and ld >= 3*H*dk", 64 * kDkVpl);
+  if (B == 0) return MVML_OK;
+  token_attn_fwd_kernel<<<(unsigned)ceil_div(B * H, 4), 256, 0, as_stream(stream)>>>(
+      B, H, dk, qkv, ld, scale, att, P);
+  return check_launch("token_attn_fwd_kernel");
+}
+
+extern "C" int mvml_token_attn_bwd(int64_t B, int H, int dk, const float* qkv, int64_t ld,
+                                   float scale, const float* P, const float* g_att,
+                                   float* g_qkv, int64_t ldg, void* stream) {
+  clear_error();
+  MVML_REQUIRE(B >= 0 && H > 0 && dk == 64 * kDkVpl && ld >= 3 * (int64_t)H * dk &&
+                   ldg >= 3 * (int64_t)H * dk,
+               "token_attn_bwd: bad shape");
+  if (B == 0) return MVML_OK;
+  token_attn_bwd_kernel<<<(unsigned)ceil_div(B * H, 4), 256, 0, as_stream(stream)>>>(
+      B, H, dk, qkv, ld, scale, P, g_att, g_qkv, ldg);
+  return check_launch("token_attn_bwd_kernel");
+}
+
+extern "C" int mvml_conv3_fwd(int64_t B, int C, int O, int W, const float* in, const float* weight,
+                              const float* bias, float* out, void* stream) {
+  clear_error();
+  MVML_REQUIRE(C == kConvC && O == kConvO && W >= 3 && W <= 384, "conv3_fwd: C = O = 12, 3 <= W <= 384");
+  if (B == 0) return MVML_OK;
+  conv3_fwd_kernel<<<(unsigned)B, kConvThreads, 0, as_stream(stream)>>>(B, W, in, weight, bias, out);
+  return check_launch("conv3_fwd_kernel");
+}
+
+static int64_t conv3_blocks(int64_t B) { return std::min<int64_t>(B, 2048); }
+
+extern "C" size_t mvml_conv3_bwd_workspace_size(int64_t B) {
+  return carve_size((size_t)conv3_blocks(B > 0 ? B : 1) * (kConvWg + kConvO) * sizeof(float));
+}
+
+extern "C" int mvml_conv3_bwd(int64_t B, int C, int O, int W, const float* in, const float* weight,
+                              const float* out, const float* g_out, float* g_in, float* g_weight,
+                              float* g_bias, void* workspace, size_t workspace_bytes,
+                              void* stream) {
+  clear_error();
+  MVML_REQUIRE(C == kConvC && O == kConvO && W >= 3 && W <= 384, "conv3_bwd: C = O = 12, 3 <= W <= 384");
+  if (B == 0) return MVML_OK;
+  if (!workspace || workspace_bytes < mvml_conv3_bwd_workspace_size(B)) {
+    set_error("conv3_bwd: workspace of mvml_conv3_bwd_workspace_size bytes required");
+    return MVML_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  const int64_t nblk = conv3_blocks(B), per = ceil_div(B, nblk);
+  const int64_t used = ceil_div(B, per);
+  float* part = static_cast<float*>(workspace);
+  conv3_bwd_kernel<<<(unsigned)used, kConvThreads, 0, st>>>(B, W, per, in, weight, out, g_out,
+                                                            g_in, part);
+  int rc = check_launch("conv3_bwd_kernel");
+  if (rc) return rc;
+  const int n = kConvWg + kConvO;  // partial row: 1296 weight sums, then 12 bias sums
+  partial_sum_kernel<<<(unsigned)ceil_div(kConvWg, 256), 256, 0, st>>>((int)used, kConvWg, n, part,
+                                                                       g_weight);
+  rc = check_launch("partial_sum_kernel(w)");
+  if (rc) return rc;
+  partial_sum_kernel<<<1, 64, 0, st>>>((int)used, kConvO, n, part + kConvWg, g_bias);
+  return check_launch("partial_sum_kernel(b)");
+}
+
+extern "C" int mvml_bce_logits(int64_t n, const float* z, const float* y, float* loss_terms,
+                               float* g_z, void* stream) {
+  clear_error();
+  MVML_REQUIRE(n >= 0, "bce_logits: bad size");
+  if (n == 0) return MVML_OK;
+  bce_logits_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, as_stream(stream)>>>(n, z, y, loss_terms, g_z);
+  return check_launch("bce_logits_kernel");
+}

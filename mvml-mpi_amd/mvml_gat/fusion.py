@@ -1,0 +1,175 @@
+"""Multi-view attention fusion head of MVP (model.py:23, 27-48, 54-72) on the HIP path — the
+consumer of the graph view.
+
+    MVFusion(final_hidden_feats=384, num_heads=12, num_classes=11, dropout)(smiles_x, graph_x, fp_x)
+
+takes the three RAW view embeddings (B, 384) (what MVP gets from RNNModule, GNNModule and
+FPNModule before its shared LayerNorm, model.py:54-56) and returns the logits (B, num_classes)
+of model.py:72.  Parameter names / shapes equal MVP's, so ``MVP.state_dict()`` entries under
+``norm_layer_module.``, ``conv.``, ``linear_{q,k,v}.``, ``norm_layer.``, ``mlp.`` load unchanged.
+``bce_with_logits`` is main.py:91's BCEWithLogitsLoss.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from ._lib import call, ptr
+from .functional import (LinearReLUFunction, _c, _check_cuda_f32, _stream, colsum, gemm)
+
+
+class LinearFunction(torch.autograd.Function):
+    """nn.Linear (model.py:44, the classifier) as one MFMA GEMM with a bias epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        _check_cuda_f32(x, "x")
+        x = _c(x)
+        M, K = x.shape
+        Nout = weight.shape[0]
+        y = torch.empty((M, Nout), dtype=torch.float32, device=x.device)
+        gemm(x, _c(weight), M, Nout, K, 0, 0, K, K, y, Nout, bias=_c(bias))
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, g_y):
+        x, weight = ctx.saved_tensors
+        g_y = _c(g_y)
+        M, K = x.shape
+        Nout = weight.shape[0]
+        gw = torch.empty_like(weight)
+        gemm(g_y, x, Nout, K, M, 1, 1, Nout, K, gw, K)
+        gb = torch.empty((Nout,), dtype=torch.float32, device=x.device)
+        colsum(g_y, M, Nout, Nout, gb)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            gemm(g_y, _c(weight), M, K, Nout, 0, 1, Nout, K, gx, K)
+        return gx, gw, gb
+
+
+class FusionAttnConvFunction(torch.autograd.Function):
+    """model.py:54-71 up to the Conv2d+ReLU: shared LayerNorm of the three views, Q/K/V (one
+    GEMM over the concatenated [W_q; W_k; W_v]), 3-token attention per head, Conv2d(nh, nh, 3)
+    + ReLU.  Returns (B, nh * (dim - 2)) like ``self.conv(att).view(B, -1)`` before Dropout."""
+
+    @staticmethod
+    def forward(ctx, smiles_x, graph_x, fp_x, ln_w, ln_b, wq, wk, wv, conv_w, conv_b, eps):
+        for t, n in ((smiles_x, "smiles_x"), (graph_x, "graph_x"), (fp_x, "fp_x")):
+            _check_cuda_f32(t, n)
+        B, D = graph_x.shape
+        H = wq.shape[0] // D
+        dev = graph_x.device
+        st = _stream(dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        X = torch.stack([_c(smiles_x), _c(graph_x), _c(fp_x)], dim=1).reshape(3 * B, D)  # row 3b+t
+        Xn = torch.empty((3 * B, D), **f32)
+        mean = torch.empty((3 * B,), **f32)
+        rstd = torch.empty((3 * B,), **f32)
+        call("mvml_layernorm_fwd", 3 * B, D, ptr(X), D, ptr(_c(ln_w)), ptr(_c(ln_b)), float(eps),
+             ptr(Xn), D, ptr(mean), ptr(rstd), st)
+        Wqkv = torch.cat([_c(wq), _c(wk), _c(wv)], dim=0)  # (3 H D, D)
+        HD3 = 3 * H * D
+        QKV = torch.empty((3 * B, HD3), **f32)
+        gemm(Xn, Wqkv, 3 * B, HD3, D, 0, 0, D, D, QKV, HD3)
+        att = torch.empty((B, H, 3, D), **f32)
+        P = torch.empty((B, H, 3, 3), **f32)
+        scale = 1.0 / math.sqrt(D)
+        call("mvml_token_attn_fwd", B, H, D, ptr(QKV), HD3, float(scale), ptr(att), ptr(P), st)
+        out = torch.empty((B, H, D - 2), **f32)
+        call("mvml_conv3_fwd", B, H, H, D, ptr(att), ptr(_c(conv_w)), ptr(_c(conv_b)), ptr(out), st)
+        ctx.save_for_backward(X, Xn, mean, rstd, ln_w, Wqkv, QKV, P, att, out, conv_w)
+        ctx.dims = (B, D, H, scale)
+        return out.view(B, H * (D - 2))
+
+    @staticmethod
+    def backward(ctx, g_out):
+        X, Xn, mean, rstd, ln_w, Wqkv, QKV, P, att, out, conv_w = ctx.saved_tensors
+        B, D, H, scale = ctx.dims
+        dev = X.device
+        st = _stream(dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        L = _lib.lib()
+        g_out = _c(g_out)
+        g_att = torch.empty_like(att)
+        g_cw = torch.empty_like(conv_w)
+        g_cb = torch.empty((H,), **f32)
+        wp, wn = _lib.ws_ptr_size(L.mvml_conv3_bwd_workspace_size(B), dev)
+        call("mvml_conv3_bwd", B, H, H, D, ptr(att), ptr(_c(conv_w)), ptr(out), ptr(g_out), ptr(g_att),
+             ptr(g_cw), ptr(g_cb), wp, wn, st)
+        HD3 = 3 * H * D
+        gQKV = torch.empty((3 * B, HD3), **f32)
+        call("mvml_token_attn_bwd", B, H, D, ptr(QKV), HD3, float(scale), ptr(P), ptr(g_att),
+             ptr(gQKV), HD3, st)
+        gW = torch.empty_like(Wqkv)
+        gemm(gQKV, Xn, HD3, D, 3 * B, 1, 1, HD3, D, gW, D)
+        gXn = torch.empty((3 * B, D), **f32)
+        gemm(gQKV, Wqkv, 3 * B, D, HD3, 0, 1, HD3, D, gXn, D)
+        gX = torch.empty((3 * B, D), **f32)
+        gyxh = torch.empty((3 * B, D), **f32)
+        call("mvml_layernorm_bwd", 3 * B, D, ptr(X), D, ptr(_c(ln_w)), ptr(mean), ptr(rstd), ptr(gXn), D,
+             ptr(gX), D, ptr(gyxh), st)
+        g_lnw = torch.empty((D,), **f32)
+        g_lnb = torch.empty((D,), **f32)
+        colsum(gyxh, 3 * B, D, D, g_lnw)
+        colsum(gXn, 3 * B, D, D, g_lnb)
+        gX = gX.view(B, 3, D)
+        HD = H * D
+        return (gX[:, 0], gX[:, 1], gX[:, 2], g_lnw, g_lnb, gW[:HD], gW[HD:2 * HD], gW[2 * HD:],
+                g_cw, g_cb, None)
+
+
+class BCEWithLogitsFunction(torch.autograd.Function):
+    """torch.nn.BCEWithLogitsLoss() (mean), main.py:91."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        _check_cuda_f32(logits, "logits")
+        z, y = _c(logits), _c(labels.float())
+        terms = torch.empty_like(z)
+        gz = torch.empty_like(z)
+        call("mvml_bce_logits", z.numel(), ptr(z), ptr(y), ptr(terms), ptr(gz), _stream(z.device))
+        ctx.save_for_backward(gz)
+        return terms.sum() / z.numel()
+
+    @staticmethod
+    def backward(ctx, g):
+        (gz,) = ctx.saved_tensors
+        return gz * g, None
+
+
+def bce_with_logits(logits, labels):
+    return BCEWithLogitsFunction.apply(logits, labels)
+
+
+class MVFusion(nn.Module):
+    """The fusion part of MVP (model.py:23, 27-48, 54-72) with MVP's parameter names."""
+
+    def __init__(self, final_hidden_feats=384, num_heads=12, num_classes=11, dropout=0.2):
+        super().__init__()
+        d = final_hidden_feats
+        self.final_hidden_feats, self.num_heads = d, num_heads
+        self.norm_layer_module = nn.LayerNorm(d)
+        self.conv = nn.Sequential(nn.Conv2d(num_heads, num_heads, kernel_size=3), nn.ReLU(),
+                                  nn.Dropout(dropout))
+        self.dim_in, self.dim_k, self.dim_v = d, d * num_heads, d * num_heads
+        self.linear_q = nn.Linear(d, self.dim_k, bias=False)
+        self.linear_k = nn.Linear(d, self.dim_k, bias=False)
+        self.linear_v = nn.Linear(d, self.dim_v, bias=False)
+        self._norm_fact = 1 / math.sqrt(self.dim_k // num_heads)
+        self.norm_layer = nn.LayerNorm((d - 2) * num_heads)  # constructed, unused (model.py:39)
+        self.mlp = nn.Sequential(nn.Linear((d - 2) * num_heads, 1024), nn.ReLU(), nn.Dropout(dropout),
+                                 nn.Linear(1024, num_classes))
+
+    def forward(self, smiles_x, graph_x, fp_x):
+        ln = self.norm_layer_module
+        out = FusionAttnConvFunction.apply(smiles_x, graph_x, fp_x, ln.weight, ln.bias,
+                                           self.linear_q.weight, self.linear_k.weight,
+                                           self.linear_v.weight, self.conv[0].weight,
+                                           self.conv[0].bias, ln.eps)
+        out = self.conv[2](out)
+        out = LinearReLUFunction.apply(out, self.mlp[0].weight, self.mlp[0].bias)
+        out = self.mlp[2](out)
+        return LinearFunction.apply(out, self.mlp[3].weight, self.mlp[3].bias)
