@@ -35,7 +35,9 @@ BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA peak (same table; the 5 PF figure
 TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32x3", "mvml_gat_proj_fwd", "mvml_set2set_seg_fwd",
          "mvml_set2set_seg_bwd", "mvml_lstm_cell_fwd", "mvml_lstm_cell_bwd", "mvml_set2set_gx",
          "mvml_graphnorm_fwd", "mvml_graphnorm_bwd", "mvml_colsum_f32", "mvml_gat_fold_weights",
-         "mvml_gat_unfold_grads", "mvml_relu_bwd"]
+         "mvml_gat_unfold_grads", "mvml_relu_bwd", "mvml_layernorm_fwd", "mvml_layernorm_bwd",
+         "mvml_token_attn_fwd", "mvml_token_attn_bwd", "mvml_conv3_fwd", "mvml_conv3_bwd",
+         "mvml_bce_logits"]
 
 
 def parse():
@@ -49,6 +51,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--with-fusion", action="store_true",
+                    help="config 3 with its consumer: the MVP fusion head (SURVEY 8f-1) + BCE loss "
+                         "on the GAT view's output (the SMILES / fingerprint views, out of scope, "
+                         "are synthetic fixed embeddings)")
     return ap.parse_args()
 
 
@@ -161,11 +167,22 @@ def main():
     reducer = FlatGradAllReduce(model.parameters(), average=True)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     upstream = torch.randn((B, 384), device=dev, generator=gen) * 1e-3
+    if args.with_fusion:
+        fusion = mvml_gat.MVFusion(384, 12, 11, 0.5).to(dev).train()
+        params = list(model.parameters()) + list(fusion.parameters())
+        opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-4)
+        reducer = FlatGradAllReduce(params, average=True)
+        smiles_x = torch.randn((B, 384), device=dev, generator=gen)
+        fp_x = torch.randn((B, 384), device=dev, generator=gen)
+        labels = (torch.rand((B, 11), device=dev, generator=gen) > 0.8).float()
 
     def step():
         opt.zero_grad(set_to_none=False)
         out = model(g, feats)
-        out.backward(upstream)
+        if args.with_fusion:
+            mvml_gat.bce_with_logits(fusion(smiles_x, out, fp_x), labels).backward()
+        else:
+            out.backward(upstream)
         reducer()
         opt.step()
 
@@ -228,7 +245,10 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded KEGG-like drug-like molecules, random-init weights)",
             "config": {"workload": "BASELINE config 3: GNNModule (GAT [192,384] x4 heads, Set2Set 6x3, "
-                                   "GraphNorm, fc) fwd+bwd+Adam over KEGG-like molecules",
+                                   "GraphNorm, fc) fwd+bwd+Adam over KEGG-like molecules"
+                                   + (" + MVP fusion head (12-head 3-token attention, Conv2d, MLP) "
+                                      "+ BCEWithLogits" if args.with_fusion else
+                                      " (fixed upstream gradient at the view output)"),
                        "mols_per_gpu": B, "atoms_per_gpu": N, "edges_per_gpu": E,
                        "graphnorm_group": args.group_size, "parallelism": f"dp{world}"},
             "roofline": roofline, "cpu_baseline": cpu,

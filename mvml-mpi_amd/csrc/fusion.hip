@@ -246,34 +246,57 @@ token_attn_bwd_kernel(int64_t B, int H, int dk, const float* __restrict__ qkv, i
 // equals the token count, so the output is (O, 1, W - 2); + bias, ReLU (model.py:27-28).
 constexpr int kConvC = 12, kConvO = 12, kConvH = 3;
 constexpr int kConvThreads = 384;
+constexpr int kConvWg = kConvO * kConvC * kConvH * 3;  // 1296 weights
 constexpr int kConvLd = 385;  // LDS row stride (W <= 384): rows land on different banks
+
+// rows x W floats from global (row-contiguous) into LDS rows of stride kConvLd
+__device__ __forceinline__ void conv_stage(float* dst, const float* __restrict__ src, int rows, int W,
+                                           int tid) {
+  if ((W & 3) == 0 && ((uintptr_t)src & 15) == 0) {
+    const int w4 = W >> 2;
+    for (int i = tid; i < rows * w4; i += kConvThreads) {
+      const int r = i / w4, c = (i - r * w4) * 4;
+      const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)r * W + c);
+      float* d = dst + r * kConvLd + c;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+  } else {
+    for (int i = tid; i < rows * W; i += kConvThreads) dst[(i / W) * kConvLd + i % W] = src[i];
+  }
+}
 
 __global__ void __launch_bounds__(kConvThreads)
 conv3_fwd_kernel(int64_t B, int W, const float* __restrict__ in, const float* __restrict__ wgt,
                  const float* __restrict__ bias, float* __restrict__ out) {
   __shared__ float s_in[kConvC * kConvH * kConvLd];
-  __shared__ float s_w[kConvO * kConvC * 9];
+  __shared__ __attribute__((aligned(16))) float s_wt[kConvC * kConvH * 3][kConvO];  // [(c,dy,dx)][o]
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x;
   const int Wo = W - 2;
-  const float* src = in + b * (int64_t)(kConvC * kConvH * W);
-  for (int i = tid; i < kConvC * kConvH * W; i += kConvThreads) s_in[(i / W) * kConvLd + i % W] = src[i];
-  for (int i = tid; i < kConvO * kConvC * 9; i += kConvThreads) s_w[i] = wgt[i];
+  for (int i = tid; i < kConvWg; i += kConvThreads) s_wt[i % (kConvC * 9)][i / (kConvC * 9)] = wgt[i];
+  conv_stage(s_in, in + b * (int64_t)(kConvC * kConvH * W), kConvC * kConvH, W, tid);
   __syncthreads();
   const int x = tid;
   if (x >= Wo) return;
   float acc[kConvO];
 #pragma unroll
   for (int o = 0; o < kConvO; ++o) acc[o] = bias[o];
-  for (int c = 0; c < kConvC; ++c)
+#pragma unroll 2
+  for (int cd = 0; cd < kConvC * kConvH; ++cd) {
 #pragma unroll
-    for (int dy = 0; dy < kConvH; ++dy)
+    for (int dx = 0; dx < 3; ++dx) {
+      const float a = s_in[cd * kConvLd + x + dx];
+      const float4* wr = reinterpret_cast<const float4*>(s_wt[cd * 3 + dx]);  // uniform: broadcast
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const float a = s_in[(c * kConvH + dy) * kConvLd + x + dx];
-#pragma unroll
-        for (int o = 0; o < kConvO; ++o) acc[o] = fmaf(s_w[((o * kConvC + c) * 3 + dy) * 3 + dx], a, acc[o]);
+      for (int j = 0; j < kConvO / 4; ++j) {
+        const float4 w4 = wr[j];
+        acc[4 * j] = fmaf(w4.x, a, acc[4 * j]);
+        acc[4 * j + 1] = fmaf(w4.y, a, acc[4 * j + 1]);
+        acc[4 * j + 2] = fmaf(w4.z, a, acc[4 * j + 2]);
+        acc[4 * j + 3] = fmaf(w4.w, a, acc[4 * j + 3]);
       }
+    }
+  }
   float* dst = out + b * (int64_t)(kConvO * Wo);
 #pragma unroll
   for (int o = 0; o < kConvO; ++o) dst[o * Wo + x] = fmaxf(acc[o], 0.f);
@@ -283,100 +306,138 @@ conv3_fwd_kernel(int64_t B, int W, const float* __restrict__ in, const float* __
 //   g_in[c][dy][x'] = sum_o sum_dx w[o][c][dy][dx] g_pre[o][x' - dx]   (0 <= x' - dx < W - 2)
 // and per-workgroup weight / bias gradient partials over molecules [b0, b1):
 //   part[blk][(o, c, dy, dx)] = sum_b sum_x g_pre[o][x] in[c][dy][x + dx], part[blk][1296 + o].
-constexpr int kConvWg = kConvO * kConvC * kConvH * 3;  // 1296 weights
 
-__global__ void __launch_bounds__(kConvThreads)
+// Weight-gradient role: thread (o, c, half) with o, c < 12 and half < 2 sums over the half of
+// the columns x in [x0, x1) all nine (dy, dx) products g_pre[o][x] * in[c][dy][x + dx] with a
+// three-column sliding window per dy (4 LDS reads per 9 FMAs); the two halves land in separate
+// partial slots.  Thread o < 12 (half 0, c 0) also sums the bias of channel o.
+constexpr int kConvPart = 2 * kConvWg + kConvO;  // per-workgroup partial row
+
+__global__ void __launch_bounds__(kConvThreads, 3)  // two workgroups per CU
 conv3_bwd_kernel(int64_t B, int W, int64_t per_block, const float* __restrict__ in,
                  const float* __restrict__ wgt, const float* __restrict__ out,
                  const float* __restrict__ g_out, float* __restrict__ g_in,
                  float* __restrict__ part) {
   __shared__ float s_in[kConvC * kConvH * kConvLd];
   __shared__ float s_g[kConvO * kConvLd];
-  __shared__ float s_w[kConvWg];
+  __shared__ __attribute__((aligned(16))) float s_wt[kConvO * 3][kConvC * kConvH];  // [(o,dx)][(c,dy)]
   const int tid = threadIdx.x;
+  for (int i = tid; i < kConvWg; i += kConvThreads) {
+    const int o = i / (kConvC * 9), c = (i / 9) % kConvC, dy = (i / 3) % 3, dx = i % 3;
+    s_wt[o * 3 + dx][c * kConvH + dy] = wgt[i];
+  }
   const int Wo = W - 2;
-  for (int i = tid; i < kConvWg; i += kConvThreads) s_w[i] = wgt[i];
-  // weight-gradient role: thread t < 432 would own (o, c, dy); 384 threads own 384 of the 432
-  // (o, c, dy) triples in a first sweep and the remaining 48 in a second (dx = 0..2 each), plus
-  // thread o < 12 the bias of channel o
-  float pw[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+  const int wo = tid / (2 * kConvC), wc = (tid / 2) % kConvC, wh = tid & 1;  // weight role
+  const bool wrole = tid < kConvO * kConvC * 2;
+  const int xmid = (Wo + 1) / 2;
+  const int x0 = wh ? xmid : 0, x1 = wh ? Wo : xmid;
+  float pw[kConvH][3];
+#pragma unroll
+  for (int dy = 0; dy < kConvH; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) pw[dy][dx] = 0.f;
   float pb = 0.f;
   const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(B, b0 + per_block);
   for (int64_t b = b0; b < b1; ++b) {
     __syncthreads();  // previous molecule's LDS reads done
-    const float* src = in + b * (int64_t)(kConvC * kConvH * W);
-    for (int i = tid; i < kConvC * kConvH * W; i += kConvThreads) s_in[(i / W) * kConvLd + i % W] = src[i];
+    conv_stage(s_in, in + b * (int64_t)(kConvC * kConvH * W), kConvC * kConvH, W, tid);
     const float* go = g_out + b * (int64_t)(kConvO * Wo);
     const float* oo = out + b * (int64_t)(kConvO * Wo);
-    for (int i = tid; i < kConvO * 384; i += kConvThreads) {
-      const int o = i / 384, x = i % 384;
-      s_g[o * kConvLd + x] = (x < Wo && oo[o * Wo + x] > 0.f) ? go[o * Wo + x] : 0.f;  // zero-padded
+    for (int i = tid; i < kConvO * kConvLd; i += kConvThreads) {
+      const int o = i / kConvLd, x = i % kConvLd;
+      s_g[i] = (x < Wo && oo[o * Wo + x] > 0.f) ? go[o * Wo + x] : 0.f;  // zero-padded
     }
     __syncthreads();
-    // input gradient: thread per column x' (< W), all (c, dy)
+    // input gradient: thread per column x' < W, all 36 (c, dy) outputs in registers; each
+    // g_pre[o][x' - dx] is read once, the weights are wave-uniform (scalar) loads
+#ifndef MVML_CONV_NOIN
     if (tid < W) {
       const int xp = tid;
-      float* dst = g_in + b * (int64_t)(kConvC * kConvH * W);
+      float acc[kConvC][kConvH];
+#pragma unroll
       for (int c = 0; c < kConvC; ++c)
 #pragma unroll
-        for (int dy = 0; dy < kConvH; ++dy) {
-          float acc = 0.f;
+        for (int dy = 0; dy < kConvH; ++dy) acc[c][dy] = 0.f;
+#pragma unroll 1
+      for (int od = 0; od < kConvO * 3; ++od) {
+        const int o = od / 3, dx = od % 3;
+        const int x = xp - dx;
+        const float gv = x >= 0 ? s_g[o * kConvLd + x] : 0.f;  // x >= Wo reads the padding
+        const float4* wr = reinterpret_cast<const float4*>(s_wt[od]);  // uniform: broadcast
 #pragma unroll
-          for (int dx = 0; dx < 3; ++dx) {
-            const int x = xp - dx;
-            if (x < 0) continue;  // x >= Wo reads the zero padding
-#pragma unroll
-            for (int o = 0; o < kConvO; ++o) acc = fmaf(s_w[((o * kConvC + c) * 3 + dy) * 3 + dx], s_g[o * kConvLd + x], acc);
-          }
-          dst[(c * kConvH + dy) * W + xp] = acc;
-        }
-    }
-    // weight / bias gradient partials
-#pragma unroll
-    for (int sweep = 0; sweep < 2; ++sweep) {
-      const int t = tid + sweep * kConvThreads;
-      if (t < kConvO * kConvC * kConvH) {
-        const int o = t / (kConvC * kConvH), c = (t / kConvH) % kConvC, dy = t % kConvH;
-        const float* gi = s_g + o * kConvLd;
-        const float* ai = s_in + (c * kConvH + dy) * kConvLd;
-        float a0 = ai[0], a1 = ai[1];
-        for (int x = 0; x < Wo; ++x) {
-          const float a2 = ai[x + 2];
-          const float gv = gi[x];
-          pw[sweep][0] = fmaf(gv, a0, pw[sweep][0]);
-          pw[sweep][1] = fmaf(gv, a1, pw[sweep][1]);
-          pw[sweep][2] = fmaf(gv, a2, pw[sweep][2]);
-          a0 = a1;
-          a1 = a2;
+        for (int j = 0; j < kConvC * kConvH / 4; ++j) {
+          const float4 w4 = wr[j];
+          float* a = &acc[0][0] + 4 * j;
+          a[0] = fmaf(w4.x, gv, a[0]);
+          a[1] = fmaf(w4.y, gv, a[1]);
+          a[2] = fmaf(w4.z, gv, a[2]);
+          a[3] = fmaf(w4.w, gv, a[3]);
         }
       }
-    }
-    if (tid < kConvO) {
-      float s = 0.f;
-      for (int x = 0; x < Wo; ++x) s += s_g[tid * kConvLd + x];
-      pb += s;
-    }
-  }
-  float* dst = part + (int64_t)blockIdx.x * (kConvWg + kConvO);
+      float* dst = g_in + b * (int64_t)(kConvC * kConvH * W);
 #pragma unroll
-  for (int sweep = 0; sweep < 2; ++sweep) {
-    const int t = tid + sweep * kConvThreads;
-    if (t < kConvO * kConvC * kConvH) {
+      for (int c = 0; c < kConvC; ++c)
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) dst[t * 3 + dx] = pw[sweep][dx];
+        for (int dy = 0; dy < kConvH; ++dy) dst[(c * kConvH + dy) * W + xp] = acc[c][dy];
     }
+#endif
+#ifndef MVML_CONV_NOW
+    if (wrole) {
+      const float* gi = s_g + wo * kConvLd;
+      const float* a0p = s_in + (wc * kConvH + 0) * kConvLd;
+      const float* a1p = s_in + (wc * kConvH + 1) * kConvLd;
+      const float* a2p = s_in + (wc * kConvH + 2) * kConvLd;
+      float w0[kConvH] = {a0p[x0], a1p[x0], a2p[x0]};
+      float w1[kConvH] = {a0p[x0 + 1], a1p[x0 + 1], a2p[x0 + 1]};
+#pragma unroll 4
+      for (int x = x0; x < x1; ++x) {
+        const float gv = gi[x];
+        const float w2[kConvH] = {a0p[x + 2], a1p[x + 2], a2p[x + 2]};
+#pragma unroll
+        for (int dy = 0; dy < kConvH; ++dy) {
+          pw[dy][0] = fmaf(gv, w0[dy], pw[dy][0]);
+          pw[dy][1] = fmaf(gv, w1[dy], pw[dy][1]);
+          pw[dy][2] = fmaf(gv, w2[dy], pw[dy][2]);
+          w0[dy] = w1[dy];
+          w1[dy] = w2[dy];
+        }
+      }
+      if (wh == 0 && wc == 0) {
+        float s = 0.f;
+        for (int x = 0; x < Wo; ++x) s += gi[x];
+        pb += s;
+      }
+    }
+#endif
   }
-  if (tid < kConvO) dst[kConvWg + tid] = pb;
+  if (wrole) {
+    float* dst = part + (int64_t)blockIdx.x * kConvPart + wh * kConvWg;
+#pragma unroll
+    for (int dy = 0; dy < kConvH; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) dst[((wo * kConvC + wc) * 3 + dy) * 3 + dx] = pw[dy][dx];
+    if (wh == 0 && wc == 0) part[(int64_t)blockIdx.x * kConvPart + 2 * kConvWg + wo] = pb;
+  }
 }
 
-// Fixed-order sum of the per-workgroup partials: out[i] = sum_blk part[blk * stride + i].
-__global__ void partial_sum_kernel(int nblk, int count, int stride, const float* __restrict__ part,
-                                   float* __restrict__ out) {
+// Fixed-order sum of the per-workgroup partials: out[i] = sum_blk sum_j<nsub
+// part[blk * stride + j * sub_stride + i].
+__global__ void partial_sum_kernel(int nblk, int count, int stride, int nsub, int sub_stride,
+                                   const float* __restrict__ part, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
-  float s = 0.f;
-  for (int k = 0; k < nblk; ++k) s += part[(int64_t)k * stride + i];
-  out[i] = s;
+  // eight independent partial sums keep eight loads in flight (the loop is latency-bound);
+  // the fixed combination order keeps the result deterministic
+  const int n = nblk * nsub;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto at = [&](int r) { return part[(int64_t)(r / nsub) * stride + (r % nsub) * sub_stride + i]; };
+  int r = 0;
+  for (; r + 8 <= n; r += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += at(r + u);
+  }
+  for (; r < n; ++r) a[0] += at(r);
+  out[i] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
 // BCEWithLogitsLoss (mean over all B x C logits, main.py:91): per-element loss terms (summed by
@@ -454,10 +515,10 @@ extern "C" int mvml_conv3_fwd(int64_t B, int C, int O, int W, const float* in, c
   return check_launch("conv3_fwd_kernel");
 }
 
-static int64_t conv3_blocks(int64_t B) { return std::min<int64_t>(B, 2048); }
+static int64_t conv3_blocks(int64_t B) { return std::min<int64_t>(B, 512); }  // 2 per CU
 
 extern "C" size_t mvml_conv3_bwd_workspace_size(int64_t B) {
-  return carve_size((size_t)conv3_blocks(B > 0 ? B : 1) * (kConvWg + kConvO) * sizeof(float));
+  return carve_size((size_t)conv3_blocks(B > 0 ? B : 1) * kConvPart * sizeof(float));
 }
 
 extern "C" int mvml_conv3_bwd(int64_t B, int C, int O, int W, const float* in, const float* weight,
@@ -479,12 +540,12 @@ extern "C" int mvml_conv3_bwd(int64_t B, int C, int O, int W, const float* in, c
                                                             g_in, part);
   int rc = check_launch("conv3_bwd_kernel");
   if (rc) return rc;
-  const int n = kConvWg + kConvO;  // partial row: 1296 weight sums, then 12 bias sums
-  partial_sum_kernel<<<(unsigned)ceil_div(kConvWg, 256), 256, 0, st>>>((int)used, kConvWg, n, part,
-                                                                       g_weight);
+  // partial row: two column halves of the 1296 weight sums, then the 12 bias sums
+  partial_sum_kernel<<<(unsigned)ceil_div(kConvWg, 256), 256, 0, st>>>(
+      (int)used, kConvWg, kConvPart, 2, kConvWg, part, g_weight);
   rc = check_launch("partial_sum_kernel(w)");
   if (rc) return rc;
-  partial_sum_kernel<<<1, 64, 0, st>>>((int)used, kConvO, n, part + kConvWg, g_bias);
+  partial_sum_kernel<<<1, 64, 0, st>>>((int)used, kConvO, kConvPart, 1, 0, part + 2 * kConvWg, g_bias);
   return check_launch("partial_sum_kernel(b)");
 }
 
