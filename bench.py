@@ -223,6 +223,7 @@ def main():
             roofline["traffic"] = load_traffic("gat_agg_fwd")
         if summ.get("mvml_gat_agg_bwd"):
             extra["roofline_agg_bwd"] = roofline_entry(summ["mvml_gat_agg_bwd"], "hbm")
+            extra["roofline_agg_bwd"]["traffic"] = load_traffic("gat_agg_bwd")
         gemm_ev = summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", []) + summ.get("mvml_gat_proj_fwd", [])
         if gemm_ev:
             extra["roofline_gemm"] = roofline_entry(gemm_ev, "mfma")

@@ -19,7 +19,7 @@ from collections import defaultdict
 
 ENTRIES = {  # C-ABI entry point -> its kernels (name substrings)
     "gat_agg_fwd": ["gat_softmax_kernel", "gat_agg_fwd_lds_kernel", "gat_agg_fwd_gather_kernel"],
-    "gat_agg_bwd": ["gat_agg_bwd_dst_kernel", "gat_agg_bwd_src_kernel"],
+    "gat_agg_bwd": ["gat_agg_bwd_lds_kernel", "gat_agg_bwd_dst_kernel", "gat_agg_bwd_src_kernel"],
     "set2set_seg_fwd": ["seg_fwd_kernel"],
 }
 
