@@ -131,3 +131,38 @@ def test_state_dict_layout_matches_reference():
     assert keys[:5] == ["conv.gnn_layers.0.gat_conv.attn_l", "conv.gnn_layers.0.gat_conv.attn_r",
                         "conv.gnn_layers.0.gat_conv.bias", "conv.gnn_layers.0.gat_conv.fc.weight",
                         "conv.gnn_layers.0.gat_conv.res_fc.weight"]
+
+
+# ------------------------------------------------------------------ fusion head / node groups
+def test_fusion_state_dict_matches_reference_layout():
+    """MVFusion carries MVP's fusion parameters under MVP's names and shapes (model.py:23-45)."""
+    from oracle.fusion_ref import MVFusionRef
+    ref, mod = MVFusionRef(), mvml_gat.MVFusion()
+    assert {k: tuple(v.shape) for k, v in ref.state_dict().items()} == \
+           {k: tuple(v.shape) for k, v in mod.state_dict().items()}
+    assert tuple(mod.linear_q.weight.shape) == (4608, 384) and mod.mlp[3].out_features == 11
+
+
+def test_node_group_plan_oracle_invariants():
+    """Every group is a run of whole molecules, groups tile the atoms, and the kinds route
+    exactly the groups that exceed the LDS kernels' caps to the fallback lists."""
+    sb = synth.config5(12, seed=2)  # 150-400-atom molecules with hubs: fallback groups too
+    ref = graph_ref.batch_ref(sb.num_nodes, sb.src_local, sb.dst_local, sb.num_edges)
+    N = int(ref["node_offsets"][-1])
+    csr = graph_ref.csr_ref(ref["src"], ref["dst"], N)
+    starts, kinds, fwd, bwd = graph_ref.node_group_plan_ref(ref["node_offsets"], csr["in_rowptr"])
+    mol_starts = set(int(x) for x in ref["node_offsets"])
+    assert starts[0] == 0 and starts[-1] == N and np.all(np.diff(starts) >= 0)
+    assert all(int(s) in mol_starts for s in starts)
+    rp = csr["in_rowptr"]
+    for g in range(len(kinds)):
+        a0, a1 = int(starts[g]), int(starts[g + 1])
+        if a1 == a0:
+            assert kinds[g] == 0 and g not in fwd and g not in bwd
+            continue
+        # edges stay inside the group (molecule-closed)
+        srcs = csr["in_src"][rp[a0]:rp[a1]]
+        assert srcs.min() >= a0 and srcs.max() < a1
+        fits = a1 - a0 <= 128 and rp[a1] - rp[a0] <= 512
+        assert bool(kinds[g] & 2) == fits and (g in bwd) == (not fits)
+        assert bool(kinds[g] & 1) == (fits and np.max(np.diff(rp[a0:a1 + 1])) <= 5)

@@ -182,3 +182,22 @@ def test_fp32_reference_error_budget():
         y32 = ref.float()(gd, X.float())
         y64 = ref.double()(gd, X.double())
     assert rel_err(y32, y64) < 1e-5
+
+
+def test_fusion_identical_views_give_uniform_attention():
+    """model.py:62-68: with the three view tokens identical, every score row is constant, so the
+    softmax is uniform and each token's attention output equals v."""
+    from oracle.fusion_ref import MVFusionRef
+    torch.manual_seed(0)
+    m = MVFusionRef(dim=8, num_heads=2, num_classes=3, dropout=0.0).double().eval()
+    x = torch.randn(4, 8, **D64)
+    ln = m.norm_layer_module(x)
+    v = m.linear_v(ln).reshape(4, 2, 8)                      # (B, nh, dk)
+    q = m.linear_q(ln).reshape(4, 1, 2, 8).expand(4, 3, 2, 8).transpose(1, 2)
+    k = m.linear_k(ln).reshape(4, 1, 2, 8).expand(4, 3, 2, 8).transpose(1, 2)
+    p = torch.softmax(q @ k.transpose(2, 3) * m._norm_fact, -1)
+    assert torch.allclose(p, torch.full_like(p, 1 / 3))
+    att = p @ v.unsqueeze(2).expand(4, 2, 3, 8)
+    assert torch.allclose(att, v.unsqueeze(2).expand(4, 2, 3, 8))
+    out = m.conv(att).view(4, -1)
+    assert torch.allclose(m.mlp(out), m(x, x, x))
