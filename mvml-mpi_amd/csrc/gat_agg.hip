@@ -524,19 +524,24 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
 #define MVML_BWD_WAVES 4
 #endif
 // Backward LDS layout: Z and g_rst chunks of the group's rows, 16-B slot c of row r at
-// r*8 + (c ^ bwd_sw(r)) (spreads whole-row reads of different atoms over the banks).
-__device__ __forceinline__ int bwd_sw(int r) { return (r >> 1) & 7; }
+// r*LPD + (c ^ bwd_sw<LPD>(r)): 128-B rows (LPD = 8) are XOR-swizzled so whole-row reads of
+// different atoms spread over the banks; 256-B rows (LPD = 16) already span all 64 banks.
+template <int LPD>
+__device__ __forceinline__ int bwd_sw(int r) { return LPD == 8 ? (r >> 1) & 7 : 0; }
 
 // DPP move within a row of 16 lanes (bound_ctrl: sources outside the row read 0).
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
-// Sum over each aligned octet of lanes; the result is valid in the octet's lanes 4..7.
-__device__ __forceinline__ float octet_sum_hi(float v) {
+// Sum over each aligned group of LPD (8 or 16) lanes; valid in the group's last four lanes.
+template <int LPD>
+__device__ __forceinline__ float grp_sum_hi(float v) {
   v += dppf<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dppf<0x4E>(v);   // quad_perm [2,3,0,1]
-  return v + dppf<0x114>(v);  // row_shr:4
+  v += dppf<0x114>(v);  // row_shr:4
+  if (LPD == 16) v += dppf<0x118>(v);  // row_shr:8
+  return v;
 }
 
 // Chunk loop of the backward LDS kernel for a group of at most NPA * 64 atoms: 8 lanes per row
@@ -551,14 +556,14 @@ __device__ __forceinline__ float octet_sum_hi(float v) {
 // its slice of g_rst[d], a DPP octet sum finishes the dot, and one lane per edge adds it to
 // s_ga (zeroed by the caller; every (edge, head) has exactly one writer).  That reads each
 // source row slice once per in-edge: half the LDS bytes of an edge-per-thread dot.
-template <int H, int MODE, int NPA>
+template <int H, int MODE, int NPA, int CW>
 __device__ __forceinline__ void bwd_lds_chunks(
     float4* zs, float4* gs, const float* s_att, const int* s_odst, const int* s_oslot,
     const int* s_orp, const int* s_rp, const int* s_src, float* s_ga,
     __amdgpu_buffer_rsrc_t rY, int ldyi, __amdgpu_buffer_rsrc_t rGo, __amdgpu_buffer_rsrc_t rO,
     __amdgpu_buffer_rsrc_t rG, int ldgi, int nr, int F) {
   static_assert(kEC == 5, "in-edge writer lanes assume 5 cached in-edges");
-  constexpr int CW = 32, LPD = CW / 4, DPP = kAggThreads / LPD;
+  constexpr int LPD = CW / 4, NT = 16 * CW, DPP = NT / LPD;
   const int tid = threadIdx.x, ds = tid / LPD, q = tid % LPD;
   const int HF = H * F, nfc = F / CW, nch = H * nfc;
   const int ocols = MODE == 1 ? F : HF;
@@ -589,7 +594,7 @@ __device__ __forceinline__ void bwd_lds_chunks(
     for (int i = 0; i < kEC; ++i) {
       const bool ok = ob[p] + i < oend[p];
       const int rr = ok ? s_odst[ob[p] + i] : r;
-      gsl[p][i] = (uint32_t)(rr * LPD + (q ^ bwd_sw(rr))) |
+      gsl[p][i] = (uint32_t)(rr * LPD + (q ^ bwd_sw<LPD>(rr))) |
                   ((uint32_t)(ok ? s_oslot[ob[p] + i] * H : kECap * H) << 16);
     }
   }
@@ -605,7 +610,7 @@ __device__ __forceinline__ void bwd_lds_chunks(
 #pragma unroll
     for (int i = 0; i < kEC; ++i) {
       const int sr = i < ideg[p] ? s_src[ieb[p] + i] : d;
-      zsl[p][i] = (uint32_t)(sr * LPD + (q ^ bwd_sw(sr)));
+      zsl[p][i] = (uint32_t)(sr * LPD + (q ^ bwd_sw<LPD>(sr)));
     }
   }
   auto head_of = [&](int k) { return MODE == 1 ? k % H : k / nfc; };
@@ -642,8 +647,8 @@ __device__ __forceinline__ void bwd_lds_chunks(
         const float hh = (float)H;
         g = make_float4(g.x / hh, g.y / hh, g.z / hh, g.w / hh);
       }
-      zs[r * LPD + (q ^ bwd_sw(r))] = R.z[p];
-      gs[r * LPD + (q ^ bwd_sw(r))] = g;
+      zs[r * LPD + (q ^ bwd_sw<LPD>(r))] = R.z[p];
+      gs[r * LPD + (q ^ bwd_sw<LPD>(r))] = g;
       if (MODE != 1) buf_st4(rG, ok ? grow(p) + 4u * (uint32_t)(HF + col_of(k)) : noG, g);
       else if (h == 0)  // uniform branch: an all-out-of-range store is not free
         buf_st4(rG, ok ? grow(p) + 4u * (uint32_t)(HF + fc * CW + 4 * q) : noG, R.g[p]);
@@ -666,20 +671,20 @@ __device__ __forceinline__ void bwd_lds_chunks(
 #pragma unroll
     for (int p = 0; p < NPA; ++p) {  // g_a partials of the in-edges of destination d
       const int d = ds + DPP * p;
-      const float4 gd = gs[d * LPD + (q ^ bwd_sw(d))];
+      const float4 gd = gs[d * LPD + (q ^ bwd_sw<LPD>(d))];
       float t[kEC];
 #pragma unroll
-      for (int i = 0; i < kEC; ++i) t[i] = octet_sum_hi(dot4(zs[zsl[p][i]], gd));
-      if (q >= 4) {  // lanes 4..7 write in-edges 0..3, lane 4 also in-edge 4
-        const int i0 = q - 4;
+      for (int i = 0; i < kEC; ++i) t[i] = grp_sum_hi<LPD>(dot4(zs[zsl[p][i]], gd));
+      if (q >= LPD - 4) {  // the group's last 4 lanes write in-edges 0..3, the first of them 4
+        const int i0 = q - (LPD - 4);
         const float v = i0 == 0 ? t[0] : i0 == 1 ? t[1] : i0 == 2 ? t[2] : t[3];
         if (i0 < ideg[p]) s_ga[(ieb[p] + i0) * H + h] += v;
         if (i0 == 0 && ideg[p] > 4) s_ga[(ieb[p] + 4) * H + h] += t[4];
       }
       for (int i = kEC; i < ideg[p]; ++i) {  // hubs (octet-uniform trip count)
         const int sr = s_src[ieb[p] + i];
-        const float v = octet_sum_hi(dot4(zs[sr * LPD + (q ^ bwd_sw(sr))], gd));
-        if (q == 4) s_ga[(ieb[p] + i) * H + h] += v;
+        const float v = grp_sum_hi<LPD>(dot4(zs[sr * LPD + (q ^ bwd_sw<LPD>(sr))], gd));
+        if (q == LPD - 4) s_ga[(ieb[p] + i) * H + h] += v;
       }
     }
 #endif
@@ -692,7 +697,7 @@ __device__ __forceinline__ void bwd_lds_chunks(
       for (int i = 0; i < kEC; ++i)
         acc[p] = fma4(s_att[(gsl[p][i] >> 16) + h], gs[gsl[p][i] & 0xFFFFu], acc[p]);
       for (int o = ob[p] + kEC; o < oend[p]; ++o)
-        acc[p] = fma4(s_att[s_oslot[o] * H + h], gs[s_odst[o] * LPD + (q ^ bwd_sw(s_odst[o]))], acc[p]);
+        acc[p] = fma4(s_att[s_oslot[o] * H + h], gs[s_odst[o] * LPD + (q ^ bwd_sw<LPD>(s_odst[o]))], acc[p]);
 #endif
     }
     __syncthreads();
@@ -710,8 +715,8 @@ __device__ __forceinline__ void bwd_lds_chunks(
 // One workgroup of 512 threads per node group (2 per CU): the group's CSR, out-CSR and
 // attention are staged in LDS, the column chunks stream through bwd_lds_chunks (one pass for
 // groups of <= 64 atoms, two up to kWinL), then the softmax backward runs in LDS.
-template <int H, int MODE>
-__global__ void __launch_bounds__(kAggThreads, MVML_BWD_WAVES)
+template <int H, int MODE, int CW>
+__global__ void __launch_bounds__(16 * CW, MVML_BWD_WAVES)
 gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                        const int32_t* __restrict__ in_src, const int32_t* __restrict__ out_rowptr,
                        const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
@@ -719,7 +724,7 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
                        const float* __restrict__ attn, const float* __restrict__ out,
                        const float* __restrict__ g_out, float slope, float* __restrict__ gY,
                        int64_t ldgy, int C) {
-  constexpr int NT = kAggThreads, LPD = 8;
+  constexpr int NT = 16 * CW, LPD = CW / 4;
   static_assert(NT / LPD * 2 == kWinL, "two passes of 64 rows");
   __shared__ float4 zs[kWinL * LPD];
   __shared__ float4 gs[kWinL * LPD];
@@ -755,10 +760,10 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   for (int i = tid; i < ne * H; i += NT) s_ga[i] = 0.f;
   __syncthreads();  // CSR / attention staged
   if (nr <= NT / LPD)
-    bwd_lds_chunks<H, MODE, 1>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp, s_src, s_ga, rY,
+    bwd_lds_chunks<H, MODE, 1, CW>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp, s_src, s_ga, rY,
                                ldyi, rGo, rO, rG, ldgi, nr, F);
   else
-    bwd_lds_chunks<H, MODE, 2>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp, s_src, s_ga, rY,
+    bwd_lds_chunks<H, MODE, 2, CW>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp, s_src, s_ga, rY,
                                ldyi, rGo, rO, rG, ldgi, nr, F);
   __syncthreads();
   // edge_softmax backward per (destination, head); g_pre replaces g_a in LDS
@@ -1032,13 +1037,24 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
                const float* g_out, int F, float slope, int mode, float* gpre, float* gY,
                int64_t ldgy, int C, hipStream_t st) {
   if (F % 32 == 0 && G > 0) {  // molecule groups: one pass over Z / g_out / dZ per group
-#define MVML_BWD_LDS(M)                                                                          \
-    gat_agg_bwd_lds_kernel<H, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, G, rp, src, orp, odst, \
-                                                                     oslot, Y, ldy, F, elr, attn, \
-                                                                     out, g_out, slope, gY, ldgy, C)
-    if (mode == 0) MVML_BWD_LDS(0);
-    else if (mode == 1) MVML_BWD_LDS(1);
-    else MVML_BWD_LDS(2);
+#ifndef MVML_BWD_CW64
+#define MVML_BWD_CW64 1
+#endif
+    // 64-column chunks (256-B row segments, half the chunks and barriers; one 1024-thread
+    // workgroup per CU) when F allows, else 32-column chunks (two 512-thread workgroups per CU)
+#define MVML_BWD_LDS(M, CW)                                                                       \
+    gat_agg_bwd_lds_kernel<H, M, CW><<<(unsigned)G, 16 * CW, 0, st>>>(groups, G, rp, src, orp, odst, \
+                                                                      oslot, Y, ldy, F, elr, attn, \
+                                                                      out, g_out, slope, gY, ldgy, C)
+    if (MVML_BWD_CW64 && F % 64 == 0) {
+      if (mode == 0) MVML_BWD_LDS(0, 64);
+      else if (mode == 1) MVML_BWD_LDS(1, 64);
+      else MVML_BWD_LDS(2, 64);
+    } else {
+      if (mode == 0) MVML_BWD_LDS(0, 32);
+      else if (mode == 1) MVML_BWD_LDS(1, 32);
+      else MVML_BWD_LDS(2, 32);
+    }
 #undef MVML_BWD_LDS
     int rc = check_launch("gat_agg_bwd_lds_kernel");
     if (rc) return rc;
