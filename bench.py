@@ -32,7 +32,7 @@ METRIC = "molecules/sec GAT-view fwd+bwd at 1/2/4/8 GPU; % HBM peak on aggregati
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 FP32_MFMA_PEAK_TFS = 157.3  # f32-input MFMA = f32 vector peak (same table)
 BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA peak (same table; the 5 PF figure is 2:1 sparse)
-TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32x3", "mvml_gat_proj_fwd", "mvml_set2set_seg_fwd",
+TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32x3", "mvml_gemm_bf16", "mvml_gat_proj_fwd", "mvml_set2set_seg_fwd",
          "mvml_set2set_seg_bwd", "mvml_lstm_cell_fwd", "mvml_lstm_cell_bwd", "mvml_set2set_gx",
          "mvml_graphnorm_fwd", "mvml_graphnorm_bwd", "mvml_colsum_f32", "mvml_gat_fold_weights",
          "mvml_gat_unfold_grads", "mvml_relu_bwd", "mvml_layernorm_fwd", "mvml_layernorm_bwd",
@@ -55,6 +55,10 @@ def parse():
                     help="config 3 with its consumer: the MVP fusion head (SURVEY 8f-1) + BCE loss "
                          "on the GAT view's output (the SMILES / fingerprint views, out of scope, "
                          "are synthetic fixed embeddings)")
+    ap.add_argument("--proj-bf16", action="store_true",
+                    help="BASELINE config 4: the GAT projection GEMMs (fc / res_fc, forward and "
+                         "backward) on bf16 operands with fp32 accumulation (mvml_gemm_bf16); "
+                         "everything else stays fp32")
     return ap.parse_args()
 
 
@@ -162,7 +166,8 @@ def main():
     log(f"[rank {rank}] data: {B} molecules, {N} atoms, {E} edges ({time.perf_counter() - t_gen:.1f}s)")
 
     torch.manual_seed(args.seed)
-    model = mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3).to(dev).train()
+    model = mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3,
+                               proj_dtype=torch.bfloat16 if args.proj_bf16 else None).to(dev).train()
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4)
     reducer = FlatGradAllReduce(model.parameters(), average=True)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -224,7 +229,14 @@ def main():
         if summ.get("mvml_gat_agg_bwd"):
             extra["roofline_agg_bwd"] = roofline_entry(summ["mvml_gat_agg_bwd"], "hbm")
             extra["roofline_agg_bwd"]["traffic"] = load_traffic("gat_agg_bwd")
-        gemm_ev = summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", []) + summ.get("mvml_gat_proj_fwd", [])
+        proj_ev = summ.get("mvml_gat_proj_fwd", [])
+        gemm_ev = summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", []) + ([] if args.proj_bf16 else proj_ev)
+        bf_ev = summ.get("mvml_gemm_bf16", []) + (proj_ev if args.proj_bf16 else [])
+        if bf_ev:
+            extra["roofline_gemm_bf16"] = roofline_entry(bf_ev, "mfma")
+            extra["roofline_gemm_bf16"].update(
+                peak=BF16_MFMA_PEAK_TFS, note="GAT projection GEMMs on bf16 operands (config 4)",
+                frac=round(extra["roofline_gemm_bf16"]["achieved"] / BF16_MFMA_PEAK_TFS, 4))
         if gemm_ev:
             extra["roofline_gemm"] = roofline_entry(gemm_ev, "mfma")
             if summ.get("mvml_gemm_f32x3"):
@@ -243,7 +255,8 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "molecules/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16 projection, f32 elsewhere" if args.proj_bf16 else "f32",
             "data": "synthetic (seeded KEGG-like drug-like molecules, random-init weights)",
             "config": {"workload": "BASELINE config 3: GNNModule (GAT [192,384] x4 heads, Set2Set 6x3, "
                                    "GraphNorm, fc) fwd+bwd+Adam over KEGG-like molecules"
@@ -251,7 +264,9 @@ def main():
                                       "+ BCEWithLogits" if args.with_fusion else
                                       " (fixed upstream gradient at the view output)"),
                        "mols_per_gpu": B, "atoms_per_gpu": N, "edges_per_gpu": E,
-                       "graphnorm_group": args.group_size, "parallelism": f"dp{world}"},
+                       "graphnorm_group": args.group_size, "parallelism": f"dp{world}",
+                       "projection": "bf16 operands, fp32 accumulate (config 4)" if args.proj_bf16
+                       else "fp32-accurate split-bf16 x3"},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         line.update(extra)

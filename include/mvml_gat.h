@@ -104,8 +104,16 @@ int mvml_gemm_f32x3(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                     const float* A, int64_t lda, const float* B, int64_t ldb,
                     const float* bias, float beta, int act, float* C, int64_t ldc,
                     void* workspace, size_t workspace_bytes, void* stream);
+/* bf16 operands (round-to-nearest-even from the fp32 inputs), one v_mfma_f32_32x32x16_bf16 per
+ * fragment pair, fp32 accumulate: the "bf16 projection on MFMA" of BASELINE.json config 4
+ * (accuracy bar 2e-2 relative, north_star).  Same arguments / workspace as mvml_gemm_f32. */
+int mvml_gemm_bf16(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                   const float* A, int64_t lda, const float* B, int64_t ldb,
+                   const float* bias, float beta, int act, float* C, int64_t ldc,
+                   void* workspace, size_t workspace_bytes, void* stream);
 #define MVML_GEMM_F32 0   /* algo: v_mfma_f32_32x32x2_f32 */
 #define MVML_GEMM_F32X3 1 /* algo: split-bf16 x3 */
+#define MVML_GEMM_BF16 2  /* algo: bf16 operands, fp32 accumulate */
 /* Column sums: out[n] = beta*out[n] + alpha * sum_m X[m*ldx + n], deterministic two-stage
  * tree.  Replaces the bias gradients torch autograd computes for GATConv.bias / LSTM / Linear. */
 size_t mvml_colsum_workspace_size(int64_t M, int64_t N);

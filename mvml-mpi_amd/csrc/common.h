@@ -95,7 +95,7 @@ __device__ __forceinline__ int64_t xcd_block(unsigned b, unsigned nb) {
 }
 
 // gemm_f32.hip: projection GEMM with the GAT logits-partial epilogue (see ProjEpi there).
-int gemm_proj_epi(bool x3, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                   const float* B, int64_t ldb, float* C, int64_t ldc, const float* vec, int cols,
                   int logw, float* part, hipStream_t st);
 // Partial-logit group width of mvml_gat_proj_fwd: the largest power of two <= 32 dividing F.

@@ -1238,8 +1238,9 @@ extern "C" int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx,
   MVML_REQUIRE(attn_lr != nullptr && elr != nullptr, "gat_proj_fwd: attn_lr and elr are required");
   hipStream_t st = as_stream(stream);
   float* part = static_cast<float*>(workspace);
-  MVML_REQUIRE(algo == MVML_GEMM_F32 || algo == MVML_GEMM_F32X3, "gat_proj_fwd: bad algo %d", algo);
-  int rc = gemm_proj_epi(algo == MVML_GEMM_F32X3, num_nodes, C, K, X, ldx, Wcat, ldw, Y, ldy,
+  MVML_REQUIRE(algo == MVML_GEMM_F32 || algo == MVML_GEMM_F32X3 || algo == MVML_GEMM_BF16,
+               "gat_proj_fwd: bad algo %d", algo);
+  int rc = gemm_proj_epi(algo, num_nodes, C, K, X, ldx, Wcat, ldw, Y, ldy,
                          attn_lr, H * F, proj_logw(F), part, st);
   if (rc) return rc;
   const int W = 1 << proj_logw(F);

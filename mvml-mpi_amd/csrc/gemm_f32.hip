@@ -678,10 +678,10 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-template <bool KMAJ>
+template <bool KMAJ, int NP = 3>
 struct XOp {
   static constexpr int kPlane = KMAJ ? XBK * kXKmajPitch : 256 * 32;
-  static constexpr int kBytes = 3 * kPlane;
+  static constexpr int kBytes = NP * kPlane;  // NP = 3 split-bf16 planes, 1 = plain bf16
 
   // This thread's 8 values of a 256 x 16 operand tile (rows r0.., k0..):
   //  K-contiguous: rows (tid >> 2) + 128 i, k = 4 (tid & 3) + [0, 4) in v[i] (16 rows x 64 B per
@@ -740,7 +740,13 @@ struct XOp {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       uint2 p0, p1, p2;
-      split4(v[i].x, v[i].y, v[i].z, v[i].w, p0, p1, p2);
+      if constexpr (NP == 3) {
+        split4(v[i].x, v[i].y, v[i].z, v[i].w, p0, p1, p2);
+      } else {  // bf16 operands: round-to-nearest-even, one plane
+        const f32x2 u = {v[i].x, v[i].y}, w = {v[i].z, v[i].w};
+        p0.x = __builtin_bit_cast(uint32_t, __builtin_convertvector(u, bf16x2));
+        p0.y = __builtin_bit_cast(uint32_t, __builtin_convertvector(w, bf16x2));
+      }
       uint32_t off;
       if (!KMAJ) {
         const int row = (tid >> 2) + 128 * i, q = tid & 3;
@@ -749,8 +755,10 @@ struct XOp {
         off = (2 * (tid >> 6) + i) * kXKmajPitch + 8 * (tid & 63);
       }
       *reinterpret_cast<uint2*>(op + off) = p0;
-      *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
-      *reinterpret_cast<uint2*>(op + 2 * kPlane + off) = p2;
+      if constexpr (NP == 3) {
+        *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
+        *reinterpret_cast<uint2*>(op + 2 * kPlane + off) = p2;
+      }
     }
   }
 
@@ -781,14 +789,16 @@ struct XOp {
 // FAST (host-checked: both operands 16-B aligned rows, K-major row counts % 4 == 0): whole
 // stages by unguarded loads from clamped rows, the K tail as one guarded stage; !FAST: every
 // stage guarded.
-template <bool AK, bool BKM, int EPI_LOGW = -1, bool FAST = true>
+// NP = 3: fp32-accurate split-bf16 (six MFMAs per fragment pair); NP = 1: bf16 operands
+// (one MFMA per pair, fp32 accumulate) — the bf16 projection of BASELINE config 4.
+template <bool AK, bool BKM, int EPI_LOGW = -1, bool FAST = true, int NP = 3>
 __global__ void __launch_bounds__(kXThreads, MVML_X3W_WAVES)  // one workgroup per CU
 gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
                 float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{}) {
-  using OA = XOp<AK>;
-  using OB = XOp<BKM>;
+  using OA = XOp<AK, NP>;
+  using OB = XOp<BKM, NP>;
   constexpr int kStage = OA::kBytes + OB::kBytes;
   __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kStage];
   const int64_t tiles_n = ceil_div(N, XBN);
@@ -873,11 +883,11 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   auto body = [&](int64_t t, auto STAGE, auto LOAD) {
     const uint8_t* sa = lds + (t & 1) * kStage;
     const uint8_t* sb = sa + OA::kBytes;
-    bf16x8 fb[2][3];
+    bf16x8 fb[2][NP];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) fb[j][p] = OB::frag(sb, p, wn * 64 + 32 * j, lane);
+      for (int p = 0; p < NP; ++p) fb[j][p] = OB::frag(sb, p, wn * 64 + 32 * j, lane);
     if constexpr (decltype(STAGE)::value) stage((t + 1) & 1);
     if constexpr (decltype(LOAD)::value == 1) load_fast();
     if constexpr (decltype(LOAD)::value == 2) load_guarded(t + 2);
@@ -885,11 +895,16 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      bf16x8 fa[3];
+      bf16x8 fa[NP];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) fa[p] = OA::frag(sa, p, wm * 128 + 32 * i, lane);
+      for (int p = 0; p < NP; ++p) fa[p] = OA::frag(sa, p, wm * 128 + 32 * i, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x3(fa, fb[j], acc[i][j]);
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (NP == 3)
+          acc[i][j] = mfma_x3(fa, fb[j], acc[i][j]);
+        else
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][0], acc[i][j], 0, 0, 0);
+      }
     }
     if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
@@ -1005,10 +1020,15 @@ struct GemmPlan {
   bool wide;
   int S;
 };
-GemmPlan plan_gemm(bool x3, int64_t M, int64_t N, int64_t K) {
+constexpr int kPrecF32 = 0, kPrecX3 = 1, kPrecBf16 = 2;  // = MVML_GEMM_* algo ids
+GemmPlan plan_gemm(int prec, int64_t M, int64_t N, int64_t K) {
   const char* env = getenv("MVML_X3_TILE");
   const int force = env ? atoi(env) : 0;
-  if (x3) {
+  if (prec == kPrecBf16) {  // bf16 operands exist only in the 256x256 kernel
+    const int64_t tw = ceil_div(M, XBM) * ceil_div(N, XBN);
+    return {true, choose_splits_t(tw, K, 256)};
+  }
+  if (prec == kPrecX3) {
     const int64_t tw = ceil_div(M, XBM) * ceil_div(N, XBN);
     const int Sw = choose_splits_t(tw, K, 256);
     if (force == 256 || (force != 128 && tw * Sw >= 192)) return {true, Sw};
@@ -1072,7 +1092,7 @@ extern "C" size_t mvml_gemm_workspace_size(int64_t M, int64_t N, int64_t K) {
 }
 
 namespace {
-int gemm_launch(bool x3, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                 const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
                 float beta, int act, float* C, int64_t ldc, void* workspace,
                 size_t workspace_bytes, void* stream);
@@ -1082,7 +1102,7 @@ extern "C" int mvml_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, i
                              const float* A, int64_t lda, const float* B, int64_t ldb,
                              const float* bias, float beta, int act, float* C, int64_t ldc,
                              void* workspace, size_t workspace_bytes, void* stream) {
-  return gemm_launch(false, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
+  return gemm_launch(kPrecF32, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
                      workspace, workspace_bytes, stream);
 }
 
@@ -1090,12 +1110,20 @@ extern "C" int mvml_gemm_f32x3(int a_kmajor, int b_kmajor, int64_t M, int64_t N,
                                const float* A, int64_t lda, const float* B, int64_t ldb,
                                const float* bias, float beta, int act, float* C, int64_t ldc,
                                void* workspace, size_t workspace_bytes, void* stream) {
-  return gemm_launch(true, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
+  return gemm_launch(kPrecX3, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
                      workspace, workspace_bytes, stream);
 }
 
+extern "C" int mvml_gemm_bf16(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                              const float* A, int64_t lda, const float* B, int64_t ldb,
+                              const float* bias, float beta, int act, float* C, int64_t ldc,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  return gemm_launch(kPrecBf16, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C,
+                     ldc, workspace, workspace_bytes, stream);
+}
+
 namespace {
-int gemm_launch(bool x3, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                 const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
                 float beta, int act, float* C, int64_t ldc, void* workspace,
                 size_t workspace_bytes, void* stream) {
@@ -1107,7 +1135,8 @@ int gemm_launch(bool x3, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
   MVML_REQUIRE(b_kmajor ? ldb >= N : ldb >= K, "gemm: bad ldb");
   MVML_REQUIRE(act == 0 || act == 1, "gemm: bad act");
   hipStream_t st = as_stream(stream);
-  const GemmPlan plan = plan_gemm(x3, M, N, K);
+  const bool x3 = prec == kPrecX3, bf = prec == kPrecBf16;
+  const GemmPlan plan = plan_gemm(prec, M, N, K);
   const int S = plan.S;
   float* slab = nullptr;
   if (S > 1) {
@@ -1125,7 +1154,13 @@ int gemm_launch(bool x3, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
   dim3 grid((unsigned)tiles, (unsigned)S);
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
   do {                                                                                          \
-    if (plan.wide && x3w_fast(AKV, BKV, M, N, K, av, bv))                                          \
+    if (bf && x3w_fast(AKV, BKV, M, N, K, av, bv))                                              \
+      gemm_x3w_kernel<AKV, BKV, -1, true, 1><<<grid, kXThreads, 0, st>>>(                       \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+    else if (bf)                                                                                \
+      gemm_x3w_kernel<AKV, BKV, -1, false, 1><<<grid, kXThreads, 0, st>>>(                      \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+    else if (plan.wide && x3w_fast(AKV, BKV, M, N, K, av, bv))                                  \
       gemm_x3w_kernel<AKV, BKV, -1, true><<<grid, kXThreads, 0, st>>>(                          \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
     else if (plan.wide)                                                                         \
@@ -1161,10 +1196,11 @@ int gemm_launch(bool x3, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
 namespace mvml {
 // Projection GEMM with the logits-partial epilogue: C[M,N] = A[M,K] B[N,K]^T (both
 // K-contiguous, no split-K: K is the small feature dimension), part as in ProjEpi.
-int gemm_proj_epi(bool x3, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                   const float* B, int64_t ldb, float* C, int64_t ldc, const float* vec, int cols,
                   int logw, float* part, hipStream_t st) {
-  const bool wide = x3 && plan_gemm(true, M, N, K).wide;
+  const bool x3 = prec == kPrecX3, bf = prec == kPrecBf16;
+  const bool wide = bf || (x3 && plan_gemm(kPrecX3, M, N, K).wide);
   const int64_t tiles = wide ? ceil_div(M, XBM) * ceil_div(N, XBN) : ceil_div(M, BM) * ceil_div(N, BN);
   MVML_REQUIRE(tiles < (int64_t(1) << 31), "gat_proj_fwd: too many tiles");
   MVML_REQUIRE(cols <= N && (logw >= 2 && logw <= 5), "gat_proj_fwd: bad partial width");
@@ -1173,7 +1209,15 @@ int gemm_proj_epi(bool x3, int64_t M, int64_t N, int64_t K, const float* A, int6
   dim3 grid((unsigned)tiles, 1);
 #define MVML_PROJ(LW)                                                                          \
   do {                                                                                         \
-    if (wide && x3w_fast(false, false, M, N, K, av, bv))                                          \
+    if (bf && x3w_fast(false, false, M, N, K, av, bv))                                         \
+      gemm_x3w_kernel<false, false, LW, true, 1><<<grid, kXThreads, 0, st>>>(                  \
+          M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
+          ProjEpi{vec, cols, part});                                                           \
+    else if (bf)                                                                               \
+      gemm_x3w_kernel<false, false, LW, false, 1><<<grid, kXThreads, 0, st>>>(                 \
+          M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
+          ProjEpi{vec, cols, part});                                                           \
+    else if (wide && x3w_fast(false, false, M, N, K, av, bv))                                  \
       gemm_x3w_kernel<false, false, LW, true><<<grid, kXThreads, 0, st>>>(                     \
           M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
           ProjEpi{vec, cols, part});                                                           \

@@ -60,7 +60,8 @@ def agg_bwd_bytes(N, E, H, F, gout_cols, mode):
 # (mvml_gemm_f32x3, the default), "f32" = f32-input MFMA (mvml_gemm_f32).  Both are parity-
 # tested against fp64 at the fp32 bar; override with MVML_GEMM_ALGO=f32.
 GEMM_ALGO = os.environ.get("MVML_GEMM_ALGO", "x3")
-_GEMM_ENTRY = {"f32": ("mvml_gemm_f32", 0), "x3": ("mvml_gemm_f32x3", 1)}
+_GEMM_ENTRY = {"f32": ("mvml_gemm_f32", 0), "x3": ("mvml_gemm_f32x3", 1),
+               "bf16": ("mvml_gemm_bf16", 2)}  # bf16: the projection option of config 4
 
 
 def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0, algo=None):
@@ -89,7 +90,7 @@ class GATLayerFunction(torch.autograd.Function):
     flatten/ELU or head-mean kernel."""
 
     @staticmethod
-    def forward(ctx, X, fc_w, res_w, attn_l, attn_r, bias, g, H, F, slope, mode):
+    def forward(ctx, X, fc_w, res_w, attn_l, attn_r, bias, g, H, F, slope, mode, algo=None):
         for t, n in ((X, "feat"), (fc_w, "fc.weight"), (res_w, "res_fc.weight")):
             _check_cuda_f32(t, n)
         X = _c(X)
@@ -117,7 +118,7 @@ class GATLayerFunction(torch.autograd.Function):
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_proj_fwd_workspace_size(N, H, F), dev)
         _lib.call_tag[0] = {"flops": 2 * N * C * Fp}
         call("mvml_gat_proj_fwd", N, ptr(Xp), Fp, Fp, ptr(Wcat), Fp, ptr(attn_lr), H, F, mean_res,
-             _GEMM_ENTRY[GEMM_ALGO][1], ptr(Y), ldy, ptr(elr), wp, wn, st)
+             _GEMM_ENTRY[algo or GEMM_ALGO][1], ptr(Y), ldy, ptr(elr), wp, wn, st)
         out_cols = F if mode == MODE_MEAN else HF
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()
@@ -129,6 +130,7 @@ class GATLayerFunction(torch.autograd.Function):
         ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr)
         ctx.Fin = Fin
         ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode, ctx.ldy = g, H, F, slope, mode, ldy
+        ctx.algo = algo
         return out
 
     @staticmethod
@@ -155,7 +157,7 @@ class GATLayerFunction(torch.autograd.Function):
              ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldg, wp, wn, st)
         # dL/d[Wcat ; A_l ; A_r] = gY^T X  (split-K over atoms)
         gW = torch.empty((CE, Fp), dtype=torch.float32, device=dev)
-        gemm(gY, Xp, CE, Fp, N, 1, 1, ldg, Fp, gW, Fp)
+        gemm(gY, Xp, CE, Fp, N, 1, 1, ldg, Fp, gW, Fp, algo=ctx.algo)
         g_fc = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_res = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_al = torch.empty_like(attn_l)
@@ -177,8 +179,8 @@ class GATLayerFunction(torch.autograd.Function):
         gX = None
         if ctx.needs_input_grad[0]:
             gX = torch.empty((N, Fin), dtype=torch.float32, device=dev)
-            gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin)
-        return gX, g_fc, g_res, g_al, g_ar, g_bias, None, None, None, None, None
+            gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, algo=ctx.algo)
+        return gX, g_fc, g_res, g_al, g_ar, g_bias, None, None, None, None, None, None
 
 
 class Set2SetFunction(torch.autograd.Function):

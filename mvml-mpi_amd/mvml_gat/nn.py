@@ -42,6 +42,10 @@ class GATConv(nn.Module):
         self.attn_r = nn.Parameter(torch.empty(1, num_heads, out_feats))
         self.bias = nn.Parameter(torch.empty(num_heads * out_feats))
         self.res_fc = nn.Linear(in_feats, num_heads * out_feats, bias=False)
+        # GEMM operand precision of fc / res_fc (forward and both backward products): None =
+        # fp32-accurate (the reference's fp32), torch.bfloat16 = bf16 operands with fp32
+        # accumulation (BASELINE config 4, accuracy bar 2e-2).  Parameters stay fp32.
+        self.proj_dtype = None
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -68,7 +72,8 @@ class GATConv(nn.Module):
         self._check_graph(graph)
         return Fn.GATLayerFunction.apply(feat, self.fc.weight, self.res_fc.weight, self.attn_l,
                                          self.attn_r, self.bias, graph, self._num_heads,
-                                         self._out_feats, self.negative_slope, mode)
+                                         self._out_feats, self.negative_slope, mode,
+                                         "bf16" if self.proj_dtype == torch.bfloat16 else None)
 
     def forward(self, graph, feat):
         rst = self.fused(graph, feat, Fn.MODE_FLATTEN).view(-1, self._num_heads, self._out_feats)
@@ -206,7 +211,7 @@ class GNNModule(nn.Module):
     """
 
     def __init__(self, in_feats=64, hidden_feats=None, dropout=0.2, num_step_set2set=6,
-                 num_layer_set2set=3):
+                 num_layer_set2set=3, proj_dtype=None):
         super().__init__()
         if hidden_feats is None:
             raise TypeError("GNNModule needs hidden_feats (the reference indexes hidden_feats[-1])")
@@ -217,6 +222,15 @@ class GNNModule(nn.Module):
         self.norm = GraphNorm(hidden_feats[-1] * 2)
         self.fc = nn.Sequential(nn.Linear(hidden_feats[-1] * 2, hidden_feats[-1]), nn.ReLU(),
                                 nn.Dropout(p=dropout))
+        self.set_projection_dtype(proj_dtype)
+
+    def set_projection_dtype(self, dtype):
+        """GAT projection GEMM precision: None (fp32-accurate, default) or torch.bfloat16
+        (bf16 operands on MFMA, fp32 accumulate — BASELINE config 4)."""
+        if dtype not in (None, torch.float32, torch.bfloat16):
+            raise ValueError("proj_dtype must be None, torch.float32 or torch.bfloat16")
+        for layer in self.conv.gnn_layers:
+            layer.gat_conv.proj_dtype = None if dtype == torch.float32 else dtype
 
     def forward(self, graphs, atom_feats):
         node_x = self.conv(graphs, atom_feats)
