@@ -247,7 +247,14 @@ class Set2SetFunction(torch.autograd.Function):
         dev = X.device
         st = _stream(dev)
         f32 = dict(dtype=torch.float32, device=dev)
-        g_qstars = torch.empty((T, B, 2 * D), **f32)
+        # Recurrent data gradients as ONE GEMM per cell against [W_ih | W_hh] (4D x (kin+D)):
+        # the outputs [dL/dx_l(t) | dL/dh_l(t-1)] land side by side — for layer 0 in the rows of
+        # g_qs3[t-1] = [dL/dq*_{t-1} (2D) | dL/dh_0(t-1) (D)], for layers l > 0 in gxh[l] =
+        # [dL/dh_{l-1}(t) | dL/dh_l(t-1)].  N = kin + D fills whole 256-column GEMM tiles
+        # (768 / 1152) where two products of N = 384 would each waste a quarter of theirs.
+        Wcat = [torch.cat([w[0], w[1]], dim=1).contiguous() for w in W]
+        g_qs3 = torch.empty((T, B, 3 * D), **f32)
+        g_qstars = g_qs3[:, :, :2 * D]
         g_qstars[T - 1].copy_(g_out)
         alphas = torch.empty((T, N), **f32)
         g_es = torch.empty((T, N), **f32)
@@ -258,31 +265,32 @@ class Set2SetFunction(torch.autograd.Function):
         # all T*B rows after the recurrence (K = 393k instead of 6 launches of 65k)
         g_gates_all = torch.empty((Lr, T, B, 4 * D), **f32)
         g_h = torch.empty((B, D), **f32)
-        g_hrec = [torch.zeros((B, D), **f32) for _ in range(Lr)]  # dL/dh_l(t-1) from step t
+        gxh = [None] + [torch.empty((B, 2 * D), **f32) for _ in range(1, Lr)]
         g_c = [torch.zeros((B, D), **f32) for _ in range(Lr)]
         g_c_new = torch.empty((B, D), **f32)
-        g_below = torch.empty((B, D), **f32)  # dL/dh_{l-1}(t) from layer l's input
         for t in range(T - 1, -1, -1):
             # readout segment backward: dL/dq_t = g_qstar_t[:, :D] + segment term -> g_h
             call("mvml_set2set_seg_bwd", B, D, ptr(g.node_offsets), ptr(X), ptr(qstars[t]), 2 * D,
-                 ptr(lse[t]), ptr(g_qstars[t]), 2 * D, ptr(g_h), D, ptr(alphas[t]), ptr(g_es[t]), st)
+                 ptr(lse[t]), ptr(g_qs3[t]), 3 * D, ptr(g_h), D, ptr(alphas[t]), ptr(g_es[t]), st)
             for l in range(Lr - 1, -1, -1):
-                w_ih, w_hh, b_ih, b_hh = W[l]
                 kin = 2 * D if l == 0 else D
-                gh = g_h if l == Lr - 1 else g_below
-                if t < T - 1:
-                    gh.add_(g_hrec[l])  # dL/dh_l(t) through the recurrence at step t+1
+                if l == Lr - 1:
+                    gh, ldgh = g_h, D
+                else:
+                    gh, ldgh = gxh[l + 1][:, :D], 2 * D  # dL/dh_l(t) from layer l+1's input
+                if t < T - 1:  # dL/dh_l(t) through the recurrence at step t+1
+                    gh.add_(g_qs3[t][:, 2 * D:] if l == 0 else gxh[l][:, D:])
                 c_prev = cs[t - 1, l] if t > 0 else None
                 g_gates = g_gates_all[l, t]
-                call("mvml_lstm_cell_bwd", B, D, ptr(acts[t, l]), ptr(cs[t, l]), ptr(c_prev), ptr(gh), D,
+                call("mvml_lstm_cell_bwd", B, D, ptr(acts[t, l]), ptr(cs[t, l]), ptr(c_prev), ptr(gh), ldgh,
                      ptr(g_c[l]) if t < T - 1 else None, ptr(g_gates), ptr(g_c_new), st)
                 g_c[l], g_c_new = g_c_new, g_c[l]
-                if t > 0:
-                    gemm(g_gates, w_hh, B, D, 4 * D, 0, 1, 4 * D, D, g_hrec[l], D)
-                if l > 0:
-                    gemm(g_gates, w_ih, B, D, 4 * D, 0, 1, 4 * D, D, g_below, D)
-                elif t > 0:  # layer-0 input at step t is q*_{t-1}
-                    gemm(g_gates, w_ih, B, 2 * D, 4 * D, 0, 1, 4 * D, 2 * D, g_qstars[t - 1], 2 * D)
+                # N = kin + D with the recurrent part (t > 0), kin alone at t = 0; layer 0 at
+                # t = 0 has neither (its input q*_{-1} = 0 is a constant)
+                ncols = kin + D if t > 0 else (kin if l > 0 else 0)
+                if ncols:
+                    out, ldo = (g_qs3[t - 1], 3 * D) if l == 0 else (gxh[l], 2 * D)
+                    gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo)
         # weight / bias gradients, one product per parameter over all steps:
         #   dW_ih[l] = sum_t g_gates[l,t]^T x_l(t),  dW_hh[l] = sum_{t>=1} g_gates[l,t]^T h_l(t-1)
         # (layer 0's input x_0(t) = q*_{t-1} is zero at t = 0; h_l(-1) = 0)
@@ -300,7 +308,7 @@ class Set2SetFunction(torch.autograd.Function):
             colsum(G, T * B, 4 * D, 4 * D, gb[l])
         gX = torch.empty((N, D), **f32)
         call("mvml_set2set_gx", N, D, T, ptr(g.node_graph), ptr(qstars), 2 * D, B * 2 * D,
-             ptr(g_qstars), 2 * D, B * 2 * D, ptr(alphas), ptr(g_es), ptr(gX), st)
+             ptr(g_qs3), 3 * D, B * 3 * D, ptr(alphas), ptr(g_es), ptr(gX), st)
         grads = []
         for l in range(Lr):
             grads += [gW_ih[l], gW_hh[l], gb[l], gb[l].clone()]
