@@ -1031,7 +1031,13 @@ GemmPlan plan_gemm(int prec, int64_t M, int64_t N, int64_t K) {
   if (prec == kPrecX3) {
     const int64_t tw = ceil_div(M, XBM) * ceil_div(N, XBN);
     const int Sw = choose_splits_t(tw, K, 256);
-    if (force == 256 || (force != 128 && tw * Sw >= 192)) return {true, Sw};
+    // skinny outputs (N = 76 / 384 columns of weight gradients): the 256x256 tile computes
+    // mostly padding; prefer 128x128 when it wastes clearly less (measured: L1 dW N=76 7.3 ->
+    // 4.8 ms, LSTM dW N=384 2.52 -> 2.46 ms, tools/gemm_bench.py)
+    const double u256 = (double)M * N / ((double)tw * XBM * XBN);
+    const double u128 = (double)M * N / ((double)ceil_div(M, BM) * ceil_div(N, BN) * BM * BN);
+    const bool skinny = u128 > 1.3 * u256;
+    if (force == 256 || (force != 128 && !skinny && tw * Sw >= 192)) return {true, Sw};
   }
   return {false, choose_splits_t(ceil_div(M, BM) * ceil_div(N, BN), K, 512)};
 }

@@ -20,6 +20,10 @@ SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor
     ("LSTM dW batched l0", 1536, 768, 5 * B, 1, 1),
     ("LSTM dW batched hh", 1536, 384, 5 * B, 1, 1),
     ("LSTM dW batched l1", 1536, 384, 6 * B, 1, 1),
+    ("L1 dW   gY^T*X N=76", 1552, 76, N_ATOMS, 1, 1),
+    ("L1 fwd  K=76", N_ATOMS, 1544, 76, 0, 0),
+    ("LSTM dxh l>0 merged", B, 768, 1536, 0, 1),
+    ("LSTM dxh l0 merged", B, 1152, 1536, 0, 1),
 ]
 
 
