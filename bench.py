@@ -55,6 +55,9 @@ def parse():
                     help="config 3 with its consumer: the MVP fusion head (SURVEY 8f-1) + BCE loss "
                          "on the GAT view's output (the SMILES / fingerprint views, out of scope, "
                          "are synthetic fixed embeddings)")
+    ap.add_argument("--workload", choices=["config3", "config5"], default="config3",
+                    help="config5 = BASELINE config 5 skewed-size stress (150-400 atoms + hubs of "
+                         "in-degree 32-128; --mols-per-gpu defaults to 8192 there)")
     ap.add_argument("--proj-bf16", action="store_true",
                     help="BASELINE config 4: the GAT projection GEMMs (fc / res_fc, forward and "
                          "backward) on bf16 operands with fp32 accumulation (mvml_gemm_bf16); "
@@ -159,7 +162,11 @@ def main():
     mvml_gat.lib()
 
     t_gen = time.perf_counter()
-    sb = synth.config3(args.mols_per_gpu, seed=1000 * args.seed + rank)
+    if args.workload == "config5":
+        n5 = args.mols_per_gpu if args.mols_per_gpu != 65536 else 8192
+        sb = synth.config5(n5, seed=1 + 1000 * args.seed + rank)
+    else:
+        sb = synth.config3(args.mols_per_gpu, seed=1000 * args.seed + rank)
     g = sb.to_graph(group_size=args.group_size).to(dev)
     feats = g.ndata["h"]
     N, E, B = g.num_nodes(), g.num_edges(), g.batch_size
@@ -258,7 +265,9 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16 projection, f32 elsewhere" if args.proj_bf16 else "f32",
             "data": "synthetic (seeded KEGG-like drug-like molecules, random-init weights)",
-            "config": {"workload": "BASELINE config 3: GNNModule (GAT [192,384] x4 heads, Set2Set 6x3, "
+            "config": {"workload": ("BASELINE config 5 (150-400-atom molecules with 1-4 hubs of in-degree "
+                                    "32-128): " if args.workload == "config5" else "BASELINE config 3: ") +
+                                   "GNNModule (GAT [192,384] x4 heads, Set2Set 6x3, "
                                    "GraphNorm, fc) fwd+bwd+Adam over KEGG-like molecules"
                                    + (" + MVP fusion head (12-head 3-token attention, Conv2d, MLP) "
                                       "+ BCEWithLogits" if args.with_fusion else

@@ -179,16 +179,42 @@ gat_softmax_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
     sc[t] = (eb + t < ee) ? leaky(elr[(int64_t)in_src[eb + t] * 2 * H + h] + er, slope) : -INFINITY;
     m = fmaxf(m, sc[t]);
   }
-  for (int e = eb + DC; e < ee; ++e) m = fmaxf(m, leaky(elr[(int64_t)in_src[e] * 2 * H + h] + er, slope));
+  // hubs (in-degree > DC): the tail in batches of 8 independent index + logit loads, so a
+  // hub costs deg / 8 memory round trips per pass instead of 2 deg (same summation order)
+  auto tail8 = [&](int e, float (&t8)[8]) {
+    int sv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sv[j] = (e + j < ee) ? in_src[e + j] : -1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      t8[j] = sv[j] >= 0 ? leaky(elr[(int64_t)sv[j] * 2 * H + h] + er, slope) : -INFINITY;
+  };
+  for (int e = eb + DC; e < ee; e += 8) {
+    float t8[8];
+    tail8(e, t8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, t8[j]);
+  }
 #pragma unroll
   for (int t = 0; t < DC; ++t)
     if (eb + t < ee) sum += expf(sc[t] - m);
-  for (int e = eb + DC; e < ee; ++e) sum += expf(leaky(elr[(int64_t)in_src[e] * 2 * H + h] + er, slope) - m);
+  for (int e = eb + DC; e < ee; e += 8) {
+    float t8[8];
+    tail8(e, t8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (e + j < ee) sum += expf(t8[j] - m);
+  }
 #pragma unroll
   for (int t = 0; t < DC; ++t)
     if (eb + t < ee) attn[(int64_t)(eb + t) * H + h] = expf(sc[t] - m) / sum;
-  for (int e = eb + DC; e < ee; ++e)
-    attn[(int64_t)e * H + h] = expf(leaky(elr[(int64_t)in_src[e] * 2 * H + h] + er, slope) - m) / sum;
+  for (int e = eb + DC; e < ee; e += 8) {
+    float t8[8];
+    tail8(e, t8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (e + j < ee) attn[(int64_t)(e + j) * H + h] = expf(t8[j] - m) / sum;
+  }
 }
 
 // Aggregation over NODE GROUPS.  A node group is a contiguous range of whole molecules of about
@@ -413,6 +439,7 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
   for (int w0 = a0; w0 < a1; w0 += kWin) {
     const int nr = min(kWin, a1 - w0);
     const int e0 = rowptr[w0];
+
     const float* __restrict__ attw = attn + (int64_t)e0 * H;
     const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)w0 * ocols, (uint32_t)(nr * ocols) * 4u);
     // this thread's destinations: in-CSR ranges and the cached source-row offsets
@@ -471,13 +498,25 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
           for (int i = 0; i < kEC; ++i)
             if (i < deg[p]) acc[p] = fma4(a[p][i], z[p][i], acc[p]);
       }
-      if (dmax > kEC) {  // hubs
+      if (dmax > kEC) {  // hubs: batches of 8 independent gathers (same summation order)
 #pragma unroll
         for (int p = 0; p < NP; ++p)
-          for (int i = kEC; i < deg[p]; ++i) {
-            const int e = eb[p] + i;
-            const uint32_t ob = (uint32_t)(in_src[e0 + e] - a0) * rowb + colb;
-            acc[p] = fma4(att(e, h), buf_ld4(rY, ob), acc[p]);
+          for (int i = kEC; i < deg[p]; i += 8) {
+            uint32_t ob[8];
+            float av[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const bool ok = i + j < deg[p];
+              const int e = eb[p] + (ok ? i + j : i);
+              ob[j] = ok ? (uint32_t)(in_src[e0 + e] - a0) * rowb + colb : kNone;
+              av[j] = ok ? att(e, h) : 0.f;
+            }
+            float4 zv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) zv[j] = buf_ld4(rY, ob[j]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (i + j < deg[p]) acc[p] = fma4(av[j], zv[j], acc[p]);
           }
       }
 #pragma unroll
@@ -857,6 +896,7 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
     const int u_l = (base + lane < deg) ? in_src[beg + base + lane] : 0;
 #pragma unroll
     for (int h = 0; h < H; ++h) ga_l[h] = 0.f;
+#pragma unroll 4
     for (int j = 0; j < cnt; ++j) {
       const float* zu = Y + (int64_t)rl(u_l, j) * ldy;
       float part[H];
@@ -973,6 +1013,7 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
     HeadReduce<H>::template all<false>(gp_l, lane);
 #pragma unroll
     for (int h = 0; h < H; ++h) gel[h] += gp_l[h];
+#pragma unroll 4
     for (int j = 0; j < cnt; ++j) {
       const int w = rl(w_l, j);
       float a[H];
