@@ -205,11 +205,13 @@ int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_
  * mvml_gemm_f32), then
  *   c = sigmoid(f)*c_prev + sigmoid(i)*tanh(g);  h = sigmoid(o)*tanh(c)
  * act_out[B,4D] saves the activated gates for the backward.  c_prev may be NULL (zeros).
- * h is written with leading dimension ldh (so the top layer can write straight into q*).
+ * h is written with leading dimension ldh, and again to h_out2 (ld ldh2) when h_out2 is not
+ * NULL: the cell's output is both its own recurrent input and the next layer's input, each
+ * stored inside a combined [x | h_prev] GEMM operand row.
  * ------------------------------------------------------------------------------------- */
 int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_ih,
                        const float* b_hh, const float* c_prev, float* c_out, float* h_out,
-                       int64_t ldh, float* act_out, void* stream);
+                       int64_t ldh, float* act_out, float* h_out2, int64_t ldh2, void* stream);
 /* g_h [B,D] (ld ldgh), g_c [B,D] (carry from t+1, may be NULL) -> g_gates [B,4D] (pre-act),
  * g_c_prev [B,D] (may be NULL). */
 int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const float* c, const float* c_prev,

@@ -21,7 +21,8 @@ __device__ __forceinline__ float dot4(float4 a, float4 b) {
 __global__ void lstm_cell_fwd_kernel(int64_t B, int D, const float* __restrict__ gp,
                                      const float* __restrict__ b_ih, const float* __restrict__ b_hh,
                                      const float* __restrict__ c_prev, float* __restrict__ c_out,
-                                     float* __restrict__ h_out, int64_t ldh, float* __restrict__ act) {
+                                     float* __restrict__ h_out, int64_t ldh, float* __restrict__ act,
+                                     float* __restrict__ h_out2, int64_t ldh2) {
   const int64_t total = B * D;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -36,7 +37,9 @@ __global__ void lstm_cell_fwd_kernel(int64_t B, int D, const float* __restrict__
     const float cp = c_prev ? c_prev[e] : 0.f;
     const float c = f * cp + i * gt;
     c_out[e] = c;
-    h_out[b * ldh + d] = o * tanhf(c);
+    const float h = o * tanhf(c);
+    h_out[b * ldh + d] = h;
+    if (h_out2) h_out2[b * ldh2 + d] = h;
     float* a = act + b * 4 * D;
     a[d] = i;
     a[D + d] = f;
@@ -243,13 +246,14 @@ using namespace mvml;
 
 extern "C" int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_ih,
                                   const float* b_hh, const float* c_prev, float* c_out,
-                                  float* h_out, int64_t ldh, float* act_out, void* stream) {
+                                  float* h_out, int64_t ldh, float* act_out, float* h_out2,
+                                  int64_t ldh2, void* stream) {
   clear_error();
-  MVML_REQUIRE(B >= 0 && D > 0 && ldh >= D, "lstm_cell_fwd: bad shape");
+  MVML_REQUIRE(B >= 0 && D > 0 && ldh >= D && (!h_out2 || ldh2 >= D), "lstm_cell_fwd: bad shape");
   if (B == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
   lstm_cell_fwd_kernel<<<grid_for(B * D), 256, 0, st>>>(B, D, gates_pre, b_ih, b_hh, c_prev, c_out,
-                                                        h_out, ldh, act_out);
+                                                        h_out, ldh, act_out, h_out2, ldh2);
   return check_launch("lstm_cell_fwd_kernel");
 }
 

@@ -185,7 +185,7 @@ class GATLayerFunction(torch.autograd.Function):
 
 class Set2SetFunction(torch.autograd.Function):
     """dgl Set2Set.forward (model.py:92): n_iters x {n_layers LSTM cell steps, fused segment
-    softmax readout}.  LSTM gates: two MFMA GEMMs per cell + pointwise kernel."""
+    softmax readout}.  LSTM gates: one MFMA GEMM per cell over [x | h_prev] + pointwise kernel."""
 
     @staticmethod
     def forward(ctx, X, g, n_iters, n_layers, *lstm_params):
@@ -198,50 +198,48 @@ class Set2SetFunction(torch.autograd.Function):
         T, Lr = n_iters, n_layers
         W = [tuple(_c(p) for p in lstm_params[4 * l:4 * l + 4]) for l in range(Lr)]  # w_ih, w_hh, b_ih, b_hh
         f32 = dict(dtype=torch.float32, device=dev)
-        qstars = torch.empty((T, B, 2 * D), **f32)
+        # Combined GEMM operands: XH[l][t] = [x_l(t) | h_l(t-1)] (kin_l + D columns) so each
+        # cell's gates are ONE GEMM against [W_ih | W_hh]; layer 0's x is q*_{t-1}, so
+        # XH[0][t+1][:, :2D] IS q*_t (the readout writes r_t there).  Each cell writes its h
+        # twice: its own recurrence slot XH[l][t+1][:, kin:] and its consumer's input slot
+        # (XH[l+1][t][:, :D], or q_t = XH[0][t+1][:, :D] for the top layer).
+        kin = [2 * D] + [D] * (Lr - 1)
+        XH = [torch.empty((T + 1, B, kin[l] + D), **f32) for l in range(Lr)]
+        XH[0][0].zero_()
+        for l in range(1, Lr):
+            XH[l][0, :, D:].zero_()
+        Wcat = [torch.cat([w[0], w[1]], dim=1).contiguous() for w in W]
         acts = torch.empty((T, Lr, B, 4 * D), **f32)
         cs = torch.empty((T, Lr, B, D), **f32)
-        hs = torch.empty((max(Lr - 1, 1), T, B, D), **f32)  # non-top layer outputs, [layer][t]
         lse = torch.empty((T, B), **f32)
         gates = torch.empty((B, 4 * D), **f32)
         for t in range(T):
             for l in range(Lr):
                 w_ih, w_hh, b_ih, b_hh = W[l]
-                kin = 2 * D if l == 0 else D
-                if l == 0:
-                    x, ldx, x_zero = (qstars[t - 1] if t > 0 else None), 2 * D, t == 0
+                K = kin[l] + D if t > 0 else kin[l]  # h_l(-1) = 0: the recurrent half is skipped
+                if t == 0 and l == 0:
+                    gates.zero_()  # q*_{-1} = 0 and h_0(-1) = 0
                 else:
-                    x, ldx, x_zero = hs[l - 1, t], D, False
-                if t > 0:
-                    hp, ldhp = (qstars[t - 1] if l == Lr - 1 else hs[l, t - 1]), (2 * D if l == Lr - 1 else D)
-                else:
-                    hp = None
-                if x_zero:
-                    gates.zero_()
-                    beta = 1.0
-                else:
-                    gemm(x, w_ih, B, 4 * D, kin, 0, 0, ldx, kin, gates, 4 * D)
-                    beta = 1.0
-                if hp is not None:
-                    gemm(hp, w_hh, B, 4 * D, D, 0, 0, ldhp, D, gates, 4 * D, beta=beta)
-                if l == Lr - 1:
-                    h_out, ldh = qstars[t], 2 * D
-                else:
-                    h_out, ldh = hs[l, t], D
+                    gemm(XH[l][t], Wcat[l], B, 4 * D, K, 0, 0, kin[l] + D, kin[l] + D, gates, 4 * D)
+                own = XH[l][t + 1][:, kin[l]:]
+                nxt = XH[l + 1][t] if l < Lr - 1 else XH[0][t + 1]
                 c_prev = cs[t - 1, l] if t > 0 else None
                 call("mvml_lstm_cell_fwd", B, D, ptr(gates), ptr(b_ih), ptr(b_hh), ptr(c_prev),
-                     ptr(cs[t, l]), ptr(h_out), ldh, ptr(acts[t, l]), st)
-            call("mvml_set2set_seg_fwd", B, D, ptr(g.node_offsets), ptr(X), ptr(qstars[t]), 2 * D,
+                     ptr(cs[t, l]), ptr(own), kin[l] + D, ptr(acts[t, l]), ptr(nxt),
+                     kin[l + 1] + D if l < Lr - 1 else 3 * D, st)
+            call("mvml_set2set_seg_fwd", B, D, ptr(g.node_offsets), ptr(X), ptr(XH[0][t + 1]), 3 * D,
                  ptr(lse[t]), st)
-        ctx.save_for_backward(X, qstars, acts, cs, hs, lse, *[p for w in W for p in w])
+        ctx.save_for_backward(X, acts, cs, lse, *XH, *[p for w in W for p in w])
         ctx.g, ctx.T, ctx.Lr = g, T, Lr
-        return qstars[T - 1].clone()
+        return XH[0][T][:, :2 * D].clone()
 
     @staticmethod
     def backward(ctx, g_out):
-        X, qstars, acts, cs, hs, lse, *flat = ctx.saved_tensors
+        X, acts, cs, lse, *rest = ctx.saved_tensors
         g, T, Lr = ctx.g, ctx.T, ctx.Lr
+        XH, flat = rest[:Lr], rest[Lr:]
         W = [tuple(flat[4 * l:4 * l + 4]) for l in range(Lr)]
+        qs = XH[0][1:]  # q*_t = XH[0][t+1][:, :2D], row stride 3D
         N, D = X.shape
         B = g.batch_size
         dev = X.device
@@ -270,7 +268,7 @@ class Set2SetFunction(torch.autograd.Function):
         g_c_new = torch.empty((B, D), **f32)
         for t in range(T - 1, -1, -1):
             # readout segment backward: dL/dq_t = g_qstar_t[:, :D] + segment term -> g_h
-            call("mvml_set2set_seg_bwd", B, D, ptr(g.node_offsets), ptr(X), ptr(qstars[t]), 2 * D,
+            call("mvml_set2set_seg_bwd", B, D, ptr(g.node_offsets), ptr(X), ptr(qs[t]), 3 * D,
                  ptr(lse[t]), ptr(g_qs3[t]), 3 * D, ptr(g_h), D, ptr(alphas[t]), ptr(g_es[t]), st)
             for l in range(Lr - 1, -1, -1):
                 kin = 2 * D if l == 0 else D
@@ -297,17 +295,19 @@ class Set2SetFunction(torch.autograd.Function):
         for l in range(Lr):
             G = g_gates_all[l]
             kin = 2 * D if l == 0 else D
+            ldx = kin + D
+            # dW_ih[l] = sum_t g_gates[l,t]^T x_l(t): x_l(t) = XH[l][t][:, :kin] (zero at l = 0,
+            # t = 0); dW_hh[l] = sum_{t>=1} g_gates[l,t]^T h_l(t-1), h_l(t-1) = XH[l][t][:, kin:]
             if l == 0:
                 if T > 1:
-                    gemm(G[1:], qstars[:T - 1], 4 * D, kin, (T - 1) * B, 1, 1, 4 * D, 2 * D, gW_ih[0], kin)
+                    gemm(G[1:], XH[0][1:T], 4 * D, kin, (T - 1) * B, 1, 1, 4 * D, ldx, gW_ih[0], kin)
             else:
-                gemm(G, hs[l - 1], 4 * D, kin, T * B, 1, 1, 4 * D, D, gW_ih[l], kin)
+                gemm(G, XH[l][0:T], 4 * D, kin, T * B, 1, 1, 4 * D, ldx, gW_ih[l], kin)
             if T > 1:
-                hp, ldhp = (qstars[:T - 1], 2 * D) if l == Lr - 1 else (hs[l, :T - 1], D)
-                gemm(G[1:], hp, 4 * D, D, (T - 1) * B, 1, 1, 4 * D, ldhp, gW_hh[l], D)
+                gemm(G[1:], XH[l][1:T, :, kin:], 4 * D, D, (T - 1) * B, 1, 1, 4 * D, ldx, gW_hh[l], D)
             colsum(G, T * B, 4 * D, 4 * D, gb[l])
         gX = torch.empty((N, D), **f32)
-        call("mvml_set2set_gx", N, D, T, ptr(g.node_graph), ptr(qstars), 2 * D, B * 2 * D,
+        call("mvml_set2set_gx", N, D, T, ptr(g.node_graph), ptr(qs), 3 * D, B * 3 * D,
              ptr(g_qs3), 3 * D, B * 3 * D, ptr(alphas), ptr(g_es), ptr(gX), st)
         grads = []
         for l in range(Lr):
