@@ -292,19 +292,19 @@ class Set2SetFunction(torch.autograd.Function):
         # weight / bias gradients, one product per parameter over all steps:
         #   dW_ih[l] = sum_t g_gates[l,t]^T x_l(t),  dW_hh[l] = sum_{t>=1} g_gates[l,t]^T h_l(t-1)
         # (layer 0's input x_0(t) = q*_{t-1} is zero at t = 0; h_l(-1) = 0)
+        # [dW_ih | dW_hh][l] = sum_t g_gates[l,t]^T XH[l][t] as ONE GEMM with N = kin + D: the
+        # recurrent half of XH[l][0] is zero (h_l(-1) = 0) and for layer 0 the whole t = 0 block
+        # is (q*_{-1} = 0), so it is skipped there.
         for l in range(Lr):
             G = g_gates_all[l]
             kin = 2 * D if l == 0 else D
             ldx = kin + D
-            # dW_ih[l] = sum_t g_gates[l,t]^T x_l(t): x_l(t) = XH[l][t][:, :kin] (zero at l = 0,
-            # t = 0); dW_hh[l] = sum_{t>=1} g_gates[l,t]^T h_l(t-1), h_l(t-1) = XH[l][t][:, kin:]
-            if l == 0:
-                if T > 1:
-                    gemm(G[1:], XH[0][1:T], 4 * D, kin, (T - 1) * B, 1, 1, 4 * D, ldx, gW_ih[0], kin)
-            else:
-                gemm(G, XH[l][0:T], 4 * D, kin, T * B, 1, 1, 4 * D, ldx, gW_ih[l], kin)
-            if T > 1:
-                gemm(G[1:], XH[l][1:T, :, kin:], 4 * D, D, (T - 1) * B, 1, 1, 4 * D, ldx, gW_hh[l], D)
+            t0 = 1 if l == 0 else 0
+            if T > t0:
+                gWcat = torch.empty((4 * D, ldx), **f32)
+                gemm(G[t0:], XH[l][t0:T], 4 * D, ldx, (T - t0) * B, 1, 1, 4 * D, ldx, gWcat, ldx)
+                gW_ih[l].copy_(gWcat[:, :kin])
+                gW_hh[l].copy_(gWcat[:, kin:])
             colsum(G, T * B, 4 * D, 4 * D, gb[l])
         gX = torch.empty((N, D), **f32)
         call("mvml_set2set_gx", N, D, T, ptr(g.node_graph), ptr(qs), 3 * D, B * 3 * D,
