@@ -243,6 +243,8 @@ constexpr int kECap = kPlanEdgeCap;   // LDS kernel: in-edges per group (attenti
 constexpr int kWin = 64;              // gather kernel: destination atoms per pass set
 constexpr int kEC = kPlanDegCap;      // in-edges per destination with cached offsets
 constexpr int kAggThreads = 512;
+constexpr int kHubDeg = 16;           // gather kernel: in-degree above which the hub pass runs
+constexpr int kHubCols = 1024;        // gather kernel: float4 columns of the hub pass (H*F <= 4096)
 
 #ifndef MVML_LDS_WAVES
 #define MVML_LDS_WAVES 4
@@ -435,6 +437,11 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
   const uint32_t rowb = (uint32_t)ldy * 4u;
   const __amdgpu_buffer_rsrc_t rY = make_rsrc(Yg, (uint32_t)(a1 - a0) * rowb);
   constexpr uint32_t kNone = 0xFFFFFFF0u;  // out of range: the load returns 0, moves no data
+  // Hub destinations (in-degree > kHubDeg) leave the chunk sweep: after it, the whole block
+  // aggregates one hub at a time over ALL its columns at once, so a hub costs deg / 8 memory
+  // round trips instead of (column chunks) x deg / 8 on 16 lanes.  Same summation order.
+  __shared__ float4 s_hub[kHubCols];
+  const bool hubpass = HF / 4 <= kHubCols;
 
   for (int w0 = a0; w0 < a1; w0 += kWin) {
     const int nr = min(kWin, a1 - w0);
@@ -444,6 +451,7 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
     const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)w0 * ocols, (uint32_t)(nr * ocols) * 4u);
     // this thread's destinations: in-CSR ranges and the cached source-row offsets
     int eb[NP], deg[NP];
+    bool hub[NP];
     uint32_t so[NP][kEC];
     int dmax = 0;
 #pragma unroll
@@ -455,6 +463,8 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
         eb[p] = rowptr[w0 + d] - e0;
         deg[p] = rowptr[w0 + d + 1] - e0 - eb[p];
       }
+      hub[p] = hubpass && deg[p] > kHubDeg;
+      if (hub[p]) deg[p] = 0;  // aggregated by the hub pass below
 #pragma unroll
       for (int i = 0; i < kEC; ++i)
         so[p][i] = (i < deg[p]) ? (uint32_t)(in_src[e0 + eb[p] + i] - a0) * rowb : kNone;
@@ -522,7 +532,7 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         const int d = ds + DPP * p;
-        if (d < nr) {
+        if (d < nr && !hub[p]) {
           if (MODE == 1) {
             const float4 t = add4(acc[p], ld4(bias + col));
             tot[p] = (h == 0) ? t : add4(tot[p], t);
@@ -538,6 +548,55 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
             buf_st4(rO, 4u * (uint32_t)(d * HF + col), o);
           }
         }
+      }
+    }
+    if (!hubpass) continue;
+    for (int d = 0; d < nr; ++d) {  // block-uniform walk over the window's hubs
+      const int hb = rowptr[w0 + d] - e0, hdeg = rowptr[w0 + d + 1] - e0 - hb;
+      if (hdeg <= kHubDeg) continue;
+      const uint32_t vb = (uint32_t)(w0 + d - a0) * rowb;
+      for (int c4 = tid; c4 < HF / 4; c4 += kAggThreads) {
+        const int col = 4 * c4, h = col / F;
+        const uint32_t colb = 4u * (uint32_t)col;
+        float4 acc = f4(0.f);
+        for (int i = 0; i < hdeg; i += 8) {
+          uint32_t ob[8];
+          float av[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const bool ok = i + j < hdeg;
+            const int e = hb + (ok ? i + j : i);
+            ob[j] = ok ? (uint32_t)(in_src[e0 + e] - a0) * rowb + colb : kNone;
+            av[j] = ok ? attw[e * H + h] : 0.f;
+          }
+          float4 zv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) zv[j] = buf_ld4(rY, ob[j]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (i + j < hdeg) acc = fma4(av[j], zv[j], acc);
+        }
+        if (MODE == 1) {
+          s_hub[c4] = add4(acc, ld4(bias + col));
+        } else {
+          const float4 res = buf_ld4(rY, vb + 4u * (uint32_t)(HF + col));
+          float4 o = add4(add4(acc, res), ld4(bias + col));
+          if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
+          buf_st4(rO, 4u * (uint32_t)(d * HF + col), o);
+        }
+      }
+      if (MODE == 1) {  // head mean, heads summed in order as in the chunk sweep
+        __syncthreads();
+        for (int f4 = tid; f4 < F / 4; f4 += kAggThreads) {
+          float4 tot = s_hub[f4];
+          for (int hh = 1; hh < H; ++hh) tot = add4(tot, s_hub[hh * (F / 4) + f4]);
+          const float4 rmv = buf_ld4(rY, vb + 4u * (uint32_t)(HF + 4 * f4));
+          const float invh = (float)H;
+          buf_st4(rO, 4u * (uint32_t)(d * F + 4 * f4),
+                  make_float4(tot.x / invh + rmv.x, tot.y / invh + rmv.y, tot.z / invh + rmv.z,
+                              tot.w / invh + rmv.w));
+        }
+        __syncthreads();
       }
     }
   }
