@@ -173,3 +173,28 @@ class MVFusion(nn.Module):
         out = LinearReLUFunction.apply(out, self.mlp[0].weight, self.mlp[0].bias)
         out = self.mlp[2](out)
         return LinearFunction.apply(out, self.mlp[3].weight, self.mlp[3].bias)
+
+
+class FPNModule(nn.Module):
+    """The fingerprint view's MLP, model.py:138-155, on the HIP GEMMs:
+    fc1 (2513 -> fp_2_dim) -> Dropout -> ReLU -> fc2 (-> out_feats), parameter names as in the
+    reference.  fc1 + ReLU run as one GEMM with a bias+ReLU epilogue and the Dropout follows:
+    ReLU(mask * z / (1-p)) == mask * ReLU(z) / (1-p) exactly, and the mask is drawn for the same
+    shape, so this equals the reference order.  The 2513-bit fingerprints themselves (MACCS,
+    ErG, PubChem, Morgan; dataset.py:37-45) need RDKit and are out of scope."""
+
+    def __init__(self, fp_2_dim, out_feats, dropout=0.2):
+        super().__init__()
+        self.fp_2_dim = fp_2_dim
+        self.dropout_fpn = dropout
+        self.out_feats = out_feats
+        self.fp_dim = 2513
+        self.fc1 = nn.Linear(self.fp_dim, self.fp_2_dim)
+        self.act_func = nn.ReLU()
+        self.fc2 = nn.Linear(self.fp_2_dim, self.out_feats)
+        self.dropout = nn.Dropout(p=self.dropout_fpn)
+
+    def forward(self, fp):
+        h = LinearReLUFunction.apply(fp, self.fc1.weight, self.fc1.bias)
+        h = self.dropout(h)
+        return LinearFunction.apply(h, self.fc2.weight, self.fc2.bias)

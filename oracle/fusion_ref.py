@@ -55,3 +55,17 @@ class MVFusionRef(nn.Module):
 def bce_logits_ref(logits, labels):
     """main.py:91: torch.nn.BCEWithLogitsLoss() (mean reduction)."""
     return nn.functional.binary_cross_entropy_with_logits(logits, labels)
+
+
+class FPNModuleRef(nn.Module):
+    """model.py:138-155 restated (reference order: fc1 -> Dropout -> ReLU -> fc2)."""
+
+    def __init__(self, fp_2_dim=128, out_feats=384, dropout=0.2):
+        super().__init__()
+        self.fc1 = nn.Linear(2513, fp_2_dim)
+        self.act_func = nn.ReLU()
+        self.fc2 = nn.Linear(fp_2_dim, out_feats)
+        self.dropout = nn.Dropout(p=dropout)
+
+    def forward(self, fp):
+        return self.fc2(self.act_func(self.dropout(self.fc1(fp))))

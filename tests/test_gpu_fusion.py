@@ -112,3 +112,29 @@ def test_fusion_deterministic_bitwise():
                     [p.grad.clone() for n, p in mod.named_parameters() if p.grad is not None])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [1, 64, 300])
+def test_fpn_module_parity(B):
+    """Fingerprint-view MLP (model.py:138-155): 2513 fingerprint bits -> 128 -> 384, eval mode,
+    forward and gradients against the float64 restatement."""
+    from mvml_gat import FPNModule
+    from oracle.fusion_ref import FPNModuleRef
+    torch.manual_seed(B)
+    ref = FPNModuleRef(128, 384, 0.5).double().eval()
+    mod = FPNModule(128, 384, 0.5).to(DEV).eval()
+    mod.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    g = torch.Generator().manual_seed(B + 1)
+    fp = (torch.rand(B, 2513, generator=g) > 0.7).double()
+    fp[:, 167:608] = torch.rand(B, 441, generator=g, dtype=torch.float64) * 3  # ErG block: real-valued
+    xr = fp.clone().requires_grad_(True)
+    xd = fp.float().to(DEV).requires_grad_(True)
+    zr, zd = ref(xr), mod(xd)
+    assert rel_err(zd, zr) < TOL
+    up = torch.randn(zr.shape, generator=g, dtype=torch.float64)
+    (zr * up).sum().backward()
+    (zd * up.float().to(DEV)).sum().backward()
+    assert rel_err(xd.grad, xr.grad) < TOL
+    pr = dict(ref.named_parameters())
+    for name, p in mod.named_parameters():
+        assert rel_err(p.grad, pr[name].grad) < TOL, name
