@@ -290,6 +290,28 @@ int mvml_conv3_bwd(int64_t B, int C, int O, int W, const float* in, const float*
 int mvml_bce_logits(int64_t n, const float* z, const float* y, float* loss_terms, float* g_z,
                     void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * SMILES BiLSTM view (RNNModule, model.py:98-135; nn.Embedding + nn.LSTM(bidirectional,
+ * batch_first) over pack_padded_sequence(enforce_sorted=False) + the last-step selection of
+ * model.py:131-133).  Packed layout: rows t*B + i, batch sorted by descending length
+ * (perm[i] = original index of sorted row i, pos = perm^-1), tokens int32 [B, ldtok] in the
+ * original order, lens int32 [B] >= 1.  The recurrence is mvml_gemm_* + mvml_lstm_cell_*.
+ *   gather_rows: out[t*B+i, :] = t < lens[perm[i]] ? table[tokens[perm[i], t], :] : 0
+ *                (layer 0's x W_ih^T as rows of the [vocab, 4H] table E W_ih^T; cols % 4 == 0)
+ *   token_grad:  out[v, :] = sum of g[t*B+i, :] over live positions holding token v
+ *                (fixed order, deterministic; replaces Embedding / W_ih_l0 backward)
+ *   select_last: dir 0: fea[b] = [out[(lens[b]-1)*B + pos[b], 0:H] | out[pos[b], H:2H]];
+ *                dir 1: the transpose, fea -> out rows (out must be zeroed by the caller).
+ * ------------------------------------------------------------------------------------- */
+int mvml_bilstm_gather_rows(int64_t T, int64_t B, int64_t cols, const float* table,
+                            const int32_t* tokens, int64_t ldtok, const int32_t* lens,
+                            const int32_t* perm, float* out, void* stream);
+int mvml_bilstm_token_grad(int64_t T, int64_t B, int64_t cols, const float* g,
+                           const int32_t* tokens, int64_t ldtok, const int32_t* lens,
+                           const int32_t* perm, int vocab, float* out, void* stream);
+int mvml_bilstm_select_last(int64_t B, int64_t H, const int32_t* lens, const int32_t* pos,
+                            float* out, float* fea, int dir, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

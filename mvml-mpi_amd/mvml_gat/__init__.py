@@ -13,8 +13,9 @@ tensors are not on the GPU.
 from ._lib import MvmlError, lib
 from .batching import BatchedMolGraph, MolGraph, batch, bigraph_from_bonds, from_arrays, graph
 from .fusion import FPNModule, MVFusion, bce_with_logits
+from .smiles import RNNModule, collate_smiles, tokens_struct
 from .nn import GAT, GATConv, GATLayer, GNNModule, GraphNorm, Set2Set
 
-__all__ = ["GNNModule", "MVFusion", "FPNModule", "bce_with_logits", "GAT", "GATLayer", "GATConv", "Set2Set", "GraphNorm", "BatchedMolGraph",
+__all__ = ["GNNModule", "MVFusion", "FPNModule", "RNNModule", "tokens_struct", "collate_smiles", "bce_with_logits", "GAT", "GATLayer", "GATConv", "Set2Set", "GraphNorm", "BatchedMolGraph",
            "MolGraph", "batch", "graph", "bigraph_from_bonds", "from_arrays", "lib", "MvmlError"]
 __version__ = "0.1.0"

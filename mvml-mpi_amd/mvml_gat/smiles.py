@@ -1,0 +1,277 @@
+"""SMILES BiLSTM view of MVP (RNNModule, /root/reference/model.py:98-135) on
+the HIP path, plus the reference's SMILES vocabulary (tokens_struct, utils.py:55-88).
+
+    RNNModule(vocab, embed_dim=128, blstm_dim=384, num_layers=2, out_dim=384, dropout)(batch)
+
+``batch`` is the reference's ``{"smiles": padded tokens [B, T], "seq_len": [len_b]}`` dict
+(dataset.py:56-59).  Parameter names / shapes equal the reference's (``embeddings.weight``,
+``rnn.weight_ih_l{k}[_reverse]``, ``rnn.weight_hh_…``, ``rnn.bias_{ih,hh}_…``, ``norm_layer.*``,
+``fc.0.*``), so a reference state_dict loads unchanged.
+
+Design (not a cuDNN/MIOpen RNN call): the packed sequence of pack_padded_sequence
+(enforce_sorted=False) is kept as a time-major [T, B, 2H] buffer with the batch sorted by
+descending length, so the sequences alive at step t are a row prefix.  Per layer and direction
+one MFMA GEMM projects every position's input at once (layer 0: a [vocab, 4H] table lookup,
+mvml_bilstm_gather_rows), then each time step is one GEMM h_prev W_hh^T (beta = 1 onto the
+projection, M = the live prefix) + the LSTM cell kernel, which writes h straight into its half of
+the bidirectional output row.  Backward mirrors it (mvml_lstm_cell_bwd, recurrent GEMM, weight
+gradients as single GEMMs over all positions, deterministic per-token reduction for the
+embedding / W_ih_l0).  Padded positions stay zero, as pad_packed_sequence's output is.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ._lib import call, ptr
+from .functional import LinearReLUFunction, _c, _check_cuda_f32, _stream, colsum, gemm
+
+
+class tokens_struct:
+    """The reference's SMILES character vocabulary (utils.py:55-88): 39 tokens, pad ' ' = 0,
+    '<unk>' = 1 for characters outside the list."""
+
+    def __init__(self):
+        self.tokens = [' ', '<unk>', 'C', 'O', '(', ')', 'c', '=', '1', '2', 'N', '3', 'n', 'P',
+                       '4', '[', ']', 'S', 'H', '5', 'l', '-', '*', 'o', '+', '6', '#', 'M', 'F',
+                       'g', '7', 'B', 'r', 's', 'I', 'e', 'i', '8', 'Z']
+        self.tokens_length = len(self.tokens)
+        self.tokens_vocab = dict(zip(self.tokens, range(len(self.tokens))))
+        self.reversed_tokens_vocab = {v: k for k, v in self.tokens_vocab.items()}
+
+    @property
+    def unk(self):
+        return self.tokens_vocab['<unk>']
+
+    @property
+    def pad(self):
+        return self.tokens_vocab[' ']
+
+    def get_default_tokens(self):
+        return self.tokens
+
+    def get_tokens_length(self):
+        return self.tokens_length
+
+    def encode(self, char_list):
+        """Characters -> float32 indices, unknown -> unk (utils.py:80-88)."""
+        return np.array([self.tokens_vocab.get(ch, self.unk) for ch in char_list], dtype=np.float32)
+
+    def decode(self, matrix):
+        return "".join(self.reversed_tokens_vocab[int(i)] for i in matrix)
+
+
+def collate_smiles(smiles_list, vocab):
+    """dataset.py:47-59's SMILES half: per-character encode, pad_sequence(batch_first) with 0."""
+    enc = [vocab.encode(list(s)) for s in smiles_list]
+    seq_len = [e.size for e in enc]
+    T = max(seq_len) if enc else 0
+    out = np.zeros((len(enc), T), dtype=np.float32)
+    for i, e in enumerate(enc):
+        out[i, :e.size] = e
+    return {"smiles": torch.from_numpy(out), "seq_len": seq_len}
+
+
+class Packing:
+    """Host-side pack_padded_sequence(enforce_sorted=False) metadata (the reference computes it on
+    the CPU from the ``seq_len`` list as well): descending-length order, batch_sizes per step."""
+
+    def __init__(self, seq_lens, tokens, vocab_size):
+        lens = np.asarray(list(seq_lens), dtype=np.int64)
+        if lens.ndim != 1 or lens.size == 0:
+            raise ValueError("seq_len must be a non-empty list of lengths")
+        if tokens.dim() != 2 or tokens.shape[0] != lens.size:
+            raise ValueError(f"smiles must be [B, T] with B = len(seq_len), got {tuple(tokens.shape)}")
+        if lens.min() < 1 or lens.max() > tokens.shape[1]:
+            # pack_padded_sequence: "Length of all samples has to be greater than 0"
+            raise RuntimeError("Length of all samples has to be greater than 0 and at most T")
+        self.B = int(lens.size)
+        self.T = int(lens.max())
+        perm = np.argsort(-lens, kind="stable")
+        pos = np.empty_like(perm)
+        pos[perm] = np.arange(self.B)
+        self.batch_sizes = [int((lens > t).sum()) for t in range(self.T)]
+        dev = tokens.device
+        tok = tokens.to(torch.int64)
+        if int(tok.min()) < 0 or int(tok.max()) >= vocab_size:
+            raise IndexError("token index out of range of the embedding table")
+        self.tokens = tok.to(torch.int32).contiguous()
+        self.ldtok = int(tokens.shape[1])
+        self.lens = torch.from_numpy(lens.astype(np.int32)).to(dev)
+        self.perm = torch.from_numpy(perm.astype(np.int32)).to(dev)
+        self.pos = torch.from_numpy(pos.astype(np.int32)).to(dev)
+
+
+class BiLSTMLayerFunction(torch.autograd.Function):
+    """One bidirectional nn.LSTM layer over the packed batch.  ``x`` is the previous layer's
+    [T, B, 2H] output, or for layer 0 (``pk_tokens`` = True) the embedding table [V, E]."""
+
+    @staticmethod
+    def forward(ctx, x, pk, layer0, *w):
+        _check_cuda_f32(x, "x")
+        dev = x.device
+        st = _stream(dev)
+        T, B = pk.T, pk.B
+        H = w[1].shape[1]
+        G = 4 * H
+        x = _c(x)
+        In = x.shape[-1]
+        out = torch.zeros((T, B, 2 * H), dtype=torch.float32, device=dev)
+        saved = []
+        for d in range(2):
+            w_ih, w_hh, b_ih, b_hh = (_c(t) for t in w[4 * d:4 * d + 4])
+            gates = torch.empty((T, B, G), dtype=torch.float32, device=dev)
+            if layer0:
+                V = x.shape[0]
+                P = torch.empty((V, G), dtype=torch.float32, device=dev)
+                gemm(x, w_ih, V, G, In, 0, 0, In, In, P, G)
+                call("mvml_bilstm_gather_rows", T, B, G, ptr(P), ptr(pk.tokens), pk.ldtok,
+                     ptr(pk.lens), ptr(pk.perm), ptr(gates), st)
+            else:
+                gemm(x, w_ih, T * B, G, In, 0, 0, In, In, gates, G)
+            c = torch.zeros((T, B, H), dtype=torch.float32, device=dev)
+            act = torch.empty((T, B, G), dtype=torch.float32, device=dev)
+            order = range(T) if d == 0 else range(T - 1, -1, -1)
+            prev = None
+            for t in order:
+                bs = pk.batch_sizes[t]
+                c_prev = None
+                if prev is not None:
+                    gemm(out[prev, :, d * H:], w_hh, bs, G, H, 0, 0, 2 * H, H, gates[t], G, beta=1.0)
+                    c_prev = c[prev]
+                call("mvml_lstm_cell_fwd", bs, H, ptr(gates[t]), ptr(b_ih), ptr(b_hh), ptr(c_prev),
+                     ptr(c[t]), ptr(out[t, :, d * H:]), 2 * H, ptr(act[t]), None, 0, st)
+                prev = t
+            saved += [c, act]
+        ctx.pk, ctx.layer0, ctx.H = pk, layer0, H
+        ctx.save_for_backward(x, out, *saved, *w)
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        x, out, c0, a0, c1, a1, *w = ctx.saved_tensors
+        pk, layer0, H = ctx.pk, ctx.layer0, ctx.H
+        dev = x.device
+        st = _stream(dev)
+        T, B, G = pk.T, pk.B, 4 * H
+        In = x.shape[-1]
+        g = g_out.contiguous().clone()
+        cs, acts = (c0, c1), (a0, a1)
+        g_w = [None] * 8
+        g_x = torch.empty_like(x)
+        for d in range(2):
+            w_ih, w_hh = _c(w[4 * d]), _c(w[4 * d + 1])
+            c, act = cs[d], acts[d]
+            gg = torch.zeros((T, B, G), dtype=torch.float32, device=dev)
+            carry = [torch.zeros((B, H), dtype=torch.float32, device=dev) for _ in range(2)]
+            order = range(T - 1, -1, -1) if d == 0 else range(T)
+            nxt, k = None, 0
+            for t in order:
+                bs = pk.batch_sizes[t]
+                if nxt is not None:  # recurrent gradient from the step this one fed
+                    rows = min(bs, pk.batch_sizes[nxt])
+                    gemm(gg[nxt], w_hh, rows, H, G, 0, 1, G, H, g[t, :, d * H:], 2 * H, beta=1.0)
+                tp = t - 1 if d == 0 else t + 1
+                c_prev = c[tp] if 0 <= tp < T else None
+                g_c = carry[k % 2] if nxt is not None else None
+                call("mvml_lstm_cell_bwd", bs, H, ptr(act[t]), ptr(c[t]), ptr(c_prev),
+                     ptr(g[t, :, d * H:]), 2 * H, ptr(g_c), ptr(gg[t]), ptr(carry[(k + 1) % 2]), st)
+                nxt, k = t, k + 1
+            gb = torch.empty(G, dtype=torch.float32, device=dev)
+            colsum(gg, T * B, G, G, gb)
+            g_whh = torch.zeros((G, H), dtype=torch.float32, device=dev)
+            if T > 1:
+                A, Bm = (gg[1:], out[:-1, :, d * H:]) if d == 0 else (gg[:-1], out[1:, :, d * H:])
+                gemm(A, Bm, G, H, (T - 1) * B, 1, 1, G, 2 * H, g_whh, H)
+            g_wih = torch.empty((G, In), dtype=torch.float32, device=dev)
+            beta = 1.0 if d else 0.0
+            if layer0:
+                V = x.shape[0]
+                Gt = torch.empty((V, G), dtype=torch.float32, device=dev)
+                call("mvml_bilstm_token_grad", T, B, G, ptr(gg), ptr(pk.tokens), pk.ldtok,
+                     ptr(pk.lens), ptr(pk.perm), V, ptr(Gt), st)
+                gemm(Gt, x, G, In, V, 1, 1, G, In, g_wih, In)
+                gemm(Gt, w_ih, V, In, G, 0, 1, G, In, g_x, In, beta=beta)
+            else:
+                gemm(gg, x, G, In, T * B, 1, 1, G, In, g_wih, In)
+                gemm(gg, w_ih, T * B, In, G, 0, 1, G, In, g_x, In, beta=beta)
+            g_w[4 * d:4 * d + 4] = [g_wih, g_whh, gb, gb.clone()]
+        return (g_x, None, None, *g_w)
+
+
+class SelectLastFunction(torch.autograd.Function):
+    """text_fea = [output[b, len_b - 1, :H] | output[b, 0, H:]] (model.py:131-133)."""
+
+    @staticmethod
+    def forward(ctx, out, pk):
+        T, B, H2 = out.shape
+        fea = torch.empty((B, H2), dtype=torch.float32, device=out.device)
+        call("mvml_bilstm_select_last", B, H2 // 2, ptr(pk.lens), ptr(pk.pos), ptr(out), ptr(fea), 0,
+             _stream(out.device))
+        ctx.pk, ctx.shape = pk, out.shape
+        return fea
+
+    @staticmethod
+    def backward(ctx, g_fea):
+        T, B, H2 = ctx.shape
+        g_out = torch.zeros((T, B, H2), dtype=torch.float32, device=g_fea.device)
+        call("mvml_bilstm_select_last", B, H2 // 2, ptr(ctx.pk.lens), ptr(ctx.pk.pos), ptr(g_out),
+             ptr(_c(g_fea)), 1, _stream(g_fea.device))
+        return g_out, None
+
+
+class _LSTMParams(nn.Module):
+    """Parameter container with nn.LSTM's names and init (uniform +-1/sqrt(H))."""
+
+    def __init__(self, input_size, hidden_size, num_layers, dropout):
+        super().__init__()
+        self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
+        self.dropout, self.bidirectional, self.batch_first = dropout, True, True
+        for l in range(num_layers):
+            In = input_size if l == 0 else 2 * hidden_size
+            for sfx in ("", "_reverse"):
+                self.register_parameter(f"weight_ih_l{l}{sfx}", nn.Parameter(torch.empty(4 * hidden_size, In)))
+                self.register_parameter(f"weight_hh_l{l}{sfx}", nn.Parameter(torch.empty(4 * hidden_size, hidden_size)))
+                self.register_parameter(f"bias_ih_l{l}{sfx}", nn.Parameter(torch.empty(4 * hidden_size)))
+                self.register_parameter(f"bias_hh_l{l}{sfx}", nn.Parameter(torch.empty(4 * hidden_size)))
+        stdv = 1.0 / math.sqrt(hidden_size)
+        for p in self.parameters():
+            nn.init.uniform_(p, -stdv, stdv)
+
+    def layer_weights(self, l):
+        return [getattr(self, f"{n}_l{l}{sfx}") for sfx in ("", "_reverse")
+                for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
+
+
+class RNNModule(nn.Module):
+    """model.py:98-135 (bidirectional only, as MVP builds it, model.py:25)."""
+
+    def __init__(self, vocab, embed_dim, blstm_dim, num_layers, out_dim=2, dropout=0.2,
+                 bidirectional=True, device='cpu'):
+        super().__init__()
+        if not bidirectional:
+            raise NotImplementedError("MVP builds RNNModule bidirectional (model.py:25)")
+        self.vocab, self.embed_dim, self.blstm_dim = vocab, embed_dim, blstm_dim
+        self.hidden_size, self.num_layers, self.out_dim = blstm_dim, num_layers, out_dim
+        self.bidirectional, self.device, self.num_dir = True, device, 2
+        self.embeddings = nn.Embedding(vocab.tokens_length, embed_dim, padding_idx=vocab.pad)
+        self.rnn = _LSTMParams(embed_dim, blstm_dim, num_layers, dropout)
+        self.drop = nn.Dropout(p=dropout)
+        self.norm_layer = nn.LayerNorm(2 * blstm_dim)  # built but unused by forward (model.py:120)
+        self.fc = nn.Sequential(nn.Linear(2 * blstm_dim, out_dim), nn.ReLU(), nn.Dropout(p=dropout))
+
+    def forward(self, batch):
+        tokens = batch["smiles"]
+        dev = self.embeddings.weight.device
+        if tokens.device != dev:
+            tokens = tokens.to(dev)
+        pk = Packing(batch["seq_len"], tokens, self.vocab.tokens_length)
+        x = self.embeddings.weight
+        for l in range(self.num_layers):
+            x = BiLSTMLayerFunction.apply(x, pk, l == 0, *self.rnn.layer_weights(l))
+            if l + 1 < self.num_layers and self.training and self.rnn.dropout > 0:
+                x = nn.functional.dropout(x, self.rnn.dropout, True)  # nn.LSTM inter-layer dropout
+        fea = SelectLastFunction.apply(x, pk)
+        out = LinearReLUFunction.apply(fea, self.fc[0].weight, self.fc[0].bias)
+        return self.fc[2](out)

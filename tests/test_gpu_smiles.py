@@ -1,0 +1,71 @@
+"""SMILES BiLSTM view (RNNModule, model.py:98-135): HIP path vs the float64
+restatement on torch's nn.LSTM + pack_padded_sequence (oracle/smiles_ref.py)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 1e-5
+
+
+def _batch(B, seed, Tmax=60, ragged=True):
+    from mvml_gat.smiles import collate_smiles, tokens_struct
+    vocab = tokens_struct()
+    rng = np.random.default_rng(seed)
+    chars = [t for t in vocab.tokens if len(t) == 1 and t != ' '] + ['X', '%']  # '%','X' -> unk
+    lens = rng.integers(1, Tmax + 1, size=B) if ragged else np.full(B, Tmax)
+    smiles = ["".join(rng.choice(chars, size=int(n))) for n in lens]
+    return vocab, collate_smiles(smiles, vocab)
+
+
+@pytest.mark.parametrize("B,Tmax,layers,ragged", [(1, 7, 2, True), (5, 1, 1, True),
+                                                   (64, 60, 2, True), (33, 40, 3, False)])
+def test_rnn_module_parity(B, Tmax, layers, ragged):
+    from mvml_gat.smiles import RNNModule
+    from oracle.smiles_ref import RNNModuleRef
+    torch.manual_seed(B + layers)
+    vocab, batch = _batch(B, B * 7 + Tmax, Tmax, ragged)
+    ref = RNNModuleRef(39, 128, 384, layers, 384, 0.5).double().eval()
+    mod = RNNModule(vocab, 128, 384, layers, 384, 0.5).to(DEV).eval()
+    mod.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    zr = ref(batch)
+    zd = mod({"smiles": batch["smiles"].to(DEV), "seq_len": batch["seq_len"]})
+    assert zd.shape == (B, 384)
+    assert rel_err(zd, zr) < TOL
+    g = torch.Generator().manual_seed(B)
+    up = torch.randn(zr.shape, generator=g, dtype=torch.float64)
+    (zr * up).sum().backward()
+    (zd * up.float().to(DEV)).sum().backward()
+    pr = dict(ref.named_parameters())
+    for name, p in mod.named_parameters():
+        if pr[name].grad is None:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, name
+            continue
+        assert rel_err(p.grad, pr[name].grad) < TOL, name
+
+
+def test_rnn_module_deterministic():
+    from mvml_gat.smiles import RNNModule
+    vocab, batch = _batch(16, 3, 30)
+    torch.manual_seed(0)
+    mod = RNNModule(vocab, 128, 384, 2, 384, 0.5).to(DEV).eval()
+    b = {"smiles": batch["smiles"].to(DEV), "seq_len": batch["seq_len"]}
+    outs = []
+    for _ in range(2):
+        mod.zero_grad()
+        z = mod(b)
+        z.square().sum().backward()
+        outs.append((z.detach().clone(), mod.rnn.weight_hh_l0.grad.clone(), mod.embeddings.weight.grad.clone()))
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+
+
+def test_rnn_module_rejects_empty_sequence():
+    from mvml_gat.smiles import RNNModule
+    vocab, batch = _batch(4, 1, 10)
+    mod = RNNModule(vocab, 128, 384, 1, 384).to(DEV)
+    with pytest.raises(RuntimeError):
+        mod({"smiles": batch["smiles"].to(DEV), "seq_len": [0] + batch["seq_len"][1:]})
