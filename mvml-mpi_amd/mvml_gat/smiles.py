@@ -162,6 +162,9 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         g_x = torch.empty_like(x)
         for d in range(2):
             w_ih, w_hh = _c(w[4 * d]), _c(w[4 * d + 1])
+            # W_hh^T [H, 4H] once per backward: the per-step recurrent GEMM then reads its B
+            # operand k-contiguous (the same kernel variant as the forward, ~3x faster per step)
+            w_hhT = w_hh.t().contiguous()
             c, act = cs[d], acts[d]
             gg = torch.zeros((T, B, G), dtype=torch.float32, device=dev)
             carry = [torch.zeros((B, H), dtype=torch.float32, device=dev) for _ in range(2)]
@@ -171,7 +174,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                 bs = pk.batch_sizes[t]
                 if nxt is not None:  # recurrent gradient from the step this one fed
                     rows = min(bs, pk.batch_sizes[nxt])
-                    gemm(gg[nxt], w_hh, rows, H, G, 0, 1, G, H, g[t, :, d * H:], 2 * H, beta=1.0)
+                    gemm(gg[nxt], w_hhT, rows, H, G, 0, 0, G, G, g[t, :, d * H:], 2 * H, beta=1.0)
                 tp = t - 1 if d == 0 else t + 1
                 c_prev = c[tp] if 0 <= tp < T else None
                 g_c = carry[k % 2] if nxt is not None else None
