@@ -1,18 +1,28 @@
 #!/usr/bin/env python3
 """bench.py — molecules/sec of MVML-MPI's molecular-graph view (GNNModule, model.py:77-95)
-forward + backward on MI355X, plus the aggregation kernel's fraction of the HBM roofline.
+forward + backward + the multi-view fusion head on MI355X, plus the aggregation kernel's
+fraction of the HBM roofline.
 
-Step = one data-parallel training step of the graph view over a resident synthetic batch:
-GNNModule forward (GAT 74->4x192 flatten+ELU -> 4x384 mean, Set2Set 6 iters x 3-layer LSTM,
-GraphNorm per 64-molecule group, Linear+ReLU+Dropout), backward from a fixed upstream gradient
-(what the multi-view fusion would send back), one flat RCCL all-reduce of the gradients when
-N > 1, and the reference's Adam step (main.py:88, lr 1e-3, wd 1e-4).
-Workload = BASELINE config 3 (KEGG-like molecule sizes, GraphNorm groups of 64 = config.py:21
-batch size); each rank owns --mols-per-gpu molecules (weak scaling, no data-path collective).
+Workload (default) = BASELINE config 3 as written: ONE global set of 1,000,000 synthetic
+KEGG-like molecules (mvml_gat.synth.Config3Set), sharded over the ranks in whole 64-molecule
+GraphNorm groups (the reference's mini-batches, config.py:21 / main.py:79-81 / model.py:93)
+balanced by edges (mvml_gat.dist.shard_groups), resident in HBM and streamed through steps of
+--mols-per-step molecules per GPU.  Step = one data-parallel training step of model.py:51-72
+restricted to the graph view: GNNModule forward -> MVFusion (shared LayerNorm, 12-head 3-token
+attention, Conv2d, MLP) -> BCEWithLogits (main.py:91) -> backward -> one flat RCCL all-reduce of
+the gradients (N > 1) -> Adam (main.py:88).  The SMILES and fingerprint view embeddings that
+the fusion also consumes are fixed synthetic tensors (their views are not this workload).
+After the timed steps: a view-only figure (fixed upstream gradient, the round-1 headline) and
+one inference pass over the rank's whole shard whose (B_shard, 384) embeddings are all-gathered
+into the full 1M x 384 matrix (north_star's final embedding gather).
 
-    python bench.py [--gpus N --steps K --warmup W]     (N>1: launched by torch.distributed.run)
+    python bench.py [--gpus N --steps K --warmup W]
 
-Prints ONE JSON line on rank 0 (the driver's contract); a per-kernel breakdown goes to stderr.
+--gpus N without WORLD_SIZE in the environment starts N ranks itself (torch.distributed.run as
+a child process, before any GPU call); rank 0 prints the ONE JSON line (the driver's contract),
+a per-kernel breakdown goes to stderr.  --workload config5 = the skewed-size stress (per-rank
+sets, weak scaling).  --dry-run = CPU/gloo rehearsal of the launcher, sharding, all-reduce and
+gather plumbing with a trivial stand-in model (never a measurement: no HIP code runs).
 """
 import argparse
 import json
@@ -37,38 +47,41 @@ TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32
          "mvml_graphnorm_fwd", "mvml_graphnorm_bwd", "mvml_colsum_f32", "mvml_gat_fold_weights",
          "mvml_gat_unfold_grads", "mvml_relu_bwd", "mvml_layernorm_fwd", "mvml_layernorm_bwd",
          "mvml_token_attn_fwd", "mvml_token_attn_bwd", "mvml_conv3_fwd", "mvml_conv3_bwd",
-         "mvml_bce_logits"]
+         "mvml_bce_logits", "mvml_gat_attn_grad"]
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--mols-per-gpu", type=int, default=65536)
+    ap.add_argument("--workload", choices=["config3", "config5"], default="config3")
+    ap.add_argument("--total-mols", type=int, default=1_000_000,
+                    help="config 3: size of the ONE global molecule set sharded over the ranks")
+    ap.add_argument("--mols-per-step", type=int, default=65536,
+                    help="molecules per GPU per step (whole GraphNorm groups); config5 default 8192")
     ap.add_argument("--group-size", type=int, default=64)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--view-only-steps", type=int, default=3,
+                    help="extra steps timed without the fusion head (fixed upstream gradient)")
+    ap.add_argument("--no-inference", action="store_true",
+                    help="skip the inference pass + embedding all-gather over the whole shard")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
-    ap.add_argument("--with-fusion", action="store_true",
-                    help="config 3 with its consumer: the MVP fusion head (SURVEY 8f-1) + BCE loss "
-                         "on the GAT view's output (the SMILES / fingerprint views, out of scope, "
-                         "are synthetic fixed embeddings)")
-    ap.add_argument("--workload", choices=["config3", "config5"], default="config3",
-                    help="config5 = BASELINE config 5 skewed-size stress (150-400 atoms + hubs of "
-                         "in-degree 32-128; --mols-per-gpu defaults to 8192 there)")
     ap.add_argument("--proj-bf16", action="store_true",
                     help="BASELINE config 4: the GAT projection GEMMs (fc / res_fc, forward and "
-                         "backward) on bf16 operands with fp32 accumulation (mvml_gemm_bf16); "
-                         "everything else stays fp32")
-    return ap.parse_args()
+                         "backward) on bf16 operands with fp32 accumulation (mvml_gemm_bf16)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo plumbing rehearsal with a stand-in model (no measurement)")
+    return ap.parse_args(argv)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# ----------------------------------------------------------------------------- reporting
 def kernel_report(summary, elapsed_ms_per_step, steps):
     """Per entry point: calls/step, avg ms, share of the step, achieved GB/s or TFLOP/s."""
     rows = {}
@@ -99,129 +112,286 @@ def roofline_entry(ev, kind):
             "frac": round(ach / FP32_MFMA_PEAK_TFS, 4), "avg_launch_ms": round(tot_ms / len(ev), 4)}
 
 
-def load_traffic(kernel):
-    """HBM traffic per launch from the committed rocprofv3 PMC summary (profiles/), if any."""
+def load_traffic(workload_key, entry):
+    """HBM traffic per launch of `entry` from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json), ONLY if it was profiled on this exact workload; else None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+    return d.get(workload_key, {}).get(entry, {}).get("hbm_bytes_per_launch")
 
 
-def cpu_baseline(seconds, group_size):
-    """The CPU restatement of the reference path (oracle/, DGL semantics in plain PyTorch,
-    fp32) timed on this host's cores on a bounded sample of the same workload."""
+# ----------------------------------------------------------------------------- CPU baseline
+def usable_cores():
+    """CPUs this process may actually run on: the affinity mask, capped by a cgroup v2 quota
+    (on the GPU box os.cpu_count() reports the whole machine, not this job's share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds, group_size, with_fusion):
+    """The CPU restatement of the reference path (oracle/: DGL / PyG semantics in plain PyTorch,
+    fp32 — NOT DGL, which cannot be installed here) timed on this host's cores on a bounded
+    sample of the same workload (BASELINE.md plan: all usable cores, 3 warm-ups, median of >= 10
+    timed steps over whole 64-molecule groups)."""
     from mvml_gat import synth
+    from oracle.fusion_ref import MVFusionRef, bce_logits_ref
     from oracle.gnn_ref import GNNModuleRef
     from oracle.graph_ref import batch_ref
+    cores = usable_cores()
+    torch.set_num_threads(cores)
     n_mols = 4 * group_size
-    sb = synth.config3(n_mols, seed=7)
+    sb = synth.Config3Set(n_mols, seed=7).molecules(0, n_mols)
     gd = batch_ref(sb.num_nodes, sb.src_local, sb.dst_local, sb.num_edges)
     gd["group_offsets"] = list(range(0, n_mols, group_size)) + [n_mols]
     torch.manual_seed(0)
     ref = GNNModuleRef(74, [192, 384], 0.5, 6, 3).train()
-    opt = torch.optim.Adam(ref.parameters(), lr=1e-3, weight_decay=1e-4)
+    params = list(ref.parameters())
+    fus = None
+    if with_fusion:
+        fus = MVFusionRef(384, 12, 11, 0.5).train()
+        params += list(fus.parameters())
+    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-4)
     X = torch.as_tensor(sb.feats)
-    up = torch.randn(n_mols, 384) * 1e-3
+    g = torch.Generator().manual_seed(1)
+    up = torch.randn(n_mols, 384, generator=g) * 1e-3
+    sx, fx = torch.randn(n_mols, 384, generator=g), torch.randn(n_mols, 384, generator=g)
+    labels = (torch.rand(n_mols, 11, generator=g) > 0.8).float()
 
     def step():
         opt.zero_grad()
-        ref(gd, X).backward(up)
+        out = ref(gd, X)
+        if fus is not None:
+            bce_logits_ref(fus(sx, out, fx), labels).backward()
+        else:
+            out.backward(up)
         opt.step()
 
-    step()
-    t0, n = time.perf_counter(), 0
-    while n < 2 or time.perf_counter() - t0 < seconds:
+    for _ in range(3):
         step()
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n * n_mols / dt, 2), "unit": "molecules/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"{n} steps x {n_mols} KEGG-like molecules ({int(sb.num_nodes.sum())} atoms), "
-                      f"fwd+bwd+Adam, oracle/gnn_ref.py GNNModuleRef in fp32 (DGL-semantics CPU "
-                      f"restatement, not DGL)"}
+    times = []
+    t_end = time.perf_counter() + seconds
+    while len(times) < 10 or time.perf_counter() < t_end:
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+        if len(times) >= 200:
+            break
+    med = float(np.median(times))
+    return {"value": round(n_mols / med, 2), "unit": "molecules/s", "cores": cores,
+            "kind": "port", "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": f"median of {len(times)} steps (3 warm-ups) x {n_mols} KEGG-like molecules "
+                      f"({int(sb.num_nodes.sum())} atoms, {n_mols // group_size} GraphNorm groups of "
+                      f"{group_size}), fwd+bwd{' + MVFusion + BCE' if with_fusion else ''} + Adam, "
+                      "oracle/gnn_ref.py + oracle/fusion_ref.py in fp32 (DGL-semantics CPU "
+                      "restatement, not DGL)"}
 
 
-def main():
-    args = parse()
+# ----------------------------------------------------------------------------- data
+class Batch:
+    """One step's resident inputs: the device-built graph + features, and the fusion head's
+    other two view embeddings / labels (seeded by the batch's first global molecule index, so
+    they do not depend on how the set was sharded)."""
+
+    def __init__(self, sb, first_mol, group_size, dev, with_fusion):
+        self.g = sb.to_graph(group_size=group_size).to(dev)
+        self.feats = self.g.ndata["h"]
+        self.B, self.N, self.E = self.g.batch_size, self.g.num_nodes(), self.g.num_edges()
+        if with_fusion:
+            gen = torch.Generator(device=dev).manual_seed(1234 + first_mol)
+            self.smiles_x = torch.randn((self.B, 384), device=dev, generator=gen)
+            self.fp_x = torch.randn((self.B, 384), device=dev, generator=gen)
+            self.labels = (torch.rand((self.B, 11), device=dev, generator=gen) > 0.8).float()
+
+
+def build_batches(args, rank, world, dev, with_fusion):
+    from mvml_gat import dist as mdist
+    from mvml_gat import synth
+    gs = args.group_size
+    if args.workload == "config3":
+        gset = synth.Config3Set(args.total_mols, seed=args.seed)
+        g0, g1 = mdist.shard_groups(gset.group_costs(gs), world, rank)
+        lo, hi = g0 * gs, min(g1 * gs, args.total_mols)
+        per = max(gs, args.mols_per_step // gs * gs)
+        out = []
+        for m in range(lo, hi, per):
+            sb = gset.molecules(m, min(hi, m + per))
+            out.append(Batch(sb, m, gs, dev, with_fusion))
+        return out, (lo, hi)
+    n5 = args.mols_per_step if args.mols_per_step != 65536 else 8192
+    sb = synth.config5(n5, seed=1 + 1000 * args.seed + rank)
+    return [Batch(sb, rank * n5, gs, dev, with_fusion)], (rank * n5, (rank + 1) * n5)
+
+
+# ----------------------------------------------------------------------------- dry-run stand-in
+class _PlumbingStandIn(torch.nn.Module):
+    """--dry-run only: a trivial CPU model with the view's call signature (segment mean of the
+    atom features -> Linear), so the launcher / sharding / all-reduce / all-gather plumbing can
+    be rehearsed on gloo without a GPU.  Never used for any reported number."""
+
+    def __init__(self):
+        super().__init__()
+        self.lin = torch.nn.Linear(74, 384)
+        self.head = torch.nn.Linear(3 * 384, 11)
+
+    def view(self, g, feats):
+        B = g.batch_size
+        gid = torch.repeat_interleave(torch.arange(B), torch.as_tensor(g._bnn))
+        s = torch.zeros(B, 74).index_add(0, gid, feats)
+        return self.lin(s / torch.as_tensor(g._bnn).clamp(min=1).unsqueeze(1).float())
+
+    def forward(self, g, feats):
+        return self.view(g, feats)
+
+    def fuse(self, sx, gx, fx):
+        return self.head(torch.cat([sx, gx, fx], 1))
+
+
+# ----------------------------------------------------------------------------- worker
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    if args.dry_run:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+        if world > 1:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
-    import mvml_gat
-    from mvml_gat import _lib, synth
-    from mvml_gat.dist import FlatGradAllReduce
-    mvml_gat.lib()
+    from mvml_gat.dist import EmbeddingAllGather, FlatGradAllReduce
+    if not args.dry_run:
+        import mvml_gat
+        from mvml_gat import _lib
+        mvml_gat.lib()
+
+    def sync():
+        if not args.dry_run:
+            torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
 
     t_gen = time.perf_counter()
-    if args.workload == "config5":
-        n5 = args.mols_per_gpu if args.mols_per_gpu != 65536 else 8192
-        sb = synth.config5(n5, seed=1 + 1000 * args.seed + rank)
+    if args.dry_run:
+        from mvml_gat import dist as mdist
+        from mvml_gat import synth
+        gs = args.group_size
+        gset = synth.Config3Set(args.total_mols, seed=args.seed)
+        g0, g1 = mdist.shard_groups(gset.group_costs(gs), world, rank)
+        lo, hi = g0 * gs, min(g1 * gs, args.total_mols)
+        batches = []
+        for m in range(lo, hi, args.mols_per_step):
+            sb = gset.molecules(m, min(hi, m + args.mols_per_step))
+            b = Batch.__new__(Batch)
+            b.g = sb.to_graph(group_size=gs)
+            b.feats = torch.as_tensor(sb.feats)
+            b.B, b.N, b.E = b.g.batch_size, b.g.num_nodes(), b.g.num_edges()
+            gen = torch.Generator().manual_seed(1234 + m)
+            b.smiles_x, b.fp_x = torch.randn((b.B, 384), generator=gen), torch.randn((b.B, 384), generator=gen)
+            b.labels = (torch.rand((b.B, 11), generator=gen) > 0.8).float()
+            batches.append(b)
+        shard = (lo, hi)
     else:
-        sb = synth.config3(args.mols_per_gpu, seed=1000 * args.seed + rank)
-    g = sb.to_graph(group_size=args.group_size).to(dev)
-    feats = g.ndata["h"]
-    N, E, B = g.num_nodes(), g.num_edges(), g.batch_size
-    log(f"[rank {rank}] data: {B} molecules, {N} atoms, {E} edges ({time.perf_counter() - t_gen:.1f}s)")
+        batches, shard = build_batches(args, rank, world, dev, with_fusion=True)
+    n_local = sum(b.B for b in batches)
+    log(f"[rank {rank}] shard molecules [{shard[0]}, {shard[1]}): {len(batches)} batches, "
+        f"{n_local} molecules, {sum(b.N for b in batches)} atoms, {sum(b.E for b in batches)} edges "
+        f"({time.perf_counter() - t_gen:.1f}s)")
 
     torch.manual_seed(args.seed)
-    model = mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3,
-                               proj_dtype=torch.bfloat16 if args.proj_bf16 else None).to(dev).train()
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4)
-    reducer = FlatGradAllReduce(model.parameters(), average=True)
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    upstream = torch.randn((B, 384), device=dev, generator=gen) * 1e-3
-    if args.with_fusion:
+    if args.dry_run:
+        model = _PlumbingStandIn()
+        fusion = None
+        params = list(model.parameters())
+    else:
+        model = mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3,
+                                   proj_dtype=torch.bfloat16 if args.proj_bf16 else None).to(dev).train()
         fusion = mvml_gat.MVFusion(384, 12, 11, 0.5).to(dev).train()
         params = list(model.parameters()) + list(fusion.parameters())
-        opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-4)
-        reducer = FlatGradAllReduce(params, average=True)
-        smiles_x = torch.randn((B, 384), device=dev, generator=gen)
-        fp_x = torch.randn((B, 384), device=dev, generator=gen)
-        labels = (torch.rand((B, 11), device=dev, generator=gen) > 0.8).float()
+    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-4)
+    reducer = FlatGradAllReduce(params, average=True)
 
-    def step():
+    def step(b, fused=True):
         opt.zero_grad(set_to_none=False)
-        out = model(g, feats)
-        if args.with_fusion:
-            mvml_gat.bce_with_logits(fusion(smiles_x, out, fp_x), labels).backward()
+        out = model(b.g, b.feats)
+        if args.dry_run:
+            torch.nn.functional.binary_cross_entropy_with_logits(
+                model.fuse(b.smiles_x, out, b.fp_x), b.labels).backward()
+        elif fused:
+            mvml_gat.bce_with_logits(fusion(b.smiles_x, out, b.fp_x), b.labels).backward()
         else:
-            out.backward(upstream)
+            out.backward(b.upstream)
         reducer()
         opt.step()
 
-    for _ in range(args.warmup):
-        step()
-    if not args.no_kernel_timer:
+    nb = len(batches)
+    for i in range(args.warmup):
+        step(batches[i % nb])
+    timer_on = not args.no_kernel_timer and not args.dry_run
+    if timer_on:
         _lib.timer.enable(TIMED)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    barrier()
+    sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    mols = 0
+    for i in range(args.steps):
+        b = batches[(args.warmup + i) % nb]
+        step(b)
+        mols += b.B
+    sync()
+    barrier()
     elapsed = time.perf_counter() - t0
-    _lib.timer.disable()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if timer_on:
+        _lib.timer.disable()
+
+    def reduce_max(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = world * B * args.steps / elapsed
+        return t.item()
+
+    def reduce_sum(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.item()
+
+    elapsed = reduce_max(elapsed)
+    total_mols = reduce_sum(mols)
+    ms_per_step = elapsed * 1e3 / max(args.steps, 1)
+    value = total_mols / elapsed if elapsed > 0 else 0.0
 
     roofline, extra = None, {}
-    if not args.no_kernel_timer:
+    wkey = f"{args.workload}/mols_per_step={args.mols_per_step}" + ("/proj_bf16" if args.proj_bf16 else "")
+    if timer_on:
         summ = _lib.timer.summary()
         rows = kernel_report(summ, ms_per_step, args.steps)
         if rank == 0:
@@ -232,10 +402,11 @@ def main():
         if summ.get("mvml_gat_agg_fwd"):
             roofline = roofline_entry(summ["mvml_gat_agg_fwd"], "hbm")
             roofline["kernel"] = "mvml_gat_agg_fwd (both GAT layers; fused edge-softmax + u_mul_e-sum)"
-            roofline["traffic"] = load_traffic("gat_agg_fwd")
+            roofline["traffic"] = load_traffic(wkey, "gat_agg_fwd")
+            roofline["traffic_profile"] = wkey if roofline["traffic"] else None
         if summ.get("mvml_gat_agg_bwd"):
             extra["roofline_agg_bwd"] = roofline_entry(summ["mvml_gat_agg_bwd"], "hbm")
-            extra["roofline_agg_bwd"]["traffic"] = load_traffic("gat_agg_bwd")
+            extra["roofline_agg_bwd"]["traffic"] = load_traffic(wkey, "gat_agg_bwd")
         proj_ev = summ.get("mvml_gat_proj_fwd", [])
         gemm_ev = summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", []) + ([] if args.proj_bf16 else proj_ev)
         bf_ev = summ.get("mvml_gemm_bf16", []) + (proj_ev if args.proj_bf16 else [])
@@ -254,26 +425,83 @@ def main():
                 extra["roofline_gemm"]["frac"] = round(extra["roofline_gemm"]["achieved"] / (BF16_MFMA_PEAK_TFS / 6), 4)
         extra["kernel_ms_per_step"] = {k: round(v["ms_per_step"], 3) for k, v in rows.items()}
 
+    # ---- view-only figure (the graph view alone, fixed upstream gradient at its output)
+    if args.view_only_steps > 0 and not args.dry_run:
+        for b in batches:
+            gen = torch.Generator(device=dev).manual_seed(99 + b.B)
+            b.upstream = torch.randn((b.B, 384), device=dev, generator=gen) * 1e-3
+        step(batches[0], fused=False)
+        barrier()
+        sync()
+        t1 = time.perf_counter()
+        vm = 0
+        for i in range(args.view_only_steps):
+            b = batches[i % nb]
+            step(b, fused=False)
+            vm += b.B
+        sync()
+        barrier()
+        ve = reduce_max(time.perf_counter() - t1)
+        extra["view_only"] = {"value": round(reduce_sum(vm) / ve, 2), "unit": "molecules/s",
+                              "ms_per_step": round(ve * 1e3 / args.view_only_steps, 3),
+                              "steps": args.view_only_steps,
+                              "what": "GNNModule fwd+bwd from a fixed upstream gradient + all-reduce + Adam"}
+        for b in batches:
+            b.upstream = None
+
+    # ---- inference over the whole shard + the final embedding all-gather
+    if not args.no_inference:
+        model.eval()
+        gather = EmbeddingAllGather()
+        with torch.no_grad():
+            model(batches[0].g, batches[0].feats)  # warm
+            barrier()
+            sync()
+            t1 = time.perf_counter()
+            emb = torch.cat([model(b.g, b.feats) for b in batches], 0)
+            sync()
+            t2 = time.perf_counter()
+            barrier()
+            full = gather(emb)
+            sync()
+            t3 = time.perf_counter()
+        fwd_s, gat_s = reduce_max(t2 - t1), reduce_max(t3 - t2)
+        extra["inference"] = {
+            "molecules": int(full.shape[0]), "value": round(full.shape[0] / fwd_s, 2),
+            "unit": "molecules/s", "forward_ms": round(fwd_s * 1e3, 2),
+            "allgather_ms": round(gat_s * 1e3, 2), "allgather_bytes": int(full.numel() * 4),
+            "checksum": float(full.double().sum().item()),
+            "what": "GNNModule eval forward over every molecule of the shard, then one all-gather "
+                    "of the (B_shard, 384) embeddings into the full matrix on every rank"}
+        model.train()
+
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds, args.group_size)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
+        cpu = cpu_baseline(args.cpu_seconds, args.group_size, with_fusion=True)
 
     if rank == 0:
+        gsz = args.group_size
+        if args.workload == "config3":
+            wl = (f"BASELINE config 3: one global set of {args.total_mols} KEGG-like molecules, "
+                  f"sharded in whole {gsz}-molecule GraphNorm groups, streamed through "
+                  f"{args.mols_per_step}-molecule steps per GPU; view + fusion: GNNModule (GAT "
+                  "[192,384] x4 heads, Set2Set 6x3, GraphNorm, fc) -> MVFusion (12-head 3-token "
+                  "attention, Conv2d, MLP) -> BCEWithLogits, fwd+bwd+Adam")
+        else:
+            wl = ("BASELINE config 5 (150-400-atom molecules with 1-4 hubs of in-degree 32-128, "
+                  "per-rank sets): GNNModule -> MVFusion -> BCEWithLogits, fwd+bwd+Adam")
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "molecules/s", "n_gpus": world,
+            "metric": METRIC if not args.dry_run else "DRY RUN (plumbing rehearsal, not a measurement)",
+            "value": round(value, 2), "unit": "molecules/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16 projection, f32 elsewhere" if args.proj_bf16 else "f32",
-            "data": "synthetic (seeded KEGG-like drug-like molecules, random-init weights)",
-            "config": {"workload": ("BASELINE config 5 (150-400-atom molecules with 1-4 hubs of in-degree "
-                                    "32-128): " if args.workload == "config5" else "BASELINE config 3: ") +
-                                   "GNNModule (GAT [192,384] x4 heads, Set2Set 6x3, "
-                                   "GraphNorm, fc) fwd+bwd+Adam over KEGG-like molecules"
-                                   + (" + MVP fusion head (12-head 3-token attention, Conv2d, MLP) "
-                                      "+ BCEWithLogits" if args.with_fusion else
-                                      " (fixed upstream gradient at the view output)"),
-                       "mols_per_gpu": B, "atoms_per_gpu": N, "edges_per_gpu": E,
-                       "graphnorm_group": args.group_size, "parallelism": f"dp{world}",
+            "data": "synthetic (seeded KEGG-like drug-like molecules, random-init weights; the "
+                    "SMILES / fingerprint view embeddings fed to the fusion are fixed random tensors)",
+            "config": {"workload": wl, "global_mols": args.total_mols if args.workload == "config3" else None,
+                       "mols_per_step_per_gpu": batches[0].B, "batches_on_rank0": nb,
+                       "atoms_per_step_rank0": batches[0].N, "edges_per_step_rank0": batches[0].E,
+                       "graphnorm_group": gsz, "parallelism": f"dp{world}",
                        "projection": "bf16 operands, fp32 accumulate (config 4)" if args.proj_bf16
                        else "fp32-accurate split-bf16 x3"},
             "roofline": roofline, "cpu_baseline": cpu,
@@ -282,6 +510,15 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launcher: N ranks as child processes (no GPU call has happened in this process)
+        from mvml_gat.dist import launch_local_ranks
+        sys.exit(launch_local_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    run(args)
 
 
 if __name__ == "__main__":

@@ -152,11 +152,17 @@ _ws = {}
 
 
 def workspace(nbytes, device):
-    """Per-device scratch buffer (stream-ordered reuse through the caching allocator)."""
-    key = torch.device(device).index or 0
+    """Scratch buffer of the calling stream: one per (device, stream), so entry points enqueued
+    on different streams never share scratch (the header's re-entrancy contract), and calls on
+    one stream reuse it in stream order.  Growing allocates on the current stream and drops the
+    old buffer there too, so the caching allocator hands it out again only behind the work that
+    was enqueued on that stream before it."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
         _ws[key] = buf
     return buf
 

@@ -26,6 +26,54 @@ def shard_groups(group_costs, world_size, rank):
     return int(cuts[rank]), int(cuts[rank + 1])
 
 
+class EmbeddingAllGather:
+    """The final embedding gather of north_star: every rank holds the (B_r, D) view embeddings
+    of its own contiguous molecule shard; one all-gather (RCCL over xGMI; gloo on CPU) makes
+    the whole (sum_r B_r, D) matrix, in global molecule order, on every rank.
+
+    Shards may differ in size (groups are balanced by edges, not molecules): each rank's rows
+    are padded to the largest shard so the collective is a single fixed-size
+    all_gather_into_tensor, and the padding is dropped when the result is assembled."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def __call__(self, emb):
+        if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            return emb
+        world = dist.get_world_size(self.group)
+        dev = emb.device
+        n = torch.tensor([emb.shape[0]], dtype=torch.int64, device=dev)
+        counts = torch.empty(world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(counts, n, group=self.group)
+        counts = counts.cpu().tolist()
+        rows = max(counts)
+        D = emb.shape[1]
+        send = emb.new_zeros((rows, D))
+        send[:emb.shape[0]].copy_(emb)
+        recv = emb.new_empty((world * rows, D))
+        dist.all_gather_into_tensor(recv, send, group=self.group)
+        return torch.cat([recv[r * rows:r * rows + c] for r, c in enumerate(counts)], 0)
+
+
+def launch_local_ranks(nprocs, script, argv, port=None):
+    """Start `nprocs` ranks of `script` on this node (one process per GPU) with
+    torch.distributed.run as a CHILD process — the caller has not touched the GPU and never
+    exec()s — and return the exit code.  Rendezvous on 127.0.0.1 (the container hostname may
+    not resolve).  The ranks inherit stdout, so rank 0's output is the caller's output."""
+    import socket
+    import subprocess
+    import sys
+    if port is None:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nprocs}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", script, *argv]
+    return subprocess.call(cmd)
+
+
 class FlatGradAllReduce:
     """Packs every parameter gradient into one contiguous fp32 buffer and all-reduces it in a
     single call (the view's 6.9 M params = 27.7 MB: latency-, not bandwidth-bound on xGMI,

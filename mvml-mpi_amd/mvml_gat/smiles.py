@@ -77,7 +77,8 @@ class Packing:
     """Host-side pack_padded_sequence(enforce_sorted=False) metadata (the reference computes it on
     the CPU from the ``seq_len`` list as well): descending-length order, batch_sizes per step."""
 
-    def __init__(self, seq_lens, tokens, vocab_size):
+    def __init__(self, seq_lens, tokens, vocab_size, pad=None):
+        self.pad = pad
         lens = np.asarray(list(seq_lens), dtype=np.int64)
         if lens.ndim != 1 or lens.size == 0:
             raise ValueError("seq_len must be a non-empty list of lengths")
@@ -196,6 +197,10 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                      ptr(pk.lens), ptr(pk.perm), V, ptr(Gt), st)
                 gemm(Gt, x, G, In, V, 1, 1, G, In, g_wih, In)
                 gemm(Gt, w_ih, V, In, G, 0, 1, G, In, g_x, In, beta=beta)
+                if d == 1 and pk.pad is not None:
+                    # nn.Embedding(padding_idx=pad) (model.py:113): the padding row never
+                    # receives a gradient, even where the pad token occurs inside a sequence
+                    g_x[pk.pad].zero_()
             else:
                 gemm(gg, x, G, In, T * B, 1, 1, G, In, g_wih, In)
                 gemm(gg, w_ih, T * B, In, G, 0, 1, G, In, g_x, In, beta=beta)
@@ -269,7 +274,7 @@ class RNNModule(nn.Module):
         dev = self.embeddings.weight.device
         if tokens.device != dev:
             tokens = tokens.to(dev)
-        pk = Packing(batch["seq_len"], tokens, self.vocab.tokens_length)
+        pk = Packing(batch["seq_len"], tokens, self.vocab.tokens_length, self.embeddings.padding_idx)
         x = self.embeddings.weight
         for l in range(self.num_layers):
             x = BiLSTMLayerFunction.apply(x, pk, l == 0, *self.rnn.layer_weights(l))

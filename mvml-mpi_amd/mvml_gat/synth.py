@@ -168,6 +168,66 @@ def config3(n_mols=65536, seed=0):
                       lambda M, n: np.minimum(rng.poisson(2.4, size=M), max(n // 5, 1)))
 
 
+class Config3Set:
+    """The ONE global config-3 molecule set (BASELINE.json config 3: 1M molecules) as a cheap
+    global plan — every molecule's atom count and requested ring closures, drawn up front — from
+    which any contiguous range of molecules is generated on demand, identically whatever range
+    asks for it: the structures / features of chunk c (molecules [c*chunk, (c+1)*chunk)) come
+    from their own seeded stream, so a rank generating only its shard gets exactly the rows of
+    the single-process set.
+
+    group_costs(group_size): the expected edge count of each GraphNorm group (2 (n-1+rings) + n
+    per molecule; a ring closure that fails its 64 attempts makes the real count lower), the
+    cost mvml_gat.dist.shard_groups balances."""
+
+    def __init__(self, n_mols=1_000_000, seed=0, chunk=65536):
+        self.n_mols, self.seed, self.chunk = int(n_mols), int(seed), int(chunk)
+        rng = np.random.default_rng([self.seed, 0x5EED])
+        self.sizes = kegg_like_sizes(rng, self.n_mols)
+        self.rings = np.minimum(rng.poisson(2.4, size=self.n_mols), np.maximum(self.sizes // 5, 1))
+
+    def group_costs(self, group_size):
+        e = 2 * (self.sizes - 1 + self.rings) + self.sizes
+        G = -(-self.n_mols // group_size)
+        pad = np.zeros(G * group_size, dtype=np.int64)
+        pad[:self.n_mols] = e
+        return pad.reshape(G, group_size).sum(1)
+
+    def _chunk(self, c):
+        lo, hi = c * self.chunk, min(self.n_mols, (c + 1) * self.chunk)
+        sizes, rings = self.sizes[lo:hi], self.rings[lo:hi]
+        rng = np.random.default_rng([self.seed, c])
+        return _gen_sizes(rng, sizes, lambda M, n: rings[sizes == n])
+
+    def molecules(self, lo, hi):
+        """SynthBatch of molecules [lo, hi) of the global set."""
+        lo, hi = max(0, int(lo)), min(self.n_mols, int(hi))
+        parts = []
+        for c in range(lo // self.chunk, -(-hi // self.chunk)):
+            sb = self._chunk(c)
+            c0 = c * self.chunk
+            parts.append(slice_batch(sb, max(lo, c0) - c0, min(hi, c0 + sb.batch_size) - c0))
+        return concat_batches(parts)
+
+
+def slice_batch(sb, lo, hi):
+    """Molecules [lo, hi) of a SynthBatch."""
+    e0, e1 = int(sb.num_edges[:lo].sum()), int(sb.num_edges[:hi].sum())
+    n0, n1 = int(sb.num_nodes[:lo].sum()), int(sb.num_nodes[:hi].sum())
+    return SynthBatch(sb.num_nodes[lo:hi], sb.num_edges[lo:hi], sb.src_local[e0:e1],
+                      sb.dst_local[e0:e1], sb.feats[n0:n1])
+
+
+def concat_batches(parts):
+    if len(parts) == 1:
+        return parts[0]
+    return SynthBatch(np.concatenate([p.num_nodes for p in parts]),
+                      np.concatenate([p.num_edges for p in parts]),
+                      np.concatenate([p.src_local for p in parts]),
+                      np.concatenate([p.dst_local for p in parts]),
+                      np.concatenate([p.feats for p in parts]))
+
+
 def config5(n_mols=4096, seed=1):
     """BASELINE config 5: 150-400 atoms plus 1-4 hubs with 32-128 extra bonds (non-chemical)."""
     rng = np.random.default_rng(seed)

@@ -86,3 +86,86 @@ def test_shard_groups_balanced_and_covering():
     assert all(cuts[i][1] == cuts[i + 1][0] for i in range(3))
     loads = [costs[a:b].sum() for a, b in cuts]
     assert max(loads) <= 1.5 * (costs.sum() / 4)
+
+
+def _gather_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mvml_gat.dist import EmbeddingAllGather
+    sb, ref = _setup()
+    costs = [int(sb.num_edges[2 * i:2 * i + 2].sum()) for i in range(5)]
+    g0, g1 = shard_groups(costs, world, rank)
+    gd, X = _subbatch(sb, 2 * g0, 2 * g1)
+    with torch.no_grad():
+        emb = ref(gd, X) if g1 > g0 else torch.zeros((0, 12), dtype=torch.float64)
+        full = EmbeddingAllGather()(emb)
+    out.put((rank, full.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_embedding_allgather_matches_single_process():
+    """north_star's final embedding gather: per-rank (B_shard, D) embeddings of whole GraphNorm
+    groups, all-gathered, equal the single-process embeddings of the whole batch, in order."""
+    sb, ref = _setup()
+    gd, X = _subbatch(sb, 0, 10)
+    with torch.no_grad():
+        want = ref(gd, X).numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in range(2):
+        assert got[r].shape == want.shape
+        np.testing.assert_allclose(got[r], want, rtol=1e-12, atol=1e-14)
+
+
+def test_config3_set_shards_are_slices_of_the_global_set():
+    """Config3Set.molecules(lo, hi) is independent of which range asks (chunk-seeded), so a
+    rank's shard is exactly its slice of the single-process 1M-molecule set."""
+    from mvml_gat.synth import Config3Set, slice_batch
+    s = Config3Set(300, seed=5, chunk=128)
+    full = s.molecules(0, 300)
+    assert full.batch_size == 300 and int(full.num_nodes.sum()) == full.feats.shape[0]
+    for lo, hi in ((0, 64), (64, 200), (192, 300), (127, 129)):
+        part = s.molecules(lo, hi)
+        ref = slice_batch(full, lo, hi)
+        for k in ("num_nodes", "num_edges", "src_local", "dst_local", "feats"):
+            np.testing.assert_array_equal(getattr(part, k), getattr(ref, k), err_msg=k)
+    costs = s.group_costs(64)
+    assert len(costs) == 5 and costs.sum() >= full.num_edges.sum()
+
+
+def _run_bench(*args):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--dry-run", *args],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_launcher_two_ranks_dry_run():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts 2 ranks itself; one JSON line comes back
+    with n_gpus 2; sharding + all-gather reproduce the single-rank embeddings exactly, and the
+    DP training steps (flat all-reduce) run."""
+    common = ["--total-mols", "1024", "--mols-per-step", "256"]
+    one = _run_bench("--gpus", "1", "--steps", "0", "--warmup", "0", *common)
+    two = _run_bench("--gpus", "2", "--steps", "0", "--warmup", "0", *common)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["inference"]["molecules"] == one["inference"]["molecules"] == 1024
+    assert two["inference"]["checksum"] == one["inference"]["checksum"]
+    trained = _run_bench("--gpus", "2", "--steps", "2", "--warmup", "1", *common)
+    assert trained["n_gpus"] == 2 and trained["value"] > 0 and trained["config"]["parallelism"] == "dp2"

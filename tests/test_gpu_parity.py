@@ -153,6 +153,32 @@ def test_gemm_x3_error_matches_fp32(K):
         assert errs[algo][0] <= 2 * base[0] and errs[algo][1] <= 2 * base[1], errs
 
 
+def test_gemm_two_streams_concurrent():
+    """Split-K GEMMs (which use workspace slabs) enqueued on two streams at once: each stream
+    has its own scratch, so neither result is corrupted by the other's partial sums."""
+    from mvml_gat import _lib
+    from mvml_gat.functional import gemm
+    g = torch.Generator().manual_seed(9)
+    M, N, K = 384, 76, 200000  # long K: split-K with slabs in the workspace
+    As = [torch.randn(K, M, generator=g) for _ in range(2)]
+    Bs = [torch.randn(K, N, generator=g) for _ in range(2)]
+    refs = [(a.double().t() @ b.double()) for a, b in zip(As, Bs)]
+    Ad = [a.to(DEV) for a in As]
+    Bd = [b.to(DEV) for b in Bs]
+    Cs = [torch.zeros(M, N, device=DEV) for _ in range(2)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for i, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                gemm(Ad[i], Bd[i], M, N, K, 1, 1, M, N, Cs[i], N)
+    torch.cuda.synchronize()
+    keys = {k for k in _lib._ws if k[1] in (s.cuda_stream for s in streams)}
+    assert len(keys) == 2, keys
+    for C, ref in zip(Cs, refs):
+        assert rel_err(C, ref) < TOL
+
+
 def test_colsum():
     from mvml_gat.functional import colsum
     X = torch.randn(5000, 37, dtype=torch.float64)

@@ -11,23 +11,28 @@ DEV = "cuda"
 TOL = 1e-5
 
 
-def _batch(B, seed, Tmax=60, ragged=True):
+def _batch(B, seed, Tmax=60, ragged=True, space=False):
     from mvml_gat.smiles import collate_smiles, tokens_struct
     vocab = tokens_struct()
     rng = np.random.default_rng(seed)
     chars = [t for t in vocab.tokens if len(t) == 1 and t != ' '] + ['X', '%']  # '%','X' -> unk
+    if space:  # the pad token ' ' (index 0) inside live positions
+        chars += [' '] * 4
     lens = rng.integers(1, Tmax + 1, size=B) if ragged else np.full(B, Tmax)
     smiles = ["".join(rng.choice(chars, size=int(n))) for n in lens]
     return vocab, collate_smiles(smiles, vocab)
 
 
-@pytest.mark.parametrize("B,Tmax,layers,ragged", [(1, 7, 2, True), (5, 1, 1, True),
-                                                   (64, 60, 2, True), (33, 40, 3, False)])
-def test_rnn_module_parity(B, Tmax, layers, ragged):
+@pytest.mark.parametrize("B,Tmax,layers,ragged,space", [(1, 7, 2, True, False), (5, 1, 1, True, False),
+                                                         (64, 60, 2, True, False), (33, 40, 3, False, False),
+                                                         (24, 30, 2, True, True)])
+def test_rnn_module_parity(B, Tmax, layers, ragged, space):
     from mvml_gat.smiles import RNNModule
     from oracle.smiles_ref import RNNModuleRef
     torch.manual_seed(B + layers)
-    vocab, batch = _batch(B, B * 7 + Tmax, Tmax, ragged)
+    vocab, batch = _batch(B, B * 7 + Tmax, Tmax, ragged, space)
+    if space:
+        assert any((row[:n] == 0).any() for row, n in zip(batch["smiles"], batch["seq_len"]))
     ref = RNNModuleRef(39, 128, 384, layers, 384, 0.5).double().eval()
     mod = RNNModule(vocab, 128, 384, layers, 384, 0.5).to(DEV).eval()
     mod.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})

@@ -6,9 +6,11 @@ of the bytes of wide (16 B/lane) coalesced reads, so hbm_read = 2 * FETCH_SIZE *
 WRITE_SIZE (KB) is exact for 16-B stores.  The aggregation kernels read their streams with
 16-B buffer loads; their small 4-B index / logit reads are uncalibrated (documented in
 DESIGN.md).  One entry-point launch = one launch of each of its kernels, so its traffic is the
-sum of the per-kernel averages.
+sum of the per-kernel averages.  The result is stored under the WORKLOAD key bench.py computes
+("<workload>/mols_per_step=<n>[/proj_bf16]"), so a bench line only ever reports traffic that was
+profiled on its own workload.
 
-    python tools/pmc_traffic.py FETCH_DIR WRITE_DIR [--out profiles/pmc_traffic.json]
+    python tools/pmc_traffic.py FETCH_DIR WRITE_DIR --workload KEY [--out profiles/pmc_traffic.json]
 """
 import argparse
 import csv
@@ -43,6 +45,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
+    ap.add_argument("--workload", required=True)
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     fetch = read_counter(a.fetch_dir, "FETCH_SIZE")
@@ -61,8 +64,14 @@ def main():
                       "hbm_bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024),
                       "correction": "read = 2 x FETCH_SIZE (gfx950 16-B/lane reads), write = WRITE_SIZE; "
                                     "averaged over both GAT layers"}
+    try:
+        with open(a.out) as f:
+            allw = json.load(f)
+    except (OSError, ValueError):
+        allw = {}
+    allw[a.workload] = out
     with open(a.out, "w") as f:
-        json.dump(out, f, indent=1)
+        json.dump(allw, f, indent=1)
     print(json.dumps(out, indent=1))
 
 
