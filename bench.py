@@ -55,11 +55,14 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["config3", "config5"], default="config3")
+    ap.add_argument("--workload", choices=["config3", "config5", "mvp"], default="config3",
+                    help="mvp = BASELINE config 4: the whole MVP model (SMILES BiLSTM + graph view + "
+                         "fingerprint MLP + fusion) DP training step on shards of the config-3 set")
     ap.add_argument("--total-mols", type=int, default=1_000_000,
                     help="config 3: size of the ONE global molecule set sharded over the ranks")
     ap.add_argument("--mols-per-step", type=int, default=65536,
-                    help="molecules per GPU per step (whole GraphNorm groups); config5 default 8192")
+                    help="molecules per GPU per step (whole GraphNorm groups); config5 / mvp "
+                         "default 8192")
     ap.add_argument("--group-size", type=int, default=64)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--view-only-steps", type=int, default=3,
@@ -212,9 +215,11 @@ def cpu_baseline(seconds, group_size, with_fusion):
 class Batch:
     """One step's resident inputs: the device-built graph + features, and the fusion head's
     other two view embeddings / labels (seeded by the batch's first global molecule index, so
-    they do not depend on how the set was sharded)."""
+    they do not depend on how the set was sharded).  mvp: the SMILES token batch (synthetic
+    characters, ~1.8 per atom like KEGG's 50 characters for 28 atoms) and 2513-bit
+    fingerprints (~10 % set) instead of the two fixed view embeddings."""
 
-    def __init__(self, sb, first_mol, group_size, dev, with_fusion):
+    def __init__(self, sb, first_mol, group_size, dev, with_fusion, mvp=False):
         self.g = sb.to_graph(group_size=group_size).to(dev)
         self.feats = self.g.ndata["h"]
         self.B, self.N, self.E = self.g.batch_size, self.g.num_nodes(), self.g.num_edges()
@@ -223,12 +228,29 @@ class Batch:
             self.smiles_x = torch.randn((self.B, 384), device=dev, generator=gen)
             self.fp_x = torch.randn((self.B, 384), device=dev, generator=gen)
             self.labels = (torch.rand((self.B, 11), device=dev, generator=gen) > 0.8).float()
+        if mvp:
+            rng = np.random.default_rng([first_mol, 77])
+            lens = np.clip(np.rint(1.8 * sb.num_nodes * rng.uniform(0.8, 1.2, self.B)), 5, 462).astype(np.int64)
+            T = int(lens.max())
+            tok = rng.integers(2, 39, size=(self.B, T)).astype(np.float32)
+            tok[np.arange(T)[None, :] >= lens[:, None]] = 0.0
+            self.smiles = {"smiles": torch.from_numpy(tok).to(dev), "seq_len": lens.tolist()}
+            self.fp = (torch.rand((self.B, 2513), device=dev, generator=gen) < 0.1).float()
 
 
 def build_batches(args, rank, world, dev, with_fusion):
     from mvml_gat import dist as mdist
     from mvml_gat import synth
     gs = args.group_size
+    if args.workload == "mvp":
+        gset = synth.Config3Set(args.total_mols, seed=args.seed)
+        g0, g1 = mdist.shard_groups(gset.group_costs(gs), world, rank)
+        lo, hi = g0 * gs, min(g1 * gs, args.total_mols)
+        per = args.mols_per_step if args.mols_per_step != 65536 else 8192
+        per = max(gs, per // gs * gs)
+        hi = min(hi, lo + 16 * per)  # at most 16 resident steps per rank
+        return ([Batch(gset.molecules(m, min(hi, m + per)), m, gs, dev, True, mvp=True)
+                 for m in range(lo, hi, per)], (lo, hi))
     if args.workload == "config3":
         gset = synth.Config3Set(args.total_mols, seed=args.seed)
         g0, g1 = mdist.shard_groups(gset.group_costs(gs), world, rank)
@@ -325,10 +347,20 @@ def run(args):
         f"({time.perf_counter() - t_gen:.1f}s)")
 
     torch.manual_seed(args.seed)
+    mvp = args.workload == "mvp"
     if args.dry_run:
         model = _PlumbingStandIn()
         fusion = None
         params = list(model.parameters())
+    elif mvp:
+        from mvml_gat.mvp import MVP
+        # main.py:85-87 with config.py defaults: hidden [192, 384], rnn 128 / 384 x 2, fp 512,
+        # 12 fusion heads, dropout 0.5
+        full = MVP(11, 74, [192, 384], 6, 3, 128, 384, 2, 512, 12, 0.5,
+                   proj_dtype=torch.bfloat16 if args.proj_bf16 else None).to(dev).train()
+        model, fusion = full.gnn, None
+        params = [p for n, p in full.named_parameters()
+                  if not (n.startswith("norm_layer.") or n.startswith("rnn.norm_layer."))]
     else:
         model = mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3,
                                    proj_dtype=torch.bfloat16 if args.proj_bf16 else None).to(dev).train()
@@ -339,6 +371,11 @@ def run(args):
 
     def step(b, fused=True):
         opt.zero_grad(set_to_none=False)
+        if mvp and fused:
+            mvml_gat.bce_with_logits(full(b.smiles, b.g, b.feats, b.fp), b.labels).backward()
+            reducer()
+            opt.step()
+            return
         out = model(b.g, b.feats)
         if args.dry_run:
             torch.nn.functional.binary_cross_entropy_with_logits(
@@ -476,7 +513,7 @@ def run(args):
         model.train()
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run and not mvp:
         cpu = cpu_baseline(args.cpu_seconds, args.group_size, with_fusion=True)
 
     if rank == 0:
@@ -487,6 +524,12 @@ def run(args):
                   f"{args.mols_per_step}-molecule steps per GPU; view + fusion: GNNModule (GAT "
                   "[192,384] x4 heads, Set2Set 6x3, GraphNorm, fc) -> MVFusion (12-head 3-token "
                   "attention, Conv2d, MLP) -> BCEWithLogits, fwd+bwd+Adam")
+        elif args.workload == "mvp":
+            wl = (f"BASELINE config 4: the whole MVP model (model.py:13-75; RNNModule BiLSTM 2x384 "
+                  f"over synthetic SMILES tokens, GNNModule, FPNModule 2513->512->384 over synthetic "
+                  f"fingerprints, fusion head) -> BCEWithLogits -> backward -> one flat all-reduce of "
+                  f"the {sum(p.numel() for p in params)} gradients -> Adam, on shards of the "
+                  f"{args.total_mols}-molecule config-3 set")
         else:
             wl = ("BASELINE config 5 (150-400-atom molecules with 1-4 hubs of in-degree 32-128, "
                   "per-rank sets): GNNModule -> MVFusion -> BCEWithLogits, fwd+bwd+Adam")

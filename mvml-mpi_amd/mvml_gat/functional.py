@@ -30,8 +30,9 @@ def _stream(dev):
     return _lib.stream_ptr(dev)
 
 
-# Diagnostics hook (tools/diag_golden.py): when a dict, GATLayerFunction.backward stores its
-# saved el/er, attention and el/er gradients into it.  None in normal use.
+# Diagnostics hook (tools/diag_golden.py, the parity tests' LeakyReLU-branch capture): when a
+# dict, GATLayerFunction.forward appends each layer's el/er to DEBUG_CAPTURE["elr_fwd"] and the
+# backward stores its saved el/er, attention and el/er gradients.  None in normal use.
 DEBUG_CAPTURE = None
 
 
@@ -127,6 +128,8 @@ class GATLayerFunction(torch.autograd.Function):
         call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
              ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(_c(bias)), float(slope), int(mode),
              ptr(out), ptr(attn), st)
+        if DEBUG_CAPTURE is not None:
+            DEBUG_CAPTURE.setdefault("elr_fwd", []).append(elr.detach().clone())
         ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr)
         ctx.Fin = Fin
         ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode, ctx.ldy = g, H, F, slope, mode, ldy

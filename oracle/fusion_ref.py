@@ -69,3 +69,24 @@ class FPNModuleRef(nn.Module):
 
     def forward(self, fp):
         return self.fc2(self.act_func(self.dropout(self.fc1(fp))))
+
+
+class MVPRef(MVFusionRef):
+    """model.py:13-75 restated: MVP = RNNModule + GNNModule + FPNModule views -> the fusion head
+    above, with the reference's state_dict keys (gnn.*, rnn.*, fp_mlp.*, fusion keys).
+    forward(smiles_batch, graph_dict, atom_feats, fp_t, branches=None) -> logits (B, C)."""
+
+    def __init__(self, num_classes=11, in_feats=74, hidden_feats=(192, 384), num_step_set2set=6,
+                 num_layer_set2set=3, rnn_embed_dim=128, blstm_dim=384, blstm_layers=2,
+                 fp_2_dim=512, num_heads=12, dropout=0.5):
+        from .gnn_ref import GNNModuleRef
+        from .smiles_ref import RNNModuleRef
+        hidden_feats = list(hidden_feats)
+        super().__init__(hidden_feats[-1], num_heads, num_classes, dropout)
+        self.gnn = GNNModuleRef(in_feats, hidden_feats, dropout, num_step_set2set, num_layer_set2set)
+        self.rnn = RNNModuleRef(39, rnn_embed_dim, blstm_dim, blstm_layers, hidden_feats[-1], dropout)
+        self.fp_mlp = FPNModuleRef(fp_2_dim, hidden_feats[-1], dropout)
+
+    def forward(self, smiles, graph, atom_feats, fp_t, branches=None):
+        return MVFusionRef.forward(self, self.rnn(smiles), self.gnn(graph, atom_feats, branches),
+                                   self.fp_mlp(fp_t))

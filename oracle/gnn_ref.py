@@ -49,8 +49,18 @@ def edge_softmax_ref(score, dst, num_nodes):
     return ex / ssum[dst]
 
 
+def leaky_relu_branch(x, slope, positive):
+    """LeakyReLU whose branch is GIVEN per element (positive: bool, same shape): equal to
+    leaky_relu(x) wherever sign(x) agrees with `positive`, and its gradient is 1 / slope by
+    `positive`.  Used by the parity tests to evaluate the float64 oracle on the SAME side of the
+    kink at 0 as the fp32 path under test: at |x| ~ 1e-8 the side is decided by fp32 rounding
+    of el + er, and the two one-sided derivatives differ by 0.8 (a subgradient choice, not an
+    error of either implementation)."""
+    return torch.where(positive, x, x * slope)
+
+
 def gatconv_ref(src, dst, X, fc_w, res_w, attn_l, attn_r, bias, num_heads, out_feats,
-                negative_slope=0.2, return_attention=False):
+                negative_slope=0.2, return_attention=False, branch=None):
     src = _as_long(src)
     dst = _as_long(dst)
     n = X.shape[0]
@@ -58,7 +68,10 @@ def gatconv_ref(src, dst, X, fc_w, res_w, attn_l, attn_r, bias, num_heads, out_f
     Z = (X @ fc_w.t()).view(n, H, Fo)
     el = (Z * attn_l).sum(-1)
     er = (Z * attn_r).sum(-1)
-    e = F.leaky_relu(el[src] + er[dst], negative_slope)
+    if branch is None:
+        e = F.leaky_relu(el[src] + er[dst], negative_slope)
+    else:
+        e = leaky_relu_branch(el[src] + er[dst], negative_slope, branch)
     a = edge_softmax_ref(e, dst, n)
     rst = torch.zeros((n, H, Fo), dtype=X.dtype).index_add(0, dst, a.unsqueeze(-1) * Z[src])
     rst = rst + (X @ res_w.t()).view(n, H, Fo)
@@ -68,24 +81,25 @@ def gatconv_ref(src, dst, X, fc_w, res_w, attn_l, attn_r, bias, num_heads, out_f
     return rst
 
 
-def gat_layer_ref(src, dst, X, p, num_heads, out_feats, agg_mode, activation):
+def gat_layer_ref(src, dst, X, p, num_heads, out_feats, agg_mode, activation, branch=None):
     """dgllife GATLayer.forward: gat_conv -> flatten(1) | mean(1) -> activation."""
     rst = gatconv_ref(src, dst, X, p["fc.weight"], p["res_fc.weight"], p["attn_l"],
-                      p["attn_r"], p["bias"], num_heads, out_feats)
+                      p["attn_r"], p["bias"], num_heads, out_feats, branch=branch)
     out = rst.flatten(1) if agg_mode == "flatten" else rst.mean(1)
     if activation is not None:
         out = activation(out)
     return out
 
 
-def gat_ref(src, dst, X, layer_params, hidden_feats, num_heads=None):
+def gat_ref(src, dst, X, layer_params, hidden_feats, num_heads=None, branches=None):
     L = len(hidden_feats)
     num_heads = num_heads or [4] * L
     h = X
     for i in range(L):
         last = i == L - 1
         h = gat_layer_ref(src, dst, h, layer_params[i], num_heads[i], hidden_feats[i],
-                          "mean" if last else "flatten", None if last else F.elu)
+                          "mean" if last else "flatten", None if last else F.elu,
+                          branch=None if branches is None else branches[i])
     return h
 
 
@@ -203,9 +217,10 @@ class GNNModuleRef(nn.Module):
                         "attn_l": c.attn_l, "attn_r": c.attn_r, "bias": c.bias})
         return out
 
-    def forward(self, graph, atom_feats):
+    def forward(self, graph, atom_feats, branches=None):
+        """branches: optional per-GAT-layer bool (E, H) LeakyReLU sides (leaky_relu_branch)."""
         node_x = gat_ref(graph["src"], graph["dst"], atom_feats, self.layer_params(),
-                         self.hidden_feats)
+                         self.hidden_feats, branches=branches)
         graph_x = set2set_ref(graph["node_offsets"], node_x, self.readout.lstm,
                               self.readout.n_iters)
         out = graphnorm_ref(graph_x, self.norm.weight, self.norm.bias, self.norm.mean_scale,
