@@ -80,6 +80,15 @@ __device__ __forceinline__ f32x16 mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b
   return acc;
 }
 
+// NP = 3: the split-bf16 product above; NP = 1: one bf16 MFMA (bf16 operands, fp32 accumulate).
+template <int NP>
+__device__ __forceinline__ f32x16 mfma_np(const bf16x8 (&a)[NP], const bf16x8 (&b)[NP], f32x16 acc) {
+  if constexpr (NP == 3)
+    return mfma_x3(a, b, acc);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
 constexpr int BM = 128, BN = 128, BKT = 32, kThreads = 256;
 constexpr int kTileFloats = 128 * BKT;  // one operand tile in LDS (16 KB)
 
@@ -263,7 +272,7 @@ struct ProjEpi {
 
 // Epilogue of a wave's FM x FN 32x32 accumulators (rows r0 + 32 i .., columns c0 + 32 j ..):
 // optional GAT logit partials, then bias / beta*C / ReLU, or the raw split-K slab.
-template <int EPI_LOGW, int FM = 2, int FN = 2>
+template <int EPI_LOGW, int FM = 2, int FN = 2, bool STORE_C = true>
 __device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[FM][FN], int64_t M, int64_t N,
                                               int64_t r0, int64_t c0, int lane,
                                               const float* __restrict__ bias, float beta, int act,
@@ -312,6 +321,7 @@ __device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[FM][FN], int64
         }
       }
   }
+  if constexpr (!STORE_C) return;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -783,8 +793,93 @@ struct XOp {
   }
 };
 
+// Epilogue of the 256x256 kernel through LDS: a wave's 128 x 64 accumulator block goes out in
+// four 32-row passes; each pass writes the 32x32 MFMA layout (lane = column, 16 rows per lane)
+// into a wave-private LDS tile and reads it back as whole-row float4s, so C (or the split-K
+// slab) is stored with 16-B row-contiguous stores instead of 4-B column scatters — the
+// epilogue of an output-bound GEMM (L2 forward: 13.5 GB of C) is store-issue-bound otherwise.
+// Rows / columns outside C and unaligned C fall back to guarded scalar stores per element.
+constexpr int kEpiLd = 68;  // floats per LDS row (64 + 4: the column writes hit distinct banks)
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], float* wl, int64_t M,
+                                                 int64_t N, int64_t r0, int64_t c0, int lane,
+                                                 const float* __restrict__ bias, float beta, int act,
+                                                 float* __restrict__ C, int64_t ldc,
+                                                 float* __restrict__ slab) {
+  const int li = lane & 31, lk = lane >> 5;
+  float* out = slab ? slab + (int64_t)blockIdx.y * M * N : C;
+  const int64_t ld = slab ? N : ldc;
+  const bool vec = (ld % 4 == 0) && (((uintptr_t)out & 15) == 0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i > 0) wave_sync_lds();  // the previous pass's reads are done
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        wl[((r & 3) + 8 * (r >> 2) + 4 * lk) * kEpiLd + 32 * j + li] = acc[i][j][r];
+    wave_sync_lds();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int idx = q * 64 + lane, rr = idx >> 4, c4 = (idx & 15) * 4;
+      const int64_t row = r0 + 32 * i + rr, col = c0 + c4;
+      if (row >= M || col >= N) continue;
+      float4 v = *reinterpret_cast<const float4*>(wl + rr * kEpiLd + c4);
+      float* cp = out + row * ld + col;
+      if (vec && col + 3 < N) {
+        if (!slab) {
+          if (bias) {
+            const float4 b = *reinterpret_cast<const float4*>(bias + col);
+            v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+          }
+          if (beta != 0.f) {
+            const float4 o = *reinterpret_cast<const float4*>(cp);
+            v.x += beta * o.x; v.y += beta * o.y; v.z += beta * o.z; v.w += beta * o.w;
+          }
+          if (act == 1) {
+            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+          }
+        }
+        *reinterpret_cast<float4*>(cp) = v;
+      } else {
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (col + u >= N) break;
+          float x = e[u];
+          if (!slab) {
+            if (bias) x += bias[col + u];
+            if (beta != 0.f) x += beta * cp[u];
+            if (act == 1) x = fmaxf(x, 0.f);
+          }
+          cp[u] = x;
+        }
+      }
+    }
+  }
+}
+
 #ifndef MVML_X3W_WAVES
 #define MVML_X3W_WAVES 2
+#endif
+#ifndef MVML_X3W_LDSEPI
+#define MVML_X3W_LDSEPI 1
+#endif
+#ifndef MVML_X3W_SGB
+#define MVML_X3W_SGB 0
+#endif
+#ifndef MVML_X3W_PF2
+#define MVML_X3W_PF2 0
+#endif
+#ifndef MVML_X3W_STAGGER
+#define MVML_X3W_STAGGER 0
+#endif
+#ifndef MVML_X3W_SGB_V
+#define MVML_X3W_SGB_V 3
 #endif
 // FAST (host-checked: both operands 16-B aligned rows, K-major row counts % 4 == 0): whole
 // stages by unguarded loads from clamped rows, the K tail as one guarded stage; !FAST: every
@@ -800,9 +895,22 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   using OA = XOp<AK, NP>;
   using OB = XOp<BKM, NP>;
   constexpr int kStage = OA::kBytes + OB::kBytes;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kStage];
+  // double-buffered stages; the LDS epilogue reuses the space (8 waves x 32 rows x kEpiLd)
+  constexpr int kLdsBytes = 2 * kStage > 8 * 32 * kEpiLd * 4 ? 2 * kStage : 8 * 32 * kEpiLd * 4;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const int64_t tiles_n = ceil_div(N, XBN);
-  const int64_t tile = xcd_block(blockIdx.x, gridDim.x);
+  // Tile loop (persistent when the host launches fewer workgroups than tiles): XCD x = the
+  // blocks b with b % 8 == x walks ONE contiguous range of tiles (the xcd_block partition),
+  // its cnt blocks interleaved, so the tiles in flight on an XCD share A row panels in its L2.
+  // A workgroup's next tile starts while its last tile's C stores drain.
+  const int64_t n_tiles = ceil_div(M, XBM) * tiles_n;
+  const unsigned xq = n_tiles / 8, xr = n_tiles % 8, bx = blockIdx.x % 8;
+  const int64_t t_beg = (bx < xr) ? bx * (xq + 1) : xr * (xq + 1) + (bx - xr) * xq;
+  const int64_t t_end = t_beg + xq + (bx < xr ? 1 : 0);
+  const unsigned bq = gridDim.x / 8, br = gridDim.x % 8;
+  const int64_t t_step = bq + (bx < br ? 1 : 0);  // blocks on this XCD
+  for (int64_t tile = t_beg + blockIdx.x / 8; tile < t_end; tile += t_step) {
+  if (tile != t_beg + blockIdx.x / 8) __syncthreads();  // the previous tile's epilogue LDS reads
   const int64_t m0 = (tile / tiles_n) * XBM, n0 = (tile % tiles_n) * XBN;
   const int64_t kbeg = (int64_t)blockIdx.y * k_split;
   const int64_t kend = min(K, kbeg + k_split);
@@ -830,13 +938,15 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     for (int i = 0; i < 2; ++i) {
       va[i] = *reinterpret_cast<const float4*>(pa[i]);
       vb[i] = *reinterpret_cast<const float4*>(pb[i]);
+#ifndef MVML_X3W_NOMEM  // ablation: re-read the first stage forever (cache hits, wrong results)
       pa[i] += sa_step;
       pb[i] += sb_step;
+#endif
     }
   };
   // fast load of a stage that may be the K tail: addresses clamped to k < kend (host: kend %
   // 4 == 0), A's values at k >= kend zeroed, so B's clamped (finite) values add nothing
-  auto load_masked = [&](int64_t t) {
+  auto load_masked_into = [&](int64_t t, float4 (&xa)[2], float4 (&xb)[2]) {
     const int64_t k0 = kbeg + t * XBK;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -858,12 +968,13 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
         qb = pb[i] + (min(kb_, kend - 1) - kb_) * ldb;
       }
       const float4 a = *reinterpret_cast<const float4*>(qa);
-      va[i] = ka < kend ? a : make_float4(0.f, 0.f, 0.f, 0.f);
-      vb[i] = *reinterpret_cast<const float4*>(qb);
+      xa[i] = ka < kend ? a : make_float4(0.f, 0.f, 0.f, 0.f);
+      xb[i] = *reinterpret_cast<const float4*>(qb);
       pa[i] += sa_step;
       pb[i] += sb_step;
     }
   };
+  auto load_masked = [&](int64_t t) { load_masked_into(t, va, vb); };
   auto load_guarded = [&](int64_t t) {
     const int64_t k0 = kbeg + t * XBK;
     const bool kin = k0 + XBK <= kend;
@@ -888,10 +999,61 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int p = 0; p < NP; ++p) fb[j][p] = OB::frag(sb, p, wn * 64 + 32 * j, lane);
-    if constexpr (decltype(STAGE)::value) stage((t + 1) & 1);
-    if constexpr (decltype(LOAD)::value == 1) load_fast();
-    if constexpr (decltype(LOAD)::value == 2) load_guarded(t + 2);
-    if constexpr (decltype(LOAD)::value == 3) load_masked(t + 2);
+#if MVML_X3W_SGB
+    if constexpr (decltype(STAGE)::value && NP == 3) {
+      // Interleaved schedule: every fragment of stage t is read from LDS FIRST (so the split's
+      // LDS writes into the other buffer, which the compiler cannot prove disjoint, do not pin
+      // the reads behind them), then the split of stage t+1 (VALU + LDS writes) and the global
+      // loads of stage t+2 ride in the MFMA stream of stage t (an MFMA leaves 24 of its 32 issue
+      // cycles to other instructions), instead of running as a VALU-only phase in front of it
+      // while the SIMD's matrix pipe idles (both waves of a SIMD reach that phase together).
+      bf16x8 fa[4][NP];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) fa[i][p] = OA::frag(sa, p, wm * 128 + 32 * i, lane);
+      stage((t + 1) & 1);
+      if constexpr (decltype(LOAD)::value == 1) load_fast();
+      if constexpr (decltype(LOAD)::value == 2) load_guarded(t + 2);
+      if constexpr (decltype(LOAD)::value == 3) load_masked(t + 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_np<NP>(fa[i], fb[j], acc[i][j]);
+      // 0x8 MFMA, 0x2 VALU, 0x100 DS read, 0x200 DS write, 0x20 VMEM read
+      __builtin_amdgcn_sched_group_barrier(0x100, 6 * NP, 0);  // fb + fa[0] + fa[1]
+#pragma unroll
+      for (int k = 0; k < 24; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x2, MVML_X3W_SGB_V, 0);
+        if (k % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        if (k == 2) __builtin_amdgcn_sched_group_barrier(0x100, 2 * NP, 0);  // fa[2] + fa[3]
+      }
+      __builtin_amdgcn_sched_group_barrier(0x20, 4, 0);  // next stage's global loads
+#pragma unroll
+      for (int k = 0; k < 24; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x2, 1, 0);
+      }
+      __syncthreads();
+      return;
+    }
+#endif
+    auto stage_and_load = [&]() {
+      if constexpr (decltype(STAGE)::value) stage((t + 1) & 1);
+      if constexpr (decltype(LOAD)::value == 1) load_fast();
+      if constexpr (decltype(LOAD)::value == 2) load_guarded(t + 2);
+      if constexpr (decltype(LOAD)::value == 3) load_masked(t + 2);
+    };
+#if MVML_X3W_STAGGER
+    // Stagger: waves 0-3 (one per SIMD) split stage t+1 BEFORE their MFMAs of stage t, waves
+    // 4-7 (the SIMD partners) AFTER theirs, so each SIMD's matrix pipe runs one wave's MFMAs
+    // while its partner does the VALU split, instead of both splitting together behind the
+    // barrier.  The branches are wave-uniform and leave the accumulators alone.
+    if (wid < 4) stage_and_load();
+#else
+    stage_and_load();
+#endif
     if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -907,6 +1069,9 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       }
     }
     if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(0);
+#if MVML_X3W_STAGGER
+    if (wid >= 4) stage_and_load();
+#endif
     __syncthreads();
   };
   using T_ = std::true_type;
@@ -914,6 +1079,78 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   using L0 = std::integral_constant<int, 0>;
   using L1 = std::integral_constant<int, 1>;
   using L2 = std::integral_constant<int, 2>;
+#if MVML_X3W_PF2
+  if constexpr (FAST) {
+    // Prefetch distance 2: tile k's fp32 values live in register set k % 2 from their load (in
+    // body k - 3) to their split (in body k - 1), so a global load has two whole stages to land
+    // instead of one (the loads of a stage are issued right after the split that frees the set).
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    using LM = std::integral_constant<int, 3>;
+    float4 ra[2][2], rb[2][2];
+    auto ldf = [&](auto SET) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        ra[decltype(SET)::value][i] = *reinterpret_cast<const float4*>(pa[i]);
+        rb[decltype(SET)::value][i] = *reinterpret_cast<const float4*>(pb[i]);
+        pa[i] += sa_step;
+        pb[i] += sb_step;
+      }
+    };
+    auto ldm = [&](auto SET, int64_t k) {  // tile k, the K tail: as load_masked
+      load_masked_into(k, ra[decltype(SET)::value], rb[decltype(SET)::value]);
+    };
+    auto stg = [&](auto SET, int buf) {
+      OA::split_store(lds + buf * kStage, tid, ra[decltype(SET)::value]);
+      OB::split_store(lds + buf * kStage + OA::kBytes, tid, rb[decltype(SET)::value]);
+    };
+    auto body2 = [&](int64_t t, auto SET, auto STAGE, auto LOAD) {
+      const uint8_t* sa = lds + (t & 1) * kStage;
+      const uint8_t* sb = sa + OA::kBytes;
+      bf16x8 fb[2][NP];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) fb[j][p] = OB::frag(sb, p, wn * 64 + 32 * j, lane);
+      if constexpr (decltype(STAGE)::value) stg(SET, (int)((t + 1) & 1));
+      if constexpr (decltype(LOAD)::value == 1) ldf(SET);
+      if constexpr (decltype(LOAD)::value == 3) ldm(SET, t + 3);
+      if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bf16x8 fa[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) fa[p] = OA::frag(sa, p, wm * 128 + 32 * i, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_np<NP>(fa, fb[j], acc[i][j]);
+      }
+      if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(0);
+      __syncthreads();
+    };
+    if (ntiles >= 1) { if (ntiles == 1) ldm(S0{}, 0); else ldf(S0{}); }
+    if (ntiles >= 2) { if (ntiles == 2) ldm(S1{}, 1); else ldf(S1{}); }
+    if (ntiles >= 1) stg(S0{}, 0);
+    if (ntiles >= 3) { if (ntiles == 3) ldm(S0{}, 2); else ldf(S0{}); }
+    __syncthreads();
+    int64_t t = 0;
+    for (; t + 5 < ntiles; t += 2) {  // body t loads tile t + 3 (a whole stage: t + 4 < ntiles)
+      body2(t, S1{}, T_{}, L1{});
+      body2(t + 1, S0{}, T_{}, L1{});
+    }
+    for (; t < ntiles; ++t) {  // at most 5 bodies: runtime parity / stage / load kind
+      const bool st = t + 1 < ntiles;
+      const int lk = (t + 4 < ntiles) ? 1 : (t + 4 == ntiles ? 3 : 0);
+      auto tail = [&](auto SET) {
+        if (!st) body2(t, SET, F_{}, L0{});
+        else if (lk == 1) body2(t, SET, T_{}, L1{});
+        else if (lk == 3) body2(t, SET, T_{}, LM{});
+        else body2(t, SET, T_{}, L0{});
+      };
+      if ((t & 1) == 0) tail(S1{});
+      else tail(S0{});
+    }
+  } else
+#endif
   if constexpr (FAST) {
     using LM = std::integral_constant<int, 3>;
     if (ntiles >= 3) {
@@ -964,10 +1201,21 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[i][j]));
-  return;
+  continue;
 #endif
+#if MVML_X3W_LDSEPI
+  // the projection's logit partials straight from the accumulators, then C through LDS (every
+  // K loop ends with a workgroup barrier, so the staging buffers are free)
+  if constexpr (EPI_LOGW >= 0)
+    tile_epilogue<EPI_LOGW, 4, 2, false>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta,
+                                         act, C, ldc, slab, epi);
+  epilogue_lds_256(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
+                   n0 + wn * 64, lane, bias, beta, act, C, ldc, slab);
+#else
   tile_epilogue<EPI_LOGW, 4, 2>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta, act, C,
                                 ldc, slab, epi);
+#endif
+  }  // tile loop
 }
 
 // Host check for gemm_x3w_kernel<FAST = true>: aligned rows; a K-major operand's row count
@@ -1047,6 +1295,19 @@ int choose_splits(int64_t M, int64_t N, int64_t K) {  // the larger of the two p
 }
 
 int64_t k_chunk(int64_t K, int S) { return ceil_div(ceil_div(K, S), BKT) * BKT; }
+
+// Workgroups of a 256x256 launch: one per tile by default; MVML_X3W_PERSIST = P > 0 caps a
+// launch without split-K at P workgroups that loop over their XCD's tiles (measured neutral at
+// P = 256 / 512 on the step's shapes: the dispatcher already overlaps one tile's C stores with
+// the next tile's start).
+unsigned x3w_grid_x(int64_t tiles, int S) {
+  static const int persist = [] {
+    const char* e = getenv("MVML_X3W_PERSIST");
+    return e ? atoi(e) : 0;
+  }();
+  if (S > 1 || persist <= 0 || tiles <= persist) return (unsigned)tiles;
+  return (unsigned)persist;
+}
 
 // Column sums, stage 1: each thread owns one column of a row chunk; eight independent partial
 // sums keep eight loads in flight per lane (the loop is otherwise latency-bound).
@@ -1157,7 +1418,7 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   MVML_REQUIRE(tiles < (int64_t(1) << 31), "gemm: too many tiles");
   const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0);
   const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0);
-  dim3 grid((unsigned)tiles, (unsigned)S);
+  dim3 grid(plan.wide || bf ? x3w_grid_x(tiles, S) : (unsigned)tiles, (unsigned)S);
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
   do {                                                                                          \
     if (bf && x3w_fast(AKV, BKV, M, N, K, av, bv))                                              \
@@ -1212,7 +1473,7 @@ int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int
   MVML_REQUIRE(cols <= N && (logw >= 2 && logw <= 5), "gat_proj_fwd: bad partial width");
   const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0);
   const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0);
-  dim3 grid((unsigned)tiles, 1);
+  dim3 grid(wide ? x3w_grid_x(tiles, 1) : (unsigned)tiles, 1);
 #define MVML_PROJ(LW)                                                                          \
   do {                                                                                         \
     if (bf && x3w_fast(false, false, M, N, K, av, bv))                                         \
