@@ -420,6 +420,134 @@ conv3_bwd_kernel(int64_t B, int W, int64_t per_block, const float* __restrict__ 
   }
 }
 
+// ---- conv3, register-blocked (round 2) ---------------------------------------------------
+// Forward: thread per output column x holds its 108 inputs in[c][dy][x + dx] in registers and
+// walks the 12 output channels with the weights as wave-uniform (scalar) loads — 1296 FMAs per
+// thread with no LDS traffic in the loop (the LDS-broadcast weight reads of conv3_fwd_kernel
+// made it LDS-bound).  Same summation order per output as conv3_fwd_kernel ((c, dy) outer, dx
+// inner).
+__global__ void __launch_bounds__(kConvThreads, 2)
+conv3_fwd2_kernel(int64_t B, int W, const float* __restrict__ in, const float* __restrict__ wgt,
+                  const float* __restrict__ bias, float* __restrict__ out) {
+  __shared__ float s_in[kConvC * kConvH * kConvLd + 4];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int Wo = W - 2;
+  conv_stage(s_in, in + b * (int64_t)(kConvC * kConvH * W), kConvC * kConvH, W, tid);
+  __syncthreads();
+  const int x = tid;
+  if (x >= Wo) return;
+  float a[kConvC * kConvH * 3];
+#pragma unroll
+  for (int cd = 0; cd < kConvC * kConvH; ++cd)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) a[cd * 3 + dx] = s_in[cd * kConvLd + x + dx];
+  float* dst = out + b * (int64_t)(kConvO * Wo) + x;
+#pragma unroll
+  for (int o = 0; o < kConvO; ++o) {
+    const float* w = wgt + o * (kConvC * kConvH * 3);
+    float acc = bias[o];
+#pragma unroll
+    for (int j = 0; j < kConvC * kConvH * 3; ++j) acc = fmaf(w[j], a[j], acc);
+    dst[o * Wo] = fmaxf(acc, 0.f);
+  }
+}
+
+// Backward, one workgroup (6 waves) per range of molecules:
+//  * input gradient: thread per column x' holds g_pre[o][x' - dx] (36 values) in registers and
+//    accumulates the 36 (c, dy) outputs with scalar-loaded weights (1296 FMAs, no LDS in the
+//    loop);
+//  * weight / bias gradient on the f32 matrix cores: per molecule gW[o][n] += sum_x g_pre[o][x]
+//    im2col[x][n] with n = (c, dy, dx) < 108 and n = 108 a column of ones (the bias), as
+//    v_mfma_f32_16x16x4_f32 over 7 column tiles of 16; wave w owns the x-steps [64 w, 64 w + 64)
+//    of every molecule, the fragments are per-lane LDS reads of the staged rows.  The six waves'
+//    16 x 112 partial tiles are summed in fixed order at the end (deterministic, no atomics).
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+constexpr int kConvWaves = kConvThreads / 64;  // 6
+constexpr int kConvNT = 7;                     // 16-column tiles of n (108 weights + bias)
+__global__ void __launch_bounds__(kConvThreads, 2)
+conv3_bwd2_kernel(int64_t B, int W, int64_t per_block, const float* __restrict__ in,
+                  const float* __restrict__ wgt, const float* __restrict__ out,
+                  const float* __restrict__ g_out, float* __restrict__ g_in,
+                  float* __restrict__ part) {
+  __shared__ float s_in[kConvC * kConvH * kConvLd + 8];
+  __shared__ float s_g[kConvO * kConvLd];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int Wo = W - 2;
+  if (tid < 8) s_in[kConvC * kConvH * kConvLd + tid] = 0.f;  // reads past the last row: finite
+  f32x4_t acc[kConvNT];
+#pragma unroll
+  for (int j = 0; j < kConvNT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // this lane's fixed fragment coordinates: A row o = lane & 15; B column n = 16 j + (lane & 15)
+  const int lo = lane & 15, lk = lane >> 4;
+  int boff[kConvNT];  // LDS offset of im2col(x = 0, n) (row (c, dy), column dx), or -1 / -2
+#pragma unroll
+  for (int j = 0; j < kConvNT; ++j) {
+    const int n = 16 * j + lo;
+    boff[j] = n < 108 ? (n / 3) * kConvLd + n % 3 : (n == 108 ? -1 : -2);
+  }
+  const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(B, b0 + per_block);
+  for (int64_t b = b0; b < b1; ++b) {
+    __syncthreads();  // previous molecule's LDS reads done
+    conv_stage(s_in, in + b * (int64_t)(kConvC * kConvH * W), kConvC * kConvH, W, tid);
+    const float* go = g_out + b * (int64_t)(kConvO * Wo);
+    const float* oo = out + b * (int64_t)(kConvO * Wo);
+    for (int i = tid; i < kConvO * kConvLd; i += kConvThreads) {
+      const int o = i / kConvLd, x = i % kConvLd;
+      s_g[i] = (x < Wo && oo[o * Wo + x] > 0.f) ? go[o * Wo + x] : 0.f;  // zero-padded
+    }
+    __syncthreads();
+    if (tid < W) {  // input gradient
+      const int xp = tid;
+      float g[kConvO][3];
+#pragma unroll
+      for (int o = 0; o < kConvO; ++o)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) g[o][dx] = xp - dx >= 0 ? s_g[o * kConvLd + xp - dx] : 0.f;
+      float acc_in[kConvC * kConvH];
+#pragma unroll
+      for (int i = 0; i < kConvC * kConvH; ++i) acc_in[i] = 0.f;
+#pragma unroll
+      for (int o = 0; o < kConvO; ++o) {  // (o, dx) order as conv3_bwd_kernel
+        const float* w = wgt + o * (kConvC * kConvH * 3);
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int cd = 0; cd < kConvC * kConvH; ++cd)
+            acc_in[cd] = fmaf(w[cd * 3 + dx], g[o][dx], acc_in[cd]);
+      }
+      float* dst = g_in + b * (int64_t)(kConvC * kConvH * W) + xp;
+#pragma unroll
+      for (int cd = 0; cd < kConvC * kConvH; ++cd) dst[cd * W] = acc_in[cd];
+    }
+    // weight / bias gradient: x-steps of 4 columns, wave w takes steps [16 w, 16 w + 16)
+    for (int ks = 16 * wid; ks < 16 * wid + 16; ++ks) {
+      const int x = 4 * ks + lk;
+      const float av = lo < kConvO ? s_g[lo * kConvLd + x] : 0.f;  // 0 past Wo (padding)
+#pragma unroll
+      for (int j = 0; j < kConvNT; ++j) {
+        const float bv = boff[j] >= 0 ? s_in[boff[j] + x] : (boff[j] == -1 ? 1.f : 0.f);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
+      }
+    }
+  }
+  // fixed-order reduction of the six waves' 16 x 112 tiles: C[i][n], i = 4 (lane >> 4) + r
+  __syncthreads();
+  float* red = s_in;  // 6 x 16 x 112 floats = 42 KB <= s_in
+#pragma unroll
+  for (int j = 0; j < kConvNT; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(wid * 16 + 4 * lk + r) * 112 + 16 * j + lo] = acc[j][r];
+  __syncthreads();
+  for (int i = tid; i < kConvO * 109; i += kConvThreads) {
+    const int o = i / 109, n = i % 109;
+    float s = 0.f;
+    for (int w = 0; w < kConvWaves; ++w) s += red[(w * 16 + o) * 112 + n];
+    if (n < 108) part[(int64_t)blockIdx.x * kConvPart + o * 108 + n] = s;
+    else part[(int64_t)blockIdx.x * kConvPart + 2 * kConvWg + o] = s;
+  }
+}
+
 // Fixed-order sum of the per-workgroup partials: out[i] = sum_blk sum_j<nsub
 // part[blk * stride + j * sub_stride + i].
 __global__ void partial_sum_kernel(int nblk, int count, int stride, int nsub, int sub_stride,
@@ -511,7 +639,11 @@ extern "C" int mvml_conv3_fwd(int64_t B, int C, int O, int W, const float* in, c
   clear_error();
   MVML_REQUIRE(C == kConvC && O == kConvO && W >= 3 && W <= 384, "conv3_fwd: C = O = 12, 3 <= W <= 384");
   if (B == 0) return MVML_OK;
+#ifndef MVML_CONV_V1
+  conv3_fwd2_kernel<<<(unsigned)B, kConvThreads, 0, as_stream(stream)>>>(B, W, in, weight, bias, out);
+#else
   conv3_fwd_kernel<<<(unsigned)B, kConvThreads, 0, as_stream(stream)>>>(B, W, in, weight, bias, out);
+#endif
   return check_launch("conv3_fwd_kernel");
 }
 
@@ -536,13 +668,19 @@ extern "C" int mvml_conv3_bwd(int64_t B, int C, int O, int W, const float* in, c
   const int64_t nblk = conv3_blocks(B), per = ceil_div(B, nblk);
   const int64_t used = ceil_div(B, per);
   float* part = static_cast<float*>(workspace);
+#ifndef MVML_CONV_V1
+  conv3_bwd2_kernel<<<(unsigned)used, kConvThreads, 0, st>>>(B, W, per, in, weight, out, g_out,
+                                                             g_in, part);
+  const int nsub = 1;  // partial row: the 1296 weight sums, then (at 2 * 1296) the 12 bias sums
+#else
   conv3_bwd_kernel<<<(unsigned)used, kConvThreads, 0, st>>>(B, W, per, in, weight, out, g_out,
                                                             g_in, part);
+  const int nsub = 2;  // partial row: two column halves of the 1296 weight sums, then the biases
+#endif
   int rc = check_launch("conv3_bwd_kernel");
   if (rc) return rc;
-  // partial row: two column halves of the 1296 weight sums, then the 12 bias sums
   partial_sum_kernel<<<(unsigned)ceil_div(kConvWg, 256), 256, 0, st>>>(
-      (int)used, kConvWg, kConvPart, 2, kConvWg, part, g_weight);
+      (int)used, kConvWg, kConvPart, nsub, kConvWg, part, g_weight);
   rc = check_launch("partial_sum_kernel(w)");
   if (rc) return rc;
   partial_sum_kernel<<<1, 64, 0, st>>>((int)used, kConvO, kConvPart, 1, 0, part + 2 * kConvWg, g_bias);
