@@ -70,7 +70,9 @@ int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local,
  * The PLAN (int32[mvml_node_group_plan_size(N)]) holds, for G groups:
  *   [0, G]          group_start (group_start[G] = N)
  *   [G+1, 2G+1)     kind: bit 0 = forward LDS kernel (<= 128 atoms, <= 512 in-edges, every
- *                   in-degree <= 5), bit 1 = backward LDS kernel (<= 128 atoms, <= 512 edges)
+ *                   in-degree <= 5), bit 1 = backward LDS kernel (<= 128 atoms, <= 512 edges),
+ *                   bit 2 = big LDS window (<= 512 atoms, <= 2432 in-edges, any in-degree:
+ *                   the fallback-list groups the big-window kernels take, H <= 4)
  *   2G+1, 2G+2      number of non-empty groups without bit 0 / bit 1
  *   [2G+3, 3G+3)    those groups for the forward fallback kernel (any order)
  *   [3G+3, 4G+3)    those groups for the backward fallback kernels
@@ -295,20 +297,42 @@ int mvml_bce_logits(int64_t n, const float* z, const float* y, float* loss_terms
  * batch_first) over pack_padded_sequence(enforce_sorted=False) + the last-step selection of
  * model.py:131-133).  Packed layout: rows t*B + i, batch sorted by descending length
  * (perm[i] = original index of sorted row i, pos = perm^-1), tokens int32 [B, ldtok] in the
- * original order, lens int32 [B] >= 1.  The recurrence is mvml_gemm_* + mvml_lstm_cell_*.
+ * original order, lens int32 [B] >= 1.  batch_sizes (HOST int32 [T], non-increasing) is the
+ * number of sequences alive per step.
  *   gather_rows: out[t*B+i, :] = t < lens[perm[i]] ? table[tokens[perm[i], t], :] : 0
  *                (layer 0's x W_ih^T as rows of the [vocab, 4H] table E W_ih^T; cols % 4 == 0)
  *   token_grad:  out[v, :] = sum of g[t*B+i, :] over live positions holding token v
- *                (fixed order, deterministic; replaces Embedding / W_ih_l0 backward)
+ *                (fixed order, deterministic; replaces Embedding / W_ih_l0 backward; vocab <= 64;
+ *                workspace of mvml_bilstm_token_grad_workspace bytes)
  *   select_last: dir 0: fea[b] = [out[(lens[b]-1)*B + pos[b], 0:H] | out[pos[b], H:2H]];
  *                dir 1: the transpose, fea -> out rows (out must be zeroed by the caller).
+ *   seq_fwd:     one layer's recurrence, both directions (torch.nn.LSTM bidirectional over the
+ *                packed batch, model.py:121-129): per step t (direction 0) / T-1-t (direction 1)
+ *                pre = gates_d[t] + h_prev W_hh_d^T + b_ih_d + b_hh_d, the LSTM cell, h into
+ *                out[t*B+i, d*H : (d+1)*H], c into c_d, (i, f, g, o) into act_d.  gates_d =
+ *                x W_ih_d^T [T*B, 4H]; out / c_d must be zeroed by the caller (dead rows are
+ *                read as the zero state); H % 16 == 0.
+ *   seq_bwd:     its backward: g_out [T*B, 2H] (dL/d out); gg_d [T*B, 4H] (zeroed by the
+ *                caller) receives dL/d pre; w_hhT_d = W_hh_d^T [H, 4H]; carry [2, B, H] zeroed
+ *                scratch (the dL/dc chain).  dW / db / dx follow from gg_d by GEMMs.
  * ------------------------------------------------------------------------------------- */
 int mvml_bilstm_gather_rows(int64_t T, int64_t B, int64_t cols, const float* table,
                             const int32_t* tokens, int64_t ldtok, const int32_t* lens,
                             const int32_t* perm, float* out, void* stream);
+int64_t mvml_bilstm_token_grad_workspace(int64_t T, int64_t B, int64_t cols, int vocab);
 int mvml_bilstm_token_grad(int64_t T, int64_t B, int64_t cols, const float* g,
                            const int32_t* tokens, int64_t ldtok, const int32_t* lens,
-                           const int32_t* perm, int vocab, float* out, void* stream);
+                           const int32_t* perm, int vocab, float* out, void* workspace,
+                           size_t workspace_bytes, void* stream);
+int mvml_bilstm_seq_fwd(int64_t T, int64_t B, int H, const int32_t* batch_sizes,
+                        const float* gates0, const float* gates1, const float* w_hh0,
+                        const float* w_hh1, const float* b_ih0, const float* b_hh0,
+                        const float* b_ih1, const float* b_hh1, float* out, float* c0, float* c1,
+                        float* act0, float* act1, void* stream);
+int mvml_bilstm_seq_bwd(int64_t T, int64_t B, int H, const int32_t* batch_sizes,
+                        const float* w_hhT0, const float* w_hhT1, const float* act0,
+                        const float* act1, const float* c0, const float* c1, const float* g_out,
+                        float* gg0, float* gg1, float* carry, void* stream);
 int mvml_bilstm_select_last(int64_t B, int64_t H, const int32_t* lens, const int32_t* pos,
                             float* out, float* fea, int dir, void* stream);
 

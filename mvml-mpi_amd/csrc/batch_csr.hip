@@ -256,7 +256,9 @@ __global__ void node_groups_kernel(int64_t B, int64_t N, const int64_t* __restri
 
 // Group kinds (one wave per group): bit 0 = the forward LDS kernel takes the group (<=
 // kPlanWinAtoms atoms, <= kPlanEdgeCap in-edges, in-degree <= kPlanDegCap everywhere), bit 1 =
-// the backward LDS kernel does (atom and edge caps only).  Non-empty groups without a bit are
+// the backward LDS kernel does (atom and edge caps only), bit 2 = the group fits the big LDS
+// window (<= kPlanBigAtoms atoms, <= kPlanBigEdgeCap in-edges, any in-degree): groups on a
+// fallback list with bit 2 are taken by the big-window kernels.  Non-empty groups without a bit are
 // appended to that direction's fallback list (order irrelevant: groups are independent).
 __global__ void node_group_kind_kernel(int64_t G, const int32_t* __restrict__ rowptr,
                                        int32_t* __restrict__ plan) {
@@ -264,7 +266,6 @@ __global__ void node_group_kind_kernel(int64_t G, const int32_t* __restrict__ ro
   const int lane = threadIdx.x & 63;
   if (g >= G) return;
   int32_t* kind = plan + G + 1;
-  int32_t* count = plan + 2 * G + 1;
   const int a0 = plan[g], a1 = plan[g + 1];
   int dmax = 0;
   for (int v = a0 + lane; v < a1; v += 64) dmax = max(dmax, rowptr[v + 1] - rowptr[v]);
@@ -274,11 +275,52 @@ __global__ void node_group_kind_kernel(int64_t G, const int32_t* __restrict__ ro
   int k = 0;
   if (a1 > a0) {
     const bool fits = a1 - a0 <= kPlanWinAtoms && rowptr[a1] - rowptr[a0] <= kPlanEdgeCap;
-    k = (fits && dmax <= kPlanDegCap ? 1 : 0) | (fits ? 2 : 0);
-    if (!(k & 1)) plan[2 * G + 3 + atomicAdd(&count[0], 1)] = (int32_t)g;
-    if (!(k & 2)) plan[3 * G + 3 + atomicAdd(&count[1], 1)] = (int32_t)g;
+    const bool big = a1 - a0 <= kPlanBigAtoms && rowptr[a1] - rowptr[a0] <= kPlanBigEdgeCap;
+    k = (fits && dmax <= kPlanDegCap ? 1 : 0) | (fits ? 2 : 0) | (big ? 4 : 0);
   }
   kind[g] = k;
+}
+
+// The fallback lists in group order (one workgroup: a running exclusive scan over chunks of
+// 1024 groups), so the fallback kernels can hand each XCD a contiguous run of molecules.
+__global__ void __launch_bounds__(1024) node_group_lists_kernel(int64_t G, int32_t* __restrict__ plan) {
+  const int32_t* start = plan;
+  const int32_t* kind = plan + G + 1;
+  int32_t* count = plan + 2 * G + 1;
+  __shared__ int s_off[2][1024];
+  __shared__ int s_base[2];
+  const int tid = threadIdx.x;
+  if (tid < 2) s_base[tid] = 0;
+  __syncthreads();
+  for (int64_t c0 = 0; c0 < G; c0 += 1024) {
+    const int64_t g = c0 + tid;
+    int f[2] = {0, 0};
+    if (g < G && start[g + 1] > start[g]) {
+      f[0] = !(kind[g] & 1);
+      f[1] = !(kind[g] & 2);
+    }
+    // inclusive Hillis-Steele scan of both flags
+    s_off[0][tid] = f[0];
+    s_off[1][tid] = f[1];
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+      int v0 = 0, v1 = 0;
+      if (tid >= d) { v0 = s_off[0][tid - d]; v1 = s_off[1][tid - d]; }
+      __syncthreads();
+      s_off[0][tid] += v0;
+      s_off[1][tid] += v1;
+      __syncthreads();
+    }
+    if (f[0]) plan[2 * G + 3 + s_base[0] + s_off[0][tid] - 1] = (int32_t)g;
+    if (f[1]) plan[3 * G + 3 + s_base[1] + s_off[1][tid] - 1] = (int32_t)g;
+    __syncthreads();
+    if (tid == 0) {
+      s_base[0] += s_off[0][1023];
+      s_base[1] += s_off[1][1023];
+    }
+    __syncthreads();
+  }
+  if (tid < 2) count[tid] = s_base[tid];
 }
 
 }  // namespace
@@ -354,11 +396,14 @@ extern "C" int mvml_build_node_groups(int64_t num_graphs, int64_t num_nodes,
   if (G == 0) return MVML_OK;
   MVML_REQUIRE(num_graphs > 0 && node_offsets && in_rowptr && plan, "build_node_groups: null input");
   hipStream_t st = as_stream(stream);
-  (void)hipMemsetAsync(plan + 2 * G + 1, 0, 2 * sizeof(int32_t), st);
+  // fallback counts and lists: node_group_lists_kernel
   node_groups_kernel<<<(unsigned)ceil_div(G + 1, 256), 256, 0, st>>>(num_graphs, num_nodes,
                                                                     node_offsets, G, plan);
   int rc = check_launch("node_groups_kernel");
   if (rc) return rc;
   node_group_kind_kernel<<<(unsigned)ceil_div(G, 4), 256, 0, st>>>(G, in_rowptr, plan);
-  return check_launch("node_group_kind_kernel");
+  rc = check_launch("node_group_kind_kernel");
+  if (rc) return rc;
+  node_group_lists_kernel<<<1, 1024, 0, st>>>(G, plan);
+  return check_launch("node_group_lists_kernel");
 }

@@ -21,6 +21,10 @@ constexpr int kNodeGroupAtoms = 64;
 constexpr int kPlanWinAtoms = 128;  // atoms per group
 constexpr int kPlanEdgeCap = 512;   // in-edges per group
 constexpr int kPlanDegCap = 5;      // forward: in-degree of every atom
+// Big LDS window (kind bit 2): node groups of up to kPlanBigAtoms atoms / kPlanBigEdgeCap
+// in-edges (a 150-400-atom molecule with hubs, BASELINE config 5) staged 16 columns at a time.
+constexpr int kPlanBigAtoms = 512;
+constexpr int kPlanBigEdgeCap = 2432;
 // Plan layout (int32, G = mvml_node_group_count(N)): [0, G] group starts | [G+1, 2G+1) kinds |
 // 2G+1, 2G+2: forward / backward fallback counts | [2G+3, 3G+3) forward fallback groups |
 // [3G+3, 4G+3) backward fallback groups.

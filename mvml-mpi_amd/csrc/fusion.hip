@@ -475,6 +475,10 @@ conv3_bwd2_kernel(int64_t B, int W, int64_t per_block, const float* __restrict__
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int Wo = W - 2;
   if (tid < 8) s_in[kConvC * kConvH * kConvLd + tid] = 0.f;  // reads past the last row: finite
+  // the pad columns [W, kConvLd) of every row are read by the weight-gradient MFMA steps past
+  // Wo (against a zero g_out): they must be finite (0 x NaN of stale LDS would be NaN)
+  for (int i = tid; i < kConvC * kConvH * (kConvLd - W); i += kConvThreads)
+    s_in[(i / (kConvLd - W)) * kConvLd + W + i % (kConvLd - W)] = 0.f;
   f32x4_t acc[kConvNT];
 #pragma unroll
   for (int j = 0; j < kConvNT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};

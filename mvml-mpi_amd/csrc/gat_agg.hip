@@ -245,6 +245,95 @@ constexpr int kEC = kPlanDegCap;      // in-edges per destination with cached of
 constexpr int kAggThreads = 512;
 constexpr int kHubDeg = 16;           // gather kernel: in-degree above which the hub pass runs
 constexpr int kHubCols = 1024;        // gather kernel: float4 columns of the hub pass (H*F <= 4096)
+// Fallback-list entry of block b in a grid of nb >= count blocks: XCD x (the blocks b % 8 == x)
+// walks ONE contiguous range of the list (the lists are in group order), so the molecules in
+// flight on an XCD are neighbours and their rows share its L2; -1 for idle blocks.
+__device__ __forceinline__ int list_block(unsigned b, unsigned nb, int count) {
+  const unsigned x = b % 8, i = b / 8;
+  const unsigned q = count / 8, r = count % 8;
+  const unsigned beg = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  const unsigned len = q + (x < r ? 1 : 0);
+  return i < len ? (int)(beg + i) : -1;
+}
+constexpr int kBigThreads = 512;      // big-window kernels: 128 rows per pass (16-column chunks),
+                                      // up to 4 passes; 2 waves per SIMD leave 256 registers
+constexpr int kBigBlocks = 256;       // ... one workgroup per CU walking the fallback list
+// Hub segments of a big window: the edges of a row past its kEC cached ones are cut into
+// segments of kSegI in-edges (kSegO out-edges), each one a task for any lane group of the chunk
+// sweep (a partial sum / edge dots), so a hub's 32-128 edges cost one LDS round trip per chunk
+// instead of a serial walk on its own lanes.  Rows whose segments would pass the table keep the
+// serial walk (correct for any graph; the tables cover config 5's 1-4 hubs per molecule).  The
+// backward's out-edge partials are short of LDS: there rows of out-degree <= kSegMinO (a hub's
+// partners: one or two edges past kEC, staged in s_oxe) walk theirs too.
+constexpr int kSegI = 8, kSegO = 16, kSegMinO = 12;
+constexpr int kSegCapI = 256, kSegCapO = 48;
+constexpr int kOXCap = 640;  // backward: out-edges past kEC staged in LDS (dst row << 16 | slot)
+
+// Block-wide exclusive prefix sum of one int per thread (NT / 64 waves); *total = the sum.
+template <int NT>
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wsum, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_wsum[w] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) {
+    const int t = s_wsum[i];
+    base += i < w ? t : 0;
+    tot += t;
+  }
+  *total = tot;
+  return base + x - v;
+}
+
+// The segment table of rows d = threadIdx.x < nr (edge range [eb, eb + deg) of the window's
+// CSR; rows of degree <= MIN get none): seg[t] = row << 16 | first edge << 4 | (count - 1);
+// *rs = first segment | count << 12 for this thread's row (0: no segments, or segments past
+// CAP: the owner walks them).  Returns the table length.  Ends with a barrier (the table is
+// visible to the block).
+template <int NT, int SEG, int CAP, int MIN = kEC>
+__device__ __forceinline__ int hub_segments(int nr, int eb, int deg, uint32_t* s_seg, int* rs,
+                                            int* s_wsum) {
+  static_assert(CAP < 4096 && SEG <= 16, "segment packing");
+  const int d = threadIdx.x;
+  int n = (d < nr && deg > MIN) ? (deg - kEC + SEG - 1) / SEG : 0;
+  int total;
+  const int sb = block_excl_scan<NT>(n, s_wsum, &total);
+  if (sb + n > CAP) n = 0;  // rows are in order: every later row is past the table too
+  for (int j = 0; j < n; ++j) {
+    const int e = eb + kEC + SEG * j;
+    s_seg[sb + j] = (uint32_t)d << 16 | (uint32_t)e << 4 | (uint32_t)(min(SEG, eb + deg - e) - 1);
+  }
+  *rs = n ? (sb | n << 12) : 0;
+  // the table length: the end of the last row that fits (a block max over the rows)
+  const int end = n ? sb + n : 0;
+  int m = end;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+  __syncthreads();  // s_wsum reads of the scan are done
+  if ((threadIdx.x & 63) == 0) s_wsum[threadIdx.x >> 6] = m;
+  __syncthreads();
+  int len = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) len = max(len, s_wsum[i]);
+  __syncthreads();  // s_wsum reusable
+  return len;
+}
+
+// The big-window kernels stage 16-column chunks (F % 16 == 0) and their LDS holds the per-edge
+// attention of up to kPlanBigEdgeCap edges for H <= 4 heads.  On config 5 (8192 molecules) they
+// take fwd / bwd L1 6.4 / 13.5 ms and L2 7.0 / 21.7 ms against the per-atom fallbacks' 7.0 /
+// 15.9 and 10.2 / 29.7 ms.  MVML_BIG_WINDOW=0 routes those groups to the fallbacks (tests).
+inline bool use_big_window(int H, int F) {
+  const char* e = getenv("MVML_BIG_WINDOW");
+  return !(e && atoi(e) == 0) && H <= 4 && F % 16 == 0;
+}
 
 #ifndef MVML_LDS_WAVES
 #define MVML_LDS_WAVES 4
@@ -258,16 +347,20 @@ constexpr int kHubCols = 1024;        // gather kernel: float4 columns of the hu
 // resource's range check; chunks past the end use an out-of-range offset), so the loop is
 // straight-line and the compiler's vmcnt waits are exact; stores of rows past the group are
 // skipped (an out-of-range store is not free).
-template <int H, int CW, int MODE, int NT, int NPA>
-__device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)], const float* s_att,
+template <int H, int CW, int MODE, int NT, int NPA, int WIN = kWinL, int ECAP = kECap, bool BIG = false>
+__device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], const float* s_att,
                                                const int32_t* __restrict__ rowptr,
                                                const int32_t* __restrict__ in_src,
                                                __amdgpu_buffer_rsrc_t rY, uint32_t rowb,
                                                __amdgpu_buffer_rsrc_t rO, int a0, int nr, int e0,
-                                               int F, const float* __restrict__ bias) {
+                                               int F, const float* __restrict__ bias,
+                                               const uint16_t* s_srcs = nullptr,
+                                               const uint32_t* s_seg = nullptr,
+                                               const int* s_rs = nullptr, float4* s_part = nullptr,
+                                               int nseg = 0) {
   constexpr int LPD = CW / 4;                        // lanes per destination atom
   constexpr int DPP = NT / LPD;                      // destinations per pass
-  constexpr int RING = MVML_FWD_RING;
+  constexpr int RING = NPA >= 3 ? 1 : MVML_FWD_RING;  // 3-4 pass groups: registers
   const int tid = threadIdx.x;
   const int ds = tid / LPD, q = tid % LPD;
   const int HF = H * F;
@@ -302,6 +395,15 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)],
     rb[p] = (uint32_t)d * rowb;            // d >= nr: past the resource, reads 0
     ob[p] = 4u * (uint32_t)(d * ocols);
   }
+  // BIG: this thread's rows' hub segments (first | count << 12); the edges of a row with none
+  // past kEC are walked by the row's own lanes (hend)
+  int sbn[NPA], hend[NPA];
+#pragma unroll
+  for (int p = 0; p < NPA; ++p) {
+    sbn[p] = 0;
+    if constexpr (BIG) sbn[p] = live[p] ? s_rs[ds + DPP * p] : 0;
+    hend[p] = sbn[p] ? kEC : ad[p];
+  }
   // chunk k -> global column of this lane
   auto col_of = [&](int k) {
     return (MODE == 1 ? (k % H) * F + (k / H) * CW : (k / nfc) * F + (k % nfc) * CW) + 4 * q;
@@ -324,20 +426,23 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)],
 #pragma unroll
     for (int j = 0; j < NPA; ++j) zbuf[buf][(ds + DPP * j) * LPD + q] = src[j];
   };
-  float4 ring[RING][NPA], rres[NPA], rnx[NPA], tot[NPA];
+  // BIG emits after the barrier: chunk k's residual is loaded at the top of iteration k (no
+  // second residual set in registers)
+  float4 ring[RING][NPA], rres[NPA], rnx[BIG ? 1 : NPA], tot[NPA];
   {
     float4 z0[NPA];
     load_rows(0, z0);
 #pragma unroll
     for (int i = 0; i < RING; ++i) load_rows(1 + i, ring[i]);
-    load_res(0, rres);
+    if constexpr (!BIG) load_res(0, rres);
     store_rows(0, z0);
   }
   __syncthreads();  // chunk 0 and s_att staged
   for (int k = 0; k < nch; ++k) {
     const int h = MODE == 1 ? k % H : k / nfc;
     const int col = col_of(k);
-    load_res(k + 1, rnx);
+    if constexpr (BIG) load_res(k, rres);
+    else load_res(k + 1, rnx);
     const float4 b4 = ld4(bias + col);
     const float4* zl = zbuf[k & 1];
     float4 acc[NPA];
@@ -347,9 +452,49 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)],
     for (int p = 0; p < NPA; ++p)
 #pragma unroll
       for (int i = 0; i < kEC; ++i)
-        acc[p] = fma4(s_att[(i < ad[p] ? ab[p] + i * H : kECap * H) + h], zl[so[p][i]], acc[p]);
+        acc[p] = fma4(s_att[(i < ad[p] ? ab[p] + i * H : ECAP * H) + h], zl[so[p][i]], acc[p]);
+    if constexpr (BIG) {
+      // rows past the segment table: their in-edges past kEC on their own lanes (edge order)
 #pragma unroll
-    for (int p = 0; p < NPA; ++p) {
+      for (int p = 0; p < NPA; ++p)
+        for (int i = kEC; i < hend[p]; i += 4) {
+          float av[4];
+          float4 zv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bool ok = i + j < ad[p];
+            const int e = ab[p] / H + (ok ? i + j : i);
+            av[j] = ok ? s_att[e * H + h] : 0.f;
+            zv[j] = zl[(int)s_srcs[e] * LPD + q];
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (i + j < ad[p]) acc[p] = fma4(av[j], zv[j], acc[p]);
+        }
+      // hub segments: any lane group, kSegI independent LDS reads each; partials to s_part[k & 1]
+      float4* sp = s_part + (k & 1) * (kSegCapI * LPD);
+      for (int t = ds; t < nseg; t += DPP) {
+        const uint32_t sg = s_seg[t];
+        const int eb = (int)((sg >> 4) & 0xFFFu), c = (int)(sg & 15u) + 1;
+        float4 part = f4(0.f);
+#pragma unroll
+        for (int j0 = 0; j0 < kSegI; j0 += 4) {  // two batches of 4 reads (registers)
+          float av[4];
+          float4 zv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bool ok = j0 + j < c;
+            const int e = eb + (ok ? j0 + j : 0);
+            av[j] = ok ? s_att[e * H + h] : 0.f;
+            zv[j] = zl[(int)s_srcs[e] * LPD + q];
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) part = fma4(av[j], zv[j], part);
+        }
+        sp[t * LPD + q] = part;
+      }
+    }
+    auto emit = [&](int p) {
       if (MODE == 1) {
         const float4 t = add4(acc[p], b4);
         tot[p] = (h == 0) ? t : add4(tot[p], t);
@@ -365,6 +510,10 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)],
         if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
         buf_st4(rO, ob[p] + 4u * (uint32_t)col, o);  // rows past the group: dropped
       }
+    };
+    if constexpr (!BIG) {
+#pragma unroll
+      for (int p = 0; p < NPA; ++p) emit(p);
     }
     // stage chunk k+1 into the other buffer (read by nobody until the barrier) and rotate
     store_rows((k + 1) & 1, ring[0]);
@@ -373,16 +522,29 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[kWinL * (CW / 4)],
 #pragma unroll
       for (int j = 0; j < NPA; ++j) ring[i][j] = ring[i + 1][j];
     load_rows(k + 1 + RING, ring[RING - 1]);
-#pragma unroll
-    for (int j = 0; j < NPA; ++j) rres[j] = rnx[j];
     __syncthreads();
+    if constexpr (BIG) {  // the segment partials of chunk k are complete: add them in order, emit
+      const float4* sp = s_part + (k & 1) * (kSegCapI * LPD);
+#pragma unroll
+      for (int p = 0; p < NPA; ++p) {
+        const int n = sbn[p] >> 12;
+        for (int j = 0; j < n; ++j) acc[p] = add4(acc[p], sp[((sbn[p] & 0xFFF) + j) * LPD + q]);
+        emit(p);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NPA; ++j)
+      if constexpr (!BIG) rres[j] = rnx[j];
   }
 }
 
 // NT = 16 * CW threads: 64 destinations per pass; groups of <= 64 atoms (most of them: the
 // target is kNodeGroupAtoms) run one pass, larger ones two (kWinL = 128 atoms).  16 waves per
 // CU either way (2 x 512 threads for CW = 32, 1 x 1024 for CW = 64).
-template <int H, int CW, int MODE, int NT>
+// BIG (kind bit 2): the big-window variant for the groups on the forward fallback list (config
+// 5's 150-400-atom molecules with hubs): 16-column chunks so that 512 rows fit LDS, in-degree
+// unbounded (the hub loop above), one workgroup per CU walking the list.
+template <int H, int CW, int MODE, int NT, int WIN = kWinL, int ECAP = kECap, bool BIG = false>
 __global__ void __launch_bounds__(NT, MVML_LDS_WAVES)
 gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                        const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
@@ -390,26 +552,54 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
                        float* __restrict__ out) {
   constexpr int LPD = CW / 4;
   constexpr int DPP = NT / LPD;
-  static_assert(2 * DPP == kWinL, "two passes must tile the LDS rows exactly");
-  __shared__ float4 zbuf[2][kWinL * LPD];
-  __shared__ float s_att[(kECap + 1) * H];  // + H zeros: the attention of a missing edge
+  constexpr int NPM = WIN / DPP;  // passes over a full window
+  static_assert(NPM * DPP == WIN && (NPM == 2 || NPM == 4), "the passes must tile the LDS rows exactly");
+  __shared__ float4 zbuf[2][WIN * LPD];
+  __shared__ float s_att[(ECAP + 1) * H];  // + H zeros: the attention of a missing edge
+  // BIG: in-edge sources (window rows), the hub segment table, per-row segments, the
+  // double-buffered segment partials and the scan's wave sums
+  __shared__ uint16_t s_srcs[BIG ? ECAP : 1];
+  __shared__ uint32_t s_seg[BIG ? kSegCapI : 1];
+  __shared__ int s_rs[BIG ? WIN : 1];
+  __shared__ float4 s_part[BIG ? 2 * kSegCapI * LPD : 1];
+  __shared__ int s_wsum[BIG ? NT / 64 : 1];
   const int tid = threadIdx.x;
   const GroupPlan gp(plan, G);
-  if (!(gp.kind[blockIdx.x] & 1)) return;
-  const int a0 = gp.start[blockIdx.x], a1 = gp.start[blockIdx.x + 1];
+  const int nlist = BIG ? gp.count[0] : (int)blockIdx.x + 1;
+  for (int li = blockIdx.x; li < nlist; li += BIG ? gridDim.x : 1) {
+  const int g = BIG ? gp.fwd_list[li] : li;
+  if (BIG) __syncthreads();  // the previous group's LDS reads are done
+  if (!(gp.kind[g] & (BIG ? 4 : 1))) continue;
+  const int a0 = gp.start[g], a1 = gp.start[g + 1];
   const int nr = a1 - a0;
   const int ocols = MODE == 1 ? F : H * F;
   const int e0 = rowptr[a0];
   const int ne = rowptr[a1] - e0;
   for (int i = tid; i < ne * H; i += NT) s_att[i] = attn[(int64_t)e0 * H + i];
-  if (tid < H) s_att[kECap * H + tid] = 0.f;
+  if (tid < H) s_att[ECAP * H + tid] = 0.f;
+  int nseg = 0;
+  if constexpr (BIG) {
+    static_assert(NT >= WIN, "one row per thread for the segment scan");
+    for (int i = tid; i < ne; i += NT) s_srcs[i] = (uint16_t)(in_src[e0 + i] - a0);
+    const int eb = tid < nr ? rowptr[a0 + tid] - e0 : 0;
+    const int deg = tid < nr ? rowptr[a0 + tid + 1] - e0 - eb : 0;
+    int rs;
+    nseg = hub_segments<NT, kSegI, kSegCapI>(nr, eb, deg, s_seg, &rs, s_wsum);
+    if (tid < nr) s_rs[tid] = rs;
+    __syncthreads();
+  }
   const uint32_t rowb = (uint32_t)ldy * 4u;
   const __amdgpu_buffer_rsrc_t rY = make_rsrc(Y + (int64_t)a0 * ldy, (uint32_t)nr * rowb);
   const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)a0 * ocols, (uint32_t)(nr * ocols) * 4u);
   if (nr <= DPP)
-    fwd_lds_chunks<H, CW, MODE, NT, 1>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias);
+    fwd_lds_chunks<H, CW, MODE, NT, 1, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg);
+  else if (NPM == 2 || nr <= 2 * DPP)
+    fwd_lds_chunks<H, CW, MODE, NT, 2, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg);
+  else if (nr <= 3 * DPP)
+    fwd_lds_chunks<H, CW, MODE, NT, (NPM > 2 ? 3 : 2), WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg);
   else
-    fwd_lds_chunks<H, CW, MODE, NT, 2>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias);
+    fwd_lds_chunks<H, CW, MODE, NT, NPM, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg);
+  }
 }
 
 template <int H, int CW, int MODE>
@@ -417,7 +607,7 @@ __global__ void __launch_bounds__(kAggThreads, 4)  // 2 workgroups (16 waves) pe
 gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                    const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
                    int F, const float* __restrict__ bias, const float* __restrict__ attn,
-                   float* __restrict__ out) {
+                   float* __restrict__ out, int skip_big) {
   constexpr int LPD = CW / 4;                        // lanes per destination atom
   constexpr int DPP = kAggThreads / LPD;             // destinations per pass
   constexpr int NP = (kWin + DPP - 1) / DPP;         // passes over a full window
@@ -425,8 +615,10 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
   const int ds = tid / LPD, q = tid % LPD;
   const int HF = H * F;
   const GroupPlan gp(plan, G);
-  if ((int)blockIdx.x >= gp.count[0]) return;
-  const int g = gp.fwd_list[blockIdx.x];
+  const int li = list_block(blockIdx.x, gridDim.x, gp.count[0]);
+  if (li < 0) return;
+  const int g = gp.fwd_list[li];
+  if (skip_big && (gp.kind[g] & 4)) return;  // the big-window kernel takes it
   const int a0 = gp.start[g], a1 = gp.start[g + 1];
   const int nfc = F / CW;     // column chunks per head
   const int nch = H * nfc;
@@ -625,19 +817,19 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
 // r*LPD + (c ^ bwd_sw<LPD>(r)): 128-B rows (LPD = 8) are XOR-swizzled so whole-row reads of
 // different atoms spread over the banks; 256-B rows (LPD = 16) already span all 64 banks.
 template <int LPD>
-__device__ __forceinline__ int bwd_sw(int r) { return LPD == 8 ? (r >> 1) & 7 : 0; }
+__device__ __forceinline__ int bwd_sw(int r) { return LPD == 8 ? (r >> 1) & 7 : 0; }  // 4, 16: none
 
 // DPP move within a row of 16 lanes (bound_ctrl: sources outside the row read 0).
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
-// Sum over each aligned group of LPD (8 or 16) lanes; valid in the group's last four lanes.
+// Sum over each aligned group of LPD (4, 8 or 16) lanes; valid in the group's last four lanes.
 template <int LPD>
 __device__ __forceinline__ float grp_sum_hi(float v) {
   v += dppf<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dppf<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dppf<0x114>(v);  // row_shr:4
+  if (LPD >= 8) v += dppf<0x114>(v);  // row_shr:4
   if (LPD == 16) v += dppf<0x118>(v);  // row_shr:8
   return v;
 }
@@ -654,14 +846,23 @@ __device__ __forceinline__ float grp_sum_hi(float v) {
 // its slice of g_rst[d], a DPP octet sum finishes the dot, and one lane per edge adds it to
 // s_ga (zeroed by the caller; every (edge, head) has exactly one writer).  That reads each
 // source row slice once per in-edge: half the LDS bytes of an edge-per-thread dot.
-template <int H, int MODE, int NPA, int CW>
+// BIG: the out-CSR (s_odst / s_oslot) is read from global memory (g_odst / g_oslot, group
+// edge base e0, first atom a0) instead of LDS, which the big window needs for its rows.
+template <int H, int MODE, int NPA, int CW, int NT = 16 * CW, int WIN = kWinL, int ECAP = kECap,
+          bool BIG = false>
 __device__ __forceinline__ void bwd_lds_chunks(
     float4* zs, float4* gs, const float* s_att, const int* s_odst, const int* s_oslot,
-    const int* s_orp, const int* s_rp, const int* s_src, float* s_ga,
+    const int* s_orp, const int* s_rp, const uint16_t* s_src, float* s_ga,
     __amdgpu_buffer_rsrc_t rY, int ldyi, __amdgpu_buffer_rsrc_t rGo, __amdgpu_buffer_rsrc_t rO,
-    __amdgpu_buffer_rsrc_t rG, int ldgi, int nr, int F) {
+    __amdgpu_buffer_rsrc_t rG, int ldgi, int nr, int F, const int32_t* __restrict__ g_odst = nullptr,
+    const int32_t* __restrict__ g_oslot = nullptr, int e0 = 0, int a0 = 0,
+    const uint32_t* s_segI = nullptr, int nsegI = 0, const uint32_t* s_segO = nullptr,
+    int nsegO = 0, const int* s_rs = nullptr, float4* s_part = nullptr,
+    const uint32_t* s_oxe = nullptr, const uint16_t* s_oxb = nullptr) {
   static_assert(kEC == 5, "in-edge writer lanes assume 5 cached in-edges");
-  constexpr int LPD = CW / 4, NT = 16 * CW, DPP = NT / LPD;
+  constexpr int LPD = CW / 4, DPP = NT / LPD;
+  auto odst = [&](int o) -> int { if constexpr (BIG) return g_odst[e0 + o] - a0; else return s_odst[o]; };
+  auto oslot = [&](int o) -> int { if constexpr (BIG) return g_oslot[e0 + o] - e0; else return s_oslot[o]; };
   const int tid = threadIdx.x, ds = tid / LPD, q = tid % LPD;
   const int HF = H * F, nfc = F / CW, nch = H * nfc;
   const int ocols = MODE == 1 ? F : HF;
@@ -679,7 +880,7 @@ __device__ __forceinline__ void bwd_lds_chunks(
   // first kEC out-edges of this octet's source atoms in registers (a missing edge reads the
   // atom's own row with a zero attention), so a chunk's gathers are independent LDS reads;
   // more out-edges (hubs) loop.
-  static_assert(kWinL * LPD <= 65536 && (kECap + 1) * H <= 65536, "16-bit slots");
+  static_assert(WIN * LPD <= 65536 && (ECAP + 1) * H <= 65536, "16-bit slots");
   uint32_t gsl[NPA][kEC];
   int ob[NPA], oend[NPA];
 #pragma unroll
@@ -691,15 +892,27 @@ __device__ __forceinline__ void bwd_lds_chunks(
 #pragma unroll
     for (int i = 0; i < kEC; ++i) {
       const bool ok = ob[p] + i < oend[p];
-      const int rr = ok ? s_odst[ob[p] + i] : r;
+      const int rr = ok ? odst(ob[p] + i) : r;
       gsl[p][i] = (uint32_t)(rr * LPD + (q ^ bwd_sw<LPD>(rr))) |
-                  ((uint32_t)(ok ? s_oslot[ob[p] + i] * H : kECap * H) << 16);
+                  ((uint32_t)(ok ? oslot(ob[p] + i) * H : ECAP * H) << 16);
     }
   }
   // destination role: Z row slots of the first kEC in-edges (own row when missing; the dot is
   // then discarded), the in-edge base and in-degree
   uint32_t zsl[NPA][kEC];
   int ieb[NPA], ideg[NPA];
+  // BIG: hub segments of this octet's rows — in-edges past kEC (segmented rows: none walked
+  // here, bit 31) and out-edges past kEC (first | count << 12; their partials are added below)
+  int rsg[NPA], oxb[NPA];
+#pragma unroll
+  for (int p = 0; p < NPA; ++p) {
+    rsg[p] = 0;
+    oxb[p] = 0xFFFF;
+    if constexpr (BIG) {
+      rsg[p] = live[p] ? s_rs[ds + DPP * p] : 0;
+      oxb[p] = live[p] ? (int)s_oxb[ds + DPP * p] : 0xFFFF;
+    }
+  }
 #pragma unroll
   for (int p = 0; p < NPA; ++p) {
     const int d = ds + DPP * p;
@@ -779,13 +992,54 @@ __device__ __forceinline__ void bwd_lds_chunks(
         if (i0 < ideg[p]) s_ga[(ieb[p] + i0) * H + h] += v;
         if (i0 == 0 && ideg[p] > 4) s_ga[(ieb[p] + 4) * H + h] += t[4];
       }
-      for (int i = kEC; i < ideg[p]; ++i) {  // hubs (octet-uniform trip count)
+      for (int i = kEC; i < (rsg[p] < 0 ? kEC : ideg[p]); ++i) {  // hubs (octet-uniform trip count)
         const int sr = s_src[ieb[p] + i];
         const float v = grp_sum_hi<LPD>(dot4(zs[sr * LPD + (q ^ bwd_sw<LPD>(sr))], gd));
         if (q == LPD - 4) s_ga[(ieb[p] + i) * H + h] += v;
       }
     }
+    if constexpr (BIG) {  // hub in-edge segments: edge dots straight into s_ga (one writer each)
+      for (int t = ds; t < nsegI; t += DPP) {
+        const uint32_t sg = s_segI[t];
+        const int d = (int)(sg >> 16), eb = (int)((sg >> 4) & 0xFFFu), c = (int)(sg & 15u) + 1;
+        const float4 gd = gs[d * LPD + (q ^ bwd_sw<LPD>(d))];
+        float v[kSegI];
+#pragma unroll
+        for (int j = 0; j < kSegI; ++j) {
+          const int sr = s_src[eb + (j < c ? j : 0)];
+          v[j] = grp_sum_hi<LPD>(dot4(zs[sr * LPD + (q ^ bwd_sw<LPD>(sr))], gd));
+        }
+        if (q >= LPD - 4) {  // lane i0 of the last four writes edges i0, i0 + 4
+          const int i0 = q - (LPD - 4);
+#pragma unroll
+          for (int j = 0; j < kSegI; ++j)
+            if (j % 4 == i0 && j < c) s_ga[(eb + j) * H + h] += v[j];
+        }
+      }
+    }
 #endif
+    if constexpr (BIG) {  // hub out-edge segments: partial dZ sums to s_part
+      for (int t = ds; t < nsegO; t += DPP) {
+        const uint32_t sg = s_segO[t];
+        const int c = (int)(sg & 15u) + 1;
+        const uint32_t* oe = s_oxe + ((sg >> 4) & 0xFFFu);
+        float4 part = f4(0.f);
+        for (int j0 = 0; j0 < c; j0 += 4) {  // batches of 4 edges (registers)
+          int od[4], sl[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t x = oe[j0 + j < c ? j0 + j : 0];
+            od[j] = (int)(x >> 16);
+            sl[j] = (int)(x & 0xFFFFu);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            part = fma4(j0 + j < c ? s_att[sl[j] * H + h] : 0.f,
+                        gs[od[j] * LPD + (q ^ bwd_sw<LPD>(od[j]))], part);
+        }
+        s_part[t * LPD + q] = part;
+      }
+    }
     float4 acc[NPA];  // dZ_agg of the source atoms over their out-edges
 #pragma unroll
     for (int p = 0; p < NPA; ++p) {
@@ -794,11 +1048,28 @@ __device__ __forceinline__ void bwd_lds_chunks(
 #pragma unroll
       for (int i = 0; i < kEC; ++i)
         acc[p] = fma4(s_att[(gsl[p][i] >> 16) + h], gs[gsl[p][i] & 0xFFFFu], acc[p]);
-      for (int o = ob[p] + kEC; o < oend[p]; ++o)
-        acc[p] = fma4(s_att[s_oslot[o] * H + h], gs[s_odst[o] * LPD + (q ^ bwd_sw<LPD>(s_odst[o]))], acc[p]);
+      for (int o = ob[p] + kEC; o < ((rsg[p] & 0xFFFFFF) ? ob[p] + kEC : oend[p]); ++o) {
+        int od, sl;
+        if (BIG && oxb[p] != 0xFFFF) {  // staged (hub partners: one or two edges past kEC)
+          const uint32_t x = s_oxe[oxb[p] + o - ob[p] - kEC];
+          od = (int)(x >> 16);
+          sl = (int)(x & 0xFFFFu);
+        } else {
+          od = odst(o);
+          sl = oslot(o);
+        }
+        acc[p] = fma4(s_att[sl * H + h], gs[od * LPD + (q ^ bwd_sw<LPD>(od))], acc[p]);
+      }
 #endif
     }
     __syncthreads();
+    if constexpr (BIG) {  // this chunk's out-edge segment partials, in order
+#pragma unroll
+      for (int p = 0; p < NPA; ++p) {
+        const int n = (rsg[p] >> 12) & 0xFFF, sb = rsg[p] & 0xFFF;
+        for (int j = 0; j < n; ++j) acc[p] = add4(acc[p], s_part[(sb + j) * LPD + q]);
+      }
+    }
     stage(k + 1, ring[0]);
 #pragma unroll
     for (int i = 0; i + 1 < RB; ++i) ring[i] = ring[i + 1];
@@ -813,8 +1084,12 @@ __device__ __forceinline__ void bwd_lds_chunks(
 // One workgroup of 512 threads per node group (2 per CU): the group's CSR, out-CSR and
 // attention are staged in LDS, the column chunks stream through bwd_lds_chunks (one pass for
 // groups of <= 64 atoms, two up to kWinL), then the softmax backward runs in LDS.
-template <int H, int MODE, int CW>
-__global__ void __launch_bounds__(16 * CW, MVML_BWD_WAVES)
+// BIG (kind bit 2): the big-window variant for the groups on the backward fallback list: 16-column
+// chunks, 1024 threads (two passes of 256 rows), out-CSR and logits read from global memory
+// (LDS holds the rows, the attention, the edge gradients and the in-CSR), one workgroup per CU
+// walking the list.
+template <int H, int MODE, int CW, int NT = 16 * CW, int WIN = kWinL, int ECAP = kECap, bool BIG = false>
+__global__ void __launch_bounds__(NT, MVML_BWD_WAVES)
 gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                        const int32_t* __restrict__ in_src, const int32_t* __restrict__ out_rowptr,
                        const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
@@ -822,18 +1097,34 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
                        const float* __restrict__ attn, const float* __restrict__ out,
                        const float* __restrict__ g_out, float slope, float* __restrict__ gY,
                        int64_t ldgy, int C) {
-  constexpr int NT = 16 * CW, LPD = CW / 4;
-  static_assert(NT / LPD * 2 == kWinL, "two passes of 64 rows");
-  __shared__ float4 zs[kWinL * LPD];
-  __shared__ float4 gs[kWinL * LPD];
-  __shared__ float s_att[(kECap + 1) * H];  // + H zeros: the attention of a missing edge
-  __shared__ float s_ga[kECap * H];
-  __shared__ int s_src[kECap], s_odst[kECap], s_oslot[kECap];
-  __shared__ int s_rp[kWinL + 1], s_orp[kWinL + 1];
-  __shared__ float s_elr[kWinL * 2 * H];
+  constexpr int LPD = CW / 4;
+  constexpr int DPP = NT / LPD;
+  constexpr int NPM = WIN / DPP;  // passes over a full window
+  static_assert(NPM * DPP == WIN && (NPM == 2 || NPM == 4), "the passes must tile the LDS rows exactly");
+  __shared__ float4 zs[WIN * LPD];
+  __shared__ float4 gs[WIN * LPD];
+  __shared__ float s_att[(ECAP + 1) * H];  // + H zeros: the attention of a missing edge
+  __shared__ float s_ga[ECAP * H];
+  __shared__ uint16_t s_src[ECAP];
+  __shared__ int s_odst[BIG ? 1 : ECAP], s_oslot[BIG ? 1 : ECAP];
+  __shared__ int s_rp[WIN + 1], s_orp[WIN + 1];
+  __shared__ float s_elr[BIG ? 1 : WIN * 2 * H];
+  // BIG: hub segment tables (in-edges, out-edges), per-row segments, out-segment partials
+  __shared__ uint32_t s_segI[BIG ? kSegCapI : 1], s_segO[BIG ? kSegCapO : 1];
+  __shared__ int s_rs[BIG ? WIN : 1];
+  __shared__ float4 s_part[BIG ? kSegCapO * LPD : 1];
+  // out-edges past kEC of every row (dst row << 16 | in-slot), from row base s_oxb (0xFFFF:
+  // past the table, read from global memory)
+  __shared__ uint32_t s_oxe[BIG ? kOXCap : 1];
+  __shared__ uint16_t s_oxb[BIG ? WIN : 1];
+  __shared__ int s_wsum[BIG ? NT / 64 : 1];
   const GroupPlan gp(plan, G);
-  if (!(gp.kind[blockIdx.x] & 2)) return;
-  const int a0 = gp.start[blockIdx.x], a1 = gp.start[blockIdx.x + 1];
+  const int nlist = BIG ? gp.count[1] : (int)blockIdx.x + 1;
+  for (int li = blockIdx.x; li < nlist; li += BIG ? gridDim.x : 1) {
+  const int grp = BIG ? gp.bwd_list[li] : li;
+  if (BIG) __syncthreads();  // the previous group's LDS reads are done
+  if (!(gp.kind[grp] & (BIG ? 4 : 2))) continue;
+  const int a0 = gp.start[grp], a1 = gp.start[grp + 1];
   const int tid = threadIdx.x;
   const int nr = a1 - a0, HF = H * F;
   const int ocols = MODE == 1 ? F : HF;
@@ -843,13 +1134,24 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
     s_orp[i] = out_rowptr[a0 + i] - e0;
   }
   for (int i = tid; i < ne; i += NT) {
-    s_src[i] = in_src[e0 + i] - a0;
-    s_odst[i] = out_dst[e0 + i] - a0;
-    s_oslot[i] = out_inslot[e0 + i] - e0;
+    s_src[i] = (uint16_t)(in_src[e0 + i] - a0);
+    if constexpr (!BIG) {
+      s_odst[i] = out_dst[e0 + i] - a0;
+      s_oslot[i] = out_inslot[e0 + i] - e0;
+    }
   }
   for (int i = tid; i < ne * H; i += NT) s_att[i] = attn[(int64_t)e0 * H + i];
-  if (tid < H) s_att[kECap * H + tid] = 0.f;
-  for (int i = tid; i < nr * 2 * H; i += NT) s_elr[i] = elr[(int64_t)a0 * 2 * H + i];
+  if (tid < H) s_att[ECAP * H + tid] = 0.f;
+  if constexpr (!BIG)
+    for (int i = tid; i < nr * 2 * H; i += NT) s_elr[i] = elr[(int64_t)a0 * 2 * H + i];
+  // BIG: after the chunk sweep the row buffers are free and hold the group's logits (zs) and
+  // out-edge slots (gs) for the softmax backward and the d el sums
+  float* s_elr_b = reinterpret_cast<float*>(zs);
+  int* s_oslot_b = reinterpret_cast<int*>(gs);
+  static_assert(!BIG || (WIN * 2 * H <= WIN * LPD * 4 && ECAP <= WIN * LPD * 4), "row buffers hold elr / slots");
+  auto elr_at = [&](int r, int c) -> float {  // elr of group row r, column c (el | er)
+    if constexpr (BIG) return s_elr_b[r * 2 * H + c]; else return s_elr[r * 2 * H + c];
+  };
   const int ldyi = (int)ldy, ldgi = (int)ldgy;
   const __amdgpu_buffer_rsrc_t rY = make_rsrc(Y + (int64_t)a0 * ldy, (uint32_t)(nr * ldyi) * 4u);
   const __amdgpu_buffer_rsrc_t rG = make_rsrc(gY + (int64_t)a0 * ldgy, (uint32_t)(nr * ldgi) * 4u);
@@ -857,24 +1159,56 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)a0 * HF, MODE == 0 ? (uint32_t)(nr * HF) * 4u : 0u);
   for (int i = tid; i < ne * H; i += NT) s_ga[i] = 0.f;
   __syncthreads();  // CSR / attention staged
-  if (nr <= NT / LPD)
-    bwd_lds_chunks<H, MODE, 1, CW>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp, s_src, s_ga, rY,
-                               ldyi, rGo, rO, rG, ldgi, nr, F);
-  else
-    bwd_lds_chunks<H, MODE, 2, CW>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp, s_src, s_ga, rY,
-                               ldyi, rGo, rO, rG, ldgi, nr, F);
+  int nsegI = 0, nsegO = 0;
+  if constexpr (BIG) {
+    static_assert(NT >= WIN, "one row per thread for the segment scans");
+    const bool lv = tid < nr;
+    int rsI, rsO;
+    nsegI = hub_segments<NT, kSegI, kSegCapI>(nr, lv ? s_rp[tid] : 0, lv ? s_rp[tid + 1] - s_rp[tid] : 0,
+                                              s_segI, &rsI, s_wsum);
+    const int ob = lv ? s_orp[tid] : 0, odeg = lv ? s_orp[tid + 1] - ob : 0;
+    const int m = max(0, odeg - kEC);
+    int mt;
+    const int xb = block_excl_scan<NT>(m, s_wsum, &mt);
+    const bool xok = xb + m <= kOXCap;
+    for (int j = 0; j < (xok ? m : 0); ++j) {
+      const int o = ob + kEC + j;
+      s_oxe[xb + j] = (uint32_t)(out_dst[e0 + o] - a0) << 16 | (uint32_t)(out_inslot[e0 + o] - e0);
+    }
+    if (lv) s_oxb[tid] = (uint16_t)(xok && m ? xb : 0xFFFF);
+    __syncthreads();  // s_wsum reads of the scan are done
+    // out-edge segments index the table: "edge" e = xb + (out-edge - kEC)
+    nsegO = hub_segments<NT, kSegO, kSegCapO, kSegMinO>(nr, xb - kEC, xok ? odeg : 0, s_segO, &rsO, s_wsum);
+    if (lv) s_rs[tid] = rsO | (rsI ? (int)0x80000000 : 0);
+    __syncthreads();
+  }
+#define MVML_BWD_CHUNKS(NPA)                                                                       \
+  bwd_lds_chunks<H, MODE, NPA, CW, NT, WIN, ECAP, BIG>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp,  \
+                                                       s_src, s_ga, rY, ldyi, rGo, rO, rG, ldgi, nr, F, \
+                                                       out_dst, out_inslot, e0, a0, s_segI, nsegI, \
+                                                       s_segO, nsegO, s_rs, s_part, s_oxe, s_oxb)
+  if (nr <= DPP) MVML_BWD_CHUNKS(1);
+  else if (NPM == 2 || nr <= 2 * DPP) MVML_BWD_CHUNKS(2);
+  else if (nr <= 3 * DPP) MVML_BWD_CHUNKS((NPM > 2 ? 3 : 2));
+  else MVML_BWD_CHUNKS(NPM);
+#undef MVML_BWD_CHUNKS
   __syncthreads();
+  if constexpr (BIG) {
+    for (int i = tid; i < nr * 2 * H; i += NT) s_elr_b[i] = elr[(int64_t)a0 * 2 * H + i];
+    for (int i = tid; i < ne; i += NT) s_oslot_b[i] = out_inslot[e0 + i] - e0;
+    __syncthreads();
+  }
   // edge_softmax backward per (destination, head); g_pre replaces g_a in LDS
   for (int i = tid; i < nr * H; i += NT) {
     const int d = i / H, h = i % H;
     const int eb = s_rp[d], ee = s_rp[d + 1];
-    const float er = s_elr[d * 2 * H + H + h];
+    const float er = elr_at(d, H + h);
     float dots = 0.f;
     for (int e = eb; e < ee; ++e) dots += s_att[e * H + h] * s_ga[e * H + h];
     float der = 0.f;
     for (int e = eb; e < ee; ++e) {
       const float g_s = s_att[e * H + h] * (s_ga[e * H + h] - dots);
-      const float gp = (s_elr[s_src[e] * 2 * H + h] + er) > 0.f ? g_s : g_s * slope;
+      const float gp = (elr_at(s_src[e], h) + er) > 0.f ? g_s : g_s * slope;
       s_ga[e * H + h] = gp;
       der += gp;
     }
@@ -884,8 +1218,13 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   for (int i = tid; i < nr * H; i += NT) {  // d el: sums over out-edges
     const int u = i / H, h = i % H;
     float del = 0.f;
-    for (int o = s_orp[u]; o < s_orp[u + 1]; ++o) del += s_ga[s_oslot[o] * H + h];
+    for (int o = s_orp[u]; o < s_orp[u + 1]; ++o) {
+      int sl;
+      if constexpr (BIG) sl = s_oslot_b[o]; else sl = s_oslot[o];
+      del += s_ga[sl * H + h];
+    }
     gY[(int64_t)(a0 + u) * ldgy + C + h] = del;
+  }
   }
 }
 
@@ -898,15 +1237,17 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
                        const float* __restrict__ attn, const float* __restrict__ out,
                        const float* __restrict__ g_out, int F, float slope, int mode,
                        float* __restrict__ gpre, float* __restrict__ gY, int64_t ldgy,
-                       float* __restrict__ gelr, int64_t ldgl) {
+                       float* __restrict__ gelr, int64_t ldgl, int skip_big) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   // G > 0: one block per backward fallback group of the plan; G == 0: one wave per atom over
   // all atoms
   int64_t v, vend, vstep;
   if (G > 0) {
     const GroupPlan gp(groups, G);
-    if ((int)blockIdx.x >= gp.count[1]) return;
-    const int g = gp.bwd_list[blockIdx.x];
+    const int li = list_block(blockIdx.x, gridDim.x, gp.count[1]);
+    if (li < 0) return;
+    const int g = gp.bwd_list[li];
+    if (skip_big && (gp.kind[g] & 4)) return;  // the big-window kernel takes it
     const int a0 = gp.start[g], a1 = gp.start[g + 1];
     v = a0 + wid;
     vend = a1;
@@ -1021,15 +1362,17 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
                        const float* __restrict__ attn, const float* __restrict__ gpre,
                        const float* __restrict__ out, const float* __restrict__ g_out, int F,
                        int mode, float* __restrict__ gY, int64_t ldgy, float* __restrict__ gelr,
-                       int64_t ldgl) {
+                       int64_t ldgl, int skip_big) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   // G > 0: one block per backward fallback group of the plan; G == 0: one wave per atom over
   // all atoms
   int64_t u, vend, vstep;
   if (G > 0) {
     const GroupPlan gp(groups, G);
-    if ((int)blockIdx.x >= gp.count[1]) return;
-    const int g = gp.bwd_list[blockIdx.x];
+    const int li = list_block(blockIdx.x, gridDim.x, gp.count[1]);
+    if (li < 0) return;
+    const int g = gp.bwd_list[li];
+    if (skip_big && (gp.kind[g] & 4)) return;  // the big-window kernel takes it
     const int a0 = gp.start[g], a1 = gp.start[g + 1];
     u = a0 + wid;
     vend = a1;
@@ -1107,12 +1450,18 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
   rc = check_launch("gat_softmax_kernel");
   if (rc) return rc;
   if (G == 0) return MVML_OK;
+  const bool big = use_big_window(H, F);
 #define MVML_AGG_FWD_M(CW, M)                                                                       \
   do {                                                                                              \
     gat_agg_fwd_lds_kernel<H, CW, M, CW * 16><<<(unsigned)G, CW * 16, 0, st>>>(groups, G, rp, src, Y, ldy, F, \
                                                                          bias, attn, out);          \
     gat_agg_fwd_gather_kernel<H, CW, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, G, rp, src, Y, ldy, \
-                                                                            F, bias, attn, out);    \
+                                                                            F, bias, attn, out, big); \
+    if constexpr (H <= 4)                                                                           \
+      if (big)                                                                                      \
+        gat_agg_fwd_lds_kernel<H, 16, M, kBigThreads, kPlanBigAtoms, kPlanBigEdgeCap, true>          \
+            <<<(unsigned)std::min<int64_t>(G, kBigBlocks), kBigThreads, 0, st>>>(                    \
+                groups, G, rp, src, Y, ldy, F, bias, attn, out);                                    \
   } while (0)
 #define MVML_AGG_FWD(CW)                                  \
   do {                                                    \
@@ -1136,6 +1485,7 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
                int64_t ldy, const float* elr, const float* attn, const float* out,
                const float* g_out, int F, float slope, int mode, float* gpre, float* gY,
                int64_t ldgy, int C, hipStream_t st) {
+  if (getenv("MVML_BWD_ATOMWISE")) G = 0;  // experiment: per-atom pair over every atom
   if (F % 32 == 0 && G > 0) {  // molecule groups: one pass over Z / g_out / dZ per group
 #ifndef MVML_BWD_CW64
 #define MVML_BWD_CW64 1
@@ -1161,13 +1511,28 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
   } else {
     G = 0;  // no LDS groups: the per-atom pair covers every atom
   }
+  const int big = G > 0 && use_big_window(H, F);
+  if constexpr (H <= 4) {
+    if (big) {
+#define MVML_BWD_BIG(M)                                                                             \
+      gat_agg_bwd_lds_kernel<H, M, 16, kBigThreads, kPlanBigAtoms, kPlanBigEdgeCap, true>            \
+          <<<(unsigned)std::min<int64_t>(G, kBigBlocks), kBigThreads, 0, st>>>(                      \
+              groups, G, rp, src, orp, odst, oslot, Y, ldy, F, elr, attn, out, g_out, slope, gY, ldgy, C)
+      if (mode == 0) MVML_BWD_BIG(0);
+      else if (mode == 1) MVML_BWD_BIG(1);
+      else MVML_BWD_BIG(2);
+#undef MVML_BWD_BIG
+      int rc = check_launch("gat_agg_bwd_lds_kernel(big)");
+      if (rc) return rc;
+    }
+  }
   const unsigned blocks = G > 0 ? (unsigned)G : (unsigned)ceil_div(N, kWavesPerBlock);
   gat_agg_bwd_dst_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
-      N, groups, G, rp, src, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, gY + C, ldgy);
+      N, groups, G, rp, src, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, gY + C, ldgy, big);
   int rc = check_launch("gat_agg_bwd_dst_kernel");
   if (rc) return rc;
   gat_agg_bwd_src_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
-      N, groups, G, rp, orp, odst, oslot, attn, gpre, out, g_out, F, mode, gY, ldgy, gY + C, ldgy);
+      N, groups, G, rp, orp, odst, oslot, attn, gpre, out, g_out, F, mode, gY, ldgy, gY + C, ldgy, big);
   return check_launch("gat_agg_bwd_src_kernel");
 }
 

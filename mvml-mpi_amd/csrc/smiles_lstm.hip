@@ -1,7 +1,5 @@
 // SMILES BiLSTM view (RNNModule, /root/reference/model.py:98-135): the
-// index kernels around the packed bidirectional LSTM.  The recurrence itself reuses the MFMA
-// GEMM (h_prev W_hh^T per time step, beta = 1 onto the input projection) and the LSTM cell
-// kernels of set2set.hip.
+// index kernels around the packed bidirectional LSTM and its fused recurrence.
 //
 // Packed layout (what pack_padded_sequence(enforce_sorted=False) builds, model.py:128): the
 // batch is ordered by descending length (perm[i] = original index of sorted row i) and stored
@@ -11,6 +9,17 @@
 // host computes P = E W_ih^T once ([V, 4H], V = 39 tokens) and mvml_bilstm_gather_rows expands
 // it; the backward sums the gate gradients per token (mvml_bilstm_token_grad) and multiplies the
 // [V, 4H] result into dE and dW_ih with two small GEMMs.
+//
+// Recurrence (mvml_bilstm_seq_fwd / _bwd): one launch per time step carries BOTH directions
+// (forward direction at t, reverse at T-1-t) and fuses the recurrent product with the cell:
+// a workgroup owns 16 batch rows x 4 hidden units, a quad of lanes one (row, unit) with the
+// K = H (forward: h_prev . W_hh rows of the unit's four gates) or K = 4H (backward: gg_next .
+// W_hh columns) dot split four ways and summed by two xor shuffles, then the cell runs in the
+// quad.  At KEGG batch sizes (B <= 64, ~20 rows alive per step on average) a step is a few
+// microseconds of latency, not FLOPs: a kernel boundary (~1.5 us, MI355X_MICROARCH.md price
+// table, row boundary) is cheaper than an in-launch grid barrier (barrier-xcd ~4-5 us), so the
+// time loop lives on the host side of the C ABI (no Python per step) rather than in a persistent
+// grid; W_hh stays L2-resident across the step launches (2.4 MB per direction).
 #include "common.h"
 
 namespace mvml {
@@ -69,6 +78,171 @@ __global__ void select_last_kernel(int64_t B, int64_t H, const int32_t* lens, co
   }
 }
 
+
+// ------------------------------------------------------------------ fused recurrence steps
+constexpr int kStepRows = 16, kStepUnits = 4;  // workgroup: 16 rows x 4 units x 4 K parts
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// sum over the 4 lanes of a quad; every lane gets the same bits (a + b == b + a)
+__device__ __forceinline__ float quad_sum(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  return v;
+}
+
+struct FwdDir {          // one direction of a forward step
+  const float* gin;      // [T*B][4H] input projection x W_ih^T
+  const float* w;        // W_hh [4H][H]
+  const float* b_ih;
+  const float* b_hh;
+  float* c;              // [T*B][H]
+  float* act;            // [T*B][4H] (i, f, g, o)
+  int t, prev, bs;       // prev: the step whose h / c feed this one (-1: none)
+};
+
+// pre = x W_ih^T + h_prev W_hh^T + b_ih + b_hh; i, f, o = sigmoid, g = tanh;
+// c = f c_prev + i g; h = o tanh(c)      (nn.LSTM, model.py:121; lstm_cell_fwd_kernel's order)
+__global__ void __launch_bounds__(256)
+bilstm_step_fwd_kernel(int B, int H, FwdDir d0, FwdDir d1, float* __restrict__ out) {
+  const int dir = blockIdx.y;
+  const FwdDir D = dir ? d1 : d0;
+  const int nsl = H / kStepUnits;
+  const int sl = blockIdx.x % nsl, rb = blockIdx.x / nsl;
+  if (rb * kStepRows >= D.bs) return;
+  const int tid = threadIdx.x, kp = tid & 3;
+  const int j = sl * kStepUnits + ((tid >> 2) & 3);
+  const int r = rb * kStepRows + (tid >> 4);
+  const bool live = r < D.bs;
+  const int row = live ? r : 0;  // rows past bs compute on row 0 and store nothing
+  const int G = 4 * H;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (D.prev >= 0) {
+    const int kq = H / 4;
+    const float* hp = out + ((int64_t)D.prev * B + row) * 2 * H + dir * H + kp * kq;
+    const float* wp = D.w + (int64_t)j * H + kp * kq;
+#pragma unroll 4
+    for (int k = 0; k < kq; k += 4) {
+      const float4 h = ld4(hp + k);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 w = ld4(wp + (int64_t)q * H * H + k);
+        acc[q] = fmaf(h.x, w.x, acc[q]);
+        acc[q] = fmaf(h.y, w.y, acc[q]);
+        acc[q] = fmaf(h.z, w.z, acc[q]);
+        acc[q] = fmaf(h.w, w.w, acc[q]);
+      }
+    }
+  }
+  const int64_t rt = (int64_t)D.t * B + row;
+  float a[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    a[q] = D.gin[rt * G + q * H + j] + quad_sum(acc[q]) + D.b_ih[q * H + j] + D.b_hh[q * H + j];
+  const float i = sigm(a[0]), f = sigm(a[1]), gt = tanhf(a[2]), o = sigm(a[3]);
+  const float cp = D.prev >= 0 ? D.c[((int64_t)D.prev * B + row) * H + j] : 0.f;
+  const float c = f * cp + i * gt;
+  const float h = o * tanhf(c);
+  if (!live) return;
+  D.act[rt * G + kp * H + j] = kp == 0 ? i : kp == 1 ? f : kp == 2 ? gt : o;
+  if (kp == 0) {
+    D.c[rt * H + j] = c;
+    out[rt * 2 * H + dir * H + j] = h;
+  }
+}
+
+struct BwdDir {          // one direction of a backward step
+  const float* wT;       // W_hh^T [H][4H]
+  const float* act;      // [T*B][4H]
+  const float* c;        // [T*B][H]
+  float* gg;             // [T*B][4H] gate gradients (out)
+  float* carry;          // [B][H] dL/dc carried between steps (zeroed by the caller)
+  int t, nxt, tp, bs, bs_nxt;  // nxt: the step this one fed (-1: none); tp: c_prev's step
+};
+
+// g_h = g_out[t] + gg[nxt] W_hh (rows alive at nxt); lstm_cell_bwd_kernel's cell backward with
+// the carried dL/dc (in place: each (row, unit) is read and rewritten by its own quad)
+__global__ void __launch_bounds__(256)
+bilstm_step_bwd_kernel(int B, int H, BwdDir d0, BwdDir d1, const float* __restrict__ g_out) {
+  const int dir = blockIdx.y;
+  const BwdDir D = dir ? d1 : d0;
+  const int nsl = H / kStepUnits;
+  const int sl = blockIdx.x % nsl, rb = blockIdx.x / nsl;
+  if (rb * kStepRows >= D.bs) return;
+  const int tid = threadIdx.x, kp = tid & 3;
+  const int j = sl * kStepUnits + ((tid >> 2) & 3);
+  const int r = rb * kStepRows + (tid >> 4);
+  const bool live = r < D.bs;
+  const int row = live ? r : 0;
+  const int G = 4 * H;
+  float acc = 0.f, acc2 = 0.f;
+  if (D.nxt >= 0 && row < D.bs_nxt) {
+    const float* gp = D.gg + ((int64_t)D.nxt * B + row) * G + kp * H;
+    const float* wp = D.wT + (int64_t)j * G + kp * H;
+#pragma unroll 4
+    for (int k = 0; k < H; k += 8) {
+      const float4 g0 = ld4(gp + k), w0 = ld4(wp + k);
+      const float4 g1 = ld4(gp + k + 4), w1 = ld4(wp + k + 4);
+      acc = fmaf(g0.x, w0.x, acc);
+      acc = fmaf(g0.y, w0.y, acc);
+      acc = fmaf(g0.z, w0.z, acc);
+      acc = fmaf(g0.w, w0.w, acc);
+      acc2 = fmaf(g1.x, w1.x, acc2);
+      acc2 = fmaf(g1.y, w1.y, acc2);
+      acc2 = fmaf(g1.z, w1.z, acc2);
+      acc2 = fmaf(g1.w, w1.w, acc2);
+    }
+  }
+  const int64_t rt = (int64_t)D.t * B + row;
+  const float gh = g_out[rt * 2 * H + dir * H + j] + quad_sum(acc + acc2);
+  const float* av = D.act + rt * G + j;
+  const float i = av[0], f = av[H], gt = av[2 * H], o = av[3 * H];
+  const float tc = tanhf(D.c[rt * H + j]);
+  const float gc = D.carry[(int64_t)row * H + j] + gh * o * (1.f - tc * tc);
+  const float cp = D.tp >= 0 ? D.c[((int64_t)D.tp * B + row) * H + j] : 0.f;
+  if (!live) return;
+  const float gq = kp == 0 ? gc * gt * i * (1.f - i)
+                 : kp == 1 ? gc * cp * f * (1.f - f)
+                 : kp == 2 ? gc * i * (1.f - gt * gt)
+                           : gh * tc * o * (1.f - o);
+  D.gg[rt * G + kp * H + j] = gq;
+  if (kp == 0) D.carry[(int64_t)row * H + j] = gc * f;
+}
+
+// Deterministic token gradient: chunk k of kTokChunk positions (t-major) x 256-column slab sums
+// its live positions per token in LDS, then partial_tok_kernel adds the chunks in order.
+constexpr int kTokChunk = 256;
+constexpr int kTokMaxVocab = 64;
+__global__ void __launch_bounds__(256)
+token_grad_chunk_kernel(int64_t T, int64_t B, int64_t cols, const float* __restrict__ g,
+                        const int32_t* __restrict__ tokens, int64_t ldtok,
+                        const int32_t* __restrict__ lens, const int32_t* __restrict__ perm,
+                        int vocab, float* __restrict__ part) {
+  __shared__ float s_acc[kTokMaxVocab][256];
+  const int tid = threadIdx.x;
+  const int64_t j = blockIdx.y * 256 + tid;
+  for (int v = 0; v < vocab; ++v) s_acc[v][tid] = 0.f;
+  const int64_t p0 = (int64_t)blockIdx.x * kTokChunk, p1 = min<int64_t>(T * B, p0 + kTokChunk);
+  for (int64_t p = p0; p < p1; ++p) {  // same token order in every lane: no LDS races
+    const int64_t t = p / B, i = p - t * B;
+    const int32_t b = perm[i];
+    if (t >= lens[b]) continue;
+    const int v = tokens[b * ldtok + t];
+    if (j < cols) s_acc[v][tid] += g[p * cols + j];
+  }
+  if (j < cols)
+    for (int v = 0; v < vocab; ++v) part[((int64_t)blockIdx.x * vocab + v) * cols + j] = s_acc[v][tid];
+}
+
+__global__ void token_grad_sum_kernel(int64_t nchunk, int64_t n, const float* __restrict__ part,
+                                      float* __restrict__ out) {
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  float acc = 0.f;
+  for (int64_t k = 0; k < nchunk; ++k) acc += part[k * n + e];
+  out[e] = acc;
+}
+
 }  // namespace
 }  // namespace mvml
 
@@ -88,16 +262,85 @@ extern "C" int mvml_bilstm_gather_rows(int64_t T, int64_t B, int64_t cols, const
   return check_launch("bilstm_gather_rows");
 }
 
+extern "C" int64_t mvml_bilstm_token_grad_workspace(int64_t T, int64_t B, int64_t cols, int vocab) {
+  return ceil_div(T * B, kTokChunk) * vocab * cols * (int64_t)sizeof(float);
+}
+
 extern "C" int mvml_bilstm_token_grad(int64_t T, int64_t B, int64_t cols, const float* g,
                                       const int32_t* tokens, int64_t ldtok, const int32_t* lens,
-                                      const int32_t* perm, int vocab, float* out, void* stream) {
+                                      const int32_t* perm, int vocab, float* out, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
   clear_error();
-  MVML_REQUIRE(T >= 0 && B >= 0 && cols > 0 && vocab > 0 && ldtok >= T,
-               "bilstm_token_grad: bad shape");
-  dim3 grid(vocab, (unsigned)ceil_div(cols, 256));
-  token_grad_kernel<<<grid, 256, 0, as_stream(stream)>>>(T, B, cols, g, tokens, ldtok, lens, perm,
-                                                         out);
-  return check_launch("bilstm_token_grad");
+  MVML_REQUIRE(T >= 0 && B >= 0 && cols > 0 && vocab > 0 && vocab <= kTokMaxVocab && ldtok >= T,
+               "bilstm_token_grad: bad shape (vocab <= 64)");
+  hipStream_t st = as_stream(stream);
+  const int64_t nchunk = ceil_div(T * B, kTokChunk);
+  if (nchunk == 0) {
+    (void)hipMemsetAsync(out, 0, (size_t)vocab * cols * sizeof(float), st);
+    return check_launch("bilstm_token_grad(empty)");
+  }
+  MVML_REQUIRE(workspace && (int64_t)workspace_bytes >= mvml_bilstm_token_grad_workspace(T, B, cols, vocab),
+               "bilstm_token_grad: workspace too small");
+  float* part = static_cast<float*>(workspace);
+  dim3 grid((unsigned)nchunk, (unsigned)ceil_div(cols, 256));
+  token_grad_chunk_kernel<<<grid, 256, 0, st>>>(T, B, cols, g, tokens, ldtok, lens, perm, vocab, part);
+  int rc = check_launch("bilstm_token_grad(chunks)");
+  if (rc) return rc;
+  const int64_t n = (int64_t)vocab * cols;
+  token_grad_sum_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(nchunk, n, part, out);
+  return check_launch("bilstm_token_grad(sum)");
+}
+
+extern "C" int mvml_bilstm_seq_fwd(int64_t T, int64_t B, int H, const int32_t* batch_sizes,
+                                   const float* gates0, const float* gates1, const float* w_hh0,
+                                   const float* w_hh1, const float* b_ih0, const float* b_hh0,
+                                   const float* b_ih1, const float* b_hh1, float* out, float* c0,
+                                   float* c1, float* act0, float* act1, void* stream) {
+  clear_error();
+  MVML_REQUIRE(T >= 0 && B > 0 && B <= (1 << 20) && H > 0 && H % 16 == 0 && batch_sizes,
+               "bilstm_seq_fwd: bad shape (H %% 16 == 0, host batch_sizes)");
+  for (int64_t t = 0; t < T; ++t)
+    MVML_REQUIRE(batch_sizes[t] >= 0 && batch_sizes[t] <= B && (t == 0 || batch_sizes[t] <= batch_sizes[t - 1]),
+                 "bilstm_seq_fwd: batch_sizes must be non-increasing in [0, B]");
+  hipStream_t st = as_stream(stream);
+  const int nsl = H / kStepUnits;
+  for (int64_t s = 0; s < T; ++s) {
+    const int ta = (int)s, tb = (int)(T - 1 - s);
+    const FwdDir da{gates0, w_hh0, b_ih0, b_hh0, c0, act0, ta, ta - 1, batch_sizes[ta]};
+    const FwdDir db{gates1, w_hh1, b_ih1, b_hh1, c1, act1, tb, tb + 1 < T ? tb + 1 : -1, batch_sizes[tb]};
+    const int rbs = (int)ceil_div(std::max(da.bs, db.bs), kStepRows);
+    if (rbs == 0) continue;
+    bilstm_step_fwd_kernel<<<dim3((unsigned)(nsl * rbs), 2), 256, 0, st>>>((int)B, H, da, db, out);
+  }
+  return check_launch("bilstm_step_fwd_kernel");
+}
+
+extern "C" int mvml_bilstm_seq_bwd(int64_t T, int64_t B, int H, const int32_t* batch_sizes,
+                                   const float* w_hhT0, const float* w_hhT1, const float* act0,
+                                   const float* act1, const float* c0, const float* c1,
+                                   const float* g_out, float* gg0, float* gg1, float* carry,
+                                   void* stream) {
+  clear_error();
+  MVML_REQUIRE(T >= 0 && B > 0 && B <= (1 << 20) && H > 0 && H % 16 == 0 && batch_sizes,
+               "bilstm_seq_bwd: bad shape (H %% 16 == 0, host batch_sizes)");
+  for (int64_t t = 0; t < T; ++t)
+    MVML_REQUIRE(batch_sizes[t] >= 0 && batch_sizes[t] <= B && (t == 0 || batch_sizes[t] <= batch_sizes[t - 1]),
+                 "bilstm_seq_bwd: batch_sizes must be non-increasing in [0, B]");
+  hipStream_t st = as_stream(stream);
+  const int nsl = H / kStepUnits;
+  float* carry1 = carry + B * (int64_t)H;
+  for (int64_t s = 0; s < T; ++s) {
+    const int ta = (int)(T - 1 - s), tb = (int)s;  // forward direction walks back, reverse forth
+    const int na = ta + 1 < T ? ta + 1 : -1, nb = tb - 1;
+    const BwdDir da{w_hhT0, act0, c0, gg0, carry, ta, na, ta - 1, batch_sizes[ta],
+                    na >= 0 ? batch_sizes[na] : 0};
+    const BwdDir db{w_hhT1, act1, c1, gg1, carry1, tb, nb, tb + 1 < T ? tb + 1 : -1, batch_sizes[tb],
+                    nb >= 0 ? batch_sizes[nb] : 0};
+    const int rbs = (int)ceil_div(std::max(da.bs, db.bs), kStepRows);
+    if (rbs == 0) continue;
+    bilstm_step_bwd_kernel<<<dim3((unsigned)(nsl * rbs), 2), 256, 0, st>>>((int)B, H, da, db, g_out);
+  }
+  return check_launch("bilstm_step_bwd_kernel");
 }
 
 extern "C" int mvml_bilstm_select_last(int64_t B, int64_t H, const int32_t* lens,

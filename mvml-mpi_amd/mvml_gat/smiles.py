@@ -12,11 +12,13 @@ Design (not a cuDNN/MIOpen RNN call): the packed sequence of pack_padded_sequenc
 (enforce_sorted=False) is kept as a time-major [T, B, 2H] buffer with the batch sorted by
 descending length, so the sequences alive at step t are a row prefix.  Per layer and direction
 one MFMA GEMM projects every position's input at once (layer 0: a [vocab, 4H] table lookup,
-mvml_bilstm_gather_rows), then each time step is one GEMM h_prev W_hh^T (beta = 1 onto the
-projection, M = the live prefix) + the LSTM cell kernel, which writes h straight into its half of
-the bidirectional output row.  Backward mirrors it (mvml_lstm_cell_bwd, recurrent GEMM, weight
-gradients as single GEMMs over all positions, deterministic per-token reduction for the
-embedding / W_ih_l0).  Padded positions stay zero, as pad_packed_sequence's output is.
+mvml_bilstm_gather_rows).  The recurrence then runs in ONE C-ABI call per layer
+(mvml_bilstm_seq_fwd / _bwd): one fused launch per time step carries both directions, the
+recurrent product and the LSTM cell, with the step loop on the native side (no Python per step).
+Batches wider than SEQ_MAX_B rows take the per-step MFMA GEMM (h_prev W_hh^T, beta = 1 onto the
+projection, M = the live prefix) + cell-kernel path instead, where the product is FLOP-bound.
+Weight gradients are single GEMMs over all positions; the embedding / W_ih_l0 gradient is a
+deterministic per-token reduction.  Padded positions stay zero, as pad_packed_sequence's are.
 """
 import math
 
@@ -24,7 +26,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ._lib import call, ptr
+from ._lib import call, lib, ptr, workspace
 from .functional import LinearReLUFunction, _c, _check_cuda_f32, _stream, colsum, gemm
 
 
@@ -93,6 +95,8 @@ class Packing:
         pos = np.empty_like(perm)
         pos[perm] = np.arange(self.B)
         self.batch_sizes = [int((lens > t).sum()) for t in range(self.T)]
+        # host int32 copy for the native step loops (mvml_bilstm_seq_*)
+        self.batch_sizes_host = torch.tensor(self.batch_sizes, dtype=torch.int32)
         dev = tokens.device
         tok = tokens.to(torch.int64)
         if int(tok.min()) < 0 or int(tok.max()) >= vocab_size:
@@ -102,6 +106,13 @@ class Packing:
         self.lens = torch.from_numpy(lens.astype(np.int32)).to(dev)
         self.perm = torch.from_numpy(perm.astype(np.int32)).to(dev)
         self.pos = torch.from_numpy(pos.astype(np.int32)).to(dev)
+
+
+SEQ_MAX_B = 512  # fused step path up to this batch width (the GEMM path above)
+
+
+def _use_seq(pk):
+    return pk.B <= SEQ_MAX_B
 
 
 class BiLSTMLayerFunction(torch.autograd.Function):
@@ -119,9 +130,9 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         x = _c(x)
         In = x.shape[-1]
         out = torch.zeros((T, B, 2 * H), dtype=torch.float32, device=dev)
-        saved = []
+        saved, gates_d = [], []
         for d in range(2):
-            w_ih, w_hh, b_ih, b_hh = (_c(t) for t in w[4 * d:4 * d + 4])
+            w_ih = _c(w[4 * d])
             gates = torch.empty((T, B, G), dtype=torch.float32, device=dev)
             if layer0:
                 V = x.shape[0]
@@ -131,20 +142,33 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                      ptr(pk.lens), ptr(pk.perm), ptr(gates), st)
             else:
                 gemm(x, w_ih, T * B, G, In, 0, 0, In, In, gates, G)
-            c = torch.zeros((T, B, H), dtype=torch.float32, device=dev)
-            act = torch.empty((T, B, G), dtype=torch.float32, device=dev)
-            order = range(T) if d == 0 else range(T - 1, -1, -1)
-            prev = None
-            for t in order:
-                bs = pk.batch_sizes[t]
-                c_prev = None
-                if prev is not None:
-                    gemm(out[prev, :, d * H:], w_hh, bs, G, H, 0, 0, 2 * H, H, gates[t], G, beta=1.0)
-                    c_prev = c[prev]
-                call("mvml_lstm_cell_fwd", bs, H, ptr(gates[t]), ptr(b_ih), ptr(b_hh), ptr(c_prev),
-                     ptr(c[t]), ptr(out[t, :, d * H:]), 2 * H, ptr(act[t]), None, 0, st)
-                prev = t
-            saved += [c, act]
+            gates_d.append(gates)
+        if _use_seq(pk):  # one native call: every step of both directions
+            wc = [_c(t) for t in w]
+            c = [torch.zeros((T, B, H), dtype=torch.float32, device=dev) for _ in range(2)]
+            act = [torch.empty((T, B, G), dtype=torch.float32, device=dev) for _ in range(2)]
+            call("mvml_bilstm_seq_fwd", T, B, H, ptr(pk.batch_sizes_host), ptr(gates_d[0]),
+                 ptr(gates_d[1]), ptr(wc[1]), ptr(wc[5]), ptr(wc[2]), ptr(wc[3]), ptr(wc[6]),
+                 ptr(wc[7]), ptr(out), ptr(c[0]), ptr(c[1]), ptr(act[0]), ptr(act[1]), st)
+            saved = [c[0], act[0], c[1], act[1]]
+        else:  # wide batches: per-step MFMA GEMM (beta = 1 onto the projection) + cell kernel
+            for d in range(2):
+                w_hh, b_ih, b_hh = (_c(t) for t in w[4 * d + 1:4 * d + 4])
+                gates = gates_d[d]
+                c = torch.zeros((T, B, H), dtype=torch.float32, device=dev)
+                act = torch.empty((T, B, G), dtype=torch.float32, device=dev)
+                order = range(T) if d == 0 else range(T - 1, -1, -1)
+                prev = None
+                for t in order:
+                    bs = pk.batch_sizes[t]
+                    c_prev = None
+                    if prev is not None:
+                        gemm(out[prev, :, d * H:], w_hh, bs, G, H, 0, 0, 2 * H, H, gates[t], G, beta=1.0)
+                        c_prev = c[prev]
+                    call("mvml_lstm_cell_fwd", bs, H, ptr(gates[t]), ptr(b_ih), ptr(b_hh), ptr(c_prev),
+                         ptr(c[t]), ptr(out[t, :, d * H:]), 2 * H, ptr(act[t]), None, 0, st)
+                    prev = t
+                saved += [c, act]
         ctx.pk, ctx.layer0, ctx.H = pk, layer0, H
         ctx.save_for_backward(x, out, *saved, *w)
         return out
@@ -157,31 +181,39 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         st = _stream(dev)
         T, B, G = pk.T, pk.B, 4 * H
         In = x.shape[-1]
-        g = g_out.contiguous().clone()
+        g = g_out.contiguous()
         cs, acts = (c0, c1), (a0, a1)
         g_w = [None] * 8
         g_x = torch.empty_like(x)
-        for d in range(2):
-            w_ih, w_hh = _c(w[4 * d]), _c(w[4 * d + 1])
-            # W_hh^T [H, 4H] once per backward: the per-step recurrent GEMM then reads its B
-            # operand k-contiguous (the same kernel variant as the forward, ~3x faster per step)
-            w_hhT = w_hh.t().contiguous()
-            c, act = cs[d], acts[d]
-            gg = torch.zeros((T, B, G), dtype=torch.float32, device=dev)
-            carry = [torch.zeros((B, H), dtype=torch.float32, device=dev) for _ in range(2)]
-            order = range(T - 1, -1, -1) if d == 0 else range(T)
-            nxt, k = None, 0
-            for t in order:
-                bs = pk.batch_sizes[t]
-                if nxt is not None:  # recurrent gradient from the step this one fed
-                    rows = min(bs, pk.batch_sizes[nxt])
-                    gemm(gg[nxt], w_hhT, rows, H, G, 0, 0, G, G, g[t, :, d * H:], 2 * H, beta=1.0)
-                tp = t - 1 if d == 0 else t + 1
-                c_prev = c[tp] if 0 <= tp < T else None
-                g_c = carry[k % 2] if nxt is not None else None
-                call("mvml_lstm_cell_bwd", bs, H, ptr(act[t]), ptr(c[t]), ptr(c_prev),
-                     ptr(g[t, :, d * H:]), 2 * H, ptr(g_c), ptr(gg[t]), ptr(carry[(k + 1) % 2]), st)
-                nxt, k = t, k + 1
+        # W_hh^T [H, 4H] once per backward: the recurrent product reads it k-contiguous
+        w_hhT = [_c(w[4 * d + 1]).t().contiguous() for d in range(2)]
+        seq = _use_seq(pk)
+        ggs = [torch.zeros((T, B, G), dtype=torch.float32, device=dev) for _ in range(2)]
+        if seq:
+            carry = torch.zeros((2, B, H), dtype=torch.float32, device=dev)
+            call("mvml_bilstm_seq_bwd", T, B, H, ptr(pk.batch_sizes_host), ptr(w_hhT[0]),
+                 ptr(w_hhT[1]), ptr(a0), ptr(a1), ptr(c0), ptr(c1), ptr(g), ptr(ggs[0]),
+                 ptr(ggs[1]), ptr(carry), st)
+        else:  # wide batches: per-step recurrent GEMM (beta = 1 into g) + cell kernel
+            g = g.clone()
+            for d in range(2):
+                c, act, gg = cs[d], acts[d], ggs[d]
+                carry = [torch.zeros((B, H), dtype=torch.float32, device=dev) for _ in range(2)]
+                order = range(T - 1, -1, -1) if d == 0 else range(T)
+                nxt, k = None, 0
+                for t in order:
+                    bs = pk.batch_sizes[t]
+                    if nxt is not None:  # recurrent gradient from the step this one fed
+                        rows = min(bs, pk.batch_sizes[nxt])
+                        gemm(gg[nxt], w_hhT[d], rows, H, G, 0, 0, G, G, g[t, :, d * H:], 2 * H, beta=1.0)
+                    tp = t - 1 if d == 0 else t + 1
+                    c_prev = c[tp] if 0 <= tp < T else None
+                    g_c = carry[k % 2] if nxt is not None else None
+                    call("mvml_lstm_cell_bwd", bs, H, ptr(act[t]), ptr(c[t]), ptr(c_prev),
+                         ptr(g[t, :, d * H:]), 2 * H, ptr(g_c), ptr(gg[t]), ptr(carry[(k + 1) % 2]), st)
+                    nxt, k = t, k + 1
+        for d in range(2):  # weight / input gradients: GEMMs over all positions
+            w_ih, gg = _c(w[4 * d]), ggs[d]
             gb = torch.empty(G, dtype=torch.float32, device=dev)
             colsum(gg, T * B, G, G, gb)
             g_whh = torch.zeros((G, H), dtype=torch.float32, device=dev)
@@ -193,8 +225,10 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             if layer0:
                 V = x.shape[0]
                 Gt = torch.empty((V, G), dtype=torch.float32, device=dev)
+                nws = int(lib().mvml_bilstm_token_grad_workspace(T, B, G, V))
+                ws = workspace(nws, dev)
                 call("mvml_bilstm_token_grad", T, B, G, ptr(gg), ptr(pk.tokens), pk.ldtok,
-                     ptr(pk.lens), ptr(pk.perm), V, ptr(Gt), st)
+                     ptr(pk.lens), ptr(pk.perm), V, ptr(Gt), ptr(ws), nws, st)
                 gemm(Gt, x, G, In, V, 1, 1, G, In, g_wih, In)
                 gemm(Gt, w_ih, V, In, G, 0, 1, G, In, g_x, In, beta=beta)
                 if d == 1 and pk.pad is not None:

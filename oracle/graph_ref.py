@@ -83,7 +83,7 @@ def csr_ref(src, dst, num_nodes_total):
 
 
 def node_group_plan_ref(node_offsets, in_rowptr, group_atoms=64, win_atoms=128, edge_cap=512,
-                        deg_cap=5):
+                        deg_cap=5, big_atoms=512, big_edge_cap=2432):
     """Node-group plan of mvml_build_node_groups (launch geometry; no reference counterpart):
     group g starts at the first atom of the molecule containing atom group_atoms*g; kind bit 0
     = forward LDS kernel (atom, edge and in-degree caps), bit 1 = backward LDS kernel (atom and
@@ -105,7 +105,8 @@ def node_group_plan_ref(node_offsets, in_rowptr, group_atoms=64, win_atoms=128, 
             continue
         fits = a1 - a0 <= win_atoms and rp[a1] - rp[a0] <= edge_cap
         dmax = int(np.max(rp[a0 + 1:a1 + 1] - rp[a0:a1]))
-        kinds[g] = (1 if fits and dmax <= deg_cap else 0) | (2 if fits else 0)
+        big = a1 - a0 <= big_atoms and rp[a1] - rp[a0] <= big_edge_cap
+        kinds[g] = (1 if fits and dmax <= deg_cap else 0) | (2 if fits else 0) | (4 if big else 0)
         if not kinds[g] & 1:
             fwd.add(g)
         if not kinds[g] & 2:

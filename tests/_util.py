@@ -7,24 +7,29 @@ from mvml_gat.nn import GNNModule
 from oracle.gnn_ref import GNNModuleRef
 
 
-def batch_of_sizes(sizes, seed=0, rings=2, hubs=False):
+def batch_of_sizes(sizes, seed=0, rings=2, hubs=False, n_hubs=1, partners=100):
+    """Chain + ring molecules of the given sizes; hubs: n_hubs atoms per molecule bonded to
+    `partners` random other atoms each (in / out degree partners + 3)."""
     rng = np.random.default_rng(seed)
     sizes = np.asarray(sizes, dtype=np.int64)
     hub_fn = None
     if hubs:
         def hub_fn(M, n, bonds, nb, deg):
-            out = np.full((M, bonds.shape[1] + 100, 2), -1, dtype=np.int32)
+            k = min(n - 1, partners)
+            out = np.full((M, bonds.shape[1] + n_hubs * k, 2), -1, dtype=np.int32)
             nb2 = nb.copy()
             for i in range(M):
                 row = bonds[i][bonds[i, :, 0] >= 0]
                 out[i, :len(row)] = row
-                h = int(rng.integers(0, n))
-                partners = rng.choice(np.setdiff1d(np.arange(n), [h]), size=min(n - 1, 100), replace=False)
-                out[i, len(row):len(row) + len(partners), 0] = h
-                out[i, len(row):len(row) + len(partners), 1] = partners
-                deg[i, h] += len(partners)
-                deg[i, partners] += 1
-                nb2[i] = len(row) + len(partners)
+                pos = len(row)
+                for h in rng.choice(n, size=min(n_hubs, n), replace=False):
+                    pt = rng.choice(np.setdiff1d(np.arange(n), [h]), size=k, replace=False)
+                    out[i, pos:pos + k, 0] = h
+                    out[i, pos:pos + k, 1] = pt
+                    deg[i, h] += k
+                    deg[i, pt] += 1
+                    pos += k
+                nb2[i] = pos
             return out, nb2, deg
     return synth._gen_sizes(rng, sizes, lambda M, n: np.minimum(np.full(M, rings), max(n // 5, 0)),
                             hubs=hub_fn)

@@ -192,10 +192,28 @@ def test_gat_layer_config2(layer):
 
 
 def test_gat_layer0_hubs_flatten_elu():
-    """Layer 0 (F = 192, flatten + ELU) on hub molecules > 128 atoms: the fallback forward
-    gather and the per-atom dst / src backward kernels at the production width."""
+    """Layer 0 (F = 192, flatten + ELU) on hub molecules > 128 atoms: the big-window kernels
+    (kind bit 2) with their hub segments, at the production width."""
     _layer_case(0, batch_of_sizes([150, 90, 210], seed=7, hubs=True), seed=2)
 
 
 def test_gat_layer1_config5():
     _layer_case(1, synth.config5(2, seed=3), seed=4)
+
+
+@pytest.mark.parametrize("layer", [0, 1])
+def test_gat_layer_config5_fallback_kernels(layer, monkeypatch):
+    """MVML_BIG_WINDOW=0: config-5 groups through the per-atom fallbacks (forward gather with
+    its hub pass, dst / src backward pair) — the path of groups past the big window's caps."""
+    monkeypatch.setenv("MVML_BIG_WINDOW", "0")
+    _layer_case(layer, synth.config5(2, seed=3), seed=4 + layer)
+
+
+@pytest.mark.parametrize("layer", [0, 1])
+def test_gat_layer_big_window_table_overflow(layer):
+    """A 300-atom molecule with 7 hubs of 109 partners (2428 edges, at the big window's edge
+    cap): the backward's staged out-edges (640) and out-edge segments (48) overflow, so the
+    last hubs walk their out-edges from global memory on their own lanes."""
+    sb = batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109)
+    assert int(sb.num_edges[0]) <= 2432
+    _layer_case(layer, sb, seed=5 + layer)

@@ -27,6 +27,19 @@ def _batch(B, seed, Tmax=60, ragged=True, space=False):
                                                          (64, 60, 2, True, False), (33, 40, 3, False, False),
                                                          (24, 30, 2, True, True)])
 def test_rnn_module_parity(B, Tmax, layers, ragged, space):
+    """The fused step path (mvml_bilstm_seq_fwd / _bwd: B <= SEQ_MAX_B)."""
+    _rnn_parity(B, Tmax, layers, ragged, space)
+
+
+@pytest.mark.parametrize("B,Tmax,layers,ragged,space", [(64, 60, 2, True, False), (24, 30, 2, True, True)])
+def test_rnn_module_parity_gemm_path(B, Tmax, layers, ragged, space, monkeypatch):
+    """The wide-batch path (per-step MFMA GEMM + cell kernels), forced at a small batch."""
+    import mvml_gat.smiles as sm
+    monkeypatch.setattr(sm, "SEQ_MAX_B", 0)
+    _rnn_parity(B, Tmax, layers, ragged, space)
+
+
+def _rnn_parity(B, Tmax, layers, ragged, space):
     from mvml_gat.smiles import RNNModule
     from oracle.smiles_ref import RNNModuleRef
     torch.manual_seed(B + layers)
