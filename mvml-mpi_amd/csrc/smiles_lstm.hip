@@ -11,15 +11,13 @@
 // [V, 4H] result into dE and dW_ih with two small GEMMs.
 //
 // Recurrence (mvml_bilstm_seq_fwd / _bwd): one launch per time step carries BOTH directions
-// (forward direction at t, reverse at T-1-t) and fuses the recurrent product with the cell:
-// a workgroup owns 16 batch rows x 4 hidden units, a quad of lanes one (row, unit) with the
-// K = H (forward: h_prev . W_hh rows of the unit's four gates) or K = 4H (backward: gg_next .
-// W_hh columns) dot split four ways and summed by two xor shuffles, then the cell runs in the
-// quad.  At KEGG batch sizes (B <= 64, ~20 rows alive per step on average) a step is a few
-// microseconds of latency, not FLOPs: a kernel boundary (~1.5 us, MI355X_MICROARCH.md price
-// table, row boundary) is cheaper than an in-launch grid barrier (barrier-xcd ~4-5 us), so the
-// time loop lives on the host side of the C ABI (no Python per step) rather than in a persistent
-// grid; W_hh stays L2-resident across the step launches (2.4 MB per direction).
+// (forward direction at t, reverse at T-1-t) and fuses the recurrent product with the cell (the
+// tile layout is described above the step kernels).  At KEGG batch sizes (B <= 64, ~20 rows
+// alive per step on average) a step is a few microseconds of latency, not FLOPs: a kernel
+// boundary (~1.5 us, MI355X_MICROARCH.md price table, row boundary) is cheaper than an
+// in-launch grid barrier (barrier-xcd ~4-5 us), so the time loop lives on the host side of the
+// C ABI (no Python per step) rather than in a persistent grid; W_hh (2.4 MB per direction)
+// stays L2-resident across the step launches.
 #include "common.h"
 
 namespace mvml {
@@ -80,15 +78,30 @@ __global__ void select_last_kernel(int64_t B, int64_t H, const int32_t* lens, co
 
 
 // ------------------------------------------------------------------ fused recurrence steps
-constexpr int kStepRows = 16, kStepUnits = 4;  // workgroup: 16 rows x 4 units x 4 K parts
+// A workgroup owns a 16-row x 16-column output tile of the step's recurrent product and splits
+// its K over the waves: v_mfma_f32_16x16x4_f32 (exact f32), operands straight from global
+// memory (L2-resident W_hh, the previous step's rows), every lane's loads issued before the
+// first MFMA (one memory round trip), wave partials summed in LDS in a fixed order, then the
+// cell runs on the tile.
+//   forward:  tile = 16 rows x (4 units x 4 gates); K = H over 4 waves (96 each)
+//   backward: tile = 16 rows x 16 units;            K = 4H over 8 waves (192 each)
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+constexpr int kStepRows = 16;
+constexpr int kFwdUnits = 4, kFwdWaves = 4;
+constexpr int kBwdUnits = 16, kBwdWaves = 8;
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-// sum over the 4 lanes of a quad; every lane gets the same bits (a + b == b + a)
-__device__ __forceinline__ float quad_sum(float v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  return v;
+
+// acc += A (16 x 16 k) B (16 k x 16) for one float4 of each operand per lane: lane l holds
+// A[l % 16][k0 + 4 (l / 16) + s] and B[k0 + 4 (l / 16) + s][l % 16], s = 0..3 (the four MFMA
+// k-steps see k = k0 + 4 (l / 16) + s: a permutation of k0 .. k0 + 15, the same on both sides)
+__device__ __forceinline__ f32x4_t mfma4(float4 a, float4 b, f32x4_t acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+  return acc;
 }
 
 struct FwdDir {          // one direction of a forward step
@@ -103,52 +116,80 @@ struct FwdDir {          // one direction of a forward step
 
 // pre = x W_ih^T + h_prev W_hh^T + b_ih + b_hh; i, f, o = sigmoid, g = tanh;
 // c = f c_prev + i g; h = o tanh(c)      (nn.LSTM, model.py:121; lstm_cell_fwd_kernel's order)
-__global__ void __launch_bounds__(256)
-bilstm_step_fwd_kernel(int B, int H, FwdDir d0, FwdDir d1, float* __restrict__ out) {
+template <int H>
+__global__ void __launch_bounds__(64 * kFwdWaves)
+bilstm_step_fwd_kernel(int B, FwdDir d0, FwdDir d1, float* __restrict__ out) {
+  constexpr int KW = H / kFwdWaves;  // K per wave
+  constexpr int NF = KW / 16;        // float4 loads per lane and operand
+  constexpr int G = 4 * H;
+  static_assert(KW % 16 == 0, "H % 64 == 0");
+  __shared__ float s_part[kFwdWaves][16][17];
   const int dir = blockIdx.y;
   const FwdDir D = dir ? d1 : d0;
-  const int nsl = H / kStepUnits;
+  constexpr int nsl = H / kFwdUnits;
   const int sl = blockIdx.x % nsl, rb = blockIdx.x / nsl;
-  if (rb * kStepRows >= D.bs) return;
-  const int tid = threadIdx.x, kp = tid & 3;
-  const int j = sl * kStepUnits + ((tid >> 2) & 3);
-  const int r = rb * kStepRows + (tid >> 4);
-  const bool live = r < D.bs;
-  const int row = live ? r : 0;  // rows past bs compute on row 0 and store nothing
-  const int G = 4 * H;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (D.prev >= 0) {
-    const int kq = H / 4;
-    const float* hp = out + ((int64_t)D.prev * B + row) * 2 * H + dir * H + kp * kq;
-    const float* wp = D.w + (int64_t)j * H + kp * kq;
-#pragma unroll 4
-    for (int k = 0; k < kq; k += 4) {
-      const float4 h = ld4(hp + k);
+  const int r0 = rb * kStepRows;
+  if (r0 >= D.bs) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = sl * kFwdUnits;
+  // the cell's operands first (threads < 64: one (row, unit) each), in flight with the MFMA
+  // operands below
+  const int row = (tid >> 2) & 15, u = tid & 3, r = r0 + row, j = j0 + u;
+  const bool cell = tid < 64 && r < D.bs;
+  const int64_t rt = (int64_t)D.t * B + (cell ? r : r0);
+  float pre[4], bi[4], bh[4], cp = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 w = ld4(wp + (int64_t)q * H * H + k);
-        acc[q] = fmaf(h.x, w.x, acc[q]);
-        acc[q] = fmaf(h.y, w.y, acc[q]);
-        acc[q] = fmaf(h.z, w.z, acc[q]);
-        acc[q] = fmaf(h.w, w.w, acc[q]);
-      }
+  for (int q = 0; q < 4; ++q) pre[q] = bi[q] = bh[q] = 0.f;
+  if (cell) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pre[q] = D.gin[rt * G + q * H + j];
+      bi[q] = D.b_ih[q * H + j];
+      bh[q] = D.b_hh[q * H + j];
     }
+    if (D.prev >= 0) cp = D.c[((int64_t)D.prev * B + r) * H + j];
   }
-  const int64_t rt = (int64_t)D.t * B + row;
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  if (D.prev >= 0) {
+    // A: h_prev rows (dead rows read the zero state, rows past B clamp to a live row)
+    const int ra = min(r0 + (lane & 15), B - 1);
+    const float* ap = out + ((int64_t)D.prev * B + ra) * 2 * H + dir * H + w * KW + 4 * (lane >> 4);
+    // B: W_hh row of gate column n = lane % 16 (gate n / 4, unit j0 + n % 4)
+    const int n = lane & 15;
+    const float* bp = D.w + (int64_t)((n >> 2) * H + j0 + (n & 3)) * H + w * KW + 4 * (lane >> 4);
+    float4 a[NF], b[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      a[i] = ld4(ap + 16 * i);
+      b[i] = ld4(bp + 16 * i);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA
+#pragma unroll
+    for (int i = 0; i < NF; ++i) acc = mfma4(a[i], b[i], acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s_part[w][4 * (lane >> 4) + r][lane & 15] = acc[r];
+  __syncthreads();
+  // 64 (row, unit) pairs: the four gates of unit u sit in columns 4q + u
+  if (!cell) return;
   float a[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    a[q] = D.gin[rt * G + q * H + j] + quad_sum(acc[q]) + D.b_ih[q * H + j] + D.b_hh[q * H + j];
+  for (int q = 0; q < 4; ++q) {
+    float sum = s_part[0][row][4 * q + u];
+#pragma unroll
+    for (int ww = 1; ww < kFwdWaves; ++ww) sum += s_part[ww][row][4 * q + u];
+    a[q] = pre[q] + sum + bi[q] + bh[q];
+  }
   const float i = sigm(a[0]), f = sigm(a[1]), gt = tanhf(a[2]), o = sigm(a[3]);
-  const float cp = D.prev >= 0 ? D.c[((int64_t)D.prev * B + row) * H + j] : 0.f;
   const float c = f * cp + i * gt;
   const float h = o * tanhf(c);
-  if (!live) return;
-  D.act[rt * G + kp * H + j] = kp == 0 ? i : kp == 1 ? f : kp == 2 ? gt : o;
-  if (kp == 0) {
-    D.c[rt * H + j] = c;
-    out[rt * 2 * H + dir * H + j] = h;
-  }
+  float* av = D.act + rt * G + j;
+  av[0] = i;
+  av[H] = f;
+  av[2 * H] = gt;
+  av[3 * H] = o;
+  D.c[rt * H + j] = c;
+  out[rt * 2 * H + dir * H + j] = h;
 }
 
 struct BwdDir {          // one direction of a backward step
@@ -161,52 +202,73 @@ struct BwdDir {          // one direction of a backward step
 };
 
 // g_h = g_out[t] + gg[nxt] W_hh (rows alive at nxt); lstm_cell_bwd_kernel's cell backward with
-// the carried dL/dc (in place: each (row, unit) is read and rewritten by its own quad)
-__global__ void __launch_bounds__(256)
-bilstm_step_bwd_kernel(int B, int H, BwdDir d0, BwdDir d1, const float* __restrict__ g_out) {
+// the carried dL/dc (in place: each (row, unit) is read and rewritten by its own thread)
+template <int H>
+__global__ void __launch_bounds__(64 * kBwdWaves)
+bilstm_step_bwd_kernel(int B, BwdDir d0, BwdDir d1, const float* __restrict__ g_out) {
+  constexpr int G = 4 * H;
+  constexpr int KW = G / kBwdWaves;
+  constexpr int NF = KW / 16;
+  constexpr int NB = NF / 2;  // two batches of loads (registers)
+  static_assert(KW % 32 == 0, "H % 64 == 0");
+  __shared__ float s_part[kBwdWaves][16][17];
   const int dir = blockIdx.y;
   const BwdDir D = dir ? d1 : d0;
-  const int nsl = H / kStepUnits;
+  constexpr int nsl = H / kBwdUnits;
   const int sl = blockIdx.x % nsl, rb = blockIdx.x / nsl;
-  if (rb * kStepRows >= D.bs) return;
-  const int tid = threadIdx.x, kp = tid & 3;
-  const int j = sl * kStepUnits + ((tid >> 2) & 3);
-  const int r = rb * kStepRows + (tid >> 4);
-  const bool live = r < D.bs;
-  const int row = live ? r : 0;
-  const int G = 4 * H;
-  float acc = 0.f, acc2 = 0.f;
-  if (D.nxt >= 0 && row < D.bs_nxt) {
-    const float* gp = D.gg + ((int64_t)D.nxt * B + row) * G + kp * H;
-    const float* wp = D.wT + (int64_t)j * G + kp * H;
-#pragma unroll 4
-    for (int k = 0; k < H; k += 8) {
-      const float4 g0 = ld4(gp + k), w0 = ld4(wp + k);
-      const float4 g1 = ld4(gp + k + 4), w1 = ld4(wp + k + 4);
-      acc = fmaf(g0.x, w0.x, acc);
-      acc = fmaf(g0.y, w0.y, acc);
-      acc = fmaf(g0.z, w0.z, acc);
-      acc = fmaf(g0.w, w0.w, acc);
-      acc2 = fmaf(g1.x, w1.x, acc2);
-      acc2 = fmaf(g1.y, w1.y, acc2);
-      acc2 = fmaf(g1.z, w1.z, acc2);
-      acc2 = fmaf(g1.w, w1.w, acc2);
+  const int r0 = rb * kStepRows;
+  if (r0 >= D.bs) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = sl * kBwdUnits;
+  // the cell's operands first (threads < 256: one (row, unit) each)
+  const int row = (tid >> 4) & 15, u = tid & 15, r = r0 + row, j = j0 + u;
+  const bool cell = tid < 256 && r < D.bs;
+  const int64_t rt = (int64_t)D.t * B + (cell ? r : r0);
+  float go = 0.f, gcar = 0.f, cc = 0.f, cp = 0.f, av[4] = {0.f, 0.f, 0.f, 0.f};
+  if (cell) {
+    go = g_out[rt * 2 * H + dir * H + j];
+    gcar = D.carry[(int64_t)r * H + j];
+    cc = D.c[rt * H + j];
+    if (D.tp >= 0) cp = D.c[((int64_t)D.tp * B + r) * H + j];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) av[q] = D.act[rt * G + q * H + j];
+  }
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  if (D.nxt >= 0 && r0 < D.bs_nxt) {
+    // A: gg[nxt] rows (rows past bs_nxt hold zeros: the caller zeroes gg), B: W_hh^T rows
+    const int ra = min(r0 + (lane & 15), B - 1);
+    const float* ap = D.gg + ((int64_t)D.nxt * B + ra) * G + w * KW + 4 * (lane >> 4);
+    const float* bp = D.wT + (int64_t)(j0 + (lane & 15)) * G + w * KW + 4 * (lane >> 4);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float4 a[NB], b[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        a[i] = ld4(ap + 16 * (h * NB + i));
+        b[i] = ld4(bp + 16 * (h * NB + i));
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the batch's loads in flight before its MFMAs
+#pragma unroll
+      for (int i = 0; i < NB; ++i) acc = mfma4(a[i], b[i], acc);
     }
   }
-  const int64_t rt = (int64_t)D.t * B + row;
-  const float gh = g_out[rt * 2 * H + dir * H + j] + quad_sum(acc + acc2);
-  const float* av = D.act + rt * G + j;
-  const float i = av[0], f = av[H], gt = av[2 * H], o = av[3 * H];
-  const float tc = tanhf(D.c[rt * H + j]);
-  const float gc = D.carry[(int64_t)row * H + j] + gh * o * (1.f - tc * tc);
-  const float cp = D.tp >= 0 ? D.c[((int64_t)D.tp * B + row) * H + j] : 0.f;
-  if (!live) return;
-  const float gq = kp == 0 ? gc * gt * i * (1.f - i)
-                 : kp == 1 ? gc * cp * f * (1.f - f)
-                 : kp == 2 ? gc * i * (1.f - gt * gt)
-                           : gh * tc * o * (1.f - o);
-  D.gg[rt * G + kp * H + j] = gq;
-  if (kp == 0) D.carry[(int64_t)row * H + j] = gc * f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s_part[w][4 * (lane >> 4) + r][lane & 15] = acc[r];
+  __syncthreads();
+  if (!cell) return;
+  float rec = s_part[0][row][u];
+#pragma unroll
+  for (int ww = 1; ww < kBwdWaves; ++ww) rec += s_part[ww][row][u];
+  const float gh = go + rec;
+  const float i = av[0], f = av[1], gt = av[2], o = av[3];
+  const float tc = tanhf(cc);
+  const float gc = gcar + gh * o * (1.f - tc * tc);
+  float* gq = D.gg + rt * G + j;
+  gq[0] = gc * gt * i * (1.f - i);
+  gq[H] = gc * cp * f * (1.f - f);
+  gq[2 * H] = gc * i * (1.f - gt * gt);
+  gq[3 * H] = gh * tc * o * (1.f - o);
+  D.carry[(int64_t)r * H + j] = gc * f;
 }
 
 // Deterministic token gradient: chunk k of kTokChunk positions (t-major) x 256-column slab sums
@@ -297,20 +359,21 @@ extern "C" int mvml_bilstm_seq_fwd(int64_t T, int64_t B, int H, const int32_t* b
                                    const float* b_ih1, const float* b_hh1, float* out, float* c0,
                                    float* c1, float* act0, float* act1, void* stream) {
   clear_error();
-  MVML_REQUIRE(T >= 0 && B > 0 && B <= (1 << 20) && H > 0 && H % 16 == 0 && batch_sizes,
-               "bilstm_seq_fwd: bad shape (H %% 16 == 0, host batch_sizes)");
+  MVML_REQUIRE(T >= 0 && B > 0 && B <= (1 << 20) && H == 384 && batch_sizes,
+               "bilstm_seq_fwd: bad shape (H = 384, MVP's blstm_dim; host batch_sizes)");
   for (int64_t t = 0; t < T; ++t)
     MVML_REQUIRE(batch_sizes[t] >= 0 && batch_sizes[t] <= B && (t == 0 || batch_sizes[t] <= batch_sizes[t - 1]),
                  "bilstm_seq_fwd: batch_sizes must be non-increasing in [0, B]");
   hipStream_t st = as_stream(stream);
-  const int nsl = H / kStepUnits;
+  constexpr int kH = 384;
+  const int nsl = kH / kFwdUnits;
   for (int64_t s = 0; s < T; ++s) {
     const int ta = (int)s, tb = (int)(T - 1 - s);
     const FwdDir da{gates0, w_hh0, b_ih0, b_hh0, c0, act0, ta, ta - 1, batch_sizes[ta]};
     const FwdDir db{gates1, w_hh1, b_ih1, b_hh1, c1, act1, tb, tb + 1 < T ? tb + 1 : -1, batch_sizes[tb]};
     const int rbs = (int)ceil_div(std::max(da.bs, db.bs), kStepRows);
     if (rbs == 0) continue;
-    bilstm_step_fwd_kernel<<<dim3((unsigned)(nsl * rbs), 2), 256, 0, st>>>((int)B, H, da, db, out);
+    bilstm_step_fwd_kernel<kH><<<dim3((unsigned)(nsl * rbs), 2), 64 * kFwdWaves, 0, st>>>((int)B, da, db, out);
   }
   return check_launch("bilstm_step_fwd_kernel");
 }
@@ -321,13 +384,14 @@ extern "C" int mvml_bilstm_seq_bwd(int64_t T, int64_t B, int H, const int32_t* b
                                    const float* g_out, float* gg0, float* gg1, float* carry,
                                    void* stream) {
   clear_error();
-  MVML_REQUIRE(T >= 0 && B > 0 && B <= (1 << 20) && H > 0 && H % 16 == 0 && batch_sizes,
-               "bilstm_seq_bwd: bad shape (H %% 16 == 0, host batch_sizes)");
+  MVML_REQUIRE(T >= 0 && B > 0 && B <= (1 << 20) && H == 384 && batch_sizes,
+               "bilstm_seq_bwd: bad shape (H = 384, MVP's blstm_dim; host batch_sizes)");
   for (int64_t t = 0; t < T; ++t)
     MVML_REQUIRE(batch_sizes[t] >= 0 && batch_sizes[t] <= B && (t == 0 || batch_sizes[t] <= batch_sizes[t - 1]),
                  "bilstm_seq_bwd: batch_sizes must be non-increasing in [0, B]");
   hipStream_t st = as_stream(stream);
-  const int nsl = H / kStepUnits;
+  constexpr int kH = 384;
+  const int nsl = kH / kBwdUnits;
   float* carry1 = carry + B * (int64_t)H;
   for (int64_t s = 0; s < T; ++s) {
     const int ta = (int)(T - 1 - s), tb = (int)s;  // forward direction walks back, reverse forth
@@ -338,7 +402,7 @@ extern "C" int mvml_bilstm_seq_bwd(int64_t T, int64_t B, int H, const int32_t* b
                     nb >= 0 ? batch_sizes[nb] : 0};
     const int rbs = (int)ceil_div(std::max(da.bs, db.bs), kStepRows);
     if (rbs == 0) continue;
-    bilstm_step_bwd_kernel<<<dim3((unsigned)(nsl * rbs), 2), 256, 0, st>>>((int)B, H, da, db, g_out);
+    bilstm_step_bwd_kernel<kH><<<dim3((unsigned)(nsl * rbs), 2), 64 * kBwdWaves, 0, st>>>((int)B, da, db, g_out);
   }
   return check_launch("bilstm_step_bwd_kernel");
 }

@@ -109,10 +109,11 @@ class Packing:
 
 
 SEQ_MAX_B = 512  # fused step path up to this batch width (the GEMM path above)
+SEQ_H = 384      # the fused step kernels are built for MVP's blstm_dim (config.py)
 
 
-def _use_seq(pk):
-    return pk.B <= SEQ_MAX_B
+def _use_seq(pk, H):
+    return pk.B <= SEQ_MAX_B and H == SEQ_H
 
 
 class BiLSTMLayerFunction(torch.autograd.Function):
@@ -143,7 +144,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             else:
                 gemm(x, w_ih, T * B, G, In, 0, 0, In, In, gates, G)
             gates_d.append(gates)
-        if _use_seq(pk):  # one native call: every step of both directions
+        if _use_seq(pk, H):  # one native call: every step of both directions
             wc = [_c(t) for t in w]
             c = [torch.zeros((T, B, H), dtype=torch.float32, device=dev) for _ in range(2)]
             act = [torch.empty((T, B, G), dtype=torch.float32, device=dev) for _ in range(2)]
@@ -187,7 +188,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         g_x = torch.empty_like(x)
         # W_hh^T [H, 4H] once per backward: the recurrent product reads it k-contiguous
         w_hhT = [_c(w[4 * d + 1]).t().contiguous() for d in range(2)]
-        seq = _use_seq(pk)
+        seq = _use_seq(pk, H)
         ggs = [torch.zeros((T, B, G), dtype=torch.float32, device=dev) for _ in range(2)]
         if seq:
             carry = torch.zeros((2, B, H), dtype=torch.float32, device=dev)
