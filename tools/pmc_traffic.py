@@ -19,11 +19,25 @@ import json
 import os
 from collections import defaultdict
 
-ENTRIES = {  # C-ABI entry point -> its kernels (name substrings)
-    "gat_agg_fwd": ["gat_softmax_kernel", "gat_agg_fwd_lds_kernel", "gat_agg_fwd_gather_kernel"],
-    "gat_agg_bwd": ["gat_agg_bwd_lds_kernel", "gat_agg_bwd_dst_kernel", "gat_agg_bwd_src_kernel"],
+ENTRIES = {  # C-ABI entry point -> its kernels (name substrings; "[big]": the big-window
+    # instantiation, template argument BIG = true, launched beside the molecule-window one)
+    "gat_agg_fwd": ["gat_softmax_kernel", "gat_agg_fwd_lds_kernel", "gat_agg_fwd_lds_kernel[big]",
+                    "gat_agg_fwd_gather_kernel"],
+    "gat_agg_bwd": ["gat_agg_bwd_lds_kernel", "gat_agg_bwd_lds_kernel[big]", "gat_agg_bwd_dst_kernel",
+                    "gat_agg_bwd_src_kernel"],
     "set2set_seg_fwd": ["seg_fwd_kernel"],
 }
+
+
+def _pattern(name, pat):
+    """Does kernel `name` (demangled) belong to pattern `pat`?"""
+    big = pat.endswith("[big]")
+    base = pat[:-5] if big else pat
+    if base not in name:
+        return False
+    if "lds_kernel" in base:
+        return ("true>" in name) == big
+    return True
 
 
 def read_counter(d, counter):
@@ -36,7 +50,7 @@ def read_counter(d, counter):
                 name = row.get("Kernel_Name", "")
                 for entry, pats in ENTRIES.items():
                     for pat in pats:
-                        if pat in name:
+                        if _pattern(name, pat):
                             per[(entry, pat)].append(float(row["Counter_Value"]))
     return per
 
