@@ -46,8 +46,9 @@ TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32
          "mvml_set2set_seg_bwd", "mvml_lstm_cell_fwd", "mvml_lstm_cell_bwd", "mvml_set2set_gx",
          "mvml_graphnorm_fwd", "mvml_graphnorm_bwd", "mvml_colsum_f32", "mvml_gat_fold_weights",
          "mvml_gat_unfold_grads", "mvml_relu_bwd", "mvml_layernorm_fwd", "mvml_layernorm_bwd",
-         "mvml_token_attn_fwd", "mvml_token_attn_bwd", "mvml_conv3_fwd", "mvml_conv3_bwd",
-         "mvml_bce_logits", "mvml_gat_attn_grad"]
+         "mvml_token_attn_fwd", "mvml_token_attn_bwd", "mvml_token_attn_fold_fwd",
+         "mvml_token_attn_fold_bwd", "mvml_gemm_f32x3_batched", "mvml_conv3_fwd", "mvml_conv3_bwd",
+         "mvml_bce_logits", "mvml_gat_attn_grad", "mvml_bilstm_seq_fwd", "mvml_bilstm_seq_bwd"]
 
 
 def parse(argv=None):
@@ -99,6 +100,18 @@ def kernel_report(summary, elapsed_ms_per_step, steps):
                           gbs=(byts / (tot * 1e-3) / 1e9) if byts else None,
                           tfs=(flops / (tot * 1e-3) / 1e12) if flops else None)
     return rows
+
+
+def gemm_shape_report(ev, steps):
+    """MVML_GEMM_SHAPES=1: the GEMM time per (M, N, K, A K-major, B K-major), to stderr."""
+    by = {}
+    for ms, t in ev:
+        k = (t or {}).get("shape")
+        c, tot, fl = by.get(k, (0, 0.0, 0))
+        by[k] = (c + 1, tot + ms, fl + (t or {}).get("flops", 0))
+    for k, (c, tot, fl) in sorted(by.items(), key=lambda x: -x[1][1]):
+        log(f"  gemm {str(k):40s} {c / steps:5.1f}/step {tot / steps:8.3f} ms/step "
+            f"{fl / (tot * 1e-3) / 1e12:7.1f} TF/s")
 
 
 def roofline_entry(ev, kind):
@@ -431,6 +444,9 @@ def run(args):
     if timer_on:
         summ = _lib.timer.summary()
         rows = kernel_report(summ, ms_per_step, args.steps)
+        if os.environ.get("MVML_GEMM_SHAPES") and rank == 0:
+            gemm_shape_report(summ.get("mvml_gemm_f32x3", []) + summ.get("mvml_gemm_f32x3_batched", [])
+                              + summ.get("mvml_gat_proj_fwd", []), args.steps)
         if rank == 0:
             for name, r in sorted(rows.items(), key=lambda kv: -kv[1]["ms_per_step"]):
                 perf = (f"{r['gbs']:8.1f} GB/s" if r["gbs"] else "") + (f"{r['tfs']:7.2f} TF/s" if r["tfs"] else "")
@@ -445,7 +461,8 @@ def run(args):
             extra["roofline_agg_bwd"] = roofline_entry(summ["mvml_gat_agg_bwd"], "hbm")
             extra["roofline_agg_bwd"]["traffic"] = load_traffic(wkey, "gat_agg_bwd")
         proj_ev = summ.get("mvml_gat_proj_fwd", [])
-        gemm_ev = summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", []) + ([] if args.proj_bf16 else proj_ev)
+        gemm_ev = (summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", [])
+                   + summ.get("mvml_gemm_f32x3_batched", []) + ([] if args.proj_bf16 else proj_ev))
         bf_ev = summ.get("mvml_gemm_bf16", []) + (proj_ev if args.proj_bf16 else [])
         if bf_ev:
             extra["roofline_gemm_bf16"] = roofline_entry(bf_ev, "mfma")

@@ -106,6 +106,14 @@ int mvml_gemm_f32x3(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                     const float* A, int64_t lda, const float* B, int64_t ldb,
                     const float* bias, float beta, int act, float* C, int64_t ldc,
                     void* workspace, size_t workspace_bytes, void* stream);
+/* mvml_gemm_f32x3 over `batch` independent products (grid z): product z reads A + z stride_a,
+ * B + z stride_b and writes C + z stride_c (floats); no split-K, so no workspace.  For the
+ * fusion head's per-head 384 x 384 weight products (one launch instead of twelve). */
+int mvml_gemm_f32x3_batched(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                            int64_t batch, const float* A, int64_t lda, int64_t stride_a,
+                            const float* B, int64_t ldb, int64_t stride_b, const float* bias,
+                            float beta, int act, float* C, int64_t ldc, int64_t stride_c,
+                            void* stream);
 /* bf16 operands (round-to-nearest-even from the fp32 inputs), one v_mfma_f32_32x32x16_bf16 per
  * fragment pair, fp32 accumulate: the "bf16 projection on MFMA" of BASELINE.json config 4
  * (accuracy bar 2e-2 relative, north_star).  Same arguments / workspace as mvml_gemm_f32. */
@@ -267,6 +275,10 @@ int mvml_relu_bwd(int64_t n, const float* y, const float* g_y, float* g_x, void*
  *   mvml_token_attn_fwd/_bwd: the 3-token attention of model.py:62-68 per (molecule, head);
  *     qkv rows 3b+t = [q (H*dk) | k (H*dk) | v (H*dk)] (ld >= 3 H dk), dk = 384; att [B, H, 3,
  *     dk] (the Conv2d input layout), P [B, H, 3, 3] saved softmax; scale = 1/sqrt(dk).
+ *   mvml_token_attn_fold_fwd/_bwd: the same attention with Q.K re-associated: s_ij =
+ *     <p_i, x_j> scale, p = x M_h (M_h = W_q,h^T W_k,h), pv rows 3b+t = [p (H*dk) | v (H*dk)]
+ *     (ld >= 2 H dk), x = the LayerNorm rows (keys of every head, ldx >= dk); the backward
+ *     writes g_pv [3B, 2 H dk] and g_k = sum over heads of dL/dx through the keys [3B, dk].
  *   mvml_conv3_fwd/_bwd: Conv2d(12, 12, kernel 3) + ReLU on att (model.py:27, 69):
  *     in [B, 12, 3, W] -> out [B, 12, W-2] (post-ReLU); bwd gives g_in, g_weight [12,12,3,3],
  *     g_bias [12] (deterministic partial sums; workspace mvml_conv3_bwd_workspace_size(B)).
@@ -283,6 +295,13 @@ int mvml_token_attn_fwd(int64_t B, int H, int dk, const float* qkv, int64_t ld, 
 int mvml_token_attn_bwd(int64_t B, int H, int dk, const float* qkv, int64_t ld, float scale,
                         const float* P, const float* g_att, float* g_qkv, int64_t ldg,
                         void* stream);
+int mvml_token_attn_fold_fwd(int64_t B, int H, int dk, const float* pv, int64_t ld,
+                             const float* x, int64_t ldx, float scale, float* att, float* P,
+                             void* stream);
+int mvml_token_attn_fold_bwd(int64_t B, int H, int dk, const float* pv, int64_t ld,
+                             const float* x, int64_t ldx, float scale, const float* P,
+                             const float* g_att, float* g_pv, int64_t ldg, float* g_k,
+                             int64_t ldgk, void* stream);
 int mvml_conv3_fwd(int64_t B, int C, int O, int W, const float* in, const float* weight,
                    const float* bias, float* out, void* stream);
 size_t mvml_conv3_bwd_workspace_size(int64_t B);

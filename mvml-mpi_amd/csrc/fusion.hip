@@ -242,6 +242,171 @@ token_attn_bwd_kernel(int64_t B, int H, int dk, const float* __restrict__ qkv, i
   }
 }
 
+// Folded Q.K (the QK^T of model.py:65-68 re-associated): s_ij = <q_i, k_j> = x_i W_q^T W_k x_j^T
+// = <p_i, x_j> with p = x M_h, M_h = W_q,h^T W_k,h (D x D per head), so the product GEMM forms
+// [P | V] = X [M_1 .. M_H | W_v^T] (2 H D columns instead of 3 H D) and the attention reads the
+// LayerNorm rows x_j themselves as the keys of every head.  One wave per MOLECULE walks the
+// heads in order: the three key rows are loaded once, and the backward sums the key gradient
+// over the heads in registers (fixed order) into g_k = sum_h g_k,h, so the data-gradient GEMM
+// also runs over 2 H D columns.
+//   pv rows 3b+t = [p (H dk) | v (H dk)] (ld >= 2 H dk); x rows 3b+t (dk); att, P as above.
+__global__ void __launch_bounds__(256)
+token_attn_fold_fwd_kernel(int64_t B, int H, int dk, const float* __restrict__ pv, int64_t ld,
+                           const float* __restrict__ x, int64_t ldx, float scale,
+                           float* __restrict__ att, float* __restrict__ P) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= B) return;
+  const int64_t HD = (int64_t)H * dk;
+  float k[NT][kDkVpl];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < kDkVpl; ++i) k[t][i] = x[(b * NT + t) * ldx + lane + 64 * i];
+  for (int h = 0; h < H; ++h) {
+    float q[NT][kDkVpl], v[NT][kDkVpl];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float* row = pv + (b * NT + t) * ld + (int64_t)h * dk;
+#pragma unroll
+      for (int i = 0; i < kDkVpl; ++i) {
+        q[t][i] = row[lane + 64 * i];
+        v[t][i] = row[HD + lane + 64 * i];
+      }
+    }
+    float p[NT][NT];
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        float sc = 0.f;
+#pragma unroll
+        for (int i = 0; i < kDkVpl; ++i) sc = fmaf(q[a][i], k[c][i], sc);
+        p[a][c] = wsum(sc) * scale;
+      }
+#pragma unroll
+    for (int a = 0; a < NT; ++a) {
+      const float m = fmaxf(p[a][0], fmaxf(p[a][1], p[a][2]));
+      float z = 0.f;
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        p[a][c] = expf(p[a][c] - m);
+        z += p[a][c];
+      }
+#pragma unroll
+      for (int c = 0; c < NT; ++c) p[a][c] /= z;
+    }
+    const int64_t w = b * H + h;
+    float* out = att + w * NT * dk;
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int i = 0; i < kDkVpl; ++i) {
+        float o = 0.f;
+#pragma unroll
+        for (int c = 0; c < NT; ++c) o = fmaf(p[a][c], v[c][i], o);
+        out[a * dk + lane + 64 * i] = o;
+      }
+    if (lane < NT * NT) {
+      float pvv = p[0][0];
+#pragma unroll
+      for (int e = 1; e < NT * NT; ++e) pvv = lane == e ? p[e / NT][e % NT] : pvv;
+      P[w * NT * NT + lane] = pvv;
+    }
+  }
+}
+
+// Backward of token_attn_fold_fwd: g_v_j = sum_i p_ij g_i; g_s = p (g_p - <p, g_p>) scale;
+// g_p_i = sum_j g_s_ij x_j; g_k_j = sum_h sum_i g_s_ij p_i (heads in order).
+__global__ void __launch_bounds__(256)
+token_attn_fold_bwd_kernel(int64_t B, int H, int dk, const float* __restrict__ pv, int64_t ld,
+                           const float* __restrict__ x, int64_t ldx, float scale,
+                           const float* __restrict__ P, const float* __restrict__ g_att,
+                           float* __restrict__ gpv, int64_t ldg, float* __restrict__ gk,
+                           int64_t ldgk) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= B) return;
+  const int64_t HD = (int64_t)H * dk;
+  float k[NT][kDkVpl], gks[NT][kDkVpl];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < kDkVpl; ++i) {
+      k[t][i] = x[(b * NT + t) * ldx + lane + 64 * i];
+      gks[t][i] = 0.f;
+    }
+  for (int h = 0; h < H; ++h) {
+    const int64_t w = b * H + h;
+    float p[NT][NT];
+#pragma unroll
+    for (int e = 0; e < NT * NT; ++e) p[e / NT][e % NT] = P[w * NT * NT + e];
+    float g[NT][kDkVpl], v[NT][kDkVpl];
+    const float* ga = g_att + w * NT * dk;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float* row = pv + (b * NT + t) * ld + (int64_t)h * dk;
+#pragma unroll
+      for (int i = 0; i < kDkVpl; ++i) {
+        g[t][i] = ga[t * dk + lane + 64 * i];
+        v[t][i] = row[HD + lane + 64 * i];
+      }
+    }
+    float gs[NT][NT];
+#pragma unroll
+    for (int a = 0; a < NT; ++a) {
+      float gp[NT];
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        float sc = 0.f;
+#pragma unroll
+        for (int i = 0; i < kDkVpl; ++i) sc = fmaf(g[a][i], v[c][i], sc);
+        gp[c] = wsum(sc);
+      }
+      const float dot = p[a][0] * gp[0] + p[a][1] * gp[1] + p[a][2] * gp[2];
+#pragma unroll
+      for (int c = 0; c < NT; ++c) gs[a][c] = p[a][c] * (gp[c] - dot) * scale;
+    }
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      float* grow = gpv + (b * NT + c) * ldg + (int64_t)h * dk;
+#pragma unroll
+      for (int i = 0; i < kDkVpl; ++i) {
+        float o = 0.f;
+#pragma unroll
+        for (int a = 0; a < NT; ++a) o = fmaf(p[a][c], g[a][i], o);
+        grow[HD + lane + 64 * i] = o;
+      }
+    }
+    float q[NT][kDkVpl];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float* row = pv + (b * NT + t) * ld + (int64_t)h * dk;
+#pragma unroll
+      for (int i = 0; i < kDkVpl; ++i) q[t][i] = row[lane + 64 * i];
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float* grow = gpv + (b * NT + t) * ldg + (int64_t)h * dk;
+#pragma unroll
+      for (int i = 0; i < kDkVpl; ++i) {
+        float oq = 0.f, ok = 0.f;
+#pragma unroll
+        for (int c = 0; c < NT; ++c) {
+          oq = fmaf(gs[t][c], k[c][i], oq);
+          ok = fmaf(gs[c][t], q[c][i], ok);
+        }
+        grow[lane + 64 * i] = oq;
+        gks[t][i] += ok;
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < kDkVpl; ++i) gk[(b * NT + t) * ldgk + lane + 64 * i] = gks[t][i];
+}
+
 // Conv2d(C, O, 3) over the (C, 3, W) cube of one molecule (model.py:27, 69): the kernel height
 // equals the token count, so the output is (O, 1, W - 2); + bias, ReLU (model.py:27-28).
 constexpr int kConvC = 12, kConvO = 12, kConvH = 3;
@@ -636,6 +801,32 @@ extern "C" int mvml_token_attn_bwd(int64_t B, int H, int dk, const float* qkv, i
   token_attn_bwd_kernel<<<(unsigned)ceil_div(B * H, 4), 256, 0, as_stream(stream)>>>(
       B, H, dk, qkv, ld, scale, P, g_att, g_qkv, ldg);
   return check_launch("token_attn_bwd_kernel");
+}
+
+extern "C" int mvml_token_attn_fold_fwd(int64_t B, int H, int dk, const float* pv, int64_t ld,
+                                        const float* x, int64_t ldx, float scale, float* att,
+                                        float* P, void* stream) {
+  clear_error();
+  MVML_REQUIRE(B >= 0 && H > 0 && dk == 64 * kDkVpl && ld >= 2 * (int64_t)H * dk && ldx >= dk,
+               "token_attn_fold_fwd: dk must be %d, ld >= 2*H*dk", 64 * kDkVpl);
+  if (B == 0) return MVML_OK;
+  token_attn_fold_fwd_kernel<<<(unsigned)ceil_div(B, 4), 256, 0, as_stream(stream)>>>(
+      B, H, dk, pv, ld, x, ldx, scale, att, P);
+  return check_launch("token_attn_fold_fwd_kernel");
+}
+
+extern "C" int mvml_token_attn_fold_bwd(int64_t B, int H, int dk, const float* pv, int64_t ld,
+                                        const float* x, int64_t ldx, float scale, const float* P,
+                                        const float* g_att, float* g_pv, int64_t ldg, float* g_k,
+                                        int64_t ldgk, void* stream) {
+  clear_error();
+  MVML_REQUIRE(B >= 0 && H > 0 && dk == 64 * kDkVpl && ld >= 2 * (int64_t)H * dk && ldx >= dk &&
+                   ldg >= 2 * (int64_t)H * dk && ldgk >= dk,
+               "token_attn_fold_bwd: bad shape");
+  if (B == 0) return MVML_OK;
+  token_attn_fold_bwd_kernel<<<(unsigned)ceil_div(B, 4), 256, 0, as_stream(stream)>>>(
+      B, H, dk, pv, ld, x, ldx, scale, P, g_att, g_pv, ldg, g_k, ldgk);
+  return check_launch("token_attn_fold_bwd_kernel");
 }
 
 extern "C" int mvml_conv3_fwd(int64_t B, int C, int O, int W, const float* in, const float* weight,

@@ -264,6 +264,11 @@ __device__ __forceinline__ float comp(const float4& v, int s) {
 // the lane holds a column and 16 rows: a halving butterfly over the W lanes of a group
 // (values 32 -> 32/W, masks W/2 .. 1) leaves lane li with the values of index
 // ((li & (W-1)) << (5 - EPI_LOGW)) | t, index = side * 16 + row register.
+// Strided batch (blockIdx.z): product z reads A + z a, B + z b and writes C + z c (floats).
+struct BatchStrides {
+  int64_t a = 0, b = 0, c = 0;
+};
+
 struct ProjEpi {
   const float* vec;  // [2][cols]
   int cols;          // H*F
@@ -352,7 +357,13 @@ __global__ void __launch_bounds__(kThreads, 2)
 gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
-                float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{}) {
+                float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{},
+                BatchStrides bst = BatchStrides{}) {
+  if (blockIdx.z) {  // strided batch
+    A += blockIdx.z * bst.a;
+    B += blockIdx.z * bst.b;
+    C += blockIdx.z * bst.c;
+  }
   using SA = Stager<AK>;
   using SB = Stager<BKM>;
   // [stage][A tile | B tile], one __shared__ object (a second one can de-pipeline glds waits).
@@ -607,7 +618,13 @@ __global__ void __launch_bounds__(kThreads, MVML_X3S_WAVES)  // 2 workgroups per
 gemm_x3s_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
-                float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{}) {
+                float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{},
+                BatchStrides bst = BatchStrides{}) {
+  if (blockIdx.z) {  // strided batch
+    A += blockIdx.z * bst.a;
+    B += blockIdx.z * bst.b;
+    C += blockIdx.z * bst.c;
+  }
   using SA = SplitStager<AK>;
   using SB = SplitStager<BKM>;
   __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kOpBytes];
@@ -891,7 +908,13 @@ __global__ void __launch_bounds__(kXThreads, MVML_X3W_WAVES)  // one workgroup p
 gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
-                float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{}) {
+                float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{},
+                BatchStrides bst = BatchStrides{}) {
+  if (blockIdx.z) {  // strided batch
+    A += blockIdx.z * bst.a;
+    B += blockIdx.z * bst.b;
+    C += blockIdx.z * bst.c;
+  }
   using OA = XOp<AK, NP>;
   using OB = XOp<BKM, NP>;
   constexpr int kStage = OA::kBytes + OB::kBytes;
@@ -1362,13 +1385,15 @@ namespace {
 int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                 const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
                 float beta, int act, float* C, int64_t ldc, void* workspace,
-                size_t workspace_bytes, void* stream);
+                size_t workspace_bytes, void* stream, int64_t batch = 1,
+                BatchStrides bst = BatchStrides{});
 }
 
 extern "C" int mvml_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                              const float* A, int64_t lda, const float* B, int64_t ldb,
                              const float* bias, float beta, int act, float* C, int64_t ldc,
                              void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
   return gemm_launch(kPrecF32, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
                      workspace, workspace_bytes, stream);
 }
@@ -1377,14 +1402,28 @@ extern "C" int mvml_gemm_f32x3(int a_kmajor, int b_kmajor, int64_t M, int64_t N,
                                const float* A, int64_t lda, const float* B, int64_t ldb,
                                const float* bias, float beta, int act, float* C, int64_t ldc,
                                void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
   return gemm_launch(kPrecX3, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
                      workspace, workspace_bytes, stream);
+}
+
+extern "C" int mvml_gemm_f32x3_batched(int a_kmajor, int b_kmajor, int64_t M, int64_t N,
+                                       int64_t K, int64_t batch, const float* A, int64_t lda,
+                                       int64_t stride_a, const float* B, int64_t ldb,
+                                       int64_t stride_b, const float* bias, float beta, int act,
+                                       float* C, int64_t ldc, int64_t stride_c, void* stream) {
+  clear_error();
+  MVML_REQUIRE(batch >= 1 && batch <= 65535 && stride_a >= 0 && stride_b >= 0 && stride_c >= 0,
+               "gemm_batched: bad batch / strides");
+  return gemm_launch(kPrecX3, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
+                     nullptr, 0, stream, batch, BatchStrides{stride_a, stride_b, stride_c});
 }
 
 extern "C" int mvml_gemm_bf16(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                               const float* A, int64_t lda, const float* B, int64_t ldb,
                               const float* bias, float beta, int act, float* C, int64_t ldc,
                               void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
   return gemm_launch(kPrecBf16, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C,
                      ldc, workspace, workspace_bytes, stream);
 }
@@ -1393,8 +1432,7 @@ namespace {
 int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                 const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
                 float beta, int act, float* C, int64_t ldc, void* workspace,
-                size_t workspace_bytes, void* stream) {
-  clear_error();
+                size_t workspace_bytes, void* stream, int64_t batch, BatchStrides bst) {
   MVML_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
   if (M == 0 || N == 0) return MVML_OK;
   MVML_REQUIRE(ldc >= N, "gemm: ldc < N");
@@ -1403,7 +1441,8 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   MVML_REQUIRE(act == 0 || act == 1, "gemm: bad act");
   hipStream_t st = as_stream(stream);
   const bool x3 = prec == kPrecX3, bf = prec == kPrecBf16;
-  const GemmPlan plan = plan_gemm(prec, M, N, K);
+  GemmPlan plan = plan_gemm(prec, M, N, K);
+  if (batch > 1) plan.S = 1;  // batched products are small: no split-K slab
   const int S = plan.S;
   float* slab = nullptr;
   if (S > 1) {
@@ -1416,32 +1455,33 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   const int64_t kc = S > 1 ? k_chunk(K, S) : (K > 0 ? K : 1);
   const int64_t tiles = plan.wide ? ceil_div(M, XBM) * ceil_div(N, XBN) : ceil_div(M, BM) * ceil_div(N, BN);
   MVML_REQUIRE(tiles < (int64_t(1) << 31), "gemm: too many tiles");
-  const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0);
-  const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0);
-  dim3 grid(plan.wide || bf ? x3w_grid_x(tiles, S) : (unsigned)tiles, (unsigned)S);
+  const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0) && bst.a % 4 == 0;
+  const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0) && bst.b % 4 == 0;
+  dim3 grid(plan.wide || bf ? x3w_grid_x(tiles, S) : (unsigned)tiles, (unsigned)S, (unsigned)batch);
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
   do {                                                                                          \
     if (bf && x3w_fast(AKV, BKV, M, N, K, av, bv))                                              \
       gemm_x3w_kernel<AKV, BKV, -1, true, 1><<<grid, kXThreads, 0, st>>>(                       \
-          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst);  \
     else if (bf)                                                                                \
       gemm_x3w_kernel<AKV, BKV, -1, false, 1><<<grid, kXThreads, 0, st>>>(                      \
-          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst);  \
     else if (plan.wide && x3w_fast(AKV, BKV, M, N, K, av, bv))                                  \
       gemm_x3w_kernel<AKV, BKV, -1, true><<<grid, kXThreads, 0, st>>>(                          \
-          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst);  \
     else if (plan.wide)                                                                         \
       gemm_x3w_kernel<AKV, BKV, -1, false><<<grid, kXThreads, 0, st>>>(                         \
-          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst);  \
     else if (x3 && AKV && BKV) /* both k-major: fragment split measured faster at 128x128 */    \
       gemm_f32_kernel<AKV, BKV, -1, true><<<grid, kThreads, 0, st>>>(                           \
-          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst);  \
     else if (x3)                                                                                \
       gemm_x3s_kernel<AKV, BKV><<<grid, kThreads, 0, st>>>(                                     \
-          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv);                  \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst);  \
     else                                                                                        \
       gemm_f32_kernel<AKV, BKV><<<grid, kThreads, 0, st>>>(M, N, K, A, lda, B, ldb, bias, beta, \
-                                                           act, C, ldc, kc, slab, av, bv);      \
+                                                           act, C, ldc, kc, slab, av, bv,       \
+                                                           ProjEpi{}, bst);                     \
   } while (0)
   if (!a_kmajor && !b_kmajor) MVML_GEMM_LAUNCH(false, false);
   else if (!a_kmajor && b_kmajor) MVML_GEMM_LAUNCH(false, true);

@@ -67,13 +67,21 @@ _GEMM_ENTRY = {"f32": ("mvml_gemm_f32", 0), "x3": ("mvml_gemm_f32x3", 1),
 
 def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0, algo=None):
     """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32 / mvml_gemm_f32x3)."""
-    _lib.call_tag[0] = {"flops": 2 * M * N * K}
+    _lib.call_tag[0] = {"flops": 2 * M * N * K, "shape": (M, N, K, int(a_kmajor), int(b_kmajor))}
     L = _lib.lib()
     dev = C.device
     wsz = L.mvml_gemm_workspace_size(M, N, K)
     wp, wn = _lib.ws_ptr_size(wsz, dev)
     call(_GEMM_ENTRY[algo or GEMM_ALGO][0], int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda,
          ptr(B), ldb, ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
+
+
+def gemm_batched(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, batch, sa, sb, sc, beta=0.0):
+    """C_z = A_z * B_z (+ beta C_z) for z < batch, operands at float strides sa / sb / sc
+    (mvml_gemm_f32x3_batched: fp32-accurate split-bf16 MFMA, no split-K)."""
+    _lib.call_tag[0] = {"flops": 2 * M * N * K * batch, "shape": (M, N, K, int(a_kmajor), int(b_kmajor), batch)}
+    call("mvml_gemm_f32x3_batched", int(a_kmajor), int(b_kmajor), M, N, K, batch, ptr(A), lda, sa,
+         ptr(B), ldb, sb, None, float(beta), 0, ptr(C), ldc, sc, _stream(C.device))
 
 
 def colsum(X, M, N, ldx, out, beta=0.0, offset=0, alpha=1.0):

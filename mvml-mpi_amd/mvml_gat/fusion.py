@@ -16,7 +16,8 @@ import torch.nn as nn
 
 from . import _lib
 from ._lib import call, ptr
-from .functional import (LinearReLUFunction, _c, _check_cuda_f32, _stream, colsum, gemm)
+from .functional import (LinearReLUFunction, _c, _check_cuda_f32, _stream, colsum, gemm,
+                         gemm_batched)
 
 
 class LinearFunction(torch.autograd.Function):
@@ -50,6 +51,12 @@ class LinearFunction(torch.autograd.Function):
         return gx, gw, gb
 
 
+# Q.K re-associated (mvml_token_attn_fold_*): s = (x M_h) . x with M_h = W_q,h^T W_k,h, so the
+# token GEMMs run over 2 H D columns (P, V) instead of 3 H D (Q, K, V) in the forward, the data
+# gradient and the weight gradient; False = the literal Q / K / V path (kept, tested).
+FOLD_QK = True
+
+
 class FusionAttnConvFunction(torch.autograd.Function):
     """model.py:54-71 up to the Conv2d+ReLU: shared LayerNorm of the three views, Q/K/V (one
     GEMM over the concatenated [W_q; W_k; W_v]), 3-token attention per head, Conv2d(nh, nh, 3)
@@ -70,24 +77,38 @@ class FusionAttnConvFunction(torch.autograd.Function):
         rstd = torch.empty((3 * B,), **f32)
         call("mvml_layernorm_fwd", 3 * B, D, ptr(X), D, ptr(_c(ln_w)), ptr(_c(ln_b)), float(eps),
              ptr(Xn), D, ptr(mean), ptr(rstd), st)
-        Wqkv = torch.cat([_c(wq), _c(wk), _c(wv)], dim=0)  # (3 H D, D)
-        HD3 = 3 * H * D
-        QKV = torch.empty((3 * B, HD3), **f32)
-        gemm(Xn, Wqkv, 3 * B, HD3, D, 0, 0, D, D, QKV, HD3)
         att = torch.empty((B, H, 3, D), **f32)
         P = torch.empty((B, H, 3, 3), **f32)
         scale = 1.0 / math.sqrt(D)
-        call("mvml_token_attn_fwd", B, H, D, ptr(QKV), HD3, float(scale), ptr(att), ptr(P), st)
+        HD = H * D
+        fold = FOLD_QK
+        if fold:
+            wq3, wk3 = _c(wq).view(H, D, D), _c(wk).view(H, D, D)
+            # Bcat [D, 2 H D] = [M_1 .. M_H | W_v^T]: M_h[i][j] = sum_o Wq_h[o][i] Wk_h[o][j]
+            Bcat = torch.empty((D, 2 * HD), **f32)
+            gemm_batched(wq3, wk3, D, D, D, 1, 1, D, D, Bcat, 2 * HD, H, D * D, D * D, D)
+            Bcat[:, HD:].copy_(_c(wv).t())  # parameter layout (7 MB), not a product
+            PV = torch.empty((3 * B, 2 * HD), **f32)  # rows 3b+t: [x M_1 .. x M_H | x W_v^T]
+            gemm(Xn, Bcat, 3 * B, 2 * HD, D, 0, 1, D, 2 * HD, PV, 2 * HD)
+            call("mvml_token_attn_fold_fwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
+                 ptr(att), ptr(P), st)
+            saved = (Bcat, PV)
+        else:
+            Wqkv = torch.cat([_c(wq), _c(wk), _c(wv)], dim=0)  # (3 H D, D)
+            QKV = torch.empty((3 * B, 3 * HD), **f32)
+            gemm(Xn, Wqkv, 3 * B, 3 * HD, D, 0, 0, D, D, QKV, 3 * HD)
+            call("mvml_token_attn_fwd", B, H, D, ptr(QKV), 3 * HD, float(scale), ptr(att), ptr(P), st)
+            saved = (Wqkv, QKV)
         out = torch.empty((B, H, D - 2), **f32)
         call("mvml_conv3_fwd", B, H, H, D, ptr(att), ptr(_c(conv_w)), ptr(_c(conv_b)), ptr(out), st)
-        ctx.save_for_backward(X, Xn, mean, rstd, ln_w, Wqkv, QKV, P, att, out, conv_w)
-        ctx.dims = (B, D, H, scale)
+        ctx.save_for_backward(X, Xn, mean, rstd, ln_w, wq, wk, wv, *saved, P, att, out, conv_w)
+        ctx.dims = (B, D, H, scale, fold)
         return out.view(B, H * (D - 2))
 
     @staticmethod
     def backward(ctx, g_out):
-        X, Xn, mean, rstd, ln_w, Wqkv, QKV, P, att, out, conv_w = ctx.saved_tensors
-        B, D, H, scale = ctx.dims
+        X, Xn, mean, rstd, ln_w, wq, wk, wv, S0, S1, P, att, out, conv_w = ctx.saved_tensors
+        B, D, H, scale, fold = ctx.dims
         dev = X.device
         st = _stream(dev)
         f32 = dict(dtype=torch.float32, device=dev)
@@ -99,14 +120,33 @@ class FusionAttnConvFunction(torch.autograd.Function):
         wp, wn = _lib.ws_ptr_size(L.mvml_conv3_bwd_workspace_size(B), dev)
         call("mvml_conv3_bwd", B, H, H, D, ptr(att), ptr(_c(conv_w)), ptr(out), ptr(g_out), ptr(g_att),
              ptr(g_cw), ptr(g_cb), wp, wn, st)
-        HD3 = 3 * H * D
-        gQKV = torch.empty((3 * B, HD3), **f32)
-        call("mvml_token_attn_bwd", B, H, D, ptr(QKV), HD3, float(scale), ptr(P), ptr(g_att),
-             ptr(gQKV), HD3, st)
-        gW = torch.empty_like(Wqkv)
-        gemm(gQKV, Xn, HD3, D, 3 * B, 1, 1, HD3, D, gW, D)
+        HD = H * D
         gXn = torch.empty((3 * B, D), **f32)
-        gemm(gQKV, Wqkv, 3 * B, D, HD3, 0, 1, HD3, D, gXn, D)
+        if fold:
+            Bcat, PV = S0, S1
+            gPV = torch.empty((3 * B, 2 * HD), **f32)
+            # g_k (the keys' gradient, summed over heads) lands in gXn: the GEMMs add onto it
+            call("mvml_token_attn_fold_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
+                 ptr(P), ptr(g_att), ptr(gPV), 2 * HD, ptr(gXn), D, st)
+            G2 = torch.empty((2 * HD, D), **f32)  # [h D + j][i] = dL/dM_h[i][j]; then dL/dW_v
+            gemm(gPV, Xn, 2 * HD, D, 3 * B, 1, 1, 2 * HD, D, G2, D)
+            wq3, wk3 = _c(wq).view(H, D, D), _c(wk).view(H, D, D)
+            gWq = torch.empty((H, D, D), **f32)
+            gWk = torch.empty((H, D, D), **f32)
+            # per head h (G2 rows h D .. h D + D): W_k,h dM_h^T and W_q,h dM_h
+            gemm_batched(wk3, G2, D, D, D, 0, 1, D, D, gWq, D, H, D * D, D * D, D * D)
+            gemm_batched(wq3, G2, D, D, D, 0, 0, D, D, gWk, D, H, D * D, D * D, D * D)
+            gemm(gPV, Bcat, 3 * B, D, 2 * HD, 0, 0, 2 * HD, 2 * HD, gXn, D, beta=1.0)
+            g_wq, g_wk, g_wv = gWq.view(HD, D), gWk.view(HD, D), G2[HD:]
+        else:
+            Wqkv, QKV = S0, S1
+            gQKV = torch.empty((3 * B, 3 * HD), **f32)
+            call("mvml_token_attn_bwd", B, H, D, ptr(QKV), 3 * HD, float(scale), ptr(P), ptr(g_att),
+                 ptr(gQKV), 3 * HD, st)
+            gW = torch.empty_like(Wqkv)
+            gemm(gQKV, Xn, 3 * HD, D, 3 * B, 1, 1, 3 * HD, D, gW, D)
+            gemm(gQKV, Wqkv, 3 * B, D, 3 * HD, 0, 1, 3 * HD, D, gXn, D)
+            g_wq, g_wk, g_wv = gW[:HD], gW[HD:2 * HD], gW[2 * HD:]
         gX = torch.empty((3 * B, D), **f32)
         gyxh = torch.empty((3 * B, D), **f32)
         call("mvml_layernorm_bwd", 3 * B, D, ptr(X), D, ptr(_c(ln_w)), ptr(mean), ptr(rstd), ptr(gXn), D,
@@ -116,9 +156,7 @@ class FusionAttnConvFunction(torch.autograd.Function):
         colsum(gyxh, 3 * B, D, D, g_lnw)
         colsum(gXn, 3 * B, D, D, g_lnb)
         gX = gX.view(B, 3, D)
-        HD = H * D
-        return (gX[:, 0], gX[:, 1], gX[:, 2], g_lnw, g_lnb, gW[:HD], gW[HD:2 * HD], gW[2 * HD:],
-                g_cw, g_cb, None)
+        return (gX[:, 0], gX[:, 1], gX[:, 2], g_lnw, g_lnb, g_wq, g_wk, g_wv, g_cw, g_cb, None)
 
 
 class BCEWithLogitsFunction(torch.autograd.Function):

@@ -37,8 +37,13 @@ def _pair(B, seed=0, dim=384, heads=12, classes=11, relu_margin=False):
     return ref, mod, xs
 
 
+@pytest.mark.parametrize("fold", [True, False])
 @pytest.mark.parametrize("B,margin", [(1, False), (5, False), (64, True), (300, True)])
-def test_fusion_forward_backward_parity(B, margin):
+def test_fusion_forward_backward_parity(B, margin, fold, monkeypatch):
+    """fold: the Q.K re-associated path (mvml_token_attn_fold_*, the default); False: the
+    literal Q / K / V GEMM + mvml_token_attn_*."""
+    import mvml_gat.fusion as fu
+    monkeypatch.setattr(fu, "FOLD_QK", fold)
     ref, mod, xs = _pair(B, seed=B, relu_margin=margin)
     xr = [x.clone().requires_grad_(True) for x in xs]
     xd = [x.float().to(DEV).requires_grad_(True) for x in xs]

@@ -155,6 +155,28 @@ def test_gemm_x3_error_matches_fp32(K):
         assert errs[algo][0] <= 2 * base[0] and errs[algo][1] <= 2 * base[1], errs
 
 
+@pytest.mark.parametrize("ak,bk", [(1, 1), (0, 1), (0, 0), (1, 0)])
+@pytest.mark.parametrize("M,N,K,batch", [(384, 384, 384, 12), (100, 70, 36, 3), (300, 260, 520, 2)])
+def test_gemm_batched(ak, bk, M, N, K, batch):
+    """mvml_gemm_f32x3_batched: product z at operand strides, C blocks side by side in one wide
+    matrix (column stride, as the fusion head's [M_1 .. M_H] panel), beta onto C."""
+    from mvml_gat.functional import gemm_batched
+    g = torch.Generator().manual_seed(M + N + K + batch)
+    A = torch.randn(batch, M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(batch, K, N, generator=g, dtype=torch.float64)
+    Np = ((N + 3) // 4) * 4
+    C0 = torch.randn(M, batch * Np, generator=g, dtype=torch.float64)
+    Ad = (A.transpose(1, 2) if ak else A).contiguous().float().to(DEV)
+    Bd = (B if bk else B.transpose(1, 2)).contiguous().float().to(DEV)
+    C = C0.float().to(DEV)
+    gemm_batched(Ad, Bd, M, N, K, ak, bk, M if ak else K, N if bk else K, C, batch * Np, batch,
+                 M * K, K * N, Np, beta=0.5)
+    ref = C0.clone()
+    for z in range(batch):
+        ref[:, z * Np:z * Np + N] = A[z] @ B[z] + 0.5 * C0[:, z * Np:z * Np + N]
+    assert rel_err(C, ref) < TOL
+
+
 def test_gemm_two_streams_concurrent():
     """Split-K GEMMs (which use workspace slabs) enqueued on two streams at once: each stream
     has its own scratch, so neither result is corrupted by the other's partial sums."""
