@@ -414,16 +414,31 @@ constexpr int kConvThreads = 384;
 constexpr int kConvWg = kConvO * kConvC * kConvH * 3;  // 1296 weights
 constexpr int kConvLd = 385;  // LDS row stride (W <= 384): rows land on different banks
 
-// rows x W floats from global (row-contiguous) into LDS rows of stride kConvLd
+// rows x W floats from global (row-contiguous) into LDS rows of stride kConvLd.  The aligned path
+// issues all of a thread's loads (<= kStageIt float4: 36 rows x 384 / 384 threads = 9) before its
+// first LDS store — one memory round trip per molecule instead of one per float4.
+constexpr int kStageIt = 9;
 __device__ __forceinline__ void conv_stage(float* dst, const float* __restrict__ src, int rows, int W,
                                            int tid) {
-  if ((W & 3) == 0 && ((uintptr_t)src & 15) == 0) {
-    const int w4 = W >> 2;
-    for (int i = tid; i < rows * w4; i += kConvThreads) {
-      const int r = i / w4, c = (i - r * w4) * 4;
-      const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)r * W + c);
-      float* d = dst + r * kConvLd + c;
-      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  const int w4 = W >> 2;
+  if ((W & 3) == 0 && ((uintptr_t)src & 15) == 0 && rows * w4 <= kStageIt * kConvThreads) {
+    float4 v[kStageIt];
+#pragma unroll
+    for (int it = 0; it < kStageIt; ++it) {
+      const int i = tid + it * kConvThreads;
+      if (i < rows * w4) {
+        const int r = i / w4, c = (i - r * w4) * 4;
+        v[it] = *reinterpret_cast<const float4*>(src + (int64_t)r * W + c);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < kStageIt; ++it) {
+      const int i = tid + it * kConvThreads;
+      if (i < rows * w4) {
+        const int r = i / w4, c = (i - r * w4) * 4;
+        float* d = dst + r * kConvLd + c;
+        d[0] = v[it].x; d[1] = v[it].y; d[2] = v[it].z; d[3] = v[it].w;
+      }
     }
   } else {
     for (int i = tid; i < rows * W; i += kConvThreads) dst[(i / W) * kConvLd + i % W] = src[i];
@@ -629,8 +644,16 @@ conv3_fwd2_kernel(int64_t B, int W, const float* __restrict__ in, const float* _
 //    16 x 112 partial tiles are summed in fixed order at the end (deterministic, no atomics).
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 constexpr int kConvWaves = kConvThreads / 64;  // 6
+#ifndef MVML_CONV_MFMA_DX
+// 1: the input gradient on v_mfma_f32_16x16x4_f32 (36 x 36 weight matrix in 27 registers per
+// lane) — measured 6.34 vs 5.75 ms for the VALU loop at 65,536 molecules (register pressure)
+#define MVML_CONV_MFMA_DX 0
+#endif
 constexpr int kConvNT = 7;                     // 16-column tiles of n (108 weights + bias)
-__global__ void __launch_bounds__(kConvThreads, 2)
+#ifndef MVML_CONV_BWD_WAVES
+#define MVML_CONV_BWD_WAVES 2  // waves per SIMD the register budget is cut for (3: two workgroups per CU)
+#endif
+__global__ void __launch_bounds__(kConvThreads, MVML_CONV_BWD_WAVES)
 conv3_bwd2_kernel(int64_t B, int W, int64_t per_block, const float* __restrict__ in,
                   const float* __restrict__ wgt, const float* __restrict__ out,
                   const float* __restrict__ g_out, float* __restrict__ g_in,
@@ -655,17 +678,76 @@ conv3_bwd2_kernel(int64_t B, int W, int64_t per_block, const float* __restrict__
     const int n = 16 * j + lo;
     boff[j] = n < 108 ? (n / 3) * kConvLd + n % 3 : (n == 108 ? -1 : -2);
   }
+#if MVML_CONV_MFMA_DX
+  // input-gradient A fragments: W[o][(c, dy)][dx] as a 36 x 36 matrix, rows (c, dy) = 16 rt + lo,
+  // columns k = (o, dx) = 4 ks + lk; loaded once, held in 27 registers
+  float wfr[3][9];
+#pragma unroll
+  for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+    for (int ks = 0; ks < 9; ++ks) {
+      const int cd = 16 * rt + lo, k = 4 * ks + lk;
+      wfr[rt][ks] = cd < kConvC * kConvH ? wgt[(k / 3) * 108 + cd * 3 + k % 3] : 0.f;
+    }
+#endif
   const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(B, b0 + per_block);
   for (int64_t b = b0; b < b1; ++b) {
     __syncthreads();  // previous molecule's LDS reads done
     conv_stage(s_in, in + b * (int64_t)(kConvC * kConvH * W), kConvC * kConvH, W, tid);
     const float* go = g_out + b * (int64_t)(kConvO * Wo);
     const float* oo = out + b * (int64_t)(kConvO * Wo);
-    for (int i = tid; i < kConvO * kConvLd; i += kConvThreads) {
-      const int o = i / kConvLd, x = i % kConvLd;
-      s_g[i] = (x < Wo && oo[o * Wo + x] > 0.f) ? go[o * Wo + x] : 0.f;  // zero-padded
+    {  // g_pre = g_out where out > 0, zero-padded rows; all loads before the stores
+      constexpr int kIt = (kConvO * kConvLd + kConvThreads - 1) / kConvThreads;
+      float gv[kIt], ov[kIt];
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        const int i = tid + it * kConvThreads, o = i / kConvLd, x = i % kConvLd;
+        const bool ok = i < kConvO * kConvLd && x < Wo;
+        gv[it] = ok ? go[o * Wo + x] : 0.f;
+        ov[it] = ok ? oo[o * Wo + x] : 0.f;
+      }
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        const int i = tid + it * kConvThreads;
+        if (i < kConvO * kConvLd) s_g[i] = ov[it] > 0.f ? gv[it] : 0.f;
+      }
     }
     __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);  // phases stay apart (registers)
+#if MVML_CONV_MFMA_DX
+    {  // input gradient on the matrix cores: g_in[(c, dy)][x'] = sum_(o, dx) W g_pre[o][x' - dx];
+       // wave w owns the columns [64 w, 64 w + 64) (4 tiles), all three row tiles
+      f32x4_t gacc[3][4];
+#pragma unroll
+      for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) gacc[rt][ct] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 9; ++ks) {
+        const int k = 4 * ks + lk, o = k / 3, dx = k % 3;
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const int xi = 64 * wid + 16 * ct + lo - dx;
+          const float bv = xi >= 0 ? s_g[o * kConvLd + max(xi, 0)] : 0.f;
+#pragma unroll
+          for (int rt = 0; rt < 3; ++rt)
+            gacc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(wfr[rt][ks], bv, gacc[rt][ct], 0, 0, 0);
+        }
+      }
+      float* gb = g_in + b * (int64_t)(kConvC * kConvH * W);
+#pragma unroll
+      for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const int xp = 64 * wid + 16 * ct + lo;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int cd = 16 * rt + 4 * lk + r;
+            if (cd < kConvC * kConvH && xp < W) gb[cd * W + xp] = gacc[rt][ct][r];
+          }
+        }
+    }
+#else
     if (tid < W) {  // input gradient
       const int xp = tid;
       float g[kConvO][3];
@@ -689,6 +771,8 @@ conv3_bwd2_kernel(int64_t B, int W, int64_t per_block, const float* __restrict__
 #pragma unroll
       for (int cd = 0; cd < kConvC * kConvH; ++cd) dst[cd * W] = acc_in[cd];
     }
+#endif
+    __builtin_amdgcn_sched_barrier(0);
     // weight / bias gradient: x-steps of 4 columns, wave w takes steps [16 w, 16 w + 16)
     for (int ks = 16 * wid; ks < 16 * wid + 16; ++ks) {
       const int x = 4 * ks + lk;
@@ -714,6 +798,57 @@ conv3_bwd2_kernel(int64_t B, int W, int64_t per_block, const float* __restrict__
     for (int w = 0; w < kConvWaves; ++w) s += red[(w * 16 + o) * 112 + n];
     if (n < 108) part[(int64_t)blockIdx.x * kConvPart + o * 108 + n] = s;
     else part[(int64_t)blockIdx.x * kConvPart + 2 * kConvWg + o] = s;
+  }
+}
+
+// Forward on the matrix cores: out[o][x] = ReLU(b[o] + sum_k W[o][k] im2col[k][x]), k = (c, dy,
+// dx) < 108 in 27 steps of v_mfma_f32_16x16x4_f32, M = 12 output channels (one 16-row tile), wave w
+// the columns [64 w, 64 w + 64); the weight fragments (27 per lane) are loaded once per
+// workgroup, the im2col operand is a per-lane LDS read of the staged rows.  Replaces the
+// per-thread VALU loop, whose 1296 weights arrived as 81 serialised scalar loads per molecule.
+__global__ void __launch_bounds__(kConvThreads, 3)  // two workgroups per CU (3 waves per SIMD)
+conv3_fwd3_kernel(int64_t B, int W, int64_t per_block, const float* __restrict__ in,
+                  const float* __restrict__ wgt, const float* __restrict__ bias,
+                  float* __restrict__ out) {
+  __shared__ float s_in[kConvC * kConvH * kConvLd + 8];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lo = lane & 15, lk = lane >> 4;
+  const int Wo = W - 2;
+  float wfr[27];
+#pragma unroll
+  for (int ks = 0; ks < 27; ++ks) wfr[ks] = lo < kConvO ? wgt[lo * 108 + 4 * ks + lk] : 0.f;
+  float bo[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bo[r] = 4 * lk + r < kConvO ? bias[4 * lk + r] : 0.f;
+  if (tid < 8) s_in[kConvC * kConvH * kConvLd + tid] = 0.f;
+  const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(B, b0 + per_block);
+  for (int64_t b = b0; b < b1; ++b) {
+    __syncthreads();  // previous molecule's LDS reads done
+    conv_stage(s_in, in + b * (int64_t)(kConvC * kConvH * W), kConvC * kConvH, W, tid);
+    __syncthreads();
+    f32x4_t acc[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[ct] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 27; ++ks) {
+      const int k = 4 * ks + lk;  // im2col row: (c, dy) = k / 3, shift dx = k % 3
+      const int koff = (k / 3) * kConvLd + k % 3;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const float bv = s_in[koff + 64 * wid + 16 * ct + lo];  // columns >= Wo: discarded
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(wfr[ks], bv, acc[ct], 0, 0, 0);
+      }
+    }
+    float* ob = out + b * (int64_t)(kConvO * Wo);
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int x = 64 * wid + 16 * ct + lo;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = 4 * lk + r;
+        if (o < kConvO && x < Wo) ob[o * Wo + x] = fmaxf(acc[ct][r] + bo[r], 0.f);
+      }
+    }
   }
 }
 
@@ -829,20 +964,23 @@ extern "C" int mvml_token_attn_fold_bwd(int64_t B, int H, int dk, const float* p
   return check_launch("token_attn_fold_bwd_kernel");
 }
 
+static int64_t conv3_blocks(int64_t B) { return std::min<int64_t>(B, 512); }  // 2 per CU
+
 extern "C" int mvml_conv3_fwd(int64_t B, int C, int O, int W, const float* in, const float* weight,
                               const float* bias, float* out, void* stream) {
   clear_error();
   MVML_REQUIRE(C == kConvC && O == kConvO && W >= 3 && W <= 384, "conv3_fwd: C = O = 12, 3 <= W <= 384");
   if (B == 0) return MVML_OK;
 #ifndef MVML_CONV_V1
-  conv3_fwd2_kernel<<<(unsigned)B, kConvThreads, 0, as_stream(stream)>>>(B, W, in, weight, bias, out);
+  const int64_t nblk = conv3_blocks(B), per = ceil_div(B, nblk);
+  conv3_fwd3_kernel<<<(unsigned)ceil_div(B, per), kConvThreads, 0, as_stream(stream)>>>(
+      B, W, per, in, weight, bias, out);
 #else
   conv3_fwd_kernel<<<(unsigned)B, kConvThreads, 0, as_stream(stream)>>>(B, W, in, weight, bias, out);
 #endif
   return check_launch("conv3_fwd_kernel");
 }
 
-static int64_t conv3_blocks(int64_t B) { return std::min<int64_t>(B, 512); }  // 2 per CU
 
 extern "C" size_t mvml_conv3_bwd_workspace_size(int64_t B) {
   return carve_size((size_t)conv3_blocks(B > 0 ? B : 1) * kConvPart * sizeof(float));

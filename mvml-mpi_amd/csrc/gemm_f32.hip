@@ -789,6 +789,27 @@ struct XOp {
     }
   }
 
+  // ablation only: the planes' stores with no split arithmetic (float bits as bf16 pairs)
+  __device__ static __forceinline__ void raw_store(uint8_t* op, int tid, const float4 (&v)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint2 p0 = make_uint2(__float_as_uint(v[i].x), __float_as_uint(v[i].y));
+      const uint2 p1 = make_uint2(__float_as_uint(v[i].z), __float_as_uint(v[i].w));
+      uint32_t off;
+      if (!KMAJ) {
+        const int row = (tid >> 2) + 128 * i, q = tid & 3;
+        off = row * 32 + (((q >> 1) ^ ((row >> 3) & 1)) << 4) + 8 * (q & 1);
+      } else {
+        off = (2 * (tid >> 6) + i) * kXKmajPitch + 8 * (tid & 63);
+      }
+      *reinterpret_cast<uint2*>(op + off) = p0;
+      if constexpr (NP == 3) {
+        *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
+        *reinterpret_cast<uint2*>(op + 2 * kPlane + off) = p0;
+      }
+    }
+  }
+
   // 32x32x16 operand fragment of tile rows R0 .. R0+31, plane p: lane l holds row R0 + (l & 31),
   // k = 8 (l >> 5) + [0, 8).
   __device__ static __forceinline__ bf16x8 frag(const uint8_t* op, int p, int R0, int lane) {
@@ -1006,7 +1027,11 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   };
   auto stage = [&](int buf) {
     OA::split_store(lds + buf * kStage, tid, va);
+#ifdef MVML_ABL_NOSPLIT_B  // ablation: B's planes written without the split (wrong results)
+    OB::raw_store(lds + buf * kStage + OA::kBytes, tid, vb);
+#else
     OB::split_store(lds + buf * kStage + OA::kBytes, tid, vb);
+#endif
   };
 #ifndef MVML_X3W_PRIO
 #define MVML_X3W_PRIO 1
