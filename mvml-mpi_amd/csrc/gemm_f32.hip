@@ -1467,6 +1467,28 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   hipStream_t st = as_stream(stream);
   const bool x3 = prec == kPrecX3, bf = prec == kPrecBf16;
   GemmPlan plan = plan_gemm(prec, M, N, K);
+  // N = 256 q + r with 0 < r <= 128 (384-column products: the fusion head's data / weight
+  // gradients, the LSTM hh weight gradients): a last 256-wide tile column would be at least half
+  // padding (so such products fell back to the 128x128 kernel entirely); instead the first
+  // 256 q columns run on the 256x256 kernel and the last r on their own (narrow) plan — two
+  // launches on the stream, one workspace reused in stream order.
+  static const bool nsplit_on = [] {
+    const char* e = getenv("MVML_GEMM_NSPLIT");
+    return !(e && atoi(e) == 0);
+  }();
+  if (nsplit_on && x3 && batch == 1 && N > XBN && N % XBN != 0 && N % XBN <= XBN / 2 &&
+      plan_gemm(prec, M, N / XBN * XBN, K).wide) {
+    const int64_t N1 = N / XBN * XBN, N2 = N - N1;
+    if (mvml_gemm_workspace_size(M, N1, K) <= workspace_bytes &&
+        mvml_gemm_workspace_size(M, N2, K) <= workspace_bytes) {
+      int rc = gemm_launch(prec, a_kmajor, b_kmajor, M, N1, K, A, lda, B, ldb, bias, beta, act, C,
+                           ldc, workspace, workspace_bytes, stream);
+      if (rc) return rc;
+      return gemm_launch(prec, a_kmajor, b_kmajor, M, N2, K, A, lda, b_kmajor ? B + N1 : B + N1 * ldb,
+                         ldb, bias ? bias + N1 : nullptr, beta, act, C + N1, ldc, workspace,
+                         workspace_bytes, stream);
+    }
+  }
   if (batch > 1) plan.S = 1;  // batched products are small: no split-K slab
   const int S = plan.S;
   float* slab = nullptr;

@@ -110,7 +110,8 @@ def _x3_tile(algo):
 @pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (130, 70, 74), (257, 300, 768), (96, 40, 20000),
                                    (256, 384, 1000), (640, 512, 4000), (1000, 1928, 768),
-                                   (512, 384, 65536 + 17)])
+                                   (512, 384, 65536 + 17),
+                                   (49152, 384, 100), (6144, 384, 20000)])  # N = 256 + 128 splits
 def test_gemm_layouts(ak, bk, M, N, K, algo):
     from mvml_gat.functional import gemm
     if K > 50000 and algo in ("f32", "x3-128"):
