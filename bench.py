@@ -48,7 +48,8 @@ TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32
          "mvml_gat_unfold_grads", "mvml_relu_bwd", "mvml_layernorm_fwd", "mvml_layernorm_bwd",
          "mvml_token_attn_fwd", "mvml_token_attn_bwd", "mvml_token_attn_fold_fwd",
          "mvml_token_attn_fold_bwd", "mvml_gemm_f32x3_batched", "mvml_conv3_fwd", "mvml_conv3_bwd",
-         "mvml_bce_logits", "mvml_gat_attn_grad", "mvml_bilstm_seq_fwd", "mvml_bilstm_seq_bwd"]
+         "mvml_bce_logits", "mvml_gat_attn_grad", "mvml_bilstm_seq_fwd", "mvml_bilstm_seq_bwd",
+         "mvml_lstm_gates_cell_fwd"]
 
 
 def parse(argv=None):
@@ -446,6 +447,7 @@ def run(args):
         rows = kernel_report(summ, ms_per_step, args.steps)
         if os.environ.get("MVML_GEMM_SHAPES") and rank == 0:
             gemm_shape_report(summ.get("mvml_gemm_f32x3", []) + summ.get("mvml_gemm_f32x3_batched", [])
+                              + summ.get("mvml_lstm_gates_cell_fwd", [])
                               + summ.get("mvml_gat_proj_fwd", []), args.steps)
         if rank == 0:
             for name, r in sorted(rows.items(), key=lambda kv: -kv[1]["ms_per_step"]):
@@ -462,7 +464,8 @@ def run(args):
             extra["roofline_agg_bwd"]["traffic"] = load_traffic(wkey, "gat_agg_bwd")
         proj_ev = summ.get("mvml_gat_proj_fwd", [])
         gemm_ev = (summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", [])
-                   + summ.get("mvml_gemm_f32x3_batched", []) + ([] if args.proj_bf16 else proj_ev))
+                   + summ.get("mvml_gemm_f32x3_batched", []) + summ.get("mvml_lstm_gates_cell_fwd", [])
+                   + ([] if args.proj_bf16 else proj_ev))
         bf_ev = summ.get("mvml_gemm_bf16", []) + (proj_ev if args.proj_bf16 else [])
         if bf_ev:
             extra["roofline_gemm_bf16"] = roofline_entry(bf_ev, "mfma")

@@ -219,6 +219,16 @@ int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_
  * NULL: the cell's output is both its own recurrent input and the next layer's input, each
  * stored inside a combined [x | h_prev] GEMM operand row.
  * ------------------------------------------------------------------------------------- */
+/* The gates GEMM with the LSTM cell as its epilogue (Set2Set's cells): pre = A w_perm^T for the
+ * D units with w_perm's rows INTERLEAVED (row 4 j + q = row q D + j of [W_ih | W_hh]; K of its
+ * columns used, row stride ldw), then exactly mvml_lstm_cell_fwd (b_ih, b_hh gate-major; c_prev
+ * may be null) — the gate pre-activations are never stored.  Requires the 256x256 plan without
+ * split-K (mvml_lstm_gates_cell_plan_ok(M, D, K) != 0) and 16-B aligned rows. */
+int mvml_lstm_gates_cell_plan_ok(int64_t M, int D, int64_t K);
+int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float* A, int64_t lda,
+                             const float* w_perm, int64_t ldw, const float* b_ih,
+                             const float* b_hh, const float* c_prev, float* c_out, float* h_out,
+                             int64_t ldh, float* act, float* h_out2, int64_t ldh2, void* stream);
 int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_ih,
                        const float* b_hh, const float* c_prev, float* c_out, float* h_out,
                        int64_t ldh, float* act_out, float* h_out2, int64_t ldh2, void* stream);

@@ -269,6 +269,24 @@ struct BatchStrides {
   int64_t a = 0, b = 0, c = 0;
 };
 
+// LSTM cell in the GEMM epilogue (D > 0): the product is the gate pre-activation block of D
+// units with the weight rows INTERLEAVED (column 4 j + q = gate q of unit j), so a lane's
+// row-contiguous float4 is one unit's (i, f, g, o); it adds b_ih + b_hh (gate-major, as
+// nn.LSTM stores them), runs lstm_cell_fwd_kernel's arithmetic in its order and writes c, h
+// (twice), and the activations act[row][q D + j] (gate-major) instead of the gates.
+struct CellEpi {
+  const float* b_ih = nullptr;
+  const float* b_hh = nullptr;
+  const float* c_prev = nullptr;  // [M][D] or null (zero state)
+  float* c_out = nullptr;         // [M][D]
+  float* h_out = nullptr;         // row stride ldh
+  float* h_out2 = nullptr;        // row stride ldh2, or null
+  float* act = nullptr;           // [M][4 D]
+  int64_t ldh = 0, ldh2 = 0;
+  int D = 0;
+};
+__device__ __forceinline__ float sigm_epi(float x) { return 1.f / (1.f + expf(-x)); }
+
 struct ProjEpi {
   const float* vec;  // [2][cols]
   int cols;          // H*F
@@ -847,7 +865,8 @@ __device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], floa
                                                  int64_t N, int64_t r0, int64_t c0, int lane,
                                                  const float* __restrict__ bias, float beta, int act,
                                                  float* __restrict__ C, int64_t ldc,
-                                                 float* __restrict__ slab) {
+                                                 float* __restrict__ slab,
+                                                 const CellEpi& cep = CellEpi{}) {
   const int li = lane & 31, lk = lane >> 5;
   float* out = slab ? slab + (int64_t)blockIdx.y * M * N : C;
   const int64_t ld = slab ? N : ldc;
@@ -867,6 +886,27 @@ __device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], floa
       const int64_t row = r0 + 32 * i + rr, col = c0 + c4;
       if (row >= M || col >= N) continue;
       float4 v = *reinterpret_cast<const float4*>(wl + rr * kEpiLd + c4);
+      if (cep.D > 0) {  // LSTM cell (host: N = 4 D, no split-K): one unit's four gates
+        const int D = cep.D;
+        const int64_t j = col >> 2;
+        const float gi = v.x + cep.b_ih[j] + cep.b_hh[j];
+        const float gf = v.y + cep.b_ih[D + j] + cep.b_hh[D + j];
+        const float gg = v.z + cep.b_ih[2 * D + j] + cep.b_hh[2 * D + j];
+        const float go = v.w + cep.b_ih[3 * D + j] + cep.b_hh[3 * D + j];
+        const float ig = sigm_epi(gi), fg = sigm_epi(gf), gt = tanhf(gg), og = sigm_epi(go);
+        const float cpv = cep.c_prev ? cep.c_prev[row * D + j] : 0.f;
+        const float c = fg * cpv + ig * gt;
+        const float h = og * tanhf(c);
+        cep.c_out[row * D + j] = c;
+        cep.h_out[row * cep.ldh + j] = h;
+        if (cep.h_out2) cep.h_out2[row * cep.ldh2 + j] = h;
+        float* a = cep.act + row * 4 * (int64_t)D + j;
+        a[0] = ig;
+        a[D] = fg;
+        a[2 * D] = gt;
+        a[3 * D] = og;
+        continue;
+      }
       float* cp = out + row * ld + col;
       if (vec && col + 3 < N) {
         if (!slab) {
@@ -930,7 +970,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
                 float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{},
-                BatchStrides bst = BatchStrides{}) {
+                BatchStrides bst = BatchStrides{}, CellEpi cep = CellEpi{}) {
   if (blockIdx.z) {  // strided batch
     A += blockIdx.z * bst.a;
     B += blockIdx.z * bst.b;
@@ -1026,7 +1066,11 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     OB::load(B, ldb, n0, N, k0, kend, b_vec && n0 + XBN <= N && kin, tid, vb);
   };
   auto stage = [&](int buf) {
+#ifdef MVML_ABL_NOSPLIT_A  // ablation: A's planes written without the split (wrong results)
+    OA::raw_store(lds + buf * kStage, tid, va);
+#else
     OA::split_store(lds + buf * kStage, tid, va);
+#endif
 #ifdef MVML_ABL_NOSPLIT_B  // ablation: B's planes written without the split (wrong results)
     OB::raw_store(lds + buf * kStage + OA::kBytes, tid, vb);
 #else
@@ -1258,7 +1302,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     tile_epilogue<EPI_LOGW, 4, 2, false>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta,
                                          act, C, ldc, slab, epi);
   epilogue_lds_256(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
-                   n0 + wn * 64, lane, bias, beta, act, C, ldc, slab);
+                   n0 + wn * 64, lane, bias, beta, act, C, ldc, slab, cep);
 #else
   tile_epilogue<EPI_LOGW, 4, 2>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta, act, C,
                                 ldc, slab, epi);
@@ -1442,6 +1486,39 @@ extern "C" int mvml_gemm_f32x3_batched(int a_kmajor, int b_kmajor, int64_t M, in
                "gemm_batched: bad batch / strides");
   return gemm_launch(kPrecX3, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
                      nullptr, 0, stream, batch, BatchStrides{stride_a, stride_b, stride_c});
+}
+
+extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float* A, int64_t lda,
+                                        const float* w_perm, int64_t ldw, const float* b_ih,
+                                        const float* b_hh,
+                                        const float* c_prev, float* c_out, float* h_out,
+                                        int64_t ldh, float* act, float* h_out2, int64_t ldh2,
+                                        void* stream) {
+  clear_error();
+  MVML_REQUIRE(M >= 0 && D > 0 && K > 0 && lda >= K && ldw >= K && ldh >= D &&
+                   (!h_out2 || ldh2 >= D) && MVML_X3W_LDSEPI,
+               "lstm_gates_cell_fwd: bad shape");
+  if (M == 0) return MVML_OK;
+  const int64_t N = 4 * (int64_t)D;
+  const GemmPlan plan = plan_gemm(kPrecX3, M, N, K);
+  const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0);
+  const int bv = (ldw % 4 == 0) && ((uintptr_t)w_perm % 16 == 0);
+  MVML_REQUIRE(plan.wide && plan.S == 1 && x3w_fast(false, false, M, N, K, av, bv),
+               "lstm_gates_cell_fwd: needs the 256x256 plan without split-K and aligned rows "
+               "(use mvml_gemm_f32x3 + mvml_lstm_cell_fwd)");
+  const int64_t tiles = ceil_div(M, XBM) * ceil_div(N, XBN);
+  CellEpi cep;
+  cep.b_ih = b_ih; cep.b_hh = b_hh; cep.c_prev = c_prev; cep.c_out = c_out; cep.h_out = h_out;
+  cep.h_out2 = h_out2; cep.act = act; cep.ldh = ldh; cep.ldh2 = ldh2; cep.D = D;
+  gemm_x3w_kernel<false, false, -1, true><<<dim3(x3w_grid_x(tiles, 1), 1, 1), kXThreads, 0, as_stream(stream)>>>(
+      M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
+      BatchStrides{}, cep);
+  return check_launch("gemm_x3w_kernel(lstm cell)");
+}
+
+extern "C" int mvml_lstm_gates_cell_plan_ok(int64_t M, int D, int64_t K) {
+  const GemmPlan plan = plan_gemm(kPrecX3, M, 4 * (int64_t)D, K);
+  return plan.wide && plan.S == 1 && K % 4 == 0;
 }
 
 extern "C" int mvml_gemm_bf16(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,

@@ -194,6 +194,11 @@ class GATLayerFunction(torch.autograd.Function):
         return gX, g_fc, g_res, g_al, g_ar, g_bias, None, None, None, None, None, None
 
 
+# Set2Set's gates GEMM + LSTM cell as one launch (mvml_lstm_gates_cell_fwd: the cell in the
+# GEMM epilogue, interleaved weight rows) where the 256x256 plan applies; False: GEMM + cell
+CELL_EPI = True
+
+
 class Set2SetFunction(torch.autograd.Function):
     """dgl Set2Set.forward (model.py:92): n_iters x {n_layers LSTM cell steps, fused segment
     softmax readout}.  LSTM gates: one MFMA GEMM per cell over [x | h_prev] + pointwise kernel."""
@@ -220,6 +225,10 @@ class Set2SetFunction(torch.autograd.Function):
         for l in range(1, Lr):
             XH[l][0, :, D:].zero_()
         Wcat = [torch.cat([w[0], w[1]], dim=1).contiguous() for w in W]
+        L = _lib.lib()
+        # interleaved rows for the cell epilogue: row 4 j + q = row q D + j (unit j's i, f, g, o)
+        Wperm = [Wcat[l].view(4, D, kin[l] + D).transpose(0, 1).reshape(4 * D, kin[l] + D).contiguous()
+                 if CELL_EPI else None for l in range(Lr)]
         acts = torch.empty((T, Lr, B, 4 * D), **f32)
         cs = torch.empty((T, Lr, B, D), **f32)
         lse = torch.empty((T, B), **f32)
@@ -228,16 +237,22 @@ class Set2SetFunction(torch.autograd.Function):
             for l in range(Lr):
                 w_ih, w_hh, b_ih, b_hh = W[l]
                 K = kin[l] + D if t > 0 else kin[l]  # h_l(-1) = 0: the recurrent half is skipped
+                own = XH[l][t + 1][:, kin[l]:]
+                nxt = XH[l + 1][t] if l < Lr - 1 else XH[0][t + 1]
+                c_prev = cs[t - 1, l] if t > 0 else None
+                ldn = kin[l + 1] + D if l < Lr - 1 else 3 * D
+                if CELL_EPI and not (t == 0 and l == 0) and L.mvml_lstm_gates_cell_plan_ok(B, D, K):
+                    _lib.call_tag[0] = {"flops": 2 * B * 4 * D * K, "shape": (B, 4 * D, K, 0, 0, "cell")}
+                    call("mvml_lstm_gates_cell_fwd", B, D, K, ptr(XH[l][t]), kin[l] + D, ptr(Wperm[l]),
+                         kin[l] + D, ptr(b_ih), ptr(b_hh), ptr(c_prev), ptr(cs[t, l]), ptr(own),
+                         kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, st)
+                    continue
                 if t == 0 and l == 0:
                     gates.zero_()  # q*_{-1} = 0 and h_0(-1) = 0
                 else:
                     gemm(XH[l][t], Wcat[l], B, 4 * D, K, 0, 0, kin[l] + D, kin[l] + D, gates, 4 * D)
-                own = XH[l][t + 1][:, kin[l]:]
-                nxt = XH[l + 1][t] if l < Lr - 1 else XH[0][t + 1]
-                c_prev = cs[t - 1, l] if t > 0 else None
                 call("mvml_lstm_cell_fwd", B, D, ptr(gates), ptr(b_ih), ptr(b_hh), ptr(c_prev),
-                     ptr(cs[t, l]), ptr(own), kin[l] + D, ptr(acts[t, l]), ptr(nxt),
-                     kin[l + 1] + D if l < Lr - 1 else 3 * D, st)
+                     ptr(cs[t, l]), ptr(own), kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, st)
             call("mvml_set2set_seg_fwd", B, D, ptr(g.node_offsets), ptr(X), ptr(XH[0][t + 1]), 3 * D,
                  ptr(lse[t]), st)
         ctx.save_for_backward(X, acts, cs, lse, *XH, *[p for w in W for p in w])

@@ -281,6 +281,37 @@ def test_set2set_parity():
         assert rel_err(p.grad, p2.grad) < TOL, n
 
 
+def test_set2set_cell_epilogue_bitwise():
+    """Set2Set at a width where the gates GEMM takes the 256x256 plan (16,384 molecules): the
+    fused gates + LSTM-cell epilogue (mvml_lstm_gates_cell_fwd) equals the GEMM + cell kernel
+    path bit for bit (same MFMA accumulation per element, same cell arithmetic), forward and
+    backward; the unfused path is the one pinned to the float64 oracle above."""
+    import mvml_gat.functional as fn
+    from mvml_gat import _lib
+    from mvml_gat.nn import Set2Set
+    sb = batch_of_sizes([3, 5, 2, 7] * 4096, seed=4)
+    assert _lib.lib().mvml_lstm_gates_cell_plan_ok(16384, 384, 1152)
+    g = _to_dev(sb)
+    torch.manual_seed(1)
+    s2s = Set2Set(384, 6, 3).to(DEV)
+    X = torch.randn(int(sb.num_nodes.sum()), 384, device=DEV)
+    gout = torch.randn(16384, 768, device=DEV)
+    res = []
+    for fused in (True, False):
+        old = fn.CELL_EPI
+        fn.CELL_EPI = fused
+        try:
+            s2s.zero_grad()
+            Xp = X.clone().requires_grad_()
+            out = s2s(g, Xp)
+            out.backward(gout)
+            res.append([out.detach().clone(), Xp.grad.clone()] + [p.grad.clone() for p in s2s.parameters()])
+        finally:
+            fn.CELL_EPI = old
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_graphnorm_parity():
     from mvml_gat.nn import GraphNorm
     x = torch.randn(164, 768, dtype=torch.float64) * 3 + 1
