@@ -49,7 +49,7 @@ TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32
          "mvml_token_attn_fwd", "mvml_token_attn_bwd", "mvml_token_attn_fold_fwd",
          "mvml_token_attn_fold_bwd", "mvml_gemm_f32x3_batched", "mvml_conv3_fwd", "mvml_conv3_bwd",
          "mvml_bce_logits", "mvml_gat_attn_grad", "mvml_bilstm_seq_fwd", "mvml_bilstm_seq_bwd",
-         "mvml_lstm_gates_cell_fwd"]
+         "mvml_lstm_gates_cell_fwd", "mvml_gemm_f16x2", "mvml_gemm_f16x2_amax", "mvml_absmax_f32"]
 
 
 def parse(argv=None):
@@ -320,6 +320,7 @@ def run(args):
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     from mvml_gat.dist import EmbeddingAllGather, FlatGradAllReduce
+    from mvml_gat import functional as F
     if not args.dry_run:
         import mvml_gat
         from mvml_gat import _lib
@@ -447,6 +448,7 @@ def run(args):
         rows = kernel_report(summ, ms_per_step, args.steps)
         if os.environ.get("MVML_GEMM_SHAPES") and rank == 0:
             gemm_shape_report(summ.get("mvml_gemm_f32x3", []) + summ.get("mvml_gemm_f32x3_batched", [])
+                              + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])
                               + summ.get("mvml_lstm_gates_cell_fwd", [])
                               + summ.get("mvml_gat_proj_fwd", []), args.steps)
         if rank == 0:
@@ -464,6 +466,7 @@ def run(args):
             extra["roofline_agg_bwd"]["traffic"] = load_traffic(wkey, "gat_agg_bwd")
         proj_ev = summ.get("mvml_gat_proj_fwd", [])
         gemm_ev = (summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", [])
+                   + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])
                    + summ.get("mvml_gemm_f32x3_batched", []) + summ.get("mvml_lstm_gates_cell_fwd", [])
                    + ([] if args.proj_bf16 else proj_ev))
         bf_ev = summ.get("mvml_gemm_bf16", []) + (proj_ev if args.proj_bf16 else [])
@@ -474,7 +477,15 @@ def run(args):
                 frac=round(extra["roofline_gemm_bf16"]["achieved"] / BF16_MFMA_PEAK_TFS, 4))
         if gemm_ev:
             extra["roofline_gemm"] = roofline_entry(gemm_ev, "mfma")
-            if summ.get("mvml_gemm_f32x3"):
+            if summ.get("mvml_gemm_f16x2") or summ.get("mvml_gemm_f16x2_amax"):
+                # scaled split-fp16: 3 fp16 MFMA per fp32 multiply-add -> fp32-equivalent peak
+                # 2.5 PF / 3 (the skinny products that fall back to split-bf16 count against it too)
+                extra["roofline_gemm"].update(
+                    peak=BF16_MFMA_PEAK_TFS / 3, note="fp32-accurate scaled split-fp16 on fp16 MFMA "
+                    "(3 MFMA per fp32 product); achieved is fp32-equivalent TFLOP/s, peak = dense "
+                    "fp16 MFMA peak / 3; operand |max| passes (mvml_absmax_f32) timed separately")
+                extra["roofline_gemm"]["frac"] = round(extra["roofline_gemm"]["achieved"] / (BF16_MFMA_PEAK_TFS / 3), 4)
+            elif summ.get("mvml_gemm_f32x3"):
                 # split-bf16: 6 bf16 MFMA per fp32 multiply-add -> fp32-equivalent peak 2.5 PF / 6
                 extra["roofline_gemm"].update(
                     peak=BF16_MFMA_PEAK_TFS / 6, note="fp32-accurate split-bf16 (x3) on bf16 MFMA; "
@@ -566,7 +577,8 @@ def run(args):
                        "atoms_per_step_rank0": batches[0].N, "edges_per_step_rank0": batches[0].E,
                        "graphnorm_group": gsz, "parallelism": f"dp{world}",
                        "projection": "bf16 operands, fp32 accumulate (config 4)" if args.proj_bf16
-                       else "fp32-accurate split-bf16 x3"},
+                       else {"x3": "fp32-accurate split-bf16 x3", "f16x2": "fp32-accurate scaled split-fp16",
+                             "f32": "f32 MFMA"}.get(F.GEMM_ALGO, F.GEMM_ALGO)},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         line.update(extra)

@@ -121,9 +121,36 @@ int mvml_gemm_bf16(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                    const float* A, int64_t lda, const float* B, int64_t ldb,
                    const float* bias, float beta, int act, float* C, int64_t ldc,
                    void* workspace, size_t workspace_bytes, void* stream);
+/* Same contract at fp32 accuracy on fp16 MFMA (v_mfma_f32_32x32x16_f16), half the MFMAs of
+ * mvml_gemm_f32x3: each operand is scaled by a power of two s (|max| s in [2^14, 2^15), from a
+ * deterministic |max| pass over the operand) and split into x s = h + l with h = f16(x s),
+ * l = f16(x s - h) (22 significant bits; representation error <= 2^-22 relative, plus 2^-40 of
+ * the operand's |max| absolute where l is subnormal); the product keeps h_a h_b + h_a l_b +
+ * l_a h_b (the dropped l_a l_b is < 2^-22 relative), fp32 accumulate, and the result is scaled
+ * back by 1 / (s_a s_b) exactly.  Errors against fp64 are those of an fp32 GEMM
+ * (tests/test_gpu_parity.py).  Products whose plan is not the 256x256 tile (skinny outputs)
+ * run the split-bf16 kernels.  Workspace as mvml_gemm_f32 (its first 256 B hold the maxima). */
+int mvml_gemm_f16x2(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                    const float* A, int64_t lda, const float* B, int64_t ldb,
+                    const float* bias, float beta, int act, float* C, int64_t ldc,
+                    void* workspace, size_t workspace_bytes, void* stream);
+/* mvml_gemm_f16x2 with the operand maxima supplied: *amax_a / *amax_b = bits of max |A| /
+ * max |B| over (at least) the elements the product reads, e.g. from mvml_absmax_f32 — one pass
+ * serves every product that reads the operand.  A bound above the true max is allowed (costs
+ * accuracy only if it exceeds it by more than ~2^10). */
+int mvml_gemm_f16x2_amax(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                         const float* A, int64_t lda, const float* B, int64_t ldb,
+                         const uint32_t* amax_a, const uint32_t* amax_b, const float* bias,
+                         float beta, int act, float* C, int64_t ldc, void* workspace,
+                         size_t workspace_bytes, void* stream);
+/* out[0] = bits of max |P[r*ld + c]| over r < rows, c < cols (accumulate != 0: max with the
+ * current out[0]); deterministic (unsigned atomicMax of non-negative float bits). */
+int mvml_absmax_f32(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32_t* out,
+                    int accumulate, void* stream);
 #define MVML_GEMM_F32 0   /* algo: v_mfma_f32_32x32x2_f32 */
 #define MVML_GEMM_F32X3 1 /* algo: split-bf16 x3 */
 #define MVML_GEMM_BF16 2  /* algo: bf16 operands, fp32 accumulate */
+#define MVML_GEMM_F16X2 3 /* algo: scaled split-fp16 (mvml_gemm_f16x2) */
 /* Column sums: out[n] = beta*out[n] + alpha * sum_m X[m*ldx + n], deterministic two-stage
  * tree.  Replaces the bias gradients torch autograd computes for GATConv.bias / LSTM / Linear. */
 size_t mvml_colsum_workspace_size(int64_t M, int64_t N);
@@ -161,12 +188,14 @@ int mvml_gat_unfold_grads(const float* gWcat, const float* attn_lr, int H, int F
  * (`(feat_src * attn_l).sum(-1)`), computed in the GEMM epilogue as per-32-column partial dots
  * of the fp32 Z tile and summed per head in fixed order — no second pass over Z.
  * attn_lr: [2, H*F] = [attn_l | attn_r]; elr: [N, 2H] = [el | er].  F % 32 == 0.
- * workspace: mvml_gat_proj_fwd_workspace_size(N, H, F) bytes (the partials). */
+ * algo MVML_GEMM_F16X2: amax_x / amax_w = bits of max |X| / max |Wcat| (mvml_absmax_f32), or
+ * both NULL (computed here).  workspace: mvml_gat_proj_fwd_workspace_size(N, H, F) bytes. */
 size_t mvml_gat_proj_fwd_workspace_size(int64_t num_nodes, int H, int F);
 int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx, int64_t K,
                       const float* Wcat, int64_t ldw, const float* attn_lr, int H, int F,
                       int mean_residual, int algo /* MVML_GEMM_* */, float* Y, int64_t ldy,
-                      float* elr, void* workspace, size_t workspace_bytes, void* stream);
+                      float* elr, const uint32_t* amax_x, const uint32_t* amax_w,
+                      void* workspace, size_t workspace_bytes, void* stream);
 /* dL/dattn_l[h,f] = sum_n gelr[n, h] * Z[n, h*F+f] and dL/dattn_r with gelr[n, H+h] (autograd
  * of `(feat * attn_l).sum(-1)` in GATConv.forward); gelr rows [d el | d er] have stride ldgl
  * (the backward's gY + C, ldgy); deterministic two-stage reduction. */
@@ -228,7 +257,10 @@ int mvml_lstm_gates_cell_plan_ok(int64_t M, int D, int64_t K);
 int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float* A, int64_t lda,
                              const float* w_perm, int64_t ldw, const float* b_ih,
                              const float* b_hh, const float* c_prev, float* c_out, float* h_out,
-                             int64_t ldh, float* act, float* h_out2, int64_t ldh2, void* stream);
+                             int64_t ldh, float* act, float* h_out2, int64_t ldh2,
+                             const uint32_t* amax_a, const uint32_t* amax_b /* both NULL:
+                               split-bf16; else split-fp16 with these |A|, |w_perm| max bits */,
+                             void* stream);
 int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_ih,
                        const float* b_hh, const float* c_prev, float* c_out, float* h_out,
                        int64_t ldh, float* act_out, float* h_out2, int64_t ldh2, void* stream);

@@ -1681,14 +1681,15 @@ extern "C" int mvml_gat_proj_cols(int H, int F, int mean_residual) {
 }
 
 extern "C" size_t mvml_gat_proj_fwd_workspace_size(int64_t num_nodes, int H, int F) {
-  return carve_size((size_t)num_nodes * 2 * (H * F / (1 << proj_logw(F))) * sizeof(float));
+  // logit partials, then 256 B for the split-fp16 operand maxima
+  return carve_size((size_t)num_nodes * 2 * (H * F / (1 << proj_logw(F))) * sizeof(float)) + 256;
 }
 
 extern "C" int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx, int64_t K,
                                  const float* Wcat, int64_t ldw, const float* attn_lr, int H,
                                  int F, int mean_residual, int algo, float* Y, int64_t ldy,
-                                 float* elr, void* workspace, size_t workspace_bytes,
-                                 void* stream) {
+                                 float* elr, const uint32_t* amax_x, const uint32_t* amax_w,
+                                 void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
   MVML_REQUIRE(H == 1 || H == 2 || H == 4 || H == 8, "gat_proj_fwd: num_heads must be 1, 2, 4 or 8 (got %d)", H);
   MVML_REQUIRE(F > 0 && F % 4 == 0, "gat_proj_fwd: out_feats must be a positive multiple of 4 (got %d)", F);
@@ -1703,10 +1704,14 @@ extern "C" int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx,
   MVML_REQUIRE(attn_lr != nullptr && elr != nullptr, "gat_proj_fwd: attn_lr and elr are required");
   hipStream_t st = as_stream(stream);
   float* part = static_cast<float*>(workspace);
-  MVML_REQUIRE(algo == MVML_GEMM_F32 || algo == MVML_GEMM_F32X3 || algo == MVML_GEMM_BF16,
+  MVML_REQUIRE(algo == MVML_GEMM_F32 || algo == MVML_GEMM_F32X3 || algo == MVML_GEMM_BF16 ||
+                   algo == MVML_GEMM_F16X2,
                "gat_proj_fwd: bad algo %d", algo);
+  uint32_t* amax_ws = reinterpret_cast<uint32_t*>(
+      static_cast<uint8_t*>(workspace) +
+      carve_size((size_t)num_nodes * 2 * (H * F / (1 << proj_logw(F))) * sizeof(float)));
   int rc = gemm_proj_epi(algo, num_nodes, C, K, X, ldx, Wcat, ldw, Y, ldy,
-                         attn_lr, H * F, proj_logw(F), part, st);
+                         attn_lr, H * F, proj_logw(F), part, amax_ws, amax_x, amax_w, st);
   if (rc) return rc;
   const int W = 1 << proj_logw(F);
   const unsigned blocks = (unsigned)ceil_div(num_nodes * 2 * H, 256);

@@ -80,13 +80,50 @@ __device__ __forceinline__ f32x16 mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b
   return acc;
 }
 
-// NP = 3: the split-bf16 product above; NP = 1: one bf16 MFMA (bf16 operands, fp32 accumulate).
+// Scaled split-fp16 (NP = 2): an operand scaled by a power of two s (its |max| lands in
+// [2^14, 2^15)) is split into x s = h + l, h = f16(x s), l = f16(x s - h): 2 x 11 significant
+// bits, representation error <= 2^-22 |x s| (plus 2^-25 absolute in scaled units for values
+// 2^18 below the operand's max, where l is subnormal).  The product keeps h_a h_b + h_a l_b +
+// l_a h_b (dropped l_a l_b < 2^-22 relative); fp16 products are exact in fp32, so the result has
+// the accuracy of an fp32 GEMM at 3 MFMAs per fragment pair instead of 6.  The epilogue
+// multiplies by 1/(s_a s_b) (exact).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void split2h(const float4& v, float s, uint2& p0, uint2& p1) {
+  const f32x2 u = {v.x * s, v.y * s}, w = {v.z * s, v.w * s};
+  const f16x2 hu = __builtin_convertvector(u, f16x2), hw = __builtin_convertvector(w, f16x2);
+  const f32x2 ru = u - __builtin_convertvector(hu, f32x2), rw = w - __builtin_convertvector(hw, f32x2);
+  p0.x = __builtin_bit_cast(uint32_t, hu);
+  p0.y = __builtin_bit_cast(uint32_t, hw);
+  p1.x = __builtin_bit_cast(uint32_t, __builtin_convertvector(ru, f16x2));
+  p1.y = __builtin_bit_cast(uint32_t, __builtin_convertvector(rw, f16x2));
+}
+
+// Scale of an operand from its |max| bits (non-negative float bits order as integers): 2^k with
+// k = 141 - biased exponent, so |max| s < 2^15 (fp16 max 65504); k clamped to [-100, 100] (zero
+// / tiny operands: any scale works; a NaN max gives NaN results either way).
+__device__ __forceinline__ int amax_shift(uint32_t bits) {
+  const int k = 141 - (int)((bits >> 23) & 0xff);
+  return k < -100 ? -100 : (k > 100 ? 100 : k);
+}
+__device__ __forceinline__ float pow2f(int k) { return __uint_as_float((uint32_t)(k + 127) << 23); }
+
+// NP = 3: the split-bf16 product above; NP = 2: scaled split-fp16; NP = 1: one bf16 MFMA (bf16
+// operands, fp32 accumulate).
 template <int NP>
 __device__ __forceinline__ f32x16 mfma_np(const bf16x8 (&a)[NP], const bf16x8 (&b)[NP], f32x16 acc) {
-  if constexpr (NP == 3)
+  if constexpr (NP == 3) {
     return mfma_x3(a, b, acc);
-  else
+  } else if constexpr (NP == 2) {
+    const f16x8 a0 = __builtin_bit_cast(f16x8, a[0]), a1 = __builtin_bit_cast(f16x8, a[1]);
+    const f16x8 b0 = __builtin_bit_cast(f16x8, b[0]), b1 = __builtin_bit_cast(f16x8, b[1]);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
+  } else {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  }
 }
 
 constexpr int BM = 128, BN = 128, BKT = 32, kThreads = 256;
@@ -265,6 +302,12 @@ __device__ __forceinline__ float comp(const float4& v, int s) {
 // (values 32 -> 32/W, masks W/2 .. 1) leaves lane li with the values of index
 // ((li & (W-1)) << (5 - EPI_LOGW)) | t, index = side * 16 + row register.
 // Strided batch (blockIdx.z): product z reads A + z a, B + z b and writes C + z c (floats).
+// Split-fp16 operand maxima: bits of max |A| and max |B| (device pointers, may alias).
+struct AmaxPtrs {
+  const uint32_t* a = nullptr;
+  const uint32_t* b = nullptr;
+};
+
 struct BatchStrides {
   int64_t a = 0, b = 0, c = 0;
 };
@@ -781,12 +824,15 @@ struct XOp {
   __device__ static __forceinline__ int64_t kstep(int64_t ld) { return KMAJ ? XBK * ld : XBK; }
 
 
-  __device__ static __forceinline__ void split_store(uint8_t* op, int tid, const float4 (&v)[2]) {
+  __device__ static __forceinline__ void split_store(uint8_t* op, int tid, const float4 (&v)[2],
+                                                     float s = 1.f) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       uint2 p0, p1, p2;
       if constexpr (NP == 3) {
         split4(v[i].x, v[i].y, v[i].z, v[i].w, p0, p1, p2);
+      } else if constexpr (NP == 2) {
+        split2h(v[i], s, p0, p1);
       } else {  // bf16 operands: round-to-nearest-even, one plane
         const f32x2 u = {v[i].x, v[i].y}, w = {v[i].z, v[i].w};
         p0.x = __builtin_bit_cast(uint32_t, __builtin_convertvector(u, bf16x2));
@@ -800,10 +846,8 @@ struct XOp {
         off = (2 * (tid >> 6) + i) * kXKmajPitch + 8 * (tid & 63);
       }
       *reinterpret_cast<uint2*>(op + off) = p0;
-      if constexpr (NP == 3) {
-        *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
-        *reinterpret_cast<uint2*>(op + 2 * kPlane + off) = p2;
-      }
+      if constexpr (NP >= 2) *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
+      if constexpr (NP == 3) *reinterpret_cast<uint2*>(op + 2 * kPlane + off) = p2;
     }
   }
 
@@ -821,10 +865,8 @@ struct XOp {
         off = (2 * (tid >> 6) + i) * kXKmajPitch + 8 * (tid & 63);
       }
       *reinterpret_cast<uint2*>(op + off) = p0;
-      if constexpr (NP == 3) {
-        *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
-        *reinterpret_cast<uint2*>(op + 2 * kPlane + off) = p0;
-      }
+      if constexpr (NP >= 2) *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
+      if constexpr (NP == 3) *reinterpret_cast<uint2*>(op + 2 * kPlane + off) = p0;
     }
   }
 
@@ -970,7 +1012,8 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
                 float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{},
-                BatchStrides bst = BatchStrides{}, CellEpi cep = CellEpi{}) {
+                BatchStrides bst = BatchStrides{}, CellEpi cep = CellEpi{},
+                AmaxPtrs amax = AmaxPtrs{}) {
   if (blockIdx.z) {  // strided batch
     A += blockIdx.z * bst.a;
     B += blockIdx.z * bst.b;
@@ -978,6 +1021,13 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   }
   using OA = XOp<AK, NP>;
   using OB = XOp<BKM, NP>;
+  // NP = 2: operand scales from the |max| bits of A and B
+  int ka = 0, kb = 0;
+  if constexpr (NP == 2) {
+    ka = amax_shift(*amax.a);
+    kb = amax_shift(*amax.b);
+  }
+  const float s_a = pow2f(ka), s_b = pow2f(kb);
   constexpr int kStage = OA::kBytes + OB::kBytes;
   // double-buffered stages; the LDS epilogue reuses the space (8 waves x 32 rows x kEpiLd)
   constexpr int kLdsBytes = 2 * kStage > 8 * 32 * kEpiLd * 4 ? 2 * kStage : 8 * 32 * kEpiLd * 4;
@@ -1069,12 +1119,12 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #ifdef MVML_ABL_NOSPLIT_A  // ablation: A's planes written without the split (wrong results)
     OA::raw_store(lds + buf * kStage, tid, va);
 #else
-    OA::split_store(lds + buf * kStage, tid, va);
+    OA::split_store(lds + buf * kStage, tid, va, s_a);
 #endif
 #ifdef MVML_ABL_NOSPLIT_B  // ablation: B's planes written without the split (wrong results)
     OB::raw_store(lds + buf * kStage + OA::kBytes, tid, vb);
 #else
-    OB::split_store(lds + buf * kStage + OA::kBytes, tid, vb);
+    OB::split_store(lds + buf * kStage + OA::kBytes, tid, vb, s_b);
 #endif
   };
 #ifndef MVML_X3W_PRIO
@@ -1153,12 +1203,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #pragma unroll
       for (int p = 0; p < NP; ++p) fa[p] = OA::frag(sa, p, wm * 128 + 32 * i, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if constexpr (NP == 3)
-          acc[i][j] = mfma_x3(fa, fb[j], acc[i][j]);
-        else
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][0], acc[i][j], 0, 0, 0);
-      }
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma_np<NP>(fa, fb[j], acc[i][j]);
     }
     if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(0);
 #if MVML_X3W_STAGGER
@@ -1193,8 +1238,8 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       load_masked_into(k, ra[decltype(SET)::value], rb[decltype(SET)::value]);
     };
     auto stg = [&](auto SET, int buf) {
-      OA::split_store(lds + buf * kStage, tid, ra[decltype(SET)::value]);
-      OB::split_store(lds + buf * kStage + OA::kBytes, tid, rb[decltype(SET)::value]);
+      OA::split_store(lds + buf * kStage, tid, ra[decltype(SET)::value], s_a);
+      OB::split_store(lds + buf * kStage + OA::kBytes, tid, rb[decltype(SET)::value], s_b);
     };
     auto body2 = [&](int64_t t, auto SET, auto STAGE, auto LOAD) {
       const uint8_t* sa = lds + (t & 1) * kStage;
@@ -1295,6 +1340,15 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[i][j]));
   continue;
 #endif
+  if constexpr (NP == 2) {  // undo the operand scales (exact: powers of two)
+    const float ua = pow2f(-ka), ub = pow2f(-kb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ua * ub;
+  }
 #if MVML_X3W_LDSEPI
   // the projection's logit partials straight from the accumulators, then C through LDS (every
   // K loop ends with a workgroup barrier, so the staging buffers are free)
@@ -1360,7 +1414,7 @@ struct GemmPlan {
   bool wide;
   int S;
 };
-constexpr int kPrecF32 = 0, kPrecX3 = 1, kPrecBf16 = 2;  // = MVML_GEMM_* algo ids
+constexpr int kPrecF32 = 0, kPrecX3 = 1, kPrecBf16 = 2, kPrecF16x2 = 3;  // = MVML_GEMM_* ids
 GemmPlan plan_gemm(int prec, int64_t M, int64_t N, int64_t K) {
   const char* env = getenv("MVML_X3_TILE");
   const int force = env ? atoi(env) : 0;
@@ -1368,7 +1422,8 @@ GemmPlan plan_gemm(int prec, int64_t M, int64_t N, int64_t K) {
     const int64_t tw = ceil_div(M, XBM) * ceil_div(N, XBN);
     return {true, choose_splits_t(tw, K, 256)};
   }
-  if (prec == kPrecX3) {
+  // split-fp16 exists only in the 256x256 kernel; its 128x128 fallback is the split-bf16 plan
+  if (prec == kPrecX3 || prec == kPrecF16x2) {
     const int64_t tw = ceil_div(M, XBM) * ceil_div(N, XBN);
     const int Sw = choose_splits_t(tw, K, 256);
     // skinny outputs (N = 76 / 384 columns of weight gradients): the 256x256 tile computes
@@ -1433,6 +1488,59 @@ __global__ void colsum_final_kernel(int64_t N, int S, const float* __restrict__ 
   out[col] = (beta != 0.f ? beta * out[col] : 0.f) + alpha * t;
 }
 
+// |max| of a stored rows x cols fp32 matrix (row pitch ld) folded into *out as float bits:
+// non-negative float bits order like the values, so an unsigned atomicMax per workgroup is
+// order-independent (deterministic).  Four independent rows in flight per thread.
+__global__ void __launch_bounds__(256) absmax_kernel(int64_t rows, int64_t cols,
+                                                     const float* __restrict__ P, int64_t ld,
+                                                     int vec, uint32_t* __restrict__ out) {
+  float m[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t rs = gridDim.y;
+  if (vec) {  // cols % 4 == 0, ld % 4 == 0, 16-B aligned base: c indexes float4 columns
+    if (c < cols / 4) {
+      int64_t r = blockIdx.y;
+      for (; r + 3 * rs < rows; r += 4 * rs) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(P + (r + u * rs) * ld + 4 * c);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          m[u] = fmaxf(m[u], fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+      }
+      for (; r < rows; r += rs) {
+        const float4 v = *reinterpret_cast<const float4*>(P + r * ld + 4 * c);
+        m[0] = fmaxf(m[0], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      }
+    }
+  } else if (c < cols) {
+    for (int64_t r = blockIdx.y; r < rows; r += rs) m[0] = fmaxf(m[0], fabsf(P[r * ld + c]));
+  }
+  float v = wave_max(fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3])));
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    v = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(out, __float_as_uint(v));
+  }
+}
+
+int absmax_launch(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32_t* out,
+                  bool accumulate, hipStream_t st) {
+  if (!accumulate && hipMemsetAsync(out, 0, sizeof(uint32_t), st) != hipSuccess) {
+    set_error("absmax: hipMemsetAsync failed");
+    return MVML_ERR_LAUNCH;
+  }
+  if (rows <= 0 || cols <= 0) return MVML_OK;
+  const int vec = (cols % 4 == 0) && (ld % 4 == 0) && ((uintptr_t)P % 16 == 0);
+  const int64_t cx = ceil_div(vec ? cols / 4 : cols, 256);
+  // ~16 K workgroups of 256 threads in flight at most (4 rows each): HBM-rate for big operands
+  const int64_t ry = std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, 4), ceil_div(8192, cx)));
+  absmax_kernel<<<dim3((unsigned)cx, (unsigned)ry), 256, 0, st>>>(rows, cols, P, ld, vec, out);
+  return check_launch("absmax_kernel");
+}
+
 int colsum_splits(int64_t M, int64_t N) {
   const int64_t colblocks = ceil_div(N, 256);
   int64_t s = ceil_div(2048, colblocks);
@@ -1445,9 +1553,11 @@ int colsum_splits(int64_t M, int64_t N) {
 
 using namespace mvml;
 
+// Workspace: [256 B: the split-fp16 operand maxima | split-K slab (S M N floats)].
+constexpr size_t kAmaxBytes = 256;
 extern "C" size_t mvml_gemm_workspace_size(int64_t M, int64_t N, int64_t K) {
   const int S = choose_splits(M, N, K);
-  return S > 1 ? carve_size((size_t)S * M * N * sizeof(float)) : 0;
+  return kAmaxBytes + (S > 1 ? carve_size((size_t)S * M * N * sizeof(float)) : 0);
 }
 
 namespace {
@@ -1455,7 +1565,7 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
                 const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
                 float beta, int act, float* C, int64_t ldc, void* workspace,
                 size_t workspace_bytes, void* stream, int64_t batch = 1,
-                BatchStrides bst = BatchStrides{});
+                BatchStrides bst = BatchStrides{}, AmaxPtrs amax = AmaxPtrs{});
 }
 
 extern "C" int mvml_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
@@ -1476,6 +1586,35 @@ extern "C" int mvml_gemm_f32x3(int a_kmajor, int b_kmajor, int64_t M, int64_t N,
                      workspace, workspace_bytes, stream);
 }
 
+extern "C" int mvml_gemm_f16x2(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                               const float* A, int64_t lda, const float* B, int64_t ldb,
+                               const float* bias, float beta, int act, float* C, int64_t ldc,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  return gemm_launch(kPrecF16x2, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C,
+                     ldc, workspace, workspace_bytes, stream);
+}
+
+extern "C" int mvml_gemm_f16x2_amax(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                                    const float* A, int64_t lda, const float* B, int64_t ldb,
+                                    const uint32_t* amax_a, const uint32_t* amax_b,
+                                    const float* bias, float beta, int act,
+                                    float* C, int64_t ldc, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  clear_error();
+  MVML_REQUIRE(amax_a != nullptr && amax_b != nullptr, "gemm_f16x2_amax: amax_a / amax_b are required");
+  return gemm_launch(kPrecF16x2, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C,
+                     ldc, workspace, workspace_bytes, stream, 1, BatchStrides{},
+                     AmaxPtrs{amax_a, amax_b});
+}
+
+extern "C" int mvml_absmax_f32(int64_t rows, int64_t cols, const float* P, int64_t ld,
+                               uint32_t* out, int accumulate, void* stream) {
+  clear_error();
+  MVML_REQUIRE(rows >= 0 && cols >= 0 && (rows == 0 || ld >= cols) && out, "absmax: bad shape");
+  return absmax_launch(rows, cols, P, ld, out, accumulate != 0, as_stream(stream));
+}
+
 extern "C" int mvml_gemm_f32x3_batched(int a_kmajor, int b_kmajor, int64_t M, int64_t N,
                                        int64_t K, int64_t batch, const float* A, int64_t lda,
                                        int64_t stride_a, const float* B, int64_t ldb,
@@ -1493,6 +1632,7 @@ extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float
                                         const float* b_hh,
                                         const float* c_prev, float* c_out, float* h_out,
                                         int64_t ldh, float* act, float* h_out2, int64_t ldh2,
+                                        const uint32_t* amax_a, const uint32_t* amax_b,
                                         void* stream) {
   clear_error();
   MVML_REQUIRE(M >= 0 && D > 0 && K > 0 && lda >= K && ldw >= K && ldh >= D &&
@@ -1510,9 +1650,16 @@ extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float
   CellEpi cep;
   cep.b_ih = b_ih; cep.b_hh = b_hh; cep.c_prev = c_prev; cep.c_out = c_out; cep.h_out = h_out;
   cep.h_out2 = h_out2; cep.act = act; cep.ldh = ldh; cep.ldh2 = ldh2; cep.D = D;
-  gemm_x3w_kernel<false, false, -1, true><<<dim3(x3w_grid_x(tiles, 1), 1, 1), kXThreads, 0, as_stream(stream)>>>(
-      M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
-      BatchStrides{}, cep);
+  const dim3 grid(x3w_grid_x(tiles, 1), 1, 1);
+  MVML_REQUIRE(!amax_a == !amax_b, "lstm_gates_cell_fwd: give both maxima or neither");
+  if (amax_a)
+    gemm_x3w_kernel<false, false, -1, true, 2><<<grid, kXThreads, 0, as_stream(stream)>>>(
+        M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
+        BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b});
+  else
+    gemm_x3w_kernel<false, false, -1, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
+        M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
+        BatchStrides{}, cep);
   return check_launch("gemm_x3w_kernel(lstm cell)");
 }
 
@@ -1534,7 +1681,8 @@ namespace {
 int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                 const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
                 float beta, int act, float* C, int64_t ldc, void* workspace,
-                size_t workspace_bytes, void* stream, int64_t batch, BatchStrides bst) {
+                size_t workspace_bytes, void* stream, int64_t batch, BatchStrides bst,
+                AmaxPtrs amax) {
   MVML_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
   if (M == 0 || N == 0) return MVML_OK;
   MVML_REQUIRE(ldc >= N, "gemm: ldc < N");
@@ -1542,8 +1690,20 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   MVML_REQUIRE(b_kmajor ? ldb >= N : ldb >= K, "gemm: bad ldb");
   MVML_REQUIRE(act == 0 || act == 1, "gemm: bad act");
   hipStream_t st = as_stream(stream);
-  const bool x3 = prec == kPrecX3, bf = prec == kPrecBf16;
+  const bool hf = prec == kPrecF16x2;
+  const bool x3 = prec == kPrecX3 || hf, bf = prec == kPrecBf16;
   GemmPlan plan = plan_gemm(prec, M, N, K);
+  if (hf && plan.wide && !amax.a) {  // operand maxima into the workspace head, once per product
+    if (!workspace || workspace_bytes < kAmaxBytes) {
+      set_error("gemm: workspace too small (need %zu)", mvml_gemm_workspace_size(M, N, K));
+      return MVML_ERR_WORKSPACE;
+    }
+    uint32_t* mx = static_cast<uint32_t*>(workspace);
+    int rc = absmax_launch(a_kmajor ? K : M, a_kmajor ? M : K, A, lda, mx, false, st);
+    if (!rc) rc = absmax_launch(b_kmajor ? K : N, b_kmajor ? N : K, B, ldb, mx + 1, false, st);
+    if (rc) return rc;
+    amax = AmaxPtrs{mx, mx + 1};
+  }
   // N = 256 q + r with 0 < r <= 128 (384-column products: the fusion head's data / weight
   // gradients, the LSTM hh weight gradients): a last 256-wide tile column would be at least half
   // padding (so such products fell back to the 128x128 kernel entirely); instead the first
@@ -1559,11 +1719,11 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
     if (mvml_gemm_workspace_size(M, N1, K) <= workspace_bytes &&
         mvml_gemm_workspace_size(M, N2, K) <= workspace_bytes) {
       int rc = gemm_launch(prec, a_kmajor, b_kmajor, M, N1, K, A, lda, B, ldb, bias, beta, act, C,
-                           ldc, workspace, workspace_bytes, stream);
+                           ldc, workspace, workspace_bytes, stream, 1, BatchStrides{}, amax);
       if (rc) return rc;
       return gemm_launch(prec, a_kmajor, b_kmajor, M, N2, K, A, lda, b_kmajor ? B + N1 : B + N1 * ldb,
                          ldb, bias ? bias + N1 : nullptr, beta, act, C + N1, ldc, workspace,
-                         workspace_bytes, stream);
+                         workspace_bytes, stream, 1, BatchStrides{}, amax);
     }
   }
   if (batch > 1) plan.S = 1;  // batched products are small: no split-K slab
@@ -1574,7 +1734,7 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
       set_error("gemm: workspace too small (need %zu)", mvml_gemm_workspace_size(M, N, K));
       return MVML_ERR_WORKSPACE;
     }
-    slab = static_cast<float*>(workspace);
+    slab = reinterpret_cast<float*>(static_cast<uint8_t*>(workspace) + kAmaxBytes);
   }
   const int64_t kc = S > 1 ? k_chunk(K, S) : (K > 0 ? K : 1);
   const int64_t tiles = plan.wide ? ceil_div(M, XBM) * ceil_div(N, XBN) : ceil_div(M, BM) * ceil_div(N, BN);
@@ -1584,7 +1744,15 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   dim3 grid(plan.wide || bf ? x3w_grid_x(tiles, S) : (unsigned)tiles, (unsigned)S, (unsigned)batch);
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
   do {                                                                                          \
-    if (bf && x3w_fast(AKV, BKV, M, N, K, av, bv))                                              \
+    if (hf && plan.wide && x3w_fast(AKV, BKV, M, N, K, av, bv))                                 \
+      gemm_x3w_kernel<AKV, BKV, -1, true, 2><<<grid, kXThreads, 0, st>>>(                       \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst,   \
+          CellEpi{}, amax);                                                                     \
+    else if (hf && plan.wide)                                                                   \
+      gemm_x3w_kernel<AKV, BKV, -1, false, 2><<<grid, kXThreads, 0, st>>>(                      \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst,   \
+          CellEpi{}, amax);                                                                     \
+    else if (bf && x3w_fast(AKV, BKV, M, N, K, av, bv))                                         \
       gemm_x3w_kernel<AKV, BKV, -1, true, 1><<<grid, kXThreads, 0, st>>>(                       \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst);  \
     else if (bf)                                                                                \
@@ -1629,9 +1797,19 @@ namespace mvml {
 // K-contiguous, no split-K: K is the small feature dimension), part as in ProjEpi.
 int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                   const float* B, int64_t ldb, float* C, int64_t ldc, const float* vec, int cols,
-                  int logw, float* part, hipStream_t st) {
-  const bool x3 = prec == kPrecX3, bf = prec == kPrecBf16;
+                  int logw, float* part, uint32_t* amax_ws, const uint32_t* amax_x,
+                  const uint32_t* amax_w, hipStream_t st) {
+  const bool hf = prec == kPrecF16x2;
+  const bool x3 = prec == kPrecX3 || hf, bf = prec == kPrecBf16;
   const bool wide = bf || (x3 && plan_gemm(kPrecX3, M, N, K).wide);
+  AmaxPtrs amx{amax_x, amax_w};
+  if (hf && wide && !(amax_x && amax_w)) {  // maxima not supplied: one pass per operand
+    MVML_REQUIRE(amax_ws != nullptr, "gat_proj_fwd: split-fp16 needs the maxima workspace");
+    int rc = absmax_launch(M, K, A, lda, amax_ws, false, st);
+    if (!rc) rc = absmax_launch(N, K, B, ldb, amax_ws + 1, false, st);
+    if (rc) return rc;
+    amx = AmaxPtrs{amax_ws, amax_ws + 1};
+  }
   const int64_t tiles = wide ? ceil_div(M, XBM) * ceil_div(N, XBN) : ceil_div(M, BM) * ceil_div(N, BN);
   MVML_REQUIRE(tiles < (int64_t(1) << 31), "gat_proj_fwd: too many tiles");
   MVML_REQUIRE(cols <= N && (logw >= 2 && logw <= 5), "gat_proj_fwd: bad partial width");
@@ -1640,7 +1818,15 @@ int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int
   dim3 grid(wide ? x3w_grid_x(tiles, 1) : (unsigned)tiles, 1);
 #define MVML_PROJ(LW)                                                                          \
   do {                                                                                         \
-    if (bf && x3w_fast(false, false, M, N, K, av, bv))                                         \
+    if (hf && wide && x3w_fast(false, false, M, N, K, av, bv))                                 \
+      gemm_x3w_kernel<false, false, LW, true, 2><<<grid, kXThreads, 0, st>>>(                  \
+          M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
+          ProjEpi{vec, cols, part}, BatchStrides{}, CellEpi{}, amx);                       \
+    else if (hf && wide)                                                                       \
+      gemm_x3w_kernel<false, false, LW, false, 2><<<grid, kXThreads, 0, st>>>(                 \
+          M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
+          ProjEpi{vec, cols, part}, BatchStrides{}, CellEpi{}, amx);                       \
+    else if (bf && x3w_fast(false, false, M, N, K, av, bv))                                    \
       gemm_x3w_kernel<false, false, LW, true, 1><<<grid, kXThreads, 0, st>>>(                  \
           M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
           ProjEpi{vec, cols, part});                                                           \

@@ -57,22 +57,44 @@ def agg_bwd_bytes(N, E, H, F, gout_cols, mode):
     return 4 * (reads + idx + writes)
 
 
-# GEMM algorithm for every dense product of the view: "x3" = split-bf16 MFMA at fp32 accuracy
-# (mvml_gemm_f32x3, the default), "f32" = f32-input MFMA (mvml_gemm_f32).  Both are parity-
-# tested against fp64 at the fp32 bar; override with MVML_GEMM_ALGO=f32.
-GEMM_ALGO = os.environ.get("MVML_GEMM_ALGO", "x3")
+# GEMM algorithm for every dense product of the view: "f16x2" = scaled split-fp16 MFMA at fp32
+# accuracy (mvml_gemm_f16x2, the default; 3 fp16 MFMAs per product), "x3" = split-bf16
+# (mvml_gemm_f32x3, 6 bf16 MFMAs), "f32" = f32-input MFMA (mvml_gemm_f32).  All are parity-
+# tested against fp64 at the fp32 bar; override with MVML_GEMM_ALGO=x3 / f32.
+GEMM_ALGO = os.environ.get("MVML_GEMM_ALGO", "f16x2")
 _GEMM_ENTRY = {"f32": ("mvml_gemm_f32", 0), "x3": ("mvml_gemm_f32x3", 1),
-               "bf16": ("mvml_gemm_bf16", 2)}  # bf16: the projection option of config 4
+               "bf16": ("mvml_gemm_bf16", 2),  # bf16: the projection option of config 4
+               "f16x2": ("mvml_gemm_f16x2", 3)}
 
 
-def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0, algo=None):
-    """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32 / mvml_gemm_f32x3)."""
+def absmax(P, rows, cols, ld, out, slot=0, offset=0, accumulate=False):
+    """out[slot] (int32 tensor) = bits of max |P[r, offset + c]| (mvml_absmax_f32)."""
+    pp = ctypes.c_void_p(ptr(P).value + 4 * offset)
+    op = ctypes.c_void_p(ptr(out).value + 4 * slot)
+    call("mvml_absmax_f32", rows, cols, pp, ld, op, int(accumulate), _stream(out.device))
+
+
+def slot(t, i):
+    """Device pointer to element i of an int32 maxima tensor (None passes through)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr() + 4 * i)
+
+
+def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0, algo=None,
+         amax=None):
+    """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32 / mvml_gemm_f32x3 /
+    mvml_gemm_f16x2).  amax = (pointer to |A| max bits, pointer to |B| max bits) from absmax()
+    lets split-fp16 products that share an operand share its max pass."""
     _lib.call_tag[0] = {"flops": 2 * M * N * K, "shape": (M, N, K, int(a_kmajor), int(b_kmajor))}
     L = _lib.lib()
     dev = C.device
     wsz = L.mvml_gemm_workspace_size(M, N, K)
     wp, wn = _lib.ws_ptr_size(wsz, dev)
-    call(_GEMM_ENTRY[algo or GEMM_ALGO][0], int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda,
+    algo = algo or GEMM_ALGO
+    if algo == "f16x2" and amax is not None:
+        call("mvml_gemm_f16x2_amax", int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda, ptr(B), ldb,
+             amax[0], amax[1], ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
+        return
+    call(_GEMM_ENTRY[algo][0], int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda,
          ptr(B), ldb, ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
 
 
@@ -124,10 +146,18 @@ class GATLayerFunction(torch.autograd.Function):
         Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
         elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
         L = _lib.lib()
+        # split-fp16: |max| of X, Wcat (all C + 2H rows) and, in the backward, gY — each operand's
+        # pass serves all of its products (projection, dL/dW, dL/dX)
+        amx = None
+        if (algo or GEMM_ALGO) == "f16x2":
+            amx = torch.empty(3, dtype=torch.int32, device=dev)
+            absmax(Xp, N, Fp, Fp, amx, 0)
+            absmax(Wcat, C + 2 * H, Fp, Fp, amx, 1)
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_proj_fwd_workspace_size(N, H, F), dev)
         _lib.call_tag[0] = {"flops": 2 * N * C * Fp}
         call("mvml_gat_proj_fwd", N, ptr(Xp), Fp, Fp, ptr(Wcat), Fp, ptr(attn_lr), H, F, mean_res,
-             _GEMM_ENTRY[algo or GEMM_ALGO][1], ptr(Y), ldy, ptr(elr), wp, wn, st)
+             _GEMM_ENTRY[algo or GEMM_ALGO][1], ptr(Y), ldy, ptr(elr), slot(amx, 0), slot(amx, 1),
+             wp, wn, st)
         out_cols = F if mode == MODE_MEAN else HF
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()
@@ -142,6 +172,7 @@ class GATLayerFunction(torch.autograd.Function):
         ctx.Fin = Fin
         ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode, ctx.ldy = g, H, F, slope, mode, ldy
         ctx.algo = algo
+        ctx.amx = amx
         return out
 
     @staticmethod
@@ -166,9 +197,13 @@ class GATLayerFunction(torch.autograd.Function):
         call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
              ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr),
              ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldg, wp, wn, st)
+        amx = ctx.amx
+        if amx is not None:
+            absmax(gY, N, CE, ldg, amx, 2)
         # dL/d[Wcat ; A_l ; A_r] = gY^T X  (split-K over atoms)
         gW = torch.empty((CE, Fp), dtype=torch.float32, device=dev)
-        gemm(gY, Xp, CE, Fp, N, 1, 1, ldg, Fp, gW, Fp, algo=ctx.algo)
+        gemm(gY, Xp, CE, Fp, N, 1, 1, ldg, Fp, gW, Fp, algo=ctx.algo,
+             amax=None if amx is None else (slot(amx, 2), slot(amx, 0)))
         g_fc = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_res = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_al = torch.empty_like(attn_l)
@@ -190,7 +225,8 @@ class GATLayerFunction(torch.autograd.Function):
         gX = None
         if ctx.needs_input_grad[0]:
             gX = torch.empty((N, Fin), dtype=torch.float32, device=dev)
-            gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, algo=ctx.algo)
+            gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, algo=ctx.algo,
+                 amax=None if amx is None else (slot(amx, 2), slot(amx, 1)))
         return gX, g_fc, g_res, g_al, g_ar, g_bias, None, None, None, None, None, None
 
 
@@ -233,6 +269,12 @@ class Set2SetFunction(torch.autograd.Function):
         cs = torch.empty((T, Lr, B, D), **f32)
         lse = torch.empty((T, B), **f32)
         gates = torch.empty((B, 4 * D), **f32)
+        amax_buf = amax_w = None
+        if GEMM_ALGO == "f16x2" and CELL_EPI:
+            amax_buf = torch.empty(T * Lr, dtype=torch.int32, device=dev)
+            amax_w = torch.empty(Lr, dtype=torch.int32, device=dev)
+            for l in range(Lr):
+                absmax(Wperm[l], 4 * D, kin[l] + D, kin[l] + D, amax_w, l)
         for t in range(T):
             for l in range(Lr):
                 w_ih, w_hh, b_ih, b_hh = W[l]
@@ -242,10 +284,14 @@ class Set2SetFunction(torch.autograd.Function):
                 c_prev = cs[t - 1, l] if t > 0 else None
                 ldn = kin[l + 1] + D if l < Lr - 1 else 3 * D
                 if CELL_EPI and not (t == 0 and l == 0) and L.mvml_lstm_gates_cell_plan_ok(B, D, K):
+                    pa = pw = None
+                    if GEMM_ALGO == "f16x2":  # split-fp16: the operand maxima of this cell's GEMM
+                        absmax(XH[l][t], B, K, kin[l] + D, amax_buf, t * Lr + l)
+                        pa, pw = slot(amax_buf, t * Lr + l), slot(amax_w, l)
                     _lib.call_tag[0] = {"flops": 2 * B * 4 * D * K, "shape": (B, 4 * D, K, 0, 0, "cell")}
                     call("mvml_lstm_gates_cell_fwd", B, D, K, ptr(XH[l][t]), kin[l] + D, ptr(Wperm[l]),
                          kin[l] + D, ptr(b_ih), ptr(b_hh), ptr(c_prev), ptr(cs[t, l]), ptr(own),
-                         kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, st)
+                         kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, pa, pw, st)
                     continue
                 if t == 0 and l == 0:
                     gates.zero_()  # q*_{-1} = 0 and h_0(-1) = 0

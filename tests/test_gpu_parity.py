@@ -94,10 +94,10 @@ import os  # noqa: E402
 
 @contextlib.contextmanager
 def _x3_tile(algo):
-    """'x3-128' / 'x3-256' force the split-bf16 tile size (MVML_X3_TILE, read per call)."""
+    """'x3-128' / 'x3-256' / 'f16x2-256' force the tile size (MVML_X3_TILE, read per call)."""
     old = os.environ.pop("MVML_X3_TILE", None)
-    if algo.startswith("x3-"):
-        os.environ["MVML_X3_TILE"] = algo[3:]
+    if "-" in algo:
+        os.environ["MVML_X3_TILE"] = algo.split("-")[1]
     try:
         yield algo.split("-")[0]
     finally:
@@ -106,7 +106,7 @@ def _x3_tile(algo):
             os.environ["MVML_X3_TILE"] = old
 
 
-@pytest.mark.parametrize("algo", ["f32", "x3", "x3-128", "x3-256"])
+@pytest.mark.parametrize("algo", ["f32", "x3", "x3-128", "x3-256", "f16x2", "f16x2-256"])
 @pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (130, 70, 74), (257, 300, 768), (96, 40, 20000),
                                    (256, 384, 1000), (640, 512, 4000), (1000, 1928, 768),
@@ -143,7 +143,7 @@ def test_gemm_x3_error_matches_fp32(K):
     B = torch.randn(K, N, generator=g, dtype=torch.float64)
     ref = A @ B
     errs = {}
-    for algo in ("f32", "x3", "x3-256"):
+    for algo in ("f32", "x3", "x3-256", "f16x2-256"):
         C = torch.zeros(M, N, device=DEV)
         with _x3_tile(algo) as a:
             gemm(A.float().to(DEV), B.t().contiguous().float().to(DEV), M, N, K, 0, 0, K, K, C, N, algo=a)
@@ -152,8 +152,43 @@ def test_gemm_x3_error_matches_fp32(K):
     cpu = (A.float() @ B.float()).double() - ref
     errs["cpu"] = (cpu.abs().max().item(), cpu.pow(2).mean().sqrt().item())
     base = max(errs["f32"][0], errs["cpu"][0]), max(errs["f32"][1], errs["cpu"][1])
-    for algo in ("x3", "x3-256"):
+    for algo in ("x3", "x3-256", "f16x2-256"):
         assert errs[algo][0] <= 2 * base[0] and errs[algo][1] <= 2 * base[1], errs
+
+
+@pytest.mark.parametrize("sa,sb", [(1e-30, 1e25), (1e30, 1e-32), (3e-8, 1.0), (0.0, 1.0)])
+def test_gemm_f16x2_scales(sa, sb):
+    """Split-fp16 operand scaling: operands far outside fp16 range (either direction), a zero
+    operand, plus a product through caller-supplied maxima (mvml_gemm_f16x2_amax) and the
+    mvml_absmax_f32 pass itself (bits of max |x|)."""
+    from mvml_gat import _lib
+    from mvml_gat.functional import absmax, gemm, ptr, slot, _stream
+    g = torch.Generator().manual_seed(5)
+    M, N, K = 700, 520, 300
+    A = torch.randn(M, K, generator=g, dtype=torch.float64) * sa
+    B = torch.randn(K, N, generator=g, dtype=torch.float64) * sb
+    ref = A @ B
+    Ad, Bd = A.float().to(DEV), B.t().contiguous().float().to(DEV)
+    C = torch.zeros(M, N, device=DEV)
+    with _x3_tile("f16x2-256") as a:
+        gemm(Ad, Bd, M, N, K, 0, 0, K, K, C, N, algo=a)
+    if sa == 0.0:
+        assert torch.count_nonzero(C).item() == 0
+    else:
+        assert rel_err(C, ref) < TOL
+    amx = torch.zeros(2, dtype=torch.int32, device=DEV)
+    absmax(Ad, M, K, K, amx, 0)
+    absmax(Bd, N, K, K, amx, 1)
+    got = amx.cpu().view(torch.float32)
+    assert got[0].item() == Ad.abs().max().item() and got[1].item() == Bd.abs().max().item()
+    C2 = torch.zeros(M, N, device=DEV)
+    L = _lib.lib()
+    wsz = L.mvml_gemm_workspace_size(M, N, K)
+    wp, wn = _lib.ws_ptr_size(wsz, DEV)
+    with _x3_tile("f16x2-256"):
+        _lib.call("mvml_gemm_f16x2_amax", 0, 0, M, N, K, ptr(Ad), K, ptr(Bd), K, slot(amx, 0),
+                  slot(amx, 1), None, 0.0, 0, ptr(C2), N, wp, wn, _stream(C2.device))
+    assert torch.equal(C, C2)
 
 
 @pytest.mark.parametrize("ak,bk", [(1, 1), (0, 1), (0, 0), (1, 0)])

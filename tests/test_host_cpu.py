@@ -108,7 +108,11 @@ def test_abi_argument_validation_without_gpu():
     rc = L.mvml_build_csr(None, None, None, None, 1, 1 << 31, 5, *([None] * 12), None, 0, None)
     assert rc == 1 and b"overflow" in L.mvml_last_error()
     assert L.mvml_gemm_workspace_size(3080, 768, 1_000_000) > 0
-    assert L.mvml_gemm_workspace_size(100000, 3080, 768) == 0
+    assert L.mvml_gemm_workspace_size(100000, 3080, 768) == 256  # the split-fp16 maxima only
+    rc = L.mvml_gemm_f16x2_amax(0, 0, 4, 4, 4, None, 4, None, 4, None, None, None, 0.0, 0, None, 4, None, 0, None)
+    assert rc == 1 and b"amax" in L.mvml_last_error()
+    rc = L.mvml_absmax_f32(-1, 4, None, 4, None, 0, None)
+    assert rc == 1 and b"absmax" in L.mvml_last_error()
 
 
 def test_no_cpu_fallback():

@@ -60,8 +60,8 @@ def main():
                 ms, t = tf(lambda: torch.matmul(At, Bt, out=C), flops)
             else:
                 os.environ.pop("MVML_X3_TILE", None)
-                if algo.startswith("x3-"):
-                    os.environ["MVML_X3_TILE"] = algo[3:]
+                if "-" in algo:
+                    os.environ["MVML_X3_TILE"] = algo.split("-")[1]
                 a = algo.split("-")[0]
                 ms, t = tf(lambda: gemm(A, Bm, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N, algo=a), flops)
             cols.append(f"{algo} {ms:8.3f} ms {t:6.1f} TF/s")
