@@ -415,7 +415,7 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], c
     for (int j = 0; j < NPA; ++j) dst[j] = buf_ld4(rY, ok ? rb[j] + cb : noY);
   };
   // residual of chunk k (mean mode: of its f-chunk, re-read per head from L2 so that the loop
-  // stays branch-free)
+  // stays branch-free; loading it for the last head only measured slower, L2 mean 3.86 -> 4.20 ms)
   auto load_res = [&](int k, float4 (&dst)[NPA]) {
     const bool ok = k < nch;
     const uint32_t cb = 4u * (uint32_t)(HF + (MODE == 1 ? (k / H) * CW + 4 * q : col_of(k)));
@@ -928,14 +928,18 @@ __device__ __forceinline__ void bwd_lds_chunks(
   auto fch_of = [&](int k) { return MODE == 1 ? k / H : k % nfc; };
   auto col_of = [&](int k) { return head_of(k) * F + fch_of(k) * CW + 4 * q; };
   struct Rows { float4 z[NPA], g[NPA], o[NPA]; };
+  // Mean mode: chunks are f-chunk-major (k = fc H + h), and g_rst = g_out / H is the same for
+  // the H heads of an f-chunk, so g_out is loaded and gs staged only at h == 0 (the gs image of
+  // chunk k stays valid for chunks k+1 .. k+H-1).
   auto load = [&](int k, Rows& R) {
     const bool ok = k < nch;
     const int col = col_of(k);
     const int gcol = MODE == 1 ? fch_of(k) * CW + 4 * q : col;
+    const bool gload = MODE != 1 || head_of(k) == 0;  // uniform
 #pragma unroll
     for (int p = 0; p < NPA; ++p) {
       R.z[p] = buf_ld4(rY, ok ? yrow(p) + 4u * (uint32_t)col : noY);
-      R.g[p] = buf_ld4(rGo, ok ? gorow(p) + 4u * (uint32_t)gcol : noGo);
+      if (gload) R.g[p] = buf_ld4(rGo, ok ? gorow(p) + 4u * (uint32_t)gcol : noGo);
       if (MODE == 0) R.o[p] = buf_ld4(rO, ok ? orow(p) + 4u * (uint32_t)col : noO);
     }
   };
@@ -959,10 +963,13 @@ __device__ __forceinline__ void bwd_lds_chunks(
         g = make_float4(g.x / hh, g.y / hh, g.z / hh, g.w / hh);
       }
       zs[r * LPD + (q ^ bwd_sw<LPD>(r))] = R.z[p];
-      gs[r * LPD + (q ^ bwd_sw<LPD>(r))] = g;
-      if (MODE != 1) buf_st4(rG, ok ? grow(p) + 4u * (uint32_t)(HF + col_of(k)) : noG, g);
-      else if (h == 0)  // uniform branch: an all-out-of-range store is not free
+      if (MODE != 1) {
+        gs[r * LPD + (q ^ bwd_sw<LPD>(r))] = g;
+        buf_st4(rG, ok ? grow(p) + 4u * (uint32_t)(HF + col_of(k)) : noG, g);
+      } else if (h == 0) {  // uniform branch: an all-out-of-range store is not free
+        gs[r * LPD + (q ^ bwd_sw<LPD>(r))] = g;
         buf_st4(rG, ok ? grow(p) + 4u * (uint32_t)(HF + fc * CW + 4 * q) : noG, R.g[p]);
+      }
     }
   };
   // chunks k+1 .. k+RB in flight (two-pass groups already move twice the bytes per chunk)

@@ -766,10 +766,12 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-template <bool KMAJ, int NP = 3>
+template <bool KMAJ, int NP = 3, int NTH = kXThreads>
 struct XOp {
   static constexpr int kPlane = KMAJ ? XBK * kXKmajPitch : 256 * 32;
   static constexpr int kBytes = NP * kPlane;  // NP = 3 split-bf16 planes, 1 = plain bf16
+  // float4 pieces per thread of a 256 x 16 tile (1024 pieces), the K-contiguous row stride
+  static constexpr int NI = 1024 / NTH, RS = NTH / 4;
 
   // This thread's 8 values of a 256 x 16 operand tile (rows r0.., k0..):
   //  K-contiguous: rows (tid >> 2) + 128 i, k = 4 (tid & 3) + [0, 4) in v[i] (16 rows x 64 B per
@@ -777,11 +779,11 @@ struct XOp {
   //  contiguous per wave-instruction).  Guarded path zero-fills rows >= rows, k >= kend.
   __device__ static __forceinline__ void load(const float* __restrict__ P, int64_t ld, int64_t r0,
                                               int64_t rows, int64_t k0, int64_t kend, bool fast,
-                                              int tid, float4 (&v)[2]) {
+                                              int tid, float4 (&v)[NI]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       if (!KMAJ) {
-        const int64_t row = r0 + (tid >> 2) + 128 * i, k = k0 + 4 * (tid & 3);
+        const int64_t row = r0 + (tid >> 2) + RS * i, k = k0 + 4 * (tid & 3);
         if (fast) {
           v[i] = *reinterpret_cast<const float4*>(P + row * ld + k);
         } else {
@@ -791,7 +793,7 @@ struct XOp {
           v[i] = make_float4(e[0], e[1], e[2], e[3]);
         }
       } else {
-        const int64_t k = k0 + 2 * (tid >> 6) + i, row = r0 + 4 * (tid & 63);
+        const int64_t k = k0 + NI * (tid >> 6) + i, row = r0 + 4 * (tid & 63);
         if (fast) {
           v[i] = *reinterpret_cast<const float4*>(P + k * ld + row);
         } else {
@@ -809,25 +811,25 @@ struct XOp {
   // tile so that no float4 straddles the edge), advanced by kStep floats per stage.
   __device__ static __forceinline__ void ptrs(const float* __restrict__ P, int64_t ld, int64_t r0,
                                               int64_t rows, int64_t k0, int tid,
-                                              const float* (&p)[2]) {
+                                              const float* (&p)[NI]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       if (!KMAJ) {
-        const int64_t row = min(r0 + (tid >> 2) + 128 * i, rows - 1);
+        const int64_t row = min(r0 + (tid >> 2) + RS * i, rows - 1);
         p[i] = P + row * ld + k0 + 4 * (tid & 3);
       } else {
         const int64_t row = min(r0 + 4 * (tid & 63), rows - 4);
-        p[i] = P + (k0 + 2 * (tid >> 6) + i) * ld + row;
+        p[i] = P + (k0 + NI * (tid >> 6) + i) * ld + row;
       }
     }
   }
   __device__ static __forceinline__ int64_t kstep(int64_t ld) { return KMAJ ? XBK * ld : XBK; }
 
 
-  __device__ static __forceinline__ void split_store(uint8_t* op, int tid, const float4 (&v)[2],
+  __device__ static __forceinline__ void split_store(uint8_t* op, int tid, const float4 (&v)[NI],
                                                      float s = 1.f) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       uint2 p0, p1, p2;
       if constexpr (NP == 3) {
         split4(v[i].x, v[i].y, v[i].z, v[i].w, p0, p1, p2);
@@ -840,10 +842,10 @@ struct XOp {
       }
       uint32_t off;
       if (!KMAJ) {
-        const int row = (tid >> 2) + 128 * i, q = tid & 3;
+        const int row = (tid >> 2) + RS * i, q = tid & 3;
         off = row * 32 + (((q >> 1) ^ ((row >> 3) & 1)) << 4) + 8 * (q & 1);
       } else {
-        off = (2 * (tid >> 6) + i) * kXKmajPitch + 8 * (tid & 63);
+        off = (NI * (tid >> 6) + i) * kXKmajPitch + 8 * (tid & 63);
       }
       *reinterpret_cast<uint2*>(op + off) = p0;
       if constexpr (NP >= 2) *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
@@ -852,17 +854,17 @@ struct XOp {
   }
 
   // ablation only: the planes' stores with no split arithmetic (float bits as bf16 pairs)
-  __device__ static __forceinline__ void raw_store(uint8_t* op, int tid, const float4 (&v)[2]) {
+  __device__ static __forceinline__ void raw_store(uint8_t* op, int tid, const float4 (&v)[NI]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const uint2 p0 = make_uint2(__float_as_uint(v[i].x), __float_as_uint(v[i].y));
       const uint2 p1 = make_uint2(__float_as_uint(v[i].z), __float_as_uint(v[i].w));
       uint32_t off;
       if (!KMAJ) {
-        const int row = (tid >> 2) + 128 * i, q = tid & 3;
+        const int row = (tid >> 2) + RS * i, q = tid & 3;
         off = row * 32 + (((q >> 1) ^ ((row >> 3) & 1)) << 4) + 8 * (q & 1);
       } else {
-        off = (2 * (tid >> 6) + i) * kXKmajPitch + 8 * (tid & 63);
+        off = (NI * (tid >> 6) + i) * kXKmajPitch + 8 * (tid & 63);
       }
       *reinterpret_cast<uint2*>(op + off) = p0;
       if constexpr (NP >= 2) *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
@@ -1001,6 +1003,9 @@ __device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], floa
 #ifndef MVML_X3W_SGB_V
 #define MVML_X3W_SGB_V 3
 #endif
+#ifndef MVML_H2_KS
+#define MVML_H2_KS 2
+#endif
 // FAST (host-checked: both operands 16-B aligned rows, K-major row counts % 4 == 0): whole
 // stages by unguarded loads from clamped rows, the K tail as one guarded stage; !FAST: every
 // stage guarded.
@@ -1028,7 +1033,11 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     kb = amax_shift(*amax.b);
   }
   const float s_a = pow2f(ka), s_b = pow2f(kb);
-  constexpr int kStage = OA::kBytes + OB::kBytes;
+  // KS 16-deep sub-stages per barrier (split-fp16: 2, so a stage carries as many MFMAs as the
+  // split-bf16 one); a sub-stage's LDS image is exactly the KS = 1 stage layout
+  constexpr int KS = (NP == 2) ? MVML_H2_KS : 1;
+  constexpr int kSub = OA::kBytes + OB::kBytes;
+  constexpr int kStage = KS * kSub;
   // double-buffered stages; the LDS epilogue reuses the space (8 waves x 32 rows x kEpiLd)
   constexpr int kLdsBytes = 2 * kStage > 8 * 32 * kEpiLd * 4 ? 2 * kStage : 8 * 32 * kEpiLd * 4;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -1059,29 +1068,33 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int64_t ntiles = (kend > kbeg) ? ceil_div(kend - kbeg, XBK) : 0;
-  const int64_t nfull = (kend > kbeg) ? (kend - kbeg) / XBK : 0;  // whole 16-deep stages
+  const int64_t ntiles = (kend > kbeg) ? ceil_div(kend - kbeg, XBK * KS) : 0;
   const float* pa[2];
   const float* pb[2];
   OA::ptrs(A, lda, m0, M, kbeg, tid, pa);
   OB::ptrs(B, ldb, n0, N, kbeg, tid, pb);
-  const int64_t sa_step = OA::kstep(lda), sb_step = OB::kstep(ldb);
-  float4 va[2], vb[2];
+  const int64_t sa_step = OA::kstep(lda), sb_step = OB::kstep(ldb);  // per 16-deep sub-stage
+  float4 va[KS][2], vb[KS][2];
   auto load_fast = [&]() {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      va[i] = *reinterpret_cast<const float4*>(pa[i]);
-      vb[i] = *reinterpret_cast<const float4*>(pb[i]);
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        va[s][i] = *reinterpret_cast<const float4*>(pa[i] + s * sa_step);
+        vb[s][i] = *reinterpret_cast<const float4*>(pb[i] + s * sb_step);
+      }
 #ifndef MVML_X3W_NOMEM  // ablation: re-read the first stage forever (cache hits, wrong results)
-      pa[i] += sa_step;
-      pb[i] += sb_step;
-#endif
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      pa[i] += KS * sa_step;
+      pb[i] += KS * sb_step;
     }
+#endif
   };
   // fast load of a stage that may be the K tail: addresses clamped to k < kend (host: kend %
   // 4 == 0), A's values at k >= kend zeroed, so B's clamped (finite) values add nothing
   auto load_masked_into = [&](int64_t t, float4 (&xa)[2], float4 (&xb)[2]) {
-    const int64_t k0 = kbeg + t * XBK;
+    const int64_t k0 = kbeg + t * XBK;  // t counts 16-deep sub-stages here
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       int64_t ka, kb_;  // this thread's k for operand A / B piece i
@@ -1108,24 +1121,34 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       pb[i] += sb_step;
     }
   };
-  auto load_masked = [&](int64_t t) { load_masked_into(t, va, vb); };
+  auto load_masked = [&](int64_t t) {  // stage t (KS sub-stages), each masked at kend
+#pragma unroll
+    for (int s = 0; s < KS; ++s) load_masked_into(t * KS + s, va[s], vb[s]);  // advances pa / pb
+  };
   auto load_guarded = [&](int64_t t) {
-    const int64_t k0 = kbeg + t * XBK;
-    const bool kin = k0 + XBK <= kend;
-    OA::load(A, lda, m0, M, k0, kend, a_vec && m0 + XBM <= M && kin, tid, va);
-    OB::load(B, ldb, n0, N, k0, kend, b_vec && n0 + XBN <= N && kin, tid, vb);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int64_t k0 = kbeg + (t * KS + s) * XBK;
+      const bool kin = k0 + XBK <= kend;
+      OA::load(A, lda, m0, M, k0, kend, a_vec && m0 + XBM <= M && kin, tid, va[s]);
+      OB::load(B, ldb, n0, N, k0, kend, b_vec && n0 + XBN <= N && kin, tid, vb[s]);
+    }
   };
   auto stage = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      uint8_t* op = lds + buf * kStage + s * kSub;
 #ifdef MVML_ABL_NOSPLIT_A  // ablation: A's planes written without the split (wrong results)
-    OA::raw_store(lds + buf * kStage, tid, va);
+      OA::raw_store(op, tid, va[s]);
 #else
-    OA::split_store(lds + buf * kStage, tid, va, s_a);
+      OA::split_store(op, tid, va[s], s_a);
 #endif
 #ifdef MVML_ABL_NOSPLIT_B  // ablation: B's planes written without the split (wrong results)
-    OB::raw_store(lds + buf * kStage + OA::kBytes, tid, vb);
+      OB::raw_store(op + OA::kBytes, tid, vb[s]);
 #else
-    OB::split_store(lds + buf * kStage + OA::kBytes, tid, vb, s_b);
+      OB::split_store(op + OA::kBytes, tid, vb[s], s_b);
 #endif
+    }
   };
 #ifndef MVML_X3W_PRIO
 #define MVML_X3W_PRIO 1
@@ -1134,6 +1157,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   // stage t+1 (in va / vb) into the other buffer; LOAD: 0 none, 1 fast, 2 guarded load of t+2.
   // Each (STAGE, LOAD) is its own straight-line body: no control flow around the accumulators.
   auto body = [&](int64_t t, auto STAGE, auto LOAD) {
+#if MVML_X3W_SGB
     const uint8_t* sa = lds + (t & 1) * kStage;
     const uint8_t* sb = sa + OA::kBytes;
     bf16x8 fb[2][NP];
@@ -1141,7 +1165,6 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int p = 0; p < NP; ++p) fb[j][p] = OB::frag(sb, p, wn * 64 + 32 * j, lane);
-#if MVML_X3W_SGB
     if constexpr (decltype(STAGE)::value && NP == 3) {
       // Interleaved schedule: every fragment of stage t is read from LDS FIRST (so the split's
       // LDS writes into the other buffer, which the compiler cannot prove disjoint, do not pin
@@ -1196,16 +1219,29 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #else
     stage_and_load();
 #endif
-    if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(1);
+    // s_setprio around the MFMA block: measured +1-3 % slower for split-fp16 (NP = 2), kept for
+    // the split-bf16 / bf16 instantiations
+    constexpr bool kPrio = MVML_X3W_PRIO && NP != 2;
+    if (kPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bf16x8 fa[NP];
+    for (int s = 0; s < KS; ++s) {
+      const uint8_t* sa = lds + (t & 1) * kStage + s * kSub;
+      const uint8_t* sb = sa + OA::kBytes;
+      bf16x8 fb[2][NP];
 #pragma unroll
-      for (int p = 0; p < NP; ++p) fa[p] = OA::frag(sa, p, wm * 128 + 32 * i, lane);
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma_np<NP>(fa, fb[j], acc[i][j]);
+        for (int p = 0; p < NP; ++p) fb[j][p] = OB::frag(sb, p, wn * 64 + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bf16x8 fa[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) fa[p] = OA::frag(sa, p, wm * 128 + 32 * i, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_np<NP>(fa, fb[j], acc[i][j]);
+      }
     }
-    if (MVML_X3W_PRIO) __builtin_amdgcn_s_setprio(0);
+    if (kPrio) __builtin_amdgcn_s_setprio(0);
 #if MVML_X3W_STAGGER
     if (wid >= 4) stage_and_load();
 #endif
@@ -1217,7 +1253,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   using L1 = std::integral_constant<int, 1>;
   using L2 = std::integral_constant<int, 2>;
 #if MVML_X3W_PF2
-  if constexpr (FAST) {
+  if constexpr (FAST && KS == 1) {
     // Prefetch distance 2: tile k's fp32 values live in register set k % 2 from their load (in
     // body k - 3) to their split (in body k - 1), so a global load has two whole stages to land
     // instead of one (the loads of a stage are issued right after the split that frees the set).
