@@ -269,12 +269,17 @@ class Set2SetFunction(torch.autograd.Function):
         cs = torch.empty((T, Lr, B, D), **f32)
         lse = torch.empty((T, B), **f32)
         gates = torch.empty((B, 4 * D), **f32)
-        amax_buf = amax_w = None
-        if GEMM_ALGO == "f16x2" and CELL_EPI:
-            amax_buf = torch.empty(T * Lr, dtype=torch.int32, device=dev)
+        amax_x = amax_w = None
+        if GEMM_ALGO == "f16x2":
+            # split-fp16 operand maxima of the cells' GEMMs: every A row [x | h_prev] holds
+            # LSTM outputs h = o tanh(c) (|h| < 1) and, in layer 0, the readout r = sum_n a_n x_n
+            # (a convex combination: |r| <= max |X|), so max(1, max |X|) bounds every cell's A
+            # (an upper bound is all the scale needs) — one pass instead of one per cell
+            amax_x = torch.full((1,), 0x3F800000, dtype=torch.int32, device=dev)  # bits of 1.0f
+            absmax(X, N, D, D, amax_x, 0, accumulate=True)
             amax_w = torch.empty(Lr, dtype=torch.int32, device=dev)
             for l in range(Lr):
-                absmax(Wperm[l], 4 * D, kin[l] + D, kin[l] + D, amax_w, l)
+                absmax(Wcat[l], 4 * D, kin[l] + D, kin[l] + D, amax_w, l)  # = Wperm's max
         for t in range(T):
             for l in range(Lr):
                 w_ih, w_hh, b_ih, b_hh = W[l]
@@ -285,9 +290,8 @@ class Set2SetFunction(torch.autograd.Function):
                 ldn = kin[l + 1] + D if l < Lr - 1 else 3 * D
                 if CELL_EPI and not (t == 0 and l == 0) and L.mvml_lstm_gates_cell_plan_ok(B, D, K):
                     pa = pw = None
-                    if GEMM_ALGO == "f16x2":  # split-fp16: the operand maxima of this cell's GEMM
-                        absmax(XH[l][t], B, K, kin[l] + D, amax_buf, t * Lr + l)
-                        pa, pw = slot(amax_buf, t * Lr + l), slot(amax_w, l)
+                    if amax_x is not None:  # split-fp16: the operand maxima of this cell's GEMM
+                        pa, pw = slot(amax_x, 0), slot(amax_w, l)
                     _lib.call_tag[0] = {"flops": 2 * B * 4 * D * K, "shape": (B, 4 * D, K, 0, 0, "cell")}
                     call("mvml_lstm_gates_cell_fwd", B, D, K, ptr(XH[l][t]), kin[l] + D, ptr(Wperm[l]),
                          kin[l] + D, ptr(b_ih), ptr(b_hh), ptr(c_prev), ptr(cs[t, l]), ptr(own),
@@ -296,7 +300,8 @@ class Set2SetFunction(torch.autograd.Function):
                 if t == 0 and l == 0:
                     gates.zero_()  # q*_{-1} = 0 and h_0(-1) = 0
                 else:
-                    gemm(XH[l][t], Wcat[l], B, 4 * D, K, 0, 0, kin[l] + D, kin[l] + D, gates, 4 * D)
+                    gemm(XH[l][t], Wcat[l], B, 4 * D, K, 0, 0, kin[l] + D, kin[l] + D, gates, 4 * D,
+                         amax=None if amax_x is None else (slot(amax_x, 0), slot(amax_w, l)))
                 call("mvml_lstm_cell_fwd", B, D, ptr(gates), ptr(b_ih), ptr(b_hh), ptr(c_prev),
                      ptr(cs[t, l]), ptr(own), kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, st)
             call("mvml_set2set_seg_fwd", B, D, ptr(g.node_offsets), ptr(X), ptr(XH[0][t + 1]), 3 * D,
