@@ -90,14 +90,24 @@ __device__ __forceinline__ f32x16 mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
+// l = f16(x s - h) of a pair: v_fma_mix{lo,hi}_f16 forms -h * 1 + x s from the f16 h and the
+// f32 x s with one rounding (the difference is exact in f32, so this is f16(x s - f32(h))) —
+// 2 VALU per pair instead of 2 converts, a packed subtract and a packed convert.
+__device__ __forceinline__ uint32_t lo_pair(f16x2 h, f32x2 xs) {
+  uint32_t r;
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(r)
+      : "v"(h), "v"(xs.x), "v"(xs.y));
+  return r;
+}
 __device__ __forceinline__ void split2h(const float4& v, float s, uint2& p0, uint2& p1) {
   const f32x2 u = {v.x * s, v.y * s}, w = {v.z * s, v.w * s};
   const f16x2 hu = __builtin_convertvector(u, f16x2), hw = __builtin_convertvector(w, f16x2);
-  const f32x2 ru = u - __builtin_convertvector(hu, f32x2), rw = w - __builtin_convertvector(hw, f32x2);
   p0.x = __builtin_bit_cast(uint32_t, hu);
   p0.y = __builtin_bit_cast(uint32_t, hw);
-  p1.x = __builtin_bit_cast(uint32_t, __builtin_convertvector(ru, f16x2));
-  p1.y = __builtin_bit_cast(uint32_t, __builtin_convertvector(rw, f16x2));
+  p1.x = lo_pair(hu, u);
+  p1.y = lo_pair(hw, w);
 }
 
 // Scale of an operand from its |max| bits (non-negative float bits order as integers): 2^k with
