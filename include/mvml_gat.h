@@ -265,10 +265,11 @@ int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_
                        const float* b_hh, const float* c_prev, float* c_out, float* h_out,
                        int64_t ldh, float* act_out, float* h_out2, int64_t ldh2, void* stream);
 /* g_h [B,D] (ld ldgh), g_c [B,D] (carry from t+1, may be NULL) -> g_gates [B,4D] (pre-act),
- * g_c_prev [B,D] (may be NULL). */
+ * g_c_prev [B,D] (may be NULL).  gg_amax (may be NULL): *gg_amax = max(*gg_amax, bits of
+ * max |g_gates|) — the split-fp16 operand max of the GEMMs that read g_gates. */
 int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const float* c, const float* c_prev,
                        const float* g_h, int64_t ldgh, const float* g_c, float* g_gates,
-                       float* g_c_prev, void* stream);
+                       float* g_c_prev, uint32_t* gg_amax, void* stream);
 /* Readout segment pass (one wavefront per molecule): e_n = <x_n, q_g>, alpha = softmax over
  * the molecule's atoms (softmax_nodes), r_g = sum_n alpha_n x_n (sum_nodes).  Writes r into
  * qstar[:, D:2D] (ld ldq, q itself already sits in qstar[:, 0:D]) and lse[g] for backward. */

@@ -52,8 +52,9 @@ __global__ void lstm_cell_bwd_kernel(int64_t B, int D, const float* __restrict__
                                      const float* __restrict__ c, const float* __restrict__ c_prev,
                                      const float* __restrict__ g_h, int64_t ldgh,
                                      const float* __restrict__ g_c, float* __restrict__ g_gates,
-                                     float* __restrict__ g_c_prev) {
+                                     float* __restrict__ g_c_prev, uint32_t* __restrict__ gg_amax) {
   const int64_t total = B * D;
+  float mx = 0.f;  // |max| of this thread's gate gradients (split-fp16 operand scale)
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = e / D;
@@ -65,11 +66,22 @@ __global__ void lstm_cell_bwd_kernel(int64_t B, int D, const float* __restrict__
     const float gc = (g_c ? g_c[e] : 0.f) + gh * o * (1.f - tc * tc);
     const float cp = c_prev ? c_prev[e] : 0.f;
     float* gg = g_gates + b * 4 * D;
-    gg[d] = gc * gt * i * (1.f - i);
-    gg[D + d] = gc * cp * f * (1.f - f);
-    gg[2 * D + d] = gc * i * (1.f - gt * gt);
-    gg[3 * D + d] = gh * tc * o * (1.f - o);
+    const float g0 = gc * gt * i * (1.f - i), g1 = gc * cp * f * (1.f - f);
+    const float g2 = gc * i * (1.f - gt * gt), g3 = gh * tc * o * (1.f - o);
+    gg[d] = g0;
+    gg[D + d] = g1;
+    gg[2 * D + d] = g2;
+    gg[3 * D + d] = g3;
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(g0), fabsf(g1)), fmaxf(fabsf(g2), fabsf(g3))));
     if (g_c_prev) g_c_prev[e] = gc * f;
+  }
+  if (gg_amax) {  // block max -> one unsigned atomicMax of the non-negative float bits
+    mx = wave_max(mx);
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      atomicMax(gg_amax, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
   }
 }
 
@@ -259,13 +271,14 @@ extern "C" int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, cons
 
 extern "C" int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const float* c,
                                   const float* c_prev, const float* g_h, int64_t ldgh,
-                                  const float* g_c, float* g_gates, float* g_c_prev, void* stream) {
+                                  const float* g_c, float* g_gates, float* g_c_prev,
+                                  uint32_t* gg_amax, void* stream) {
   clear_error();
   MVML_REQUIRE(B >= 0 && D > 0 && ldgh >= D, "lstm_cell_bwd: bad shape");
   if (B == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
   lstm_cell_bwd_kernel<<<grid_for(B * D), 256, 0, st>>>(B, D, act, c, c_prev, g_h, ldgh, g_c,
-                                                        g_gates, g_c_prev);
+                                                        g_gates, g_c_prev, gg_amax);
   return check_launch("lstm_cell_bwd_kernel");
 }
 

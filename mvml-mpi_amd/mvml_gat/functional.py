@@ -308,6 +308,7 @@ class Set2SetFunction(torch.autograd.Function):
                  ptr(lse[t]), st)
         ctx.save_for_backward(X, acts, cs, lse, *XH, *[p for w in W for p in w])
         ctx.g, ctx.T, ctx.Lr = g, T, Lr
+        ctx.amax = (amax_x, amax_w)
         return XH[0][T][:, :2 * D].clone()
 
     @staticmethod
@@ -343,6 +344,11 @@ class Set2SetFunction(torch.autograd.Function):
         gxh = [None] + [torch.empty((B, 2 * D), **f32) for _ in range(1, Lr)]
         g_c = [torch.zeros((B, D), **f32) for _ in range(Lr)]
         g_c_new = torch.empty((B, D), **f32)
+        # split-fp16 maxima: the forward's bounds for XH (|x|, |h|) and [W_ih | W_hh], and a
+        # running |max| of each layer's gate gradients, folded in by mvml_lstm_cell_bwd (the
+        # running value bounds every cell seen so far, which is all a scale needs)
+        amax_x, amax_w = ctx.amax
+        amax_g = torch.zeros(Lr, dtype=torch.int32, device=dev) if amax_x is not None else None
         for t in range(T - 1, -1, -1):
             # readout segment backward: dL/dq_t = g_qstar_t[:, :D] + segment term -> g_h
             call("mvml_set2set_seg_bwd", B, D, ptr(g.node_offsets), ptr(X), ptr(qs[t]), 3 * D,
@@ -358,14 +364,15 @@ class Set2SetFunction(torch.autograd.Function):
                 c_prev = cs[t - 1, l] if t > 0 else None
                 g_gates = g_gates_all[l, t]
                 call("mvml_lstm_cell_bwd", B, D, ptr(acts[t, l]), ptr(cs[t, l]), ptr(c_prev), ptr(gh), ldgh,
-                     ptr(g_c[l]) if t < T - 1 else None, ptr(g_gates), ptr(g_c_new), st)
+                     ptr(g_c[l]) if t < T - 1 else None, ptr(g_gates), ptr(g_c_new), slot(amax_g, l), st)
                 g_c[l], g_c_new = g_c_new, g_c[l]
                 # N = kin + D with the recurrent part (t > 0), kin alone at t = 0; layer 0 at
                 # t = 0 has neither (its input q*_{-1} = 0 is a constant)
                 ncols = kin + D if t > 0 else (kin if l > 0 else 0)
                 if ncols:
                     out, ldo = (g_qs3[t - 1], 3 * D) if l == 0 else (gxh[l], 2 * D)
-                    gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo)
+                    gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo,
+                         amax=None if amax_g is None else (slot(amax_g, l), slot(amax_w, l)))
         # weight / bias gradients, one product per parameter over all steps:
         #   dW_ih[l] = sum_t g_gates[l,t]^T x_l(t),  dW_hh[l] = sum_{t>=1} g_gates[l,t]^T h_l(t-1)
         # (layer 0's input x_0(t) = q*_{t-1} is zero at t = 0; h_l(-1) = 0)
@@ -379,7 +386,8 @@ class Set2SetFunction(torch.autograd.Function):
             t0 = 1 if l == 0 else 0
             if T > t0:
                 gWcat = torch.empty((4 * D, ldx), **f32)
-                gemm(G[t0:], XH[l][t0:T], 4 * D, ldx, (T - t0) * B, 1, 1, 4 * D, ldx, gWcat, ldx)
+                gemm(G[t0:], XH[l][t0:T], 4 * D, ldx, (T - t0) * B, 1, 1, 4 * D, ldx, gWcat, ldx,
+                     amax=None if amax_g is None else (slot(amax_g, l), slot(amax_x, 0)))
                 gW_ih[l].copy_(gWcat[:, :kin])
                 gW_hh[l].copy_(gWcat[:, kin:])
             colsum(G, T * B, 4 * D, 4 * D, gb[l])

@@ -16,7 +16,8 @@ import torch.nn as nn
 
 from . import _lib
 from ._lib import call, ptr
-from .functional import (LinearReLUFunction, _c, _check_cuda_f32, _stream, colsum, gemm,
+from . import functional as _F
+from .functional import (LinearReLUFunction, _c, _check_cuda_f32, _stream, absmax, colsum, gemm, slot,
                          gemm_batched)
 
 
@@ -128,15 +129,23 @@ class FusionAttnConvFunction(torch.autograd.Function):
             # g_k (the keys' gradient, summed over heads) lands in gXn: the GEMMs add onto it
             call("mvml_token_attn_fold_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
                  ptr(P), ptr(g_att), ptr(gPV), 2 * HD, ptr(gXn), D, st)
+            amx = None
+            if _F.GEMM_ALGO == "f16x2":  # split-fp16 maxima, one pass per operand: gPV, Xn, Bcat
+                amx = torch.empty(3, dtype=torch.int32, device=dev)
+                absmax(gPV, 3 * B, 2 * HD, 2 * HD, amx, 0)
+                absmax(Xn, 3 * B, D, D, amx, 1)
+                absmax(Bcat, D, 2 * HD, 2 * HD, amx, 2)
             G2 = torch.empty((2 * HD, D), **f32)  # [h D + j][i] = dL/dM_h[i][j]; then dL/dW_v
-            gemm(gPV, Xn, 2 * HD, D, 3 * B, 1, 1, 2 * HD, D, G2, D)
+            gemm(gPV, Xn, 2 * HD, D, 3 * B, 1, 1, 2 * HD, D, G2, D,
+                 amax=None if amx is None else (slot(amx, 0), slot(amx, 1)))
             wq3, wk3 = _c(wq).view(H, D, D), _c(wk).view(H, D, D)
             gWq = torch.empty((H, D, D), **f32)
             gWk = torch.empty((H, D, D), **f32)
             # per head h (G2 rows h D .. h D + D): W_k,h dM_h^T and W_q,h dM_h
             gemm_batched(wk3, G2, D, D, D, 0, 1, D, D, gWq, D, H, D * D, D * D, D * D)
             gemm_batched(wq3, G2, D, D, D, 0, 0, D, D, gWk, D, H, D * D, D * D, D * D)
-            gemm(gPV, Bcat, 3 * B, D, 2 * HD, 0, 0, 2 * HD, 2 * HD, gXn, D, beta=1.0)
+            gemm(gPV, Bcat, 3 * B, D, 2 * HD, 0, 0, 2 * HD, 2 * HD, gXn, D, beta=1.0,
+                 amax=None if amx is None else (slot(amx, 0), slot(amx, 2)))
             g_wq, g_wk, g_wv = gWq.view(HD, D), gWk.view(HD, D), G2[HD:]
         else:
             Wqkv, QKV = S0, S1

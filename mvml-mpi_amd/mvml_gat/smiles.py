@@ -211,7 +211,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                     c_prev = c[tp] if 0 <= tp < T else None
                     g_c = carry[k % 2] if nxt is not None else None
                     call("mvml_lstm_cell_bwd", bs, H, ptr(act[t]), ptr(c[t]), ptr(c_prev),
-                         ptr(g[t, :, d * H:]), 2 * H, ptr(g_c), ptr(gg[t]), ptr(carry[(k + 1) % 2]), st)
+                         ptr(g[t, :, d * H:]), 2 * H, ptr(g_c), ptr(gg[t]), ptr(carry[(k + 1) % 2]), None, st)
                     nxt, k = t, k + 1
         for d in range(2):  # weight / input gradients: GEMMs over all positions
             w_ih, gg = _c(w[4 * d]), ggs[d]
