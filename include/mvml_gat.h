@@ -229,14 +229,17 @@ int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_
  * (d el x attn_l + d er x attn_r) reach dL/dX and dL/dfc.weight through the 2H extra columns
  * (GEMM against mvml_gat_fold_weights' A rows; mvml_gat_unfold_grads), and dL/dattn through
  * mvml_gat_attn_grad(gelr = gY + C, ldgl = ldgy).
- * out is the forward output (mode 0 uses ELU'(x) = out + 1 for x <= 0).  workspace: [E, H]. */
+ * out is the forward output (mode 0 uses ELU'(x) = out + 1 for x <= 0).  gy_amax (may be NULL):
+ * *gy_amax = max(*gy_amax, bits of max |gY[:, :C + 2H]|), folded into the stores (the split-fp16
+ * operand max of the two GEMMs that read gY; the caller zeroes it).  workspace: [E, H]. */
 size_t mvml_gat_agg_bwd_workspace_size(int64_t num_edges, int H);
 int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
                      const int32_t* in_rowptr, const int32_t* in_src, const int32_t* out_rowptr,
                      const int32_t* out_dst, const int32_t* out_inslot, const float* Y,
                      int64_t ldy, const float* elr, const float* attn, const float* out,
                      const float* g_out, int H, int F, float slope, int mode, float* gY,
-                     int64_t ldgy, void* workspace, size_t workspace_bytes, void* stream);
+                     int64_t ldgy, uint32_t* gy_amax, void* workspace, size_t workspace_bytes,
+                     void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Set2Set (dgl 0.9.1, model.py:82-84, 92) building blocks.

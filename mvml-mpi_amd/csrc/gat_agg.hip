@@ -84,6 +84,26 @@ __device__ __forceinline__ void store_heads(float* p, const float (&a)[H], int l
   if (lane < H) p[lane] = pick<H>(a, lane);
 }
 
+// |max| bookkeeping of the backward's gY stores (the split-fp16 scale of the GEMMs that read gY)
+__device__ __forceinline__ float amax4(float m, float4 v) {
+  return fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+}
+// Block |max| -> one unsigned atomicMax of the (non-negative) float bits: order-independent.
+// Every thread of the block calls it (a barrier inside).
+template <int NT>
+__device__ __forceinline__ void block_amax_commit(float m, uint32_t* out) {
+  __shared__ float red[NT / 64];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = red[0];
+#pragma unroll
+    for (int i = 1; i < NT / 64; ++i) r = fmaxf(r, red[i]);
+    atomicMax(out, __float_as_uint(r));
+  }
+}
+
 // All-reduce of H per-lane values over the 64 lanes in (H - 1) + (6 - log2 H) shuffles instead
 // of 6 H: a butterfly that halves the value count per step (lanes with the mask bit set keep
 // the upper half) and then finishes the single remaining value inside 64/H-lane groups.  After
@@ -850,7 +870,7 @@ __device__ __forceinline__ float grp_sum_hi(float v) {
 // edge base e0, first atom a0) instead of LDS, which the big window needs for its rows.
 template <int H, int MODE, int NPA, int CW, int NT = 16 * CW, int WIN = kWinL, int ECAP = kECap,
           bool BIG = false>
-__device__ __forceinline__ void bwd_lds_chunks(
+__device__ __forceinline__ float bwd_lds_chunks(
     float4* zs, float4* gs, const float* s_att, const int* s_odst, const int* s_oslot,
     const int* s_orp, const int* s_rp, const uint16_t* s_src, float* s_ga,
     __amdgpu_buffer_rsrc_t rY, int ldyi, __amdgpu_buffer_rsrc_t rGo, __amdgpu_buffer_rsrc_t rO,
@@ -875,6 +895,7 @@ __device__ __forceinline__ void bwd_lds_chunks(
   // unconditional, so the compiler's vmcnt counts are exact
   const uint32_t noY = 4u * (uint32_t)(nr * ldyi), noGo = 4u * (uint32_t)(nr * ocols);
   const uint32_t noO = 4u * (uint32_t)(nr * HF), noG = 4u * (uint32_t)(nr * ldgi);
+  float gmx = 0.f;  // |max| of this thread's stores into gY (live rows, real chunks)
   bool live[NPA];
   // node role: the g_rst row slot (low 16 bits) and attention slot (high 16 bits) of the
   // first kEC out-edges of this octet's source atoms in registers (a missing edge reads the
@@ -966,9 +987,11 @@ __device__ __forceinline__ void bwd_lds_chunks(
       if (MODE != 1) {
         gs[r * LPD + (q ^ bwd_sw<LPD>(r))] = g;
         buf_st4(rG, ok ? grow(p) + 4u * (uint32_t)(HF + col_of(k)) : noG, g);
+        if (ok && r < nr) gmx = amax4(gmx, g);
       } else if (h == 0) {  // uniform branch: an all-out-of-range store is not free
         gs[r * LPD + (q ^ bwd_sw<LPD>(r))] = g;
         buf_st4(rG, ok ? grow(p) + 4u * (uint32_t)(HF + fc * CW + 4 * q) : noG, R.g[p]);
+        if (ok && r < nr) gmx = amax4(gmx, R.g[p]);
       }
     }
   };
@@ -1082,10 +1105,13 @@ __device__ __forceinline__ void bwd_lds_chunks(
     for (int i = 0; i + 1 < RB; ++i) ring[i] = ring[i + 1];
     load(k + 1 + RB, ring[RB - 1]);
 #pragma unroll
-    for (int p = 0; p < NPA; ++p)
+    for (int p = 0; p < NPA; ++p) {
       buf_st4(rG, grow(p) + 4u * (uint32_t)col_of(k), acc[p]);  // rows past the group: dropped
+      if (ds + DPP * p < nr) gmx = amax4(gmx, acc[p]);
+    }
     __syncthreads();
   }
+  return gmx;
 }
 
 // One workgroup of 512 threads per node group (2 per CU): the group's CSR, out-CSR and
@@ -1103,7 +1129,7 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
                        const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ elr,
                        const float* __restrict__ attn, const float* __restrict__ out,
                        const float* __restrict__ g_out, float slope, float* __restrict__ gY,
-                       int64_t ldgy, int C) {
+                       int64_t ldgy, int C, uint32_t* __restrict__ gy_amax) {
   constexpr int LPD = CW / 4;
   constexpr int DPP = NT / LPD;
   constexpr int NPM = WIN / DPP;  // passes over a full window
@@ -1127,6 +1153,7 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   __shared__ int s_wsum[BIG ? NT / 64 : 1];
   const GroupPlan gp(plan, G);
   const int nlist = BIG ? gp.count[1] : (int)blockIdx.x + 1;
+  float gmx = 0.f;  // |max| of this thread's gY stores, committed once after the group loop
   for (int li = blockIdx.x; li < nlist; li += BIG ? gridDim.x : 1) {
   const int grp = BIG ? gp.bwd_list[li] : li;
   if (BIG) __syncthreads();  // the previous group's LDS reads are done
@@ -1190,10 +1217,10 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
     __syncthreads();
   }
 #define MVML_BWD_CHUNKS(NPA)                                                                       \
-  bwd_lds_chunks<H, MODE, NPA, CW, NT, WIN, ECAP, BIG>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp,  \
+  gmx = fmaxf(gmx, bwd_lds_chunks<H, MODE, NPA, CW, NT, WIN, ECAP, BIG>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp,  \
                                                        s_src, s_ga, rY, ldyi, rGo, rO, rG, ldgi, nr, F, \
                                                        out_dst, out_inslot, e0, a0, s_segI, nsegI, \
-                                                       s_segO, nsegO, s_rs, s_part, s_oxe, s_oxb)
+                                                       s_segO, nsegO, s_rs, s_part, s_oxe, s_oxb))
   if (nr <= DPP) MVML_BWD_CHUNKS(1);
   else if (NPM == 2 || nr <= 2 * DPP) MVML_BWD_CHUNKS(2);
   else if (nr <= 3 * DPP) MVML_BWD_CHUNKS((NPM > 2 ? 3 : 2));
@@ -1220,6 +1247,7 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
       der += gp;
     }
     gY[(int64_t)(a0 + d) * ldgy + C + H + h] = der;
+    gmx = fmaxf(gmx, fabsf(der));
   }
   __syncthreads();
   for (int i = tid; i < nr * H; i += NT) {  // d el: sums over out-edges
@@ -1231,8 +1259,10 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
       del += s_ga[sl * H + h];
     }
     gY[(int64_t)(a0 + u) * ldgy + C + h] = del;
+    gmx = fmaxf(gmx, fabsf(del));
   }
   }
+  if (gy_amax) block_amax_commit<NT>(gmx, gy_amax);
 }
 
 // Pass A: one wave per destination v.
@@ -1244,8 +1274,10 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
                        const float* __restrict__ attn, const float* __restrict__ out,
                        const float* __restrict__ g_out, int F, float slope, int mode,
                        float* __restrict__ gpre, float* __restrict__ gY, int64_t ldgy,
-                       float* __restrict__ gelr, int64_t ldgl, int skip_big) {
+                       float* __restrict__ gelr, int64_t ldgl, int skip_big,
+                       uint32_t* __restrict__ gy_amax) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float gmx = 0.f;  // |max| of this thread's gY stores (block-uniform early returns only)
   // G > 0: one block per backward fallback group of the plan; G == 0: one wave per atom over
   // all atoms
   int64_t v, vend, vstep;
@@ -1285,9 +1317,14 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
   for (int c = 0; c < VPL; ++c) {
     const int col = 4 * (lane + 64 * c);
     if (mode != 1) {
-      if (okc[c]) st4(gyv + HF + col, gr[c]);
+      if (okc[c]) {
+        st4(gyv + HF + col, gr[c]);
+        gmx = amax4(gmx, gr[c]);
+      }
     } else if (col < F) {
-      st4(gyv + HF + col, ld4(g_out + v * F + col));
+      const float4 go = ld4(g_out + v * F + col);
+      st4(gyv + HF + col, go);
+      gmx = amax4(gmx, go);
     }
   }
   float er[H];
@@ -1357,7 +1394,10 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
     for (int h = 0; h < H; ++h) ger[h] += gp[h];
   }
   store_heads<H>(gelr + v * ldgl + H, ger, lane);
+#pragma unroll
+  for (int h = 0; h < H; ++h) gmx = fmaxf(gmx, fabsf(ger[h]));
   }
+  if (gy_amax) block_amax_commit<kWavesPerBlock * 64>(gmx, gy_amax);
 }
 
 // Pass B: one wave per source u (out-CSR gather).
@@ -1369,8 +1409,9 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
                        const float* __restrict__ attn, const float* __restrict__ gpre,
                        const float* __restrict__ out, const float* __restrict__ g_out, int F,
                        int mode, float* __restrict__ gY, int64_t ldgy, float* __restrict__ gelr,
-                       int64_t ldgl, int skip_big) {
+                       int64_t ldgl, int skip_big, uint32_t* __restrict__ gy_amax) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float gmx = 0.f;  // |max| of this thread's gY stores (block-uniform early returns only)
   // G > 0: one block per backward fallback group of the plan; G == 0: one wave per atom over
   // all atoms
   int64_t u, vend, vstep;
@@ -1443,9 +1484,15 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
   float* gyu = gY + u * ldgy;
 #pragma unroll
   for (int c = 0; c < VPL; ++c)
-    if (okc[c]) st4(gyu + 4 * (lane + 64 * c), gz[c]);
+    if (okc[c]) {
+      st4(gyu + 4 * (lane + 64 * c), gz[c]);
+      gmx = amax4(gmx, gz[c]);
+    }
   store_heads<H>(gelr + u * ldgl, gel, lane);
+#pragma unroll
+  for (int h = 0; h < H; ++h) gmx = fmaxf(gmx, fabsf(gel[h]));
   }
+  if (gy_amax) block_amax_commit<kWavesPerBlock * 64>(gmx, gy_amax);
 }
 
 template <int H>
@@ -1491,7 +1538,7 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
                const int32_t* orp, const int32_t* odst, const int32_t* oslot, const float* Y,
                int64_t ldy, const float* elr, const float* attn, const float* out,
                const float* g_out, int F, float slope, int mode, float* gpre, float* gY,
-               int64_t ldgy, int C, hipStream_t st) {
+               int64_t ldgy, int C, uint32_t* gy_amax, hipStream_t st) {
   if (getenv("MVML_BWD_ATOMWISE")) G = 0;  // experiment: per-atom pair over every atom
   if (F % 32 == 0 && G > 0) {  // molecule groups: one pass over Z / g_out / dZ per group
 #ifndef MVML_BWD_CW64
@@ -1502,7 +1549,7 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
 #define MVML_BWD_LDS(M, CW)                                                                       \
     gat_agg_bwd_lds_kernel<H, M, CW><<<(unsigned)G, 16 * CW, 0, st>>>(groups, G, rp, src, orp, odst, \
                                                                       oslot, Y, ldy, F, elr, attn, \
-                                                                      out, g_out, slope, gY, ldgy, C)
+                                                                      out, g_out, slope, gY, ldgy, C, gy_amax)
     if (MVML_BWD_CW64 && F % 64 == 0) {
       if (mode == 0) MVML_BWD_LDS(0, 64);
       else if (mode == 1) MVML_BWD_LDS(1, 64);
@@ -1524,7 +1571,7 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
 #define MVML_BWD_BIG(M)                                                                             \
       gat_agg_bwd_lds_kernel<H, M, 16, kBigThreads, kPlanBigAtoms, kPlanBigEdgeCap, true>            \
           <<<(unsigned)std::min<int64_t>(G, kBigBlocks), kBigThreads, 0, st>>>(                      \
-              groups, G, rp, src, orp, odst, oslot, Y, ldy, F, elr, attn, out, g_out, slope, gY, ldgy, C)
+              groups, G, rp, src, orp, odst, oslot, Y, ldy, F, elr, attn, out, g_out, slope, gY, ldgy, C, gy_amax)
       if (mode == 0) MVML_BWD_BIG(0);
       else if (mode == 1) MVML_BWD_BIG(1);
       else MVML_BWD_BIG(2);
@@ -1535,11 +1582,13 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
   }
   const unsigned blocks = G > 0 ? (unsigned)G : (unsigned)ceil_div(N, kWavesPerBlock);
   gat_agg_bwd_dst_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
-      N, groups, G, rp, src, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, gY + C, ldgy, big);
+      N, groups, G, rp, src, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, gY + C, ldgy, big,
+      gy_amax);
   int rc = check_launch("gat_agg_bwd_dst_kernel");
   if (rc) return rc;
   gat_agg_bwd_src_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
-      N, groups, G, rp, orp, odst, oslot, attn, gpre, out, g_out, F, mode, gY, ldgy, gY + C, ldgy, big);
+      N, groups, G, rp, orp, odst, oslot, attn, gpre, out, g_out, F, mode, gY, ldgy, gY + C, ldgy, big,
+      gy_amax);
   return check_launch("gat_agg_bwd_src_kernel");
 }
 
@@ -1766,8 +1815,8 @@ extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, i
                                 const int32_t* out_inslot, const float* Y, int64_t ldy,
                                 const float* elr, const float* attn, const float* out,
                                 const float* g_out, int H, int F, float slope, int mode, float* gY,
-                                int64_t ldgy, void* workspace, size_t workspace_bytes,
-                                void* stream) {
+                                int64_t ldgy, uint32_t* gy_amax, void* workspace,
+                                size_t workspace_bytes, void* stream) {
   clear_error();
   int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_bwd");
   if (rc) return rc;
@@ -1787,10 +1836,10 @@ extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, i
   float* gpre = static_cast<float*>(workspace);
   const int vpl = (int)ceil_div(H * F, 256);
   switch (H) {
-    case 1: { MVML_VPL_CASES(launch_bwd, 1, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, st) break; }
-    case 2: { MVML_VPL_CASES(launch_bwd, 2, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, st) break; }
-    case 4: { MVML_VPL_CASES(launch_bwd, 4, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, st) break; }
-    case 8: { MVML_VPL_CASES(launch_bwd, 8, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, st) break; }
+    case 1: { MVML_VPL_CASES(launch_bwd, 1, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, st) break; }
+    case 2: { MVML_VPL_CASES(launch_bwd, 2, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, st) break; }
+    case 4: { MVML_VPL_CASES(launch_bwd, 4, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, st) break; }
+    case 8: { MVML_VPL_CASES(launch_bwd, 8, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, st) break; }
   }
   set_error("gat_agg_bwd: unsupported shape");
   return MVML_ERR_INVALID;

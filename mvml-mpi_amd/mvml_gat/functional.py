@@ -150,7 +150,7 @@ class GATLayerFunction(torch.autograd.Function):
         # pass serves all of its products (projection, dL/dW, dL/dX)
         amx = None
         if (algo or GEMM_ALGO) == "f16x2":
-            amx = torch.empty(3, dtype=torch.int32, device=dev)
+            amx = torch.zeros(3, dtype=torch.int32, device=dev)  # [X, Wcat, gY (backward)]
             absmax(Xp, N, Fp, Fp, amx, 0)
             absmax(Wcat, C + 2 * H, Fp, Fp, amx, 1)
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_proj_fwd_workspace_size(N, H, F), dev)
@@ -196,10 +196,11 @@ class GATLayerFunction(torch.autograd.Function):
                             "bytes": agg_bwd_bytes(N, g.num_edges(), H, F, g_out.shape[1], mode)}
         call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
              ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr),
-             ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldg, wp, wn, st)
-        amx = ctx.amx
-        if amx is not None:
-            absmax(gY, N, CE, ldg, amx, 2)
+             ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldg,
+             slot(ctx.amx, 2), wp, wn, st)
+        amx = ctx.amx  # slot 2 = max |gY|, folded in by mvml_gat_agg_bwd's stores
+        if DEBUG_CAPTURE is not None and amx is not None:
+            DEBUG_CAPTURE.setdefault("gy_amax", []).append((gY[:, :CE].clone(), amx[2:3].clone()))
         # dL/d[Wcat ; A_l ; A_r] = gY^T X  (split-K over atoms)
         gW = torch.empty((CE, Fp), dtype=torch.float32, device=dev)
         gemm(gY, Xp, CE, Fp, N, 1, 1, ldg, Fp, gW, Fp, algo=ctx.algo,

@@ -217,3 +217,42 @@ def test_gat_layer_big_window_table_overflow(layer):
     sb = batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109)
     assert int(sb.num_edges[0]) <= 2432
     _layer_case(layer, sb, seed=5 + layer)
+
+
+@pytest.mark.parametrize("layer", [0, 1])
+@pytest.mark.parametrize("case", ["config2", "config5_big", "config5_fallback", "table_overflow",
+                                  "atomwise"])
+def test_gat_bwd_fused_gy_max(layer, case, monkeypatch):
+    """mvml_gat_agg_bwd folds max |gY| (the split-fp16 scale of the dL/dW and dL/dX GEMMs) into
+    its stores: it must equal the max over every column the GEMMs read, [dZ | dR | d el | d er],
+    on every kernel path that writes gY (LDS windows, big windows, the dst / src fallback pair
+    with and without node groups)."""
+    if Fn.GEMM_ALGO != "f16x2":
+        pytest.skip("the fused max feeds the split-fp16 GEMMs only")
+    sb = {"config2": lambda: synth.config2(64, seed=0),
+          "config5_big": lambda: synth.config5(2, seed=3),
+          "config5_fallback": lambda: synth.config5(2, seed=3),
+          "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109),
+          "atomwise": lambda: synth.config3(128, seed=2)}[case]()
+    if case == "config5_fallback":
+        monkeypatch.setenv("MVML_BIG_WINDOW", "0")
+    if case == "atomwise":
+        monkeypatch.setenv("MVML_BWD_ATOMWISE", "1")
+    prod, _ = model_pair(seed=layer)
+    conv = prod.conv.gnn_layers[layer].to(DEV)
+    g = sb.to_graph().to(DEV)
+    n = int(sb.num_nodes.sum())
+    X = (torch.as_tensor(sb.feats, dtype=torch.float32) if layer == 0
+         else torch.randn(n, 768, generator=torch.Generator().manual_seed(1))).to(DEV).requires_grad_()
+    cap = {}
+    Fn.DEBUG_CAPTURE = cap
+    try:
+        out = conv(g, X)
+        out.backward(torch.randn(out.shape, generator=torch.Generator().manual_seed(2)).to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        Fn.DEBUG_CAPTURE = None
+    (gY, amx), = cap["gy_amax"]
+    want = gY.abs().max().item()
+    got = amx.cpu().view(torch.float32).item()
+    assert got == want and want > 0, (got, want)

@@ -71,10 +71,11 @@ def main():
         gY = torch.empty((N, ldg), device="cuda")
         wsz = L.mvml_gat_agg_bwd_workspace_size(E, H)
         ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
+        gmx = torch.zeros(1, dtype=torch.int32, device="cuda")  # max |gY| (split-fp16 scale)
         b = lambda: call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups,
                          ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst),
                          ptr(g.out_inslot), ptr(Y), ldy, ptr(elr), ptr(attn), ptr(out), ptr(g_out), H, F,
-                         0.2, mode, ptr(gY), ldg, ptr(ws), wsz, st)
+                         0.2, mode, ptr(gY), ldg, ptr(gmx), ptr(ws), wsz, st)
         ms = timeit(b)
         by = agg_bwd_bytes(N, E, H, F, oc, mode)
         print(f"  agg_bwd {name:16s} {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
