@@ -207,14 +207,17 @@ class GATLayerFunction(torch.autograd.Function):
              amax=None if amx is None else (slot(amx, 2), slot(amx, 0)))
         g_fc = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_res = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
-        g_al = torch.empty_like(attn_l)
-        g_ar = torch.empty_like(attn_r)
         call("mvml_gat_unfold_grads", ptr(gW), ptr(attn_lr), H, F, Fin, Fp, mean_res, ptr(g_fc),
              ptr(g_res), st)
         gelr = gY[:, C:CE]
-        wp2, wn2 = _lib.ws_ptr_size(L.mvml_gat_attn_grad_workspace_size(N, H, F), dev)
-        call("mvml_gat_attn_grad", N, H, F, ptr(Y), ldy, ctypes.c_void_p(ptr(gY).value + 4 * C), ldg,
-             ptr(g_al), ptr(g_ar), wp2, wn2, st)
+        # dL/dattn_l[h, f] = sum_n d el[n, h] Z[n, h, f] = sum_k G_l[h, k] fc.weight[h F + f, k]
+        # with G_l = [d el]^T X — rows C .. C+H of gW, already formed by the dW GEMM (and G_r
+        # rows C+H ..): re-associated, a (2 x Fp) x (Fp x F) product per head instead of a pass
+        # over the N x H F projection (mvml_gat_attn_grad, kept in the ABI)
+        g_alr = torch.empty((2, HF), dtype=torch.float32, device=dev)
+        gemm_batched(gW[C:], Wcat, 2, F, Fp, 0, 0, H * Fp, Fp, g_alr, HF, H, Fp, F * Fp, F)
+        g_al = g_alr[0].view_as(attn_l)
+        g_ar = g_alr[1].view_as(attn_r)
         if DEBUG_CAPTURE is not None:
             DEBUG_CAPTURE.update(elr=elr, gelr=gelr, attn=attn)
         g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
