@@ -213,13 +213,15 @@ int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, const float* Y, int64_t 
  * Y is the projection output (mean_residual layout iff mode 1; ldy >= its C, multiple of 4),
  * elr its logits (mvml_gat_proj_fwd).  out is [N, H*F] (modes 0, 2) or [N, F] (mode 1).
  * attn [E, H] receives the edge_softmax output in in-CSR slot order (needed by the backward).
+ * out_amax (may be NULL): *out_amax = max(*out_amax, bits of max |out|), folded into the stores
+ * (the split-fp16 operand max of the next layer's / Set2Set's GEMMs; the caller zeroes it).
  * node_groups is the plan mvml_build_node_groups built from the same in_rowptr (a plan of
  * another graph is undefined behaviour); num_groups = mvml_node_group_count(num_nodes).
  * ------------------------------------------------------------------------------------- */
 int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
                      const int32_t* in_rowptr, const int32_t* in_src, const float* Y, int64_t ldy,
                      int H, int F, const float* elr, const float* bias, float slope, int mode,
-                     float* out, float* attn, void* stream);
+                     float* out, float* attn, uint32_t* out_amax, void* stream);
 /* Backward of mvml_gat_agg_fwd (DGL GSpMM / GSDDMM / EdgeSoftmax backward + torch autograd of
  * residual, bias, ELU, mean).  Atomic-free: the u_mul_e-sum transpose is a gather over the
  * out-CSR; one workgroup per node group reads Z, g_out and writes dZ once (molecule groups).

@@ -368,7 +368,7 @@ inline bool use_big_window(int H, int F) {
 // straight-line and the compiler's vmcnt waits are exact; stores of rows past the group are
 // skipped (an out-of-range store is not free).
 template <int H, int CW, int MODE, int NT, int NPA, int WIN = kWinL, int ECAP = kECap, bool BIG = false>
-__device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], const float* s_att,
+__device__ __forceinline__ float fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], const float* s_att,
                                                const int32_t* __restrict__ rowptr,
                                                const int32_t* __restrict__ in_src,
                                                __amdgpu_buffer_rsrc_t rY, uint32_t rowb,
@@ -396,6 +396,7 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], c
   // the group's own rows, so the address still translates through a warm TLB entry (a wild
   // out-of-range offset costs a page walk per access)
   const uint32_t noY = (uint32_t)nr * rowb;
+  float omx = 0.f;  // |max| of this thread's output stores (live rows)
   bool live[NPA];
 #pragma unroll
   for (int p = 0; p < NPA; ++p) {
@@ -521,14 +522,16 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], c
         // a store whose lanes are ALL out of range still costs a real one: branch (uniform)
         if (h == H - 1) {
           const float invh = (float)H;
-          buf_st4(rO, ob[p] + 4u * (uint32_t)((k / H) * CW + 4 * q),
-                  make_float4(tot[p].x / invh + rres[p].x, tot[p].y / invh + rres[p].y,
-                              tot[p].z / invh + rres[p].z, tot[p].w / invh + rres[p].w));
+          const float4 o = make_float4(tot[p].x / invh + rres[p].x, tot[p].y / invh + rres[p].y,
+                                       tot[p].z / invh + rres[p].z, tot[p].w / invh + rres[p].w);
+          buf_st4(rO, ob[p] + 4u * (uint32_t)((k / H) * CW + 4 * q), o);
+          if (ds + DPP * p < nr) omx = amax4(omx, o);
         }
       } else {
         float4 o = add4(add4(acc[p], rres[p]), b4);
         if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
         buf_st4(rO, ob[p] + 4u * (uint32_t)col, o);  // rows past the group: dropped
+        if (ds + DPP * p < nr) omx = amax4(omx, o);
       }
     };
     if constexpr (!BIG) {
@@ -556,6 +559,7 @@ __device__ __forceinline__ void fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], c
     for (int j = 0; j < NPA; ++j)
       if constexpr (!BIG) rres[j] = rnx[j];
   }
+  return omx;
 }
 
 // NT = 16 * CW threads: 64 destinations per pass; groups of <= 64 atoms (most of them: the
@@ -569,7 +573,7 @@ __global__ void __launch_bounds__(NT, MVML_LDS_WAVES)
 gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                        const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
                        int F, const float* __restrict__ bias, const float* __restrict__ attn,
-                       float* __restrict__ out) {
+                       float* __restrict__ out, uint32_t* __restrict__ out_amax) {
   constexpr int LPD = CW / 4;
   constexpr int DPP = NT / LPD;
   constexpr int NPM = WIN / DPP;  // passes over a full window
@@ -586,6 +590,7 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   const int tid = threadIdx.x;
   const GroupPlan gp(plan, G);
   const int nlist = BIG ? gp.count[0] : (int)blockIdx.x + 1;
+  float omx = 0.f;  // |max| of this thread's output stores, committed after the group loop
   for (int li = blockIdx.x; li < nlist; li += BIG ? gridDim.x : 1) {
   const int g = BIG ? gp.fwd_list[li] : li;
   if (BIG) __syncthreads();  // the previous group's LDS reads are done
@@ -612,14 +617,15 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   const __amdgpu_buffer_rsrc_t rY = make_rsrc(Y + (int64_t)a0 * ldy, (uint32_t)nr * rowb);
   const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)a0 * ocols, (uint32_t)(nr * ocols) * 4u);
   if (nr <= DPP)
-    fwd_lds_chunks<H, CW, MODE, NT, 1, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg);
+    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, 1, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg));
   else if (NPM == 2 || nr <= 2 * DPP)
-    fwd_lds_chunks<H, CW, MODE, NT, 2, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg);
+    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, 2, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg));
   else if (nr <= 3 * DPP)
-    fwd_lds_chunks<H, CW, MODE, NT, (NPM > 2 ? 3 : 2), WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg);
+    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, (NPM > 2 ? 3 : 2), WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg));
   else
-    fwd_lds_chunks<H, CW, MODE, NT, NPM, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg);
+    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, NPM, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg));
   }
+  if (out_amax) block_amax_commit<NT>(omx, out_amax);
 }
 
 template <int H, int CW, int MODE>
@@ -627,7 +633,7 @@ __global__ void __launch_bounds__(kAggThreads, 4)  // 2 workgroups (16 waves) pe
 gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                    const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
                    int F, const float* __restrict__ bias, const float* __restrict__ attn,
-                   float* __restrict__ out, int skip_big) {
+                   float* __restrict__ out, int skip_big, uint32_t* __restrict__ out_amax) {
   constexpr int LPD = CW / 4;                        // lanes per destination atom
   constexpr int DPP = kAggThreads / LPD;             // destinations per pass
   constexpr int NP = (kWin + DPP - 1) / DPP;         // passes over a full window
@@ -639,6 +645,7 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
   if (li < 0) return;
   const int g = gp.fwd_list[li];
   if (skip_big && (gp.kind[g] & 4)) return;  // the big-window kernel takes it
+  float omx = 0.f;  // |max| of this thread's output stores (block-uniform early returns only)
   const int a0 = gp.start[g], a1 = gp.start[g + 1];
   const int nfc = F / CW;     // column chunks per head
   const int nch = H * nfc;
@@ -750,14 +757,16 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
             tot[p] = (h == 0) ? t : add4(tot[p], t);
             if (h == H - 1) {
               const float invh = (float)H;
-              buf_st4(rO, 4u * (uint32_t)(d * F + fc * CW + 4 * q),
-                      make_float4(tot[p].x / invh + rm[p].x, tot[p].y / invh + rm[p].y,
-                                  tot[p].z / invh + rm[p].z, tot[p].w / invh + rm[p].w));
+              const float4 o = make_float4(tot[p].x / invh + rm[p].x, tot[p].y / invh + rm[p].y,
+                                           tot[p].z / invh + rm[p].z, tot[p].w / invh + rm[p].w);
+              buf_st4(rO, 4u * (uint32_t)(d * F + fc * CW + 4 * q), o);
+              omx = amax4(omx, o);
             }
           } else {
             float4 o = add4(add4(acc[p], res[p]), ld4(bias + col));
             if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
             buf_st4(rO, 4u * (uint32_t)(d * HF + col), o);
+            omx = amax4(omx, o);
           }
         }
       }
@@ -795,6 +804,7 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
           float4 o = add4(add4(acc, res), ld4(bias + col));
           if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
           buf_st4(rO, 4u * (uint32_t)(d * HF + col), o);
+          omx = amax4(omx, o);
         }
       }
       if (MODE == 1) {  // head mean, heads summed in order as in the chunk sweep
@@ -804,14 +814,16 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
           for (int hh = 1; hh < H; ++hh) tot = add4(tot, s_hub[hh * (F / 4) + f4]);
           const float4 rmv = buf_ld4(rY, vb + 4u * (uint32_t)(HF + 4 * f4));
           const float invh = (float)H;
-          buf_st4(rO, 4u * (uint32_t)(d * F + 4 * f4),
-                  make_float4(tot.x / invh + rmv.x, tot.y / invh + rmv.y, tot.z / invh + rmv.z,
-                              tot.w / invh + rmv.w));
+          const float4 o = make_float4(tot.x / invh + rmv.x, tot.y / invh + rmv.y,
+                                       tot.z / invh + rmv.z, tot.w / invh + rmv.w);
+          buf_st4(rO, 4u * (uint32_t)(d * F + 4 * f4), o);
+          omx = amax4(omx, o);
         }
         __syncthreads();
       }
     }
   }
+  if (out_amax) block_amax_commit<kAggThreads>(omx, out_amax);
 }
 
 // --------------------------------------------------------------------------------- backward
@@ -1498,7 +1510,7 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
 template <int H>
 int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, const int32_t* src,
                const float* Y, int64_t ldy, int F, const float* bias, float slope, int mode,
-               float* out, float* attn, const float* elr, hipStream_t st) {
+               float* out, float* attn, const float* elr, uint32_t* out_amax, hipStream_t st) {
   int rc;
   gat_softmax_kernel<H><<<(unsigned)ceil_div(N * H, 256), 256, 0, st>>>(N, rp, src, elr, slope, attn);
   rc = check_launch("gat_softmax_kernel");
@@ -1508,14 +1520,14 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
 #define MVML_AGG_FWD_M(CW, M)                                                                       \
   do {                                                                                              \
     gat_agg_fwd_lds_kernel<H, CW, M, CW * 16><<<(unsigned)G, CW * 16, 0, st>>>(groups, G, rp, src, Y, ldy, F, \
-                                                                         bias, attn, out);          \
+                                                                         bias, attn, out, out_amax); \
     gat_agg_fwd_gather_kernel<H, CW, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, G, rp, src, Y, ldy, \
-                                                                            F, bias, attn, out, big); \
+                                                                            F, bias, attn, out, big, out_amax); \
     if constexpr (H <= 4)                                                                           \
       if (big)                                                                                      \
         gat_agg_fwd_lds_kernel<H, 16, M, kBigThreads, kPlanBigAtoms, kPlanBigEdgeCap, true>          \
             <<<(unsigned)std::min<int64_t>(G, kBigBlocks), kBigThreads, 0, st>>>(                    \
-                groups, G, rp, src, Y, ldy, F, bias, attn, out);                                    \
+                groups, G, rp, src, Y, ldy, F, bias, attn, out, out_amax);                          \
   } while (0)
 #define MVML_AGG_FWD(CW)                                  \
   do {                                                    \
@@ -1783,7 +1795,8 @@ extern "C" int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx,
 extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
                                 const int32_t* in_rowptr, const int32_t* in_src, const float* Y,
                                 int64_t ldy, int H, int F, const float* elr, const float* bias,
-                                float slope, int mode, float* out, float* attn, void* stream) {
+                                float slope, int mode, float* out, float* attn, uint32_t* out_amax,
+                                void* stream) {
   clear_error();
   int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_fwd");
   if (rc) return rc;
@@ -1796,10 +1809,10 @@ extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, i
   if (num_nodes == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
   switch (H) {
-    case 1: return launch_fwd<1>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, st);
-    case 2: return launch_fwd<2>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, st);
-    case 4: return launch_fwd<4>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, st);
-    case 8: return launch_fwd<8>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, st);
+    case 1: return launch_fwd<1>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, st);
+    case 2: return launch_fwd<2>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, st);
+    case 4: return launch_fwd<4>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, st);
+    case 8: return launch_fwd<8>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, st);
   }
   set_error("gat_agg_fwd: unsupported shape");
   return MVML_ERR_INVALID;

@@ -67,6 +67,15 @@ _GEMM_ENTRY = {"f32": ("mvml_gemm_f32", 0), "x3": ("mvml_gemm_f32x3", 1),
                "f16x2": ("mvml_gemm_f16x2", 3)}
 
 
+def known_amax(X):
+    """(int32 tensor, slot) holding max |X| bits if the kernel that produced X folded it into
+    its stores (X._mvml_amax, set by the producer; valid while X is unmodified), else None."""
+    rec = getattr(X, "_mvml_amax", None)
+    if rec is None or rec[2] != X._version:
+        return None
+    return rec[0], rec[1]
+
+
 def absmax(P, rows, cols, ld, out, slot=0, offset=0, accumulate=False):
     """out[slot] (int32 tensor) = bits of max |P[r, offset + c]| (mvml_absmax_f32)."""
     pp = ctypes.c_void_p(ptr(P).value + 4 * offset)
@@ -136,6 +145,10 @@ class GATLayerFunction(torch.autograd.Function):
         # GEMM operand row is 16-B aligned and the LDS-DMA path applies; pad columns are zero.
         Fp = _round4(Fin)
         Xp = X if Fp == Fin else torch.nn.functional.pad(X, (0, Fp - Fin))
+        # (a ones pad column that would make the dW GEMM emit the bias gradient as well was
+        # measured 1.02e-5 from float64 on config 3 — the bias sums cancel and the split-fp16
+        # representation error shows — so the bias keeps its exact fp32 column sum)
+        ones_col = False
         attn_l, attn_r = _c(attn_l), _c(attn_r)
         attn_lr = torch.cat([attn_l.reshape(-1), attn_r.reshape(-1)])
         # [fc.weight ; res_fc.weight (or its head mean) ; A_l ; A_r]: the projection GEMM uses
@@ -149,15 +162,19 @@ class GATLayerFunction(torch.autograd.Function):
         # split-fp16: |max| of X, Wcat (all C + 2H rows) and, in the backward, gY — each operand's
         # pass serves all of its products (projection, dL/dW, dL/dX)
         amx = None
+        ax = None  # (tensor, slot) of max |X|
         if (algo or GEMM_ALGO) == "f16x2":
-            amx = torch.zeros(3, dtype=torch.int32, device=dev)  # [X, Wcat, gY (backward)]
-            absmax(Xp, N, Fp, Fp, amx, 0)
+            amx = torch.zeros(4, dtype=torch.int32, device=dev)  # [X, Wcat, gY (bwd), out]
+            ax = known_amax(Xp) if Xp is X else None  # layer 2: folded by layer 1's aggregation
+            if ax is None:
+                absmax(Xp, N, Fp, Fp, amx, 0)
+                ax = (amx, 0)
             absmax(Wcat, C + 2 * H, Fp, Fp, amx, 1)
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_proj_fwd_workspace_size(N, H, F), dev)
         _lib.call_tag[0] = {"flops": 2 * N * C * Fp}
         call("mvml_gat_proj_fwd", N, ptr(Xp), Fp, Fp, ptr(Wcat), Fp, ptr(attn_lr), H, F, mean_res,
-             _GEMM_ENTRY[algo or GEMM_ALGO][1], ptr(Y), ldy, ptr(elr), slot(amx, 0), slot(amx, 1),
-             wp, wn, st)
+             _GEMM_ENTRY[algo or GEMM_ALGO][1], ptr(Y), ldy, ptr(elr),
+             None if ax is None else slot(*ax), slot(amx, 1), wp, wn, st)
         out_cols = F if mode == MODE_MEAN else HF
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()
@@ -165,7 +182,9 @@ class GATLayerFunction(torch.autograd.Function):
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}", "bytes": agg_fwd_bytes(N, E, H, F, out_cols, C - HF)}
         call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
              ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(_c(bias)), float(slope), int(mode),
-             ptr(out), ptr(attn), st)
+             ptr(out), ptr(attn), slot(amx, 3), st)
+        if amx is not None:  # max |out| for the consumer's split-fp16 GEMMs (next layer, Set2Set)
+            out._mvml_amax = (amx, 3, out._version)
         if DEBUG_CAPTURE is not None:
             DEBUG_CAPTURE.setdefault("elr_fwd", []).append(elr.detach().clone())
         ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr)
@@ -173,6 +192,8 @@ class GATLayerFunction(torch.autograd.Function):
         ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode, ctx.ldy = g, H, F, slope, mode, ldy
         ctx.algo = algo
         ctx.amx = amx
+        ctx.ax = ax
+        ctx.ones_col = ones_col
         return out
 
     @staticmethod
@@ -204,7 +225,7 @@ class GATLayerFunction(torch.autograd.Function):
         # dL/d[Wcat ; A_l ; A_r] = gY^T X  (split-K over atoms)
         gW = torch.empty((CE, Fp), dtype=torch.float32, device=dev)
         gemm(gY, Xp, CE, Fp, N, 1, 1, ldg, Fp, gW, Fp, algo=ctx.algo,
-             amax=None if amx is None else (slot(amx, 2), slot(amx, 0)))
+             amax=None if amx is None else (slot(amx, 2), slot(*ctx.ax)))
         g_fc = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_res = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         call("mvml_gat_unfold_grads", ptr(gW), ptr(attn_lr), H, F, Fin, Fp, mean_res, ptr(g_fc),
@@ -222,8 +243,14 @@ class GATLayerFunction(torch.autograd.Function):
             DEBUG_CAPTURE.update(elr=elr, gelr=gelr, attn=attn)
         g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
         if mean_res:  # every head's bias sees g_out / H: one column sum, replicated over heads
-            colsum(gY, N, F, ldg, g_bias, offset=HF, alpha=1.0 / H)
+            if ctx.ones_col:
+                g_bias[:F].copy_(gW[HF:HF + F, Fin])
+                g_bias[:F].mul_(1.0 / H)
+            else:
+                colsum(gY, N, F, ldg, g_bias, offset=HF, alpha=1.0 / H)
             g_bias.view(H, F)[1:].copy_(g_bias[:F].expand(H - 1, F))
+        elif ctx.ones_col:  # gY^T [.. | 1] from the dW GEMM (Xp's column Fin)
+            g_bias.copy_(gW[HF:2 * HF, Fin])
         else:
             colsum(gY, N, HF, ldg, g_bias, offset=HF)
         gX = None
@@ -279,8 +306,12 @@ class Set2SetFunction(torch.autograd.Function):
             # LSTM outputs h = o tanh(c) (|h| < 1) and, in layer 0, the readout r = sum_n a_n x_n
             # (a convex combination: |r| <= max |X|), so max(1, max |X|) bounds every cell's A
             # (an upper bound is all the scale needs) — one pass instead of one per cell
-            amax_x = torch.full((1,), 0x3F800000, dtype=torch.int32, device=dev)  # bits of 1.0f
-            absmax(X, N, D, D, amax_x, 0, accumulate=True)
+            kx = known_amax(X)  # folded by the last GAT layer's aggregation
+            if kx is not None:  # max(1, max |X|) on the float bits (non-negative: int order)
+                amax_x = torch.clamp_min(kx[0][kx[1]:kx[1] + 1], 0x3F800000)
+            else:
+                amax_x = torch.full((1,), 0x3F800000, dtype=torch.int32, device=dev)  # 1.0f
+                absmax(X, N, D, D, amax_x, 0, accumulate=True)
             amax_w = torch.empty(Lr, dtype=torch.int32, device=dev)
             for l in range(Lr):
                 absmax(Wcat[l], 4 * D, kin[l] + D, kin[l] + D, amax_w, l)  # = Wperm's max

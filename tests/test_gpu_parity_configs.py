@@ -256,3 +256,7 @@ def test_gat_bwd_fused_gy_max(layer, case, monkeypatch):
     want = gY.abs().max().item()
     got = amx.cpu().view(torch.float32).item()
     assert got == want and want > 0, (got, want)
+    # and max |out| folded into the forward aggregation's stores (the next GEMMs' operand max)
+    t, i, _ = out._mvml_amax
+    got_o = t[i:i + 1].cpu().view(torch.float32).item()
+    assert got_o == out.detach().abs().max().item(), (got_o, out.detach().abs().max().item())

@@ -56,7 +56,7 @@ def main():
         elr.normal_()
         f = lambda: call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.num_node_groups,
                          ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(bias), 0.2,
-                         mode, ptr(out), ptr(attn), st)
+                         mode, ptr(out), ptr(attn), None, st)
         if a.no_fwd:
             f()
             ms = float("nan")
