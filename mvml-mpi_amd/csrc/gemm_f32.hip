@@ -1013,8 +1013,14 @@ __device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], floa
 #ifndef MVML_X3W_SGB_V
 #define MVML_X3W_SGB_V 3
 #endif
+#ifndef MVML_H2_SGB
+#define MVML_H2_SGB 1
+#endif
 #ifndef MVML_H2_KS
-#define MVML_H2_KS 2
+#define MVML_H2_KS (MVML_H2_SGB ? 1 : 2)
+#endif
+#ifndef MVML_X3W_SGB_V2
+#define MVML_X3W_SGB_V2 3
 #endif
 // FAST (host-checked: both operands 16-B aligned rows, K-major row counts % 4 == 0): whole
 // stages by unguarded loads from clamped rows, the K tail as one guarded stage; !FAST: every
@@ -1167,7 +1173,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   // stage t+1 (in va / vb) into the other buffer; LOAD: 0 none, 1 fast, 2 guarded load of t+2.
   // Each (STAGE, LOAD) is its own straight-line body: no control flow around the accumulators.
   auto body = [&](int64_t t, auto STAGE, auto LOAD) {
-#if MVML_X3W_SGB
+#if MVML_X3W_SGB || MVML_H2_SGB
     const uint8_t* sa = lds + (t & 1) * kStage;
     const uint8_t* sb = sa + OA::kBytes;
     bf16x8 fb[2][NP];
@@ -1175,7 +1181,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int p = 0; p < NP; ++p) fb[j][p] = OB::frag(sb, p, wn * 64 + 32 * j, lane);
-    if constexpr (decltype(STAGE)::value && NP == 3) {
+    if constexpr (MVML_X3W_SGB && decltype(STAGE)::value && NP == 3) {
       // Interleaved schedule: every fragment of stage t is read from LDS FIRST (so the split's
       // LDS writes into the other buffer, which the compiler cannot prove disjoint, do not pin
       // the reads behind them), then the split of stage t+1 (VALU + LDS writes) and the global
@@ -1209,6 +1215,36 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       for (int k = 0; k < 24; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x2, 1, 0);
+      }
+      __syncthreads();
+      return;
+    }
+    if constexpr (MVML_H2_SGB && decltype(STAGE)::value && NP == 2 && KS == 1) {
+      // the same interleave for split-fp16 (default): 24 MFMAs carry the 32 split VALU (8 per
+      // float4: 2 pk_mul, 2 cvt_pk, 4 fma_mix), 8 LDS plane writes and the 4 global loads —
+      // measured +3 / +7 / +3 % on the L2 forward / dX / dW shapes over two sub-stages per
+      // barrier without the interleave (tools/gemm_bench.py)
+      bf16x8 fa[4][NP];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) fa[i][p] = OA::frag(sa, p, wm * 128 + 32 * i, lane);
+      stage((t + 1) & 1);
+      if constexpr (decltype(LOAD)::value == 1) load_fast();
+      if constexpr (decltype(LOAD)::value == 2) load_guarded(t + 2);
+      if constexpr (decltype(LOAD)::value == 3) load_masked(t + 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_np<NP>(fa[i], fb[j], acc[i][j]);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4 * NP, 0);  // fb + fa[0]
+#pragma unroll
+      for (int k = 0; k < 24; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x2, MVML_X3W_SGB_V2, 0);
+        if (k % 3 == 2) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        if (k == 1 || k == 4 || k == 7) __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);  // fa[1..3]
+        if (k == 12) __builtin_amdgcn_sched_group_barrier(0x20, 4, 0);
       }
       __syncthreads();
       return;
