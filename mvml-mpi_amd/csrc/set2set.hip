@@ -277,8 +277,14 @@ extern "C" int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const floa
   MVML_REQUIRE(B >= 0 && D > 0 && ldgh >= D, "lstm_cell_bwd: bad shape");
   if (B == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
-  lstm_cell_bwd_kernel<<<grid_for(B * D), 256, 0, st>>>(B, D, act, c, c_prev, g_h, ldgh, g_c,
-                                                        g_gates, g_c_prev, gg_amax);
+  // with gg_amax, one atomicMax per workgroup on a single word: a short kernel whose thousands
+  // of workgroups end together saturates it (~88 per us), so each thread takes >= 16 elements
+  // (MVP's 8k-row cells: 768 workgroups instead of 12k; Set2Set's 64k-row cells: 6k)
+  const unsigned grid = gg_amax ? (unsigned)std::min<int64_t>(
+                                      grid_for(B * D), std::max<int64_t>(256, ceil_div(B * D, 4096)))
+                                : grid_for(B * D);
+  lstm_cell_bwd_kernel<<<grid, 256, 0, st>>>(B, D, act, c, c_prev, g_h, ldgh, g_c, g_gates,
+                                             g_c_prev, gg_amax);
   return check_launch("lstm_cell_bwd_kernel");
 }
 

@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from ._lib import call, lib, ptr, workspace
-from .functional import LinearReLUFunction, _c, _check_cuda_f32, _stream, colsum, gemm
+from .functional import LinearReLUFunction, _c, _check_cuda_f32, _stream, absmax, colsum, gemm, slot
 
 
 class tokens_struct:
@@ -153,6 +153,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                  ptr(wc[7]), ptr(out), ptr(c[0]), ptr(c[1]), ptr(act[0]), ptr(act[1]), st)
             saved = [c[0], act[0], c[1], act[1]]
         else:  # wide batches: per-step MFMA GEMM (beta = 1 onto the projection) + cell kernel
+            amx = _h_bounds(w, dev)
             for d in range(2):
                 w_hh, b_ih, b_hh = (_c(t) for t in w[4 * d + 1:4 * d + 4])
                 gates = gates_d[d]
@@ -164,7 +165,8 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                     bs = pk.batch_sizes[t]
                     c_prev = None
                     if prev is not None:
-                        gemm(out[prev, :, d * H:], w_hh, bs, G, H, 0, 0, 2 * H, H, gates[t], G, beta=1.0)
+                        gemm(out[prev, :, d * H:], w_hh, bs, G, H, 0, 0, 2 * H, H, gates[t], G, beta=1.0,
+                             amax=None if amx is None else (slot(amx, 0), slot(amx, 1 + d)))
                         c_prev = c[prev]
                     call("mvml_lstm_cell_fwd", bs, H, ptr(gates[t]), ptr(b_ih), ptr(b_hh), ptr(c_prev),
                          ptr(c[t]), ptr(out[t, :, d * H:]), 2 * H, ptr(act[t]), None, 0, st)
@@ -195,7 +197,13 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             call("mvml_bilstm_seq_bwd", T, B, H, ptr(pk.batch_sizes_host), ptr(w_hhT[0]),
                  ptr(w_hhT[1]), ptr(a0), ptr(a1), ptr(c0), ptr(c1), ptr(g), ptr(ggs[0]),
                  ptr(ggs[1]), ptr(carry), st)
-        else:  # wide batches: per-step recurrent GEMM (beta = 1 into g) + cell kernel
+        amx = amg = None
+        if not seq:
+            amx = _h_bounds(w, dev)
+            # running max |dgates| per direction, folded in by mvml_lstm_cell_bwd (a bound for
+            # every step already processed, which is all a scale needs)
+            amg = torch.zeros(2, dtype=torch.int32, device=dev) if amx is not None else None
+        if not seq:  # wide batches: per-step recurrent GEMM (beta = 1 into g) + cell kernel
             g = g.clone()
             for d in range(2):
                 c, act, gg = cs[d], acts[d], ggs[d]
@@ -206,12 +214,14 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                     bs = pk.batch_sizes[t]
                     if nxt is not None:  # recurrent gradient from the step this one fed
                         rows = min(bs, pk.batch_sizes[nxt])
-                        gemm(gg[nxt], w_hhT[d], rows, H, G, 0, 0, G, G, g[t, :, d * H:], 2 * H, beta=1.0)
+                        gemm(gg[nxt], w_hhT[d], rows, H, G, 0, 0, G, G, g[t, :, d * H:], 2 * H, beta=1.0,
+                             amax=None if amg is None else (slot(amg, d), slot(amx, 1 + d)))
                     tp = t - 1 if d == 0 else t + 1
                     c_prev = c[tp] if 0 <= tp < T else None
                     g_c = carry[k % 2] if nxt is not None else None
                     call("mvml_lstm_cell_bwd", bs, H, ptr(act[t]), ptr(c[t]), ptr(c_prev),
-                         ptr(g[t, :, d * H:]), 2 * H, ptr(g_c), ptr(gg[t]), ptr(carry[(k + 1) % 2]), None, st)
+                         ptr(g[t, :, d * H:]), 2 * H, ptr(g_c), ptr(gg[t]), ptr(carry[(k + 1) % 2]),
+                         slot(amg, d), st)
                     nxt, k = t, k + 1
         for d in range(2):  # weight / input gradients: GEMMs over all positions
             w_ih, gg = _c(w[4 * d]), ggs[d]
@@ -220,7 +230,8 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             g_whh = torch.zeros((G, H), dtype=torch.float32, device=dev)
             if T > 1:
                 A, Bm = (gg[1:], out[:-1, :, d * H:]) if d == 0 else (gg[:-1], out[1:, :, d * H:])
-                gemm(A, Bm, G, H, (T - 1) * B, 1, 1, G, 2 * H, g_whh, H)
+                gemm(A, Bm, G, H, (T - 1) * B, 1, 1, G, 2 * H, g_whh, H,  # Bm = h: |h| < 1
+                     amax=None if amg is None else (slot(amg, d), slot(amx, 0)))
             g_wih = torch.empty((G, In), dtype=torch.float32, device=dev)
             beta = 1.0 if d else 0.0
             if layer0:
@@ -241,6 +252,19 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                 gemm(gg, w_ih, T * B, In, G, 0, 1, G, In, g_x, In, beta=beta)
             g_w[4 * d:4 * d + 4] = [g_wih, g_whh, gb, gb.clone()]
         return (g_x, None, None, *g_w)
+
+
+def _h_bounds(w, dev):
+    """Split-fp16 maxima of the wide-batch recurrence: [bits of 1.0 (|h| = |o tanh c| < 1 bounds
+    every recurrent operand row), max |W_hh| of the two directions]; None for other algos."""
+    from . import functional as _F
+    if _F.GEMM_ALGO != "f16x2":
+        return None
+    amx = torch.full((3,), 0x3F800000, dtype=torch.int32, device=dev)
+    for d in range(2):
+        wh = _c(w[4 * d + 1])
+        absmax(wh, wh.shape[0], wh.shape[1], wh.shape[1], amx, 1 + d)
+    return amx
 
 
 class SelectLastFunction(torch.autograd.Function):
