@@ -346,10 +346,12 @@ int mvml_token_attn_bwd(int64_t B, int H, int dk, const float* qkv, int64_t ld, 
 int mvml_token_attn_fold_fwd(int64_t B, int H, int dk, const float* pv, int64_t ld,
                              const float* x, int64_t ldx, float scale, float* att, float* P,
                              void* stream);
+/* g_pv_amax (may be NULL): *g_pv_amax = max(*g_pv_amax, bits of max |g_pv|) (split-fp16 scale
+ * of the two GEMMs that read g_pv; the caller zeroes it). */
 int mvml_token_attn_fold_bwd(int64_t B, int H, int dk, const float* pv, int64_t ld,
                              const float* x, int64_t ldx, float scale, const float* P,
                              const float* g_att, float* g_pv, int64_t ldg, float* g_k,
-                             int64_t ldgk, void* stream);
+                             int64_t ldgk, uint32_t* g_pv_amax, void* stream);
 int mvml_conv3_fwd(int64_t B, int C, int O, int W, const float* in, const float* weight,
                    const float* bias, float* out, void* stream);
 size_t mvml_conv3_bwd_workspace_size(int64_t B);

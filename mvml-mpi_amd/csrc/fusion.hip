@@ -323,10 +323,11 @@ token_attn_fold_bwd_kernel(int64_t B, int H, int dk, const float* __restrict__ p
                            const float* __restrict__ x, int64_t ldx, float scale,
                            const float* __restrict__ P, const float* __restrict__ g_att,
                            float* __restrict__ gpv, int64_t ldg, float* __restrict__ gk,
-                           int64_t ldgk) {
+                           int64_t ldgk, uint32_t* __restrict__ gpv_amax) {
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (b >= B) return;
+  float gmx = 0.f;  // |max| of this lane's gpv stores (split-fp16 scale of the two GEMMs)
   const int64_t HD = (int64_t)H * dk;
   float k[NT][kDkVpl], gks[NT][kDkVpl];
 #pragma unroll
@@ -376,6 +377,7 @@ token_attn_fold_bwd_kernel(int64_t B, int H, int dk, const float* __restrict__ p
 #pragma unroll
         for (int a = 0; a < NT; ++a) o = fmaf(p[a][c], g[a][i], o);
         grow[HD + lane + 64 * i] = o;
+        gmx = fmaxf(gmx, fabsf(o));
       }
     }
     float q[NT][kDkVpl];
@@ -397,6 +399,7 @@ token_attn_fold_bwd_kernel(int64_t B, int H, int dk, const float* __restrict__ p
           ok = fmaf(gs[c][t], q[c][i], ok);
         }
         grow[lane + 64 * i] = oq;
+        gmx = fmaxf(gmx, fabsf(oq));
         gks[t][i] += ok;
       }
     }
@@ -405,6 +408,10 @@ token_attn_fold_bwd_kernel(int64_t B, int H, int dk, const float* __restrict__ p
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int i = 0; i < kDkVpl; ++i) gk[(b * NT + t) * ldgk + lane + 64 * i] = gks[t][i];
+  if (gpv_amax) {  // one unsigned atomicMax of the float bits per wave (waves may exit early)
+    gmx = wave_max(gmx);
+    if (lane == 0) atomicMax(gpv_amax, __float_as_uint(gmx));
+  }
 }
 
 // Conv2d(C, O, 3) over the (C, 3, W) cube of one molecule (model.py:27, 69): the kernel height
@@ -953,14 +960,14 @@ extern "C" int mvml_token_attn_fold_fwd(int64_t B, int H, int dk, const float* p
 extern "C" int mvml_token_attn_fold_bwd(int64_t B, int H, int dk, const float* pv, int64_t ld,
                                         const float* x, int64_t ldx, float scale, const float* P,
                                         const float* g_att, float* g_pv, int64_t ldg, float* g_k,
-                                        int64_t ldgk, void* stream) {
+                                        int64_t ldgk, uint32_t* gpv_amax, void* stream) {
   clear_error();
   MVML_REQUIRE(B >= 0 && H > 0 && dk == 64 * kDkVpl && ld >= 2 * (int64_t)H * dk && ldx >= dk &&
                    ldg >= 2 * (int64_t)H * dk && ldgk >= dk,
                "token_attn_fold_bwd: bad shape");
   if (B == 0) return MVML_OK;
   token_attn_fold_bwd_kernel<<<(unsigned)ceil_div(B, 4), 256, 0, as_stream(stream)>>>(
-      B, H, dk, pv, ld, x, ldx, scale, P, g_att, g_pv, ldg, g_k, ldgk);
+      B, H, dk, pv, ld, x, ldx, scale, P, g_att, g_pv, ldg, g_k, ldgk, gpv_amax);
   return check_launch("token_attn_fold_bwd_kernel");
 }
 

@@ -126,14 +126,16 @@ class FusionAttnConvFunction(torch.autograd.Function):
         if fold:
             Bcat, PV = S0, S1
             gPV = torch.empty((3 * B, 2 * HD), **f32)
+            amx = None
+            if _F.GEMM_ALGO == "f16x2":  # split-fp16 maxima: gPV (folded by the kernel), Xn, Bcat
+                amx = torch.zeros(3, dtype=torch.int32, device=dev)
             # g_k (the keys' gradient, summed over heads) lands in gXn: the GEMMs add onto it
             call("mvml_token_attn_fold_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
-                 ptr(P), ptr(g_att), ptr(gPV), 2 * HD, ptr(gXn), D, st)
-            amx = None
-            if _F.GEMM_ALGO == "f16x2":  # split-fp16 maxima, one pass per operand: gPV, Xn, Bcat
-                amx = torch.empty(3, dtype=torch.int32, device=dev)
-                absmax(gPV, 3 * B, 2 * HD, 2 * HD, amx, 0)
+                 ptr(P), ptr(g_att), ptr(gPV), 2 * HD, ptr(gXn), D, slot(amx, 0), st)
+            if amx is not None:
                 absmax(Xn, 3 * B, D, D, amx, 1)
+                if _F.DEBUG_CAPTURE is not None:
+                    _F.DEBUG_CAPTURE["gpv_amax"] = (gPV.clone(), amx[0:1].clone())
                 absmax(Bcat, D, 2 * HD, 2 * HD, amx, 2)
             G2 = torch.empty((2 * HD, D), **f32)  # [h D + j][i] = dL/dM_h[i][j]; then dL/dW_v
             gemm(gPV, Xn, 2 * HD, D, 3 * B, 1, 1, 2 * HD, D, G2, D,

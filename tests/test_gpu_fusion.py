@@ -143,3 +143,24 @@ def test_fpn_module_parity(B):
     pr = dict(ref.named_parameters())
     for name, p in mod.named_parameters():
         assert rel_err(p.grad, pr[name].grad) < TOL, name
+
+
+@pytest.mark.parametrize("B", [5, 1000])
+def test_fusion_fold_bwd_gpv_max(B):
+    """mvml_token_attn_fold_bwd folds max |g_pv| (the split-fp16 scale of the two GEMMs that
+    read it) into its stores: equal to the max of the tensor it wrote."""
+    from mvml_gat import functional as Fn
+    if Fn.GEMM_ALGO != "f16x2":
+        pytest.skip("the folded max feeds the split-fp16 GEMMs only")
+    _, mod, xs = _pair(B, seed=3)
+    xd = [x.float().to(DEV).requires_grad_(True) for x in xs]
+    cap = {}
+    Fn.DEBUG_CAPTURE = cap
+    try:
+        mod(*xd).sum().backward()
+        torch.cuda.synchronize()
+    finally:
+        Fn.DEBUG_CAPTURE = None
+    gpv, amx = cap["gpv_amax"]
+    got = amx.cpu().view(torch.float32).item()
+    assert got == gpv.abs().max().item() and got > 0
