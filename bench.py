@@ -49,7 +49,8 @@ TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32
          "mvml_token_attn_fwd", "mvml_token_attn_bwd", "mvml_token_attn_fold_fwd",
          "mvml_token_attn_fold_bwd", "mvml_gemm_f32x3_batched", "mvml_conv3_fwd", "mvml_conv3_bwd",
          "mvml_bce_logits", "mvml_gat_attn_grad", "mvml_bilstm_seq_fwd", "mvml_bilstm_seq_bwd",
-         "mvml_lstm_gates_cell_fwd", "mvml_gemm_f16x2", "mvml_gemm_f16x2_amax", "mvml_absmax_f32"]
+         "mvml_lstm_gates_cell_fwd", "mvml_gemm_f16x2", "mvml_gemm_f16x2_amax", "mvml_absmax_f32",
+         "mvml_gemm_f16x2_bsplit", "mvml_split_f16x2"]
 
 
 def parse(argv=None):
@@ -449,6 +450,7 @@ def run(args):
         if os.environ.get("MVML_GEMM_SHAPES") and rank == 0:
             gemm_shape_report(summ.get("mvml_gemm_f32x3", []) + summ.get("mvml_gemm_f32x3_batched", [])
                               + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])
+                              + summ.get("mvml_gemm_f16x2_bsplit", [])
                               + summ.get("mvml_lstm_gates_cell_fwd", [])
                               + summ.get("mvml_gat_proj_fwd", []), args.steps)
         if rank == 0:
@@ -467,6 +469,7 @@ def run(args):
         proj_ev = summ.get("mvml_gat_proj_fwd", [])
         gemm_ev = (summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", [])
                    + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])
+                   + summ.get("mvml_gemm_f16x2_bsplit", [])
                    + summ.get("mvml_gemm_f32x3_batched", []) + summ.get("mvml_lstm_gates_cell_fwd", [])
                    + ([] if args.proj_bf16 else proj_ev))
         bf_ev = summ.get("mvml_gemm_bf16", []) + (proj_ev if args.proj_bf16 else [])
@@ -477,7 +480,7 @@ def run(args):
                 frac=round(extra["roofline_gemm_bf16"]["achieved"] / BF16_MFMA_PEAK_TFS, 4))
         if gemm_ev:
             extra["roofline_gemm"] = roofline_entry(gemm_ev, "mfma")
-            if summ.get("mvml_gemm_f16x2") or summ.get("mvml_gemm_f16x2_amax"):
+            if summ.get("mvml_gemm_f16x2") or summ.get("mvml_gemm_f16x2_amax") or summ.get("mvml_gemm_f16x2_bsplit"):
                 # scaled split-fp16: 3 fp16 MFMA per fp32 multiply-add -> fp32-equivalent peak
                 # 2.5 PF / 3 (the skinny products that fall back to split-bf16 count against it too)
                 extra["roofline_gemm"].update(

@@ -143,6 +143,21 @@ int mvml_gemm_f16x2_amax(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
                          const uint32_t* amax_a, const uint32_t* amax_b, const float* bias,
                          float beta, int act, float* C, int64_t ldc, void* workspace,
                          size_t workspace_bytes, void* stream);
+/* Split an fp32 matrix once into the two scaled fp16 planes the split-fp16 GEMM stages
+ * (hi at planes, lo at planes + rows * ld, both [rows][ld]; scale from *amax, as the GEMM's own
+ * split): a weight operand read by many tiles / products is then split once per step.
+ * cols % 4 == 0, ld % 4 == 0, P 16-B and planes 8-B aligned. */
+int mvml_split_f16x2(int64_t rows, int64_t cols, const float* P, int64_t ld, const uint32_t* amax,
+                     uint16_t* planes, void* stream);
+/* mvml_gemm_f16x2_amax with B also given as its pre-split planes (b_plane elements apart, the
+ * same [.][ldb] indexing as B, split with *amax_b): the 256x256 tiles read the planes; plans
+ * that do not use that kernel read the fp32 B. */
+int mvml_gemm_f16x2_bsplit(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                           const float* A, int64_t lda, const float* B, int64_t ldb,
+                           const uint16_t* b_planes, int64_t b_plane, const uint32_t* amax_a,
+                           const uint32_t* amax_b, const float* bias, float beta, int act,
+                           float* C, int64_t ldc, void* workspace, size_t workspace_bytes,
+                           void* stream);
 /* out[0] = bits of max |P[r*ld + c]| over r < rows, c < cols (accumulate != 0: max with the
  * current out[0]); deterministic (unsigned atomicMax of non-negative float bits). */
 int mvml_absmax_f32(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32_t* out,
@@ -189,13 +204,16 @@ int mvml_gat_unfold_grads(const float* gWcat, const float* attn_lr, int H, int F
  * of the fp32 Z tile and summed per head in fixed order — no second pass over Z.
  * attn_lr: [2, H*F] = [attn_l | attn_r]; elr: [N, 2H] = [el | er].  F % 32 == 0.
  * algo MVML_GEMM_F16X2: amax_x / amax_w = bits of max |X| / max |Wcat| (mvml_absmax_f32), or
- * both NULL (computed here).  workspace: mvml_gat_proj_fwd_workspace_size(N, H, F) bytes. */
+ * both NULL (computed here); w_planes (may be NULL, needs both maxima): Wcat split once by
+ * mvml_split_f16x2 with amax_w (w_plane elements between its planes), read instead of Wcat.
+ * workspace: mvml_gat_proj_fwd_workspace_size(N, H, F) bytes. */
 size_t mvml_gat_proj_fwd_workspace_size(int64_t num_nodes, int H, int F);
 int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx, int64_t K,
                       const float* Wcat, int64_t ldw, const float* attn_lr, int H, int F,
                       int mean_residual, int algo /* MVML_GEMM_* */, float* Y, int64_t ldy,
                       float* elr, const uint32_t* amax_x, const uint32_t* amax_w,
-                      void* workspace, size_t workspace_bytes, void* stream);
+                      const uint16_t* w_planes, int64_t w_plane, void* workspace,
+                      size_t workspace_bytes, void* stream);
 /* dL/dattn_l[h,f] = sum_n gelr[n, h] * Z[n, h*F+f] and dL/dattn_r with gelr[n, H+h] (autograd
  * of `(feat * attn_l).sum(-1)` in GATConv.forward); gelr rows [d el | d er] have stride ldgl
  * (the backward's gY + C, ldgy); deterministic two-stage reduction. */
@@ -265,6 +283,8 @@ int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float* A, int64_
                              int64_t ldh, float* act, float* h_out2, int64_t ldh2,
                              const uint32_t* amax_a, const uint32_t* amax_b /* both NULL:
                                split-bf16; else split-fp16 with these |A|, |w_perm| max bits */,
+                             const uint16_t* w_planes, int64_t w_plane /* NULL, or w_perm
+                               pre-split by mvml_split_f16x2 with amax_b */,
                              void* stream);
 int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_ih,
                        const float* b_hh, const float* c_prev, float* c_out, float* h_out,

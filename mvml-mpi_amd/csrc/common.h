@@ -102,7 +102,8 @@ __device__ __forceinline__ int64_t xcd_block(unsigned b, unsigned nb) {
 int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                   const float* B, int64_t ldb, float* C, int64_t ldc, const float* vec, int cols,
                   int logw, float* part, uint32_t* amax_ws, const uint32_t* amax_x,
-                  const uint32_t* amax_w, hipStream_t st);
+                  const uint32_t* amax_w, const uint16_t* w_planes, int64_t w_plane,
+                  hipStream_t st);
 // Partial-logit group width of mvml_gat_proj_fwd: the largest power of two <= 32 dividing F.
 inline int proj_logw(int F) {
   int lw = 0;

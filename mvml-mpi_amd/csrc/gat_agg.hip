@@ -1757,7 +1757,8 @@ extern "C" int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx,
                                  const float* Wcat, int64_t ldw, const float* attn_lr, int H,
                                  int F, int mean_residual, int algo, float* Y, int64_t ldy,
                                  float* elr, const uint32_t* amax_x, const uint32_t* amax_w,
-                                 void* workspace, size_t workspace_bytes, void* stream) {
+                                 const uint16_t* w_planes, int64_t w_plane, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
   clear_error();
   MVML_REQUIRE(H == 1 || H == 2 || H == 4 || H == 8, "gat_proj_fwd: num_heads must be 1, 2, 4 or 8 (got %d)", H);
   MVML_REQUIRE(F > 0 && F % 4 == 0, "gat_proj_fwd: out_feats must be a positive multiple of 4 (got %d)", F);
@@ -1779,7 +1780,8 @@ extern "C" int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx,
       static_cast<uint8_t*>(workspace) +
       carve_size((size_t)num_nodes * 2 * (H * F / (1 << proj_logw(F))) * sizeof(float)));
   int rc = gemm_proj_epi(algo, num_nodes, C, K, X, ldx, Wcat, ldw, Y, ldy,
-                         attn_lr, H * F, proj_logw(F), part, amax_ws, amax_x, amax_w, st);
+                         attn_lr, H * F, proj_logw(F), part, amax_ws, amax_x, amax_w, w_planes,
+                         w_plane, st);
   if (rc) return rc;
   const int W = 1 << proj_logw(F);
   const unsigned blocks = (unsigned)ceil_div(num_nodes * 2 * H, 256);

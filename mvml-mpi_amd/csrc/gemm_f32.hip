@@ -316,6 +316,7 @@ __device__ __forceinline__ float comp(const float4& v, int s) {
 struct AmaxPtrs {
   const uint32_t* a = nullptr;
   const uint32_t* b = nullptr;
+  int64_t b_plane = 0;  // BPS: elements from B's high fp16 plane to its low plane
 };
 
 struct BatchStrides {
@@ -863,6 +864,25 @@ struct XOp {
     }
   }
 
+  // pre-split operand (BPS): v[i] carries the piece's high plane bits in .x .y and its low plane
+  // bits in .z .w (loaded from the fp16 planes of mvml_split_f16x2); same LDS image as split_store
+  __device__ static __forceinline__ void store_planes(uint8_t* op, int tid, const float4 (&v)[NI]) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const uint2 p0 = make_uint2(__float_as_uint(v[i].x), __float_as_uint(v[i].y));
+      const uint2 p1 = make_uint2(__float_as_uint(v[i].z), __float_as_uint(v[i].w));
+      uint32_t off;
+      if (!KMAJ) {
+        const int row = (tid >> 2) + RS * i, q = tid & 3;
+        off = row * 32 + (((q >> 1) ^ ((row >> 3) & 1)) << 4) + 8 * (q & 1);
+      } else {
+        off = (NI * (tid >> 6) + i) * kXKmajPitch + 8 * (tid & 63);
+      }
+      *reinterpret_cast<uint2*>(op + off) = p0;
+      *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
+    }
+  }
+
   // ablation only: the planes' stores with no split arithmetic (float bits as bf16 pairs)
   __device__ static __forceinline__ void raw_store(uint8_t* op, int tid, const float4 (&v)[NI]) {
 #pragma unroll
@@ -1027,7 +1047,11 @@ __device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], floa
 // stage guarded.
 // NP = 3: fp32-accurate split-bf16 (six MFMAs per fragment pair); NP = 1: bf16 operands
 // (one MFMA per pair, fp32 accumulate) — the bf16 projection of BASELINE config 4.
-template <bool AK, bool BKM, int EPI_LOGW = -1, bool FAST = true, int NP = 3>
+// BPS (split-fp16, FAST only): B points at the two fp16 planes of a pre-split operand
+// (mvml_split_f16x2, amax.b_plane elements apart) instead of fp32 values: a B piece is loaded
+// as two 8-B plane reads and stored to LDS unsplit — the weights are split once per step
+// instead of once per tile.
+template <bool AK, bool BKM, int EPI_LOGW = -1, bool FAST = true, int NP = 3, bool BPS = false>
 __global__ void __launch_bounds__(kXThreads, MVML_X3W_WAVES)  // one workgroup per CU
 gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
@@ -1042,6 +1066,19 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   }
   using OA = XOp<AK, NP>;
   using OB = XOp<BKM, NP>;
+  static_assert(!BPS || (NP == 2 && FAST), "pre-split B: split-fp16 fast path only");
+  // B piece at float-indexed address p: fp32 values, or (BPS) the two planes' 8-B pieces
+  auto ldb4 = [&](const float* p) -> float4 {
+    if constexpr (BPS) {
+      const uint16_t* q = reinterpret_cast<const uint16_t*>(B) + (p - B);
+      const uint2 h = *reinterpret_cast<const uint2*>(q);
+      const uint2 l = *reinterpret_cast<const uint2*>(q + amax.b_plane);
+      return make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(l.x),
+                         __uint_as_float(l.y));
+    } else {
+      return *reinterpret_cast<const float4*>(p);
+    }
+  };
   // NP = 2: operand scales from the |max| bits of A and B
   int ka = 0, kb = 0;
   if constexpr (NP == 2) {
@@ -1097,7 +1134,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         va[s][i] = *reinterpret_cast<const float4*>(pa[i] + s * sa_step);
-        vb[s][i] = *reinterpret_cast<const float4*>(pb[i] + s * sb_step);
+        vb[s][i] = ldb4(pb[i] + s * sb_step);
       }
 #ifndef MVML_X3W_NOMEM  // ablation: re-read the first stage forever (cache hits, wrong results)
 #pragma unroll
@@ -1132,7 +1169,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       }
       const float4 a = *reinterpret_cast<const float4*>(qa);
       xa[i] = ka < kend ? a : make_float4(0.f, 0.f, 0.f, 0.f);
-      xb[i] = *reinterpret_cast<const float4*>(qb);
+      xb[i] = ldb4(qb);
       pa[i] += sa_step;
       pb[i] += sb_step;
     }
@@ -1162,7 +1199,10 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #ifdef MVML_ABL_NOSPLIT_B  // ablation: B's planes written without the split (wrong results)
       OB::raw_store(op + OA::kBytes, tid, vb[s]);
 #else
-      OB::split_store(op + OA::kBytes, tid, vb[s], s_b);
+      if constexpr (BPS)
+        OB::store_planes(op + OA::kBytes, tid, vb[s]);
+      else
+        OB::split_store(op + OA::kBytes, tid, vb[s], s_b);
 #endif
     }
   };
@@ -1299,7 +1339,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   using L1 = std::integral_constant<int, 1>;
   using L2 = std::integral_constant<int, 2>;
 #if MVML_X3W_PF2
-  if constexpr (FAST && KS == 1) {
+  if constexpr (FAST && KS == 1 && !BPS) {
     // Prefetch distance 2: tile k's fp32 values live in register set k % 2 from their load (in
     // body k - 3) to their split (in body k - 1), so a global load has two whole stages to land
     // instead of one (the loads of a stage are issued right after the split that frees the set).
@@ -1608,6 +1648,23 @@ __global__ void __launch_bounds__(256) absmax_kernel(int64_t rows, int64_t cols,
   }
 }
 
+// Split an fp32 operand once into its two scaled fp16 planes (hi at planes, lo at planes +
+// rows * ld; the same [rows][ld] layout): exactly split2h of the GEMM's own staging.
+__global__ void __launch_bounds__(256) split_f16x2_kernel(int64_t rows, int64_t cols4,
+                                                          const float* __restrict__ P, int64_t ld,
+                                                          const uint32_t* __restrict__ amax,
+                                                          uint16_t* __restrict__ planes) {
+  const float sc = pow2f(amax_shift(*amax));
+  const int64_t total = rows * cols4, lo = rows * ld;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t r = e / cols4, c = 4 * (e - r * cols4);
+    uint2 h, l;
+    split2h(*reinterpret_cast<const float4*>(P + r * ld + c), sc, h, l);
+    *reinterpret_cast<uint2*>(planes + r * ld + c) = h;
+    *reinterpret_cast<uint2*>(planes + lo + r * ld + c) = l;
+  }
+}
+
 int absmax_launch(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32_t* out,
                   bool accumulate, hipStream_t st) {
   if (!accumulate && hipMemsetAsync(out, 0, sizeof(uint32_t), st) != hipSuccess) {
@@ -1647,7 +1704,8 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
                 const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
                 float beta, int act, float* C, int64_t ldc, void* workspace,
                 size_t workspace_bytes, void* stream, int64_t batch = 1,
-                BatchStrides bst = BatchStrides{}, AmaxPtrs amax = AmaxPtrs{});
+                BatchStrides bst = BatchStrides{}, AmaxPtrs amax = AmaxPtrs{},
+                const uint16_t* bps = nullptr);
 }
 
 extern "C" int mvml_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
@@ -1690,6 +1748,34 @@ extern "C" int mvml_gemm_f16x2_amax(int a_kmajor, int b_kmajor, int64_t M, int64
                      AmaxPtrs{amax_a, amax_b});
 }
 
+extern "C" int mvml_split_f16x2(int64_t rows, int64_t cols, const float* P, int64_t ld,
+                                const uint32_t* amax, uint16_t* planes, void* stream) {
+  clear_error();
+  MVML_REQUIRE(rows >= 0 && cols >= 0 && cols % 4 == 0 && ld % 4 == 0 && ld >= cols && amax &&
+                   planes && ((uintptr_t)P % 16) == 0 && ((uintptr_t)planes % 8) == 0,
+               "split_f16x2: bad shape / alignment");
+  if (rows == 0 || cols == 0) return MVML_OK;
+  const int64_t total = rows * (cols / 4);
+  const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
+  split_f16x2_kernel<<<blocks, 256, 0, as_stream(stream)>>>(rows, cols / 4, P, ld, amax, planes);
+  return check_launch("split_f16x2_kernel");
+}
+
+extern "C" int mvml_gemm_f16x2_bsplit(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                                      const float* A, int64_t lda, const float* B, int64_t ldb,
+                                      const uint16_t* b_planes, int64_t b_plane,
+                                      const uint32_t* amax_a, const uint32_t* amax_b,
+                                      const float* bias, float beta, int act, float* C,
+                                      int64_t ldc, void* workspace, size_t workspace_bytes,
+                                      void* stream) {
+  clear_error();
+  MVML_REQUIRE(amax_a && amax_b && b_planes && b_plane > 0 && ((uintptr_t)b_planes % 8) == 0,
+               "gemm_f16x2_bsplit: maxima and B's planes are required");
+  AmaxPtrs am{amax_a, amax_b, b_plane};
+  return gemm_launch(kPrecF16x2, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C,
+                     ldc, workspace, workspace_bytes, stream, 1, BatchStrides{}, am, b_planes);
+}
+
 extern "C" int mvml_absmax_f32(int64_t rows, int64_t cols, const float* P, int64_t ld,
                                uint32_t* out, int accumulate, void* stream) {
   clear_error();
@@ -1715,6 +1801,7 @@ extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float
                                         const float* c_prev, float* c_out, float* h_out,
                                         int64_t ldh, float* act, float* h_out2, int64_t ldh2,
                                         const uint32_t* amax_a, const uint32_t* amax_b,
+                                        const uint16_t* w_planes, int64_t w_plane,
                                         void* stream) {
   clear_error();
   MVML_REQUIRE(M >= 0 && D > 0 && K > 0 && lda >= K && ldw >= K && ldh >= D &&
@@ -1734,7 +1821,11 @@ extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float
   cep.h_out2 = h_out2; cep.act = act; cep.ldh = ldh; cep.ldh2 = ldh2; cep.D = D;
   const dim3 grid(x3w_grid_x(tiles, 1), 1, 1);
   MVML_REQUIRE(!amax_a == !amax_b, "lstm_gates_cell_fwd: give both maxima or neither");
-  if (amax_a)
+  if (amax_a && w_planes)  // w_perm from its pre-split planes (mvml_split_f16x2 of w_perm)
+    gemm_x3w_kernel<false, false, -1, true, 2, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
+        M, N, K, A, lda, reinterpret_cast<const float*>(w_planes), ldw, nullptr, 0.f, 0, nullptr,
+        N, K, nullptr, av, bv, ProjEpi{}, BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, w_plane});
+  else if (amax_a)
     gemm_x3w_kernel<false, false, -1, true, 2><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
         BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b});
@@ -1764,7 +1855,7 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
                 const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
                 float beta, int act, float* C, int64_t ldc, void* workspace,
                 size_t workspace_bytes, void* stream, int64_t batch, BatchStrides bst,
-                AmaxPtrs amax) {
+                AmaxPtrs amax, const uint16_t* bps) {
   MVML_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
   if (M == 0 || N == 0) return MVML_OK;
   MVML_REQUIRE(ldc >= N, "gemm: ldc < N");
@@ -1801,11 +1892,12 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
     if (mvml_gemm_workspace_size(M, N1, K) <= workspace_bytes &&
         mvml_gemm_workspace_size(M, N2, K) <= workspace_bytes) {
       int rc = gemm_launch(prec, a_kmajor, b_kmajor, M, N1, K, A, lda, B, ldb, bias, beta, act, C,
-                           ldc, workspace, workspace_bytes, stream, 1, BatchStrides{}, amax);
+                           ldc, workspace, workspace_bytes, stream, 1, BatchStrides{}, amax, bps);
       if (rc) return rc;
-      return gemm_launch(prec, a_kmajor, b_kmajor, M, N2, K, A, lda, b_kmajor ? B + N1 : B + N1 * ldb,
-                         ldb, bias ? bias + N1 : nullptr, beta, act, C + N1, ldc, workspace,
-                         workspace_bytes, stream, 1, BatchStrides{}, amax);
+      const int64_t boff = b_kmajor ? N1 : N1 * ldb;
+      return gemm_launch(prec, a_kmajor, b_kmajor, M, N2, K, A, lda, B + boff, ldb,
+                         bias ? bias + N1 : nullptr, beta, act, C + N1, ldc, workspace,
+                         workspace_bytes, stream, 1, BatchStrides{}, amax, bps ? bps + boff : nullptr);
     }
   }
   if (batch > 1) plan.S = 1;  // batched products are small: no split-K slab
@@ -1826,7 +1918,11 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   dim3 grid(plan.wide || bf ? x3w_grid_x(tiles, S) : (unsigned)tiles, (unsigned)S, (unsigned)batch);
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
   do {                                                                                          \
-    if (hf && plan.wide && x3w_fast(AKV, BKV, M, N, K, av, bv))                                 \
+    if (hf && plan.wide && bps && batch == 1 && x3w_fast(AKV, BKV, M, N, K, av, bv))           \
+      gemm_x3w_kernel<AKV, BKV, -1, true, 2, true><<<grid, kXThreads, 0, st>>>(                 \
+          M, N, K, A, lda, reinterpret_cast<const float*>(bps), ldb, bias, beta, act, C, ldc, kc, \
+          slab, av, bv, ProjEpi{}, bst, CellEpi{}, amax);                                       \
+    else if (hf && plan.wide && x3w_fast(AKV, BKV, M, N, K, av, bv))                            \
       gemm_x3w_kernel<AKV, BKV, -1, true, 2><<<grid, kXThreads, 0, st>>>(                       \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst,   \
           CellEpi{}, amax);                                                                     \
@@ -1880,11 +1976,13 @@ namespace mvml {
 int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                   const float* B, int64_t ldb, float* C, int64_t ldc, const float* vec, int cols,
                   int logw, float* part, uint32_t* amax_ws, const uint32_t* amax_x,
-                  const uint32_t* amax_w, hipStream_t st) {
+                  const uint32_t* amax_w, const uint16_t* w_planes, int64_t w_plane,
+                  hipStream_t st) {
   const bool hf = prec == kPrecF16x2;
   const bool x3 = prec == kPrecX3 || hf, bf = prec == kPrecBf16;
   const bool wide = bf || (x3 && plan_gemm(kPrecX3, M, N, K).wide);
-  AmaxPtrs amx{amax_x, amax_w};
+  AmaxPtrs amx{amax_x, amax_w, w_plane};
+  const bool bps = hf && w_planes && amax_x && amax_w;  // B = Wcat from its pre-split planes
   if (hf && wide && !(amax_x && amax_w)) {  // maxima not supplied: one pass per operand
     MVML_REQUIRE(amax_ws != nullptr, "gat_proj_fwd: split-fp16 needs the maxima workspace");
     int rc = absmax_launch(M, K, A, lda, amax_ws, false, st);
@@ -1900,7 +1998,12 @@ int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int
   dim3 grid(wide ? x3w_grid_x(tiles, 1) : (unsigned)tiles, 1);
 #define MVML_PROJ(LW)                                                                          \
   do {                                                                                         \
-    if (hf && wide && x3w_fast(false, false, M, N, K, av, bv))                                 \
+    if (bps && wide && x3w_fast(false, false, M, N, K, av, bv))                                \
+      gemm_x3w_kernel<false, false, LW, true, 2, true><<<grid, kXThreads, 0, st>>>(            \
+          M, N, K, A, lda, reinterpret_cast<const float*>(w_planes), ldb, nullptr, 0.f, 0, C,  \
+          ldc, K > 0 ? K : 1, nullptr, av, bv, ProjEpi{vec, cols, part}, BatchStrides{},       \
+          CellEpi{}, amx);                                                                     \
+    else if (hf && wide && x3w_fast(false, false, M, N, K, av, bv))                            \
       gemm_x3w_kernel<false, false, LW, true, 2><<<grid, kXThreads, 0, st>>>(                  \
           M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
           ProjEpi{vec, cols, part}, BatchStrides{}, CellEpi{}, amx);                       \

@@ -88,8 +88,26 @@ def slot(t, i):
     return None if t is None else ctypes.c_void_p(t.data_ptr() + 4 * i)
 
 
+# MVML_BSPLIT=1: weights split once per step into fp16 planes that the split-fp16 GEMMs read
+# as B (mvml_split_f16x2 / mvml_gemm_f16x2_bsplit).  Off by default: A/B on one box, config-3
+# step 165.0 ms without vs 167.9 ms with — two 8-B plane loads per piece cost more than the
+# split VALU they save (the no-split ablation bound was ~5 % per GEMM); correct either way.
+BSPLIT = os.environ.get("MVML_BSPLIT", "0") == "1"
+
+
+def split_planes(W, rows, cols, ld, amax_ptr):
+    """W (fp32, [rows][ld]) split once into its two scaled fp16 planes (mvml_split_f16x2) for
+    the split-fp16 GEMMs that read it as B: (planes, elements between the planes); (None, 0)
+    with MVML_BSPLIT=0."""
+    if not BSPLIT:
+        return None, 0
+    planes = torch.empty(2 * rows * ld, dtype=torch.int16, device=W.device)
+    call("mvml_split_f16x2", rows, cols, ptr(W), ld, amax_ptr, ptr(planes), _stream(W.device))
+    return planes, rows * ld
+
+
 def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0, algo=None,
-         amax=None):
+         amax=None, bsplit=None):
     """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32 / mvml_gemm_f32x3 /
     mvml_gemm_f16x2).  amax = (pointer to |A| max bits, pointer to |B| max bits) from absmax()
     lets split-fp16 products that share an operand share its max pass."""
@@ -99,6 +117,11 @@ def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.
     wsz = L.mvml_gemm_workspace_size(M, N, K)
     wp, wn = _lib.ws_ptr_size(wsz, dev)
     algo = algo or GEMM_ALGO
+    if algo == "f16x2" and amax is not None and bsplit is not None:  # B from its pre-split planes
+        call("mvml_gemm_f16x2_bsplit", int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda, ptr(B), ldb,
+             ptr(bsplit[0]), bsplit[1], amax[0], amax[1], ptr(bias), float(beta), int(act), ptr(C), ldc,
+             wp, wn, _stream(dev))
+        return
     if algo == "f16x2" and amax is not None:
         call("mvml_gemm_f16x2_amax", int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda, ptr(B), ldb,
              amax[0], amax[1], ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
@@ -163,6 +186,7 @@ class GATLayerFunction(torch.autograd.Function):
         # pass serves all of its products (projection, dL/dW, dL/dX)
         amx = None
         ax = None  # (tensor, slot) of max |X|
+        wps = (None, 0)
         if (algo or GEMM_ALGO) == "f16x2":
             amx = torch.zeros(4, dtype=torch.int32, device=dev)  # [X, Wcat, gY (bwd), out]
             ax = known_amax(Xp) if Xp is X else None  # layer 2: folded by layer 1's aggregation
@@ -170,11 +194,13 @@ class GATLayerFunction(torch.autograd.Function):
                 absmax(Xp, N, Fp, Fp, amx, 0)
                 ax = (amx, 0)
             absmax(Wcat, C + 2 * H, Fp, Fp, amx, 1)
+            # Wcat split once: the projection's tiles and the backward's dL/dX read the planes
+            wps = split_planes(Wcat, C + 2 * H, Fp, Fp, slot(amx, 1))
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_proj_fwd_workspace_size(N, H, F), dev)
         _lib.call_tag[0] = {"flops": 2 * N * C * Fp}
         call("mvml_gat_proj_fwd", N, ptr(Xp), Fp, Fp, ptr(Wcat), Fp, ptr(attn_lr), H, F, mean_res,
              _GEMM_ENTRY[algo or GEMM_ALGO][1], ptr(Y), ldy, ptr(elr),
-             None if ax is None else slot(*ax), slot(amx, 1), wp, wn, st)
+             None if ax is None else slot(*ax), slot(amx, 1), ptr(wps[0]), wps[1], wp, wn, st)
         out_cols = F if mode == MODE_MEAN else HF
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()
@@ -193,6 +219,7 @@ class GATLayerFunction(torch.autograd.Function):
         ctx.algo = algo
         ctx.amx = amx
         ctx.ax = ax
+        ctx.wps = wps
         ctx.ones_col = ones_col
         return out
 
@@ -257,7 +284,8 @@ class GATLayerFunction(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gX = torch.empty((N, Fin), dtype=torch.float32, device=dev)
             gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, algo=ctx.algo,
-                 amax=None if amx is None else (slot(amx, 2), slot(amx, 1)))
+                 amax=None if amx is None else (slot(amx, 2), slot(amx, 1)),
+                 bsplit=None if ctx.wps[0] is None else ctx.wps)
         return gX, g_fc, g_res, g_al, g_ar, g_bias, None, None, None, None, None, None
 
 
@@ -301,6 +329,7 @@ class Set2SetFunction(torch.autograd.Function):
         lse = torch.empty((T, B), **f32)
         gates = torch.empty((B, 4 * D), **f32)
         amax_x = amax_w = None
+        wsp = [(None, 0)] * Lr
         if GEMM_ALGO == "f16x2":
             # split-fp16 operand maxima of the cells' GEMMs: every A row [x | h_prev] holds
             # LSTM outputs h = o tanh(c) (|h| < 1) and, in layer 0, the readout r = sum_n a_n x_n
@@ -315,6 +344,10 @@ class Set2SetFunction(torch.autograd.Function):
             amax_w = torch.empty(Lr, dtype=torch.int32, device=dev)
             for l in range(Lr):
                 absmax(Wcat[l], 4 * D, kin[l] + D, kin[l] + D, amax_w, l)  # = Wperm's max
+            # the gates' weights split once per forward (the fused path reads Wperm's planes, the
+            # unfused one Wcat's: the same values per element, so the same products)
+            wsp = [split_planes(Wperm[l] if CELL_EPI else Wcat[l], 4 * D, kin[l] + D, kin[l] + D,
+                                slot(amax_w, l)) for l in range(Lr)]
         for t in range(T):
             for l in range(Lr):
                 w_ih, w_hh, b_ih, b_hh = W[l]
@@ -330,13 +363,15 @@ class Set2SetFunction(torch.autograd.Function):
                     _lib.call_tag[0] = {"flops": 2 * B * 4 * D * K, "shape": (B, 4 * D, K, 0, 0, "cell")}
                     call("mvml_lstm_gates_cell_fwd", B, D, K, ptr(XH[l][t]), kin[l] + D, ptr(Wperm[l]),
                          kin[l] + D, ptr(b_ih), ptr(b_hh), ptr(c_prev), ptr(cs[t, l]), ptr(own),
-                         kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, pa, pw, st)
+                         kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, pa, pw, ptr(wsp[l][0]),
+                         wsp[l][1], st)
                     continue
                 if t == 0 and l == 0:
                     gates.zero_()  # q*_{-1} = 0 and h_0(-1) = 0
                 else:
                     gemm(XH[l][t], Wcat[l], B, 4 * D, K, 0, 0, kin[l] + D, kin[l] + D, gates, 4 * D,
-                         amax=None if amax_x is None else (slot(amax_x, 0), slot(amax_w, l)))
+                         amax=None if amax_x is None else (slot(amax_x, 0), slot(amax_w, l)),
+                         bsplit=None if CELL_EPI or wsp[l][0] is None else wsp[l])
                 call("mvml_lstm_cell_fwd", B, D, ptr(gates), ptr(b_ih), ptr(b_hh), ptr(c_prev),
                      ptr(cs[t, l]), ptr(own), kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, st)
             call("mvml_set2set_seg_fwd", B, D, ptr(g.node_offsets), ptr(X), ptr(XH[0][t + 1]), 3 * D,
@@ -384,6 +419,10 @@ class Set2SetFunction(torch.autograd.Function):
         # running value bounds every cell seen so far, which is all a scale needs)
         amax_x, amax_w = ctx.amax
         amax_g = torch.zeros(Lr, dtype=torch.int32, device=dev) if amax_x is not None else None
+        wsb = [None] * Lr  # [W_ih | W_hh] split once for the per-cell data-gradient products
+        if amax_g is not None and BSPLIT:
+            wsb = [split_planes(Wcat[l], 4 * D, Wcat[l].shape[1], Wcat[l].shape[1], slot(amax_w, l))
+                   for l in range(Lr)]
         for t in range(T - 1, -1, -1):
             # readout segment backward: dL/dq_t = g_qstar_t[:, :D] + segment term -> g_h
             call("mvml_set2set_seg_bwd", B, D, ptr(g.node_offsets), ptr(X), ptr(qs[t]), 3 * D,
@@ -407,7 +446,8 @@ class Set2SetFunction(torch.autograd.Function):
                 if ncols:
                     out, ldo = (g_qs3[t - 1], 3 * D) if l == 0 else (gxh[l], 2 * D)
                     gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo,
-                         amax=None if amax_g is None else (slot(amax_g, l), slot(amax_w, l)))
+                         amax=None if amax_g is None else (slot(amax_g, l), slot(amax_w, l)),
+                         bsplit=wsb[l])
         # weight / bias gradients, one product per parameter over all steps:
         #   dW_ih[l] = sum_t g_gates[l,t]^T x_l(t),  dW_hh[l] = sum_{t>=1} g_gates[l,t]^T h_l(t-1)
         # (layer 0's input x_0(t) = q*_{t-1} is zero at t = 0; h_l(-1) = 0)

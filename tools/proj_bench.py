@@ -42,7 +42,7 @@ def main():
         for algo in ("f32", "x3", "f16x2"):
             t0 = timeit(lambda: gemm(X, W, N, C, K, 0, 0, K, K, Y, ldy, algo=algo))
             t1 = timeit(lambda: call("mvml_gat_proj_fwd", N, ptr(X), K, K, ptr(W), K, ptr(attn), H, F,
-                                     mean, _GEMM_ENTRY[algo][1], ptr(Y), ldy, ptr(elr), None, None,
+                                     mean, _GEMM_ENTRY[algo][1], ptr(Y), ldy, ptr(elr), None, None, None, 0,
                                      ptr(ws), wsz, st))
             print(f"H{H} F{F} K{K} {algo}: gemm {t0:8.3f} ms ({fl / t0 / 1e9:6.1f} TF/s)   proj_fwd "
                   f"{t1:8.3f} ms ({fl / t1 / 1e9:6.1f} TF/s)")
