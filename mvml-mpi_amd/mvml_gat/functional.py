@@ -88,6 +88,10 @@ def slot(t, i):
     return None if t is None else ctypes.c_void_p(t.data_ptr() + 4 * i)
 
 
+# split-fp16 projection: el / er as 2H extra GEMM columns against Wcat's A_l / A_r rows (True)
+# or mvml_gat_proj_fwd's logit-partial epilogue over the Z tile (False)
+PROJ_ELR_GEMM = os.environ.get("MVML_PROJ_ELR_GEMM", "1") != "0"
+
 # MVML_BSPLIT=1: weights split once per step into fp16 planes that the split-fp16 GEMMs read
 # as B (mvml_split_f16x2 / mvml_gemm_f16x2_bsplit).  Off by default: A/B on one box, config-3
 # step 165.0 ms without vs 167.9 ms with — two 8-B plane loads per piece cost more than the
@@ -196,11 +200,21 @@ class GATLayerFunction(torch.autograd.Function):
             absmax(Wcat, C + 2 * H, Fp, Fp, amx, 1)
             # Wcat split once: the projection's tiles and the backward's dL/dX read the planes
             wps = split_planes(Wcat, C + 2 * H, Fp, Fp, slot(amx, 1))
-        wp, wn = _lib.ws_ptr_size(L.mvml_gat_proj_fwd_workspace_size(N, H, F), dev)
-        _lib.call_tag[0] = {"flops": 2 * N * C * Fp}
-        call("mvml_gat_proj_fwd", N, ptr(Xp), Fp, Fp, ptr(Wcat), Fp, ptr(attn_lr), H, F, mean_res,
-             _GEMM_ENTRY[algo or GEMM_ALGO][1], ptr(Y), ldy, ptr(elr),
-             None if ax is None else slot(*ax), slot(amx, 1), ptr(wps[0]), wps[1], wp, wn, st)
+        if amx is not None and PROJ_ELR_GEMM:
+            # el / er as 2H more GEMM columns: X [A_l ; A_r]^T with A_l[h] = sum_f attn_l[h, f]
+            # fc.weight[h F + f] (Wcat's last 2H rows) — the same values re-associated, no
+            # logit-partial epilogue and no finalize pass; then gathered into elr [N, 2H]
+            ldy = _round4(C + 2 * H)
+            Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
+            gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(slot(*ax), slot(amx, 1)),
+                 bsplit=None if wps[0] is None else wps)
+            elr = Y[:, C:C + 2 * H].contiguous()
+        else:
+            wp, wn = _lib.ws_ptr_size(L.mvml_gat_proj_fwd_workspace_size(N, H, F), dev)
+            _lib.call_tag[0] = {"flops": 2 * N * C * Fp}
+            call("mvml_gat_proj_fwd", N, ptr(Xp), Fp, Fp, ptr(Wcat), Fp, ptr(attn_lr), H, F, mean_res,
+                 _GEMM_ENTRY[algo or GEMM_ALGO][1], ptr(Y), ldy, ptr(elr),
+                 None if ax is None else slot(*ax), slot(amx, 1), ptr(wps[0]), wps[1], wp, wn, st)
         out_cols = F if mode == MODE_MEAN else HF
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()
