@@ -40,6 +40,16 @@ def _round4(x):
     return (x + 3) // 4 * 4
 
 
+# Row pitch of the N-row projection / gradient matrices: a multiple of 64 floats, so every row
+# starts on a 256-B boundary and the aggregation kernels' 64-column chunks (256-B row segments)
+# never straddle an extra cache line (MVML_ROW_PITCH64=0: multiples of 4 floats only)
+_PITCH64 = os.environ.get("MVML_ROW_PITCH64", "1") != "0"
+
+
+def _row_pitch(cols):
+    return (cols + 63) // 64 * 64 if _PITCH64 else _round4(cols)
+
+
 def agg_fwd_bytes(N, E, H, F, out_cols, res_cols):
     """Algorithmic HBM bytes of one mvml_gat_agg_fwd: read Z and R once,
     rowptr, src ids, el/er; write the layer output and the saved attention.  R is the
@@ -166,7 +176,7 @@ class GATLayerFunction(torch.autograd.Function):
         HF = H * F
         mean_res = int(mode == MODE_MEAN)
         C = _lib.lib().mvml_gat_proj_cols(H, F, mean_res)
-        ldy = _round4(C)
+        ldy = _row_pitch(C)
         st = _stream(dev)
         # Pad the feature dimension to a multiple of 4 (e.g. 74 atom features -> 76) so every
         # GEMM operand row is 16-B aligned and the LDS-DMA path applies; pad columns are zero.
@@ -204,7 +214,7 @@ class GATLayerFunction(torch.autograd.Function):
             # el / er as 2H more GEMM columns: X [A_l ; A_r]^T with A_l[h] = sum_f attn_l[h, f]
             # fc.weight[h F + f] (Wcat's last 2H rows) — the same values re-associated, no
             # logit-partial epilogue and no finalize pass; then gathered into elr [N, 2H]
-            ldy = _round4(C + 2 * H)
+            ldy = _row_pitch(C + 2 * H)
             Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
             gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(slot(*ax), slot(amx, 1)),
                  bsplit=None if wps[0] is None else wps)
@@ -250,7 +260,7 @@ class GATLayerFunction(torch.autograd.Function):
         L = _lib.lib()
         C = L.mvml_gat_proj_cols(H, F, mean_res)
         CE = C + 2 * H  # + [d el | d er]
-        ldg = _round4(CE)
+        ldg = _row_pitch(CE)
         st = _stream(dev)
         gY = torch.empty((N, ldg), dtype=torch.float32, device=dev)
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_agg_bwd_workspace_size(g.num_edges(), H), dev)
@@ -523,6 +533,21 @@ class GraphNormFunction(torch.autograd.Function):
         return gx, gw, gb, gms, None, None
 
 
+def linear_maxima(x, w):
+    """Split-fp16 maxima of a Linear's three products: slots [x, w, grad] (x's from its
+    producer when it folded one), one pass per operand instead of one per product; None for
+    the other algorithms."""
+    if GEMM_ALGO != "f16x2":
+        return None
+    amx = torch.zeros(3, dtype=torch.int32, device=x.device)
+    kx = known_amax(x)
+    if kx is None:
+        absmax(x, x.shape[0], x.shape[1], x.shape[1], amx, 0)
+        kx = (amx, 0)
+    absmax(w, w.shape[0], w.shape[1], w.shape[1], amx, 1)
+    return amx, kx
+
+
 class LinearReLUFunction(torch.autograd.Function):
     """nn.Linear + nn.ReLU of GNNModule.fc (model.py:86-87) as one MFMA GEMM with a bias+ReLU
     epilogue."""
@@ -534,7 +559,10 @@ class LinearReLUFunction(torch.autograd.Function):
         M, K = x.shape
         Nout = weight.shape[0]
         y = torch.empty((M, Nout), dtype=torch.float32, device=x.device)
-        gemm(x, _c(weight), M, Nout, K, 0, 0, K, K, y, Nout, bias=_c(bias), act=1)
+        weight = _c(weight)
+        lm = ctx.lm = linear_maxima(x, weight)
+        gemm(x, weight, M, Nout, K, 0, 0, K, K, y, Nout, bias=_c(bias), act=1,
+             amax=None if lm is None else (slot(*lm[1]), slot(lm[0], 1)))
         ctx.save_for_backward(x, weight, y)
         return y
 
@@ -547,12 +575,17 @@ class LinearReLUFunction(torch.autograd.Function):
         dev = x.device
         g_pre = torch.empty_like(y)
         call("mvml_relu_bwd", y.numel(), ptr(y), ptr(g_y), ptr(g_pre), _stream(dev))
+        lm = ctx.lm
+        if lm is not None:
+            absmax(g_pre, M, Nout, Nout, lm[0], 2)
         gw = torch.empty_like(weight)
-        gemm(g_pre, x, Nout, K, M, 1, 1, Nout, K, gw, K)
+        gemm(g_pre, x, Nout, K, M, 1, 1, Nout, K, gw, K,
+             amax=None if lm is None else (slot(lm[0], 2), slot(*lm[1])))
         gb = torch.empty((Nout,), dtype=torch.float32, device=dev)
         colsum(g_pre, M, Nout, Nout, gb)
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
-            gemm(g_pre, _c(weight), M, K, Nout, 0, 1, Nout, K, gx, K)
+            gemm(g_pre, weight, M, K, Nout, 0, 1, Nout, K, gx, K,
+                 amax=None if lm is None else (slot(lm[0], 2), slot(lm[0], 1)))
         return gx, gw, gb

@@ -31,7 +31,10 @@ class LinearFunction(torch.autograd.Function):
         M, K = x.shape
         Nout = weight.shape[0]
         y = torch.empty((M, Nout), dtype=torch.float32, device=x.device)
-        gemm(x, _c(weight), M, Nout, K, 0, 0, K, K, y, Nout, bias=_c(bias))
+        weight = _c(weight)
+        lm = ctx.lm = _F.linear_maxima(x, weight)
+        gemm(x, weight, M, Nout, K, 0, 0, K, K, y, Nout, bias=_c(bias),
+             amax=None if lm is None else (slot(*lm[1]), slot(lm[0], 1)))
         ctx.save_for_backward(x, weight)
         return y
 
@@ -41,14 +44,19 @@ class LinearFunction(torch.autograd.Function):
         g_y = _c(g_y)
         M, K = x.shape
         Nout = weight.shape[0]
+        lm = ctx.lm
+        if lm is not None:
+            absmax(g_y, M, Nout, Nout, lm[0], 2)
         gw = torch.empty_like(weight)
-        gemm(g_y, x, Nout, K, M, 1, 1, Nout, K, gw, K)
+        gemm(g_y, x, Nout, K, M, 1, 1, Nout, K, gw, K,
+             amax=None if lm is None else (slot(lm[0], 2), slot(*lm[1])))
         gb = torch.empty((Nout,), dtype=torch.float32, device=x.device)
         colsum(g_y, M, Nout, Nout, gb)
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
-            gemm(g_y, _c(weight), M, K, Nout, 0, 1, Nout, K, gx, K)
+            gemm(g_y, weight, M, K, Nout, 0, 1, Nout, K, gx, K,
+                 amax=None if lm is None else (slot(lm[0], 2), slot(lm[0], 1)))
         return gx, gw, gb
 
 
