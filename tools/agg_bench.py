@@ -43,7 +43,7 @@ def main():
     layers = ((4, 192, 0, "L1 flatten+ELU"), (4, 384, 1, "L2 mean"))
     for (H, F, mode, name) in [layers[int(i)] for i in a.layers]:
         C = L.mvml_gat_proj_cols(H, F, int(mode == 1))
-        ldy = (C + 3) // 4 * 4
+        ldy = (C + 63) // 64 * 64  # the product's 256-B row pitch
         Y = torch.randn((N, ldy), device="cuda") * 0.3
         bias = torch.randn(H * F, device="cuda") * 0.1
         al = torch.randn(H * F, device="cuda") * 0.1
@@ -67,7 +67,7 @@ def main():
         if a.no_bwd:
             continue
         g_out = torch.randn_like(out)
-        ldg = (C + 2 * H + 3) // 4 * 4
+        ldg = (C + 2 * H + 63) // 64 * 64
         gY = torch.empty((N, ldg), device="cuda")
         wsz = L.mvml_gat_agg_bwd_workspace_size(E, H)
         ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
