@@ -116,14 +116,35 @@ def gemm_shape_report(ev, steps):
             f"{fl / (tot * 1e-3) / 1e12:7.1f} TF/s")
 
 
-def roofline_entry(ev, kind):
+def full_batch_bytes(ev):
+    """Algorithmic bytes per launch on a FULL step batch: per layer tag the largest launch (the
+    set's short last batch, if timed, is smaller), averaged over the layers — the batch the PMC
+    traffic in profiles/pmc_traffic.json was collected on."""
+    by = {}
+    for _, t in ev:
+        by[t.get("layer")] = max(by.get(t.get("layer"), 0), t["bytes"])
+    return sum(by.values()) / len(by)
+
+
+def roofline_entry(ev, kind, traffic_full=None):
+    """traffic_full: PMC HBM bytes per launch on a full step batch (or None).  The line reports
+    the traffic SCALED to the timed launches' batch mix (traffic_full x bytes_per_launch /
+    full-batch bytes), so traffic / bytes_per_launch compares like with like; the full-batch
+    pair is reported beside it."""
     tot_ms = sum(ms for ms, _ in ev)
     if kind == "hbm":
         byts = sum(t["bytes"] for _, t in ev)
         ach = byts / (tot_ms * 1e-3) / 1e9
-        return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_ms": round(tot_ms / len(ev), 4),
-                "bytes_per_launch": int(byts / len(ev))}
+        avg = byts / len(ev)
+        full = full_batch_bytes(ev)
+        r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_ms": round(tot_ms / len(ev), 4),
+             "bytes_per_launch": int(avg), "traffic": None}
+        if traffic_full:
+            r.update(traffic=int(traffic_full * avg / full), full_batch_bytes_per_launch=int(full),
+                     full_batch_traffic_per_launch=int(traffic_full),
+                     traffic_over_algorithmic=round(traffic_full / full, 4))
+        return r
     flops = sum(t["flops"] for _, t in ev)
     ach = flops / (tot_ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
@@ -375,8 +396,9 @@ def run(args):
         full = MVP(11, 74, [192, 384], 6, 3, 128, 384, 2, 512, 12, 0.5,
                    proj_dtype=torch.bfloat16 if args.proj_bf16 else None).to(dev).train()
         model, fusion = full.gnn, None
-        params = [p for n, p in full.named_parameters()
-                  if not (n.startswith("norm_layer.") or n.startswith("rnn.norm_layer."))]
+        # every parameter, as main.py:88 passes model.parameters(): the never-used LayerNorms
+        # (model.py:42, 120) keep grad None through the reducer, so Adam skips them
+        params = list(full.parameters())
     else:
         model = mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3,
                                    proj_dtype=torch.bfloat16 if args.proj_bf16 else None).to(dev).train()
@@ -459,13 +481,12 @@ def run(args):
                 log(f"  {name:26s} {r['calls']:6.1f}/step avg {r['avg_ms']:8.3f} ms "
                     f"{r['ms_per_step']:8.2f} ms/step ({100 * r['share']:5.1f}%) {perf}")
         if summ.get("mvml_gat_agg_fwd"):
-            roofline = roofline_entry(summ["mvml_gat_agg_fwd"], "hbm")
+            roofline = roofline_entry(summ["mvml_gat_agg_fwd"], "hbm", load_traffic(wkey, "gat_agg_fwd"))
             roofline["kernel"] = "mvml_gat_agg_fwd (both GAT layers; fused edge-softmax + u_mul_e-sum)"
-            roofline["traffic"] = load_traffic(wkey, "gat_agg_fwd")
             roofline["traffic_profile"] = wkey if roofline["traffic"] else None
         if summ.get("mvml_gat_agg_bwd"):
-            extra["roofline_agg_bwd"] = roofline_entry(summ["mvml_gat_agg_bwd"], "hbm")
-            extra["roofline_agg_bwd"]["traffic"] = load_traffic(wkey, "gat_agg_bwd")
+            extra["roofline_agg_bwd"] = roofline_entry(summ["mvml_gat_agg_bwd"], "hbm",
+                                                       load_traffic(wkey, "gat_agg_bwd"))
         proj_ev = summ.get("mvml_gat_proj_fwd", [])
         gemm_ev = (summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", [])
                    + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])

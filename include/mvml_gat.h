@@ -42,6 +42,23 @@ const char* mvml_last_error(void);
 /* Library version string, and the gfx target the kernels were built for. */
 const char* mvml_version(void);
 
+/* Kernel-path options, for tests and tools (the defaults are the production paths; every path
+ * computes the same function and is parity-tested).  Each starts from the environment variable
+ * named below, read ONCE when the library loads, and changes at run time only through
+ * mvml_set_option, which returns the previous value (-1: unknown option, nothing changed).
+ * Process-wide; set them between launches, not while another thread enqueues work. */
+#define MVML_OPT_BIG_WINDOW 0   /* MVML_BIG_WINDOW: 1 (default) big-window aggregation kernels for
+                                   groups past the molecule window, 0 = per-atom fallbacks */
+#define MVML_OPT_BWD_ATOMWISE 1 /* MVML_BWD_ATOMWISE: 1 = aggregation backward by the per-atom
+                                   dst / src kernel pair for every group (default 0) */
+#define MVML_OPT_GEMM_TILE 2    /* MVML_X3_TILE: 0 (default) planned tile, 128 / 256 = forced */
+#define MVML_OPT_GEMM_PERSIST 3 /* MVML_X3W_PERSIST: P > 0 caps a 256x256 launch at P
+                                   workgroups looping over tiles (default 0: one per tile) */
+#define MVML_OPT_GEMM_NSPLIT 4  /* MVML_GEMM_NSPLIT: 1 (default) N = 256 q + r products as two
+                                   launches, 0 = one */
+int mvml_set_option(int option, int value);
+int mvml_get_option(int option);
+
 /* ---------------------------------------------------------------------------------------
  * Batching: dgl.batch (dataset.py:54) + DGL's COO->CSR conversion on first update_all.
  * Inputs are the per-graph LOCAL edge lists of mol_to_bigraph (dataset.py:34-35) concatenated

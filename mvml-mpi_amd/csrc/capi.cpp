@@ -1,6 +1,9 @@
 // Error reporting and version entry points of the mvml_gat C ABI.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+
+#include <atomic>
 
 #include "common.h"
 
@@ -26,7 +29,35 @@ int check_launch(const char* what) {
   return MVML_OK;
 }
 
+// Kernel-path options (include/mvml_gat.h, MVML_OPT_*): environment defaults read once at load.
+constexpr int kOptCount = 5;
+static std::atomic<int> g_opt[kOptCount];
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+static const bool g_opt_init = [] {
+  g_opt[MVML_OPT_BIG_WINDOW] = env_int("MVML_BIG_WINDOW", 1);
+  g_opt[MVML_OPT_BWD_ATOMWISE] = env_int("MVML_BWD_ATOMWISE", 0);
+  g_opt[MVML_OPT_GEMM_TILE] = env_int("MVML_X3_TILE", 0);
+  g_opt[MVML_OPT_GEMM_PERSIST] = env_int("MVML_X3W_PERSIST", 0);
+  g_opt[MVML_OPT_GEMM_NSPLIT] = env_int("MVML_GEMM_NSPLIT", 1);
+  return true;
+}();
+
+int option(int i) { return g_opt[i].load(std::memory_order_relaxed); }
+
 }  // namespace mvml
+
+extern "C" int mvml_set_option(int opt, int value) {
+  if (opt < 0 || opt >= mvml::kOptCount) return -1;
+  return mvml::g_opt[opt].exchange(value, std::memory_order_relaxed);
+}
+
+extern "C" int mvml_get_option(int opt) {
+  if (opt < 0 || opt >= mvml::kOptCount) return -1;
+  return mvml::option(opt);
+}
 
 extern "C" const char* mvml_last_error(void) { return mvml::g_err; }
 

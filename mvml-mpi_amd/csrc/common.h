@@ -43,6 +43,8 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 // Check the launch we just enqueued; never synchronises.
 int check_launch(const char* what);
+// Current value of a kernel-path option (MVML_OPT_*, capi.cpp).
+int option(int which);
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

@@ -349,10 +349,10 @@ __device__ __forceinline__ int hub_segments(int nr, int eb, int deg, uint32_t* s
 // The big-window kernels stage 16-column chunks (F % 16 == 0) and their LDS holds the per-edge
 // attention of up to kPlanBigEdgeCap edges for H <= 4 heads.  On config 5 (8192 molecules) they
 // take fwd / bwd L1 6.4 / 13.5 ms and L2 7.0 / 21.7 ms against the per-atom fallbacks' 7.0 /
-// 15.9 and 10.2 / 29.7 ms.  MVML_BIG_WINDOW=0 routes those groups to the fallbacks (tests).
+// 15.9 and 10.2 / 29.7 ms.  Option MVML_OPT_BIG_WINDOW = 0 routes those groups to the
+// fallbacks (tests).
 inline bool use_big_window(int H, int F) {
-  const char* e = getenv("MVML_BIG_WINDOW");
-  return !(e && atoi(e) == 0) && H <= 4 && F % 16 == 0;
+  return option(MVML_OPT_BIG_WINDOW) != 0 && H <= 4 && F % 16 == 0;
 }
 
 #ifndef MVML_LDS_WAVES
@@ -1551,7 +1551,7 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
                int64_t ldy, const float* elr, const float* attn, const float* out,
                const float* g_out, int F, float slope, int mode, float* gpre, float* gY,
                int64_t ldgy, int C, uint32_t* gy_amax, hipStream_t st) {
-  if (getenv("MVML_BWD_ATOMWISE")) G = 0;  // experiment: per-atom pair over every atom
+  if (option(MVML_OPT_BWD_ATOMWISE)) G = 0;  // tests: the per-atom pair over every atom
   if (F % 32 == 0 && G > 0) {  // molecule groups: one pass over Z / g_out / dZ per group
 #ifndef MVML_BWD_CW64
 #define MVML_BWD_CW64 1

@@ -883,25 +883,6 @@ struct XOp {
     }
   }
 
-  // ablation only: the planes' stores with no split arithmetic (float bits as bf16 pairs)
-  __device__ static __forceinline__ void raw_store(uint8_t* op, int tid, const float4 (&v)[NI]) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const uint2 p0 = make_uint2(__float_as_uint(v[i].x), __float_as_uint(v[i].y));
-      const uint2 p1 = make_uint2(__float_as_uint(v[i].z), __float_as_uint(v[i].w));
-      uint32_t off;
-      if (!KMAJ) {
-        const int row = (tid >> 2) + RS * i, q = tid & 3;
-        off = row * 32 + (((q >> 1) ^ ((row >> 3) & 1)) << 4) + 8 * (q & 1);
-      } else {
-        off = (NI * (tid >> 6) + i) * kXKmajPitch + 8 * (tid & 63);
-      }
-      *reinterpret_cast<uint2*>(op + off) = p0;
-      if constexpr (NP >= 2) *reinterpret_cast<uint2*>(op + kPlane + off) = p1;
-      if constexpr (NP == 3) *reinterpret_cast<uint2*>(op + 2 * kPlane + off) = p0;
-    }
-  }
-
   // 32x32x16 operand fragment of tile rows R0 .. R0+31, plane p: lane l holds row R0 + (l & 31),
   // k = 8 (l >> 5) + [0, 8).
   __device__ static __forceinline__ bf16x8 frag(const uint8_t* op, int p, int R0, int lane) {
@@ -1136,13 +1117,11 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
         va[s][i] = *reinterpret_cast<const float4*>(pa[i] + s * sa_step);
         vb[s][i] = ldb4(pb[i] + s * sb_step);
       }
-#ifndef MVML_X3W_NOMEM  // ablation: re-read the first stage forever (cache hits, wrong results)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       pa[i] += KS * sa_step;
       pb[i] += KS * sb_step;
     }
-#endif
   };
   // fast load of a stage that may be the K tail: addresses clamped to k < kend (host: kend %
   // 4 == 0), A's values at k >= kend zeroed, so B's clamped (finite) values add nothing
@@ -1191,19 +1170,11 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       uint8_t* op = lds + buf * kStage + s * kSub;
-#ifdef MVML_ABL_NOSPLIT_A  // ablation: A's planes written without the split (wrong results)
-      OA::raw_store(op, tid, va[s]);
-#else
       OA::split_store(op, tid, va[s], s_a);
-#endif
-#ifdef MVML_ABL_NOSPLIT_B  // ablation: B's planes written without the split (wrong results)
-      OB::raw_store(op + OA::kBytes, tid, vb[s]);
-#else
       if constexpr (BPS)
         OB::store_planes(op + OA::kBytes, tid, vb[s]);
       else
         OB::split_store(op + OA::kBytes, tid, vb[s], s_b);
-#endif
     }
   };
 #ifndef MVML_X3W_PRIO
@@ -1448,20 +1419,6 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       }
     }
   }
-#ifdef MVML_X3W_NOEPI
-  if (M < 0) {  // ablation: keep the accumulators live, store nothing
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[i][j]));
-  continue;
-#endif
   if constexpr (NP == 2) {  // undo the operand scales (exact: powers of two)
     const float ua = pow2f(-ka), ub = pow2f(-kb);
 #pragma unroll
@@ -1530,16 +1487,15 @@ int choose_splits_t(int64_t tiles, int64_t K, int64_t slots) {
 }
 
 // Kernel plan of a product: the 256x256 split-bf16 kernel (one workgroup per CU) whenever its
-// tiles x splits fill the chip, the 128x128 kernels (two per CU) otherwise.  MVML_X3_TILE=128 /
-// 256 forces a tile size (tests).
+// tiles x splits fill the chip, the 128x128 kernels (two per CU) otherwise.  Option
+// MVML_OPT_GEMM_TILE = 128 / 256 forces a tile size (tests).
 struct GemmPlan {
   bool wide;
   int S;
 };
 constexpr int kPrecF32 = 0, kPrecX3 = 1, kPrecBf16 = 2, kPrecF16x2 = 3;  // = MVML_GEMM_* ids
 GemmPlan plan_gemm(int prec, int64_t M, int64_t N, int64_t K) {
-  const char* env = getenv("MVML_X3_TILE");
-  const int force = env ? atoi(env) : 0;
+  const int force = option(MVML_OPT_GEMM_TILE);
   if (prec == kPrecBf16) {  // bf16 operands exist only in the 256x256 kernel
     const int64_t tw = ceil_div(M, XBM) * ceil_div(N, XBN);
     return {true, choose_splits_t(tw, K, 256)};
@@ -1565,15 +1521,12 @@ int choose_splits(int64_t M, int64_t N, int64_t K) {  // the larger of the two p
 
 int64_t k_chunk(int64_t K, int S) { return ceil_div(ceil_div(K, S), BKT) * BKT; }
 
-// Workgroups of a 256x256 launch: one per tile by default; MVML_X3W_PERSIST = P > 0 caps a
+// Workgroups of a 256x256 launch: one per tile by default; option MVML_OPT_GEMM_PERSIST = P > 0 caps a
 // launch without split-K at P workgroups that loop over their XCD's tiles (measured neutral at
 // P = 256 / 512 on the step's shapes: the dispatcher already overlaps one tile's C stores with
 // the next tile's start).
 unsigned x3w_grid_x(int64_t tiles, int S) {
-  static const int persist = [] {
-    const char* e = getenv("MVML_X3W_PERSIST");
-    return e ? atoi(e) : 0;
-  }();
+  const int persist = option(MVML_OPT_GEMM_PERSIST);
   if (S > 1 || persist <= 0 || tiles <= persist) return (unsigned)tiles;
   return (unsigned)persist;
 }
@@ -1882,10 +1835,7 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   // padding (so such products fell back to the 128x128 kernel entirely); instead the first
   // 256 q columns run on the 256x256 kernel and the last r on their own (narrow) plan — two
   // launches on the stream, one workspace reused in stream order.
-  static const bool nsplit_on = [] {
-    const char* e = getenv("MVML_GEMM_NSPLIT");
-    return !(e && atoi(e) == 0);
-  }();
+  const bool nsplit_on = option(MVML_OPT_GEMM_NSPLIT) != 0;
   if (nsplit_on && x3 && batch == 1 && N > XBN && N % XBN != 0 && N % XBN <= XBN / 2 &&
       plan_gemm(prec, M, N / XBN * XBN, K).wide) {
     const int64_t N1 = N / XBN * XBN, N2 = N - N1;

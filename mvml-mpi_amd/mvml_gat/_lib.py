@@ -4,6 +4,7 @@ The argument types of every entry point are parsed from the header itself, so th
 cannot drift from the ABI.  There is deliberately no fallback: if the shared library is
 missing or fails to load, every op raises.
 """
+import collections
 import ctypes
 import os
 import re
@@ -137,6 +138,29 @@ def call(name, *args):
         raise MvmlError(f"{name} failed (status {rc}): {msg}")
 
 
+# Kernel-path options (include/mvml_gat.h MVML_OPT_*): tests and tools switch paths through the
+# C ABI; the environment variables only seed the defaults when the library loads.
+OPTIONS = {"big_window": 0, "bwd_atomwise": 1, "gemm_tile": 2, "gemm_persist": 3, "gemm_nsplit": 4}
+
+
+class option:
+    """Context manager: ``with option("big_window", 0): ...`` sets a kernel-path option and
+    restores the previous value on exit."""
+
+    def __init__(self, name, value):
+        self.opt, self.value = OPTIONS[name], int(value)
+
+    def __enter__(self):
+        self.prev = lib().mvml_set_option(self.opt, self.value)
+        if self.prev < 0:
+            raise MvmlError(f"unknown option {self.opt}")
+        return self
+
+    def __exit__(self, *exc):
+        lib().mvml_set_option(self.opt, self.prev)
+        return False
+
+
 def ptr(t):
     """Raw device pointer of a tensor (None -> NULL)."""
     if t is None:
@@ -148,7 +172,8 @@ def stream_ptr(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-_ws = {}
+_ws = collections.OrderedDict()
+WS_STREAMS = 8  # scratch buffers kept (least recently used streams' buffers are dropped)
 
 
 def workspace(nbytes, device):
@@ -156,7 +181,9 @@ def workspace(nbytes, device):
     on different streams never share scratch (the header's re-entrancy contract), and calls on
     one stream reuse it in stream order.  Growing allocates on the current stream and drops the
     old buffer there too, so the caching allocator hands it out again only behind the work that
-    was enqueued on that stream before it."""
+    was enqueued on that stream before it (its blocks serve only allocations on that stream).
+    At most WS_STREAMS streams keep a buffer: a transient stream's scratch is dropped once
+    WS_STREAMS other streams have used the library since, never kept for the process lifetime."""
     dev = torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     key = (idx, torch.cuda.current_stream(idx).cuda_stream)
@@ -164,6 +191,9 @@ def workspace(nbytes, device):
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
         _ws[key] = buf
+    _ws.move_to_end(key)
+    while len(_ws) > WS_STREAMS:
+        _ws.popitem(last=False)
     return buf
 
 

@@ -77,7 +77,14 @@ def launch_local_ranks(nprocs, script, argv, port=None):
 class FlatGradAllReduce:
     """Packs every parameter gradient into one contiguous fp32 buffer and all-reduces it in a
     single call (the view's 6.9 M params = 27.7 MB: latency-, not bandwidth-bound on xGMI,
-    so one bucket beats per-tensor collectives)."""
+    so one bucket beats per-tensor collectives).
+
+    Parameters whose ``grad`` is None on EVERY rank stay None, as in the single-device
+    reference: torch Adam (main.py:88) skips them, so weight decay does not move the
+    constructed-but-unused LayerNorms (model.py:42, 120).  The buffer carries one presence
+    flag per parameter after the gradients (same collective): a parameter that has a gradient
+    on some rank but not on another gets the sum over the ranks that have one (zeros elsewhere,
+    DDP's convention); one with no gradient anywhere is left None."""
 
     def __init__(self, params, average=False, group=None):
         self.params = [p for p in params if p.requires_grad]
@@ -90,8 +97,11 @@ class FlatGradAllReduce:
         if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
             return
         dev = self.params[0].device
+        P = len(self.params)
         if self.buf is None or self.buf.device != dev:
-            self.buf = torch.empty(self.numel, dtype=self.params[0].dtype, device=dev)
+            self.buf = torch.empty(self.numel + P, dtype=self.params[0].dtype, device=dev)
+        flags = self.buf[self.numel:]
+        flags.copy_(torch.tensor([p.grad is not None for p in self.params], dtype=flags.dtype))
         off = 0
         for p in self.params:
             n = p.numel()
@@ -101,14 +111,16 @@ class FlatGradAllReduce:
                 self.buf[off:off + n].copy_(p.grad.reshape(-1))
             off += n
         dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group)
+        present = (flags > 0).tolist()
         if self.average:
-            self.buf.div_(dist.get_world_size(self.group))
+            self.buf[:self.numel].div_(dist.get_world_size(self.group))
         off = 0
-        for p in self.params:
+        for p, has in zip(self.params, present):
             n = p.numel()
-            g = self.buf[off:off + n].view_as(p)
-            if p.grad is None:
-                p.grad = g.clone()
-            else:
-                p.grad.copy_(g)
+            if has:
+                g = self.buf[off:off + n].view_as(p)
+                if p.grad is None:
+                    p.grad = g.clone()
+                else:
+                    p.grad.copy_(g)
             off += n

@@ -30,9 +30,11 @@ def _stream(dev):
     return _lib.stream_ptr(dev)
 
 
-# Diagnostics hook (tools/diag_golden.py, the parity tests' LeakyReLU-branch capture): when a
-# dict, GATLayerFunction.forward appends each layer's el/er to DEBUG_CAPTURE["elr_fwd"] and the
-# backward stores its saved el/er, attention and el/er gradients.  None in normal use.
+# Diagnostics hook (tools/diag_golden.py, the parity tests' kink-branch capture): when a dict,
+# GATLayerFunction.forward appends each layer's el/er to DEBUG_CAPTURE["elr_fwd"] and the
+# backward stores its saved el/er, attention and el/er gradients; LinearReLUFunction appends its
+# post-ReLU output to ["relu_out"] and the fusion its Conv2d+ReLU output to ["conv_out"].  None
+# in normal use.
 DEBUG_CAPTURE = None
 
 
@@ -79,11 +81,19 @@ _GEMM_ENTRY = {"f32": ("mvml_gemm_f32", 0), "x3": ("mvml_gemm_f32x3", 1),
 
 def known_amax(X):
     """(int32 tensor, slot) holding max |X| bits if the kernel that produced X folded it into
-    its stores (X._mvml_amax, set by the producer; valid while X is unmodified), else None."""
+    its stores, else None.  X._mvml_amax is set by the producer on the exact tensor it wrote;
+    the record is trusted only while that tensor is unmodified by torch (same _version) and
+    still is the storage the producer wrote (same data pointer, shape and strides) — a view, a
+    copy or an in-place update through autograd-visible ops gets a fresh |max| pass instead."""
     rec = getattr(X, "_mvml_amax", None)
-    if rec is None or rec[2] != X._version:
+    if rec is None or rec[2] != X._version or rec[3] != (X.data_ptr(), tuple(X.shape), X.stride()):
         return None
     return rec[0], rec[1]
+
+
+def fold_amax(out, amx, slot_idx):
+    """Record that out's |max| bits are in amx[slot_idx] (folded by the kernel that wrote out)."""
+    out._mvml_amax = (amx, slot_idx, out._version, (out.data_ptr(), tuple(out.shape), out.stride()))
 
 
 def absmax(P, rows, cols, ld, out, slot=0, offset=0, accumulate=False):
@@ -176,16 +186,14 @@ class GATLayerFunction(torch.autograd.Function):
         HF = H * F
         mean_res = int(mode == MODE_MEAN)
         C = _lib.lib().mvml_gat_proj_cols(H, F, mean_res)
-        ldy = _row_pitch(C)
         st = _stream(dev)
         # Pad the feature dimension to a multiple of 4 (e.g. 74 atom features -> 76) so every
         # GEMM operand row is 16-B aligned and the LDS-DMA path applies; pad columns are zero.
+        # (A ones pad column that would make the dW GEMM emit the bias gradient as well was
+        # measured 1.02e-5 from float64 on config 3 — the bias sums cancel and the split-fp16
+        # representation error shows — so the bias keeps its exact fp32 column sum.)
         Fp = _round4(Fin)
         Xp = X if Fp == Fin else torch.nn.functional.pad(X, (0, Fp - Fin))
-        # (a ones pad column that would make the dW GEMM emit the bias gradient as well was
-        # measured 1.02e-5 from float64 on config 3 — the bias sums cancel and the split-fp16
-        # representation error shows — so the bias keeps its exact fp32 column sum)
-        ones_col = False
         attn_l, attn_r = _c(attn_l), _c(attn_r)
         attn_lr = torch.cat([attn_l.reshape(-1), attn_r.reshape(-1)])
         # [fc.weight ; res_fc.weight (or its head mean) ; A_l ; A_r]: the projection GEMM uses
@@ -193,8 +201,6 @@ class GATLayerFunction(torch.autograd.Function):
         Wcat = torch.empty((C + 2 * H, Fp), dtype=torch.float32, device=dev)
         call("mvml_gat_fold_weights", ptr(_c(fc_w)), ptr(_c(res_w)), ptr(attn_lr), H, F, Fin, Fp,
              mean_res, ptr(Wcat), st)
-        Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
-        elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
         L = _lib.lib()
         # split-fp16: |max| of X, Wcat (all C + 2H rows) and, in the backward, gY — each operand's
         # pass serves all of its products (projection, dL/dW, dL/dX)
@@ -220,6 +226,9 @@ class GATLayerFunction(torch.autograd.Function):
                  bsplit=None if wps[0] is None else wps)
             elr = Y[:, C:C + 2 * H].contiguous()
         else:
+            ldy = _row_pitch(C)
+            Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
+            elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
             wp, wn = _lib.ws_ptr_size(L.mvml_gat_proj_fwd_workspace_size(N, H, F), dev)
             _lib.call_tag[0] = {"flops": 2 * N * C * Fp}
             call("mvml_gat_proj_fwd", N, ptr(Xp), Fp, Fp, ptr(Wcat), Fp, ptr(attn_lr), H, F, mean_res,
@@ -234,7 +243,7 @@ class GATLayerFunction(torch.autograd.Function):
              ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(_c(bias)), float(slope), int(mode),
              ptr(out), ptr(attn), slot(amx, 3), st)
         if amx is not None:  # max |out| for the consumer's split-fp16 GEMMs (next layer, Set2Set)
-            out._mvml_amax = (amx, 3, out._version)
+            fold_amax(out, amx, 3)
         if DEBUG_CAPTURE is not None:
             DEBUG_CAPTURE.setdefault("elr_fwd", []).append(elr.detach().clone())
         ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr)
@@ -244,7 +253,6 @@ class GATLayerFunction(torch.autograd.Function):
         ctx.amx = amx
         ctx.ax = ax
         ctx.wps = wps
-        ctx.ones_col = ones_col
         return out
 
     @staticmethod
@@ -263,6 +271,8 @@ class GATLayerFunction(torch.autograd.Function):
         ldg = _row_pitch(CE)
         st = _stream(dev)
         gY = torch.empty((N, ldg), dtype=torch.float32, device=dev)
+        if ctx.amx is not None:
+            ctx.amx[2:3].zero_()  # max |gY| of THIS backward (a second one, retain_graph, refolds it)
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_agg_bwd_workspace_size(g.num_edges(), H), dev)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}",
                             "bytes": agg_bwd_bytes(N, g.num_edges(), H, F, g_out.shape[1], mode)}
@@ -294,14 +304,8 @@ class GATLayerFunction(torch.autograd.Function):
             DEBUG_CAPTURE.update(elr=elr, gelr=gelr, attn=attn)
         g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
         if mean_res:  # every head's bias sees g_out / H: one column sum, replicated over heads
-            if ctx.ones_col:
-                g_bias[:F].copy_(gW[HF:HF + F, Fin])
-                g_bias[:F].mul_(1.0 / H)
-            else:
-                colsum(gY, N, F, ldg, g_bias, offset=HF, alpha=1.0 / H)
+            colsum(gY, N, F, ldg, g_bias, offset=HF, alpha=1.0 / H)
             g_bias.view(H, F)[1:].copy_(g_bias[:F].expand(H - 1, F))
-        elif ctx.ones_col:  # gY^T [.. | 1] from the dW GEMM (Xp's column Fin)
-            g_bias.copy_(gW[HF:2 * HF, Fin])
         else:
             colsum(gY, N, HF, ldg, g_bias, offset=HF)
         gX = None
@@ -563,6 +567,8 @@ class LinearReLUFunction(torch.autograd.Function):
         lm = ctx.lm = linear_maxima(x, weight)
         gemm(x, weight, M, Nout, K, 0, 0, K, K, y, Nout, bias=_c(bias), act=1,
              amax=None if lm is None else (slot(*lm[1]), slot(lm[0], 1)))
+        if DEBUG_CAPTURE is not None:  # the ReLU sides the product took (parity tests)
+            DEBUG_CAPTURE.setdefault("relu_out", []).append(y.detach())
         ctx.save_for_backward(x, weight, y)
         return y
 

@@ -110,6 +110,8 @@ class FusionAttnConvFunction(torch.autograd.Function):
             saved = (Wqkv, QKV)
         out = torch.empty((B, H, D - 2), **f32)
         call("mvml_conv3_fwd", B, H, H, D, ptr(att), ptr(_c(conv_w)), ptr(_c(conv_b)), ptr(out), st)
+        if _F.DEBUG_CAPTURE is not None:  # the ReLU sides the product took (parity tests)
+            _F.DEBUG_CAPTURE["conv_out"] = out.detach()
         ctx.save_for_backward(X, Xn, mean, rstd, ln_w, wq, wk, wv, *saved, P, att, out, conv_w)
         ctx.dims = (B, D, H, scale, fold)
         return out.view(B, H * (D - 2))
@@ -206,6 +208,10 @@ class MVFusion(nn.Module):
 
     def __init__(self, final_hidden_feats=384, num_heads=12, num_classes=11, dropout=0.2):
         super().__init__()
+        if final_hidden_feats != 384 or num_heads != 12:
+            raise ValueError(
+                "the HIP fusion kernels are built for the reference configuration (config.py: "
+                f"hidden_feats[-1] = 384, head = 12); got {final_hidden_feats} / {num_heads}")
         d = final_hidden_feats
         self.final_hidden_feats, self.num_heads = d, num_heads
         self.norm_layer_module = nn.LayerNorm(d)

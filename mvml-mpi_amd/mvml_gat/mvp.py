@@ -49,13 +49,18 @@ class MVP(MVFusion):
         return self.sigmoid(self.forward(smiles, graphs, atom_feats, fp_t))
 
 
-def train_step(model, optimizer, batch, reducer=None):
+def train_step(model, optimizer, batch, reducer=None, loss_fn=bce_with_logits):
     """main.py:24-36 for one batch: forward, BCEWithLogitsLoss (main.py:91), backward, the
     data-parallel flat gradient all-reduce (reducer, BASELINE config 4), optimizer step.
-    batch = (smiles, graphs, atom_feats, fp_t, labels); returns the loss tensor."""
+    batch = (smiles, graphs, atom_feats, fp_t, labels); returns the loss tensor.  Gradients are
+    zeroed in place like the reference's optimizer.zero_grad() under its pinned torch 1.12.1
+    (set_to_none=False, main.py:34); parameters that never receive a gradient (the unused
+    LayerNorms, model.py:42, 120) keep grad None — the reducer preserves that — so Adam's
+    weight decay leaves them alone.  loss_fn: the HIP BCEWithLogits by default (the CPU tests
+    pass the oracle's)."""
     smiles, graphs, atom_feats, fp_t, labels = batch
     optimizer.zero_grad(set_to_none=False)
-    loss = bce_with_logits(model(smiles, graphs, atom_feats, fp_t), labels)
+    loss = loss_fn(model(smiles, graphs, atom_feats, fp_t), labels)
     loss.backward()
     if reducer is not None:
         reducer()

@@ -37,7 +37,10 @@ class MVFusionRef(nn.Module):
         self.mlp = nn.Sequential(nn.Linear((dim - 2) * num_heads, 1024), nn.ReLU(), nn.Dropout(dropout),
                                  nn.Linear(1024, num_classes))
 
-    def forward(self, smiles_x, graph_x, fp_x):
+    def forward(self, smiles_x, graph_x, fp_x, conv_branch=None, mlp_branch=None):
+        """conv_branch (B, nh, 1, dim-2) / mlp_branch (B, 1024): optional given sides of the two
+        ReLUs (gnn_ref.relu_branch), for evaluating the float64 oracle on the fp32 product's side
+        of each kink (the parity tests); None = plain ReLU."""
         B = graph_x.shape[0]
         ln = self.norm_layer_module
         x = torch.cat([ln(smiles_x).view(B, 1, -1), ln(graph_x).view(B, 1, -1),
@@ -48,8 +51,16 @@ class MVFusionRef(nn.Module):
         v = self.linear_v(x).reshape(B, 3, nh, dk).transpose(1, 2)
         dist = torch.softmax(torch.matmul(q, k.transpose(2, 3)) * self._norm_fact, dim=-1)
         att = torch.matmul(dist, v)
-        out = self.conv(att).view(B, -1)
-        return self.mlp(out)
+        if conv_branch is None and mlp_branch is None:
+            out = self.conv(att).view(B, -1)
+            return self.mlp(out)
+        from .gnn_ref import relu_branch
+        c = self.conv[0](att)
+        c = relu_branch(c, conv_branch.view_as(c)) if conv_branch is not None else torch.relu(c)
+        out = self.conv[2](c).view(B, -1)
+        h = self.mlp[0](out)
+        h = relu_branch(h, mlp_branch) if mlp_branch is not None else torch.relu(h)
+        return self.mlp[3](self.mlp[2](h))
 
 
 def bce_logits_ref(logits, labels):
@@ -87,6 +98,7 @@ class MVPRef(MVFusionRef):
         self.rnn = RNNModuleRef(39, rnn_embed_dim, blstm_dim, blstm_layers, hidden_feats[-1], dropout)
         self.fp_mlp = FPNModuleRef(fp_2_dim, hidden_feats[-1], dropout)
 
-    def forward(self, smiles, graph, atom_feats, fp_t, branches=None):
+    def forward(self, smiles, graph, atom_feats, fp_t, branches=None, conv_branch=None,
+                mlp_branch=None):
         return MVFusionRef.forward(self, self.rnn(smiles), self.gnn(graph, atom_feats, branches),
-                                   self.fp_mlp(fp_t))
+                                   self.fp_mlp(fp_t), conv_branch, mlp_branch)

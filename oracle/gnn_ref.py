@@ -2,7 +2,9 @@
 
 TEST INFRASTRUCTURE ONLY (see oracle/__init__.py; parity unpinned against DGL/PyG).
 Every function runs in whatever dtype its inputs carry (float64 for parity, float32 for
-the CPU baseline) and is differentiable with torch autograd, which supplies the oracle
+the CPU baseline) and on whatever device they live on (the CPU normally; the bench-size
+parity tests run the same float64 torch ops on the GPU — still the checker, never the
+product path), and is differentiable with torch autograd, which supplies the oracle
 backward (a15).
 
 Restated semantics (pinned third-party versions from README.md:10-19):
@@ -34,18 +36,20 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 
-def _as_long(a):
-    return torch.as_tensor(np.asarray(a), dtype=torch.long)
+def _as_long(a, device=None):
+    if isinstance(a, torch.Tensor):
+        return a.to(device=device, dtype=torch.long)
+    return torch.as_tensor(np.asarray(a), dtype=torch.long, device=device)
 
 
 def edge_softmax_ref(score, dst, num_nodes):
     """dgl edge_softmax(norm_by='dst'): score (E,H) -> attention (E,H)."""
     H = score.shape[1]
     idx = dst.view(-1, 1).expand(-1, H)
-    smax = torch.full((num_nodes, H), -math.inf, dtype=score.dtype)
+    smax = torch.full((num_nodes, H), -math.inf, dtype=score.dtype, device=score.device)
     smax = smax.scatter_reduce(0, idx, score.detach(), reduce="amax", include_self=True)
     ex = torch.exp(score - smax[dst])
-    ssum = torch.zeros((num_nodes, H), dtype=score.dtype).index_add(0, dst, ex)
+    ssum = torch.zeros((num_nodes, H), dtype=score.dtype, device=score.device).index_add(0, dst, ex)
     return ex / ssum[dst]
 
 
@@ -59,10 +63,16 @@ def leaky_relu_branch(x, slope, positive):
     return torch.where(positive, x, x * slope)
 
 
+def relu_branch(x, positive):
+    """ReLU whose side is GIVEN per element (the product's own fp32 side, read off its post-ReLU
+    output > 0): equal to relu(x) wherever sign(x) agrees; used like leaky_relu_branch."""
+    return torch.where(positive, x, torch.zeros_like(x))
+
+
 def gatconv_ref(src, dst, X, fc_w, res_w, attn_l, attn_r, bias, num_heads, out_feats,
                 negative_slope=0.2, return_attention=False, branch=None):
-    src = _as_long(src)
-    dst = _as_long(dst)
+    src = _as_long(src, X.device)
+    dst = _as_long(dst, X.device)
     n = X.shape[0]
     H, Fo = num_heads, out_feats
     Z = (X @ fc_w.t()).view(n, H, Fo)
@@ -73,7 +83,7 @@ def gatconv_ref(src, dst, X, fc_w, res_w, attn_l, attn_r, bias, num_heads, out_f
     else:
         e = leaky_relu_branch(el[src] + er[dst], negative_slope, branch)
     a = edge_softmax_ref(e, dst, n)
-    rst = torch.zeros((n, H, Fo), dtype=X.dtype).index_add(0, dst, a.unsqueeze(-1) * Z[src])
+    rst = torch.zeros((n, H, Fo), dtype=X.dtype, device=X.device).index_add(0, dst, a.unsqueeze(-1) * Z[src])
     rst = rst + (X @ res_w.t()).view(n, H, Fo)
     rst = rst + bias.view(1, H, Fo)
     if return_attention:
@@ -107,8 +117,9 @@ def set2set_ref(node_offsets, X, lstm, n_iters):
     node_offsets = np.asarray(node_offsets, dtype=np.int64)
     B = len(node_offsets) - 1
     D = X.shape[1]
-    counts = torch.as_tensor(np.diff(node_offsets), dtype=torch.long)
-    gid = torch.repeat_interleave(torch.arange(B), counts)
+    dev = X.device
+    counts = torch.as_tensor(np.diff(node_offsets), dtype=torch.long, device=dev)
+    gid = torch.repeat_interleave(torch.arange(B, device=dev), counts)
     nl = lstm.num_layers
     h = (X.new_zeros((nl, B, D)), X.new_zeros((nl, B, D)))
     q_star = X.new_zeros((B, 2 * D))
@@ -116,12 +127,12 @@ def set2set_ref(node_offsets, X, lstm, n_iters):
         q, h = lstm(q_star.unsqueeze(0), h)
         q = q.view(B, D)
         e = (X * q[gid]).sum(-1)
-        emax = torch.full((B,), -math.inf, dtype=X.dtype).scatter_reduce(
+        emax = torch.full((B,), -math.inf, dtype=X.dtype, device=dev).scatter_reduce(
             0, gid, e.detach(), reduce="amax", include_self=True)
         ex = torch.exp(e - emax[gid])
-        esum = torch.zeros(B, dtype=X.dtype).index_add(0, gid, ex)
+        esum = torch.zeros(B, dtype=X.dtype, device=dev).index_add(0, gid, ex)
         alpha = ex / esum[gid]
-        readout = torch.zeros((B, D), dtype=X.dtype).index_add(0, gid, X * alpha.unsqueeze(-1))
+        readout = torch.zeros((B, D), dtype=X.dtype, device=dev).index_add(0, gid, X * alpha.unsqueeze(-1))
         q_star = torch.cat([q, readout], dim=-1)
     return q_star
 
@@ -217,12 +228,15 @@ class GNNModuleRef(nn.Module):
                         "attn_l": c.attn_l, "attn_r": c.attn_r, "bias": c.bias})
         return out
 
-    def forward(self, graph, atom_feats, branches=None):
-        """branches: optional per-GAT-layer bool (E, H) LeakyReLU sides (leaky_relu_branch)."""
+    def forward(self, graph, atom_feats, branches=None, fc_branch=None):
+        """branches: optional per-GAT-layer bool (E, H) LeakyReLU sides (leaky_relu_branch);
+        fc_branch: optional bool (B, out) side of the fc ReLU (relu_branch)."""
         node_x = gat_ref(graph["src"], graph["dst"], atom_feats, self.layer_params(),
                          self.hidden_feats, branches=branches)
         graph_x = set2set_ref(graph["node_offsets"], node_x, self.readout.lstm,
                               self.readout.n_iters)
         out = graphnorm_ref(graph_x, self.norm.weight, self.norm.bias, self.norm.mean_scale,
                             self.norm.eps, graph.get("group_offsets"))
-        return self.fc(out)
+        if fc_branch is None:
+            return self.fc(out)
+        return self.fc[2](relu_branch(self.fc[0](out), fc_branch))

@@ -169,3 +169,79 @@ def test_bench_launcher_two_ranks_dry_run():
     assert two["inference"]["checksum"] == one["inference"]["checksum"]
     trained = _run_bench("--gpus", "2", "--steps", "2", "--warmup", "1", *common)
     assert trained["n_gpus"] == 2 and trained["value"] > 0 and trained["config"]["parallelism"] == "dp2"
+
+
+def _mvp_setup():
+    """A small MVPRef (float64, eval: no dropout) and a 4-molecule batch in 2 GraphNorm groups."""
+    from _util import batch_of_sizes, graph_dict
+    from oracle.fusion_ref import MVPRef
+    torch.manual_seed(3)
+    ref = MVPRef(num_classes=3, in_feats=74, hidden_feats=(8, 12), num_step_set2set=2,
+                 num_layer_set2set=2, rnn_embed_dim=6, blstm_dim=5, blstm_layers=1, fp_2_dim=7,
+                 num_heads=2, dropout=0.5).double().eval()
+    sb = batch_of_sizes([9, 12, 7, 15], seed=4)
+    g = torch.Generator().manual_seed(5)
+    lens = [7, 4, 9, 6]
+    tok = torch.randint(1, 39, (4, 9), generator=g).double()
+    for i, L in enumerate(lens):
+        tok[i, L:] = 0
+    fp = (torch.rand(4, 2513, generator=g) < 0.2).double()
+    y = (torch.rand(4, 3, generator=g) < 0.4).double()
+    return ref, sb, tok, lens, fp, y
+
+
+def _mvp_batch(sb, tok, lens, fp, y, lo, hi):
+    gd, X = _subbatch(sb, lo, hi)
+    return ({"smiles": tok[lo:hi], "seq_len": lens[lo:hi]}, gd, X, fp[lo:hi], y[lo:hi])
+
+
+def _mvp_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mvml_gat.mvp import train_step
+    from oracle.fusion_ref import bce_logits_ref
+    ref, sb, tok, lens, fp, y = _mvp_setup()
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3, weight_decay=1e-4)
+    red = FlatGradAllReduce(ref.parameters(), average=True)
+    for _ in range(2):
+        train_step(ref, opt, _mvp_batch(sb, tok, lens, fp, y, 2 * rank, 2 * rank + 2), red,
+                   loss_fn=bce_logits_ref)
+    if rank == 0:
+        out.put(({n: p.detach().numpy().copy() for n, p in ref.named_parameters()},
+                 [n for n, p in ref.named_parameters() if p.grad is None]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_mvp_train_step_keeps_reference_adam_semantics():
+    """two gloo ranks of mvp.train_step (each half of the batch, one flat
+    all-reduce, Adam lr 1e-3 wd 1e-4 as main.py:88) equal the single-process steps; the
+    parameters that never get a gradient in the reference (MVP.norm_layer, RNNModule.norm_layer,
+    model.py:42, 120) keep grad None and are NOT moved by Adam's weight decay."""
+    from mvml_gat.mvp import train_step
+    from oracle.fusion_ref import bce_logits_ref
+    ref, sb, tok, lens, fp, y = _mvp_setup()
+    init = {n: p.detach().clone() for n, p in ref.named_parameters()}
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3, weight_decay=1e-4)
+    for _ in range(2):
+        train_step(ref, opt, _mvp_batch(sb, tok, lens, fp, y, 0, 4), loss_fn=bce_logits_ref)
+    want = {n: p.detach().clone() for n, p in ref.named_parameters()}
+    unused = {n for n, p in ref.named_parameters() if p.grad is None}
+    assert unused == {"norm_layer.weight", "norm_layer.bias", "rnn.norm_layer.weight",
+                      "rnn.norm_layer.bias"}, unused
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mvp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, got_unused = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert set(got_unused) == unused
+    for n in unused:
+        assert torch.equal(torch.as_tensor(got[n]), init[n]), n
+    for n, w in want.items():
+        d = (torch.as_tensor(got[n]) - w).abs().max().item()
+        assert d <= 1e-12 * max(1.0, w.abs().max().item()), (n, d)

@@ -42,6 +42,7 @@ from _util import batch_of_sizes, graph_dict, model_pair
 from conftest import rel_err
 from mvml_gat import functional as Fn
 from mvml_gat import synth
+from mvml_gat._lib import option
 from oracle import gnn_ref
 
 pytestmark = pytest.mark.gpu
@@ -202,11 +203,11 @@ def test_gat_layer1_config5():
 
 
 @pytest.mark.parametrize("layer", [0, 1])
-def test_gat_layer_config5_fallback_kernels(layer, monkeypatch):
-    """MVML_BIG_WINDOW=0: config-5 groups through the per-atom fallbacks (forward gather with
-    its hub pass, dst / src backward pair) — the path of groups past the big window's caps."""
-    monkeypatch.setenv("MVML_BIG_WINDOW", "0")
-    _layer_case(layer, synth.config5(2, seed=3), seed=4 + layer)
+def test_gat_layer_config5_fallback_kernels(layer):
+    """Option big_window = 0: config-5 groups through the per-atom fallbacks (forward gather
+    with its hub pass, dst / src backward pair) — the path of groups past the big window's caps."""
+    with option("big_window", 0):
+        _layer_case(layer, synth.config5(2, seed=3), seed=4 + layer)
 
 
 @pytest.mark.parametrize("layer", [0, 1])
@@ -222,7 +223,7 @@ def test_gat_layer_big_window_table_overflow(layer):
 @pytest.mark.parametrize("layer", [0, 1])
 @pytest.mark.parametrize("case", ["config2", "config5_big", "config5_fallback", "table_overflow",
                                   "atomwise"])
-def test_gat_bwd_fused_gy_max(layer, case, monkeypatch):
+def test_gat_bwd_fused_gy_max(layer, case):
     """mvml_gat_agg_bwd folds max |gY| (the split-fp16 scale of the dL/dW and dL/dX GEMMs) into
     its stores: it must equal the max over every column the GEMMs read, [dZ | dR | d el | d er],
     on every kernel path that writes gY (LDS windows, big windows, the dst / src fallback pair
@@ -234,10 +235,12 @@ def test_gat_bwd_fused_gy_max(layer, case, monkeypatch):
           "config5_fallback": lambda: synth.config5(2, seed=3),
           "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109),
           "atomwise": lambda: synth.config3(128, seed=2)}[case]()
-    if case == "config5_fallback":
-        monkeypatch.setenv("MVML_BIG_WINDOW", "0")
-    if case == "atomwise":
-        monkeypatch.setenv("MVML_BWD_ATOMWISE", "1")
+    opts = {"config5_fallback": ("big_window", 0), "atomwise": ("bwd_atomwise", 1)}
+    with option(*opts.get(case, ("big_window", 1))):
+        _gy_max_case(layer, sb)
+
+
+def _gy_max_case(layer, sb):
     prod, _ = model_pair(seed=layer)
     conv = prod.conv.gnn_layers[layer].to(DEV)
     g = sb.to_graph().to(DEV)
@@ -257,6 +260,6 @@ def test_gat_bwd_fused_gy_max(layer, case, monkeypatch):
     got = amx.cpu().view(torch.float32).item()
     assert got == want and want > 0, (got, want)
     # and max |out| folded into the forward aggregation's stores (the next GEMMs' operand max)
-    t, i, _ = out._mvml_amax
+    t, i = out._mvml_amax[:2]
     got_o = t[i:i + 1].cpu().view(torch.float32).item()
     assert got_o == out.detach().abs().max().item(), (got_o, out.detach().abs().max().item())

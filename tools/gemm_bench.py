@@ -6,6 +6,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "mvml-mpi_amd"), ROOT]
 import torch  # noqa: E402
+from mvml_gat._lib import option  # noqa: E402
 from mvml_gat.functional import gemm  # noqa: E402
 
 N_ATOMS, B = 1754373, 65536
@@ -59,11 +60,10 @@ def main():
                 Bt = Bm if bk else Bm.t()
                 ms, t = tf(lambda: torch.matmul(At, Bt, out=C), flops)
             else:
-                os.environ.pop("MVML_X3_TILE", None)
-                if "-" in algo:
-                    os.environ["MVML_X3_TILE"] = algo.split("-")[1]
                 a = algo.split("-")[0]
-                ms, t = tf(lambda: gemm(A, Bm, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N, algo=a), flops)
+                with option("gemm_tile", int(algo.split("-")[1]) if "-" in algo else 0):
+                    ms, t = tf(lambda: gemm(A, Bm, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N,
+                                            algo=a), flops)
             cols.append(f"{algo} {ms:8.3f} ms {t:6.1f} TF/s")
         print(f"{name:22s} M={M:8d} N={N:5d} K={K:8d}  " + " | ".join(cols), flush=True)
         del A, Bm, C
