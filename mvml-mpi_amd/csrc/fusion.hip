@@ -242,6 +242,29 @@ token_attn_bwd_kernel(int64_t B, int H, int dk, const float* __restrict__ qkv, i
   }
 }
 
+// Softmax backward of one head's 3 x 3 scores: g_p_ac = <g_a, v_c> (wave sums), then
+// g_s_ac = p_ac (g_p_ac - sum_c' p_ac' g_p_ac') scale, with every product and sum explicit (no
+// contraction left to the compiler), so the fused and unfused kernels agree bit for bit.
+__device__ __forceinline__ void fold_grad_scores(const float (&g)[NT][kDkVpl],
+                                                 const float (&v)[NT][kDkVpl],
+                                                 const float (&p)[NT][NT], float scale,
+                                                 float (&gs)[NT][NT]) {
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+    float gp[NT];
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      float sc = 0.f;
+#pragma unroll
+      for (int i = 0; i < kDkVpl; ++i) sc = fmaf(g[a][i], v[c][i], sc);
+      gp[c] = wsum(sc);
+    }
+    const float dot = fmaf(p[a][2], gp[2], fmaf(p[a][1], gp[1], __fmul_rn(p[a][0], gp[0])));
+#pragma unroll
+    for (int c = 0; c < NT; ++c) gs[a][c] = __fmul_rn(__fmul_rn(p[a][c], __fsub_rn(gp[c], dot)), scale);
+  }
+}
+
 // Folded Q.K (the QK^T of model.py:65-68 re-associated): s_ij = <q_i, k_j> = x_i W_q^T W_k x_j^T
 // = <p_i, x_j> with p = x M_h, M_h = W_q,h^T W_k,h (D x D per head), so the product GEMM forms
 // [P | V] = X [M_1 .. M_H | W_v^T] (2 H D columns instead of 3 H D) and the attention reads the
@@ -354,20 +377,7 @@ token_attn_fold_bwd_kernel(int64_t B, int H, int dk, const float* __restrict__ p
       }
     }
     float gs[NT][NT];
-#pragma unroll
-    for (int a = 0; a < NT; ++a) {
-      float gp[NT];
-#pragma unroll
-      for (int c = 0; c < NT; ++c) {
-        float sc = 0.f;
-#pragma unroll
-        for (int i = 0; i < kDkVpl; ++i) sc = fmaf(g[a][i], v[c][i], sc);
-        gp[c] = wsum(sc);
-      }
-      const float dot = p[a][0] * gp[0] + p[a][1] * gp[1] + p[a][2] * gp[2];
-#pragma unroll
-      for (int c = 0; c < NT; ++c) gs[a][c] = p[a][c] * (gp[c] - dot) * scale;
-    }
+    fold_grad_scores(g, v, p, scale, gs);
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
       float* grow = gpv + (b * NT + c) * ldg + (int64_t)h * dk;
@@ -859,6 +869,340 @@ conv3_fwd3_kernel(int64_t B, int W, int64_t per_block, const float* __restrict__
   }
 }
 
+// ---- token attention + Conv2d fused (round 3) ---------------------------------------------
+// The (12, 3, 384) attention cube of a molecule is formed in LDS and consumed there by the
+// convolution: it never makes the HBM round trip between the attention and the Conv2d (forward:
+// 55 KB written + read per molecule; backward: the cube read, its gradient written and read
+// again).  One workgroup of 12 waves per run of molecules, wave h = head h; the attention
+// arithmetic is token_attn_fold_fwd / _bwd's (same operation order, so the cube and every g_pv
+// element are bit-identical to the unfused pair), the convolution conv3_fwd3 / conv3_bwd2's
+// with the column tiles spread over 12 waves.  The backward recomputes the cube as P V (bitwise
+// the forward's values) instead of reading a saved copy, and sums the keys' gradient over heads
+// as twelve wave partials added in head order (the unfused kernel's order).
+constexpr int kFuseWaves = 12;  // = kConvC heads
+constexpr int kFuseThreads = 64 * kFuseWaves;
+constexpr int kFuseW = 64 * kDkVpl;              // 384 columns
+constexpr int kFuseCube = kConvC * kConvH * kConvLd + 8;  // cube rows (h, t) + a zero tail
+constexpr int kFuseG = kConvO * kConvLd;          // g_pre rows o
+static_assert(kFuseW <= kConvLd - 1, "one pad column per cube row");
+
+// softmax(scale * <q_a, k_c>) over c for the 3 x 3 scores of one head (token_attn_fold_fwd's order)
+__device__ __forceinline__ void fold_scores(const float (&q)[NT][kDkVpl], const float (&k)[NT][kDkVpl],
+                                            float scale, float (&p)[NT][NT]) {
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      float sc = 0.f;
+#pragma unroll
+      for (int i = 0; i < kDkVpl; ++i) sc = fmaf(q[a][i], k[c][i], sc);
+      p[a][c] = wsum(sc) * scale;
+    }
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+    const float m = fmaxf(p[a][0], fmaxf(p[a][1], p[a][2]));
+    float z = 0.f;
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      p[a][c] = expf(p[a][c] - m);
+      z += p[a][c];
+    }
+#pragma unroll
+    for (int c = 0; c < NT; ++c) p[a][c] /= z;
+  }
+}
+
+// att rows (h, a) = sum_c p_ac v_c into the LDS cube (row stride kConvLd)
+__device__ __forceinline__ void fold_att_lds(const float (&p)[NT][NT], const float (&v)[NT][kDkVpl],
+                                             float* s_rows, int lane) {
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int i = 0; i < kDkVpl; ++i) {
+      float o = 0.f;
+#pragma unroll
+      for (int c = 0; c < NT; ++c) o = fmaf(p[a][c], v[c][i], o);
+      s_rows[a * kConvLd + lane + 64 * i] = o;
+    }
+}
+
+__device__ __forceinline__ void load_rows3(const float* __restrict__ base, int64_t ld, int lane,
+                                           float (&r)[NT][kDkVpl]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < kDkVpl; ++i) r[t][i] = base[t * ld + lane + 64 * i];
+}
+
+__global__ void __launch_bounds__(kFuseThreads, 3)  // one workgroup per CU
+attn_conv_fwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv, int64_t ld,
+                     const float* __restrict__ x, int64_t ldx, float scale,
+                     const float* __restrict__ wgt, const float* __restrict__ bias,
+                     float* __restrict__ P, float* __restrict__ out) {
+  constexpr int W = kFuseW, Wo = W - 2, H = kConvC;
+  constexpr int64_t HD = (int64_t)H * W;
+  __shared__ float s_in[kFuseCube];
+  const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
+  const int lo = lane & 15, lk = lane >> 4;
+  float wfr[27];
+#pragma unroll
+  for (int ks = 0; ks < 27; ++ks) wfr[ks] = lo < kConvO ? wgt[lo * 108 + 4 * ks + lk] : 0.f;
+  float bo[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bo[r] = 4 * lk + r < kConvO ? bias[4 * lk + r] : 0.f;
+  if (tid < 8) s_in[kConvC * kConvH * kConvLd + tid] = 0.f;
+  const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(B, b0 + per_block);
+  // head h's rows of molecule b: keys (the LayerNorm rows), p and v; the next molecule's are
+  // loaded while this one's convolution runs
+  float k[NT][kDkVpl], q[NT][kDkVpl], v[NT][kDkVpl];
+  auto load = [&](int64_t b) {
+    load_rows3(x + b * NT * ldx, ldx, lane, k);
+    load_rows3(pv + b * NT * ld + (int64_t)h * W, ld, lane, q);
+    load_rows3(pv + b * NT * ld + HD + (int64_t)h * W, ld, lane, v);
+  };
+  if (b0 < b1) load(b0);
+  for (int64_t b = b0; b < b1; ++b) {
+    __syncthreads();  // the previous molecule's convolution reads of the cube are done
+    {
+      float p[NT][NT];
+      fold_scores(q, k, scale, p);
+      fold_att_lds(p, v, s_in + h * NT * kConvLd, lane);
+      if (lane < NT * NT) {
+        float pvv = p[0][0];
+#pragma unroll
+        for (int e = 1; e < NT * NT; ++e) pvv = lane == e ? p[e / NT][e % NT] : pvv;
+        P[(b * H + h) * NT * NT + lane] = pvv;
+      }
+    }
+    if (b + 1 < b1) load(b + 1);
+    __syncthreads();
+    // Conv2d + bias + ReLU on the matrix cores (conv3_fwd3_kernel): wave h the column tiles
+    // [32 h, 32 h + 32)
+    f32x4_t acc[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) acc[ct] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 27; ++ks) {
+      const int kk = 4 * ks + lk;
+      const int koff = (kk / 3) * kConvLd + kk % 3;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const float bv = s_in[koff + 32 * h + 16 * ct + lo];  // columns >= Wo: discarded
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(wfr[ks], bv, acc[ct], 0, 0, 0);
+      }
+    }
+    float* ob = out + b * (int64_t)(kConvO * Wo);
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const int xx = 32 * h + 16 * ct + lo;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = 4 * lk + r;
+        if (o < kConvO && xx < Wo) ob[o * Wo + xx] = fmaxf(acc[ct][r] + bo[r], 0.f);
+      }
+    }
+  }
+}
+
+// Backward of attn_conv_fwd per molecule: (1) g_pre = g_out (out > 0) into LDS and the cube
+// recomputed as P V into LDS, (2) the Conv2d weight / bias gradient on the matrix cores
+// (conv3_bwd2's MFMA steps, wave w the x-steps [8 w, 8 w + 8)), (3) the cube's gradient
+// (conv3_bwd2's VALU loop, threads t and t + 384 the (c, dy) rows [0, 18) / [18, 36) of column
+// t) written over the cube, (4) the attention backward of head h by wave h
+// (token_attn_fold_bwd): g_pv stores, the keys' gradient partial over its own cube rows, then
+// the twelve partials in head order.  All LDS in one array: [cube | g_pre].
+__global__ void __launch_bounds__(kFuseThreads, 3)  // one workgroup per CU
+attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv, int64_t ld,
+                     const float* __restrict__ x, int64_t ldx, float scale,
+                     const float* __restrict__ P, const float* __restrict__ wgt,
+                     const float* __restrict__ out, const float* __restrict__ g_out,
+                     float* __restrict__ gpv, int64_t ldg, float* __restrict__ gk, int64_t ldgk,
+                     uint32_t* __restrict__ gpv_amax, float* __restrict__ part) {
+  constexpr int W = kFuseW, Wo = W - 2, H = kConvC;
+  constexpr int64_t HD = (int64_t)H * W;
+  constexpr int kCD = kConvC * kConvH / 2;  // cube-gradient rows per thread
+  __shared__ float lds[kFuseCube + kFuseG];
+  float* s_in = lds;
+  float* s_g = lds + kFuseCube;
+  const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
+  const int lo = lane & 15, lk = lane >> 4;
+  if (tid < 8) s_in[kConvC * kConvH * kConvLd + tid] = 0.f;
+  for (int i = tid; i < kConvC * kConvH * (kConvLd - W); i += kFuseThreads)  // pad columns: finite
+    s_in[(i / (kConvLd - W)) * kConvLd + W + i % (kConvLd - W)] = 0.f;
+  for (int i = tid; i < kConvO * (kConvLd - Wo); i += kFuseThreads)  // g_pre pad columns: zero
+    s_g[(i / (kConvLd - Wo)) * kConvLd + Wo + i % (kConvLd - Wo)] = 0.f;
+  f32x4_t acc[kConvNT];
+#pragma unroll
+  for (int j = 0; j < kConvNT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  int boff[kConvNT];
+#pragma unroll
+  for (int j = 0; j < kConvNT; ++j) {
+    const int n = 16 * j + lo;
+    boff[j] = n < 108 ? (n / 3) * kConvLd + n % 3 : (n == 108 ? -1 : -2);
+  }
+  float gmx = 0.f, pb = 0.f;
+  // cube-gradient role; half is wave-uniform (W = 6 waves), so its weights are scalar loads
+  const int xp = tid % W, half = __builtin_amdgcn_readfirstlane(tid / W);
+  const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(B, b0 + per_block);
+  for (int64_t b = b0; b < b1; ++b) {
+    // (1) g_out / out of the molecule (12 x 382 contiguous floats each) as float4 pieces, head
+    // h's v rows and P; unconditional loads (a clamped last piece), predicated LDS stores
+    constexpr int kPieces = kConvO * Wo / 4;  // 1146
+    constexpr int kIt = (kPieces + kFuseThreads - 1) / kFuseThreads;
+    float4 gv[kIt], ov[kIt];
+    {
+      const float4* go = reinterpret_cast<const float4*>(g_out + b * (int64_t)(kConvO * Wo));
+      const float4* oo = reinterpret_cast<const float4*>(out + b * (int64_t)(kConvO * Wo));
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        const int i = min(tid + it * kFuseThreads, kPieces - 1);
+        gv[it] = go[i];
+        ov[it] = oo[i];
+      }
+    }
+    float v[NT][kDkVpl], p[NT][NT];
+#pragma unroll
+    for (int e = 0; e < NT * NT; ++e) p[e / NT][e % NT] = P[(b * H + h) * NT * NT + e];
+    load_rows3(pv + b * NT * ld + HD + (int64_t)h * W, ld, lane, v);
+    __syncthreads();  // the previous molecule's reads of the LDS are done
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int i = tid + it * kFuseThreads;
+      if (i < kPieces) {
+        const float ge[4] = {gv[it].x, gv[it].y, gv[it].z, gv[it].w};
+        const float oe[4] = {ov[it].x, ov[it].y, ov[it].z, ov[it].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = 4 * i + u, o = e / Wo;
+          s_g[o * kConvLd + e - o * Wo] = oe[u] > 0.f ? ge[u] : 0.f;
+        }
+      }
+    }
+    fold_att_lds(p, v, s_in + h * NT * kConvLd, lane);
+    __syncthreads();
+    // (2) weight / bias gradient
+#pragma unroll 2
+    for (int ks = 8 * h; ks < 8 * h + 8; ++ks) {
+      const int xx = 4 * ks + lk;
+      const float av = lo < kConvO ? s_g[lo * kConvLd + xx] : 0.f;  // 0 past Wo (padding)
+#pragma unroll
+      for (int j = 0; j < kConvNT; ++j) {
+        const float bv = boff[j] >= 0 ? s_in[boff[j] + xx] : (boff[j] == -1 ? 1.f : 0.f);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
+      }
+    }
+    {  // bias of channel h: this molecule's row sum (a wave reduction), then the running sum —
+       // short chains, where the ones column of the MFMA tile would chain ~10^3 terms per block
+       // over molecules whose sums cancel strongly
+      float sb = 0.f;
+#pragma unroll
+      for (int i = 0; i < kDkVpl; ++i) sb += s_g[h * kConvLd + lane + 64 * i];  // pads are 0
+      pb += wsum(sb);
+    }
+    // (3) the cube's gradient in registers; stored once every wave's phase-2 reads are done
+    float acc_in[kCD];
+    {
+      float g[kConvO][3];
+#pragma unroll
+      for (int o = 0; o < kConvO; ++o)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) g[o][dx] = xp - dx >= 0 ? s_g[o * kConvLd + xp - dx] : 0.f;
+#pragma unroll
+      for (int i = 0; i < kCD; ++i) acc_in[i] = 0.f;
+      // the weights as scalar loads issued per molecule: laundering the pointer keeps the
+      // compiler from hoisting all 648 of them out of the molecule loop (SGPR spills)
+      const float* wh = wgt + half * kCD * 3;
+      asm volatile("" : "+s"(wh));
+#pragma unroll
+      for (int o = 0; o < kConvO; ++o) {  // (o, dx) order as conv3_bwd2_kernel
+        const float* w = wh + o * (kConvC * kConvH * 3);
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int cd = 0; cd < kCD; ++cd) acc_in[cd] = fmaf(w[cd * 3 + dx], g[o][dx], acc_in[cd]);
+      }
+    }
+    // head h's query rows and the keys (register budget: not before phase 3)
+    float q[NT][kDkVpl], k[NT][kDkVpl];
+    load_rows3(pv + b * NT * ld + (int64_t)h * W, ld, lane, q);
+    load_rows3(x + b * NT * ldx, ldx, lane, k);
+    __syncthreads();
+#pragma unroll
+    for (int cd = 0; cd < kCD; ++cd) s_in[(half * kCD + cd) * kConvLd + xp] = acc_in[cd];
+    __syncthreads();
+    // (4) attention backward of head h (token_attn_fold_bwd_kernel's order); v and P are
+    // re-read (L2) rather than held through phases (2) and (3) (register budget)
+    {
+#pragma unroll
+      for (int e = 0; e < NT * NT; ++e) p[e / NT][e % NT] = P[(b * H + h) * NT * NT + e];
+      load_rows3(pv + b * NT * ld + HD + (int64_t)h * W, ld, lane, v);
+      float g[NT][kDkVpl];
+      load_rows3(s_in + h * NT * kConvLd, kConvLd, lane, g);
+      float gs[NT][NT];
+      fold_grad_scores(g, v, p, scale, gs);
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        float* grow = gpv + (b * NT + c) * ldg + HD + (int64_t)h * W;
+#pragma unroll
+        for (int i = 0; i < kDkVpl; ++i) {
+          float o = 0.f;
+#pragma unroll
+          for (int a = 0; a < NT; ++a) o = fmaf(p[a][c], g[a][i], o);
+          grow[lane + 64 * i] = o;
+          gmx = fmaxf(gmx, fabsf(o));
+        }
+      }
+      // the keys' gradient partial of head h goes over head h's own cube rows (read above by
+      // this wave only)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float* grow = gpv + (b * NT + t) * ldg + (int64_t)h * W;
+#pragma unroll
+        for (int i = 0; i < kDkVpl; ++i) {
+          float oq = 0.f, ok = 0.f;
+#pragma unroll
+          for (int c = 0; c < NT; ++c) {
+            oq = fmaf(gs[t][c], k[c][i], oq);
+            ok = fmaf(gs[c][t], q[c][i], ok);
+          }
+          grow[lane + 64 * i] = oq;
+          gmx = fmaxf(gmx, fabsf(oq));
+          s_in[(h * NT + t) * kConvLd + lane + 64 * i] = ok;
+        }
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < NT * W; e += kFuseThreads) {  // g_k = sum over heads in head order
+      const int t = e / W, c = e % W;
+      float s = 0.f;
+#pragma unroll
+      for (int hh = 0; hh < H; ++hh) s += s_in[(hh * NT + t) * kConvLd + c];
+      gk[(b * NT + t) * ldgk + c] = s;
+    }
+  }
+  if (gpv_amax) {  // one unsigned atomicMax of the float bits per wave
+    gmx = wave_max(gmx);
+    if (lane == 0) atomicMax(gpv_amax, __float_as_uint(gmx));
+  }
+  // fixed-order reduction of the twelve waves' 12 x 109 weight-gradient tiles (rows o < 12)
+  __syncthreads();
+  float* red = lds;  // 12 x 12 x 112 floats <= the LDS array
+  static_assert(kFuseWaves * kConvO * 112 <= kFuseCube + kFuseG, "reduction fits the LDS");
+#pragma unroll
+  for (int j = 0; j < kConvNT; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (4 * lk + r < kConvO) red[(h * kConvO + 4 * lk + r) * 112 + 16 * j + lo] = acc[j][r];
+  __syncthreads();
+  for (int i = tid; i < kConvO * 108; i += kFuseThreads) {
+    const int o = i / 108, n = i % 108;
+    float s = 0.f;
+    for (int w = 0; w < kFuseWaves; ++w) s += red[(w * kConvO + o) * 112 + n];
+    part[(int64_t)blockIdx.x * kConvPart + o * 108 + n] = s;
+  }
+  if (lane == 0) part[(int64_t)blockIdx.x * kConvPart + 2 * kConvWg + h] = pb;
+}
+
 // Fixed-order sum of the per-workgroup partials: out[i] = sum_blk sum_j<nsub
 // part[blk * stride + j * sub_stride + i].
 __global__ void partial_sum_kernel(int nblk, int count, int stride, int nsub, int sub_stride,
@@ -1021,6 +1365,57 @@ extern "C" int mvml_conv3_bwd(int64_t B, int C, int O, int W, const float* in, c
   if (rc) return rc;
   partial_sum_kernel<<<(unsigned)ceil_div(kConvWg, 256), 256, 0, st>>>(
       (int)used, kConvWg, kConvPart, nsub, kConvWg, part, g_weight);
+  rc = check_launch("partial_sum_kernel(w)");
+  if (rc) return rc;
+  partial_sum_kernel<<<1, 64, 0, st>>>((int)used, kConvO, kConvPart, 1, 0, part + 2 * kConvWg, g_bias);
+  return check_launch("partial_sum_kernel(b)");
+}
+
+static int64_t fused_blocks(int64_t B) { return std::min<int64_t>(B, 256); }  // 1 per CU
+
+extern "C" int mvml_attn_conv_fwd(int64_t B, int H, int dk, const float* pv, int64_t ld,
+                                  const float* x, int64_t ldx, float scale, const float* weight,
+                                  const float* bias, float* P, float* out, void* stream) {
+  clear_error();
+  MVML_REQUIRE(B >= 0 && H == kConvC && dk == 64 * kDkVpl && ld >= 2 * (int64_t)H * dk && ldx >= dk,
+               "attn_conv_fwd: H must be %d, dk %d, ld >= 2*H*dk, ldx >= dk", kConvC, 64 * kDkVpl);
+  if (B == 0) return MVML_OK;
+  const int64_t nblk = fused_blocks(B), per = ceil_div(B, nblk);
+  attn_conv_fwd_kernel<<<(unsigned)ceil_div(B, per), kFuseThreads, 0, as_stream(stream)>>>(
+      B, per, pv, ld, x, ldx, scale, weight, bias, P, out);
+  return check_launch("attn_conv_fwd_kernel");
+}
+
+extern "C" size_t mvml_attn_conv_bwd_workspace_size(int64_t B) {
+  return carve_size((size_t)fused_blocks(B > 0 ? B : 1) * kConvPart * sizeof(float));
+}
+
+extern "C" int mvml_attn_conv_bwd(int64_t B, int H, int dk, const float* pv, int64_t ld,
+                                  const float* x, int64_t ldx, float scale, const float* P,
+                                  const float* weight, const float* out, const float* g_out,
+                                  float* g_pv, int64_t ldg, float* g_k, int64_t ldgk,
+                                  uint32_t* g_pv_amax, float* g_weight, float* g_bias,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  MVML_REQUIRE(B >= 0 && H == kConvC && dk == 64 * kDkVpl && ld >= 2 * (int64_t)H * dk &&
+                   ldx >= dk && ldg >= 2 * (int64_t)H * dk && ldgk >= dk,
+               "attn_conv_bwd: H must be %d, dk %d, ld / ldg >= 2*H*dk, ldx / ldgk >= dk", kConvC,
+               64 * kDkVpl);
+  if (B == 0) return MVML_OK;
+  if (!workspace || workspace_bytes < mvml_attn_conv_bwd_workspace_size(B)) {
+    set_error("attn_conv_bwd: workspace of mvml_attn_conv_bwd_workspace_size bytes required");
+    return MVML_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  const int64_t nblk = fused_blocks(B), per = ceil_div(B, nblk);
+  const int64_t used = ceil_div(B, per);
+  float* part = static_cast<float*>(workspace);
+  attn_conv_bwd_kernel<<<(unsigned)used, kFuseThreads, 0, st>>>(
+      B, per, pv, ld, x, ldx, scale, P, weight, out, g_out, g_pv, ldg, g_k, ldgk, g_pv_amax, part);
+  int rc = check_launch("attn_conv_bwd_kernel");
+  if (rc) return rc;
+  partial_sum_kernel<<<(unsigned)ceil_div(kConvWg, 256), 256, 0, st>>>(
+      (int)used, kConvWg, kConvPart, 1, kConvWg, part, g_weight);
   rc = check_launch("partial_sum_kernel(w)");
   if (rc) return rc;
   partial_sum_kernel<<<1, 64, 0, st>>>((int)used, kConvO, kConvPart, 1, 0, part + 2 * kConvWg, g_bias);

@@ -64,6 +64,10 @@ class LinearFunction(torch.autograd.Function):
 # token GEMMs run over 2 H D columns (P, V) instead of 3 H D (Q, K, V) in the forward, the data
 # gradient and the weight gradient; False = the literal Q / K / V path (kept, tested).
 FOLD_QK = True
+# With FOLD_QK: the token attention and the Conv2d + ReLU run as ONE kernel each way
+# (mvml_attn_conv_fwd / _bwd), the (B, 12, 3, 384) attention cube never leaves LDS; False = the
+# separate mvml_token_attn_fold_* and mvml_conv3_* launches (kept, tested).
+FUSE_ATTN_CONV = True
 
 
 class FusionAttnConvFunction(torch.autograd.Function):
@@ -86,11 +90,13 @@ class FusionAttnConvFunction(torch.autograd.Function):
         rstd = torch.empty((3 * B,), **f32)
         call("mvml_layernorm_fwd", 3 * B, D, ptr(X), D, ptr(_c(ln_w)), ptr(_c(ln_b)), float(eps),
              ptr(Xn), D, ptr(mean), ptr(rstd), st)
-        att = torch.empty((B, H, 3, D), **f32)
         P = torch.empty((B, H, 3, 3), **f32)
         scale = 1.0 / math.sqrt(D)
         HD = H * D
         fold = FOLD_QK
+        fused = fold and FUSE_ATTN_CONV
+        att = None if fused else torch.empty((B, H, 3, D), **f32)
+        out = torch.empty((B, H, D - 2), **f32)
         if fold:
             wq3, wk3 = _c(wq).view(H, D, D), _c(wk).view(H, D, D)
             # Bcat [D, 2 H D] = [M_1 .. M_H | W_v^T]: M_h[i][j] = sum_o Wq_h[o][i] Wk_h[o][j]
@@ -99,8 +105,12 @@ class FusionAttnConvFunction(torch.autograd.Function):
             Bcat[:, HD:].copy_(_c(wv).t())  # parameter layout (7 MB), not a product
             PV = torch.empty((3 * B, 2 * HD), **f32)  # rows 3b+t: [x M_1 .. x M_H | x W_v^T]
             gemm(Xn, Bcat, 3 * B, 2 * HD, D, 0, 1, D, 2 * HD, PV, 2 * HD)
-            call("mvml_token_attn_fold_fwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
-                 ptr(att), ptr(P), st)
+            if fused:
+                call("mvml_attn_conv_fwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
+                     ptr(_c(conv_w)), ptr(_c(conv_b)), ptr(P), ptr(out), st)
+            else:
+                call("mvml_token_attn_fold_fwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
+                     ptr(att), ptr(P), st)
             saved = (Bcat, PV)
         else:
             Wqkv = torch.cat([_c(wq), _c(wk), _c(wv)], dim=0)  # (3 H D, D)
@@ -108,29 +118,30 @@ class FusionAttnConvFunction(torch.autograd.Function):
             gemm(Xn, Wqkv, 3 * B, 3 * HD, D, 0, 0, D, D, QKV, 3 * HD)
             call("mvml_token_attn_fwd", B, H, D, ptr(QKV), 3 * HD, float(scale), ptr(att), ptr(P), st)
             saved = (Wqkv, QKV)
-        out = torch.empty((B, H, D - 2), **f32)
-        call("mvml_conv3_fwd", B, H, H, D, ptr(att), ptr(_c(conv_w)), ptr(_c(conv_b)), ptr(out), st)
+        if not fused:
+            call("mvml_conv3_fwd", B, H, H, D, ptr(att), ptr(_c(conv_w)), ptr(_c(conv_b)), ptr(out), st)
         if _F.DEBUG_CAPTURE is not None:  # the ReLU sides the product took (parity tests)
             _F.DEBUG_CAPTURE["conv_out"] = out.detach()
         ctx.save_for_backward(X, Xn, mean, rstd, ln_w, wq, wk, wv, *saved, P, att, out, conv_w)
-        ctx.dims = (B, D, H, scale, fold)
+        ctx.dims = (B, D, H, scale, fold, fused)
         return out.view(B, H * (D - 2))
 
     @staticmethod
     def backward(ctx, g_out):
         X, Xn, mean, rstd, ln_w, wq, wk, wv, S0, S1, P, att, out, conv_w = ctx.saved_tensors
-        B, D, H, scale, fold = ctx.dims
+        B, D, H, scale, fold, fused = ctx.dims
         dev = X.device
         st = _stream(dev)
         f32 = dict(dtype=torch.float32, device=dev)
         L = _lib.lib()
         g_out = _c(g_out)
-        g_att = torch.empty_like(att)
         g_cw = torch.empty_like(conv_w)
         g_cb = torch.empty((H,), **f32)
-        wp, wn = _lib.ws_ptr_size(L.mvml_conv3_bwd_workspace_size(B), dev)
-        call("mvml_conv3_bwd", B, H, H, D, ptr(att), ptr(_c(conv_w)), ptr(out), ptr(g_out), ptr(g_att),
-             ptr(g_cw), ptr(g_cb), wp, wn, st)
+        if not fused:
+            g_att = torch.empty_like(att)
+            wp, wn = _lib.ws_ptr_size(L.mvml_conv3_bwd_workspace_size(B), dev)
+            call("mvml_conv3_bwd", B, H, H, D, ptr(att), ptr(_c(conv_w)), ptr(out), ptr(g_out),
+                 ptr(g_att), ptr(g_cw), ptr(g_cb), wp, wn, st)
         HD = H * D
         gXn = torch.empty((3 * B, D), **f32)
         if fold:
@@ -140,8 +151,14 @@ class FusionAttnConvFunction(torch.autograd.Function):
             if _F.GEMM_ALGO == "f16x2":  # split-fp16 maxima: gPV (folded by the kernel), Xn, Bcat
                 amx = torch.zeros(3, dtype=torch.int32, device=dev)
             # g_k (the keys' gradient, summed over heads) lands in gXn: the GEMMs add onto it
-            call("mvml_token_attn_fold_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
-                 ptr(P), ptr(g_att), ptr(gPV), 2 * HD, ptr(gXn), D, slot(amx, 0), st)
+            if fused:
+                wp, wn = _lib.ws_ptr_size(L.mvml_attn_conv_bwd_workspace_size(B), dev)
+                call("mvml_attn_conv_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
+                     ptr(P), ptr(_c(conv_w)), ptr(out), ptr(g_out), ptr(gPV), 2 * HD, ptr(gXn), D,
+                     slot(amx, 0), ptr(g_cw), ptr(g_cb), wp, wn, st)
+            else:
+                call("mvml_token_attn_fold_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
+                     ptr(P), ptr(g_att), ptr(gPV), 2 * HD, ptr(gXn), D, slot(amx, 0), st)
             if amx is not None:
                 absmax(Xn, 3 * B, D, D, amx, 1)
                 if _F.DEBUG_CAPTURE is not None:

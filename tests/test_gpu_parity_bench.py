@@ -228,6 +228,10 @@ def test_gnn_fusion_config3_bench_batch():
         f.load_state_dict(fref.state_dict())
         models[dt] = (r.to(DEV, dt).eval(), f.to(DEV, dt).eval())
     kinks = _Kinks()
+    # the oracle's nn.LSTM on the GPU would dispatch to MIOpen, whose RNN backward refuses eval
+    # mode: the native (aten) LSTM keeps the oracle's semantics and runs its backward in eval
+    nocudnn = torch.backends.cudnn.flags(enabled=False)
+    nocudnn.__enter__()
     z_r = torch.empty((n_mols, 11), dtype=torch.float64, device=DEV)
     gsx, gfx = {}, {}
     loss_r = {}
@@ -271,6 +275,7 @@ def test_gnn_fusion_config3_bench_batch():
                 for mod in (r.fc[0], f.conv[0], f.mlp[0]):
                     mod._forward_hooks.clear()
             del out, zc, lc
+    nocudnn.__exit__(None, None, None)
     (r64, f64), (r32, f32) = models[torch.float64], models[torch.float32]
     tensors = {"logits": {"err": _rel(z_p, z_r), "bar": TOL},
                "loss": {"err": abs(loss_p.item() - loss_r[torch.float64]) / abs(loss_r[torch.float64]),
