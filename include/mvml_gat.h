@@ -56,6 +56,8 @@ const char* mvml_version(void);
                                    workgroups looping over tiles (default 0: one per tile) */
 #define MVML_OPT_GEMM_NSPLIT 4  /* MVML_GEMM_NSPLIT: 1 (default) N = 256 q + r products as two
                                    launches, 0 = one */
+#define MVML_OPT_GEMM_RING 5    /* MVML_GEMM_RING: 1 = split-fp16 256x256 products on the
+                                   LDS-DMA ring kernel, 0 (default) = the register-staged one */
 int mvml_set_option(int option, int value);
 int mvml_get_option(int option);
 

@@ -14,13 +14,11 @@ Cases (BASELINE.json configs):
   synth.Config3Set (1.75 M atoms, 5.41 M edges, 1024 GraphNorm groups of 64) through
   GNNModule -> MVFusion -> BCEWithLogits, forward and every gradient.
 
-Bar (north_star): 1e-5 norm-wise relative error (max |a - b| / max |b|) against float64 for
-every output and every gradient.  ONE named exception, measured here every run: the Set2Set
-LSTM bias gradients (CANCELLATION), whose sums cancel ~300-fold because GraphNorm's upstream
-gradient is mean-free over each group — there the bar is max(1e-5, 4 x e32), e32 being what the
-SAME oracle run in fp32 loses on that tensor, and the test also asserts e32 really is large
-there (the exception is a property of the batch, not of the kernels).  Every tensor's error and
-bar is written to gpurun_out/parity_margins/<case>.json (copied to profiles/r03_parity_margins.json).
+Bar (north_star): the flat 1e-5 norm-wise relative error (max |a - b| / max |b|) against
+float64 for every output and every gradient, no exception (at this size the Set2Set LSTM bias
+gradients, whose sums cancel in small batches, sit at 2.7e-6).  Every tensor's error, the
+bar and e32 (what the SAME oracle run in fp32 loses on that tensor) go to
+gpurun_out/parity_margins/<case>.json (copied to profiles/r03_parity_margins.json).
 
 Kinks: the product's own fp32 side of every LeakyReLU (GAT logits) and ReLU (GNNModule.fc,
 the fusion Conv2d and MLP) is captured from its outputs and the float64 oracle is evaluated on
@@ -45,7 +43,6 @@ DEV = "cuda:0"
 TOL = 1e-5
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT_DIR = os.environ.get("MVML_MARGINS_DIR", os.path.join(ROOT, "gpurun_out", "parity_margins"))
-CANCELLATION = {f"readout.lstm.bias_{k}_l{l}" for k in ("ih", "hh") for l in range(3)}
 H = 4
 
 
@@ -290,14 +287,10 @@ def test_gnn_fusion_config3_bench_batch():
                 continue
             e = _rel(p.grad, p64[n].grad)
             e32 = _rel(p32[n].grad, p64[n].grad)
-            bar = max(TOL, 4 * e32) if n in CANCELLATION and prefix == "gnn." else TOL
-            tensors[prefix + n] = {"err": e, "bar": bar, "e32": e32}
+            tensors[prefix + n] = {"err": e, "bar": TOL, "e32": e32}
     rec = {"case": "config3_bench_batch", "molecules": n_mols, "atoms": g.num_nodes(),
            "edges": g.num_edges(), "graphnorm_groups": n_mols // gs, "gemm_algo": Fn.GEMM_ALGO,
-           "cancellation_tensors": sorted(CANCELLATION), "tensors": tensors, "kinks": kinks.check()}
+           "tensors": tensors, "kinks": kinks.check()}
     _write("config3_bench_batch", rec)
     for n, t in tensors.items():
         assert t["err"] < t["bar"], (n, t)
-    # the named exception is a measured property of the batch: fp32 itself loses > 1e-6 there
-    for n in CANCELLATION:
-        assert tensors["gnn." + n]["e32"] > 1e-6, (n, tensors["gnn." + n])
