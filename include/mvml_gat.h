@@ -458,6 +458,38 @@ int mvml_bilstm_seq_bwd(int64_t T, int64_t B, int H, const int32_t* batch_sizes,
                         float* gg0, float* gg1, float* carry, void* stream);
 int mvml_bilstm_select_last(int64_t B, int64_t H, const int32_t* lens, const int32_t* pos,
                             float* out, float* fea, int dir, void* stream);
+/* Wide batches (B > 512, BASELINE config 4): one launch per time step for BOTH directions of a
+ * bidirectional layer (direction 0 at step t, direction 1 at T - 1 - t; M0 / M1 live rows).
+ *   fwd: gates_d = A_d W_d^T + gx_d + b_ih_d + b_hh_d, then the LSTM cell (nn.LSTM,
+ *        model.py:114-129): c_d, h_d (row stride ldh), act_d = [i | f | g | o] (gate-major).
+ *        W_d = W_hh_d with INTERLEAVED rows (row 4 j + q = gate q of unit j); gx_d the step's
+ *        input projection rows (gate-major, ld ldgx); A_d the previous step's h rows (ld lda),
+ *        K = 0 at the directions' first step (c_prev NULL).  Split-fp16 GEMM: amax_a = bits of a
+ *        bound of |h| (1.0), amax_w_d = bits of max |W_hh_d|.
+ *   bwd: dh = gout rows + gn_d W_hh_d (gn_d = the gate gradients of the step this one fed, its
+ *        first R_d rows; R_d = 0 at the directions' first backward step), then the cell
+ *        backward (mvml_lstm_cell_bwd's arithmetic): gg_d, carry_out_d = dL/dc_prev; gg_amax_d
+ *        is the running max |gg_d| (read as gn_d's split-fp16 scale, raised by the step).
+ *        wT_d = W_hh_d^T [D][4 D]; workspace mvml_bilstm_wide_step_bwd_workspace_size(max M, D). */
+int mvml_bilstm_wide_step_fwd(int64_t M0, int64_t M1, int D, int64_t K, const float* A0,
+                              const float* A1, int64_t lda, const float* W0, const float* W1,
+                              int64_t ldw, const float* gx0, const float* gx1, int64_t ldgx,
+                              const float* bih0, const float* bhh0, const float* bih1,
+                              const float* bhh1, const float* cprev0, const float* cprev1,
+                              float* c0, float* c1, float* h0, float* h1, int64_t ldh,
+                              float* act0, float* act1, const uint32_t* amax_a,
+                              const uint32_t* amax_w0, const uint32_t* amax_w1, void* stream);
+size_t mvml_bilstm_wide_step_bwd_workspace_size(int64_t M, int D);
+int mvml_bilstm_wide_step_bwd(int64_t M0, int64_t M1, int64_t R0, int64_t R1, int D,
+                              const float* gn0, const float* gn1, const float* wT0,
+                              const float* wT1, int64_t ldwT, const float* gout0,
+                              const float* gout1, int64_t ldgo, const float* act0,
+                              const float* act1, const float* c0, const float* c1,
+                              const float* cp0, const float* cp1, const float* carry_in0,
+                              const float* carry_in1, float* carry_out0, float* carry_out1,
+                              float* gg0, float* gg1, uint32_t* gg_amax0, uint32_t* gg_amax1,
+                              const uint32_t* amax_w0, const uint32_t* amax_w1, void* workspace,
+                              size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1004,13 +1004,74 @@ attn_conv_fwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
   }
 }
 
-// Backward of attn_conv_fwd per molecule: (1) g_pre = g_out (out > 0) into LDS and the cube
-// recomputed as P V into LDS, (2) the Conv2d weight / bias gradient on the matrix cores
-// (conv3_bwd2's MFMA steps, wave w the x-steps [8 w, 8 w + 8)), (3) the cube's gradient
-// (conv3_bwd2's VALU loop, threads t and t + 384 the (c, dy) rows [0, 18) / [18, 36) of column
-// t) written over the cube, (4) the attention backward of head h by wave h
-// (token_attn_fold_bwd): g_pv stores, the keys' gradient partial over its own cube rows, then
-// the twelve partials in head order.  All LDS in one array: [cube | g_pre].
+// Backward of attn_conv_fwd, one molecule per loop trip, its inputs prefetched one molecule
+// ahead by LDS-DMA (global_load_lds_dwordx4: no registers, the loads of molecule b + 1 fly
+// while molecule b computes):
+//   (A) wait for molecule b's staged g_out / out / v / P, barrier;
+//   (B) the cube recomputed as P v into LDS (wave h: head h);
+//   (C) Conv2d weight gradient on the matrix cores (conv3_bwd2's MFMA steps, wave w the x-steps
+//       [8 w, 8 w + 8)) and the bias row sums, g_pre = g_out (out > 0) read from the staged rows;
+//   (D) the cube's gradient (conv3_bwd2's VALU loop; threads t and t + 384 the (c, dy) rows
+//       [0, 18) / [18, 36) of column t) in registers; barrier, then the cube gradient is stored
+//       over the cube, each wave moves its head's v / P rows to registers, molecule b + 1's
+//       g_out / out start into their (now free) staging rows and the wave's query / key loads
+//       are issued; barrier, then molecule b + 1's v / P start;
+//   (E) the attention backward of head h (token_attn_fold_bwd): g_pv stores, the keys'
+//       gradient partial over head h's own cube rows, then the twelve partials in head order.
+// Staging (one __shared__ array): cube [36 x 385 + 8] | g_out [18 KB] | out [18 KB] | v [3 x
+// 4608] | P [108 + pad], each region a whole number of 1-KB DMA pieces.
+constexpr int kStG = 18;                       // 1-KB pieces of a molecule's g_out (4584 floats)
+constexpr int kStV = 54;                       // v: 3 rows x 4608 floats
+constexpr int kStVP = kStV + 1;                // + P (108 floats)
+constexpr int kOffG = ((kFuseCube * 4 + 1023) / 1024) * 256;  // float offsets of the regions
+constexpr int kOffO = kOffG + kStG * 256;
+constexpr int kOffV = kOffO + kStG * 256;
+constexpr int kOffP = kOffV + kStV * 256;
+constexpr int kBwdLds = kOffP + 256;
+static_assert(kBwdLds * 4 <= 160 * 1024, "backward staging fits the CU's LDS");
+static_assert(kConvO * (kFuseW - 2) <= kStG * 256, "g_out rows fit their staging");
+constexpr int kVPWaves = (kStVP + 4) / 5;  // waves issuing the v / P pieces, 5 each (11)
+
+__device__ __forceinline__ void glds16(const float* src, float* dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+// molecule b's g_out and out rows (contiguous 4584-float blocks) into their staging rows:
+// pieces h and h + 12 of each (18 pieces), lanes past the block re-read its last float4
+__device__ __forceinline__ void stage_go(const float* __restrict__ g_out, const float* __restrict__ out,
+                                         int64_t b, float* lds, int h, int lane) {
+  constexpr int n = kConvO * (kFuseW - 2);
+  const int64_t base = b * (int64_t)n;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int piece = h + kFuseWaves * k;
+    if (piece < kStG) {
+      const int off = min(piece * 256 + 4 * lane, n - 4);
+      glds16(g_out + base + off, lds + kOffG + piece * 256);
+      glds16(out + base + off, lds + kOffO + piece * 256);
+    }
+  }
+}
+
+// molecule b's v rows (3 x 4608 floats of pv at column H dk) and P (108 floats): wave h < 11
+// issues pieces 5 h .. 5 h + 4 of the 55
+__device__ __forceinline__ void stage_vp(const float* __restrict__ pv, int64_t ld,
+                                         const float* __restrict__ P, int64_t b, float* lds, int h,
+                                         int lane) {
+  constexpr int64_t HD = (int64_t)kConvC * kFuseW;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int piece = 5 * h + k;
+    if (piece < kStV) {
+      const int t = piece / 18, c = (piece % 18) * 256 + 4 * lane;
+      glds16(pv + (b * NT + t) * ld + HD + c, lds + kOffV + piece * 256);
+    } else if (piece == kStV) {
+      glds16(P + b * (kConvC * NT * NT) + min(4 * lane, kConvC * NT * NT - 4), lds + kOffP);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kFuseThreads, 3)  // one workgroup per CU
 attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv, int64_t ld,
                      const float* __restrict__ x, int64_t ldx, float scale,
@@ -1021,16 +1082,17 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
   constexpr int W = kFuseW, Wo = W - 2, H = kConvC;
   constexpr int64_t HD = (int64_t)H * W;
   constexpr int kCD = kConvC * kConvH / 2;  // cube-gradient rows per thread
-  __shared__ float lds[kFuseCube + kFuseG];
+  __shared__ __attribute__((aligned(16))) float lds[kBwdLds];
   float* s_in = lds;
-  float* s_g = lds + kFuseCube;
-  const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
+  const float* s_o = lds + kOffO;
+  const float* s_v = lds + kOffV;   // [3][12 x 384]
+  const float* s_p = lds + kOffP;   // [12][9]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int h = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
   const int lo = lane & 15, lk = lane >> 4;
   if (tid < 8) s_in[kConvC * kConvH * kConvLd + tid] = 0.f;
   for (int i = tid; i < kConvC * kConvH * (kConvLd - W); i += kFuseThreads)  // pad columns: finite
     s_in[(i / (kConvLd - W)) * kConvLd + W + i % (kConvLd - W)] = 0.f;
-  for (int i = tid; i < kConvO * (kConvLd - Wo); i += kFuseThreads)  // g_pre pad columns: zero
-    s_g[(i / (kConvLd - Wo)) * kConvLd + Wo + i % (kConvLd - Wo)] = 0.f;
   f32x4_t acc[kConvNT];
 #pragma unroll
   for (int j = 0; j < kConvNT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -1040,73 +1102,65 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
     const int n = 16 * j + lo;
     boff[j] = n < 108 ? (n / 3) * kConvLd + n % 3 : (n == 108 ? -1 : -2);
   }
+  // g_pre[o][x] (masked in place over the staged g_out rows at (A)); 0 outside [0, Wo), by
+  // select on an always-in-range address (no branch around the LDS read)
+  float* s_gp = lds + kOffG;
+  auto gpre = [&](int o, int xx) -> float {
+    const float v = s_gp[o * Wo + min(max(xx, 0), Wo - 1)];
+    return (xx >= 0 && xx < Wo) ? v : 0.f;
+  };
   float gmx = 0.f, pb = 0.f;
   // cube-gradient role; half is wave-uniform (W = 6 waves), so its weights are scalar loads
   const int xp = tid % W, half = __builtin_amdgcn_readfirstlane(tid / W);
   const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(B, b0 + per_block);
+  if (b0 < b1) {
+    stage_go(g_out, out, b0, lds, h, lane);
+    if (h < kVPWaves) stage_vp(pv, ld, P, b0, lds, h, lane);
+  }
   for (int64_t b = b0; b < b1; ++b) {
-    // (1) g_out / out of the molecule (12 x 382 contiguous floats each) as float4 pieces, head
-    // h's v rows and P; unconditional loads (a clamped last piece), predicated LDS stores
-    constexpr int kPieces = kConvO * Wo / 4;  // 1146
-    constexpr int kIt = (kPieces + kFuseThreads - 1) / kFuseThreads;
-    float4 gv[kIt], ov[kIt];
+    const bool next = b + 1 < b1;
+    // (A) molecule b's staging landed (this wave's pieces; the barrier: everyone's); then
+    // g_pre = g_out (out > 0) in place
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int e = tid; e < kConvO * Wo; e += kFuseThreads) s_gp[e] = s_o[e] > 0.f ? s_gp[e] : 0.f;
+    // (B) the cube rows of head h
     {
-      const float4* go = reinterpret_cast<const float4*>(g_out + b * (int64_t)(kConvO * Wo));
-      const float4* oo = reinterpret_cast<const float4*>(out + b * (int64_t)(kConvO * Wo));
+      float p[NT][NT], v[NT][kDkVpl];
 #pragma unroll
-      for (int it = 0; it < kIt; ++it) {
-        const int i = min(tid + it * kFuseThreads, kPieces - 1);
-        gv[it] = go[i];
-        ov[it] = oo[i];
-      }
+      for (int e = 0; e < NT * NT; ++e) p[e / NT][e % NT] = s_p[h * NT * NT + e];
+      load_rows3(s_v + (int64_t)h * W, HD, lane, v);
+      fold_att_lds(p, v, s_in + h * NT * kConvLd, lane);
     }
-    float v[NT][kDkVpl], p[NT][NT];
-#pragma unroll
-    for (int e = 0; e < NT * NT; ++e) p[e / NT][e % NT] = P[(b * H + h) * NT * NT + e];
-    load_rows3(pv + b * NT * ld + HD + (int64_t)h * W, ld, lane, v);
-    __syncthreads();  // the previous molecule's reads of the LDS are done
-#pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-      const int i = tid + it * kFuseThreads;
-      if (i < kPieces) {
-        const float ge[4] = {gv[it].x, gv[it].y, gv[it].z, gv[it].w};
-        const float oe[4] = {ov[it].x, ov[it].y, ov[it].z, ov[it].w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = 4 * i + u, o = e / Wo;
-          s_g[o * kConvLd + e - o * Wo] = oe[u] > 0.f ? ge[u] : 0.f;
-        }
-      }
-    }
-    fold_att_lds(p, v, s_in + h * NT * kConvLd, lane);
     __syncthreads();
-    // (2) weight / bias gradient
+    __builtin_amdgcn_sched_barrier(0);
+    // (C) weight / bias gradient
 #pragma unroll 2
     for (int ks = 8 * h; ks < 8 * h + 8; ++ks) {
       const int xx = 4 * ks + lk;
-      const float av = lo < kConvO ? s_g[lo * kConvLd + xx] : 0.f;  // 0 past Wo (padding)
+      const float av = lo < kConvO ? gpre(lo, xx) : 0.f;
 #pragma unroll
       for (int j = 0; j < kConvNT; ++j) {
         const float bv = boff[j] >= 0 ? s_in[boff[j] + xx] : (boff[j] == -1 ? 1.f : 0.f);
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
       }
     }
-    {  // bias of channel h: this molecule's row sum (a wave reduction), then the running sum —
-       // short chains, where the ones column of the MFMA tile would chain ~10^3 terms per block
-       // over molecules whose sums cancel strongly
+    {  // bias of channel h: this molecule's row sum, then the running sum (short chains)
       float sb = 0.f;
 #pragma unroll
-      for (int i = 0; i < kDkVpl; ++i) sb += s_g[h * kConvLd + lane + 64 * i];  // pads are 0
+      for (int i = 0; i < kDkVpl; ++i) sb += gpre(h, lane + 64 * i);
       pb += wsum(sb);
     }
-    // (3) the cube's gradient in registers; stored once every wave's phase-2 reads are done
+    __builtin_amdgcn_sched_barrier(0);  // phases stay apart (registers)
+    // (D) the cube's gradient in registers
     float acc_in[kCD];
     {
+      int xpl = xp;  // laundered per molecule: the 36 row addresses are not hoisted out of the loop
+      asm volatile("" : "+v"(xpl));
       float g[kConvO][3];
 #pragma unroll
       for (int o = 0; o < kConvO; ++o)
 #pragma unroll
-        for (int dx = 0; dx < 3; ++dx) g[o][dx] = xp - dx >= 0 ? s_g[o * kConvLd + xp - dx] : 0.f;
+        for (int dx = 0; dx < 3; ++dx) g[o][dx] = gpre(o, xpl - dx);
 #pragma unroll
       for (int i = 0; i < kCD; ++i) acc_in[i] = 0.f;
       // the weights as scalar loads issued per molecule: laundering the pointer keeps the
@@ -1122,20 +1176,26 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
           for (int cd = 0; cd < kCD; ++cd) acc_in[cd] = fmaf(w[cd * 3 + dx], g[o][dx], acc_in[cd]);
       }
     }
-    // head h's query rows and the keys (register budget: not before phase 3)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every staged-row / cube read done
+#pragma unroll
+    for (int cd = 0; cd < kCD; ++cd) s_in[(half * kCD + cd) * kConvLd + xp] = acc_in[cd];
+    float v[NT][kDkVpl], p[NT][NT];
+#pragma unroll
+    for (int e = 0; e < NT * NT; ++e) p[e / NT][e % NT] = s_p[h * NT * NT + e];
+    load_rows3(s_v + (int64_t)h * W, HD, lane, v);
+    if (next) stage_go(g_out, out, b + 1, lds, h, lane);  // after the stores: registers
+    // head h's query rows and the keys (plain loads: the compiler's wait at their first use
+    // also covers the LDS-DMA pieces issued before it, so the next molecule's staging and these
+    // loads share one memory latency)
     float q[NT][kDkVpl], k[NT][kDkVpl];
     load_rows3(pv + b * NT * ld + (int64_t)h * W, ld, lane, q);
     load_rows3(x + b * NT * ldx, ldx, lane, k);
-    __syncthreads();
-#pragma unroll
-    for (int cd = 0; cd < kCD; ++cd) s_in[(half * kCD + cd) * kConvLd + xp] = acc_in[cd];
-    __syncthreads();
-    // (4) attention backward of head h (token_attn_fold_bwd_kernel's order); v and P are
-    // re-read (L2) rather than held through phases (2) and (3) (register budget)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // cube gradient stored; v / P read
+    if (next && h < kVPWaves) stage_vp(pv, ld, P, b + 1, lds, h, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    // (E) attention backward of head h (token_attn_fold_bwd_kernel's order)
     {
-#pragma unroll
-      for (int e = 0; e < NT * NT; ++e) p[e / NT][e % NT] = P[(b * H + h) * NT * NT + e];
-      load_rows3(pv + b * NT * ld + HD + (int64_t)h * W, ld, lane, v);
       float g[NT][kDkVpl];
       load_rows3(s_in + h * NT * kConvLd, kConvLd, lane, g);
       float gs[NT][NT];
@@ -1171,7 +1231,7 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
         }
       }
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     for (int e = tid; e < NT * W; e += kFuseThreads) {  // g_k = sum over heads in head order
       const int t = e / W, c = e % W;
       float s = 0.f;
@@ -1185,9 +1245,9 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
     if (lane == 0) atomicMax(gpv_amax, __float_as_uint(gmx));
   }
   // fixed-order reduction of the twelve waves' 12 x 109 weight-gradient tiles (rows o < 12)
-  __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   float* red = lds;  // 12 x 12 x 112 floats <= the LDS array
-  static_assert(kFuseWaves * kConvO * 112 <= kFuseCube + kFuseG, "reduction fits the LDS");
+  static_assert(kFuseWaves * kConvO * 112 <= kBwdLds, "reduction fits the LDS");
 #pragma unroll
   for (int j = 0; j < kConvNT; ++j)
 #pragma unroll

@@ -338,6 +338,21 @@ struct CellEpi {
   float* act = nullptr;           // [M][4 D]
   int64_t ldh = 0, ldh2 = 0;
   int D = 0;
+  const float* gx = nullptr;  // [M][4 D] gate-major addend (a BiLSTM step's input projection), or null
+  int64_t ldgx = 0;
+};
+
+// A second, independent product in the same launch (blockIdx.z == 1): its own A, B, row count,
+// split-K slab, B maximum and LSTM-cell epilogue pointers; K, the leading dimensions and the
+// column count are shared.  Both directions of a BiLSTM step run as one launch this way.
+struct DualPtrs {
+  const float* a = nullptr;
+  const float* b = nullptr;
+  float* slab = nullptr;
+  const uint32_t* amax_b = nullptr;
+  int64_t m = 0;
+  CellEpi cep;
+  const uint32_t* amax_a = nullptr;  // null: the first product's A maximum
 };
 __device__ __forceinline__ float sigm_epi(float x) { return 1.f / (1.f + expf(-x)); }
 
@@ -944,6 +959,10 @@ __device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], floa
       if (cep.D > 0) {  // LSTM cell (host: N = 4 D, no split-K): one unit's four gates
         const int D = cep.D;
         const int64_t j = col >> 2;
+        if (cep.gx) {  // (h W^T + x W_ih^T) first, as the GEMM's beta = 1 onto the projection
+          const float* gxr = cep.gx + row * cep.ldgx + j;
+          v.x += gxr[0]; v.y += gxr[D]; v.z += gxr[2 * D]; v.w += gxr[3 * D];
+        }
         const float gi = v.x + cep.b_ih[j] + cep.b_hh[j];
         const float gf = v.y + cep.b_ih[D + j] + cep.b_hh[D + j];
         const float gg = v.z + cep.b_ih[2 * D + j] + cep.b_hh[2 * D + j];
@@ -1039,11 +1058,20 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
                 float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{},
                 BatchStrides bst = BatchStrides{}, CellEpi cep = CellEpi{},
-                AmaxPtrs amax = AmaxPtrs{}) {
+                AmaxPtrs amax = AmaxPtrs{}, DualPtrs dual = DualPtrs{}) {
   if (blockIdx.z) {  // strided batch
     A += blockIdx.z * bst.a;
     B += blockIdx.z * bst.b;
     C += blockIdx.z * bst.c;
+  }
+  if (blockIdx.z == 1 && dual.a) {  // the second product of a dual launch
+    A = dual.a;
+    B = dual.b;
+    M = dual.m;
+    slab = dual.slab;
+    cep = dual.cep;
+    amax.b = dual.amax_b;
+    if (dual.amax_a) amax.a = dual.amax_a;
   }
   using OA = XOp<AK, NP>;
   using OB = XOp<BKM, NP>;
@@ -2287,4 +2315,147 @@ extern "C" int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx
   colsum_partial_kernel<<<g1, 256, 0, st>>>(M, N, X, ldx, rows_per, part);
   colsum_final_kernel<<<(unsigned)ceil_div(N, 256), 256, 0, st>>>(N, S, part, alpha, beta, out);
   return check_launch("colsum");
+}
+
+// ---- wide-batch BiLSTM steps (MVP's RNNModule at B > 512; BASELINE config 4) ---------------
+// The recurrence of a bidirectional nn.LSTM layer (model.py:114-129) over a batch of thousands
+// of sequences: one launch per time step for BOTH directions (direction 0 at t, direction 1 at
+// T - 1 - t; a dual launch, blockIdx.z = direction) instead of a GEMM and a cell kernel per
+// direction.
+namespace {
+struct LstmBwdArgs {
+  int64_t M = 0, R = 0;             // rows of the step; rows fed a recurrent gradient (prefix)
+  const float* gout = nullptr;      // dL/dh of the step's output rows (row stride ldgo)
+  int64_t ldgo = 0;
+  const float* slab = nullptr;      // [2][R][D] split-K halves of gg_next W_hh
+  const float* act = nullptr;       // [M][4D] i, f, g, o (gate-major)
+  const float* c = nullptr;         // [M][D]
+  const float* c_prev = nullptr;    // [M][D] or null (the direction's first step)
+  const float* carry_in = nullptr;  // [M][D] dL/dc from the step this one fed, or null
+  float* carry_out = nullptr;       // [M][D]
+  float* gg = nullptr;              // [M][4D] gate gradients (gate-major)
+  uint32_t* gg_amax = nullptr;      // running max |gg| bits (split-fp16 scale of the next GEMMs)
+};
+
+// dh = (gg_next W_hh)[row] (the two split-K halves, in order) + dL/dh of the output, then
+// lstm_cell_bwd_kernel's arithmetic in its order.
+__global__ void __launch_bounds__(256) lstm_step_bwd_kernel(LstmBwdArgs a0, LstmBwdArgs a1, int D) {
+  const LstmBwdArgs a = blockIdx.z ? a1 : a0;
+  const int64_t total = a.M * D;
+  float mx = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = e / D;
+    const int d = (int)(e - b * D);
+    float gh = a.gout[b * a.ldgo + d];
+    if (b < a.R) gh = (a.slab[e] + a.slab[a.R * D + e]) + gh;
+    const float* ac = a.act + b * 4 * D;
+    const float i = ac[d], f = ac[D + d], gt = ac[2 * D + d], o = ac[3 * D + d];
+    const float tc = tanhf(a.c[e]);
+    const float gc = (a.carry_in ? a.carry_in[e] : 0.f) + gh * o * (1.f - tc * tc);
+    const float cp = a.c_prev ? a.c_prev[e] : 0.f;
+    float* gg = a.gg + b * 4 * D;
+    const float g0 = gc * gt * i * (1.f - i), g1 = gc * cp * f * (1.f - f);
+    const float g2 = gc * i * (1.f - gt * gt), g3 = gh * tc * o * (1.f - o);
+    gg[d] = g0;
+    gg[D + d] = g1;
+    gg[2 * D + d] = g2;
+    gg[3 * D + d] = g3;
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(g0), fabsf(g1)), fmaxf(fabsf(g2), fabsf(g3))));
+    a.carry_out[e] = gc * f;
+  }
+  mx = wave_max(mx);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(a.gg_amax, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+}  // namespace
+
+extern "C" int mvml_bilstm_wide_step_fwd(
+    int64_t M0, int64_t M1, int D, int64_t K, const float* A0, const float* A1, int64_t lda,
+    const float* W0, const float* W1, int64_t ldw, const float* gx0, const float* gx1,
+    int64_t ldgx, const float* bih0, const float* bhh0, const float* bih1, const float* bhh1,
+    const float* cprev0, const float* cprev1, float* c0, float* c1, float* h0, float* h1,
+    int64_t ldh, float* act0, float* act1, const uint32_t* amax_a, const uint32_t* amax_w0,
+    const uint32_t* amax_w1, void* stream) {
+  clear_error();
+  const int64_t N = 4 * (int64_t)D;
+  MVML_REQUIRE(M0 > 0 && M1 > 0 && D > 0 && K >= 0 && K % 4 == 0 && ldw >= K && ldw % 4 == 0 &&
+                   ldgx >= N && ldh >= D && amax_a && amax_w0 && amax_w1 && MVML_X3W_LDSEPI,
+               "bilstm_wide_step_fwd: bad shape");
+  MVML_REQUIRE(K == 0 || (A0 && A1 && lda >= K && lda % 4 == 0 && (uintptr_t)A0 % 16 == 0 &&
+                          (uintptr_t)A1 % 16 == 0),
+               "bilstm_wide_step_fwd: A rows must be 16-B aligned");
+  MVML_REQUIRE((uintptr_t)W0 % 16 == 0 && (uintptr_t)W1 % 16 == 0, "bilstm_wide_step_fwd: W alignment");
+  CellEpi e0, e1;
+  e0.b_ih = bih0; e0.b_hh = bhh0; e0.c_prev = cprev0; e0.c_out = c0; e0.h_out = h0; e0.act = act0;
+  e0.ldh = ldh; e0.D = D; e0.gx = gx0; e0.ldgx = ldgx;
+  e1 = e0;
+  e1.b_ih = bih1; e1.b_hh = bhh1; e1.c_prev = cprev1; e1.c_out = c1; e1.h_out = h1; e1.act = act1;
+  e1.gx = gx1;
+  const int64_t tn = ceil_div(N, XBN);
+  const int64_t tiles = std::max(ceil_div(M0, XBM), ceil_div(M1, XBM)) * tn;
+  const dim3 grid((unsigned)tiles, 1, 2);
+  const float* a0 = K ? A0 : gx0;  // K = 0 (a direction's first step): no A rows are read
+  const float* a1 = K ? A1 : gx1;
+  gemm_x3w_kernel<false, false, -1, true, 2><<<grid, kXThreads, 0, as_stream(stream)>>>(
+      M0, N, K, a0, K ? lda : 4, W0, ldw, nullptr, 0.f, 0, nullptr, N, K > 0 ? K : 1, nullptr, 1, 1,
+      ProjEpi{}, BatchStrides{}, e0, AmaxPtrs{amax_a, amax_w0}, DualPtrs{a1, W1, nullptr, amax_w1, M1, e1});
+  return check_launch("gemm_x3w_kernel(bilstm step)");
+}
+
+extern "C" size_t mvml_bilstm_wide_step_bwd_workspace_size(int64_t M, int D) {
+  return 2 * carve_size((size_t)2 * M * D * sizeof(float));
+}
+
+extern "C" int mvml_bilstm_wide_step_bwd(
+    int64_t M0, int64_t M1, int64_t R0, int64_t R1, int D, const float* gn0, const float* gn1,
+    const float* wT0, const float* wT1, int64_t ldwT, const float* gout0, const float* gout1,
+    int64_t ldgo, const float* act0, const float* act1, const float* c0, const float* c1,
+    const float* cp0, const float* cp1, const float* carry_in0, const float* carry_in1,
+    float* carry_out0, float* carry_out1, float* gg0, float* gg1, uint32_t* gg_amax0,
+    uint32_t* gg_amax1, const uint32_t* amax_w0, const uint32_t* amax_w1, void* workspace,
+    size_t workspace_bytes, void* stream) {
+  clear_error();
+  const int64_t K = 4 * (int64_t)D, N = D;
+  MVML_REQUIRE(M0 > 0 && M1 > 0 && R0 >= 0 && R0 <= M0 && R1 >= 0 && R1 <= M1 && (R0 > 0) == (R1 > 0) &&
+                   D > 0 && D % 4 == 0 && ldwT >= K && ldwT % 4 == 0 && ldgo >= D && gg_amax0 &&
+                   gg_amax1 && amax_w0 && amax_w1,
+               "bilstm_wide_step_bwd: bad shape");
+  const int64_t M = std::max(M0, M1);
+  MVML_REQUIRE(workspace && workspace_bytes >= mvml_bilstm_wide_step_bwd_workspace_size(M, D),
+               "bilstm_wide_step_bwd: workspace of mvml_bilstm_wide_step_bwd_workspace_size bytes required");
+  hipStream_t st = as_stream(stream);
+  float* slab0 = static_cast<float*>(workspace);
+  float* slab1 = reinterpret_cast<float*>(static_cast<char*>(workspace) + carve_size((size_t)2 * M * D * sizeof(float)));
+  if (R0 > 0) {  // dL/dh through the recurrence: gg_next W_hh, K split in two halves (slabs)
+    MVML_REQUIRE(gn0 && gn1 && (uintptr_t)gn0 % 16 == 0 && (uintptr_t)gn1 % 16 == 0 &&
+                     (uintptr_t)wT0 % 16 == 0 && (uintptr_t)wT1 % 16 == 0,
+                 "bilstm_wide_step_bwd: alignment");
+    const int S = 2;
+    const int64_t kc = k_chunk(K, S);
+    const int64_t tiles = std::max(ceil_div(R0, XBM), ceil_div(R1, XBM)) * ceil_div(N, XBN);
+    const dim3 grid((unsigned)tiles, (unsigned)S, 2);
+    gemm_x3w_kernel<false, false, -1, true, 2><<<grid, kXThreads, 0, st>>>(
+        R0, N, K, gn0, K, wT0, ldwT, nullptr, 0.f, 0, nullptr, N, kc, slab0, 1, 1, ProjEpi{},
+        BatchStrides{}, CellEpi{}, AmaxPtrs{gg_amax0, amax_w0},
+        DualPtrs{gn1, wT1, slab1, amax_w1, R1, CellEpi{}, gg_amax1});
+    int rc = check_launch("gemm_x3w_kernel(bilstm step bwd)");
+    if (rc) return rc;
+  }
+  LstmBwdArgs a0, a1;
+  a0.M = M0; a0.R = R0; a0.gout = gout0; a0.ldgo = ldgo; a0.slab = slab0; a0.act = act0; a0.c = c0;
+  a0.c_prev = cp0; a0.carry_in = R0 > 0 ? carry_in0 : nullptr; a0.carry_out = carry_out0; a0.gg = gg0;
+  a0.gg_amax = gg_amax0;
+  a1 = a0;
+  a1.M = M1; a1.R = R1; a1.gout = gout1; a1.slab = slab1; a1.act = act1; a1.c = c1; a1.c_prev = cp1;
+  a1.carry_in = R1 > 0 ? carry_in1 : nullptr; a1.carry_out = carry_out1; a1.gg = gg1;
+  a1.gg_amax = gg_amax1;
+  const int64_t work = M * D;
+  const unsigned blocks = (unsigned)std::min<int64_t>(std::max<int64_t>(256, ceil_div(work, 4096)),
+                                                      ceil_div(work, 256));
+  lstm_step_bwd_kernel<<<dim3(blocks, 1, 2), 256, 0, st>>>(a0, a1, D);
+  return check_launch("lstm_step_bwd_kernel");
 }

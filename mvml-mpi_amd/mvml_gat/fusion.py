@@ -10,6 +10,7 @@ of model.py:72.  Parameter names / shapes equal MVP's, so ``MVP.state_dict()`` e
 ``bce_with_logits`` is main.py:91's BCEWithLogitsLoss.
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -67,7 +68,17 @@ FOLD_QK = True
 # With FOLD_QK: the token attention and the Conv2d + ReLU run as ONE kernel each way
 # (mvml_attn_conv_fwd / _bwd), the (B, 12, 3, 384) attention cube never leaves LDS; False = the
 # separate mvml_token_attn_fold_* and mvml_conv3_* launches (kept, tested).
-FUSE_ATTN_CONV = True
+FUSE_ATTN_CONV = os.environ.get("MVML_FUSE_ATTN_CONV", "1") != "0"
+
+
+def attn_conv_bytes(B, H, D, backward):
+    """Algorithmic HBM bytes of mvml_attn_conv_fwd / _bwd (fp32): the forward reads pv (3 rows
+    x 2 H D) and the keys (3 x D), writes P (H x 9) and the Conv2d output (H x (D - 2)) per
+    molecule; the backward reads pv, the keys, P, the output and its gradient, writes g_pv and
+    g_k.  The (H, 3, D) attention cube is on chip both ways (counted 0)."""
+    pv, keys, p, out = 3 * 2 * H * D, 3 * D, H * 9, H * (D - 2)
+    per = (pv + keys + p + out) if not backward else (2 * pv + 2 * keys + p + 2 * out)
+    return 4 * B * per
 
 
 class FusionAttnConvFunction(torch.autograd.Function):
@@ -106,6 +117,7 @@ class FusionAttnConvFunction(torch.autograd.Function):
             PV = torch.empty((3 * B, 2 * HD), **f32)  # rows 3b+t: [x M_1 .. x M_H | x W_v^T]
             gemm(Xn, Bcat, 3 * B, 2 * HD, D, 0, 1, D, 2 * HD, PV, 2 * HD)
             if fused:
+                _lib.call_tag[0] = {"bytes": attn_conv_bytes(B, H, D, False)}
                 call("mvml_attn_conv_fwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
                      ptr(_c(conv_w)), ptr(_c(conv_b)), ptr(P), ptr(out), st)
             else:
@@ -153,6 +165,7 @@ class FusionAttnConvFunction(torch.autograd.Function):
             # g_k (the keys' gradient, summed over heads) lands in gXn: the GEMMs add onto it
             if fused:
                 wp, wn = _lib.ws_ptr_size(L.mvml_attn_conv_bwd_workspace_size(B), dev)
+                _lib.call_tag[0] = {"bytes": attn_conv_bytes(B, H, D, True)}
                 call("mvml_attn_conv_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
                      ptr(P), ptr(_c(conv_w)), ptr(out), ptr(g_out), ptr(gPV), 2 * HD, ptr(gXn), D,
                      slot(amx, 0), ptr(g_cw), ptr(g_cb), wp, wn, st)

@@ -109,6 +109,10 @@ class Packing:
 
 
 SEQ_MAX_B = 512  # fused step path up to this batch width (the GEMM path above)
+# wider batches: one dual launch per time step (both directions, the LSTM cell in the GEMM
+# epilogue / a fused reduce + cell-backward kernel) on the split-fp16 GEMM; False = a GEMM and a
+# cell kernel per direction and step (kept, tested)
+WIDE_STEP = True
 SEQ_H = 384      # the fused step kernels are built for MVP's blstm_dim (config.py)
 
 
@@ -152,7 +156,29 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                  ptr(gates_d[1]), ptr(wc[1]), ptr(wc[5]), ptr(wc[2]), ptr(wc[3]), ptr(wc[6]),
                  ptr(wc[7]), ptr(out), ptr(c[0]), ptr(c[1]), ptr(act[0]), ptr(act[1]), st)
             saved = [c[0], act[0], c[1], act[1]]
-        else:  # wide batches: per-step MFMA GEMM (beta = 1 onto the projection) + cell kernel
+        elif WIDE_STEP and _h_bounds(w, dev) is not None:
+            # wide batches: one launch per time step for both directions, the recurrent product
+            # and the LSTM cell fused (mvml_bilstm_wide_step_fwd)
+            amx = _h_bounds(w, dev)
+            wperm = [_c(w[4 * d + 1]).view(4, H, H).transpose(0, 1).reshape(G, H).contiguous()
+                     for d in range(2)]  # rows 4 j + q = gate q of unit j
+            bias = [(_c(w[4 * d + 2]), _c(w[4 * d + 3])) for d in range(2)]
+            c = [torch.zeros((T, B, H), dtype=torch.float32, device=dev) for _ in range(2)]
+            act = [torch.empty((T, B, G), dtype=torch.float32, device=dev) for _ in range(2)]
+            for s in range(T):
+                t0, t1 = s, T - 1 - s
+                first = s == 0
+                p0, p1 = t0 - 1, t1 + 1
+                call("mvml_bilstm_wide_step_fwd", pk.batch_sizes[t0], pk.batch_sizes[t1], H,
+                     0 if first else H, None if first else ptr(out[p0, :, :H]),
+                     None if first else ptr(out[p1, :, H:]), 2 * H, ptr(wperm[0]), ptr(wperm[1]), H,
+                     ptr(gates_d[0][t0]), ptr(gates_d[1][t1]), G, ptr(bias[0][0]), ptr(bias[0][1]),
+                     ptr(bias[1][0]), ptr(bias[1][1]), None if first else ptr(c[0][p0]),
+                     None if first else ptr(c[1][p1]), ptr(c[0][t0]), ptr(c[1][t1]),
+                     ptr(out[t0, :, :H]), ptr(out[t1, :, H:]), 2 * H, ptr(act[0][t0]), ptr(act[1][t1]),
+                     slot(amx, 0), slot(amx, 1), slot(amx, 2), st)
+            saved = [c[0], act[0], c[1], act[1]]
+        else:  # wide batches, other GEMM algorithms: per-step GEMM (beta = 1 onto the projection) + cell kernel
             amx = _h_bounds(w, dev)
             for d in range(2):
                 w_hh, b_ih, b_hh = (_c(t) for t in w[4 * d + 1:4 * d + 4])
@@ -203,7 +229,29 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             # running max |dgates| per direction, folded in by mvml_lstm_cell_bwd (a bound for
             # every step already processed, which is all a scale needs)
             amg = torch.zeros(2, dtype=torch.int32, device=dev) if amx is not None else None
-        if not seq:  # wide batches: per-step recurrent GEMM (beta = 1 into g) + cell kernel
+        if not seq and WIDE_STEP and amx is not None:
+            # wide batches: one launch per step for both directions (the recurrent product split in
+            # two K halves) + one fused reduce / cell-backward launch (mvml_bilstm_wide_step_bwd)
+            carry = [[torch.zeros((B, H), dtype=torch.float32, device=dev) for _ in range(2)]
+                     for _ in range(2)]
+            nws = int(lib().mvml_bilstm_wide_step_bwd_workspace_size(B, H))
+            ws = workspace(nws, dev)
+            bsz = pk.batch_sizes
+            for s in range(T):
+                t0, t1 = T - 1 - s, s
+                n0, n1 = t0 + 1, t1 - 1  # the steps these fed
+                R0 = 0 if s == 0 else min(bsz[t0], bsz[n0])
+                R1 = 0 if s == 0 else min(bsz[t1], bsz[n1])
+                ci, co = s % 2, (s + 1) % 2
+                call("mvml_bilstm_wide_step_bwd", bsz[t0], bsz[t1], R0, R1, H,
+                     ptr(ggs[0][n0 if s else t0]), ptr(ggs[1][n1 if s else t1]), ptr(w_hhT[0]),
+                     ptr(w_hhT[1]), G, ptr(g[t0, :, :H]), ptr(g[t1, :, H:]), 2 * H, ptr(acts[0][t0]),
+                     ptr(acts[1][t1]), ptr(cs[0][t0]), ptr(cs[1][t1]),
+                     ptr(cs[0][t0 - 1]) if t0 >= 1 else None, ptr(cs[1][t1 + 1]) if t1 + 1 < T else None,
+                     ptr(carry[0][ci]), ptr(carry[1][ci]), ptr(carry[0][co]), ptr(carry[1][co]),
+                     ptr(ggs[0][t0]), ptr(ggs[1][t1]), slot(amg, 0), slot(amg, 1), slot(amx, 1),
+                     slot(amx, 2), ptr(ws), nws, st)
+        elif not seq:  # wide batches: per-step recurrent GEMM (beta = 1 into g) + cell kernel
             g = g.clone()
             for d in range(2):
                 c, act, gg = cs[d], acts[d], ggs[d]

@@ -31,11 +31,17 @@ def test_rnn_module_parity(B, Tmax, layers, ragged, space):
     _rnn_parity(B, Tmax, layers, ragged, space)
 
 
-@pytest.mark.parametrize("B,Tmax,layers,ragged,space", [(64, 60, 2, True, False), (24, 30, 2, True, True)])
-def test_rnn_module_parity_gemm_path(B, Tmax, layers, ragged, space, monkeypatch):
-    """The wide-batch path (per-step MFMA GEMM + cell kernels), forced at a small batch."""
+@pytest.mark.parametrize("wide_step", [True, False])
+@pytest.mark.parametrize("B,Tmax,layers,ragged,space", [(64, 60, 2, True, False), (24, 30, 2, True, True),
+                                                         (700, 25, 2, True, False)])
+def test_rnn_module_parity_gemm_path(B, Tmax, layers, ragged, space, wide_step, monkeypatch):
+    """The wide-batch paths, forced at small batches: wide_step = one dual launch per time step
+    for both directions with the cell fused (mvml_bilstm_wide_step_fwd / _bwd, the default);
+    False = a GEMM and a cell kernel per direction and step.  B = 700: three 256-row tiles with
+    a ragged last one, and the live-row prefix shrinking across tiles."""
     import mvml_gat.smiles as sm
     monkeypatch.setattr(sm, "SEQ_MAX_B", 0)
+    monkeypatch.setattr(sm, "WIDE_STEP", wide_step)
     _rnn_parity(B, Tmax, layers, ragged, space)
 
 
