@@ -479,6 +479,25 @@ int mvml_bilstm_wide_step_fwd(int64_t M0, int64_t M1, int D, int64_t K, const fl
                               float* c0, float* c1, float* h0, float* h1, int64_t ldh,
                               float* act0, float* act1, const uint32_t* amax_a,
                               const uint32_t* amax_w0, const uint32_t* amax_w1, void* stream);
+/* Live rows of a time-major [T, B, cols] buffer (row stride ld_tm) <-> consecutive packed rows
+ * (stride ld_pk): packed row offsets[k] + p <-> buffer row (t0 + k + shift) B + p for
+ * k < t_count, p < offsets[k + 1] - offsets[k] (int32 offsets[t_count + 1] on the device,
+ * nrows = offsets[t_count]).  dir 0 packs, 1 unpacks.  The wide path's products over every
+ * position run over the live rows only (pack_padded_sequence's data, model.py:125). */
+int mvml_bilstm_pack_rows(int64_t nrows, int64_t t_count, int64_t B, int64_t cols,
+                          const int32_t* offsets, int64_t t0, int shift, float* tm,
+                          int64_t ld_tm, float* packed, int64_t ld_pk, int dir, void* stream);
+/* Token of every packed live row (row offsets[t] + p = step t of sorted sequence p) and the
+ * embedding-side gradient out[v] = sum of g's packed rows with token v in packed order
+ * (mvml_bilstm_token_grad over the live rows only; workspace
+ * mvml_bilstm_token_grad_packed_workspace bytes). */
+int mvml_bilstm_packed_tokens(int64_t nrows, int64_t T, const int32_t* offsets,
+                              const int32_t* tokens, int64_t ldtok, const int32_t* perm,
+                              int32_t* tok, void* stream);
+int64_t mvml_bilstm_token_grad_packed_workspace(int64_t nrows, int64_t cols, int vocab);
+int mvml_bilstm_token_grad_packed(int64_t nrows, int64_t cols, const float* g, int64_t ldg,
+                                  const int32_t* tok, int vocab, float* out, void* workspace,
+                                  size_t workspace_bytes, void* stream);
 size_t mvml_bilstm_wide_step_bwd_workspace_size(int64_t M, int D);
 int mvml_bilstm_wide_step_bwd(int64_t M0, int64_t M1, int64_t R0, int64_t R1, int D,
                               const float* gn0, const float* gn1, const float* wT0,

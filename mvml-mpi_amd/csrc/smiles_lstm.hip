@@ -417,3 +417,141 @@ extern "C" int mvml_bilstm_select_last(int64_t B, int64_t H, const int32_t* lens
                                                                          fea, dir);
   return check_launch("bilstm_select_last");
 }
+
+// ---- packed rows (wide batches) ------------------------------------------------------------
+// The time-major [T, B, cols] buffers hold at step t only the live prefix of bs_t rows (the
+// batch sorted by descending length); the products over every position (input projections,
+// weight and input gradients) run over the N = sum_t bs_t live rows only: pack copies rows
+// (t + shift, p) for t in [t0, t1), p < bs_t, into consecutive packed rows (offsets[t - t0] =
+// sum_{t' < t} bs_t' over [t0, t)); unpack (dir 1) is the reverse copy.  A wave per row, float4.
+namespace mvml {
+namespace {
+__global__ void __launch_bounds__(256) pack_rows_kernel(int64_t nrows, int64_t t_count, int64_t B,
+                                                        int64_t cols4, const int32_t* __restrict__ offs,
+                                                        int64_t t0, int shift, float4* __restrict__ tm,
+                                                        int64_t ld_tm4, float4* __restrict__ pk,
+                                                        int64_t ld_pk4, int dir) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= nrows) return;
+  int64_t lo = 0, hi = t_count;  // the step of packed row r: offs[k] <= r < offs[k + 1]
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (offs[mid] <= r) lo = mid; else hi = mid;
+  }
+  const int64_t p = r - offs[lo];
+  float4* a = tm + ((t0 + lo + shift) * B + p) * ld_tm4;
+  float4* b = pk + r * ld_pk4;
+  for (int64_t c = lane; c < cols4; c += 64) {
+    if (dir == 0) b[c] = a[c];
+    else a[c] = b[c];
+  }
+}
+}  // namespace
+}  // namespace mvml
+
+extern "C" int mvml_bilstm_pack_rows(int64_t nrows, int64_t t_count, int64_t B, int64_t cols,
+                                     const int32_t* offsets, int64_t t0, int shift, float* tm,
+                                     int64_t ld_tm, float* packed, int64_t ld_pk, int dir,
+                                     void* stream) {
+  using namespace mvml;
+  clear_error();
+  MVML_REQUIRE(nrows >= 0 && t_count > 0 && B > 0 && cols > 0 && cols % 4 == 0 && ld_tm % 4 == 0 &&
+                   ld_pk % 4 == 0 && ld_tm >= cols && ld_pk >= cols && (dir == 0 || dir == 1) &&
+                   ((uintptr_t)tm & 15) == 0 && ((uintptr_t)packed & 15) == 0,
+               "bilstm_pack_rows: bad shape / alignment");
+  if (nrows == 0) return MVML_OK;
+  pack_rows_kernel<<<(unsigned)ceil_div(nrows, 4), 256, 0, as_stream(stream)>>>(
+      nrows, t_count, B, cols / 4, offsets, t0, shift, reinterpret_cast<float4*>(tm), ld_tm / 4,
+      reinterpret_cast<float4*>(packed), ld_pk / 4, dir);
+  return check_launch("pack_rows_kernel");
+}
+
+// ---- embedding / layer-0 input-projection gradient over the packed live rows ----------------
+// out[v, j] = sum of g[r, j] over the packed rows r whose token is v, r ascending (the packed
+// order: t ascending, then sorted row ascending, as token_grad_kernel): chunks of kTokPChunk rows
+// x 256-column slabs accumulate per token in LDS with 8 rows' loads in flight, then
+// token_grad_sum_kernel adds the chunks in order (deterministic, no atomics).
+namespace mvml {
+namespace {
+constexpr int kTokPChunk = 1024;
+__global__ void __launch_bounds__(256)
+token_grad_packed_kernel(int64_t nrows, int64_t cols, const float* __restrict__ g, int64_t ldg,
+                         const int32_t* __restrict__ tok, int vocab, float* __restrict__ part) {
+  __shared__ float s_acc[kTokMaxVocab][256];
+  const int tid = threadIdx.x;
+  const int64_t j = blockIdx.y * 256 + tid;
+  const int64_t jc = min(j, cols - 1);  // lanes past the last column read a valid one, store nothing
+  for (int v = 0; v < vocab; ++v) s_acc[v][tid] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * kTokPChunk, r1 = min<int64_t>(nrows, r0 + kTokPChunk);
+  int64_t r = r0;
+  for (; r + 8 <= r1; r += 8) {
+    float x[8];
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      x[u] = g[(r + u) * ldg + jc];
+      v[u] = tok[r + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s_acc[v[u]][tid] += x[u];  // one lane per column: no races
+  }
+  for (; r < r1; ++r) s_acc[tok[r]][tid] += g[r * ldg + jc];
+  if (j < cols)
+    for (int v = 0; v < vocab; ++v) part[((int64_t)blockIdx.x * vocab + v) * cols + j] = s_acc[v][tid];
+}
+
+// token of every packed live row: row offsets[t] + p is step t of sorted sequence p
+__global__ void packed_tokens_kernel(int64_t nrows, int64_t T, const int32_t* __restrict__ offs,
+                                     const int32_t* __restrict__ tokens, int64_t ldtok,
+                                     const int32_t* __restrict__ perm, int32_t* __restrict__ tok) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrows) return;
+  int64_t lo = 0, hi = T;
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (offs[mid] <= r) lo = mid; else hi = mid;
+  }
+  tok[r] = tokens[(int64_t)perm[r - offs[lo]] * ldtok + lo];
+}
+}  // namespace
+}  // namespace mvml
+
+extern "C" int mvml_bilstm_packed_tokens(int64_t nrows, int64_t T, const int32_t* offsets,
+                                         const int32_t* tokens, int64_t ldtok, const int32_t* perm,
+                                         int32_t* tok, void* stream) {
+  clear_error();
+  MVML_REQUIRE(nrows >= 0 && T > 0 && ldtok >= T, "bilstm_packed_tokens: bad shape");
+  if (nrows == 0) return MVML_OK;
+  packed_tokens_kernel<<<(unsigned)ceil_div(nrows, 256), 256, 0, as_stream(stream)>>>(
+      nrows, T, offsets, tokens, ldtok, perm, tok);
+  return check_launch("packed_tokens_kernel");
+}
+
+extern "C" int64_t mvml_bilstm_token_grad_packed_workspace(int64_t nrows, int64_t cols, int vocab) {
+  return ceil_div(nrows > 0 ? nrows : 1, kTokPChunk) * vocab * cols * (int64_t)sizeof(float);
+}
+
+extern "C" int mvml_bilstm_token_grad_packed(int64_t nrows, int64_t cols, const float* g,
+                                             int64_t ldg, const int32_t* tok, int vocab, float* out,
+                                             void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  MVML_REQUIRE(nrows >= 0 && cols > 0 && ldg >= cols && vocab > 0 && vocab <= kTokMaxVocab,
+               "bilstm_token_grad_packed: bad shape (vocab <= 64)");
+  MVML_REQUIRE(workspace && (int64_t)workspace_bytes >= mvml_bilstm_token_grad_packed_workspace(nrows, cols, vocab),
+               "bilstm_token_grad_packed: workspace too small");
+  hipStream_t st = as_stream(stream);
+  const int64_t nchunk = ceil_div(nrows > 0 ? nrows : 1, kTokPChunk);
+  float* part = static_cast<float*>(workspace);
+  if (nrows > 0) {
+    token_grad_packed_kernel<<<dim3((unsigned)nchunk, (unsigned)ceil_div(cols, 256)), 256, 0, st>>>(
+        nrows, cols, g, ldg, tok, vocab, part);
+    int rc = check_launch("token_grad_packed_kernel");
+    if (rc) return rc;
+  } else {
+    hipMemsetAsync(part, 0, (size_t)vocab * cols * sizeof(float), st);
+  }
+  const int64_t n = (int64_t)vocab * cols;
+  token_grad_sum_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(nchunk, n, part, out);
+  return check_launch("token_grad_sum_kernel");
+}

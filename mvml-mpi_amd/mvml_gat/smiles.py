@@ -106,9 +106,32 @@ class Packing:
         self.lens = torch.from_numpy(lens.astype(np.int32)).to(dev)
         self.perm = torch.from_numpy(perm.astype(np.int32)).to(dev)
         self.pos = torch.from_numpy(pos.astype(np.int32)).to(dev)
+        self._offs = {}
+
+    def packed_tokens(self):
+        """Device int32 token of every packed live row (mvml_bilstm_packed_tokens)."""
+        if getattr(self, "_ptok", None) is None:
+            offs, n = self.live_offsets(0, self.T)
+            self._ptok = torch.empty((max(n, 1),), dtype=torch.int32, device=self.lens.device)
+            call("mvml_bilstm_packed_tokens", n, self.T, ptr(offs), ptr(self.tokens), self.ldtok,
+                 ptr(self.perm), ptr(self._ptok), _stream(self.lens.device))
+        return self._ptok
+
+    def live_offsets(self, t0, t1):
+        """(device int32 offsets[t1 - t0 + 1], rows): the live rows of steps [t0, t1) packed
+        consecutively (mvml_bilstm_pack_rows)."""
+        key = (t0, t1)
+        if key not in self._offs:
+            o = np.concatenate([[0], np.cumsum(self.batch_sizes[t0:t1])]).astype(np.int32)
+            self._offs[key] = (torch.from_numpy(o).to(self.lens.device), int(o[-1]))
+        return self._offs[key]
 
 
 SEQ_MAX_B = 512  # fused step path up to this batch width (the GEMM path above)
+# wider batches: the products over every position (input projections, weight / input
+# gradients) run over the live rows of the packed sequence only (mvml_bilstm_pack_rows);
+# False = over all T x B rows (padding rows are zeros)
+WIDE_PACK = True
 # wider batches: one dual launch per time step (both directions, the LSTM cell in the GEMM
 # epilogue / a fused reduce + cell-backward kernel) on the split-fp16 GEMM; False = a GEMM and a
 # cell kernel per direction and step (kept, tested)
@@ -136,6 +159,8 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         In = x.shape[-1]
         out = torch.zeros((T, B, 2 * H), dtype=torch.float32, device=dev)
         saved, gates_d = [], []
+        wide_pack = WIDE_PACK and not _use_seq(pk, H) and In % 4 == 0
+        xp = None
         for d in range(2):
             w_ih = _c(w[4 * d])
             gates = torch.empty((T, B, G), dtype=torch.float32, device=dev)
@@ -145,6 +170,12 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                 gemm(x, w_ih, V, G, In, 0, 0, In, In, P, G)
                 call("mvml_bilstm_gather_rows", T, B, G, ptr(P), ptr(pk.tokens), pk.ldtok,
                      ptr(pk.lens), ptr(pk.perm), ptr(gates), st)
+            elif wide_pack:  # only the live rows (a third of T x B for KEGG-like lengths)
+                xp = _pack(pk, x, In, In) if d == 0 else xp
+                gp = torch.empty((xp.shape[0], G), dtype=torch.float32, device=dev)
+                gemm(xp, w_ih, xp.shape[0], G, In, 0, 0, In, In, gp, G)
+                _unpack(pk, gp, gates, G, G)
+                del gp
             else:
                 gemm(x, w_ih, T * B, G, In, 0, 0, In, In, gates, G)
             gates_d.append(gates)
@@ -271,35 +302,83 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                          ptr(g[t, :, d * H:]), 2 * H, ptr(g_c), ptr(gg[t]), ptr(carry[(k + 1) % 2]),
                          slot(amg, d), st)
                     nxt, k = t, k + 1
-        for d in range(2):  # weight / input gradients: GEMMs over all positions
+        # weight / input gradients: GEMMs over every position — on the wide path over the live
+        # rows only (packed), else over all T x B rows (the padding rows of gg are zeros)
+        packed = not seq and WIDE_PACK and In % 4 == 0
+        if packed:
+            offs, n_live = pk.live_offsets(0, T)
+            xp = None if layer0 else _pack(pk, x, In, In)
+            gxp = None if layer0 else torch.empty((n_live, In), dtype=torch.float32, device=dev)
+            g_x = g_x if layer0 else torch.zeros_like(x)
+        for d in range(2):
             w_ih, gg = _c(w[4 * d]), ggs[d]
             gb = torch.empty(G, dtype=torch.float32, device=dev)
-            colsum(gg, T * B, G, G, gb)
+            ggp = _pack(pk, gg, G, G) if packed else gg
+            rows = ggp.shape[0] if packed else T * B
+            colsum(ggp, rows, G, G, gb)
             g_whh = torch.zeros((G, H), dtype=torch.float32, device=dev)
             if T > 1:
-                A, Bm = (gg[1:], out[:-1, :, d * H:]) if d == 0 else (gg[:-1], out[1:, :, d * H:])
-                gemm(A, Bm, G, H, (T - 1) * B, 1, 1, G, 2 * H, g_whh, H,  # Bm = h: |h| < 1
-                     amax=None if amg is None else (slot(amg, d), slot(amx, 0)))
+                if packed:  # pairs (gg[t], h[t -+ 1]) of the live rows of gg
+                    t0, t1, sh = (1, T, -1) if d == 0 else (0, T - 1, 1)
+                    A = _pack(pk, gg, G, G, t0, t1)
+                    Bm = _pack(pk, out[:, :, d * H:], H, 2 * H, t0, t1, sh)
+                    gemm(A, Bm, G, H, A.shape[0], 1, 1, G, H, g_whh, H,  # Bm = h: |h| < 1
+                         amax=None if amg is None else (slot(amg, d), slot(amx, 0)))
+                    del A, Bm
+                else:
+                    A, Bm = (gg[1:], out[:-1, :, d * H:]) if d == 0 else (gg[:-1], out[1:, :, d * H:])
+                    gemm(A, Bm, G, H, (T - 1) * B, 1, 1, G, 2 * H, g_whh, H,  # Bm = h: |h| < 1
+                         amax=None if amg is None else (slot(amg, d), slot(amx, 0)))
             g_wih = torch.empty((G, In), dtype=torch.float32, device=dev)
             beta = 1.0 if d else 0.0
             if layer0:
                 V = x.shape[0]
                 Gt = torch.empty((V, G), dtype=torch.float32, device=dev)
-                nws = int(lib().mvml_bilstm_token_grad_workspace(T, B, G, V))
-                ws = workspace(nws, dev)
-                call("mvml_bilstm_token_grad", T, B, G, ptr(gg), ptr(pk.tokens), pk.ldtok,
-                     ptr(pk.lens), ptr(pk.perm), V, ptr(Gt), ptr(ws), nws, st)
+                if packed:  # over the live rows only
+                    nws = int(lib().mvml_bilstm_token_grad_packed_workspace(rows, G, V))
+                    ws = workspace(nws, dev)
+                    call("mvml_bilstm_token_grad_packed", rows, G, ptr(ggp), G, ptr(pk.packed_tokens()),
+                         V, ptr(Gt), ptr(ws), nws, st)
+                else:
+                    nws = int(lib().mvml_bilstm_token_grad_workspace(T, B, G, V))
+                    ws = workspace(nws, dev)
+                    call("mvml_bilstm_token_grad", T, B, G, ptr(gg), ptr(pk.tokens), pk.ldtok,
+                         ptr(pk.lens), ptr(pk.perm), V, ptr(Gt), ptr(ws), nws, st)
                 gemm(Gt, x, G, In, V, 1, 1, G, In, g_wih, In)
                 gemm(Gt, w_ih, V, In, G, 0, 1, G, In, g_x, In, beta=beta)
                 if d == 1 and pk.pad is not None:
                     # nn.Embedding(padding_idx=pad) (model.py:113): the padding row never
                     # receives a gradient, even where the pad token occurs inside a sequence
                     g_x[pk.pad].zero_()
+            elif packed:
+                gemm(ggp, xp, G, In, rows, 1, 1, G, In, g_wih, In)
+                gemm(ggp, w_ih, rows, In, G, 0, 1, G, In, gxp, In, beta=beta)
             else:
                 gemm(gg, x, G, In, T * B, 1, 1, G, In, g_wih, In)
                 gemm(gg, w_ih, T * B, In, G, 0, 1, G, In, g_x, In, beta=beta)
             g_w[4 * d:4 * d + 4] = [g_wih, g_whh, gb, gb.clone()]
+            del ggp
+        if packed and not layer0:
+            _unpack(pk, gxp, g_x, In, In)
         return (g_x, None, None, *g_w)
+
+
+def _pack(pk, tm, cols, ld, t0=0, t1=None, shift=0, out=None):
+    """Live rows (t + shift, p), t in [t0, t1), p < bs_t, of the time-major buffer tm (row
+    stride ld, first column at tm's pointer) -> a packed [rows, cols] tensor."""
+    t1 = pk.T if t1 is None else t1
+    offs, n = pk.live_offsets(t0, t1)
+    if out is None:
+        out = torch.empty((n, cols), dtype=torch.float32, device=tm.device)
+    call("mvml_bilstm_pack_rows", n, t1 - t0, pk.B, cols, ptr(offs), t0, shift, ptr(tm), ld,
+         ptr(out), out.stride(0), 0, _stream(tm.device))
+    return out
+
+
+def _unpack(pk, packed, tm, cols, ld):
+    offs, n = pk.live_offsets(0, pk.T)
+    call("mvml_bilstm_pack_rows", n, pk.T, pk.B, cols, ptr(offs), 0, 0, ptr(tm), ld, ptr(packed),
+         packed.stride(0), 1, _stream(tm.device))
 
 
 def _h_bounds(w, dev):

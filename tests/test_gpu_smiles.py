@@ -42,6 +42,7 @@ def test_rnn_module_parity_gemm_path(B, Tmax, layers, ragged, space, wide_step, 
     import mvml_gat.smiles as sm
     monkeypatch.setattr(sm, "SEQ_MAX_B", 0)
     monkeypatch.setattr(sm, "WIDE_STEP", wide_step)
+    monkeypatch.setattr(sm, "WIDE_PACK", wide_step)  # the live-row products with the step path
     _rnn_parity(B, Tmax, layers, ragged, space)
 
 
