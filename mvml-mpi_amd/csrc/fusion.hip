@@ -1030,7 +1030,15 @@ constexpr int kOffP = kOffV + kStV * 256;
 constexpr int kBwdLds = kOffP + 256;
 static_assert(kBwdLds * 4 <= 160 * 1024, "backward staging fits the CU's LDS");
 static_assert(kConvO * (kFuseW - 2) <= kStG * 256, "g_out rows fit their staging");
-constexpr int kVPWaves = (kStVP + 4) / 5;  // waves issuing the v / P pieces, 5 each (11)
+
+// a wave-uniform pointer held in SGPRs (so a global_load_lds takes the saddr + 32-bit lane
+// offset form instead of a 64-bit address per lane)
+__device__ __forceinline__ const float* uniform_ptr(const float* p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
+}
 
 __device__ __forceinline__ void glds16(const float* src, float* dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -1054,21 +1062,22 @@ __device__ __forceinline__ void stage_go(const float* __restrict__ g_out, const 
   }
 }
 
-// molecule b's v rows (3 x 4608 floats of pv at column H dk) and P (108 floats): wave h < 11
-// issues pieces 5 h .. 5 h + 4 of the 55
+// molecule b's v rows (3 x 4608 floats of pv at column H dk) and P (108 floats): wave h issues
+// pieces 5 h .. 5 h + 4 of the 55; wave 11's five (and nothing else) repeat the P piece — every
+// wave issues exactly five, so the compiler's wait for the query / key loads issued before them
+// is vmcnt(5), not a drain of the next molecule's staging
 __device__ __forceinline__ void stage_vp(const float* __restrict__ pv, int64_t ld,
                                          const float* __restrict__ P, int64_t b, float* lds, int h,
                                          int lane) {
   constexpr int64_t HD = (int64_t)kConvC * kFuseW;
+  const float* pb = uniform_ptr(P + b * (kConvC * NT * NT)) + min(4 * lane, kConvC * NT * NT - 4);
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
+  for (int k = 0; k < 5; ++k) {  // branch-free (selects): the wait counts stay exact
     const int piece = 5 * h + k;
-    if (piece < kStV) {
-      const int t = piece / 18, c = (piece % 18) * 256 + 4 * lane;
-      glds16(pv + (b * NT + t) * ld + HD + c, lds + kOffV + piece * 256);
-    } else if (piece == kStV) {
-      glds16(P + b * (kConvC * NT * NT) + min(4 * lane, kConvC * NT * NT - 4), lds + kOffP);
-    }
+    const int t = min(piece, kStV - 1) / 18;
+    const float* vb = uniform_ptr(pv + (b * NT + t) * ld + HD + (min(piece, kStV - 1) % 18) * 256) + 4 * lane;
+    const bool isv = piece < kStV;  // else the P piece (repeats write the same bytes)
+    glds16(isv ? vb : pb, lds + (isv ? kOffV + piece * 256 : kOffP));
   }
 }
 
@@ -1115,7 +1124,7 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
   const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(B, b0 + per_block);
   if (b0 < b1) {
     stage_go(g_out, out, b0, lds, h, lane);
-    if (h < kVPWaves) stage_vp(pv, ld, P, b0, lds, h, lane);
+    stage_vp(pv, ld, P, b0, lds, h, lane);
   }
   for (int64_t b = b0; b < b1; ++b) {
     const bool next = b + 1 < b1;
@@ -1156,24 +1165,27 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
     {
       int xpl = xp;  // laundered per molecule: the 36 row addresses are not hoisted out of the loop
       asm volatile("" : "+v"(xpl));
-      float g[kConvO][3];
-#pragma unroll
-      for (int o = 0; o < kConvO; ++o)
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) g[o][dx] = gpre(o, xpl - dx);
 #pragma unroll
       for (int i = 0; i < kCD; ++i) acc_in[i] = 0.f;
-      // the weights as scalar loads issued per molecule: laundering the pointer keeps the
-      // compiler from hoisting all 648 of them out of the molecule loop (SGPR spills)
+      // the weights as SCALAR loads (constant address space: s_load, K$-resident) issued per
+      // molecule; laundering the pointer keeps the compiler from hoisting all 648 of them out of
+      // the molecule loop (SGPR spills).  A generic pointer here compiles to flat vector loads,
+      // each batch drained by vmcnt(0) lgkmcnt(0) — 25 full memory latencies per molecule.
       const float* wh = wgt + half * kCD * 3;
       asm volatile("" : "+s"(wh));
-#pragma unroll
+      const __attribute__((address_space(4))) float* wc =
+          (const __attribute__((address_space(4))) float*)wh;
+      // g_pre rows one output channel at a time (3 values live, not 36)
+#pragma unroll 2
       for (int o = 0; o < kConvO; ++o) {  // (o, dx) order as conv3_bwd2_kernel
-        const float* w = wh + o * (kConvC * kConvH * 3);
+        const auto* w = wc + o * (kConvC * kConvH * 3);
+        float g[3];
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) g[dx] = gpre(o, xpl - dx);
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
-          for (int cd = 0; cd < kCD; ++cd) acc_in[cd] = fmaf(w[cd * 3 + dx], g[o][dx], acc_in[cd]);
+          for (int cd = 0; cd < kCD; ++cd) acc_in[cd] = fmaf(w[cd * 3 + dx], g[dx], acc_in[cd]);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -1192,7 +1204,9 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
     load_rows3(pv + b * NT * ld + (int64_t)h * W, ld, lane, q);
     load_rows3(x + b * NT * ldx, ldx, lane, k);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // cube gradient stored; v / P read
-    if (next && h < kVPWaves) stage_vp(pv, ld, P, b + 1, lds, h, lane);
+    // unconditional (the last molecule re-stages its own v / P, already in registers): a fixed
+    // count of DMA pieces per wave keeps the compiler's wait below at vmcnt(5)
+    stage_vp(pv, ld, P, next ? b + 1 : b, lds, h, lane);
     __builtin_amdgcn_sched_barrier(0);
     // (E) attention backward of head h (token_attn_fold_bwd_kernel's order)
     {

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-3 full pass: the whole -m gpu suite (margins on file), smoke, the default bench line, and
+# the rocprofv3 kernel stats of the same bench.  Usage: tools/gpu_r3_full.sh TAG
+set -o pipefail
+TAG=${1:-full}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
+export MVML_MARGINS_DIR=$OUT/margins
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --durations=40 --timeout 600 --timeout-method thread \
+  > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -3 $OUT/pytest_gpu.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -30 $OUT/smoke.log; exit 1; }
+cat $OUT/smoke.log
+timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json; grep -E "mvml_" $OUT/bench.err | head -40
