@@ -110,6 +110,17 @@ __device__ __forceinline__ void split2h(const float4& v, float s, uint2& p0, uin
   p1.y = lo_pair(hw, w);
 }
 
+// Eight values (two float4, k order) -> the two scaled fp16 planes of split2h, as MFMA operands.
+__device__ __forceinline__ void split2h8(const float4& lo, const float4& hi, float s, bf16x8& h,
+                                         bf16x8& l) {
+  uint2 h0, l0, h1, l1;
+  split2h(lo, s, h0, l0);
+  split2h(hi, s, h1, l1);
+  const u32x4 hv = {h0.x, h0.y, h1.x, h1.y}, lv = {l0.x, l0.y, l1.x, l1.y};
+  h = __builtin_bit_cast(bf16x8, hv);
+  l = __builtin_bit_cast(bf16x8, lv);
+}
+
 // Scale of an operand from its |max| bits (non-negative float bits order as integers): 2^k with
 // k = 141 - biased exponent, so |max| s < 2^15 (fp16 max 65504); k clamped to [-100, 100] (zero
 // / tiny operands: any scale works; a NaN max gives NaN results either way).
@@ -439,13 +450,17 @@ __device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[FM][FN], int64
     }
 }
 
-template <bool AK, bool BKM, int EPI_LOGW = -1, bool X3 = false>
+// X3: fp32-accurate products from split fp32 fragments — H2 = false: split-bf16 (six MFMAs per
+// fragment pair); H2 = true: scaled split-fp16 (three; operand scales from amax, as the 256x256
+// kernel's NP = 2), the skinny products' plan when the algorithm is f16x2.
+template <bool AK, bool BKM, int EPI_LOGW = -1, bool X3 = false, bool H2 = false>
 __global__ void __launch_bounds__(kThreads, 2)
 gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
                 float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{},
-                BatchStrides bst = BatchStrides{}) {
+                BatchStrides bst = BatchStrides{}, AmaxPtrs amax = AmaxPtrs{}) {
+  static_assert(!H2 || X3, "split-fp16 is a split product");
   if (blockIdx.z) {  // strided batch
     A += blockIdx.z * bst.a;
     B += blockIdx.z * bst.b;
@@ -475,6 +490,12 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  int ka = 0, kb = 0;  // H2: operand scales 2^ka, 2^kb from the |max| bits
+  if constexpr (H2) {
+    ka = amax_shift(*amax.a);
+    kb = amax_shift(*amax.b);
+  }
+  const float s_a = pow2f(ka), s_b = pow2f(kb);
 
   // LDS-DMA needs 16-B aligned pieces; a k-major operand's edge tile also needs rows % 4 == 0
   // (no piece straddles the edge), otherwise the guarded register path fills the stage.
@@ -523,7 +544,33 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     }
     const uint32_t sa_b = lds_b + (uint32_t)(cur * 2 * kTileFloats * 4);
     const uint32_t sb_b = sa_b + kTileFloats * 4;
-    if constexpr (X3) {
+    if constexpr (H2) {
+      // the same two 16-k steps, each fragment split into its two scaled fp16 planes; 4
+      // sub-tiles x 3 fp16 MFMAs per step
+      float4 f[2][4][2];  // [step][a0, a1, b0, b1][lo, hi]
+      bf16x8 pa[2][2], pb[2][2];
+#pragma unroll
+      for (int T = 0; T < 2; ++T) {
+        SA::frag8_asm(sa_b, ra0, 2 * T + lk, f[T][0][0], f[T][0][1]);
+        SA::frag8_asm(sa_b, ra1, 2 * T + lk, f[T][1][0], f[T][1][1]);
+        SB::frag8_asm(sb_b, rb0, 2 * T + lk, f[T][2][0], f[T][2][1]);
+        SB::frag8_asm(sb_b, rb1, 2 * T + lk, f[T][3][0], f[T][3][1]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int T = 0; T < 2; ++T) {
+        split2h8(f[T][0][0], f[T][0][1], s_a, pa[0][0], pa[0][1]);
+        split2h8(f[T][1][0], f[T][1][1], s_a, pa[1][0], pa[1][1]);
+        split2h8(f[T][2][0], f[T][2][1], s_b, pb[0][0], pb[0][1]);
+        split2h8(f[T][3][0], f[T][3][1], s_b, pb[1][0], pb[1][1]);
+        acc[0][0] = mfma_np<2>(pa[0], pb[0], acc[0][0]);
+        acc[0][1] = mfma_np<2>(pa[0], pb[1], acc[0][1]);
+        acc[1][0] = mfma_np<2>(pa[1], pb[0], acc[1][0]);
+        acc[1][1] = mfma_np<2>(pa[1], pb[1], acc[1][1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    } else if constexpr (X3) {
       // two 16-k steps; the fp32 fragments of step 1 are read under step 0's MFMAs and split
       // there (VALU beside the matrix pipe); 4 sub-tiles x 6 bf16 MFMAs per step
       float4 f[2][4][2];  // [step][a0, a1, b0, b1][lo, hi]
@@ -591,6 +638,15 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     }
   }
 
+  if constexpr (H2) {  // undo the operand scales (exact: powers of two)
+    const float ua = pow2f(-ka), ub = pow2f(-kb);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ua * ub;
+  }
   tile_epilogue<EPI_LOGW>(acc, M, N, m0 + wm * 64, n0 + wn * 64, lane, bias, beta, act, C, ldc,
                           slab, epi);
 }
@@ -668,6 +724,34 @@ struct SplitStager {
     }
   }
 
+  // Scaled split-fp16 (two planes; the 256x256 kernel's split2h): same LDS image, planes 0 / 1.
+  __device__ static __forceinline__ void split_store_h2(uint8_t* op, int tid, const float4 (&v)[4],
+                                                        float s) {
+    if (!KMAJ) {
+      const int row = tid >> 1;
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        bf16x8 h, l;
+        split2h8(v[2 * g], v[2 * g + 1], s, h, l);
+        const int chunk = 2 * (tid & 1) + g;
+        *reinterpret_cast<bf16x8*>(op + plane_off(0, row, chunk)) = h;
+        *reinterpret_cast<bf16x8*>(op + plane_off(1, row, chunk)) = l;
+      }
+    } else {
+      const int rb = 4 * (tid & 31), kk = 4 * (tid >> 5);
+      const int chunk = kk >> 3, half = (kk >> 2) & 1;
+      const float* f = reinterpret_cast<const float*>(v);  // f[4 i + j]: k = kk + i, row rb + j
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint2 h, l;
+        split2h(make_float4(f[j], f[4 + j], f[8 + j], f[12 + j]), s, h, l);
+        const int row = rb + j;
+        *reinterpret_cast<uint2*>(op + plane_off(0, row, chunk) + 8 * half) = h;
+        *reinterpret_cast<uint2*>(op + plane_off(1, row, chunk) + 8 * half) = l;
+      }
+    }
+  }
+
   __device__ static __forceinline__ void split_store(uint8_t* op, int tid, const float4 (&v)[4]) {
     if (!KMAJ) {
       const int row = tid >> 1;
@@ -700,13 +784,15 @@ struct SplitStager {
 #ifndef MVML_X3S_WAVES
 #define MVML_X3S_WAVES 2
 #endif
-template <bool AK, bool BKM, int EPI_LOGW = -1>
+// H2: scaled split-fp16 planes (two per operand, three fp16 MFMAs per fragment pair; scales from
+// amax) instead of split-bf16 (three planes, six MFMAs) — the skinny plan of the f16x2 algorithm.
+template <bool AK, bool BKM, int EPI_LOGW = -1, bool H2 = false>
 __global__ void __launch_bounds__(kThreads, MVML_X3S_WAVES)  // 2 workgroups per CU
 gemm_x3s_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
                 float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{},
-                BatchStrides bst = BatchStrides{}) {
+                BatchStrides bst = BatchStrides{}, AmaxPtrs amax = AmaxPtrs{}) {
   if (blockIdx.z) {  // strided batch
     A += blockIdx.z * bst.a;
     B += blockIdx.z * bst.b;
@@ -732,6 +818,12 @@ gemm_x3s_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  int ka = 0, kb = 0;  // H2: operand scales 2^ka, 2^kb from the |max| bits
+  if constexpr (H2) {
+    ka = amax_shift(*amax.a);
+    kb = amax_shift(*amax.b);
+  }
+  const float s_a = pow2f(ka), s_b = pow2f(kb);
   const int64_t ntiles = (kend > kbeg) ? ceil_div(kend - kbeg, BKT) : 0;
   // unguarded 16-B loads when the whole tile is in range and rows are 16-B aligned
   const bool a_in = a_vec && (AK ? m0 + BM <= M : m0 + BM <= M);
@@ -746,26 +838,41 @@ gemm_x3s_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   const int ra0 = wm * 64 + li, ra1 = ra0 + 32, rb0 = wn * 64 + li, rb1 = rb0 + 32;
   for (int64_t t = 0; t < ntiles; ++t) {
     if (t > 0) __syncthreads();  // every wave is done reading the previous tile
-    SA::split_store(lds, tid, va);
-    SB::split_store(lds + kOpBytes, tid, vb);
+    if constexpr (H2) {
+      SA::split_store_h2(lds, tid, va, s_a);
+      SB::split_store_h2(lds + kOpBytes, tid, vb, s_b);
+    } else {
+      SA::split_store(lds, tid, va);
+      SB::split_store(lds + kOpBytes, tid, vb);
+    }
     __syncthreads();
     if (t + 1 < ntiles) load_tile(kbeg + (t + 1) * BKT);  // in flight under the MFMAs
+    constexpr int NPL = H2 ? 2 : 3;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       const int chunk = 2 * st + lk;
-      bf16x8 pa[2][3], pb[2][3];
+      bf16x8 pa[2][NPL], pb[2][NPL];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < NPL; ++p) {
         pa[0][p] = *reinterpret_cast<const bf16x8*>(lds + plane_off(p, ra0, chunk));
         pa[1][p] = *reinterpret_cast<const bf16x8*>(lds + plane_off(p, ra1, chunk));
         pb[0][p] = *reinterpret_cast<const bf16x8*>(lds + kOpBytes + plane_off(p, rb0, chunk));
         pb[1][p] = *reinterpret_cast<const bf16x8*>(lds + kOpBytes + plane_off(p, rb1, chunk));
       }
-      acc[0][0] = mfma_x3(pa[0], pb[0], acc[0][0]);
-      acc[0][1] = mfma_x3(pa[0], pb[1], acc[0][1]);
-      acc[1][0] = mfma_x3(pa[1], pb[0], acc[1][0]);
-      acc[1][1] = mfma_x3(pa[1], pb[1], acc[1][1]);
+      acc[0][0] = mfma_np<NPL>(pa[0], pb[0], acc[0][0]);
+      acc[0][1] = mfma_np<NPL>(pa[0], pb[1], acc[0][1]);
+      acc[1][0] = mfma_np<NPL>(pa[1], pb[0], acc[1][0]);
+      acc[1][1] = mfma_np<NPL>(pa[1], pb[1], acc[1][1]);
     }
+  }
+  if constexpr (H2) {  // undo the operand scales (exact: powers of two)
+    const float ua = pow2f(-ka), ub = pow2f(-kb);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ua * ub;
   }
   tile_epilogue<EPI_LOGW>(acc, M, N, m0 + wm * 64, n0 + wn * 64, lane, bias, beta, act, C, ldc,
                           slab, epi);
@@ -941,6 +1048,15 @@ __device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], floa
   float* out = slab ? slab + (int64_t)blockIdx.y * M * N : C;
   const int64_t ld = slab ? N : ldc;
   const bool vec = (ld % 4 == 0) && (((uintptr_t)out & 15) == 0);
+  // LSTM cell, four units per lane (16 columns of a row): every load and store of the cell is a
+  // float4 (c, h, h2, the four activation rows, the biases, c_prev, the input projection)
+  // instead of seven dword stores per unit — the cell epilogue was store-issue-bound.  Same
+  // arithmetic per unit, so bitwise the per-unit path's results (kept for unaligned operands).
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  const bool cell4 = cep.D > 0 && cep.D % 4 == 0 && al16(cep.b_ih) && al16(cep.b_hh) &&
+                     al16(cep.c_prev) && al16(cep.c_out) && al16(cep.h_out) && al16(cep.h_out2) &&
+                     al16(cep.act) && cep.ldh % 4 == 0 && cep.ldh2 % 4 == 0 && al16(cep.gx) &&
+                     cep.ldgx % 4 == 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (i > 0) wave_sync_lds();  // the previous pass's reads are done
@@ -950,6 +1066,55 @@ __device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], floa
       for (int r = 0; r < 16; ++r)
         wl[((r & 3) + 8 * (r >> 2) + 4 * lk) * kEpiLd + 32 * j + li] = acc[i][j][r];
     wave_sync_lds();
+    if (cell4) {  // (host: N = 4 D, no split-K; N % 16 == 0, so a 4-unit group never straddles N)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int idx = q * 64 + lane, rr = idx >> 2, u = idx & 3;
+        const int64_t row = r0 + 32 * i + rr, col = c0 + 16 * u;
+        if (row >= M || col >= N) continue;
+        const int D = cep.D;
+        const int64_t j = col >> 2;  // units j .. j + 3
+        float4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(wl + rr * kEpiLd + 16 * u + 4 * k);
+        auto ld4 = [](const float* p) { return *reinterpret_cast<const float4*>(p); };
+        auto el = [](const float4& f, int k) { return k == 0 ? f.x : k == 1 ? f.y : k == 2 ? f.z : f.w; };
+        if (cep.gx) {
+          const float* gxr = cep.gx + row * cep.ldgx + j;
+          const float4 xi = ld4(gxr), xf = ld4(gxr + D), xg = ld4(gxr + 2 * D), xo = ld4(gxr + 3 * D);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[k].x += el(xi, k); v[k].y += el(xf, k); v[k].z += el(xg, k); v[k].w += el(xo, k);
+          }
+        }
+        const float4 bii = ld4(cep.b_ih + j), bif = ld4(cep.b_ih + D + j), big = ld4(cep.b_ih + 2 * D + j),
+                     bio = ld4(cep.b_ih + 3 * D + j);
+        const float4 bhi = ld4(cep.b_hh + j), bhf = ld4(cep.b_hh + D + j), bhg = ld4(cep.b_hh + 2 * D + j),
+                     bho = ld4(cep.b_hh + 3 * D + j);
+        const float4 cp4 = cep.c_prev ? ld4(cep.c_prev + row * D + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+        float cv[4], hv[4], iv[4], fv[4], gv[4], ov[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float gi = v[k].x + el(bii, k) + el(bhi, k);
+          const float gf = v[k].y + el(bif, k) + el(bhf, k);
+          const float gg = v[k].z + el(big, k) + el(bhg, k);
+          const float go = v[k].w + el(bio, k) + el(bho, k);
+          iv[k] = sigm_epi(gi); fv[k] = sigm_epi(gf); gv[k] = tanhf(gg); ov[k] = sigm_epi(go);
+          cv[k] = __fmaf_rn(fv[k], el(cp4, k), __fmul_rn(iv[k], gv[k]));  // lstm_cell_fwd_kernel's rounding
+          hv[k] = __fmul_rn(ov[k], tanhf(cv[k]));
+        }
+        auto st4 = [](float* p, const float (&a)[4]) { *reinterpret_cast<float4*>(p) = make_float4(a[0], a[1], a[2], a[3]); };
+        st4(cep.c_out + row * D + j, cv);
+        st4(cep.h_out + row * cep.ldh + j, hv);
+        if (cep.h_out2) st4(cep.h_out2 + row * cep.ldh2 + j, hv);
+        float* a = cep.act + row * 4 * (int64_t)D + j;
+        st4(a, iv);
+        st4(a + D, fv);
+        st4(a + 2 * D, gv);
+        st4(a + 3 * D, ov);
+      }
+      continue;
+    }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int idx = q * 64 + lane, rr = idx >> 4, c4 = (idx & 15) * 4;
@@ -969,8 +1134,8 @@ __device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], floa
         const float go = v.w + cep.b_ih[3 * D + j] + cep.b_hh[3 * D + j];
         const float ig = sigm_epi(gi), fg = sigm_epi(gf), gt = tanhf(gg), og = sigm_epi(go);
         const float cpv = cep.c_prev ? cep.c_prev[row * D + j] : 0.f;
-        const float c = fg * cpv + ig * gt;
-        const float h = og * tanhf(c);
+        const float c = __fmaf_rn(fg, cpv, __fmul_rn(ig, gt));  // lstm_cell_fwd_kernel's rounding
+        const float h = __fmul_rn(og, tanhf(c));
         cep.c_out[row * D + j] = c;
         cep.h_out[row * cep.ldh + j] = h;
         if (cep.h_out2) cep.h_out2[row * cep.ldh2 + j] = h;
@@ -2110,7 +2275,7 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   const bool hf = prec == kPrecF16x2;
   const bool x3 = prec == kPrecX3 || hf, bf = prec == kPrecBf16;
   GemmPlan plan = plan_gemm(prec, M, N, K);
-  if (hf && plan.wide && !amax.a) {  // operand maxima into the workspace head, once per product
+  if (hf && !amax.a) {  // operand maxima into the workspace head, once per product
     if (!workspace || workspace_bytes < kAmaxBytes) {
       set_error("gemm: workspace too small (need %zu)", mvml_gemm_workspace_size(M, N, K));
       return MVML_ERR_WORKSPACE;
@@ -2188,9 +2353,17 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
     else if (plan.wide)                                                                         \
       gemm_x3w_kernel<AKV, BKV, -1, false><<<grid, kXThreads, 0, st>>>(                         \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst);  \
+    else if (hf && AKV && BKV) /* skinny, both k-major: split-fp16 fragment split */           \
+      gemm_f32_kernel<AKV, BKV, -1, true, true><<<grid, kThreads, 0, st>>>(                     \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst,   \
+          amax);                                                                                \
     else if (x3 && AKV && BKV) /* both k-major: fragment split measured faster at 128x128 */    \
       gemm_f32_kernel<AKV, BKV, -1, true><<<grid, kThreads, 0, st>>>(                           \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst);  \
+    else if (hf) /* skinny: split-fp16 planes staged once per workgroup */                    \
+      gemm_x3s_kernel<AKV, BKV, -1, true><<<grid, kThreads, 0, st>>>(                           \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst,   \
+          amax);                                                                                \
     else if (x3)                                                                                \
       gemm_x3s_kernel<AKV, BKV><<<grid, kThreads, 0, st>>>(                                     \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst);  \

@@ -35,9 +35,11 @@ __global__ void lstm_cell_fwd_kernel(int64_t B, int D, const float* __restrict__
     const float go = g[3 * D + d] + b_ih[3 * D + d] + b_hh[3 * D + d];
     const float i = sigm(gi), f = sigm(gf), gt = tanhf(gg), o = sigm(go);
     const float cp = c_prev ? c_prev[e] : 0.f;
-    const float c = f * cp + i * gt;
+    // explicit rounding (no contraction choice left to the compiler): the split-fp16 GEMM's
+    // cell epilogue (gemm_f32.hip, CellEpi) uses the same two operations, bit for bit
+    const float c = __fmaf_rn(f, cp, __fmul_rn(i, gt));
     c_out[e] = c;
-    const float h = o * tanhf(c);
+    const float h = __fmul_rn(o, tanhf(c));
     h_out[b * ldh + d] = h;
     if (h_out2) h_out2[b * ldh2 + d] = h;
     float* a = act + b * 4 * D;
