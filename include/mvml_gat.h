@@ -310,10 +310,13 @@ int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_
                        int64_t ldh, float* act_out, float* h_out2, int64_t ldh2, void* stream);
 /* g_h [B,D] (ld ldgh), g_c [B,D] (carry from t+1, may be NULL) -> g_gates [B,4D] (pre-act),
  * g_c_prev [B,D] (may be NULL).  gg_amax (may be NULL): *gg_amax = max(*gg_amax, bits of
- * max |g_gates|) — the split-fp16 operand max of the GEMMs that read g_gates. */
+ * max |g_gates|) — the split-fp16 operand max of the GEMMs that read g_gates.  gb_part (may be
+ * NULL): [R][4D] partial column sums of g_gates, R = mvml_lstm_cell_bwd_part_rows(B, D) (the
+ * bias gradient is their column sum, over every step's partial). */
+int64_t mvml_lstm_cell_bwd_part_rows(int64_t B, int D);
 int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const float* c, const float* c_prev,
                        const float* g_h, int64_t ldgh, const float* g_c, float* g_gates,
-                       float* g_c_prev, uint32_t* gg_amax, void* stream);
+                       float* g_c_prev, uint32_t* gg_amax, float* gb_part, void* stream);
 /* Readout segment pass (one wavefront per molecule): e_n = <x_n, q_g>, alpha = softmax over
  * the molecule's atoms (softmax_nodes), r_g = sum_n alpha_n x_n (sum_nodes).  Writes r into
  * qstar[:, D:2D] (ld ldq, q itself already sits in qstar[:, 0:D]) and lse[g] for backward. */
@@ -327,9 +330,12 @@ int mvml_set2set_seg_bwd(int64_t B, int D, const int64_t* node_offsets, const fl
                          const float* g_qstar, int64_t ldgq, float* g_q, int64_t ldgout,
                          float* alpha, float* g_e, void* stream);
 /* dL/dX[n] = sum_t alpha_t[n] * g_r_t[g(n)] + g_e_t[n] * q_t[g(n)] over T iterations,
- * g(n) = node_graph[n] (from mvml_build_csr).  qstars: T consecutive [B, ldq] buffers
- * (stride qstar_stride), g_qstars likewise; alphas / g_es: T consecutive [N] buffers. */
+ * g(n) = the molecule of atom n.  With node_offsets (int64[num_graphs + 1], mvml_build_csr)
+ * and T <= 6, D <= 512: one wavefront per molecule (its 2T vectors loaded once); otherwise one
+ * per atom through node_graph[n].  qstars: T consecutive [B, ldq] buffers (stride
+ * qstar_stride), g_qstars likewise; alphas / g_es: T consecutive [N] buffers. */
 int mvml_set2set_gx(int64_t num_nodes, int D, int T, const int32_t* node_graph,
+                    const int64_t* node_offsets, int64_t num_graphs,
                     const float* qstars, int64_t ldq, int64_t qstar_stride,
                     const float* g_qstars, int64_t ldgq, int64_t g_qstar_stride,
                     const float* alphas, const float* g_es, float* gX, void* stream);

@@ -6,6 +6,8 @@
 // The segment pass gives each molecule one wavefront that streams its atoms' 384-float rows
 // once (online max/sum softmax), so the six Set2Set iterations read the node features six
 // times in total, never materialising broadcast q or per-node products.
+#include <numeric>
+
 #include "common.h"
 
 namespace mvml {
@@ -50,13 +52,20 @@ __global__ void lstm_cell_fwd_kernel(int64_t B, int D, const float* __restrict__
   }
 }
 
+// gb_part (optional): the gate gradients' column sums of this thread's rows, i.e. the partial
+// bias gradient.  The host sizes the grid so that gridDim * 256 = R D (mvml_lstm_cell_bwd_
+// part_rows): thread gid then always sees unit d = gid % D, rows gid / D + j R, and writes its
+// four gate sums to row gid / D of the [R][4 D] partial (summed over rows and time steps by one
+// column-sum pass afterwards — instead of a pass over all T x B gate-gradient rows).
 __global__ void lstm_cell_bwd_kernel(int64_t B, int D, const float* __restrict__ act,
                                      const float* __restrict__ c, const float* __restrict__ c_prev,
                                      const float* __restrict__ g_h, int64_t ldgh,
                                      const float* __restrict__ g_c, float* __restrict__ g_gates,
-                                     float* __restrict__ g_c_prev, uint32_t* __restrict__ gg_amax) {
+                                     float* __restrict__ g_c_prev, uint32_t* __restrict__ gg_amax,
+                                     float* __restrict__ gb_part) {
   const int64_t total = B * D;
   float mx = 0.f;  // |max| of this thread's gate gradients (split-fp16 operand scale)
+  float sb[4] = {0.f, 0.f, 0.f, 0.f};  // gb_part: this thread's gate column sums
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = e / D;
@@ -76,6 +85,17 @@ __global__ void lstm_cell_bwd_kernel(int64_t B, int D, const float* __restrict__
     gg[3 * D + d] = g3;
     mx = fmaxf(mx, fmaxf(fmaxf(fabsf(g0), fabsf(g1)), fmaxf(fabsf(g2), fabsf(g3))));
     if (g_c_prev) g_c_prev[e] = gc * f;
+    sb[0] += g0;
+    sb[1] += g1;
+    sb[2] += g2;
+    sb[3] += g3;
+  }
+  if (gb_part) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t r0 = gid / D, d = gid - r0 * D;
+    float* pr = gb_part + r0 * 4 * D + d;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pr[q * D] = sb[q];
   }
   if (gg_amax) {  // block max -> one unsigned atomicMax of the non-negative float bits
     mx = wave_max(mx);
@@ -236,6 +256,71 @@ seg_gx_kernel(int64_t N, int D, int T, const int32_t* __restrict__ node_graph,
   }
 }
 
+// The same sum with one wave per MOLECULE: its 2 T vectors q_t, g_r_t are loaded once into
+// registers (shared by all its atoms), the per-atom coefficients alpha_t[n], g_e_t[n] are loaded
+// 64 atoms at a time with the lanes on the atoms (coalesced), and each atom's row is formed from
+// its coefficients broadcast by v_readlane — no per-atom chain of dependent global loads (the
+// node-per-wave kernel above walked T of them per atom: latency-bound at ~1.1 TB/s of gX).
+// T <= kGxT; the same per-element expression and t order as seg_gx_kernel.
+constexpr int kGxT = 6;
+template <int NV>
+__global__ void __launch_bounds__(256)
+seg_gx_mol_kernel(int64_t B, int D, int T, const int64_t* __restrict__ node_off,
+                  const float* __restrict__ qstars, int64_t ldq, int64_t qs_stride,
+                  const float* __restrict__ g_qstars, int64_t ldgq, int64_t gqs_stride,
+                  const float* __restrict__ alphas, const float* __restrict__ g_es, int64_t N,
+                  float* __restrict__ gX) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= B) return;
+  const int64_t n0 = node_off[g], n1 = node_off[g + 1];
+  float4 qv[kGxT][NV], gv[kGxT][NV];
+#pragma unroll
+  for (int t = 0; t < kGxT; ++t)
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int col = 4 * (lane + 64 * c);
+      const bool ok = t < T && col < D;
+      qv[t][c] = ok ? ld4(qstars + t * qs_stride + g * ldq + col) : make_float4(0, 0, 0, 0);
+      gv[t][c] = ok ? ld4(g_qstars + t * gqs_stride + g * ldgq + D + col) : make_float4(0, 0, 0, 0);
+    }
+  for (int64_t base = n0; base < n1; base += 64) {
+    const int64_t n = base + lane;
+    const bool live = n < n1;
+    float al[kGxT], ge[kGxT];
+#pragma unroll
+    for (int t = 0; t < kGxT; ++t) {
+      al[t] = (live && t < T) ? alphas[(int64_t)t * N + n] : 0.f;
+      ge[t] = (live && t < T) ? g_es[(int64_t)t * N + n] : 0.f;
+    }
+    const int cnt = (int)min<int64_t>(64, n1 - base);
+    for (int i = 0; i < cnt; ++i) {
+      float4 acc[NV];
+#pragma unroll
+      for (int c = 0; c < NV; ++c) acc[c] = make_float4(0, 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < kGxT; ++t) {
+        if (t >= T) break;  // uniform
+        const float a_ = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(al[t]), i));
+        const float e_ = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ge[t]), i));
+#pragma unroll
+        for (int c = 0; c < NV; ++c) {
+          const float4 a = gv[t][c], b = qv[t][c];
+          acc[c].x += a_ * a.x + e_ * b.x;
+          acc[c].y += a_ * a.y + e_ * b.y;
+          acc[c].z += a_ * a.z + e_ * b.z;
+          acc[c].w += a_ * a.w + e_ * b.w;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        const int col = 4 * (lane + 64 * c);
+        if (col < D) st4(gX + (base + i) * D + col, acc[c]);
+      }
+    }
+  }
+}
+
 unsigned grid_for(int64_t total) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(total, 256), 16384));
 }
@@ -271,14 +356,31 @@ extern "C" int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, cons
   return check_launch("lstm_cell_fwd_kernel");
 }
 
+// Rows of the bias-gradient partial of mvml_lstm_cell_bwd: R with R D % 256 == 0 and about 16
+// rows of B per thread (the amax fold's grain).
+static int64_t cell_bwd_part_rows(int64_t B, int D) {
+  const int64_t step = 256 / std::gcd<int64_t>(D, 256);  // smallest R with R D % 256 == 0
+  return std::max<int64_t>(step, ceil_div(ceil_div(B, 16), step) * step);
+}
+extern "C" int64_t mvml_lstm_cell_bwd_part_rows(int64_t B, int D) {
+  return (B > 0 && D > 0) ? cell_bwd_part_rows(B, D) : 0;
+}
+
 extern "C" int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const float* c,
                                   const float* c_prev, const float* g_h, int64_t ldgh,
                                   const float* g_c, float* g_gates, float* g_c_prev,
-                                  uint32_t* gg_amax, void* stream) {
+                                  uint32_t* gg_amax, float* gb_part, void* stream) {
   clear_error();
   MVML_REQUIRE(B >= 0 && D > 0 && ldgh >= D, "lstm_cell_bwd: bad shape");
   if (B == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
+  if (gb_part) {  // grid * 256 = R D: every thread keeps one unit (see the kernel)
+    const int64_t R = cell_bwd_part_rows(B, D);
+    lstm_cell_bwd_kernel<<<(unsigned)(R * D / 256), 256, 0, st>>>(B, D, act, c, c_prev, g_h, ldgh,
+                                                                  g_c, g_gates, g_c_prev, gg_amax,
+                                                                  gb_part);
+    return check_launch("lstm_cell_bwd_kernel");
+  }
   // with gg_amax, one atomicMax per workgroup on a single word: a short kernel whose thousands
   // of workgroups end together saturates it (~88 per us), so each thread takes >= 16 elements
   // (MVP's 8k-row cells: 768 workgroups instead of 12k; Set2Set's 64k-row cells: 6k)
@@ -286,7 +388,7 @@ extern "C" int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const floa
                                       grid_for(B * D), std::max<int64_t>(256, ceil_div(B * D, 4096)))
                                 : grid_for(B * D);
   lstm_cell_bwd_kernel<<<grid, 256, 0, st>>>(B, D, act, c, c_prev, g_h, ldgh, g_c, g_gates,
-                                             g_c_prev, gg_amax);
+                                             g_c_prev, gg_amax, nullptr);
   return check_launch("lstm_cell_bwd_kernel");
 }
 
@@ -320,6 +422,7 @@ extern "C" int mvml_set2set_seg_bwd(int64_t B, int D, const int64_t* node_offset
 }
 
 extern "C" int mvml_set2set_gx(int64_t num_nodes, int D, int T, const int32_t* node_graph,
+                               const int64_t* node_offsets, int64_t num_graphs,
                                const float* qstars, int64_t ldq, int64_t qstar_stride,
                                const float* g_qstars, int64_t ldgq, int64_t g_qstar_stride,
                                const float* alphas, const float* g_es, float* gX, void* stream) {
@@ -329,6 +432,19 @@ extern "C" int mvml_set2set_gx(int64_t num_nodes, int D, int T, const int32_t* n
   MVML_REQUIRE(T >= 0 && ldq >= 2 * D && ldgq >= 2 * D, "set2set_gx: bad shape");
   if (num_nodes == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
+  if (node_offsets && num_graphs > 0 && T <= kGxT && D <= 512) {  // one wave per molecule
+    const unsigned grid = (unsigned)ceil_div(num_graphs, 4);
+    if (D <= 256)
+      seg_gx_mol_kernel<1><<<grid, 256, 0, st>>>(num_graphs, D, T, node_offsets, qstars, ldq,
+                                                 qstar_stride, g_qstars, ldgq, g_qstar_stride,
+                                                 alphas, g_es, num_nodes, gX);
+    else
+      seg_gx_mol_kernel<2><<<grid, 256, 0, st>>>(num_graphs, D, T, node_offsets, qstars, ldq,
+                                                 qstar_stride, g_qstars, ldgq, g_qstar_stride,
+                                                 alphas, g_es, num_nodes, gX);
+    return check_launch("seg_gx_mol_kernel");
+  }
+  MVML_REQUIRE(node_graph != nullptr, "set2set_gx: node_graph or node_offsets required");
   const unsigned grid = (unsigned)ceil_div(num_nodes, 4);
   MVML_NV_SWITCH(seg_gx_kernel, grid, num_nodes, D, T, node_graph, qstars, ldq, qstar_stride,
                  g_qstars, ldgq, g_qstar_stride, alphas, g_es, gX)

@@ -431,15 +431,14 @@ __global__ void __launch_bounds__(256) pack_rows_kernel(int64_t nrows, int64_t t
                                                         int64_t t0, int shift, float4* __restrict__ tm,
                                                         int64_t ld_tm4, float4* __restrict__ pk,
                                                         int64_t ld_pk4, int dir) {
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // blockIdx.y = step k of the range, one wave per live row p of that step (no search over
+  // the step offsets: a per-row binary search was a chain of dependent loads per wave)
+  const int64_t lo = blockIdx.y;
+  const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (r >= nrows) return;
-  int64_t lo = 0, hi = t_count;  // the step of packed row r: offs[k] <= r < offs[k + 1]
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (offs[mid] <= r) lo = mid; else hi = mid;
-  }
-  const int64_t p = r - offs[lo];
+  const int64_t rb = offs[lo];
+  if (p >= offs[lo + 1] - rb) return;
+  const int64_t r = rb + p;
   float4* a = tm + ((t0 + lo + shift) * B + p) * ld_tm4;
   float4* b = pk + r * ld_pk4;
   for (int64_t c = lane; c < cols4; c += 64) {
@@ -461,7 +460,10 @@ extern "C" int mvml_bilstm_pack_rows(int64_t nrows, int64_t t_count, int64_t B, 
                    ((uintptr_t)tm & 15) == 0 && ((uintptr_t)packed & 15) == 0,
                "bilstm_pack_rows: bad shape / alignment");
   if (nrows == 0) return MVML_OK;
-  pack_rows_kernel<<<(unsigned)ceil_div(nrows, 4), 256, 0, as_stream(stream)>>>(
+  MVML_REQUIRE(t_count <= 65535, "bilstm_pack_rows: t_count must be <= 65535");
+  // a step holds at most B live rows (the packed sequence's batch sizes never exceed B)
+  pack_rows_kernel<<<dim3((unsigned)ceil_div(std::min(nrows, B), 4), (unsigned)t_count), 256, 0,
+                     as_stream(stream)>>>(
       nrows, t_count, B, cols / 4, offsets, t0, shift, reinterpret_cast<float4*>(tm), ld_tm / 4,
       reinterpret_cast<float4*>(packed), ld_pk / 4, dir);
   return check_launch("pack_rows_kernel");

@@ -442,6 +442,11 @@ class Set2SetFunction(torch.autograd.Function):
         gxh = [None] + [torch.empty((B, 2 * D), **f32) for _ in range(1, Lr)]
         g_c = [torch.zeros((B, D), **f32) for _ in range(Lr)]
         g_c_new = torch.empty((B, D), **f32)
+        # LSTM bias gradients: every cell backward leaves [R, 4D] partial column sums of its
+        # gate gradients (mvml_lstm_cell_bwd's gb_part); one column sum over the T R partial rows
+        # per layer replaces a pass over all T B gate-gradient rows
+        R = int(_lib.lib().mvml_lstm_cell_bwd_part_rows(B, D))
+        gb_part = torch.empty((Lr, T, R, 4 * D), **f32)
         # split-fp16 maxima: the forward's bounds for XH (|x|, |h|) and [W_ih | W_hh], and a
         # running |max| of each layer's gate gradients, folded in by mvml_lstm_cell_bwd (the
         # running value bounds every cell seen so far, which is all a scale needs)
@@ -466,7 +471,8 @@ class Set2SetFunction(torch.autograd.Function):
                 c_prev = cs[t - 1, l] if t > 0 else None
                 g_gates = g_gates_all[l, t]
                 call("mvml_lstm_cell_bwd", B, D, ptr(acts[t, l]), ptr(cs[t, l]), ptr(c_prev), ptr(gh), ldgh,
-                     ptr(g_c[l]) if t < T - 1 else None, ptr(g_gates), ptr(g_c_new), slot(amax_g, l), st)
+                     ptr(g_c[l]) if t < T - 1 else None, ptr(g_gates), ptr(g_c_new), slot(amax_g, l),
+                     ptr(gb_part[l, t]), st)
                 g_c[l], g_c_new = g_c_new, g_c[l]
                 # N = kin + D with the recurrent part (t > 0), kin alone at t = 0; layer 0 at
                 # t = 0 has neither (its input q*_{-1} = 0 is a constant)
@@ -493,9 +499,9 @@ class Set2SetFunction(torch.autograd.Function):
                      amax=None if amax_g is None else (slot(amax_g, l), slot(amax_x, 0)))
                 gW_ih[l].copy_(gWcat[:, :kin])
                 gW_hh[l].copy_(gWcat[:, kin:])
-            colsum(G, T * B, 4 * D, 4 * D, gb[l])
+            colsum(gb_part[l], T * R, 4 * D, 4 * D, gb[l])
         gX = torch.empty((N, D), **f32)
-        call("mvml_set2set_gx", N, D, T, ptr(g.node_graph), ptr(qs), 3 * D, B * 3 * D,
+        call("mvml_set2set_gx", N, D, T, ptr(g.node_graph), ptr(g.node_offsets), B, ptr(qs), 3 * D, B * 3 * D,
              ptr(g_qs3), 3 * D, B * 3 * D, ptr(alphas), ptr(g_es), ptr(gX), st)
         grads = []
         for l in range(Lr):

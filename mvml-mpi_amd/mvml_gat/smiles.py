@@ -300,7 +300,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                     g_c = carry[k % 2] if nxt is not None else None
                     call("mvml_lstm_cell_bwd", bs, H, ptr(act[t]), ptr(c[t]), ptr(c_prev),
                          ptr(g[t, :, d * H:]), 2 * H, ptr(g_c), ptr(gg[t]), ptr(carry[(k + 1) % 2]),
-                         slot(amg, d), st)
+                         slot(amg, d), None, st)
                     nxt, k = t, k + 1
         # weight / input gradients: GEMMs over every position — on the wide path over the live
         # rows only (packed), else over all T x B rows (the padding rows of gg are zeros)

@@ -11,3 +11,9 @@ timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/s
 cat $OUT/smoke.log
 timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json; grep -E "mvml_" $OUT/bench.err | head -40
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --view-only-steps 0 --no-inference --no-kernel-timer > $OUT/prof.log 2>&1 || { tail -30 $OUT/prof.log; exit 1; }
+find $OUT/prof -name '*kernel_stats.csv' | head -n 1 | xargs -I{} cp {} $OUT/kernel_stats.csv
+head -n 14 $OUT/kernel_stats.csv | cut -c1-200
+timeout -k 10 400 python -u bench.py --workload mvp --steps 6 --warmup 2 --no-cpu-baseline \
+  --view-only-steps 0 --no-inference > $OUT/mvp.json 2> $OUT/mvp.err || { tail -30 $OUT/mvp.err; exit 1; }
+head -c 300 $OUT/mvp.json; echo; grep -E "mvml_" $OUT/mvp.err | head -12
