@@ -216,14 +216,21 @@ class GATLayerFunction(torch.autograd.Function):
             absmax(Wcat, C + 2 * H, Fp, Fp, amx, 1)
             # Wcat split once: the projection's tiles and the backward's dL/dX read the planes
             wps = split_planes(Wcat, C + 2 * H, Fp, Fp, slot(amx, 1))
-        if amx is not None and PROJ_ELR_GEMM:
+        bf16_elr = (algo or GEMM_ALGO) == "bf16" and PROJ_ELR_GEMM
+        if (amx is not None or bf16_elr) and PROJ_ELR_GEMM:
             # el / er as 2H more GEMM columns: X [A_l ; A_r]^T with A_l[h] = sum_f attn_l[h, f]
             # fc.weight[h F + f] (Wcat's last 2H rows) — the same values re-associated, no
-            # logit-partial epilogue and no finalize pass; then gathered into elr [N, 2H]
+            # logit-partial epilogue and no finalize pass; then gathered into elr [N, 2H].  The
+            # bf16 projection (config 4) takes the same path on the bf16-operand kernel: its C
+            # tile leaves through the LDS epilogue instead of the logit-partial one's column
+            # stores (9.5 -> ~5 ms per config-3 layer-2 launch)
             ldy = _row_pitch(C + 2 * H)
             Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
-            gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(slot(*ax), slot(amx, 1)),
-                 bsplit=None if wps[0] is None else wps)
+            if amx is not None:
+                gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(slot(*ax), slot(amx, 1)),
+                     bsplit=None if wps[0] is None else wps)
+            else:
+                gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, algo="bf16")
             elr = Y[:, C:C + 2 * H].contiguous()
         else:
             ldy = _row_pitch(C)
