@@ -81,6 +81,9 @@ def parse(argv=None):
     ap.add_argument("--proj-bf16", action="store_true",
                     help="BASELINE config 4: the GAT projection GEMMs (fc / res_fc, forward and "
                          "backward) on bf16 operands with fp32 accumulation (mvml_gemm_bf16)")
+    ap.add_argument("--no-view-overlap", action="store_true",
+                    help="mvp workload: run the SMILES view after the graph view on one stream "
+                         "(default: on a side stream beside it, mvml_gat.mvp.OVERLAP_VIEWS)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo plumbing rehearsal with a stand-in model (no measurement)")
     return ap.parse_args(argv)
@@ -393,7 +396,9 @@ def run(args):
         fusion = None
         params = list(model.parameters())
     elif mvp:
+        import mvml_gat.mvp as mvp_mod
         from mvml_gat.mvp import MVP
+        mvp_mod.OVERLAP_VIEWS = not args.no_view_overlap
         # main.py:85-87 with config.py defaults: hidden [192, 384], rnn 128 / 384 x 2, fp 512,
         # 12 fusion heads, dropout 0.5
         full = MVP(11, 74, [192, 384], 6, 3, 128, 384, 2, 512, 12, 0.5,

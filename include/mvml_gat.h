@@ -58,6 +58,9 @@ const char* mvml_version(void);
                                    launches, 0 = one */
 #define MVML_OPT_GEMM_RING 5    /* MVML_GEMM_RING: 1 = split-fp16 256x256 products on the
                                    LDS-DMA ring kernel, 0 (default) = the register-staged one */
+#define MVML_OPT_LSTM_TILE 6    /* MVML_LSTM_TILE: tile of the wide BiLSTM step products
+                                   (mvml_bilstm_wide_step_*): 0 (default) planned from the live
+                                   row count, 128 / 256 = forced */
 int mvml_set_option(int option, int value);
 int mvml_get_option(int option);
 

@@ -450,6 +450,14 @@ __device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[FM][FN], int64
     }
 }
 
+constexpr int kEpiLd = 68;  // floats per LDS row (64 + 4: the column writes hit distinct banks)
+template <int FM>
+__device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* wl, int64_t M,
+                                             int64_t N, int64_t r0, int64_t c0, int lane,
+                                             const float* __restrict__ bias, float beta, int act,
+                                             float* __restrict__ C, int64_t ldc,
+                                             float* __restrict__ slab, const CellEpi& cep = CellEpi{});
+
 // X3: fp32-accurate products from split fp32 fragments — H2 = false: split-bf16 (six MFMAs per
 // fragment pair); H2 = true: scaled split-fp16 (three; operand scales from amax, as the 256x256
 // kernel's NP = 2), the skinny products' plan when the algorithm is f16x2.
@@ -459,12 +467,22 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
                 float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{},
-                BatchStrides bst = BatchStrides{}, AmaxPtrs amax = AmaxPtrs{}) {
+                BatchStrides bst = BatchStrides{}, AmaxPtrs amax = AmaxPtrs{},
+                CellEpi cep = CellEpi{}, DualPtrs dual = DualPtrs{}) {
   static_assert(!H2 || X3, "split-fp16 is a split product");
   if (blockIdx.z) {  // strided batch
     A += blockIdx.z * bst.a;
     B += blockIdx.z * bst.b;
     C += blockIdx.z * bst.c;
+  }
+  if (blockIdx.z == 1 && dual.a) {  // the second product of a dual launch (gemm_x3w_kernel's)
+    A = dual.a;
+    B = dual.b;
+    M = dual.m;
+    slab = dual.slab;
+    cep = dual.cep;
+    amax.b = dual.amax_b;
+    if (dual.amax_a) amax.a = dual.amax_a;
   }
   using SA = Stager<AK>;
   using SB = Stager<BKM>;
@@ -476,6 +494,7 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   const int64_t tiles_n = ceil_div(N, BN);
   const int64_t tile = xcd_block(blockIdx.x, gridDim.x);
   const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  if (m0 >= M) return;  // a dual launch's shorter product (grid sized for the longer one)
   const int64_t kbeg = (int64_t)blockIdx.y * k_split;
   const int64_t kend = min(K, kbeg + k_split);
 
@@ -646,6 +665,14 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ua * ub;
+  }
+  if constexpr (H2 && EPI_LOGW < 0) {
+    if (cep.D > 0) {  // LSTM cell epilogue through LDS (host: N = 4 D, no split-K)
+      __syncthreads();  // every wave is done reading the last stage
+      epilogue_lds(acc, lds + wid * 32 * kEpiLd, M, N, m0 + wm * 64, n0 + wn * 64, lane, bias, beta,
+                   act, C, ldc, slab, cep);
+      return;
+    }
   }
   tile_epilogue<EPI_LOGW>(acc, M, N, m0 + wm * 64, n0 + wn * 64, lane, bias, beta, act, C, ldc,
                           slab, epi);
@@ -1032,18 +1059,19 @@ struct XOp {
 // slab) is stored with 16-B row-contiguous stores instead of 4-B column scatters — the
 // epilogue of an output-bound GEMM (L2 forward: 13.5 GB of C) is store-issue-bound otherwise.
 // Rows / columns outside C and unaligned C fall back to guarded scalar stores per element.
-constexpr int kEpiLd = 68;  // floats per LDS row (64 + 4: the column writes hit distinct banks)
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], float* wl, int64_t M,
+// A wave's FM x 2 accumulator tiles (rows r0 .. r0 + 32 FM, 64 columns) through its 32-row LDS
+// window: FM = 4 in the 256x256 kernels, 2 in the 128x128 one.
+template <int FM>
+__device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* wl, int64_t M,
                                                  int64_t N, int64_t r0, int64_t c0, int lane,
                                                  const float* __restrict__ bias, float beta, int act,
                                                  float* __restrict__ C, int64_t ldc,
-                                                 float* __restrict__ slab,
-                                                 const CellEpi& cep = CellEpi{}) {
+                                                 float* __restrict__ slab, const CellEpi& cep) {
   const int li = lane & 31, lk = lane >> 5;
   float* out = slab ? slab + (int64_t)blockIdx.y * M * N : C;
   const int64_t ld = slab ? N : ldc;
@@ -1058,7 +1086,7 @@ __device__ __forceinline__ void epilogue_lds_256(const f32x16 (&acc)[4][2], floa
                      al16(cep.act) && cep.ldh % 4 == 0 && cep.ldh2 % 4 == 0 && al16(cep.gx) &&
                      cep.ldgx % 4 == 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < FM; ++i) {
     if (i > 0) wave_sync_lds();  // the previous pass's reads are done
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -1627,7 +1655,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   if constexpr (EPI_LOGW >= 0)
     tile_epilogue<EPI_LOGW, 4, 2, false>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta,
                                          act, C, ldc, slab, epi);
-  epilogue_lds_256(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
+  epilogue_lds(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
                    n0 + wn * 64, lane, bias, beta, act, C, ldc, slab, cep);
 #else
   tile_epilogue<EPI_LOGW, 4, 2>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta, act, C,
@@ -1890,7 +1918,7 @@ gemm_h2g_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     // every wave is past its last ring read (and no LDS-DMA is in flight) before the ring
     // turns into the epilogue's staging tiles
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    epilogue_lds_256(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
+    epilogue_lds(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
                      n0 + wn * 64, lane, bias, beta, act, C, ldc, slab, cep);
   }
 }
@@ -2544,6 +2572,19 @@ __global__ void __launch_bounds__(256) lstm_step_bwd_kernel(LstmBwdArgs a0, Lstm
   if (threadIdx.x == 0)
     atomicMax(a.gg_amax, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
+
+// Tile of a step's products: the 256x256 tile's latency (~55 us for K = 384 however few its rows)
+// sets the step time when there are too few row tiles to fill the chip; the 128x128 split-fp16
+// kernel runs four times the workgroups at a quarter of the work each.  Measured per dual launch
+// (tools/lstm_step_bench.py, H = 384; results bitwise equal): forward 128 <= 256 at every row
+// count (24.9 / 54.0 us at 256 rows, 138.7 / 158.7 at 8192); backward 128 faster up to 4096 rows
+// (90.6 / 101.9 us), level above (137.7 / 134.1 at 6144).  Option MVML_OPT_LSTM_TILE forces one.
+constexpr int64_t kLstmBwdSmallRows = 4096;
+bool lstm_small_tile(int64_t rows, bool bwd) {
+  const int force = option(MVML_OPT_LSTM_TILE);
+  if (force == 128 || force == 256) return force == 128;
+  return !bwd || rows <= kLstmBwdSmallRows;
+}
 }  // namespace
 
 extern "C" int mvml_bilstm_wide_step_fwd(
@@ -2568,11 +2609,18 @@ extern "C" int mvml_bilstm_wide_step_fwd(
   e1 = e0;
   e1.b_ih = bih1; e1.b_hh = bhh1; e1.c_prev = cprev1; e1.c_out = c1; e1.h_out = h1; e1.act = act1;
   e1.gx = gx1;
+  const float* a0 = K ? A0 : gx0;  // K = 0 (a direction's first step): no A rows are read
+  const float* a1 = K ? A1 : gx1;
+  if (lstm_small_tile(std::max(M0, M1), false)) {
+    const int64_t tiles = ceil_div(std::max(M0, M1), BM) * ceil_div(N, BN);
+    gemm_f32_kernel<false, false, -1, true, true><<<dim3((unsigned)tiles, 1, 2), kThreads, 0, as_stream(stream)>>>(
+        M0, N, K, a0, K ? lda : 4, W0, ldw, nullptr, 0.f, 0, nullptr, N, K > 0 ? K : 1, nullptr, 1, 1,
+        ProjEpi{}, BatchStrides{}, AmaxPtrs{amax_a, amax_w0}, e0, DualPtrs{a1, W1, nullptr, amax_w1, M1, e1});
+    return check_launch("gemm_f32_kernel(bilstm step)");
+  }
   const int64_t tn = ceil_div(N, XBN);
   const int64_t tiles = std::max(ceil_div(M0, XBM), ceil_div(M1, XBM)) * tn;
   const dim3 grid((unsigned)tiles, 1, 2);
-  const float* a0 = K ? A0 : gx0;  // K = 0 (a direction's first step): no A rows are read
-  const float* a1 = K ? A1 : gx1;
   gemm_x3w_kernel<false, false, -1, true, 2><<<grid, kXThreads, 0, as_stream(stream)>>>(
       M0, N, K, a0, K ? lda : 4, W0, ldw, nullptr, 0.f, 0, nullptr, N, K > 0 ? K : 1, nullptr, 1, 1,
       ProjEpi{}, BatchStrides{}, e0, AmaxPtrs{amax_a, amax_w0}, DualPtrs{a1, W1, nullptr, amax_w1, M1, e1});
@@ -2609,6 +2657,15 @@ extern "C" int mvml_bilstm_wide_step_bwd(
                  "bilstm_wide_step_bwd: alignment");
     const int S = 2;
     const int64_t kc = k_chunk(K, S);
+    if (lstm_small_tile(std::max(R0, R1), true)) {
+      const int64_t tiles = ceil_div(std::max(R0, R1), BM) * ceil_div(N, BN);
+      gemm_f32_kernel<false, false, -1, true, true><<<dim3((unsigned)tiles, (unsigned)S, 2), kThreads, 0, st>>>(
+          R0, N, K, gn0, K, wT0, ldwT, nullptr, 0.f, 0, nullptr, N, kc, slab0, 1, 1, ProjEpi{},
+          BatchStrides{}, AmaxPtrs{gg_amax0, amax_w0}, CellEpi{},
+          DualPtrs{gn1, wT1, slab1, amax_w1, R1, CellEpi{}, gg_amax1});
+      int rc = check_launch("gemm_f32_kernel(bilstm step bwd)");
+      if (rc) return rc;
+    } else {
     const int64_t tiles = std::max(ceil_div(R0, XBM), ceil_div(R1, XBM)) * ceil_div(N, XBN);
     const dim3 grid((unsigned)tiles, (unsigned)S, 2);
     gemm_x3w_kernel<false, false, -1, true, 2><<<grid, kXThreads, 0, st>>>(
@@ -2617,6 +2674,7 @@ extern "C" int mvml_bilstm_wide_step_bwd(
         DualPtrs{gn1, wT1, slab1, amax_w1, R1, CellEpi{}, gg_amax1});
     int rc = check_launch("gemm_x3w_kernel(bilstm step bwd)");
     if (rc) return rc;
+    }
   }
   LstmBwdArgs a0, a1;
   a0.M = M0; a0.R = R0; a0.gout = gout0; a0.ldgo = ldgo; a0.slab = slab0; a0.act = act0; a0.c = c0;

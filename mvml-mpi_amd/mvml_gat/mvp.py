@@ -22,6 +22,19 @@ from .nn import GNNModule
 from .smiles import RNNModule, tokens_struct
 
 
+# run the SMILES view on a side stream beside the graph view (MVP.forward)
+OVERLAP_VIEWS = True
+_SIDE = {}
+
+
+def _side_stream(dev):
+    """One side stream per device, created once (its workspace and allocator blocks persist)."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
+
+
 class MVP(MVFusion):
     def __init__(self, num_classes, in_feats=64, hidden_feats=None, num_step_set2set=6,
                  num_layer_set2set=3, rnn_embed_dim=64, blstm_dim=128, blstm_layers=2, fp_2_dim=128,
@@ -39,8 +52,26 @@ class MVP(MVFusion):
         self.sigmoid = nn.Sigmoid()
 
     def forward(self, smiles, graphs, atom_feats, fp_t):
-        smiles_x = self.rnn(smiles)
-        graph_x = self.gnn(graphs, atom_feats)
+        # The SMILES and graph views are independent until the fusion (model.py:53-55): the
+        # BiLSTM recurrence (hundreds of short, latency-bound launches per step) runs on a side
+        # stream while the graph view's HBM / MFMA-bound kernels run on the current one, so the
+        # view kernels fill the CUs the recurrence leaves idle.  Autograd runs each op's backward
+        # on its forward stream, so the two backward passes overlap the same way; the fusion
+        # waits for both.  Same kernels, same arithmetic: results are bitwise those of running
+        # the views one after the other.
+        dev = atom_feats.device
+        if dev.type != "cuda" or not OVERLAP_VIEWS:
+            smiles_x = self.rnn(smiles)
+            graph_x = self.gnn(graphs, atom_feats)
+        else:
+            cur = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                smiles_x = self.rnn(smiles)
+            graph_x = self.gnn(graphs, atom_feats)
+            cur.wait_stream(side)
+            smiles_x.record_stream(cur)
         fp_x = self.fp_mlp(fp_t)
         # the shared LayerNorm (model.py:54-56), Q/K/V, attention, Conv2d and MLP
         return MVFusion.forward(self, smiles_x, graph_x, fp_x)

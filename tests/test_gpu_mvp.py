@@ -175,3 +175,38 @@ def test_mvp_train_step_bf16_projection():
     assert all(f < GRAD_FRO and c > GRAD_COS for f, c in worst.values()), worst
     opt.step()
     assert all(torch.isfinite(p).all() for p in mod.parameters())
+
+
+@pytest.mark.parametrize("n", [64, 600])
+def test_mvp_view_streams_bitwise(n):
+    """MVP.forward runs the SMILES view on a side stream beside the graph view: logits and every
+    parameter gradient are bitwise those of running the views one after the other (64 molecules:
+    the narrow BiLSTM path; 600 = the KEGG batch repeated: the wide path)."""
+    import mvml_gat.mvp as mvp_mod
+    from mvml_gat.featurize import MolDataSet, collate
+    from mvml_gat.smiles import collate_smiles, tokens_struct
+    ds = MolDataSet(os.path.join(HERE, "golden", "kegg_test_split.csv"))
+    idx = [i % 64 for i in range(n)]
+    bg, y = collate([ds[i] for i in idx])
+    smiles = collate_smiles([ds.smiles[i] for i in idx], tokens_struct())
+    fp = (torch.rand(n, 2513, generator=torch.Generator().manual_seed(3)) < 0.1).float()
+    mod, _, _ = _models(2)
+    g = bg.to(DEV)
+    batch = ({"smiles": smiles["smiles"].to(DEV), "seq_len": smiles["seq_len"]}, g, g.ndata["h"].to(DEV),
+             fp.to(DEV))
+    res = []
+    for overlap in (True, False):
+        old = mvp_mod.OVERLAP_VIEWS
+        mvp_mod.OVERLAP_VIEWS = overlap
+        try:
+            mod.zero_grad(set_to_none=True)
+            z = mod(*batch)
+            (z.square().mean()).backward()
+            torch.cuda.synchronize()
+            res.append([z.detach().clone()] + [p.grad.clone() for p in mod.parameters() if p.grad is not None])
+            del z  # drop this pass's autograd graph (its AccumulateGrad nodes carry their stream)
+        finally:
+            mvp_mod.OVERLAP_VIEWS = old
+    assert len(res[0]) == len(res[1])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

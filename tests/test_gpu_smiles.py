@@ -46,6 +46,17 @@ def test_rnn_module_parity_gemm_path(B, Tmax, layers, ragged, space, wide_step, 
     _rnn_parity(B, Tmax, layers, ragged, space)
 
 
+@pytest.mark.parametrize("B,Tmax,layers,ragged,space", [(64, 60, 2, True, False), (700, 25, 2, True, False)])
+def test_rnn_module_parity_wide_step_tile256(B, Tmax, layers, ragged, space, monkeypatch):
+    """The wide step launches on the 256x256 tile (option lstm_tile = 256; the planned tile at
+    these row counts is the 128x128 one, which the test above covers)."""
+    import mvml_gat.smiles as sm
+    from mvml_gat._lib import option
+    monkeypatch.setattr(sm, "SEQ_MAX_B", 0)
+    with option("lstm_tile", 256):
+        _rnn_parity(B, Tmax, layers, ragged, space)
+
+
 def _rnn_parity(B, Tmax, layers, ragged, space):
     from mvml_gat.smiles import RNNModule
     from oracle.smiles_ref import RNNModuleRef

@@ -25,10 +25,16 @@ SHAPES = [  # name, M, N, K, a_kmajor, b_kmajor
     ("L1 fwd  K=76", N_ATOMS, 1544, 76, 0, 0),
     ("LSTM dxh l>0 merged", B, 768, 1536, 0, 1),
     ("LSTM dxh l0 merged", B, 1152, 1536, 0, 1),
+    ("BiLSTM step fwd 1024", 1024, 1536, 384, 0, 0),
+    ("BiLSTM step fwd 2730", 2730, 1536, 384, 0, 0),
+    ("BiLSTM step fwd 8192", 8192, 1536, 384, 0, 0),
+    ("BiLSTM step bwd 1024", 1024, 384, 1536, 0, 1),
+    ("BiLSTM step bwd 2730", 2730, 384, 1536, 0, 1),
+    ("BiLSTM step bwd 8192", 8192, 384, 1536, 0, 1),
 ]
 
 
-def tf(fn, flops, it=10):
+def tf(fn, flops, it=30):
     fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
