@@ -2690,3 +2690,64 @@ extern "C" int mvml_bilstm_wide_step_bwd(
   lstm_step_bwd_kernel<<<dim3(blocks, 1, 2), 256, 0, st>>>(a0, a1, D);
   return check_launch("lstm_step_bwd_kernel");
 }
+
+// The whole recurrence of a wide bidirectional layer: every step's dual launch enqueued from this
+// loop (the host side of the recurrence is native, so enqueueing a step costs a few microseconds,
+// not a Python frame building some thirty arguments and tensor views per step).
+extern "C" int mvml_bilstm_wide_fwd(int64_t T, int64_t B, int D, const int32_t* batch_sizes,
+                                    const float* W0, const float* W1, const float* gx0,
+                                    const float* gx1, const float* bih0, const float* bhh0,
+                                    const float* bih1, const float* bhh1, float* c0, float* c1,
+                                    float* out, float* act0, float* act1, const uint32_t* amax,
+                                    void* stream) {
+  clear_error();
+  MVML_REQUIRE(T > 0 && B > 0 && D > 0 && batch_sizes && amax, "bilstm_wide_fwd: bad arguments");
+  for (int64_t t = 0; t < T; ++t)
+    MVML_REQUIRE(batch_sizes[t] > 0 && batch_sizes[t] <= B && (t == 0 || batch_sizes[t] <= batch_sizes[t - 1]),
+                 "bilstm_wide_fwd: batch_sizes must be positive, <= B and non-increasing");
+  const int64_t G = 4 * (int64_t)D, H2 = 2 * (int64_t)D;
+  for (int64_t s = 0; s < T; ++s) {
+    const int64_t t0 = s, t1 = T - 1 - s, p0 = t0 - 1, p1 = t1 + 1;
+    const bool first = s == 0;
+    const int rc = mvml_bilstm_wide_step_fwd(
+        batch_sizes[t0], batch_sizes[t1], D, first ? 0 : D, first ? nullptr : out + p0 * B * H2,
+        first ? nullptr : out + p1 * B * H2 + D, H2, W0, W1, D, gx0 + t0 * B * G, gx1 + t1 * B * G, G,
+        bih0, bhh0, bih1, bhh1, first ? nullptr : c0 + p0 * B * D, first ? nullptr : c1 + p1 * B * D,
+        c0 + t0 * B * D, c1 + t1 * B * D, out + t0 * B * H2, out + t1 * B * H2 + D, H2,
+        act0 + t0 * B * G, act1 + t1 * B * G, amax, amax + 1, amax + 2, stream);
+    if (rc) return rc;
+  }
+  return MVML_OK;
+}
+
+extern "C" int mvml_bilstm_wide_bwd(int64_t T, int64_t B, int D, const int32_t* batch_sizes,
+                                    const float* wT0, const float* wT1, const float* gout,
+                                    const float* act0, const float* act1, const float* c0,
+                                    const float* c1, float* carry, float* gg0, float* gg1,
+                                    uint32_t* gg_amax, const uint32_t* amax, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  clear_error();
+  MVML_REQUIRE(T > 0 && B > 0 && D > 0 && batch_sizes && carry && gg_amax && amax,
+               "bilstm_wide_bwd: bad arguments");
+  for (int64_t t = 0; t < T; ++t)
+    MVML_REQUIRE(batch_sizes[t] > 0 && batch_sizes[t] <= B && (t == 0 || batch_sizes[t] <= batch_sizes[t - 1]),
+                 "bilstm_wide_bwd: batch_sizes must be positive, <= B and non-increasing");
+  const int64_t G = 4 * (int64_t)D, H2 = 2 * (int64_t)D, BD = B * (int64_t)D;
+  // carry: [direction][ping-pong][B][D]
+  float* cr[2][2] = {{carry, carry + BD}, {carry + 2 * BD, carry + 3 * BD}};
+  for (int64_t s = 0; s < T; ++s) {
+    const int64_t t0 = T - 1 - s, t1 = s, n0 = t0 + 1, n1 = t1 - 1;  // n: the steps these fed
+    const int64_t R0 = s == 0 ? 0 : std::min(batch_sizes[t0], batch_sizes[n0]);
+    const int64_t R1 = s == 0 ? 0 : std::min(batch_sizes[t1], batch_sizes[n1]);
+    const int ci = (int)(s % 2), co = (int)((s + 1) % 2);
+    const int rc = mvml_bilstm_wide_step_bwd(
+        batch_sizes[t0], batch_sizes[t1], R0, R1, D, gg0 + (s ? n0 : t0) * B * G,
+        gg1 + (s ? n1 : t1) * B * G, wT0, wT1, G, gout + t0 * B * H2, gout + t1 * B * H2 + D, H2,
+        act0 + t0 * B * G, act1 + t1 * B * G, c0 + t0 * BD, c1 + t1 * BD,
+        t0 >= 1 ? c0 + (t0 - 1) * BD : nullptr, t1 + 1 < T ? c1 + (t1 + 1) * BD : nullptr,
+        cr[0][ci], cr[1][ci], cr[0][co], cr[1][co], gg0 + t0 * B * G, gg1 + t1 * B * G, gg_amax,
+        gg_amax + 1, amax + 1, amax + 2, workspace, workspace_bytes, stream);
+    if (rc) return rc;
+  }
+  return MVML_OK;
+}

@@ -196,18 +196,9 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             bias = [(_c(w[4 * d + 2]), _c(w[4 * d + 3])) for d in range(2)]
             c = [torch.zeros((T, B, H), dtype=torch.float32, device=dev) for _ in range(2)]
             act = [torch.empty((T, B, G), dtype=torch.float32, device=dev) for _ in range(2)]
-            for s in range(T):
-                t0, t1 = s, T - 1 - s
-                first = s == 0
-                p0, p1 = t0 - 1, t1 + 1
-                call("mvml_bilstm_wide_step_fwd", pk.batch_sizes[t0], pk.batch_sizes[t1], H,
-                     0 if first else H, None if first else ptr(out[p0, :, :H]),
-                     None if first else ptr(out[p1, :, H:]), 2 * H, ptr(wperm[0]), ptr(wperm[1]), H,
-                     ptr(gates_d[0][t0]), ptr(gates_d[1][t1]), G, ptr(bias[0][0]), ptr(bias[0][1]),
-                     ptr(bias[1][0]), ptr(bias[1][1]), None if first else ptr(c[0][p0]),
-                     None if first else ptr(c[1][p1]), ptr(c[0][t0]), ptr(c[1][t1]),
-                     ptr(out[t0, :, :H]), ptr(out[t1, :, H:]), 2 * H, ptr(act[0][t0]), ptr(act[1][t1]),
-                     slot(amx, 0), slot(amx, 1), slot(amx, 2), st)
+            call("mvml_bilstm_wide_fwd", T, B, H, ptr(pk.batch_sizes_host), ptr(wperm[0]), ptr(wperm[1]),
+                 ptr(gates_d[0]), ptr(gates_d[1]), ptr(bias[0][0]), ptr(bias[0][1]), ptr(bias[1][0]),
+                 ptr(bias[1][1]), ptr(c[0]), ptr(c[1]), ptr(out), ptr(act[0]), ptr(act[1]), ptr(amx), st)
             saved = [c[0], act[0], c[1], act[1]]
         else:  # wide batches, other GEMM algorithms: per-step GEMM (beta = 1 onto the projection) + cell kernel
             amx = _h_bounds(w, dev)
@@ -263,25 +254,12 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         if not seq and WIDE_STEP and amx is not None:
             # wide batches: one launch per step for both directions (the recurrent product split in
             # two K halves) + one fused reduce / cell-backward launch (mvml_bilstm_wide_step_bwd)
-            carry = [[torch.zeros((B, H), dtype=torch.float32, device=dev) for _ in range(2)]
-                     for _ in range(2)]
+            carry = torch.zeros((2, 2, B, H), dtype=torch.float32, device=dev)
             nws = int(lib().mvml_bilstm_wide_step_bwd_workspace_size(B, H))
             ws = workspace(nws, dev)
-            bsz = pk.batch_sizes
-            for s in range(T):
-                t0, t1 = T - 1 - s, s
-                n0, n1 = t0 + 1, t1 - 1  # the steps these fed
-                R0 = 0 if s == 0 else min(bsz[t0], bsz[n0])
-                R1 = 0 if s == 0 else min(bsz[t1], bsz[n1])
-                ci, co = s % 2, (s + 1) % 2
-                call("mvml_bilstm_wide_step_bwd", bsz[t0], bsz[t1], R0, R1, H,
-                     ptr(ggs[0][n0 if s else t0]), ptr(ggs[1][n1 if s else t1]), ptr(w_hhT[0]),
-                     ptr(w_hhT[1]), G, ptr(g[t0, :, :H]), ptr(g[t1, :, H:]), 2 * H, ptr(acts[0][t0]),
-                     ptr(acts[1][t1]), ptr(cs[0][t0]), ptr(cs[1][t1]),
-                     ptr(cs[0][t0 - 1]) if t0 >= 1 else None, ptr(cs[1][t1 + 1]) if t1 + 1 < T else None,
-                     ptr(carry[0][ci]), ptr(carry[1][ci]), ptr(carry[0][co]), ptr(carry[1][co]),
-                     ptr(ggs[0][t0]), ptr(ggs[1][t1]), slot(amg, 0), slot(amg, 1), slot(amx, 1),
-                     slot(amx, 2), ptr(ws), nws, st)
+            call("mvml_bilstm_wide_bwd", T, B, H, ptr(pk.batch_sizes_host), ptr(w_hhT[0]), ptr(w_hhT[1]),
+                 ptr(g), ptr(acts[0]), ptr(acts[1]), ptr(cs[0]), ptr(cs[1]), ptr(carry), ptr(ggs[0]),
+                 ptr(ggs[1]), ptr(amg), ptr(amx), ptr(ws), nws, st)
         elif not seq:  # wide batches: per-step recurrent GEMM (beta = 1 into g) + cell kernel
             g = g.clone()
             for d in range(2):
