@@ -17,3 +17,6 @@ head -n 14 $OUT/kernel_stats.csv | cut -c1-200
 timeout -k 10 400 python -u bench.py --workload mvp --steps 6 --warmup 2 --no-cpu-baseline \
   --view-only-steps 0 --no-inference > $OUT/mvp.json 2> $OUT/mvp.err || { tail -30 $OUT/mvp.err; exit 1; }
 head -c 300 $OUT/mvp.json; echo; grep -E "mvml_" $OUT/mvp.err | head -12
+timeout -k 10 400 python -u bench.py --workload mvp --proj-bf16 --steps 6 --warmup 2 --no-cpu-baseline \
+  --view-only-steps 0 --no-inference > $OUT/mvp_bf16.json 2> $OUT/mvp_bf16.err || { tail -30 $OUT/mvp_bf16.err; exit 1; }
+head -c 300 $OUT/mvp_bf16.json; echo
