@@ -461,7 +461,9 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
 // X3: fp32-accurate products from split fp32 fragments — H2 = false: split-bf16 (six MFMAs per
 // fragment pair); H2 = true: scaled split-fp16 (three; operand scales from amax, as the 256x256
 // kernel's NP = 2), the skinny products' plan when the algorithm is f16x2.
-template <bool AK, bool BKM, int EPI_LOGW = -1, bool X3 = false, bool H2 = false>
+// BPS (H2, K-contiguous B only): B is the interleaved pre-split of the operand
+// (split_f16x2_il_kernel), so the B fragments need no split.
+template <bool AK, bool BKM, int EPI_LOGW = -1, bool X3 = false, bool H2 = false, bool BPS = false>
 __global__ void __launch_bounds__(kThreads, 2)
 gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
@@ -470,6 +472,7 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
                 BatchStrides bst = BatchStrides{}, AmaxPtrs amax = AmaxPtrs{},
                 CellEpi cep = CellEpi{}, DualPtrs dual = DualPtrs{}) {
   static_assert(!H2 || X3, "split-fp16 is a split product");
+  static_assert(!BPS || (H2 && !BKM), "pre-split B: split-fp16, K-contiguous B");
   if (blockIdx.z) {  // strided batch
     A += blockIdx.z * bst.a;
     B += blockIdx.z * bst.b;
@@ -581,8 +584,15 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       for (int T = 0; T < 2; ++T) {
         split2h8(f[T][0][0], f[T][0][1], s_a, pa[0][0], pa[0][1]);
         split2h8(f[T][1][0], f[T][1][1], s_a, pa[1][0], pa[1][1]);
-        split2h8(f[T][2][0], f[T][2][1], s_b, pb[0][0], pb[0][1]);
-        split2h8(f[T][3][0], f[T][3][1], s_b, pb[1][0], pb[1][1]);
+        if constexpr (BPS) {
+          pb[0][0] = __builtin_bit_cast(bf16x8, f[T][2][0]);
+          pb[0][1] = __builtin_bit_cast(bf16x8, f[T][2][1]);
+          pb[1][0] = __builtin_bit_cast(bf16x8, f[T][3][0]);
+          pb[1][1] = __builtin_bit_cast(bf16x8, f[T][3][1]);
+        } else {
+          split2h8(f[T][2][0], f[T][2][1], s_b, pb[0][0], pb[0][1]);
+          split2h8(f[T][3][0], f[T][3][1], s_b, pb[1][0], pb[1][1]);
+        }
         acc[0][0] = mfma_np<2>(pa[0], pb[0], acc[0][0]);
         acc[0][1] = mfma_np<2>(pa[0], pb[1], acc[0][1]);
         acc[1][0] = mfma_np<2>(pa[1], pb[0], acc[1][0]);
@@ -2098,6 +2108,35 @@ __global__ void __launch_bounds__(256) split_f16x2_kernel(int64_t rows, int64_t 
   }
 }
 
+// Interleaved pre-split of a K-contiguous operand for the 128x128 kernel's BPS path: every
+// 8-value k group becomes its 8 scaled high fp16 halves then its 8 low halves (split2h8's h, l),
+// 32 B in place of the group's 32 B of fp32, so the LDS-DMA staging and the swizzle are unchanged
+// and a fragment read yields the two MFMA operands ready-made.  K % 8 == 0 (host).
+__global__ void __launch_bounds__(256) split_f16x2_il_kernel(int64_t rows, int64_t groups,
+                                                             const float* __restrict__ P, int64_t ld,
+                                                             const uint32_t* __restrict__ amax,
+                                                             float* __restrict__ out) {
+  const float sc = pow2f(amax_shift(*amax));
+  const int64_t total = rows * groups;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t r = e / groups, c = 8 * (e - r * groups);
+    const float* src = P + r * ld + c;
+    bf16x8 h, l;
+    split2h8(*reinterpret_cast<const float4*>(src), *reinterpret_cast<const float4*>(src + 4), sc, h, l);
+    float* dst = out + r * ld + c;
+    *reinterpret_cast<float4*>(dst) = __builtin_bit_cast(float4, h);
+    *reinterpret_cast<float4*>(dst + 4) = __builtin_bit_cast(float4, l);
+  }
+}
+
+int split_il_launch(int64_t rows, int64_t K, const float* P, const uint32_t* amax, float* out,
+                    hipStream_t st) {
+  const int64_t total = rows * (K / 8);
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(total, 256), 4096));
+  split_f16x2_il_kernel<<<blocks, 256, 0, st>>>(rows, K / 8, P, K, amax, out);
+  return check_launch("split_f16x2_il_kernel");
+}
+
 int absmax_launch(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32_t* out,
                   bool accumulate, hipStream_t st) {
   if (!accumulate && hipMemsetAsync(out, 0, sizeof(uint32_t), st) != hipSuccess) {
@@ -2587,14 +2626,15 @@ bool lstm_small_tile(int64_t rows, bool bwd) {
 }
 }  // namespace
 
-extern "C" int mvml_bilstm_wide_step_fwd(
+// Wi_d: W_d's interleaved pre-split (split_il_launch, ld K) or null — the 128x128 plan then
+// reads B ready-split (W is the same for every step of the layer).
+static int wide_step_fwd(
     int64_t M0, int64_t M1, int D, int64_t K, const float* A0, const float* A1, int64_t lda,
     const float* W0, const float* W1, int64_t ldw, const float* gx0, const float* gx1,
     int64_t ldgx, const float* bih0, const float* bhh0, const float* bih1, const float* bhh1,
     const float* cprev0, const float* cprev1, float* c0, float* c1, float* h0, float* h1,
     int64_t ldh, float* act0, float* act1, const uint32_t* amax_a, const uint32_t* amax_w0,
-    const uint32_t* amax_w1, void* stream) {
-  clear_error();
+    const uint32_t* amax_w1, void* stream, const float* Wi0, const float* Wi1) {
   const int64_t N = 4 * (int64_t)D;
   MVML_REQUIRE(M0 > 0 && M1 > 0 && D > 0 && K >= 0 && K % 4 == 0 && ldw >= K && ldw % 4 == 0 &&
                    ldgx >= N && ldh >= D && amax_a && amax_w0 && amax_w1 && MVML_X3W_LDSEPI,
@@ -2613,9 +2653,15 @@ extern "C" int mvml_bilstm_wide_step_fwd(
   const float* a1 = K ? A1 : gx1;
   if (lstm_small_tile(std::max(M0, M1), false)) {
     const int64_t tiles = ceil_div(std::max(M0, M1), BM) * ceil_div(N, BN);
-    gemm_f32_kernel<false, false, -1, true, true><<<dim3((unsigned)tiles, 1, 2), kThreads, 0, as_stream(stream)>>>(
-        M0, N, K, a0, K ? lda : 4, W0, ldw, nullptr, 0.f, 0, nullptr, N, K > 0 ? K : 1, nullptr, 1, 1,
-        ProjEpi{}, BatchStrides{}, AmaxPtrs{amax_a, amax_w0}, e0, DualPtrs{a1, W1, nullptr, amax_w1, M1, e1});
+    const dim3 grid((unsigned)tiles, 1, 2);
+    if (Wi0 && Wi1 && K % BKT == 0)
+      gemm_f32_kernel<false, false, -1, true, true, true><<<grid, kThreads, 0, as_stream(stream)>>>(
+          M0, N, K, a0, K ? lda : 4, Wi0, K, nullptr, 0.f, 0, nullptr, N, K > 0 ? K : 1, nullptr, 1, 1,
+          ProjEpi{}, BatchStrides{}, AmaxPtrs{amax_a, amax_w0}, e0, DualPtrs{a1, Wi1, nullptr, amax_w1, M1, e1});
+    else
+      gemm_f32_kernel<false, false, -1, true, true><<<grid, kThreads, 0, as_stream(stream)>>>(
+          M0, N, K, a0, K ? lda : 4, W0, ldw, nullptr, 0.f, 0, nullptr, N, K > 0 ? K : 1, nullptr, 1, 1,
+          ProjEpi{}, BatchStrides{}, AmaxPtrs{amax_a, amax_w0}, e0, DualPtrs{a1, W1, nullptr, amax_w1, M1, e1});
     return check_launch("gemm_f32_kernel(bilstm step)");
   }
   const int64_t tn = ceil_div(N, XBN);
@@ -2627,19 +2673,31 @@ extern "C" int mvml_bilstm_wide_step_fwd(
   return check_launch("gemm_x3w_kernel(bilstm step)");
 }
 
+extern "C" int mvml_bilstm_wide_step_fwd(
+    int64_t M0, int64_t M1, int D, int64_t K, const float* A0, const float* A1, int64_t lda,
+    const float* W0, const float* W1, int64_t ldw, const float* gx0, const float* gx1,
+    int64_t ldgx, const float* bih0, const float* bhh0, const float* bih1, const float* bhh1,
+    const float* cprev0, const float* cprev1, float* c0, float* c1, float* h0, float* h1,
+    int64_t ldh, float* act0, float* act1, const uint32_t* amax_a, const uint32_t* amax_w0,
+    const uint32_t* amax_w1, void* stream) {
+  clear_error();
+  return wide_step_fwd(M0, M1, D, K, A0, A1, lda, W0, W1, ldw, gx0, gx1, ldgx, bih0, bhh0, bih1,
+                       bhh1, cprev0, cprev1, c0, c1, h0, h1, ldh, act0, act1, amax_a, amax_w0, amax_w1,
+                       stream, nullptr, nullptr);
+}
+
 extern "C" size_t mvml_bilstm_wide_step_bwd_workspace_size(int64_t M, int D) {
   return 2 * carve_size((size_t)2 * M * D * sizeof(float));
 }
 
-extern "C" int mvml_bilstm_wide_step_bwd(
+static int wide_step_bwd(
     int64_t M0, int64_t M1, int64_t R0, int64_t R1, int D, const float* gn0, const float* gn1,
     const float* wT0, const float* wT1, int64_t ldwT, const float* gout0, const float* gout1,
     int64_t ldgo, const float* act0, const float* act1, const float* c0, const float* c1,
     const float* cp0, const float* cp1, const float* carry_in0, const float* carry_in1,
     float* carry_out0, float* carry_out1, float* gg0, float* gg1, uint32_t* gg_amax0,
     uint32_t* gg_amax1, const uint32_t* amax_w0, const uint32_t* amax_w1, void* workspace,
-    size_t workspace_bytes, void* stream) {
-  clear_error();
+    size_t workspace_bytes, void* stream, const float* Wi0, const float* Wi1) {
   const int64_t K = 4 * (int64_t)D, N = D;
   MVML_REQUIRE(M0 > 0 && M1 > 0 && R0 >= 0 && R0 <= M0 && R1 >= 0 && R1 <= M1 && (R0 > 0) == (R1 > 0) &&
                    D > 0 && D % 4 == 0 && ldwT >= K && ldwT % 4 == 0 && ldgo >= D && gg_amax0 &&
@@ -2659,10 +2717,17 @@ extern "C" int mvml_bilstm_wide_step_bwd(
     const int64_t kc = k_chunk(K, S);
     if (lstm_small_tile(std::max(R0, R1), true)) {
       const int64_t tiles = ceil_div(std::max(R0, R1), BM) * ceil_div(N, BN);
-      gemm_f32_kernel<false, false, -1, true, true><<<dim3((unsigned)tiles, (unsigned)S, 2), kThreads, 0, st>>>(
-          R0, N, K, gn0, K, wT0, ldwT, nullptr, 0.f, 0, nullptr, N, kc, slab0, 1, 1, ProjEpi{},
-          BatchStrides{}, AmaxPtrs{gg_amax0, amax_w0}, CellEpi{},
-          DualPtrs{gn1, wT1, slab1, amax_w1, R1, CellEpi{}, gg_amax1});
+      const dim3 grid((unsigned)tiles, (unsigned)S, 2);
+      if (Wi0 && Wi1 && kc % BKT == 0)
+        gemm_f32_kernel<false, false, -1, true, true, true><<<grid, kThreads, 0, st>>>(
+            R0, N, K, gn0, K, Wi0, K, nullptr, 0.f, 0, nullptr, N, kc, slab0, 1, 1, ProjEpi{},
+            BatchStrides{}, AmaxPtrs{gg_amax0, amax_w0}, CellEpi{},
+            DualPtrs{gn1, Wi1, slab1, amax_w1, R1, CellEpi{}, gg_amax1});
+      else
+        gemm_f32_kernel<false, false, -1, true, true><<<grid, kThreads, 0, st>>>(
+            R0, N, K, gn0, K, wT0, ldwT, nullptr, 0.f, 0, nullptr, N, kc, slab0, 1, 1, ProjEpi{},
+            BatchStrides{}, AmaxPtrs{gg_amax0, amax_w0}, CellEpi{},
+            DualPtrs{gn1, wT1, slab1, amax_w1, R1, CellEpi{}, gg_amax1});
       int rc = check_launch("gemm_f32_kernel(bilstm step bwd)");
       if (rc) return rc;
     } else {
@@ -2691,33 +2756,68 @@ extern "C" int mvml_bilstm_wide_step_bwd(
   return check_launch("lstm_step_bwd_kernel");
 }
 
+extern "C" int mvml_bilstm_wide_step_bwd(
+    int64_t M0, int64_t M1, int64_t R0, int64_t R1, int D, const float* gn0, const float* gn1,
+    const float* wT0, const float* wT1, int64_t ldwT, const float* gout0, const float* gout1,
+    int64_t ldgo, const float* act0, const float* act1, const float* c0, const float* c1,
+    const float* cp0, const float* cp1, const float* carry_in0, const float* carry_in1,
+    float* carry_out0, float* carry_out1, float* gg0, float* gg1, uint32_t* gg_amax0,
+    uint32_t* gg_amax1, const uint32_t* amax_w0, const uint32_t* amax_w1, void* workspace,
+    size_t workspace_bytes, void* stream) {
+  clear_error();
+  return wide_step_bwd(M0, M1, R0, R1, D, gn0, gn1, wT0, wT1, ldwT, gout0, gout1, ldgo, act0, act1,
+                       c0, c1, cp0, cp1, carry_in0, carry_in1, carry_out0, carry_out1, gg0, gg1,
+                       gg_amax0, gg_amax1, amax_w0, amax_w1, workspace, workspace_bytes, stream,
+                       nullptr, nullptr);
+}
+
 // The whole recurrence of a wide bidirectional layer: every step's dual launch enqueued from this
 // loop (the host side of the recurrence is native, so enqueueing a step costs a few microseconds,
 // not a Python frame building some thirty arguments and tensor views per step).
+// Both layer loops pre-split W_hh (resp. its transpose) once into the workspace: every step's
+// 128x128 launch then reads B ready-split (split_f16x2_il_kernel) instead of splitting it again in
+// every workgroup of every step.
+extern "C" size_t mvml_bilstm_wide_fwd_workspace_size(int D) {
+  return 2 * carve_size((size_t)4 * D * D * sizeof(float));
+}
+
 extern "C" int mvml_bilstm_wide_fwd(int64_t T, int64_t B, int D, const int32_t* batch_sizes,
                                     const float* W0, const float* W1, const float* gx0,
                                     const float* gx1, const float* bih0, const float* bhh0,
                                     const float* bih1, const float* bhh1, float* c0, float* c1,
                                     float* out, float* act0, float* act1, const uint32_t* amax,
-                                    void* stream) {
+                                    void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
-  MVML_REQUIRE(T > 0 && B > 0 && D > 0 && batch_sizes && amax, "bilstm_wide_fwd: bad arguments");
+  MVML_REQUIRE(T > 0 && B > 0 && D > 0 && D % 8 == 0 && batch_sizes && amax,
+               "bilstm_wide_fwd: bad arguments");
+  MVML_REQUIRE(workspace && workspace_bytes >= mvml_bilstm_wide_fwd_workspace_size(D),
+               "bilstm_wide_fwd: workspace of mvml_bilstm_wide_fwd_workspace_size bytes required");
   for (int64_t t = 0; t < T; ++t)
     MVML_REQUIRE(batch_sizes[t] > 0 && batch_sizes[t] <= B && (t == 0 || batch_sizes[t] <= batch_sizes[t - 1]),
                  "bilstm_wide_fwd: batch_sizes must be positive, <= B and non-increasing");
   const int64_t G = 4 * (int64_t)D, H2 = 2 * (int64_t)D;
+  float* Wi0 = static_cast<float*>(workspace);
+  float* Wi1 = reinterpret_cast<float*>(static_cast<char*>(workspace) + carve_size((size_t)G * D * sizeof(float)));
+  hipStream_t st = as_stream(stream);
+  int rc0 = split_il_launch(G, D, W0, amax + 1, Wi0, st);
+  if (!rc0) rc0 = split_il_launch(G, D, W1, amax + 2, Wi1, st);
+  if (rc0) return rc0;
   for (int64_t s = 0; s < T; ++s) {
     const int64_t t0 = s, t1 = T - 1 - s, p0 = t0 - 1, p1 = t1 + 1;
     const bool first = s == 0;
-    const int rc = mvml_bilstm_wide_step_fwd(
+    const int rc = wide_step_fwd(
         batch_sizes[t0], batch_sizes[t1], D, first ? 0 : D, first ? nullptr : out + p0 * B * H2,
         first ? nullptr : out + p1 * B * H2 + D, H2, W0, W1, D, gx0 + t0 * B * G, gx1 + t1 * B * G, G,
         bih0, bhh0, bih1, bhh1, first ? nullptr : c0 + p0 * B * D, first ? nullptr : c1 + p1 * B * D,
         c0 + t0 * B * D, c1 + t1 * B * D, out + t0 * B * H2, out + t1 * B * H2 + D, H2,
-        act0 + t0 * B * G, act1 + t1 * B * G, amax, amax + 1, amax + 2, stream);
+        act0 + t0 * B * G, act1 + t1 * B * G, amax, amax + 1, amax + 2, stream, Wi0, Wi1);
     if (rc) return rc;
   }
   return MVML_OK;
+}
+
+extern "C" size_t mvml_bilstm_wide_bwd_workspace_size(int64_t B, int D) {
+  return mvml_bilstm_wide_step_bwd_workspace_size(B, D) + 2 * carve_size((size_t)4 * D * D * sizeof(float));
 }
 
 extern "C" int mvml_bilstm_wide_bwd(int64_t T, int64_t B, int D, const int32_t* batch_sizes,
@@ -2727,26 +2827,35 @@ extern "C" int mvml_bilstm_wide_bwd(int64_t T, int64_t B, int D, const int32_t* 
                                     uint32_t* gg_amax, const uint32_t* amax, void* workspace,
                                     size_t workspace_bytes, void* stream) {
   clear_error();
-  MVML_REQUIRE(T > 0 && B > 0 && D > 0 && batch_sizes && carry && gg_amax && amax,
+  MVML_REQUIRE(T > 0 && B > 0 && D > 0 && D % 8 == 0 && batch_sizes && carry && gg_amax && amax,
                "bilstm_wide_bwd: bad arguments");
+  MVML_REQUIRE(workspace && workspace_bytes >= mvml_bilstm_wide_bwd_workspace_size(B, D),
+               "bilstm_wide_bwd: workspace of mvml_bilstm_wide_bwd_workspace_size bytes required");
   for (int64_t t = 0; t < T; ++t)
     MVML_REQUIRE(batch_sizes[t] > 0 && batch_sizes[t] <= B && (t == 0 || batch_sizes[t] <= batch_sizes[t - 1]),
                  "bilstm_wide_bwd: batch_sizes must be positive, <= B and non-increasing");
   const int64_t G = 4 * (int64_t)D, H2 = 2 * (int64_t)D, BD = B * (int64_t)D;
   // carry: [direction][ping-pong][B][D]
   float* cr[2][2] = {{carry, carry + BD}, {carry + 2 * BD, carry + 3 * BD}};
+  const size_t slabs = mvml_bilstm_wide_step_bwd_workspace_size(B, D);
+  float* Wi0 = reinterpret_cast<float*>(static_cast<char*>(workspace) + slabs);
+  float* Wi1 = reinterpret_cast<float*>(static_cast<char*>(workspace) + slabs + carve_size((size_t)G * D * sizeof(float)));
+  hipStream_t st = as_stream(stream);
+  int rc0 = split_il_launch(D, G, wT0, amax + 1, Wi0, st);  // W_hh^T: D rows of K = 4 D
+  if (!rc0) rc0 = split_il_launch(D, G, wT1, amax + 2, Wi1, st);
+  if (rc0) return rc0;
   for (int64_t s = 0; s < T; ++s) {
     const int64_t t0 = T - 1 - s, t1 = s, n0 = t0 + 1, n1 = t1 - 1;  // n: the steps these fed
     const int64_t R0 = s == 0 ? 0 : std::min(batch_sizes[t0], batch_sizes[n0]);
     const int64_t R1 = s == 0 ? 0 : std::min(batch_sizes[t1], batch_sizes[n1]);
     const int ci = (int)(s % 2), co = (int)((s + 1) % 2);
-    const int rc = mvml_bilstm_wide_step_bwd(
+    const int rc = wide_step_bwd(
         batch_sizes[t0], batch_sizes[t1], R0, R1, D, gg0 + (s ? n0 : t0) * B * G,
         gg1 + (s ? n1 : t1) * B * G, wT0, wT1, G, gout + t0 * B * H2, gout + t1 * B * H2 + D, H2,
         act0 + t0 * B * G, act1 + t1 * B * G, c0 + t0 * BD, c1 + t1 * BD,
         t0 >= 1 ? c0 + (t0 - 1) * BD : nullptr, t1 + 1 < T ? c1 + (t1 + 1) * BD : nullptr,
         cr[0][ci], cr[1][ci], cr[0][co], cr[1][co], gg0 + t0 * B * G, gg1 + t1 * B * G, gg_amax,
-        gg_amax + 1, amax + 1, amax + 2, workspace, workspace_bytes, stream);
+        gg_amax + 1, amax + 1, amax + 2, workspace, slabs, stream, Wi0, Wi1);
     if (rc) return rc;
   }
   return MVML_OK;

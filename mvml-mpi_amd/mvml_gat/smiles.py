@@ -196,9 +196,12 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             bias = [(_c(w[4 * d + 2]), _c(w[4 * d + 3])) for d in range(2)]
             c = [torch.zeros((T, B, H), dtype=torch.float32, device=dev) for _ in range(2)]
             act = [torch.empty((T, B, G), dtype=torch.float32, device=dev) for _ in range(2)]
+            nws = int(lib().mvml_bilstm_wide_fwd_workspace_size(H))
+            ws = workspace(nws, dev)
             call("mvml_bilstm_wide_fwd", T, B, H, ptr(pk.batch_sizes_host), ptr(wperm[0]), ptr(wperm[1]),
                  ptr(gates_d[0]), ptr(gates_d[1]), ptr(bias[0][0]), ptr(bias[0][1]), ptr(bias[1][0]),
-                 ptr(bias[1][1]), ptr(c[0]), ptr(c[1]), ptr(out), ptr(act[0]), ptr(act[1]), ptr(amx), st)
+                 ptr(bias[1][1]), ptr(c[0]), ptr(c[1]), ptr(out), ptr(act[0]), ptr(act[1]), ptr(amx),
+                 ptr(ws), nws, st)
             saved = [c[0], act[0], c[1], act[1]]
         else:  # wide batches, other GEMM algorithms: per-step GEMM (beta = 1 onto the projection) + cell kernel
             amx = _h_bounds(w, dev)
@@ -255,7 +258,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             # wide batches: one launch per step for both directions (the recurrent product split in
             # two K halves) + one fused reduce / cell-backward launch (mvml_bilstm_wide_step_bwd)
             carry = torch.zeros((2, 2, B, H), dtype=torch.float32, device=dev)
-            nws = int(lib().mvml_bilstm_wide_step_bwd_workspace_size(B, H))
+            nws = int(lib().mvml_bilstm_wide_bwd_workspace_size(B, H))
             ws = workspace(nws, dev)
             call("mvml_bilstm_wide_bwd", T, B, H, ptr(pk.batch_sizes_host), ptr(w_hhT[0]), ptr(w_hhT[1]),
                  ptr(g), ptr(acts[0]), ptr(acts[1]), ptr(cs[0]), ptr(cs[1]), ptr(carry), ptr(ggs[0]),

@@ -57,6 +57,32 @@ def test_rnn_module_parity_wide_step_tile256(B, Tmax, layers, ragged, space, mon
         _rnn_parity(B, Tmax, layers, ragged, space)
 
 
+def test_wide_step_plans_bitwise(monkeypatch):
+    """The planned wide-step launches (128x128 tile, W_hh pre-split once per layer) and the
+    256x256 tile (W_hh split in every workgroup) round identically: the same scales, the same
+    split, the same k order — output and every gradient bitwise equal."""
+    import mvml_gat.smiles as sm
+    from mvml_gat._lib import option
+    from mvml_gat.smiles import RNNModule
+    monkeypatch.setattr(sm, "SEQ_MAX_B", 0)
+    torch.manual_seed(5)
+    vocab, batch = _batch(700, 11, 25, True, False)
+    mod = RNNModule(vocab, 128, 384, 2, 384, 0.5).to(DEV).eval()
+    inp = {"smiles": batch["smiles"].to(DEV), "seq_len": batch["seq_len"]}
+    res = []
+    for tile in (0, 256):
+        with option("lstm_tile", tile):
+            mod.zero_grad(set_to_none=True)
+            z = mod(inp)
+            z.square().sum().backward()
+            torch.cuda.synchronize()
+            res.append([z.detach().clone()] + [p.grad.clone() for p in mod.parameters() if p.grad is not None])
+            del z
+    assert len(res[0]) == len(res[1]) > 1
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def _rnn_parity(B, Tmax, layers, ragged, space):
     from mvml_gat.smiles import RNNModule
     from oracle.smiles_ref import RNNModuleRef
