@@ -224,6 +224,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                     prev = t
                 saved += [c, act]
         ctx.pk, ctx.layer0, ctx.H = pk, layer0, H
+        ctx.xp = xp  # the packed live input rows: the weight gradient reads them again
         ctx.save_for_backward(x, out, *saved, *w)
         return out
 
@@ -288,7 +289,8 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         packed = not seq and WIDE_PACK and In % 4 == 0
         if packed:
             offs, n_live = pk.live_offsets(0, T)
-            xp = None if layer0 else _pack(pk, x, In, In)
+            xp = None if layer0 else (ctx.xp if ctx.xp is not None else _pack(pk, x, In, In))
+            ctx.xp = None
             gxp = None if layer0 else torch.empty((n_live, In), dtype=torch.float32, device=dev)
             g_x = g_x if layer0 else torch.zeros_like(x)
         for d in range(2):
@@ -301,7 +303,9 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             if T > 1:
                 if packed:  # pairs (gg[t], h[t -+ 1]) of the live rows of gg
                     t0, t1, sh = (1, T, -1) if d == 0 else (0, T - 1, 1)
-                    A = _pack(pk, gg, G, G, t0, t1)
+                    # gg's live rows of steps [t0, t1) are a contiguous slice of ggp (steps
+                    # [1, T): all but the first step's rows; [0, T - 1): all but the last's)
+                    A = ggp[pk.batch_sizes[0]:] if d == 0 else ggp[:rows - pk.batch_sizes[T - 1]]
                     Bm = _pack(pk, out[:, :, d * H:], H, 2 * H, t0, t1, sh)
                     gemm(A, Bm, G, H, A.shape[0], 1, 1, G, H, g_whh, H,  # Bm = h: |h| < 1
                          amax=None if amg is None else (slot(amg, d), slot(amx, 0)))
