@@ -525,19 +525,22 @@ int mvml_bilstm_wide_step_bwd(int64_t M0, int64_t M1, int64_t R0, int64_t R1, in
  *        out [T][B][2D] (direction d in columns d D ..); act_d [T][B][4D]; amax[3] = bits of
  *        (1.0, max |W_hh_0|, max |W_hh_1|); workspace mvml_bilstm_wide_fwd_workspace_size(D).
  *   bwd: wT_d = W_hh_d^T; gout [T][B][2D]; carry [2][2][B][D] ZEROED scratch; gg_d [T][B][4D]
- *        ZEROED (the padding rows stay zero); gg_amax[2] zeroed running maxima; amax as fwd;
- *        workspace mvml_bilstm_wide_bwd_workspace_size(B, D). */
+ *        ZEROED when time-major (padding rows stay zero); gg_amax[2] zeroed running maxima; amax as fwd;
+ *        workspace mvml_bilstm_wide_bwd_workspace_size(B, D).
+ *   gx_packed / gg_packed != 0: gx_d (resp. gg_d) hold the live rows only, step t's
+ *        batch_sizes[t] rows after those of steps < t (pack_padded_sequence's data layout,
+ *        mvml_bilstm_pack_rows' packed side); gg_d then needs no zeroing. */
 size_t mvml_bilstm_wide_fwd_workspace_size(int D);
 int mvml_bilstm_wide_fwd(int64_t T, int64_t B, int D, const int32_t* batch_sizes, const float* W0,
                          const float* W1, const float* gx0, const float* gx1, const float* bih0,
                          const float* bhh0, const float* bih1, const float* bhh1, float* c0,
                          float* c1, float* out, float* act0, float* act1, const uint32_t* amax,
-                         void* workspace, size_t workspace_bytes, void* stream);
+                         int gx_packed, void* workspace, size_t workspace_bytes, void* stream);
 size_t mvml_bilstm_wide_bwd_workspace_size(int64_t B, int D);
 int mvml_bilstm_wide_bwd(int64_t T, int64_t B, int D, const int32_t* batch_sizes, const float* wT0,
                          const float* wT1, const float* gout, const float* act0, const float* act1,
                          const float* c0, const float* c1, float* carry, float* gg0, float* gg1,
-                         uint32_t* gg_amax, const uint32_t* amax, void* workspace,
+                         uint32_t* gg_amax, const uint32_t* amax, int gg_packed, void* workspace,
                          size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus

@@ -25,6 +25,7 @@
 // variants against fp64) at 6 bf16 MFMAs per 16 k instead of 8 f32 MFMAs at 1/16 the rate.
 #include <cstdlib>
 #include <type_traits>
+#include <vector>
 
 #include "common.h"
 
@@ -2786,7 +2787,8 @@ extern "C" int mvml_bilstm_wide_fwd(int64_t T, int64_t B, int D, const int32_t* 
                                     const float* gx1, const float* bih0, const float* bhh0,
                                     const float* bih1, const float* bhh1, float* c0, float* c1,
                                     float* out, float* act0, float* act1, const uint32_t* amax,
-                                    void* workspace, size_t workspace_bytes, void* stream) {
+                                    int gx_packed, void* workspace, size_t workspace_bytes,
+                                    void* stream) {
   clear_error();
   MVML_REQUIRE(T > 0 && B > 0 && D > 0 && D % 8 == 0 && batch_sizes && amax,
                "bilstm_wide_fwd: bad arguments");
@@ -2796,6 +2798,9 @@ extern "C" int mvml_bilstm_wide_fwd(int64_t T, int64_t B, int D, const int32_t* 
     MVML_REQUIRE(batch_sizes[t] > 0 && batch_sizes[t] <= B && (t == 0 || batch_sizes[t] <= batch_sizes[t - 1]),
                  "bilstm_wide_fwd: batch_sizes must be positive, <= B and non-increasing");
   const int64_t G = 4 * (int64_t)D, H2 = 2 * (int64_t)D;
+  // first gx row of step t: time-major t B, or packed (step blocks of batch_sizes[t] rows)
+  std::vector<int64_t> row(T);
+  for (int64_t t = 0, acc = 0; t < T; acc += batch_sizes[t], ++t) row[t] = gx_packed ? acc : t * B;
   float* Wi0 = static_cast<float*>(workspace);
   float* Wi1 = reinterpret_cast<float*>(static_cast<char*>(workspace) + carve_size((size_t)G * D * sizeof(float)));
   hipStream_t st = as_stream(stream);
@@ -2807,7 +2812,7 @@ extern "C" int mvml_bilstm_wide_fwd(int64_t T, int64_t B, int D, const int32_t* 
     const bool first = s == 0;
     const int rc = wide_step_fwd(
         batch_sizes[t0], batch_sizes[t1], D, first ? 0 : D, first ? nullptr : out + p0 * B * H2,
-        first ? nullptr : out + p1 * B * H2 + D, H2, W0, W1, D, gx0 + t0 * B * G, gx1 + t1 * B * G, G,
+        first ? nullptr : out + p1 * B * H2 + D, H2, W0, W1, D, gx0 + row[t0] * G, gx1 + row[t1] * G, G,
         bih0, bhh0, bih1, bhh1, first ? nullptr : c0 + p0 * B * D, first ? nullptr : c1 + p1 * B * D,
         c0 + t0 * B * D, c1 + t1 * B * D, out + t0 * B * H2, out + t1 * B * H2 + D, H2,
         act0 + t0 * B * G, act1 + t1 * B * G, amax, amax + 1, amax + 2, stream, Wi0, Wi1);
@@ -2824,8 +2829,8 @@ extern "C" int mvml_bilstm_wide_bwd(int64_t T, int64_t B, int D, const int32_t* 
                                     const float* wT0, const float* wT1, const float* gout,
                                     const float* act0, const float* act1, const float* c0,
                                     const float* c1, float* carry, float* gg0, float* gg1,
-                                    uint32_t* gg_amax, const uint32_t* amax, void* workspace,
-                                    size_t workspace_bytes, void* stream) {
+                                    uint32_t* gg_amax, const uint32_t* amax, int gg_packed,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
   MVML_REQUIRE(T > 0 && B > 0 && D > 0 && D % 8 == 0 && batch_sizes && carry && gg_amax && amax,
                "bilstm_wide_bwd: bad arguments");
@@ -2837,6 +2842,8 @@ extern "C" int mvml_bilstm_wide_bwd(int64_t T, int64_t B, int D, const int32_t* 
   const int64_t G = 4 * (int64_t)D, H2 = 2 * (int64_t)D, BD = B * (int64_t)D;
   // carry: [direction][ping-pong][B][D]
   float* cr[2][2] = {{carry, carry + BD}, {carry + 2 * BD, carry + 3 * BD}};
+  std::vector<int64_t> row(T);  // first gg row of step t (time-major or packed, as the forward's gx)
+  for (int64_t t = 0, acc = 0; t < T; acc += batch_sizes[t], ++t) row[t] = gg_packed ? acc : t * B;
   const size_t slabs = mvml_bilstm_wide_step_bwd_workspace_size(B, D);
   float* Wi0 = reinterpret_cast<float*>(static_cast<char*>(workspace) + slabs);
   float* Wi1 = reinterpret_cast<float*>(static_cast<char*>(workspace) + slabs + carve_size((size_t)G * D * sizeof(float)));
@@ -2850,11 +2857,11 @@ extern "C" int mvml_bilstm_wide_bwd(int64_t T, int64_t B, int D, const int32_t* 
     const int64_t R1 = s == 0 ? 0 : std::min(batch_sizes[t1], batch_sizes[n1]);
     const int ci = (int)(s % 2), co = (int)((s + 1) % 2);
     const int rc = wide_step_bwd(
-        batch_sizes[t0], batch_sizes[t1], R0, R1, D, gg0 + (s ? n0 : t0) * B * G,
-        gg1 + (s ? n1 : t1) * B * G, wT0, wT1, G, gout + t0 * B * H2, gout + t1 * B * H2 + D, H2,
+        batch_sizes[t0], batch_sizes[t1], R0, R1, D, gg0 + row[s ? n0 : t0] * G,
+        gg1 + row[s ? n1 : t1] * G, wT0, wT1, G, gout + t0 * B * H2, gout + t1 * B * H2 + D, H2,
         act0 + t0 * B * G, act1 + t1 * B * G, c0 + t0 * BD, c1 + t1 * BD,
         t0 >= 1 ? c0 + (t0 - 1) * BD : nullptr, t1 + 1 < T ? c1 + (t1 + 1) * BD : nullptr,
-        cr[0][ci], cr[1][ci], cr[0][co], cr[1][co], gg0 + t0 * B * G, gg1 + t1 * B * G, gg_amax,
+        cr[0][ci], cr[1][ci], cr[0][co], cr[1][co], gg0 + row[t0] * G, gg1 + row[t1] * G, gg_amax,
         gg_amax + 1, amax + 1, amax + 2, workspace, slabs, stream, Wi0, Wi1);
     if (rc) return rc;
   }

@@ -160,9 +160,18 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         out = torch.zeros((T, B, 2 * H), dtype=torch.float32, device=dev)
         saved, gates_d = [], []
         wide_pack = WIDE_PACK and not _use_seq(pk, H) and In % 4 == 0
+        amx = _h_bounds(w, dev) if not _use_seq(pk, H) else None
+        # the native wide recurrence reads a packed input projection directly (no unpack)
+        gx_packed = wide_pack and not layer0 and WIDE_STEP and amx is not None
         xp = None
         for d in range(2):
             w_ih = _c(w[4 * d])
+            if gx_packed:
+                xp = _pack(pk, x, In, In) if d == 0 else xp
+                gp = torch.empty((xp.shape[0], G), dtype=torch.float32, device=dev)
+                gemm(xp, w_ih, xp.shape[0], G, In, 0, 0, In, In, gp, G)
+                gates_d.append(gp)
+                continue
             gates = torch.empty((T, B, G), dtype=torch.float32, device=dev)
             if layer0:
                 V = x.shape[0]
@@ -187,10 +196,9 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                  ptr(gates_d[1]), ptr(wc[1]), ptr(wc[5]), ptr(wc[2]), ptr(wc[3]), ptr(wc[6]),
                  ptr(wc[7]), ptr(out), ptr(c[0]), ptr(c[1]), ptr(act[0]), ptr(act[1]), st)
             saved = [c[0], act[0], c[1], act[1]]
-        elif WIDE_STEP and _h_bounds(w, dev) is not None:
+        elif WIDE_STEP and amx is not None:
             # wide batches: one launch per time step for both directions, the recurrent product
             # and the LSTM cell fused (mvml_bilstm_wide_step_fwd)
-            amx = _h_bounds(w, dev)
             wperm = [_c(w[4 * d + 1]).view(4, H, H).transpose(0, 1).reshape(G, H).contiguous()
                      for d in range(2)]  # rows 4 j + q = gate q of unit j
             bias = [(_c(w[4 * d + 2]), _c(w[4 * d + 3])) for d in range(2)]
@@ -201,10 +209,9 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             call("mvml_bilstm_wide_fwd", T, B, H, ptr(pk.batch_sizes_host), ptr(wperm[0]), ptr(wperm[1]),
                  ptr(gates_d[0]), ptr(gates_d[1]), ptr(bias[0][0]), ptr(bias[0][1]), ptr(bias[1][0]),
                  ptr(bias[1][1]), ptr(c[0]), ptr(c[1]), ptr(out), ptr(act[0]), ptr(act[1]), ptr(amx),
-                 ptr(ws), nws, st)
+                 1 if gx_packed else 0, ptr(ws), nws, st)
             saved = [c[0], act[0], c[1], act[1]]
         else:  # wide batches, other GEMM algorithms: per-step GEMM (beta = 1 onto the projection) + cell kernel
-            amx = _h_bounds(w, dev)
             for d in range(2):
                 w_hh, b_ih, b_hh = (_c(t) for t in w[4 * d + 1:4 * d + 4])
                 gates = gates_d[d]
@@ -243,15 +250,23 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         # W_hh^T [H, 4H] once per backward: the recurrent product reads it k-contiguous
         w_hhT = [_c(w[4 * d + 1]).t().contiguous() for d in range(2)]
         seq = _use_seq(pk, H)
-        ggs = [torch.zeros((T, B, G), dtype=torch.float32, device=dev) for _ in range(2)]
+        amx = None if seq else _h_bounds(w, dev)
+        packed = not seq and WIDE_PACK and In % 4 == 0
+        # the native wide recurrence writes the gate gradients packed (live rows only: no zero
+        # fill of T x B rows, no pack before the weight-gradient products)
+        gg_packed = packed and WIDE_STEP and amx is not None
+        if gg_packed:
+            n_live = pk.live_offsets(0, T)[1]
+            ggs = [torch.empty((n_live, G), dtype=torch.float32, device=dev) for _ in range(2)]
+        else:
+            ggs = [torch.zeros((T, B, G), dtype=torch.float32, device=dev) for _ in range(2)]
         if seq:
             carry = torch.zeros((2, B, H), dtype=torch.float32, device=dev)
             call("mvml_bilstm_seq_bwd", T, B, H, ptr(pk.batch_sizes_host), ptr(w_hhT[0]),
                  ptr(w_hhT[1]), ptr(a0), ptr(a1), ptr(c0), ptr(c1), ptr(g), ptr(ggs[0]),
                  ptr(ggs[1]), ptr(carry), st)
-        amx = amg = None
+        amg = None
         if not seq:
-            amx = _h_bounds(w, dev)
             # running max |dgates| per direction, folded in by mvml_lstm_cell_bwd (a bound for
             # every step already processed, which is all a scale needs)
             amg = torch.zeros(2, dtype=torch.int32, device=dev) if amx is not None else None
@@ -263,7 +278,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             ws = workspace(nws, dev)
             call("mvml_bilstm_wide_bwd", T, B, H, ptr(pk.batch_sizes_host), ptr(w_hhT[0]), ptr(w_hhT[1]),
                  ptr(g), ptr(acts[0]), ptr(acts[1]), ptr(cs[0]), ptr(cs[1]), ptr(carry), ptr(ggs[0]),
-                 ptr(ggs[1]), ptr(amg), ptr(amx), ptr(ws), nws, st)
+                 ptr(ggs[1]), ptr(amg), ptr(amx), 1 if gg_packed else 0, ptr(ws), nws, st)
         elif not seq:  # wide batches: per-step recurrent GEMM (beta = 1 into g) + cell kernel
             g = g.clone()
             for d in range(2):
@@ -286,7 +301,6 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                     nxt, k = t, k + 1
         # weight / input gradients: GEMMs over every position — on the wide path over the live
         # rows only (packed), else over all T x B rows (the padding rows of gg are zeros)
-        packed = not seq and WIDE_PACK and In % 4 == 0
         if packed:
             offs, n_live = pk.live_offsets(0, T)
             xp = None if layer0 else (ctx.xp if ctx.xp is not None else _pack(pk, x, In, In))
@@ -296,7 +310,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         for d in range(2):
             w_ih, gg = _c(w[4 * d]), ggs[d]
             gb = torch.empty(G, dtype=torch.float32, device=dev)
-            ggp = _pack(pk, gg, G, G) if packed else gg
+            ggp = _pack(pk, gg, G, G) if packed and not gg_packed else gg
             rows = ggp.shape[0] if packed else T * B
             colsum(ggp, rows, G, G, gb)
             g_whh = torch.zeros((G, H), dtype=torch.float32, device=dev)
