@@ -60,7 +60,9 @@ const char* mvml_version(void);
                                    LDS-DMA ring kernel, 0 (default) = the register-staged one */
 #define MVML_OPT_LSTM_TILE 6    /* MVML_LSTM_TILE: tile of the wide BiLSTM step products
                                    (mvml_bilstm_wide_step_*): 0 (default) planned from the live
-                                   row count, 128 / 256 = forced */
+                                   row count, 128 / 256 = forced; 128 also moves
+                                   mvml_lstm_gates_cell_fwd to the 128x128 kernel (measured
+                                   slower there at 65,536 rows: 0.78 vs 0.70 ms) */
 int mvml_set_option(int option, int value);
 int mvml_get_option(int option);
 

@@ -2294,6 +2294,14 @@ extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float
   cep.h_out2 = h_out2; cep.act = act; cep.ldh = ldh; cep.ldh2 = ldh2; cep.D = D;
   const dim3 grid(x3w_grid_x(tiles, 1), 1, 1);
   MVML_REQUIRE(!amax_a == !amax_b, "lstm_gates_cell_fwd: give both maxima or neither");
+  if (amax_a && option(MVML_OPT_LSTM_TILE) == 128 && K % BKT == 0) {
+    // the 128x128 split-fp16 kernel with the same cell epilogue (the wide BiLSTM steps' plan)
+    const int64_t t128 = ceil_div(M, BM) * ceil_div(N, BN);
+    gemm_f32_kernel<false, false, -1, true, true><<<dim3((unsigned)t128, 1, 1), kThreads, 0, as_stream(stream)>>>(
+        M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
+        BatchStrides{}, AmaxPtrs{amax_a, amax_b}, cep);
+    return check_launch("gemm_f32_kernel(lstm cell)");
+  }
   if (amax_a && w_planes)  // w_perm from its pre-split planes (mvml_split_f16x2 of w_perm)
     gemm_x3w_kernel<false, false, -1, true, 2, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, reinterpret_cast<const float*>(w_planes), ldw, nullptr, 0.f, 0, nullptr,

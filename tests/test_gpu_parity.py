@@ -353,18 +353,21 @@ def test_set2set_parity():
         assert rel_err(p.grad, p2.grad) < TOL, n
 
 
-@pytest.mark.parametrize("ring", [1, 0])
-def test_set2set_cell_epilogue_bitwise(ring):
+@pytest.mark.parametrize("ring,tile", [(1, 0), (0, 0), (0, 128)])
+def test_set2set_cell_epilogue_bitwise(ring, tile):
     """Set2Set at a width where the gates GEMM takes the 256x256 plan (16,384 molecules): the
     fused gates + LSTM-cell epilogue (mvml_lstm_gates_cell_fwd) equals the GEMM + cell kernel
     path bit for bit (same MFMA accumulation per element, same cell arithmetic), forward and
-    backward, on either split-fp16 kernel (ring: the LDS-DMA ring one, the default); the
-    unfused path is the one pinned to the float64 oracle above."""
+    backward, on either split-fp16 kernel (ring: the LDS-DMA ring one, the default) and on the
+    128x128 one (tile = 128: option lstm_tile); the unfused path is the one pinned to the
+    float64 oracle above."""
     import mvml_gat.functional as fn
     from mvml_gat import _lib
     from mvml_gat._lib import option
     opt = option("gemm_ring", ring)
     opt.__enter__()
+    opt_t = option("lstm_tile", tile)
+    opt_t.__enter__()
     from mvml_gat.nn import Set2Set
     sb = batch_of_sizes([3, 5, 2, 7] * 4096, seed=4)
     assert _lib.lib().mvml_lstm_gates_cell_plan_ok(16384, 384, 1152)
@@ -385,6 +388,7 @@ def test_set2set_cell_epilogue_bitwise(ring):
             res.append([out.detach().clone(), Xp.grad.clone()] + [p.grad.clone() for p in s2s.parameters()])
         finally:
             fn.CELL_EPI = old
+    opt_t.__exit__(None, None, None)
     opt.__exit__(None, None, None)
     for a, b in zip(*res):
         assert torch.equal(a, b)
