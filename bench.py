@@ -169,6 +169,23 @@ def load_traffic(workload_key, entry):
     return d.get(workload_key, {}).get(entry, {}).get("hbm_bytes_per_launch")
 
 
+ALLOC_KEYS = ("num_alloc_retries", "num_device_alloc", "num_device_free", "num_sync_all_streams",
+              "num_ooms")
+
+
+def alloc_stats(args):
+    """Caching-allocator counters (device mallocs / frees / retries) and the reserved bytes: a
+    step that misses the cache pays hipMalloc, and a retry frees every cached block (a device
+    synchronisation) — both show as time outside every kernel."""
+    if args.dry_run:
+        return {}
+    s = torch.cuda.memory_stats()
+    out = {k: int(s.get(k, 0)) for k in ALLOC_KEYS}
+    out["reserved_bytes"] = int(s.get("reserved_bytes.all.current", 0))
+    out["peak_allocated_bytes"] = int(s.get("allocated_bytes.all.peak", 0))
+    return out
+
+
 # ----------------------------------------------------------------------------- CPU baseline
 def usable_cores():
     """CPUs this process may actually run on: the affinity mask, capped by a cgroup v2 quota
@@ -419,6 +436,7 @@ def run(args):
         opt.zero_grad(set_to_none=False)
         if mvp and fused:
             mvml_gat.bce_with_logits(full(b.smiles, b.g, b.feats, b.fp), b.labels).backward()
+            mvp_mod.join_side_stream(dev)
             reducer()
             opt.step()
             return
@@ -441,17 +459,27 @@ def run(args):
         _lib.timer.enable(TIMED)
     barrier()
     sync()
+    mem0 = alloc_stats(args)
+    step_ev = []
     t0 = time.perf_counter()
     mols = 0
     for i in range(args.steps):
         b = batches[(args.warmup + i) % nb]
+        if not args.dry_run:
+            step_ev.append(torch.cuda.Event(enable_timing=True))
+            step_ev[-1].record()
         step(b)
         mols += b.B
+    if not args.dry_run:
+        step_ev.append(torch.cuda.Event(enable_timing=True))
+        step_ev[-1].record()
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    mem1 = alloc_stats(args)
     if timer_on:
         _lib.timer.disable()
+    step_ms = [round(a.elapsed_time(b), 3) for a, b in zip(step_ev[:-1], step_ev[1:])]
 
     def reduce_max(x):
         if world == 1:
@@ -524,6 +552,17 @@ def run(args):
                     "achieved is fp32-equivalent TFLOP/s, peak = dense bf16 MFMA peak / 6")
                 extra["roofline_gemm"]["frac"] = round(extra["roofline_gemm"]["achieved"] / (BF16_MFMA_PEAK_TFS / 6), 4)
         extra["kernel_ms_per_step"] = {k: round(v["ms_per_step"], 3) for k, v in rows.items()}
+        # time per step outside every timed entry point: torch-side kernels (Adam, zero_grad,
+        # pads / copies), launch gaps and allocator stalls (config 3: one stream, so the
+        # entry-point times do not overlap)
+        extra["untimed_ms_per_step"] = round(ms_per_step - sum(v["ms_per_step"] for v in rows.values()), 3)
+    if step_ms:
+        extra["step_ms"] = {"min": min(step_ms), "median": float(np.median(step_ms)),
+                            "max": max(step_ms), "each": step_ms}
+    if mem0:
+        extra["allocator"] = {k: mem1[k] - mem0[k] for k in ALLOC_KEYS}
+        extra["allocator"].update(reserved_gb=round(mem1["reserved_bytes"] / 2 ** 30, 2),
+                                  peak_allocated_gb=round(mem1["peak_allocated_bytes"] / 2 ** 30, 2))
 
     # ---- view-only figure (the graph view alone, fixed upstream gradient at its output)
     if args.view_only_steps > 0 and not args.dry_run:

@@ -167,6 +167,22 @@ int mvml_gemm_f16x2_amax(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
                          const uint32_t* amax_a, const uint32_t* amax_b, const float* bias,
                          float beta, int act, float* C, int64_t ldc, void* workspace,
                          size_t workspace_bytes, void* stream);
+/* mvml_gemm_f16x2 with PER-ROW A maxima: amax_a_rows[m] = bits of max_k |A[m, k]| (or an upper
+ * bound; mvml_absmax_rows_f32, or folded by the kernel that wrote A), A K-contiguous
+ * ([M][lda]); *amax_b as mvml_gemm_f16x2_amax.  Every A row is split with its own power-of-two
+ * scale and its output row scaled back by it, so (a) a row keeps fp32-GEMM accuracy relative to
+ * ITSELF however far it sits below the operand's max (the operand-wide scale loses precision
+ * ~2^17 below it, where the low fp16 plane goes subnormal), and (b) a row of C depends only on
+ * its own row of A and on B: the same molecule gives bitwise the same output in any batch. */
+int mvml_gemm_f16x2_rows(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                         const float* B, int64_t ldb, int b_kmajor, const uint32_t* amax_a_rows,
+                         const uint32_t* amax_b, const float* bias, float beta, int act,
+                         float* C, int64_t ldc, void* workspace, size_t workspace_bytes,
+                         void* stream);
+/* out[r] = bits of max_c |P[r*ld + c]|, c < cols (accumulate != 0: max with the current out[r]);
+ * one writer per row, no atomics. */
+int mvml_absmax_rows_f32(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32_t* out,
+                         int accumulate, void* stream);
 /* Split an fp32 matrix once into the two scaled fp16 planes the split-fp16 GEMM stages
  * (hi at planes, lo at planes + rows * ld, both [rows][ld]; scale from *amax, as the GEMM's own
  * split): a weight operand read by many tiles / products is then split once per step.
@@ -307,9 +323,16 @@ int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float* A, int64_
                              int64_t ldh, float* act, float* h_out2, int64_t ldh2,
                              const uint32_t* amax_a, const uint32_t* amax_b /* both NULL:
                                split-bf16; else split-fp16 with these |A|, |w_perm| max bits */,
+                             const uint32_t* amax_a_rows /* NULL, or per-row |A| max bits (M
+                               entries; replaces amax_a, see mvml_gemm_f16x2_rows) */,
                              const uint16_t* w_planes, int64_t w_plane /* NULL, or w_perm
                                pre-split by mvml_split_f16x2 with amax_b */,
                              void* stream);
+/* Per molecule b: out_bits[b] = max(floor_bits, max_{n in [node_offsets[b], node_offsets[b+1])}
+ * in_bits[n]) on non-negative float bits — a molecule's bound from its atoms' row maxima (the
+ * per-molecule split-fp16 scales of Set2Set's cells; floor 1.0f bounds the LSTM's |h| < 1). */
+int mvml_segment_max_bits(int64_t B, const int64_t* node_offsets, const uint32_t* in_bits,
+                          uint32_t floor_bits, uint32_t* out_bits, void* stream);
 int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_ih,
                        const float* b_hh, const float* c_prev, float* c_out, float* h_out,
                        int64_t ldh, float* act_out, float* h_out2, int64_t ldh2, void* stream);

@@ -325,11 +325,21 @@ __device__ __forceinline__ float comp(const float4& v, int s) {
 // ((li & (W-1)) << (5 - EPI_LOGW)) | t, index = side * 16 + row register.
 // Strided batch (blockIdx.z): product z reads A + z a, B + z b and writes C + z c (floats).
 // Split-fp16 operand maxima: bits of max |A| and max |B| (device pointers, may alias).
+// Per-row A maxima (a_rows, M entries, K-contiguous A only): every A row gets its own scale,
+// so a row's split — and with it the row of the product — depends on that row alone, not on the
+// largest row of the batch: per-row fp32 accuracy however far a row sits below the operand's
+// max, and results that do not change with the batch a row is computed in.
 struct AmaxPtrs {
   const uint32_t* a = nullptr;
   const uint32_t* b = nullptr;
   int64_t b_plane = 0;  // BPS: elements from B's high fp16 plane to its low plane
+  const uint32_t* a_rows = nullptr;
 };
+
+// Scale shift of A row `row` (clamped into range: clamped rows feed outputs never stored).
+__device__ __forceinline__ int row_shift(const AmaxPtrs& am, int64_t row, int64_t M) {
+  return amax_shift(am.a_rows[row < M ? row : M - 1]);
+}
 
 struct BatchStrides {
   int64_t a = 0, b = 0, c = 0;
@@ -457,7 +467,36 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
                                              int64_t N, int64_t r0, int64_t c0, int lane,
                                              const float* __restrict__ bias, float beta, int act,
                                              float* __restrict__ C, int64_t ldc,
-                                             float* __restrict__ slab, const CellEpi& cep = CellEpi{});
+                                             float* __restrict__ slab, const CellEpi& cep = CellEpi{},
+                                             const int* rs = nullptr);
+
+// Undo the split-fp16 operand scales of a 128x128 tile's 2 x 2 accumulators (exact: powers of
+// two).  Per-row A maxima: lane li scaled A rows 32 i + li of its wave's 64 (shift ka0 / ka1);
+// accumulator register r of block i holds row 32 i + (r & 3) + 8 (r >> 2) + 4 (lane >> 5), whose
+// shift comes from the lane that staged it.
+__device__ __forceinline__ void unscale_rows(f32x16 (&acc)[2][2], bool per_row, int ka, int ka0,
+                                             int ka1, int kb, int lane) {
+  const float ub = pow2f(-kb);
+  if (!per_row) {
+    const float ua = pow2f(-ka);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ua * ub;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int src = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const float ua = pow2f(-__shfl(i ? ka1 : ka0, src, 64));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j][r] = acc[i][j][r] * ua * ub;
+    }
+}
 
 // X3: fp32-accurate products from split fp32 fragments — H2 = false: split-bf16 (six MFMAs per
 // fragment pair); H2 = true: scaled split-fp16 (three; operand scales from amax, as the 256x256
@@ -487,6 +526,7 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     cep = dual.cep;
     amax.b = dual.amax_b;
     if (dual.amax_a) amax.a = dual.amax_a;
+    amax.a_rows = nullptr;  // (host: dual launches use operand-wide maxima)
   }
   using SA = Stager<AK>;
   using SB = Stager<BKM>;
@@ -514,11 +554,17 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   int ka = 0, kb = 0;  // H2: operand scales 2^ka, 2^kb from the |max| bits
+  int ka0 = 0, ka1 = 0;  // H2 with per-row A maxima: the scales of this lane's two A rows
   if constexpr (H2) {
-    ka = amax_shift(*amax.a);
     kb = amax_shift(*amax.b);
+    if (amax.a_rows) {
+      ka0 = row_shift(amax, m0 + wm * 64 + li, M);
+      ka1 = row_shift(amax, m0 + wm * 64 + li + 32, M);
+    } else {
+      ka = ka0 = ka1 = amax_shift(*amax.a);
+    }
   }
-  const float s_a = pow2f(ka), s_b = pow2f(kb);
+  const float s_a0 = pow2f(ka0), s_a1 = pow2f(ka1), s_b = pow2f(kb);
 
   // LDS-DMA needs 16-B aligned pieces; a k-major operand's edge tile also needs rows % 4 == 0
   // (no piece straddles the edge), otherwise the guarded register path fills the stage.
@@ -583,8 +629,8 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int T = 0; T < 2; ++T) {
-        split2h8(f[T][0][0], f[T][0][1], s_a, pa[0][0], pa[0][1]);
-        split2h8(f[T][1][0], f[T][1][1], s_a, pa[1][0], pa[1][1]);
+        split2h8(f[T][0][0], f[T][0][1], s_a0, pa[0][0], pa[0][1]);
+        split2h8(f[T][1][0], f[T][1][1], s_a1, pa[1][0], pa[1][1]);
         if constexpr (BPS) {
           pb[0][0] = __builtin_bit_cast(bf16x8, f[T][2][0]);
           pb[0][1] = __builtin_bit_cast(bf16x8, f[T][2][1]);
@@ -668,15 +714,7 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     }
   }
 
-  if constexpr (H2) {  // undo the operand scales (exact: powers of two)
-    const float ua = pow2f(-ka), ub = pow2f(-kb);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ua * ub;
-  }
+  if constexpr (H2) unscale_rows(acc, amax.a_rows != nullptr, ka, ka0, ka1, kb, lane);
   if constexpr (H2 && EPI_LOGW < 0) {
     if (cep.D > 0) {  // LSTM cell epilogue through LDS (host: N = 4 D, no split-K)
       __syncthreads();  // every wave is done reading the last stage
@@ -857,11 +895,18 @@ gemm_x3s_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   int ka = 0, kb = 0;  // H2: operand scales 2^ka, 2^kb from the |max| bits
+  int ka0 = 0, ka1 = 0, kst = 0;  // per-row A maxima: this lane's fragment rows, its staged row
   if constexpr (H2) {
-    ka = amax_shift(*amax.a);
     kb = amax_shift(*amax.b);
+    if (amax.a_rows) {  // (host: K-contiguous A)
+      ka0 = row_shift(amax, m0 + wm * 64 + li, M);
+      ka1 = row_shift(amax, m0 + wm * 64 + li + 32, M);
+      kst = row_shift(amax, m0 + (tid >> 1), M);
+    } else {
+      ka = ka0 = ka1 = kst = amax_shift(*amax.a);
+    }
   }
-  const float s_a = pow2f(ka), s_b = pow2f(kb);
+  const float s_a = pow2f(kst), s_b = pow2f(kb);
   const int64_t ntiles = (kend > kbeg) ? ceil_div(kend - kbeg, BKT) : 0;
   // unguarded 16-B loads when the whole tile is in range and rows are 16-B aligned
   const bool a_in = a_vec && (AK ? m0 + BM <= M : m0 + BM <= M);
@@ -903,15 +948,7 @@ gemm_x3s_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       acc[1][1] = mfma_np<NPL>(pa[1], pb[1], acc[1][1]);
     }
   }
-  if constexpr (H2) {  // undo the operand scales (exact: powers of two)
-    const float ua = pow2f(-ka), ub = pow2f(-kb);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ua * ub;
-  }
+  if constexpr (H2) unscale_rows(acc, amax.a_rows != nullptr, ka, ka0, ka1, kb, lane);
   tile_epilogue<EPI_LOGW>(acc, M, N, m0 + wm * 64, n0 + wn * 64, lane, bias, beta, act, C, ldc,
                           slab, epi);
 }
@@ -997,15 +1034,16 @@ struct XOp {
   __device__ static __forceinline__ int64_t kstep(int64_t ld) { return KMAJ ? XBK * ld : XBK; }
 
 
+  // s[i]: the scale of piece i (split-fp16; per-row A maxima give the pieces' rows their own)
   __device__ static __forceinline__ void split_store(uint8_t* op, int tid, const float4 (&v)[NI],
-                                                     float s = 1.f) {
+                                                     const float (&s)[NI]) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       uint2 p0, p1, p2;
       if constexpr (NP == 3) {
         split4(v[i].x, v[i].y, v[i].z, v[i].w, p0, p1, p2);
       } else if constexpr (NP == 2) {
-        split2h(v[i], s, p0, p1);
+        split2h(v[i], s[i], p0, p1);
       } else {  // bf16 operands: round-to-nearest-even, one plane
         const f32x2 u = {v[i].x, v[i].y}, w = {v[i].z, v[i].w};
         p0.x = __builtin_bit_cast(uint32_t, __builtin_convertvector(u, bf16x2));
@@ -1082,7 +1120,10 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
                                                  int64_t N, int64_t r0, int64_t c0, int lane,
                                                  const float* __restrict__ bias, float beta, int act,
                                                  float* __restrict__ C, int64_t ldc,
-                                                 float* __restrict__ slab, const CellEpi& cep) {
+                                                 float* __restrict__ slab, const CellEpi& cep,
+                                                 const int* rs) {
+  // rs (per-row A maxima): rs[32 i + rr] = the scale shift of row r0 + 32 i + rr, undone here as
+  // each row leaves (acc already carries B's)
   const int li = lane & 31, lk = lane >> 5;
   float* out = slab ? slab + (int64_t)blockIdx.y * M * N : C;
   const int64_t ld = slab ? N : ldc;
@@ -1116,6 +1157,11 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
         float4 v[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(wl + rr * kEpiLd + 16 * u + 4 * k);
+        if (rs) {
+          const float ua = pow2f(-rs[32 * i + rr]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) { v[k].x *= ua; v[k].y *= ua; v[k].z *= ua; v[k].w *= ua; }
+        }
         auto ld4 = [](const float* p) { return *reinterpret_cast<const float4*>(p); };
         auto el = [](const float4& f, int k) { return k == 0 ? f.x : k == 1 ? f.y : k == 2 ? f.z : f.w; };
         if (cep.gx) {
@@ -1160,6 +1206,10 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
       const int64_t row = r0 + 32 * i + rr, col = c0 + c4;
       if (row >= M || col >= N) continue;
       float4 v = *reinterpret_cast<const float4*>(wl + rr * kEpiLd + c4);
+      if (rs) {
+        const float ua = pow2f(-rs[32 * i + rr]);
+        v.x *= ua; v.y *= ua; v.z *= ua; v.w *= ua;
+      }
       if (cep.D > 0) {  // LSTM cell (host: N = 4 D, no split-K): one unit's four gates
         const int D = cep.D;
         const int64_t j = col >> 2;
@@ -1292,13 +1342,15 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       return *reinterpret_cast<const float4*>(p);
     }
   };
-  // NP = 2: operand scales from the |max| bits of A and B
+  // NP = 2: operand scales from the |max| bits of A and B (per-row A maxima: amax.a_rows, a
+  // shift per A row of the tile in rsh — host: K-contiguous A)
   int ka = 0, kb = 0;
   if constexpr (NP == 2) {
-    ka = amax_shift(*amax.a);
+    if (!amax.a_rows) ka = amax_shift(*amax.a);
     kb = amax_shift(*amax.b);
   }
   const float s_a = pow2f(ka), s_b = pow2f(kb);
+  __shared__ int rsh[NP == 2 ? XBM : 1];
   // KS 16-deep sub-stages per barrier (split-fp16: 2, so a stage carries as many MFMAs as the
   // split-bf16 one); a sub-stage's LDS image is exactly the KS = 1 stage layout
   constexpr int KS = (NP == 2) ? MVML_H2_KS : 1;
@@ -1325,6 +1377,20 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   const int64_t kend = min(K, kbeg + k_split);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
+  // the scales of this thread's staged A pieces (rows (tid >> 2) + 128 i when K-contiguous)
+  float sa_i[OA::NI], sb_i[OB::NI];
+#pragma unroll
+  for (int i = 0; i < OB::NI; ++i) sb_i[i] = s_b;
+#pragma unroll
+  for (int i = 0; i < OA::NI; ++i) sa_i[i] = s_a;
+  if constexpr (NP == 2 && !AK) {
+    if (amax.a_rows) {
+#pragma unroll
+      for (int i = 0; i < OA::NI; ++i) sa_i[i] = pow2f(row_shift(amax, m0 + (tid >> 2) + OA::RS * i, M));
+      // every row's shift for the epilogue (read after the K loop's barriers)
+      if (tid < XBM) rsh[tid] = row_shift(amax, m0 + tid, M);
+    }
+  }
 
   f32x16 acc[4][2];
 #pragma unroll
@@ -1402,11 +1468,11 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       uint8_t* op = lds + buf * kStage + s * kSub;
-      OA::split_store(op, tid, va[s], s_a);
+      OA::split_store(op, tid, va[s], sa_i);
       if constexpr (BPS)
         OB::store_planes(op + OA::kBytes, tid, vb[s]);
       else
-        OB::split_store(op + OA::kBytes, tid, vb[s], s_b);
+        OB::split_store(op + OA::kBytes, tid, vb[s], sb_i);
     }
   };
 #ifndef MVML_X3W_PRIO
@@ -1563,8 +1629,8 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       load_masked_into(k, ra[decltype(SET)::value], rb[decltype(SET)::value]);
     };
     auto stg = [&](auto SET, int buf) {
-      OA::split_store(lds + buf * kStage, tid, ra[decltype(SET)::value], s_a);
-      OB::split_store(lds + buf * kStage + OA::kBytes, tid, rb[decltype(SET)::value], s_b);
+      OA::split_store(lds + buf * kStage, tid, ra[decltype(SET)::value], sa_i);
+      OB::split_store(lds + buf * kStage + OA::kBytes, tid, rb[decltype(SET)::value], sb_i);
     };
     auto body2 = [&](int64_t t, auto SET, auto STAGE, auto LOAD) {
       const uint8_t* sa = lds + (t & 1) * kStage;
@@ -1652,13 +1718,23 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     }
   }
   if constexpr (NP == 2) {  // undo the operand scales (exact: powers of two)
-    const float ua = pow2f(-ka), ub = pow2f(-kb);
+    const float ub = pow2f(-kb);
+    if (amax.a_rows) {  // B's scale here, each row's own in the LDS epilogue (rsh)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ua * ub;
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ub;
+    } else {
+      const float ua = pow2f(-ka);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ua * ub;
+    }
   }
 #if MVML_X3W_LDSEPI
   // the projection's logit partials straight from the accumulators, then C through LDS (every
@@ -1667,8 +1743,10 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     tile_epilogue<EPI_LOGW, 4, 2, false>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta,
                                          act, C, ldc, slab, epi);
   epilogue_lds(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
-                   n0 + wn * 64, lane, bias, beta, act, C, ldc, slab, cep);
+                   n0 + wn * 64, lane, bias, beta, act, C, ldc, slab, cep,
+                   (NP == 2 && amax.a_rows && ntiles > 0) ? rsh + wm * 128 : nullptr);
 #else
+  static_assert(NP != 2, "per-row A maxima need the LDS epilogue");
   tile_epilogue<EPI_LOGW, 4, 2>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta, act, C,
                                 ldc, slab, epi);
 #endif
@@ -2092,6 +2170,35 @@ __global__ void __launch_bounds__(256) absmax_kernel(int64_t rows, int64_t cols,
   }
 }
 
+// Per-row |max| bits: a group of 2^lg lanes per row (float4 columns when vec), butterfly max;
+// one writer per row (accumulate: max with the stored bits), so no atomics.
+__global__ void __launch_bounds__(256) absmax_rows_kernel(int64_t rows, int64_t cols,
+                                                          const float* __restrict__ P, int64_t ld,
+                                                          int vec, int lg, int accumulate,
+                                                          uint32_t* __restrict__ out) {
+  const int L = 1 << lg;
+  const int64_t groups = (int64_t)gridDim.x * (256 >> lg);
+  const int sub = threadIdx.x & (L - 1);
+  for (int64_t row = (int64_t)blockIdx.x * (256 >> lg) + (threadIdx.x >> lg); row < rows; row += groups) {
+    const float* p = P + row * ld;
+    float m = 0.f;
+    if (vec) {
+      for (int64_t c = sub; c < cols / 4; c += L) {
+        const float4 v = *reinterpret_cast<const float4*>(p + 4 * c);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      }
+    } else {
+      for (int64_t c = sub; c < cols; c += L) m = fmaxf(m, fabsf(p[c]));
+    }
+    for (int o = L / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (sub == 0) {
+      uint32_t b = __float_as_uint(m);
+      if (accumulate) b = max(b, out[row]);
+      out[row] = b;
+    }
+  }
+}
+
 // Split an fp32 operand once into its two scaled fp16 planes (hi at planes, lo at planes +
 // rows * ld; the same [rows][ld] layout): exactly split2h of the GEMM's own staging.
 __global__ void __launch_bounds__(256) split_f16x2_kernel(int64_t rows, int64_t cols4,
@@ -2151,6 +2258,27 @@ int absmax_launch(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32
   const int64_t ry = std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, 4), ceil_div(8192, cx)));
   absmax_kernel<<<dim3((unsigned)cx, (unsigned)ry), 256, 0, st>>>(rows, cols, P, ld, vec, out);
   return check_launch("absmax_kernel");
+}
+
+int absmax_rows_launch(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32_t* out,
+                       bool accumulate, hipStream_t st) {
+  if (rows <= 0) return MVML_OK;
+  if (cols <= 0) {
+    if (accumulate) return MVML_OK;
+    if (hipMemsetAsync(out, 0, rows * sizeof(uint32_t), st) != hipSuccess) {
+      set_error("absmax_rows: hipMemsetAsync failed");
+      return MVML_ERR_LAUNCH;
+    }
+    return MVML_OK;
+  }
+  const int vec = (cols % 4 == 0) && (ld % 4 == 0) && ((uintptr_t)P % 16 == 0);
+  const int64_t units = vec ? cols / 4 : cols;
+  int lg = 0;
+  while ((1 << lg) < units && lg < 6) ++lg;  // lanes per row: enough for one unit each, <= 64
+  const int64_t per_block = 256 >> lg;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, per_block), 16384));
+  absmax_rows_kernel<<<blocks, 256, 0, st>>>(rows, cols, P, ld, vec, lg, accumulate ? 1 : 0, out);
+  return check_launch("absmax_rows_kernel");
 }
 
 int colsum_splits(int64_t M, int64_t N) {
@@ -2221,6 +2349,28 @@ extern "C" int mvml_gemm_f16x2_amax(int a_kmajor, int b_kmajor, int64_t M, int64
                      AmaxPtrs{amax_a, amax_b});
 }
 
+extern "C" int mvml_gemm_f16x2_rows(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                                    const float* B, int64_t ldb, int b_kmajor,
+                                    const uint32_t* amax_a_rows, const uint32_t* amax_b,
+                                    const float* bias, float beta, int act, float* C, int64_t ldc,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  MVML_REQUIRE(amax_a_rows != nullptr && amax_b != nullptr,
+               "gemm_f16x2_rows: amax_a_rows / amax_b are required");
+  AmaxPtrs am;
+  am.b = amax_b;
+  am.a_rows = amax_a_rows;
+  return gemm_launch(kPrecF16x2, 0, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
+                     workspace, workspace_bytes, stream, 1, BatchStrides{}, am);
+}
+
+extern "C" int mvml_absmax_rows_f32(int64_t rows, int64_t cols, const float* P, int64_t ld,
+                                    uint32_t* out, int accumulate, void* stream) {
+  clear_error();
+  MVML_REQUIRE(rows >= 0 && cols >= 0 && (rows == 0 || ld >= cols) && out, "absmax_rows: bad shape");
+  return absmax_rows_launch(rows, cols, P, ld, out, accumulate != 0, as_stream(stream));
+}
+
 extern "C" int mvml_split_f16x2(int64_t rows, int64_t cols, const float* P, int64_t ld,
                                 const uint32_t* amax, uint16_t* planes, void* stream) {
   clear_error();
@@ -2274,12 +2424,15 @@ extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float
                                         const float* c_prev, float* c_out, float* h_out,
                                         int64_t ldh, float* act, float* h_out2, int64_t ldh2,
                                         const uint32_t* amax_a, const uint32_t* amax_b,
+                                        const uint32_t* amax_a_rows,
                                         const uint16_t* w_planes, int64_t w_plane,
                                         void* stream) {
   clear_error();
   MVML_REQUIRE(M >= 0 && D > 0 && K > 0 && lda >= K && ldw >= K && ldh >= D &&
                    (!h_out2 || ldh2 >= D) && MVML_X3W_LDSEPI,
                "lstm_gates_cell_fwd: bad shape");
+  MVML_REQUIRE(!amax_a_rows || amax_b, "lstm_gates_cell_fwd: per-row A maxima need max |w_perm|");
+  if (amax_a_rows && !amax_a) amax_a = amax_a_rows;  // (unused: the rows' maxima replace it)
   if (M == 0) return MVML_OK;
   const int64_t N = 4 * (int64_t)D;
   const GemmPlan plan = plan_gemm(kPrecX3, M, N, K);
@@ -2299,21 +2452,21 @@ extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float
     const int64_t t128 = ceil_div(M, BM) * ceil_div(N, BN);
     gemm_f32_kernel<false, false, -1, true, true><<<dim3((unsigned)t128, 1, 1), kThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
-        BatchStrides{}, AmaxPtrs{amax_a, amax_b}, cep);
+        BatchStrides{}, AmaxPtrs{amax_a, amax_b, 0, amax_a_rows}, cep);
     return check_launch("gemm_f32_kernel(lstm cell)");
   }
   if (amax_a && w_planes)  // w_perm from its pre-split planes (mvml_split_f16x2 of w_perm)
     gemm_x3w_kernel<false, false, -1, true, 2, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, reinterpret_cast<const float*>(w_planes), ldw, nullptr, 0.f, 0, nullptr,
-        N, K, nullptr, av, bv, ProjEpi{}, BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, w_plane});
-  else if (amax_a && option(MVML_OPT_GEMM_RING))
+        N, K, nullptr, av, bv, ProjEpi{}, BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, w_plane, amax_a_rows});
+  else if (amax_a && !amax_a_rows && option(MVML_OPT_GEMM_RING))
     gemm_h2g_kernel<false, false><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, BatchStrides{}, cep,
         AmaxPtrs{amax_a, amax_b});
   else if (amax_a)
     gemm_x3w_kernel<false, false, -1, true, 2><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
-        BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b});
+        BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, 0, amax_a_rows});
   else
     gemm_x3w_kernel<false, false, -1, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
@@ -2351,7 +2504,9 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   const bool hf = prec == kPrecF16x2;
   const bool x3 = prec == kPrecX3 || hf, bf = prec == kPrecBf16;
   GemmPlan plan = plan_gemm(prec, M, N, K);
-  if (hf && !amax.a) {  // operand maxima into the workspace head, once per product
+  MVML_REQUIRE(!amax.a_rows || (hf && !a_kmajor && batch == 1 && amax.b),
+               "gemm: per-row A maxima need split-fp16, a K-contiguous A, no batch and max |B|");
+  if (hf && !amax.a && !amax.a_rows) {  // operand maxima into the workspace head, once per product
     if (!workspace || workspace_bytes < kAmaxBytes) {
       set_error("gemm: workspace too small (need %zu)", mvml_gemm_workspace_size(M, N, K));
       return MVML_ERR_WORKSPACE;
@@ -2398,7 +2553,7 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0) && bst.a % 4 == 0;
   const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0) && bst.b % 4 == 0;
   dim3 grid(plan.wide || bf ? x3w_grid_x(tiles, S) : (unsigned)tiles, (unsigned)S, (unsigned)batch);
-  const bool ring = option(MVML_OPT_GEMM_RING) != 0;
+  const bool ring = option(MVML_OPT_GEMM_RING) != 0 && !amax.a_rows;  // (the ring kernel: one A scale)
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
   do {                                                                                          \
     if (hf && plan.wide && ring && !bps && x3w_fast(AKV, BKV, M, N, K, av, bv))                 \

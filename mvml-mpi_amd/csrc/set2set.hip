@@ -321,6 +321,18 @@ seg_gx_mol_kernel(int64_t B, int D, int T, const int64_t* __restrict__ node_off,
   }
 }
 
+// out[b] = max(floor, max over the molecule's atoms of in[n]) on non-negative float bits (an
+// integer max): one thread per molecule, the atoms' row maxima read in order.
+__global__ void __launch_bounds__(256) segment_max_bits_kernel(int64_t B, const int64_t* __restrict__ offs,
+                                                               const uint32_t* __restrict__ in,
+                                                               uint32_t floor_bits, uint32_t* __restrict__ out) {
+  for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < B; b += (int64_t)gridDim.x * 256) {
+    uint32_t m = floor_bits;
+    for (int64_t n = offs[b]; n < offs[b + 1]; ++n) m = max(m, in[n]);
+    out[b] = m;
+  }
+}
+
 unsigned grid_for(int64_t total) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(total, 256), 16384));
 }
@@ -342,6 +354,16 @@ using namespace mvml;
     case 3: KERNEL<3><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                            \
     default: KERNEL<4><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                           \
   }
+
+extern "C" int mvml_segment_max_bits(int64_t B, const int64_t* node_offsets, const uint32_t* in_bits,
+                                     uint32_t floor_bits, uint32_t* out_bits, void* stream) {
+  clear_error();
+  MVML_REQUIRE(B >= 0 && (B == 0 || (node_offsets && in_bits && out_bits)), "segment_max_bits: bad args");
+  if (B == 0) return MVML_OK;
+  hipStream_t st = as_stream(stream);
+  segment_max_bits_kernel<<<grid_for(B), 256, 0, st>>>(B, node_offsets, in_bits, floor_bits, out_bits);
+  return check_launch("segment_max_bits_kernel");
+}
 
 extern "C" int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_ih,
                                   const float* b_hh, const float* c_prev, float* c_out,

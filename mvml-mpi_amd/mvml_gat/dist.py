@@ -92,35 +92,48 @@ class FlatGradAllReduce:
         self.average = average
         self.group = group
         self.buf = None
+        self.views = None
+        self._flags = {}    # local presence pattern -> its flags on the device (built once)
+        self._present = {}  # local presence pattern -> presence over all ranks (read back once)
+
+    def _bind(self, dev):
+        """One flat buffer; each parameter's gradient becomes a view of its segment, so autograd
+        accumulates straight into the buffer (zero_grad(set_to_none=False) zeroes it in place)
+        and the all-reduce needs no packing copies."""
+        P = len(self.params)
+        self.buf = torch.zeros(self.numel + P, dtype=self.params[0].dtype, device=dev)
+        self.views, off = [], 0
+        for p in self.params:
+            n = p.numel()
+            self.views.append(self.buf[off:off + n].view_as(p))
+            off += n
+        self._flags.clear()
 
     def __call__(self):
         if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
             return
         dev = self.params[0].device
-        P = len(self.params)
         if self.buf is None or self.buf.device != dev:
-            self.buf = torch.empty(self.numel + P, dtype=self.params[0].dtype, device=dev)
-        flags = self.buf[self.numel:]
-        flags.copy_(torch.tensor([p.grad is not None for p in self.params], dtype=flags.dtype))
-        off = 0
-        for p in self.params:
-            n = p.numel()
-            if p.grad is None:
-                self.buf[off:off + n].zero_()
-            else:
-                self.buf[off:off + n].copy_(p.grad.reshape(-1))
-            off += n
+            self._bind(dev)
+        local = tuple(p.grad is not None for p in self.params)
+        for p, v, has in zip(self.params, self.views, local):
+            if not has:
+                v.zero_()
+            elif p.grad.data_ptr() != v.data_ptr() or p.grad.shape != v.shape:
+                v.copy_(p.grad)  # a fresh gradient (first step, or zero_grad(set_to_none=True))
+                p.grad = v
+        fl = self._flags.get(local)
+        if fl is None:
+            fl = self._flags[local] = torch.tensor(local, dtype=self.buf.dtype).to(dev)
+        self.buf[self.numel:].copy_(fl)  # device to device: no host round trip per step
         dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group)
-        present = (flags > 0).tolist()
+        present = self._present.get(local)
+        if present is None:
+            # read back once per local pattern: the ranks run the same model, so the pattern a
+            # rank sees for a given local pattern does not change between steps
+            present = self._present[local] = tuple((self.buf[self.numel:] > 0).tolist())
         if self.average:
             self.buf[:self.numel].div_(dist.get_world_size(self.group))
-        off = 0
-        for p, has in zip(self.params, present):
-            n = p.numel()
-            if has:
-                g = self.buf[off:off + n].view_as(p)
-                if p.grad is None:
-                    p.grad = g.clone()
-                else:
-                    p.grad.copy_(g)
-            off += n
+        for p, v, has in zip(self.params, self.views, present):
+            if has and p.grad is None:
+                p.grad = v  # the sum over the ranks that had one (zeros elsewhere)

@@ -91,6 +91,42 @@ def known_amax(X):
     return rec[0], rec[1]
 
 
+# Per-row A maxima (mvml_gemm_f16x2_rows): the split-fp16 products whose A rows are atoms or
+# molecules split every row with its own scale — per-row fp32 accuracy, and a row's result
+# independent of the batch it is computed in (a shard gives bitwise its slice of the whole
+# batch).  MVML_ROW_SCALES=0: one scale per operand (the round-3 path).
+ROW_SCALES = os.environ.get("MVML_ROW_SCALES", "1") != "0"
+
+
+def known_rows(X):
+    """Per-row |max| bits of X (int32 [rows]) if its producer recorded them (same rule as
+    known_amax), else None."""
+    rec = getattr(X, "_mvml_rows", None)
+    if rec is None or rec[1] != X._version or rec[2] != (X.data_ptr(), tuple(X.shape), X.stride()):
+        return None
+    return rec[0]
+
+
+def fold_rows(out, rows):
+    """Record that rows[r] holds max |out[r, :]| bits (written with out by its producer)."""
+    out._mvml_rows = (rows, out._version, (out.data_ptr(), tuple(out.shape), out.stride()))
+
+
+def absmax_rows(P, rows, cols, ld, out=None, offset=0, accumulate=False):
+    """out[r] (int32 [rows]) = bits of max_c |P[r, offset + c]| (mvml_absmax_rows_f32)."""
+    if out is None:
+        out = torch.empty(max(rows, 1), dtype=torch.int32, device=P.device)
+    pp = ctypes.c_void_p(ptr(P).value + 4 * offset)
+    call("mvml_absmax_rows_f32", rows, cols, pp, ld, ptr(out), int(accumulate), _stream(P.device))
+    return out
+
+
+def row_maxima(X, rows, cols, ld):
+    """Per-row |max| bits of a K-contiguous operand: its producer's record, else one pass."""
+    r = known_rows(X)
+    return r if r is not None else absmax_rows(X, rows, cols, ld)
+
+
 def fold_amax(out, amx, slot_idx):
     """Record that out's |max| bits are in amx[slot_idx] (folded by the kernel that wrote out)."""
     out._mvml_amax = (amx, slot_idx, out._version, (out.data_ptr(), tuple(out.shape), out.stride()))
@@ -131,16 +167,24 @@ def split_planes(W, rows, cols, ld, amax_ptr):
 
 
 def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0, algo=None,
-         amax=None, bsplit=None):
+         amax=None, bsplit=None, arows=None):
     """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32 / mvml_gemm_f32x3 /
     mvml_gemm_f16x2).  amax = (pointer to |A| max bits, pointer to |B| max bits) from absmax()
-    lets split-fp16 products that share an operand share its max pass."""
+    lets split-fp16 products that share an operand share its max pass.  arows (split-fp16,
+    K-contiguous A): per-row |A| max bits (int32 [M]) — every A row gets its own scale
+    (mvml_gemm_f16x2_rows); amax then only needs B's pointer."""
     _lib.call_tag[0] = {"flops": 2 * M * N * K, "shape": (M, N, K, int(a_kmajor), int(b_kmajor))}
     L = _lib.lib()
     dev = C.device
     wsz = L.mvml_gemm_workspace_size(M, N, K)
     wp, wn = _lib.ws_ptr_size(wsz, dev)
     algo = algo or GEMM_ALGO
+    if algo == "f16x2" and arows is not None:
+        if a_kmajor or amax is None or amax[1] is None:
+            raise ValueError("gemm: per-row A maxima need a K-contiguous A and max |B|")
+        call("mvml_gemm_f16x2_rows", M, N, K, ptr(A), lda, ptr(B), ldb, int(b_kmajor), ptr(arows),
+             amax[1], ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
+        return
     if algo == "f16x2" and amax is not None and bsplit is not None:  # B from its pre-split planes
         call("mvml_gemm_f16x2_bsplit", int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda, ptr(B), ldb,
              ptr(bsplit[0]), bsplit[1], amax[0], amax[1], ptr(bias), float(beta), int(act), ptr(C), ldc,
@@ -206,10 +250,18 @@ class GATLayerFunction(torch.autograd.Function):
         # pass serves all of its products (projection, dL/dW, dL/dX)
         amx = None
         ax = None  # (tensor, slot) of max |X|
+        xr = None  # per-row max |X| bits (ROW_SCALES)
         wps = (None, 0)
         if (algo or GEMM_ALGO) == "f16x2":
             amx = torch.zeros(4, dtype=torch.int32, device=dev)  # [X, Wcat, gY (bwd), out]
-            ax = known_amax(Xp) if Xp is X else None  # layer 2: folded by layer 1's aggregation
+            if ROW_SCALES and PROJ_ELR_GEMM:
+                # the projection splits every atom row with its own scale; max |X| (the weight
+                # gradient's A-side scale) is the max of the row maxima (N floats, not N x Fp)
+                xr = row_maxima(Xp, N, Fp, Fp)
+                absmax(xr, N, 1, 1, amx, 0)
+                ax = (amx, 0)
+            else:
+                ax = known_amax(Xp) if Xp is X else None  # layer 2: folded by layer 1's aggregation
             if ax is None:
                 absmax(Xp, N, Fp, Fp, amx, 0)
                 ax = (amx, 0)
@@ -226,7 +278,10 @@ class GATLayerFunction(torch.autograd.Function):
             # stores (9.5 -> ~5 ms per config-3 layer-2 launch)
             ldy = _row_pitch(C + 2 * H)
             Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
-            if amx is not None:
+            if xr is not None:
+                gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(None, slot(amx, 1)),
+                     arows=xr)
+            elif amx is not None:
                 gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(slot(*ax), slot(amx, 1)),
                      bsplit=None if wps[0] is None else wps)
             else:
@@ -318,9 +373,13 @@ class GATLayerFunction(torch.autograd.Function):
         gX = None
         if ctx.needs_input_grad[0]:
             gX = torch.empty((N, Fin), dtype=torch.float32, device=dev)
-            gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, algo=ctx.algo,
-                 amax=None if amx is None else (slot(amx, 2), slot(amx, 1)),
-                 bsplit=None if ctx.wps[0] is None else ctx.wps)
+            if amx is not None and ROW_SCALES:  # every atom's gradient row at its own scale
+                gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, amax=(None, slot(amx, 1)),
+                     arows=absmax_rows(gY, N, CE, ldg))
+            else:
+                gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, algo=ctx.algo,
+                     amax=None if amx is None else (slot(amx, 2), slot(amx, 1)),
+                     bsplit=None if ctx.wps[0] is None else ctx.wps)
         return gX, g_fc, g_res, g_al, g_ar, g_bias, None, None, None, None, None, None
 
 
@@ -364,6 +423,7 @@ class Set2SetFunction(torch.autograd.Function):
         lse = torch.empty((T, B), **f32)
         gates = torch.empty((B, 4 * D), **f32)
         amax_x = amax_w = None
+        mrows = None  # per-molecule bound of every cell's A row (ROW_SCALES)
         wsp = [(None, 0)] * Lr
         if GEMM_ALGO == "f16x2":
             # split-fp16 operand maxima of the cells' GEMMs: every A row [x | h_prev] holds
@@ -376,6 +436,13 @@ class Set2SetFunction(torch.autograd.Function):
             else:
                 amax_x = torch.full((1,), 0x3F800000, dtype=torch.int32, device=dev)  # 1.0f
                 absmax(X, N, D, D, amax_x, 0, accumulate=True)
+            if ROW_SCALES:
+                # per molecule: max(1, max |X| over its atoms) bounds every entry of its cell rows
+                # [x | h] (h = o tanh c, the readout a convex combination of its own atoms' rows),
+                # so a molecule's cells are split at a scale of its own
+                xr = row_maxima(X, N, D, D)
+                mrows = torch.empty(max(B, 1), dtype=torch.int32, device=dev)
+                call("mvml_segment_max_bits", B, ptr(g.node_offsets), ptr(xr), 0x3F800000, ptr(mrows), st)
             amax_w = torch.empty(Lr, dtype=torch.int32, device=dev)
             for l in range(Lr):
                 absmax(Wcat[l], 4 * D, kin[l] + D, kin[l] + D, amax_w, l)  # = Wperm's max
@@ -398,15 +465,15 @@ class Set2SetFunction(torch.autograd.Function):
                     _lib.call_tag[0] = {"flops": 2 * B * 4 * D * K, "shape": (B, 4 * D, K, 0, 0, "cell")}
                     call("mvml_lstm_gates_cell_fwd", B, D, K, ptr(XH[l][t]), kin[l] + D, ptr(Wperm[l]),
                          kin[l] + D, ptr(b_ih), ptr(b_hh), ptr(c_prev), ptr(cs[t, l]), ptr(own),
-                         kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, pa, pw, ptr(wsp[l][0]),
-                         wsp[l][1], st)
+                         kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, pa, pw, ptr(mrows),
+                         ptr(wsp[l][0]), wsp[l][1], st)
                     continue
                 if t == 0 and l == 0:
                     gates.zero_()  # q*_{-1} = 0 and h_0(-1) = 0
                 else:
                     gemm(XH[l][t], Wcat[l], B, 4 * D, K, 0, 0, kin[l] + D, kin[l] + D, gates, 4 * D,
                          amax=None if amax_x is None else (slot(amax_x, 0), slot(amax_w, l)),
-                         bsplit=None if CELL_EPI or wsp[l][0] is None else wsp[l])
+                         bsplit=None if CELL_EPI or wsp[l][0] is None else wsp[l], arows=mrows)
                 call("mvml_lstm_cell_fwd", B, D, ptr(gates), ptr(b_ih), ptr(b_hh), ptr(c_prev),
                      ptr(cs[t, l]), ptr(own), kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, st)
             call("mvml_set2set_seg_fwd", B, D, ptr(g.node_offsets), ptr(X), ptr(XH[0][t + 1]), 3 * D,
@@ -459,6 +526,7 @@ class Set2SetFunction(torch.autograd.Function):
         # running value bounds every cell seen so far, which is all a scale needs)
         amax_x, amax_w = ctx.amax
         amax_g = torch.zeros(Lr, dtype=torch.int32, device=dev) if amax_x is not None else None
+        grow = torch.empty(max(B, 1), dtype=torch.int32, device=dev) if amax_g is not None else None
         wsb = [None] * Lr  # [W_ih | W_hh] split once for the per-cell data-gradient products
         if amax_g is not None and BSPLIT:
             wsb = [split_planes(Wcat[l], 4 * D, Wcat[l].shape[1], Wcat[l].shape[1], slot(amax_w, l))
@@ -486,9 +554,13 @@ class Set2SetFunction(torch.autograd.Function):
                 ncols = kin + D if t > 0 else (kin if l > 0 else 0)
                 if ncols:
                     out, ldo = (g_qs3[t - 1], 3 * D) if l == 0 else (gxh[l], 2 * D)
-                    gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo,
-                         amax=None if amax_g is None else (slot(amax_g, l), slot(amax_w, l)),
-                         bsplit=wsb[l])
+                    if amax_g is not None and ROW_SCALES:  # each molecule's gate gradients at its own scale
+                        gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo,
+                             amax=(None, slot(amax_w, l)), arows=absmax_rows(g_gates, B, 4 * D, 4 * D, grow))
+                    else:
+                        gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo,
+                             amax=None if amax_g is None else (slot(amax_g, l), slot(amax_w, l)),
+                             bsplit=wsb[l])
         # weight / bias gradients, one product per parameter over all steps:
         #   dW_ih[l] = sum_t g_gates[l,t]^T x_l(t),  dW_hh[l] = sum_{t>=1} g_gates[l,t]^T h_l(t-1)
         # (layer 0's input x_0(t) = q*_{t-1} is zero at t = 0; h_l(-1) = 0)
@@ -552,17 +624,43 @@ class GraphNormFunction(torch.autograd.Function):
 
 def linear_maxima(x, w):
     """Split-fp16 maxima of a Linear's three products: slots [x, w, grad] (x's from its
-    producer when it folded one), one pass per operand instead of one per product; None for
-    the other algorithms."""
+    producer when it folded one), one pass per operand instead of one per product, and (ROW_SCALES)
+    x's per-row maxima for the forward product; None for the other algorithms."""
     if GEMM_ALGO != "f16x2":
         return None
     amx = torch.zeros(3, dtype=torch.int32, device=x.device)
-    kx = known_amax(x)
+    xr = None
+    if ROW_SCALES:
+        xr = row_maxima(x, x.shape[0], x.shape[1], x.shape[1])
+        absmax(xr, x.shape[0], 1, 1, amx, 0)
+        kx = (amx, 0)
+    else:
+        kx = known_amax(x)
     if kx is None:
         absmax(x, x.shape[0], x.shape[1], x.shape[1], amx, 0)
         kx = (amx, 0)
     absmax(w, w.shape[0], w.shape[1], w.shape[1], amx, 1)
-    return amx, kx
+    return amx, kx, xr
+
+
+def linear_fwd(x, weight, y, M, Nout, K, lm, bias=None, act=0):
+    """y = act(x W^T + b): the forward product of a Linear (per-row x scales when lm has them)."""
+    if lm is not None and lm[2] is not None:
+        gemm(x, weight, M, Nout, K, 0, 0, K, K, y, Nout, bias=bias, act=act, amax=(None, slot(lm[0], 1)),
+             arows=lm[2])
+    else:
+        gemm(x, weight, M, Nout, K, 0, 0, K, K, y, Nout, bias=bias, act=act,
+             amax=None if lm is None else (slot(*lm[1]), slot(lm[0], 1)))
+
+
+def linear_dx(g, weight, gx, M, Nout, K, lm):
+    """gx = g W (the data gradient of a Linear; per-row g scales under ROW_SCALES)."""
+    if lm is not None and lm[2] is not None:
+        gemm(g, weight, M, K, Nout, 0, 1, Nout, K, gx, K, amax=(None, slot(lm[0], 1)),
+             arows=absmax_rows(g, M, Nout, Nout))
+    else:
+        gemm(g, weight, M, K, Nout, 0, 1, Nout, K, gx, K,
+             amax=None if lm is None else (slot(lm[0], 2), slot(lm[0], 1)))
 
 
 class LinearReLUFunction(torch.autograd.Function):
@@ -578,8 +676,7 @@ class LinearReLUFunction(torch.autograd.Function):
         y = torch.empty((M, Nout), dtype=torch.float32, device=x.device)
         weight = _c(weight)
         lm = ctx.lm = linear_maxima(x, weight)
-        gemm(x, weight, M, Nout, K, 0, 0, K, K, y, Nout, bias=_c(bias), act=1,
-             amax=None if lm is None else (slot(*lm[1]), slot(lm[0], 1)))
+        linear_fwd(x, weight, y, M, Nout, K, lm, bias=_c(bias), act=1)
         if DEBUG_CAPTURE is not None:  # the ReLU sides the product took (parity tests)
             DEBUG_CAPTURE.setdefault("relu_out", []).append(y.detach())
         ctx.save_for_backward(x, weight, y)
@@ -605,6 +702,5 @@ class LinearReLUFunction(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
-            gemm(g_pre, weight, M, K, Nout, 0, 1, Nout, K, gx, K,
-                 amax=None if lm is None else (slot(lm[0], 2), slot(lm[0], 1)))
+            linear_dx(g_pre, weight, gx, M, Nout, K, lm)
         return gx, gw, gb

@@ -34,8 +34,7 @@ class LinearFunction(torch.autograd.Function):
         y = torch.empty((M, Nout), dtype=torch.float32, device=x.device)
         weight = _c(weight)
         lm = ctx.lm = _F.linear_maxima(x, weight)
-        gemm(x, weight, M, Nout, K, 0, 0, K, K, y, Nout, bias=_c(bias),
-             amax=None if lm is None else (slot(*lm[1]), slot(lm[0], 1)))
+        _F.linear_fwd(x, weight, y, M, Nout, K, lm, bias=_c(bias))
         ctx.save_for_backward(x, weight)
         return y
 
@@ -56,8 +55,7 @@ class LinearFunction(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
-            gemm(g_y, weight, M, K, Nout, 0, 1, Nout, K, gx, K,
-                 amax=None if lm is None else (slot(lm[0], 2), slot(lm[0], 1)))
+            _F.linear_dx(g_y, weight, gx, M, Nout, K, lm)
         return gx, gw, gb
 
 
@@ -115,7 +113,13 @@ class FusionAttnConvFunction(torch.autograd.Function):
             gemm_batched(wq3, wk3, D, D, D, 1, 1, D, D, Bcat, 2 * HD, H, D * D, D * D, D)
             Bcat[:, HD:].copy_(_c(wv).t())  # parameter layout (7 MB), not a product
             PV = torch.empty((3 * B, 2 * HD), **f32)  # rows 3b+t: [x M_1 .. x M_H | x W_v^T]
-            gemm(Xn, Bcat, 3 * B, 2 * HD, D, 0, 1, D, 2 * HD, PV, 2 * HD)
+            if _F.GEMM_ALGO == "f16x2" and _F.ROW_SCALES:  # every token row at its own scale
+                bmx = torch.zeros(1, dtype=torch.int32, device=dev)
+                absmax(Bcat, D, 2 * HD, 2 * HD, bmx, 0)
+                gemm(Xn, Bcat, 3 * B, 2 * HD, D, 0, 1, D, 2 * HD, PV, 2 * HD, amax=(None, slot(bmx, 0)),
+                     arows=_F.absmax_rows(Xn, 3 * B, D, D))
+            else:
+                gemm(Xn, Bcat, 3 * B, 2 * HD, D, 0, 1, D, 2 * HD, PV, 2 * HD)
             if fused:
                 _lib.call_tag[0] = {"bytes": attn_conv_bytes(B, H, D, False)}
                 call("mvml_attn_conv_fwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
@@ -186,8 +190,12 @@ class FusionAttnConvFunction(torch.autograd.Function):
             # per head h (G2 rows h D .. h D + D): W_k,h dM_h^T and W_q,h dM_h
             gemm_batched(wk3, G2, D, D, D, 0, 1, D, D, gWq, D, H, D * D, D * D, D * D)
             gemm_batched(wq3, G2, D, D, D, 0, 0, D, D, gWk, D, H, D * D, D * D, D * D)
-            gemm(gPV, Bcat, 3 * B, D, 2 * HD, 0, 0, 2 * HD, 2 * HD, gXn, D, beta=1.0,
-                 amax=None if amx is None else (slot(amx, 0), slot(amx, 2)))
+            if amx is not None and _F.ROW_SCALES:  # every token row's gradient at its own scale
+                gemm(gPV, Bcat, 3 * B, D, 2 * HD, 0, 0, 2 * HD, 2 * HD, gXn, D, beta=1.0,
+                     amax=(None, slot(amx, 2)), arows=_F.absmax_rows(gPV, 3 * B, 2 * HD, 2 * HD))
+            else:
+                gemm(gPV, Bcat, 3 * B, D, 2 * HD, 0, 0, 2 * HD, 2 * HD, gXn, D, beta=1.0,
+                     amax=None if amx is None else (slot(amx, 0), slot(amx, 2)))
             g_wq, g_wk, g_wv = gWq.view(HD, D), gWk.view(HD, D), G2[HD:]
         else:
             Wqkv, QKV = S0, S1

@@ -80,6 +80,19 @@ class MVP(MVFusion):
         return self.sigmoid(self.forward(smiles, graphs, atom_feats, fp_t))
 
 
+def join_side_stream(dev):
+    """Make the current stream wait for the SMILES view's side stream.  After backward the
+    side stream has accumulated that view's parameter gradients; the reducer and the optimizer
+    read them on the current stream.  Autograd's end-of-backward leaf-stream sync already
+    orders this, and this explicit wait (one event) keeps the order from depending on it."""
+    dev = torch.device(dev)
+    if dev.type != "cuda" or not OVERLAP_VIEWS:
+        return
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key in _SIDE:
+        torch.cuda.current_stream(dev).wait_stream(_SIDE[key])
+
+
 def train_step(model, optimizer, batch, reducer=None, loss_fn=bce_with_logits):
     """main.py:24-36 for one batch: forward, BCEWithLogitsLoss (main.py:91), backward, the
     data-parallel flat gradient all-reduce (reducer, BASELINE config 4), optimizer step.
@@ -93,6 +106,7 @@ def train_step(model, optimizer, batch, reducer=None, loss_fn=bce_with_logits):
     optimizer.zero_grad(set_to_none=False)
     loss = loss_fn(model(smiles, graphs, atom_feats, fp_t), labels)
     loss.backward()
+    join_side_stream(atom_feats.device)
     if reducer is not None:
         reducer()
     optimizer.step()

@@ -159,10 +159,11 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         In = x.shape[-1]
         out = torch.zeros((T, B, 2 * H), dtype=torch.float32, device=dev)
         saved, gates_d = [], []
-        wide_pack = WIDE_PACK and not _use_seq(pk, H) and In % 4 == 0
+        wide_pack = WIDE_PACK and not _use_seq(pk, H) and In % 4 == 0 and H % 4 == 0
         amx = _h_bounds(w, dev) if not _use_seq(pk, H) else None
-        # the native wide recurrence reads a packed input projection directly (no unpack)
-        gx_packed = wide_pack and not layer0 and WIDE_STEP and amx is not None
+        # the native wide recurrence (H % 8 == 0) reads a packed input projection directly
+        wide_step = WIDE_STEP and amx is not None and _wide_step_ok(H)
+        gx_packed = wide_pack and not layer0 and wide_step
         xp = None
         for d in range(2):
             w_ih = _c(w[4 * d])
@@ -196,7 +197,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                  ptr(gates_d[1]), ptr(wc[1]), ptr(wc[5]), ptr(wc[2]), ptr(wc[3]), ptr(wc[6]),
                  ptr(wc[7]), ptr(out), ptr(c[0]), ptr(c[1]), ptr(act[0]), ptr(act[1]), st)
             saved = [c[0], act[0], c[1], act[1]]
-        elif WIDE_STEP and amx is not None:
+        elif wide_step:
             # wide batches: one launch per time step for both directions, the recurrent product
             # and the LSTM cell fused (mvml_bilstm_wide_step_fwd)
             wperm = [_c(w[4 * d + 1]).view(4, H, H).transpose(0, 1).reshape(G, H).contiguous()
@@ -251,10 +252,11 @@ class BiLSTMLayerFunction(torch.autograd.Function):
         w_hhT = [_c(w[4 * d + 1]).t().contiguous() for d in range(2)]
         seq = _use_seq(pk, H)
         amx = None if seq else _h_bounds(w, dev)
-        packed = not seq and WIDE_PACK and In % 4 == 0
+        packed = not seq and WIDE_PACK and In % 4 == 0 and H % 4 == 0
+        wide_step = not seq and WIDE_STEP and amx is not None and _wide_step_ok(H)
         # the native wide recurrence writes the gate gradients packed (live rows only: no zero
         # fill of T x B rows, no pack before the weight-gradient products)
-        gg_packed = packed and WIDE_STEP and amx is not None
+        gg_packed = packed and wide_step
         if gg_packed:
             n_live = pk.live_offsets(0, T)[1]
             ggs = [torch.empty((n_live, G), dtype=torch.float32, device=dev) for _ in range(2)]
@@ -270,7 +272,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
             # running max |dgates| per direction, folded in by mvml_lstm_cell_bwd (a bound for
             # every step already processed, which is all a scale needs)
             amg = torch.zeros(2, dtype=torch.int32, device=dev) if amx is not None else None
-        if not seq and WIDE_STEP and amx is not None:
+        if wide_step:
             # wide batches: one launch per step for both directions (the recurrent product split in
             # two K halves) + one fused reduce / cell-backward launch (mvml_bilstm_wide_step_bwd)
             carry = torch.zeros((2, 2, B, H), dtype=torch.float32, device=dev)
@@ -378,6 +380,12 @@ def _unpack(pk, packed, tm, cols, ld):
     offs, n = pk.live_offsets(0, pk.T)
     call("mvml_bilstm_pack_rows", n, pk.T, pk.B, cols, ptr(offs), 0, 0, ptr(tm), ld, ptr(packed),
          packed.stride(0), 1, _stream(tm.device))
+
+
+def _wide_step_ok(H):
+    """mvml_bilstm_wide_fwd / _bwd take H % 8 == 0 (16-B rows of the interleaved W_hh image
+    and of the cell epilogue); other hidden sizes run the per-step GEMM + cell kernels."""
+    return H % 8 == 0
 
 
 def _h_bounds(w, dev):

@@ -1,0 +1,127 @@
+"""Two data-parallel ranks of the HIP model on the one-GPU box.
+
+bench.py --gpus N shards the global molecule set in whole GraphNorm groups, runs the view +
+fusion step on each rank and all-reduces one flat gradient buffer (mvml_gat.dist).  The gloo
+tests cover that decomposition on the CPU oracle; here two child processes (ranks 0 and 1, both
+on cuda:0, gloo over the device tensors — RCCL refuses two ranks on one device) run the HIP
+GNNModule + MVFusion on their shards, FlatGradAllReduce sums the gradients and
+EmbeddingAllGather assembles the embeddings.  Rank 0 then runs the whole batch in one process
+and checks: reduced gradients within 1e-5 of the single-process ones, the gathered embeddings
+BITWISE equal (per-row split-fp16 scales: a molecule's embedding does not depend on its batch),
+and a second step reusing the reducer's cached presence flags.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_CHILD = textwrap.dedent(r"""
+    import json, os, sys
+    sys.path[:0] = [os.path.join(os.environ["MVML_ROOT"], "mvml-mpi_amd"), os.environ["MVML_ROOT"]]
+    import torch
+    import torch.distributed as dist
+    import mvml_gat
+    from mvml_gat import synth
+    from mvml_gat.dist import EmbeddingAllGather, FlatGradAllReduce, shard_groups
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    gs, total = 64, 6 * 64
+    gset = synth.Config3Set(total, seed=11)
+    g0, g1 = shard_groups(gset.group_costs(gs), world, rank)
+    lo, hi = g0 * gs, min(g1 * gs, total)
+    gen = torch.Generator().manual_seed(5)
+    sx = torch.randn(total, 384, generator=gen).to(dev)
+    fx = torch.randn(total, 384, generator=gen).to(dev)
+    y = (torch.rand(total, 11, generator=gen) > 0.8).float().to(dev)
+
+    def models():
+        torch.manual_seed(0)
+        m = mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3).to(dev).eval()
+        f = mvml_gat.MVFusion(384, 12, 11, 0.5).to(dev).eval()
+        return m, f, list(m.parameters()) + list(f.parameters())
+
+    def step(m, f, a, b, red):
+        sb = gset.molecules(a, b)
+        g = sb.to_graph(group_size=gs).to(dev)
+        emb = m(g, g.ndata["h"])
+        # this rank's share of the global mean BCE: the ranks' losses sum to the whole batch's
+        loss = mvml_gat.bce_with_logits(f(sx[a:b], emb, fx[a:b]), y[a:b]) * ((b - a) / total)
+        loss.backward()
+        if red is not None:
+            red()
+        return emb.detach()
+
+    m, f, params = models()
+    red = FlatGradAllReduce(params, average=False)
+    emb = step(m, f, lo, hi, red)
+    full = EmbeddingAllGather()(emb.contiguous())
+    grads = [p.grad.clone() for p in params]
+    for p in params:  # a second step: cached flags, gradients accumulated in the flat buffer
+        p.grad.zero_()
+    step(m, f, lo, hi, red)
+    grads2 = [p.grad.clone() for p in params]
+    out = {"rank": rank, "shard": [lo, hi]}
+    if rank == 0:
+        m1, f1, p1 = models()
+        emb1 = step(m1, f1, 0, total, None)
+        def rel(a, b):
+            return ((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30)).item()
+        out["emb_bitwise"] = bool(torch.equal(full, emb1))
+        out["emb_max_diff"] = float((full - emb1).abs().max())
+        out["grad_rel"] = max(rel(a, p.grad) for a, p in zip(grads, p1))
+        out["grad2_equal"] = all(torch.equal(a, b) for a, b in zip(grads, grads2))
+        out["flags_cached"] = len(red._present)
+    torch.cuda.synchronize()
+    dist.barrier()
+    dist.destroy_process_group()
+    print("DP2 " + json.dumps(out), flush=True)
+""")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_two_hip_ranks_match_single_process():
+    port = str(_free_port())
+    procs = []
+    for r in range(2):
+        env = dict(os.environ)
+        env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RANK=str(r), WORLD_SIZE="2",
+                   LOCAL_RANK="0", MVML_ROOT=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, "-c", _CHILD], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=360)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, o[-2000:] + e[-4000:]
+        outs.append(o)
+    res = [json.loads(l[4:]) for o in outs for l in o.splitlines() if l.startswith("DP2 ")]
+    r0 = next(r for r in res if r["rank"] == 0)
+    r1 = next(r for r in res if r["rank"] == 1)
+    print(res)
+    assert r0["shard"][1] == r1["shard"][0] and r0["shard"][0] == 0 and r1["shard"][1] == 384
+    assert 0 < r0["shard"][1] < 384  # both ranks hold molecules
+    assert r0["emb_bitwise"], r0
+    assert r0["grad_rel"] < 1e-5, r0
+    assert r0["grad2_equal"] and r0["flags_cached"] == 1, r0

@@ -1,0 +1,217 @@
+"""Per-row split-fp16 scales (mvml_gemm_f16x2_rows).
+
+With one power-of-two scale per operand, a row of A far below the operand's max loses relative
+precision once its low fp16 plane goes subnormal (~2^17 below the max).  With a scale per A row
+every row keeps fp32-GEMM accuracy relative to itself, and a row of the product depends only on
+its own row of A: the graph view's embedding of a molecule is then bitwise the same in any batch
+(whole GraphNorm groups), which is what data-parallel sharding needs.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+TOL = 1e-5
+
+
+def _margins_dir():
+    out = os.environ.get("MVML_MARGINS_DIR", os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "gpurun_out", "parity_margins"))
+    os.makedirs(out, exist_ok=True)
+    return out
+
+
+@pytest.mark.parametrize("tile", [0, 128, 256])
+@pytest.mark.parametrize("bk", [0, 1])
+def test_gemm_f16x2_rows_dynamic_range(tile, bk):
+    """Rows of A scaled 2^+12 .. 2^-28 (and an all-zero row): every row within 1e-5 of the
+    float64 product relative to ITS OWN max, on the 256x256 tile, the 128x128 staged tile and
+    the planner's choice; the operand-wide path is recorded beside it."""
+    from mvml_gat._lib import option
+    from mvml_gat.functional import absmax, absmax_rows, gemm, slot
+    g = torch.Generator().manual_seed(31 + bk + tile)
+    M, N, K = 1024, 448, 768
+    exps = torch.tensor([-12, 0, 8, 12, 16, 18, 20, 22, 24, 28], dtype=torch.float64)
+    row_exp = exps[torch.arange(M) % len(exps)]
+    A = (torch.randn(M, K, generator=g, dtype=torch.float64) * torch.pow(2.0, -row_exp).unsqueeze(1)).float()
+    A[7] = 0.0
+    B = torch.randn(N, K, generator=g, dtype=torch.float64).float()
+    ref = A.double() @ B.double().t()
+    Ad = A.to(DEV)
+    Bd = (B.t().contiguous() if bk else B).to(DEV)
+    ldb = N if bk else K
+    res = {}
+    with option("gemm_tile", tile):
+        C = torch.zeros(M, N, device=DEV)
+        bmx = torch.zeros(1, dtype=torch.int32, device=DEV)
+        absmax(Bd, Bd.shape[0], Bd.shape[1], Bd.shape[1], bmx, 0)
+        rows = absmax_rows(Ad, M, K, K)
+        gemm(Ad, Bd, M, N, K, 0, bk, K, ldb, C, N, amax=(None, slot(bmx, 0)), arows=rows)
+        C0 = torch.zeros(M, N, device=DEV)
+        gemm(Ad, Bd, M, N, K, 0, bk, K, ldb, C0, N, algo="f16x2")
+    for name, out in (("rows", C), ("operand", C0)):
+        den = ref.abs().max(1).values.clamp_min(1e-300)
+        d = (out.double().cpu() - ref).abs().max(1).values / den
+        d[7] = (out[7].double().cpu()).abs().max()  # the zero row must come out exactly zero
+        res[name] = {int(e): d[row_exp == e].max().item() for e in exps.tolist()}
+        res[name]["normwise"] = rel_err(out, ref)
+    with open(os.path.join(_margins_dir(), f"gemm_rows_dynamic_range_t{tile}_bk{bk}.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print(res)
+    assert float(C[7].abs().max()) == 0.0
+    for e in exps.tolist():
+        assert res["rows"][int(e)] < TOL, (e, res["rows"])
+
+
+@pytest.mark.parametrize("tile", [0, 128, 256])
+def test_gemm_f16x2_rows_batch_invariant(tile):
+    """A row's product is bitwise the same whatever other rows share the launch (and whatever
+    tile the planner picks for the smaller launch)."""
+    from mvml_gat._lib import option
+    from mvml_gat.functional import absmax, absmax_rows, gemm, slot
+    g = torch.Generator().manual_seed(5 + tile)
+    M, N, K = 1500, 640, 768
+    A = (torch.randn(M, K, generator=g) * torch.pow(2.0, torch.randint(-20, 6, (M, 1), generator=g).float())).to(DEV)
+    A[:40] *= 1e4  # the big rows sit in the first slice only
+    B = torch.randn(N, K, generator=g).to(DEV)
+    bmx = torch.zeros(1, dtype=torch.int32, device=DEV)
+    absmax(B, N, K, K, bmx, 0)
+    with option("gemm_tile", tile):
+        full = torch.empty(M, N, device=DEV)
+        gemm(A, B, M, N, K, 0, 0, K, K, full, N, amax=(None, slot(bmx, 0)), arows=absmax_rows(A, M, K, K))
+        for lo, hi in ((0, 300), (300, 1500), (777, 1001), (1499, 1500)):
+            part = torch.empty(hi - lo, N, device=DEV)
+            As = A[lo:hi].contiguous()
+            gemm(As, B, hi - lo, N, K, 0, 0, K, K, part, N, amax=(None, slot(bmx, 0)),
+                 arows=absmax_rows(As, hi - lo, K, K))
+            assert torch.equal(part, full[lo:hi]), (lo, hi)
+
+
+def test_absmax_rows_matches_torch():
+    from mvml_gat.functional import absmax_rows
+    g = torch.Generator().manual_seed(2)
+    for rows, cols, ld in ((1, 1, 1), (1000, 76, 76), (333, 1928, 1984), (64, 5, 7), (10, 3000, 3000)):
+        X = torch.randn(rows, ld, generator=g).to(DEV)
+        r = absmax_rows(X, rows, cols, ld)
+        want = X[:, :cols].abs().amax(1)
+        assert torch.equal(r[:rows].view(torch.float32), want), (rows, cols, ld)
+
+
+def _config3_batch(n, seed=3):
+    from mvml_gat import synth
+    return synth.Config3Set(n, seed=seed).molecules(0, n)
+
+
+@pytest.mark.parametrize("proj", [None, "bf16"])
+def test_gnn_module_shard_invariant_bitwise(proj):
+    """GNNModule (eval) on whole-GraphNorm-group slices of a batch gives bitwise the rows of
+    the whole batch: the per-row / per-molecule split-fp16 scales make every product row depend
+    on its own molecule only (the bf16 projection has no scales at all)."""
+    import mvml_gat
+    from mvml_gat.synth import slice_batch
+    gs = 64
+    sb = _config3_batch(8 * gs)
+    torch.manual_seed(0)
+    model = mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3,
+                               proj_dtype=torch.bfloat16 if proj else None).to(DEV).eval()
+    with torch.no_grad():
+        g = sb.to_graph(group_size=gs).to(DEV)
+        full = model(g, g.ndata["h"])
+        for lo, hi in ((0, 64), (64, 320), (320, 512), (448, 512)):
+            part_sb = slice_batch(sb, lo, hi)
+            gp = part_sb.to_graph(group_size=gs).to(DEV)
+            part = model(gp, gp.ndata["h"])
+            assert torch.equal(part, full[lo:hi]), (lo, hi, (part - full[lo:hi]).abs().max().item())
+
+
+def test_fusion_shard_invariant_bitwise():
+    """MVFusion (eval) is per molecule: its logits on a slice equal the whole batch's rows."""
+    import mvml_gat
+    torch.manual_seed(1)
+    fus = mvml_gat.MVFusion(384, 12, 11, 0.5).to(DEV).eval()
+    g = torch.Generator().manual_seed(4)
+    B = 700
+    xs = [(torch.randn(B, 384, generator=g) * torch.pow(2.0, torch.randint(-12, 4, (B, 1), generator=g).float())).to(DEV)
+          for _ in range(3)]
+    with torch.no_grad():
+        full = fus(*xs)
+        for lo, hi in ((0, 100), (100, 700), (350, 351)):
+            part = fus(*[x[lo:hi] for x in xs])
+            assert torch.equal(part, full[lo:hi]), (lo, hi)
+
+
+def test_saturated_logits_per_molecule_gradients():
+    """one config-3 step (GNNModule -> MVFusion -> BCE) whose logits mix
+    saturated molecules (every |z| >= 20: BCE gradients ~1e-9) with molecules near |z| ~ 0
+    (gradients ~0.1) in one batch — the classifier's weights scaled so that 60 % of the
+    molecules saturate.  Per molecule, dL/d(graph embedding) within 1e-5 of the float64 oracle
+    relative to that molecule's OWN largest entry (per-row split-fp16 scales), and every
+    parameter gradient within 1e-5 norm-wise; margins to profiles via MVML_MARGINS_DIR."""
+    import mvml_gat
+    from _util import graph_dict
+    from oracle.fusion_ref import MVFusionRef, bce_logits_ref
+    from oracle.gnn_ref import GNNModuleRef
+    gs = 64
+    sb = _config3_batch(4 * gs, seed=9)
+    B = sb.batch_size
+    torch.manual_seed(2)
+    model = mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3).to(DEV).eval()
+    fus = mvml_gat.MVFusion(384, 12, 11, 0.5).to(DEV).eval()
+    ref = GNNModuleRef(74, [192, 384], 0.5, 6, 3).double().eval()
+    fref = MVFusionRef(384, 12, 11, 0.5).double().eval()
+    ref.load_state_dict({k: v.double() for k, v in model.state_dict().items()})
+    g = torch.Generator().manual_seed(8)
+    sx = torch.randn(B, 384, generator=g, dtype=torch.float64)
+    fx = torch.randn(B, 384, generator=g, dtype=torch.float64)
+    gd = graph_dict(sb, group_size=gs)
+    X64 = torch.as_tensor(sb.feats, dtype=torch.float64)
+    # scale the classifier so that the 40th percentile of min_c |z| lands at 20
+    with torch.no_grad():
+        fus.mlp[3].bias.zero_()
+        fref.load_state_dict({k: v.double() for k, v in fus.state_dict().items()})
+        z0 = fref(sx, ref(gd, X64), fx)
+        c = 20.0 / float(torch.quantile(z0.abs().amin(1), 0.4))
+        fus.mlp[3].weight.mul_(c)
+    fref.load_state_dict({k: v.double() for k, v in fus.state_dict().items()})
+    emb_r = ref(gd, X64)
+    emb_r.retain_grad()
+    z_r = fref(sx, emb_r, fx)
+    y = (z_r.detach() > 0).double()  # every label agrees with its logit's sign
+    bce_logits_ref(z_r, y).backward()
+    gdev = sb.to_graph(group_size=gs).to(DEV)
+    emb = model(gdev, gdev.ndata["h"])
+    emb.retain_grad()
+    z = fus(sx.float().to(DEV), emb, fx.float().to(DEV))
+    mvml_gat.bce_with_logits(z, y.float().to(DEV)).backward()
+    zmin = z_r.detach().abs().amin(1)
+    ge_r, ge = emb_r.grad, emb.grad.double().cpu()
+    rmax = ge_r.abs().amax(1)
+    per_row = (ge - ge_r).abs().amax(1) / rmax.clamp_min(1e-300)
+    errs = {"frac_saturated_ge20": float((zmin >= 20).double().mean()),
+            "frac_near_zero_lt1": float((zmin < 1).double().mean()),
+            "emb_grad_row_span_log2": float(torch.log2(rmax.max() / rmax.min())),
+            "emb_grad_per_row_max": float(per_row.max()),
+            "emb_grad_per_row_saturated_max": float(per_row[zmin >= 20].max()),
+            "emb_grad_normwise": rel_err(ge, ge_r),
+            "logits": rel_err(z, z_r)}
+    pr = dict(ref.named_parameters())
+    for n, p in model.named_parameters():
+        errs["gnn." + n] = rel_err(p.grad, pr[n].grad)
+    fr = dict(fref.named_parameters())
+    for n, p in fus.named_parameters():
+        if p.grad is not None:
+            errs["fusion." + n] = rel_err(p.grad, fr[n].grad)
+    with open(os.path.join(_margins_dir(), "saturated_logits_config3.json"), "w") as f:
+        json.dump(errs, f, indent=1)
+    print(errs)
+    assert errs["frac_saturated_ge20"] > 0.5 and errs["emb_grad_row_span_log2"] > 20
+    assert errs["emb_grad_per_row_max"] < TOL
+    for k, v in errs.items():
+        if k.startswith(("gnn.", "fusion.")):
+            assert v < TOL, (k, v)

@@ -46,6 +46,27 @@ def test_rnn_module_parity_gemm_path(B, Tmax, layers, ragged, space, wide_step, 
     _rnn_parity(B, Tmax, layers, ragged, space)
 
 
+@pytest.mark.parametrize("wide_step,wide_pack", [(True, False), (False, True)])
+def test_rnn_module_parity_mixed_paths(wide_step, wide_pack, monkeypatch):
+    """The two mixed combinations at B = 700: the wide step over time-major gate projections
+    (the branch that relies on the zero padding rows of gg), and the packed live-row products
+    around the per-step GEMM + cell path."""
+    import mvml_gat.smiles as sm
+    monkeypatch.setattr(sm, "SEQ_MAX_B", 0)
+    monkeypatch.setattr(sm, "WIDE_STEP", wide_step)
+    monkeypatch.setattr(sm, "WIDE_PACK", wide_pack)
+    _rnn_parity(700, 25, 2, True, False)
+
+
+@pytest.mark.parametrize("H", [100, 36, 30])
+def test_rnn_module_parity_hidden_sizes(H, monkeypatch):
+    """Hidden sizes the wide step does not take (H % 8 != 0; 30: H % 4 != 0, so not packed
+    either) fall back to the per-step GEMM + cell path instead of raising."""
+    import mvml_gat.smiles as sm
+    monkeypatch.setattr(sm, "SEQ_MAX_B", 0)
+    _rnn_parity(300, 20, 2, True, False, H=H)
+
+
 @pytest.mark.parametrize("B,Tmax,layers,ragged,space", [(64, 60, 2, True, False), (700, 25, 2, True, False)])
 def test_rnn_module_parity_wide_step_tile256(B, Tmax, layers, ragged, space, monkeypatch):
     """The wide step launches on the 256x256 tile (option lstm_tile = 256; the planned tile at
@@ -83,15 +104,15 @@ def test_wide_step_plans_bitwise(monkeypatch):
         assert torch.equal(a, b)
 
 
-def _rnn_parity(B, Tmax, layers, ragged, space):
+def _rnn_parity(B, Tmax, layers, ragged, space, H=384):
     from mvml_gat.smiles import RNNModule
     from oracle.smiles_ref import RNNModuleRef
     torch.manual_seed(B + layers)
     vocab, batch = _batch(B, B * 7 + Tmax, Tmax, ragged, space)
     if space:
         assert any((row[:n] == 0).any() for row, n in zip(batch["smiles"], batch["seq_len"]))
-    ref = RNNModuleRef(39, 128, 384, layers, 384, 0.5).double().eval()
-    mod = RNNModule(vocab, 128, 384, layers, 384, 0.5).to(DEV).eval()
+    ref = RNNModuleRef(39, 128, H, layers, 384, 0.5).double().eval()
+    mod = RNNModule(vocab, 128, H, layers, 384, 0.5).to(DEV).eval()
     mod.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
     zr = ref(batch)
     zd = mod({"smiles": batch["smiles"].to(DEV), "seq_len": batch["seq_len"]})

@@ -61,7 +61,18 @@ def main():
         flops = 2 * M * N * K
         cols = []
         for algo in algos:
-            if algo == "torch":
+            if algo.startswith("f16x2r"):  # per-row A maxima (mvml_gemm_f16x2_rows)
+                if ak:
+                    cols.append(f"{algo}      n/a")
+                    continue
+                from mvml_gat.functional import absmax, absmax_rows, slot
+                bmx = torch.zeros(1, dtype=torch.int32, device=dev)
+                absmax(Bm, Bm.shape[0], Bm.shape[1], Bm.shape[1], bmx, 0)
+                rows = absmax_rows(A, M, K, K)
+                with option("gemm_tile", int(algo.split("-")[1]) if "-" in algo else 0):
+                    ms, t = tf(lambda: gemm(A, Bm, M, N, K, 0, bk, K, N if bk else K, C, N,
+                                            amax=(None, slot(bmx, 0)), arows=rows), flops)
+            elif algo == "torch":
                 At = A.t() if ak else A
                 Bt = Bm if bk else Bm.t()
                 ms, t = tf(lambda: torch.matmul(At, Bt, out=C), flops)
