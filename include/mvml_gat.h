@@ -273,13 +273,16 @@ int mvml_gat_attn_grad(int64_t num_nodes, int H, int F, const float* Y, int64_t 
  * attn [E, H] receives the edge_softmax output in in-CSR slot order (needed by the backward).
  * out_amax (may be NULL): *out_amax = max(*out_amax, bits of max |out|), folded into the stores
  * (the split-fp16 operand max of the next layer's / Set2Set's GEMMs; the caller zeroes it).
+ * out_row_amax (may be NULL): out_row_amax[n] = bits of max_c |out[n, c]| for every atom, written
+ * once per row (no atomics; the per-row scales of the next products, mvml_gemm_f16x2_rows).
  * node_groups is the plan mvml_build_node_groups built from the same in_rowptr (a plan of
  * another graph is undefined behaviour); num_groups = mvml_node_group_count(num_nodes).
  * ------------------------------------------------------------------------------------- */
 int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
                      const int32_t* in_rowptr, const int32_t* in_src, const float* Y, int64_t ldy,
                      int H, int F, const float* elr, const float* bias, float slope, int mode,
-                     float* out, float* attn, uint32_t* out_amax, void* stream);
+                     float* out, float* attn, uint32_t* out_amax, uint32_t* out_row_amax,
+                     void* stream);
 /* Backward of mvml_gat_agg_fwd (DGL GSpMM / GSDDMM / EdgeSoftmax backward + torch autograd of
  * residual, bias, ELU, mean).  Atomic-free: the u_mul_e-sum transpose is a gather over the
  * out-CSR; one workgroup per node group reads Z, g_out and writes dZ once (molecule groups).
@@ -291,15 +294,17 @@ int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_
  * mvml_gat_attn_grad(gelr = gY + C, ldgl = ldgy).
  * out is the forward output (mode 0 uses ELU'(x) = out + 1 for x <= 0).  gy_amax (may be NULL):
  * *gy_amax = max(*gy_amax, bits of max |gY[:, :C + 2H]|), folded into the stores (the split-fp16
- * operand max of the two GEMMs that read gY; the caller zeroes it).  workspace: [E, H]. */
+ * operand max of the two GEMMs that read gY; the caller zeroes it).  gy_row_amax (may be NULL):
+ * gy_row_amax[n] = bits of max_c |gY[n, c]|, c < C + 2H, for every atom (the per-row scales of the
+ * data-gradient product, mvml_gemm_f16x2_rows; no float atomics).  workspace: [E, H]. */
 size_t mvml_gat_agg_bwd_workspace_size(int64_t num_edges, int H);
 int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
                      const int32_t* in_rowptr, const int32_t* in_src, const int32_t* out_rowptr,
                      const int32_t* out_dst, const int32_t* out_inslot, const float* Y,
                      int64_t ldy, const float* elr, const float* attn, const float* out,
                      const float* g_out, int H, int F, float slope, int mode, float* gY,
-                     int64_t ldgy, uint32_t* gy_amax, void* workspace, size_t workspace_bytes,
-                     void* stream);
+                     int64_t ldgy, uint32_t* gy_amax, uint32_t* gy_row_amax, void* workspace,
+                     size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Set2Set (dgl 0.9.1, model.py:82-84, 92) building blocks.

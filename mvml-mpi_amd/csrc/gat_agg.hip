@@ -13,8 +13,9 @@
 //   a_e   = exp(s_e - max_v s) / sum_v exp(s - max_v s)       edge_softmax (norm_by = dst)
 //   rst_v = sum_e a_e * Z[src_e] + R[v] + bias                update_all(u_mul_e, sum), res, bias
 //   out_v = ELU(rst_v.flatten) | mean_h(rst_v) | rst_v        dgllife GATLayer agg / activation
-// Two launches: gat_logits_kernel streams Z once into the compact elr array, then the
-// aggregation kernel gathers 16-B logits per in-edge for the softmax and the Z rows for the sum.
+// el / er come from the projection GEMM (2H extra columns, elr); the edge_softmax runs inside
+// the aggregation kernels (softmax_pair: one thread per destination and head, before the column
+// sweep), so mvml_gat_agg_fwd is one launch per kernel kind and attn is written, never re-read.
 // (A single-pass variant that reduces el[u] from each gathered Z row with an online softmax was
 // measured 2x slower: its per-edge shuffle -> exp -> rescale chain is latency-bound.)
 //
@@ -178,20 +179,20 @@ gat_logits_finalize_kernel(int64_t N, int F, int W, const float* __restrict__ pa
   elr[v * 2 * H + sh] = acc;
 }
 
-// edge_softmax (dgl 0.9.1, norm_by='dst'): one thread per (destination, head) pair:
-//   s_e = LeakyReLU(el[src_e] + er[v]),  a_e = exp(s_e - max_v s) / sum_v exp(s - max_v s)
-// written to attn[E, H] in in-CSR slot order (the aggregation's and the backward's input).
+// edge_softmax of one (destination v, head h) pair inside the aggregation kernels (the same
+// arithmetic and order as the round-3 standalone softmax kernel: max over the in-edges, sum of
+// exp(s - max) in edge order, a_e = exp(s_e - max) / sum): writes attn[e, h] (the backward's
+// input) and, when s_att is given, the group-relative copy s_att[(e - e0) H + h] the aggregation
+// reads.  Logits past the register cache are recomputed in each pass (one more read of the
+// L2-resident el rows; no limit on the degree).
 template <int H>
-__global__ void __launch_bounds__(256)
-gat_softmax_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
-                   const float* __restrict__ elr, float slope, float* __restrict__ attn) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N * H) return;
-  const int64_t v = i / H;
-  const int h = (int)(i % H);
+__device__ __forceinline__ void softmax_pair(int64_t v, int h, const int32_t* __restrict__ rowptr,
+                                             const int32_t* __restrict__ in_src,
+                                             const float* __restrict__ elr, float slope,
+                                             float* __restrict__ attn, float* s_att, int e0) {
   const float er = elr[v * 2 * H + H + h];
   const int eb = rowptr[v], ee = rowptr[v + 1];
-  constexpr int DC = 6;  // logits of the first DC in-edges stay in registers
+  constexpr int DC = 6;
   float sc[DC];
   float m = -INFINITY, sum = 0.f;
 #pragma unroll
@@ -199,48 +200,29 @@ gat_softmax_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t*
     sc[t] = (eb + t < ee) ? leaky(elr[(int64_t)in_src[eb + t] * 2 * H + h] + er, slope) : -INFINITY;
     m = fmaxf(m, sc[t]);
   }
-  // hubs (in-degree > DC): the tail in batches of 8 independent index + logit loads, so a
-  // hub costs deg / 8 memory round trips per pass instead of 2 deg (same summation order)
-  auto tail8 = [&](int e, float (&t8)[8]) {
-    int sv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sv[j] = (e + j < ee) ? in_src[e + j] : -1;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      t8[j] = sv[j] >= 0 ? leaky(elr[(int64_t)sv[j] * 2 * H + h] + er, slope) : -INFINITY;
-  };
-  for (int e = eb + DC; e < ee; e += 8) {
-    float t8[8];
-    tail8(e, t8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) m = fmaxf(m, t8[j]);
-  }
+  for (int e = eb + DC; e < ee; ++e) m = fmaxf(m, leaky(elr[(int64_t)in_src[e] * 2 * H + h] + er, slope));
 #pragma unroll
   for (int t = 0; t < DC; ++t)
     if (eb + t < ee) sum += expf(sc[t] - m);
-  for (int e = eb + DC; e < ee; e += 8) {
-    float t8[8];
-    tail8(e, t8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (e + j < ee) sum += expf(t8[j] - m);
-  }
+  for (int e = eb + DC; e < ee; ++e) sum += expf(leaky(elr[(int64_t)in_src[e] * 2 * H + h] + er, slope) - m);
 #pragma unroll
   for (int t = 0; t < DC; ++t)
-    if (eb + t < ee) attn[(int64_t)(eb + t) * H + h] = expf(sc[t] - m) / sum;
-  for (int e = eb + DC; e < ee; e += 8) {
-    float t8[8];
-    tail8(e, t8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (e + j < ee) attn[(int64_t)(e + j) * H + h] = expf(t8[j] - m) / sum;
+    if (eb + t < ee) {
+      const float a = expf(sc[t] - m) / sum;
+      attn[(int64_t)(eb + t) * H + h] = a;
+      if (s_att) s_att[(eb + t - e0) * H + h] = a;
+    }
+  for (int e = eb + DC; e < ee; ++e) {
+    const float a = expf(leaky(elr[(int64_t)in_src[e] * 2 * H + h] + er, slope) - m) / sum;
+    attn[(int64_t)e * H + h] = a;
+    if (s_att) s_att[(e - e0) * H + h] = a;
   }
 }
 
 // Aggregation over NODE GROUPS.  A node group is a contiguous range of whole molecules of about
 // kNodeGroupAtoms atoms (mvml_build_node_groups); edges never leave a molecule, so every in-edge
 // of a group's atoms has its source inside the group, and one workgroup per group can read each
-// projection row from HBM once.  The attention comes from gat_softmax_kernel.  The projection
+// projection row from HBM once.  The attention comes from softmax_pair.  The projection
 // columns are swept CW at a time; CW/4 lanes own one destination atom (16-B column slices).
 // Flatten modes walk the chunks head-major; the mean mode walks them f-chunk-major, head-minor,
 // summing the heads in registers (+ bias per head, / H, + head-mean residual).
@@ -377,7 +359,7 @@ __device__ __forceinline__ float fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], 
                                                const uint16_t* s_srcs = nullptr,
                                                const uint32_t* s_seg = nullptr,
                                                const int* s_rs = nullptr, float4* s_part = nullptr,
-                                               int nseg = 0) {
+                                               int nseg = 0, uint32_t* __restrict__ out_rows = nullptr) {
   constexpr int LPD = CW / 4;                        // lanes per destination atom
   constexpr int DPP = NT / LPD;                      // destinations per pass
   constexpr int RING = NPA >= 3 ? 1 : MVML_FWD_RING;  // 3-4 pass groups: registers
@@ -397,6 +379,7 @@ __device__ __forceinline__ float fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], 
   // out-of-range offset costs a page walk per access)
   const uint32_t noY = (uint32_t)nr * rowb;
   float omx = 0.f;  // |max| of this thread's output stores (live rows)
+  float rmx[NPA];   // ... per destination (out_rows: each row's |max|, the next GEMM's row scale)
   bool live[NPA];
 #pragma unroll
   for (int p = 0; p < NPA; ++p) {
@@ -409,6 +392,7 @@ __device__ __forceinline__ float fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], 
     }
     ab[p] = eb * H;
     ad[p] = deg;
+    rmx[p] = 0.f;
 #pragma unroll
     for (int i = 0; i < kEC; ++i) {
       so[p][i] = ((i < deg) ? in_src[e0 + eb + i] - a0 : (live[p] ? d : 0)) * LPD + q;
@@ -525,13 +509,13 @@ __device__ __forceinline__ float fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], 
           const float4 o = make_float4(tot[p].x / invh + rres[p].x, tot[p].y / invh + rres[p].y,
                                        tot[p].z / invh + rres[p].z, tot[p].w / invh + rres[p].w);
           buf_st4(rO, ob[p] + 4u * (uint32_t)((k / H) * CW + 4 * q), o);
-          if (ds + DPP * p < nr) omx = amax4(omx, o);
+          rmx[p] = amax4(rmx[p], o);
         }
       } else {
         float4 o = add4(add4(acc[p], rres[p]), b4);
         if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
         buf_st4(rO, ob[p] + 4u * (uint32_t)col, o);  // rows past the group: dropped
-        if (ds + DPP * p < nr) omx = amax4(omx, o);
+        rmx[p] = amax4(rmx[p], o);
       }
     };
     if constexpr (!BIG) {
@@ -559,6 +543,15 @@ __device__ __forceinline__ float fwd_lds_chunks(float4 (*zbuf)[WIN * (CW / 4)], 
     for (int j = 0; j < NPA; ++j)
       if constexpr (!BIG) rres[j] = rnx[j];
   }
+  // a row's |max| over its LPD lanes (consecutive lanes of one wave); one writer per row
+#pragma unroll
+  for (int p = 0; p < NPA; ++p) {
+    float m = live[p] ? rmx[p] : 0.f;
+    omx = fmaxf(omx, m);
+#pragma unroll
+    for (int o = LPD / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (out_rows && live[p] && q == 0) out_rows[a0 + ds + DPP * p] = __float_as_uint(m);
+  }
   return omx;
 }
 
@@ -572,8 +565,9 @@ template <int H, int CW, int MODE, int NT, int WIN = kWinL, int ECAP = kECap, bo
 __global__ void __launch_bounds__(NT, MVML_LDS_WAVES)
 gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                        const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
-                       int F, const float* __restrict__ bias, const float* __restrict__ attn,
-                       float* __restrict__ out, uint32_t* __restrict__ out_amax) {
+                       int F, const float* __restrict__ bias, const float* __restrict__ elr,
+                       float slope, float* __restrict__ attn, float* __restrict__ out,
+                       uint32_t* __restrict__ out_amax, uint32_t* __restrict__ out_rows) {
   constexpr int LPD = CW / 4;
   constexpr int DPP = NT / LPD;
   constexpr int NPM = WIN / DPP;  // passes over a full window
@@ -600,7 +594,10 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   const int ocols = MODE == 1 ? F : H * F;
   const int e0 = rowptr[a0];
   const int ne = rowptr[a1] - e0;
-  for (int i = tid; i < ne * H; i += NT) s_att[i] = attn[(int64_t)e0 * H + i];
+  // the group's edge_softmax, fused: one thread per (destination, head) pair into s_att (and
+  // attn for the backward); fwd_lds_chunks' first barrier publishes it
+  for (int pr = tid; pr < nr * H; pr += NT)
+    softmax_pair<H>(a0 + pr / H, pr % H, rowptr, in_src, elr, slope, attn, s_att, e0);
   if (tid < H) s_att[ECAP * H + tid] = 0.f;
   int nseg = 0;
   if constexpr (BIG) {
@@ -617,13 +614,13 @@ gat_agg_fwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   const __amdgpu_buffer_rsrc_t rY = make_rsrc(Y + (int64_t)a0 * ldy, (uint32_t)nr * rowb);
   const __amdgpu_buffer_rsrc_t rO = make_rsrc(out + (int64_t)a0 * ocols, (uint32_t)(nr * ocols) * 4u);
   if (nr <= DPP)
-    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, 1, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg));
+    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, 1, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg, out_rows));
   else if (NPM == 2 || nr <= 2 * DPP)
-    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, 2, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg));
+    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, 2, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg, out_rows));
   else if (nr <= 3 * DPP)
-    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, (NPM > 2 ? 3 : 2), WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg));
+    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, (NPM > 2 ? 3 : 2), WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg, out_rows));
   else
-    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, NPM, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg));
+    omx = fmaxf(omx, fwd_lds_chunks<H, CW, MODE, NT, NPM, WIN, ECAP, BIG>(zbuf, s_att, rowptr, in_src, rY, rowb, rO, a0, nr, e0, F, bias, s_srcs, s_seg, s_rs, s_part, nseg, out_rows));
   }
   if (out_amax) block_amax_commit<NT>(omx, out_amax);
 }
@@ -632,8 +629,9 @@ template <int H, int CW, int MODE>
 __global__ void __launch_bounds__(kAggThreads, 4)  // 2 workgroups (16 waves) per CU
 gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_t* __restrict__ rowptr,
                    const int32_t* __restrict__ in_src, const float* __restrict__ Y, int64_t ldy,
-                   int F, const float* __restrict__ bias, const float* __restrict__ attn,
-                   float* __restrict__ out, int skip_big, uint32_t* __restrict__ out_amax) {
+                   int F, const float* __restrict__ bias, const float* __restrict__ elr, float slope,
+                   float* __restrict__ attn, float* __restrict__ out, int skip_big,
+                   uint32_t* __restrict__ out_amax, uint32_t* __restrict__ out_rows) {
   constexpr int LPD = CW / 4;                        // lanes per destination atom
   constexpr int DPP = kAggThreads / LPD;             // destinations per pass
   constexpr int NP = (kWin + DPP - 1) / DPP;         // passes over a full window
@@ -660,7 +658,13 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
   // aggregates one hub at a time over ALL its columns at once, so a hub costs deg / 8 memory
   // round trips instead of (column chunks) x deg / 8 on 16 lanes.  Same summation order.
   __shared__ float4 s_hub[kHubCols];
+  __shared__ float s_red[kAggThreads / 64];
   const bool hubpass = HF / 4 <= kHubCols;
+  // the group's edge_softmax, fused (global attn: the sweep below gathers it per edge; the
+  // barrier makes this workgroup's stores visible to it)
+  for (int pr = tid; pr < (a1 - a0) * H; pr += kAggThreads)
+    softmax_pair<H>(a0 + pr / H, pr % H, rowptr, in_src, elr, slope, attn, nullptr, 0);
+  __syncthreads();
 
   for (int w0 = a0; w0 < a1; w0 += kWin) {
     const int nr = min(kWin, a1 - w0);
@@ -694,6 +698,9 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
     auto att = [&](int e, int h) -> float { return attw[e * H + h]; };
 
     float4 tot[NP], rm[NP];
+    float rmx[NP];  // per destination |max| (out_rows)
+#pragma unroll
+    for (int p = 0; p < NP; ++p) rmx[p] = 0.f;
     for (int k = 0; k < nch; ++k) {
       const int h = MODE == 1 ? k % H : k / nfc;
       const int fc = MODE == 1 ? k / H : k % nfc;
@@ -760,22 +767,32 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
               const float4 o = make_float4(tot[p].x / invh + rm[p].x, tot[p].y / invh + rm[p].y,
                                            tot[p].z / invh + rm[p].z, tot[p].w / invh + rm[p].w);
               buf_st4(rO, 4u * (uint32_t)(d * F + fc * CW + 4 * q), o);
-              omx = amax4(omx, o);
+              rmx[p] = amax4(rmx[p], o);
             }
           } else {
             float4 o = add4(add4(acc[p], res[p]), ld4(bias + col));
             if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
             buf_st4(rO, 4u * (uint32_t)(d * HF + col), o);
-            omx = amax4(omx, o);
+            rmx[p] = amax4(rmx[p], o);
           }
         }
       }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {  // rows of the sweep: |max| over their LPD lanes, one writer
+      const int d = ds + DPP * p;
+      float m = rmx[p];
+      omx = fmaxf(omx, m);
+#pragma unroll
+      for (int o = LPD / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      if (out_rows && d < nr && !hub[p] && q == 0) out_rows[w0 + d] = __float_as_uint(m);
     }
     if (!hubpass) continue;
     for (int d = 0; d < nr; ++d) {  // block-uniform walk over the window's hubs
       const int hb = rowptr[w0 + d] - e0, hdeg = rowptr[w0 + d + 1] - e0 - hb;
       if (hdeg <= kHubDeg) continue;
       const uint32_t vb = (uint32_t)(w0 + d - a0) * rowb;
+      float hmx = 0.f;  // this thread's part of the hub row's |max|
       for (int c4 = tid; c4 < HF / 4; c4 += kAggThreads) {
         const int col = 4 * c4, h = col / F;
         const uint32_t colb = 4u * (uint32_t)col;
@@ -804,7 +821,7 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
           float4 o = add4(add4(acc, res), ld4(bias + col));
           if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
           buf_st4(rO, 4u * (uint32_t)(d * HF + col), o);
-          omx = amax4(omx, o);
+          hmx = amax4(hmx, o);
         }
       }
       if (MODE == 1) {  // head mean, heads summed in order as in the chunk sweep
@@ -817,7 +834,20 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
           const float4 o = make_float4(tot.x / invh + rmv.x, tot.y / invh + rmv.y,
                                        tot.z / invh + rmv.z, tot.w / invh + rmv.w);
           buf_st4(rO, 4u * (uint32_t)(d * F + 4 * f4), o);
-          omx = amax4(omx, o);
+          hmx = amax4(hmx, o);
+        }
+        __syncthreads();
+      }
+      omx = fmaxf(omx, hmx);
+      if (out_rows) {  // the hub row's |max| over the block (block-uniform branch)
+        hmx = wave_max(hmx);
+        if ((tid & 63) == 0) s_red[tid >> 6] = hmx;
+        __syncthreads();
+        if (tid == 0) {
+          float m = s_red[0];
+#pragma unroll
+          for (int w = 1; w < kAggThreads / 64; ++w) m = fmaxf(m, s_red[w]);
+          out_rows[w0 + d] = __float_as_uint(m);
         }
         __syncthreads();
       }
@@ -890,7 +920,7 @@ __device__ __forceinline__ float bwd_lds_chunks(
     const int32_t* __restrict__ g_oslot = nullptr, int e0 = 0, int a0 = 0,
     const uint32_t* s_segI = nullptr, int nsegI = 0, const uint32_t* s_segO = nullptr,
     int nsegO = 0, const int* s_rs = nullptr, float4* s_part = nullptr,
-    const uint32_t* s_oxe = nullptr, const uint16_t* s_oxb = nullptr) {
+    const uint32_t* s_oxe = nullptr, const uint16_t* s_oxb = nullptr, float* s_rmx = nullptr) {
   static_assert(kEC == 5, "in-edge writer lanes assume 5 cached in-edges");
   constexpr int LPD = CW / 4, DPP = NT / LPD;
   auto odst = [&](int o) -> int { if constexpr (BIG) return g_odst[e0 + o] - a0; else return s_odst[o]; };
@@ -908,6 +938,7 @@ __device__ __forceinline__ float bwd_lds_chunks(
   const uint32_t noY = 4u * (uint32_t)(nr * ldyi), noGo = 4u * (uint32_t)(nr * ocols);
   const uint32_t noO = 4u * (uint32_t)(nr * HF), noG = 4u * (uint32_t)(nr * ldgi);
   float gmx = 0.f;  // |max| of this thread's stores into gY (live rows, real chunks)
+  float rmx[NPA];   // ... per row (s_rmx: the rows' |max| over dZ and dR, for per-row scales)
   bool live[NPA];
   // node role: the g_rst row slot (low 16 bits) and attention slot (high 16 bits) of the
   // first kEC out-edges of this octet's source atoms in registers (a missing edge reads the
@@ -920,6 +951,7 @@ __device__ __forceinline__ float bwd_lds_chunks(
   for (int p = 0; p < NPA; ++p) {
     const int r = ds + DPP * p;
     live[p] = r < nr;
+    rmx[p] = 0.f;
     ob[p] = live[p] ? s_orp[r] : 0;
     oend[p] = live[p] ? s_orp[r + 1] : 0;
 #pragma unroll
@@ -999,11 +1031,11 @@ __device__ __forceinline__ float bwd_lds_chunks(
       if (MODE != 1) {
         gs[r * LPD + (q ^ bwd_sw<LPD>(r))] = g;
         buf_st4(rG, ok ? grow(p) + 4u * (uint32_t)(HF + col_of(k)) : noG, g);
-        if (ok && r < nr) gmx = amax4(gmx, g);
+        if (ok && r < nr) rmx[p] = amax4(rmx[p], g);
       } else if (h == 0) {  // uniform branch: an all-out-of-range store is not free
         gs[r * LPD + (q ^ bwd_sw<LPD>(r))] = g;
         buf_st4(rG, ok ? grow(p) + 4u * (uint32_t)(HF + fc * CW + 4 * q) : noG, R.g[p]);
-        if (ok && r < nr) gmx = amax4(gmx, R.g[p]);
+        if (ok && r < nr) rmx[p] = amax4(rmx[p], R.g[p]);
       }
     }
   };
@@ -1119,9 +1151,18 @@ __device__ __forceinline__ float bwd_lds_chunks(
 #pragma unroll
     for (int p = 0; p < NPA; ++p) {
       buf_st4(rG, grow(p) + 4u * (uint32_t)col_of(k), acc[p]);  // rows past the group: dropped
-      if (ds + DPP * p < nr) gmx = amax4(gmx, acc[p]);
+      if (ds + DPP * p < nr) rmx[p] = amax4(rmx[p], acc[p]);
     }
     __syncthreads();
+  }
+  // the rows' |max| over their LPD lanes (one writer per row; the caller adds d el / d er)
+#pragma unroll
+  for (int p = 0; p < NPA; ++p) {
+    float m = rmx[p];
+    gmx = fmaxf(gmx, m);
+#pragma unroll
+    for (int o = LPD / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (s_rmx && live[p] && q == 0) s_rmx[ds + DPP * p] = m;
   }
   return gmx;
 }
@@ -1141,7 +1182,8 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
                        const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ elr,
                        const float* __restrict__ attn, const float* __restrict__ out,
                        const float* __restrict__ g_out, float slope, float* __restrict__ gY,
-                       int64_t ldgy, int C, uint32_t* __restrict__ gy_amax) {
+                       int64_t ldgy, int C, uint32_t* __restrict__ gy_amax,
+                       uint32_t* __restrict__ gy_rows) {
   constexpr int LPD = CW / 4;
   constexpr int DPP = NT / LPD;
   constexpr int NPM = WIN / DPP;  // passes over a full window
@@ -1195,6 +1237,9 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   float* s_elr_b = reinterpret_cast<float*>(zs);
   int* s_oslot_b = reinterpret_cast<int*>(gs);
   static_assert(!BIG || (WIN * 2 * H <= WIN * LPD * 4 && ECAP <= WIN * LPD * 4), "row buffers hold elr / slots");
+  // gy_rows: the rows' |max| in the free row buffer after the sweep, past BIG's logits
+  static_assert(WIN * 2 * H + WIN <= WIN * LPD * 4, "row buffer holds the logits and the row maxima");
+  float* s_rmx = gy_rows ? reinterpret_cast<float*>(zs) + WIN * 2 * H : nullptr;
   auto elr_at = [&](int r, int c) -> float {  // elr of group row r, column c (el | er)
     if constexpr (BIG) return s_elr_b[r * 2 * H + c]; else return s_elr[r * 2 * H + c];
   };
@@ -1232,7 +1277,7 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
   gmx = fmaxf(gmx, bwd_lds_chunks<H, MODE, NPA, CW, NT, WIN, ECAP, BIG>(zs, gs, s_att, s_odst, s_oslot, s_orp, s_rp,  \
                                                        s_src, s_ga, rY, ldyi, rGo, rO, rG, ldgi, nr, F, \
                                                        out_dst, out_inslot, e0, a0, s_segI, nsegI, \
-                                                       s_segO, nsegO, s_rs, s_part, s_oxe, s_oxb))
+                                                       s_segO, nsegO, s_rs, s_part, s_oxe, s_oxb, s_rmx))
   if (nr <= DPP) MVML_BWD_CHUNKS(1);
   else if (NPM == 2 || nr <= 2 * DPP) MVML_BWD_CHUNKS(2);
   else if (nr <= 3 * DPP) MVML_BWD_CHUNKS((NPM > 2 ? 3 : 2));
@@ -1260,6 +1305,7 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
     }
     gY[(int64_t)(a0 + d) * ldgy + C + H + h] = der;
     gmx = fmaxf(gmx, fabsf(der));
+    if (s_rmx) atomicMax(reinterpret_cast<uint32_t*>(s_rmx) + d, __float_as_uint(fabsf(der)));
   }
   __syncthreads();
   for (int i = tid; i < nr * H; i += NT) {  // d el: sums over out-edges
@@ -1272,6 +1318,11 @@ gat_agg_bwd_lds_kernel(const int32_t* __restrict__ plan, int64_t G, const int32_
     }
     gY[(int64_t)(a0 + u) * ldgy + C + h] = del;
     gmx = fmaxf(gmx, fabsf(del));
+    if (s_rmx) atomicMax(reinterpret_cast<uint32_t*>(s_rmx) + u, __float_as_uint(fabsf(del)));
+  }
+  if (s_rmx) {  // (LDS max of non-negative float bits: order-independent)
+    __syncthreads();
+    for (int r = tid; r < nr; r += NT) gy_rows[a0 + r] = __float_as_uint(s_rmx[r]);
   }
   }
   if (gy_amax) block_amax_commit<NT>(gmx, gy_amax);
@@ -1287,7 +1338,7 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
                        const float* __restrict__ g_out, int F, float slope, int mode,
                        float* __restrict__ gpre, float* __restrict__ gY, int64_t ldgy,
                        float* __restrict__ gelr, int64_t ldgl, int skip_big,
-                       uint32_t* __restrict__ gy_amax) {
+                       uint32_t* __restrict__ gy_amax, uint32_t* __restrict__ gy_rows) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float gmx = 0.f;  // |max| of this thread's gY stores (block-uniform early returns only)
   // G > 0: one block per backward fallback group of the plan; G == 0: one wave per atom over
@@ -1325,18 +1376,19 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
   // dR[v]: per-head g_rst (flatten modes) or g_out (head-mean residual).  Written here so the
   // source pass can gather finished g_rst rows from gY instead of re-deriving them per edge.
   float* gyv = gY + v * ldgy;
+  float rmx = 0.f;  // this row's |max| (dR, d er) for gy_rows
 #pragma unroll
   for (int c = 0; c < VPL; ++c) {
     const int col = 4 * (lane + 64 * c);
     if (mode != 1) {
       if (okc[c]) {
         st4(gyv + HF + col, gr[c]);
-        gmx = amax4(gmx, gr[c]);
+        rmx = amax4(rmx, gr[c]);
       }
     } else if (col < F) {
       const float4 go = ld4(g_out + v * F + col);
       st4(gyv + HF + col, go);
-      gmx = amax4(gmx, go);
+      rmx = amax4(rmx, go);
     }
   }
   float er[H];
@@ -1407,7 +1459,12 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
   }
   store_heads<H>(gelr + v * ldgl + H, ger, lane);
 #pragma unroll
-  for (int h = 0; h < H; ++h) gmx = fmaxf(gmx, fabsf(ger[h]));
+  for (int h = 0; h < H; ++h) rmx = fmaxf(rmx, fabsf(ger[h]));
+  gmx = fmaxf(gmx, rmx);
+  if (gy_rows) {  // the first writer of the row's |max| (the source pass adds dZ, d el)
+    rmx = wave_max(rmx);
+    if (lane == 0) gy_rows[v] = __float_as_uint(rmx);
+  }
   }
   if (gy_amax) block_amax_commit<kWavesPerBlock * 64>(gmx, gy_amax);
 }
@@ -1421,7 +1478,8 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
                        const float* __restrict__ attn, const float* __restrict__ gpre,
                        const float* __restrict__ out, const float* __restrict__ g_out, int F,
                        int mode, float* __restrict__ gY, int64_t ldgy, float* __restrict__ gelr,
-                       int64_t ldgl, int skip_big, uint32_t* __restrict__ gy_amax) {
+                       int64_t ldgl, int skip_big, uint32_t* __restrict__ gy_amax,
+                       uint32_t* __restrict__ gy_rows) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float gmx = 0.f;  // |max| of this thread's gY stores (block-uniform early returns only)
   // G > 0: one block per backward fallback group of the plan; G == 0: one wave per atom over
@@ -1494,15 +1552,21 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
   // dZ through the aggregation only; the el / er paths (d el x attn_l + d er x attn_r) reach
   // the projection's gradients through the [d el | d er] columns (mvml_gat_agg_bwd contract)
   float* gyu = gY + u * ldgy;
+  float rmx = 0.f;
 #pragma unroll
   for (int c = 0; c < VPL; ++c)
     if (okc[c]) {
       st4(gyu + 4 * (lane + 64 * c), gz[c]);
-      gmx = amax4(gmx, gz[c]);
+      rmx = amax4(rmx, gz[c]);
     }
   store_heads<H>(gelr + u * ldgl, gel, lane);
 #pragma unroll
-  for (int h = 0; h < H; ++h) gmx = fmaxf(gmx, fabsf(gel[h]));
+  for (int h = 0; h < H; ++h) rmx = fmaxf(rmx, fabsf(gel[h]));
+  gmx = fmaxf(gmx, rmx);
+  if (gy_rows) {  // the destination pass wrote this row's first part (stream order)
+    rmx = wave_max(rmx);
+    if (lane == 0) gy_rows[u] = max(gy_rows[u], __float_as_uint(rmx));
+  }
   }
   if (gy_amax) block_amax_commit<kWavesPerBlock * 64>(gmx, gy_amax);
 }
@@ -1510,24 +1574,22 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
 template <int H>
 int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, const int32_t* src,
                const float* Y, int64_t ldy, int F, const float* bias, float slope, int mode,
-               float* out, float* attn, const float* elr, uint32_t* out_amax, hipStream_t st) {
-  int rc;
-  gat_softmax_kernel<H><<<(unsigned)ceil_div(N * H, 256), 256, 0, st>>>(N, rp, src, elr, slope, attn);
-  rc = check_launch("gat_softmax_kernel");
-  if (rc) return rc;
+               float* out, float* attn, const float* elr, uint32_t* out_amax, uint32_t* out_rows,
+               hipStream_t st) {
   if (G == 0) return MVML_OK;
   const bool big = use_big_window(H, F);
+  // the edge_softmax runs inside each kernel for its own groups (no separate softmax launch)
 #define MVML_AGG_FWD_M(CW, M)                                                                       \
   do {                                                                                              \
     gat_agg_fwd_lds_kernel<H, CW, M, CW * 16><<<(unsigned)G, CW * 16, 0, st>>>(groups, G, rp, src, Y, ldy, F, \
-                                                                         bias, attn, out, out_amax); \
+                                                                         bias, elr, slope, attn, out, out_amax, out_rows); \
     gat_agg_fwd_gather_kernel<H, CW, M><<<(unsigned)G, kAggThreads, 0, st>>>(groups, G, rp, src, Y, ldy, \
-                                                                            F, bias, attn, out, big, out_amax); \
+                                                                            F, bias, elr, slope, attn, out, big, out_amax, out_rows); \
     if constexpr (H <= 4)                                                                           \
       if (big)                                                                                      \
         gat_agg_fwd_lds_kernel<H, 16, M, kBigThreads, kPlanBigAtoms, kPlanBigEdgeCap, true>          \
             <<<(unsigned)std::min<int64_t>(G, kBigBlocks), kBigThreads, 0, st>>>(                    \
-                groups, G, rp, src, Y, ldy, F, bias, attn, out, out_amax);                          \
+                groups, G, rp, src, Y, ldy, F, bias, elr, slope, attn, out, out_amax, out_rows);    \
   } while (0)
 #define MVML_AGG_FWD(CW)                                  \
   do {                                                    \
@@ -1550,7 +1612,7 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
                const int32_t* orp, const int32_t* odst, const int32_t* oslot, const float* Y,
                int64_t ldy, const float* elr, const float* attn, const float* out,
                const float* g_out, int F, float slope, int mode, float* gpre, float* gY,
-               int64_t ldgy, int C, uint32_t* gy_amax, hipStream_t st) {
+               int64_t ldgy, int C, uint32_t* gy_amax, uint32_t* gy_rows, hipStream_t st) {
   if (option(MVML_OPT_BWD_ATOMWISE)) G = 0;  // tests: the per-atom pair over every atom
   if (F % 32 == 0 && G > 0) {  // molecule groups: one pass over Z / g_out / dZ per group
 #ifndef MVML_BWD_CW64
@@ -1561,7 +1623,7 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
 #define MVML_BWD_LDS(M, CW)                                                                       \
     gat_agg_bwd_lds_kernel<H, M, CW><<<(unsigned)G, 16 * CW, 0, st>>>(groups, G, rp, src, orp, odst, \
                                                                       oslot, Y, ldy, F, elr, attn, \
-                                                                      out, g_out, slope, gY, ldgy, C, gy_amax)
+                                                                      out, g_out, slope, gY, ldgy, C, gy_amax, gy_rows)
     if (MVML_BWD_CW64 && F % 64 == 0) {
       if (mode == 0) MVML_BWD_LDS(0, 64);
       else if (mode == 1) MVML_BWD_LDS(1, 64);
@@ -1583,7 +1645,7 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
 #define MVML_BWD_BIG(M)                                                                             \
       gat_agg_bwd_lds_kernel<H, M, 16, kBigThreads, kPlanBigAtoms, kPlanBigEdgeCap, true>            \
           <<<(unsigned)std::min<int64_t>(G, kBigBlocks), kBigThreads, 0, st>>>(                      \
-              groups, G, rp, src, orp, odst, oslot, Y, ldy, F, elr, attn, out, g_out, slope, gY, ldgy, C, gy_amax)
+              groups, G, rp, src, orp, odst, oslot, Y, ldy, F, elr, attn, out, g_out, slope, gY, ldgy, C, gy_amax, gy_rows)
       if (mode == 0) MVML_BWD_BIG(0);
       else if (mode == 1) MVML_BWD_BIG(1);
       else MVML_BWD_BIG(2);
@@ -1595,12 +1657,12 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
   const unsigned blocks = G > 0 ? (unsigned)G : (unsigned)ceil_div(N, kWavesPerBlock);
   gat_agg_bwd_dst_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
       N, groups, G, rp, src, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, gY + C, ldgy, big,
-      gy_amax);
+      gy_amax, gy_rows);
   int rc = check_launch("gat_agg_bwd_dst_kernel");
   if (rc) return rc;
   gat_agg_bwd_src_kernel<H, VPL><<<blocks, kWavesPerBlock * 64, 0, st>>>(
       N, groups, G, rp, orp, odst, oslot, attn, gpre, out, g_out, F, mode, gY, ldgy, gY + C, ldgy, big,
-      gy_amax);
+      gy_amax, gy_rows);
   return check_launch("gat_agg_bwd_src_kernel");
 }
 
@@ -1798,7 +1860,7 @@ extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, i
                                 const int32_t* in_rowptr, const int32_t* in_src, const float* Y,
                                 int64_t ldy, int H, int F, const float* elr, const float* bias,
                                 float slope, int mode, float* out, float* attn, uint32_t* out_amax,
-                                void* stream) {
+                                uint32_t* out_row_amax, void* stream) {
   clear_error();
   int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_fwd");
   if (rc) return rc;
@@ -1811,10 +1873,10 @@ extern "C" int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, i
   if (num_nodes == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
   switch (H) {
-    case 1: return launch_fwd<1>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, st);
-    case 2: return launch_fwd<2>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, st);
-    case 4: return launch_fwd<4>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, st);
-    case 8: return launch_fwd<8>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, st);
+    case 1: return launch_fwd<1>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, out_row_amax, st);
+    case 2: return launch_fwd<2>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, out_row_amax, st);
+    case 4: return launch_fwd<4>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, out_row_amax, st);
+    case 8: return launch_fwd<8>(num_nodes, node_groups, num_groups, in_rowptr, in_src, Y, ldy, F, bias, slope, mode, out, attn, elr, out_amax, out_row_amax, st);
   }
   set_error("gat_agg_fwd: unsupported shape");
   return MVML_ERR_INVALID;
@@ -1830,7 +1892,7 @@ extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, i
                                 const int32_t* out_inslot, const float* Y, int64_t ldy,
                                 const float* elr, const float* attn, const float* out,
                                 const float* g_out, int H, int F, float slope, int mode, float* gY,
-                                int64_t ldgy, uint32_t* gy_amax, void* workspace,
+                                int64_t ldgy, uint32_t* gy_amax, uint32_t* gy_row_amax, void* workspace,
                                 size_t workspace_bytes, void* stream) {
   clear_error();
   int rc = check_shapes(H, F, mode, ldy, Y, "gat_agg_bwd");
@@ -1851,10 +1913,10 @@ extern "C" int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, i
   float* gpre = static_cast<float*>(workspace);
   const int vpl = (int)ceil_div(H * F, 256);
   switch (H) {
-    case 1: { MVML_VPL_CASES(launch_bwd, 1, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, st) break; }
-    case 2: { MVML_VPL_CASES(launch_bwd, 2, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, st) break; }
-    case 4: { MVML_VPL_CASES(launch_bwd, 4, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, st) break; }
-    case 8: { MVML_VPL_CASES(launch_bwd, 8, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, st) break; }
+    case 1: { MVML_VPL_CASES(launch_bwd, 1, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, gy_row_amax, st) break; }
+    case 2: { MVML_VPL_CASES(launch_bwd, 2, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, gy_row_amax, st) break; }
+    case 4: { MVML_VPL_CASES(launch_bwd, 4, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, gy_row_amax, st) break; }
+    case 8: { MVML_VPL_CASES(launch_bwd, 8, num_nodes, node_groups, num_groups, in_rowptr, in_src, out_rowptr, out_dst, out_inslot, Y, ldy, elr, attn, out, g_out, F, slope, mode, gpre, gY, ldgy, C, gy_amax, gy_row_amax, st) break; }
   }
   set_error("gat_agg_bwd: unsupported shape");
   return MVML_ERR_INVALID;

@@ -1034,6 +1034,13 @@ struct XOp {
   __device__ static __forceinline__ int64_t kstep(int64_t ld) { return KMAJ ? XBK * ld : XBK; }
 
 
+  __device__ static __forceinline__ void split_store(uint8_t* op, int tid, const float4 (&v)[NI],
+                                                     float s = 1.f) {
+    float sv[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) sv[i] = s;
+    split_store(op, tid, v, sv);
+  }
   // s[i]: the scale of piece i (split-fp16; per-row A maxima give the pieces' rows their own)
   __device__ static __forceinline__ void split_store(uint8_t* op, int tid, const float4 (&v)[NI],
                                                      const float (&s)[NI]) {
@@ -1305,7 +1312,11 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
 // (mvml_split_f16x2, amax.b_plane elements apart) instead of fp32 values: a B piece is loaded
 // as two 8-B plane reads and stored to LDS unsplit — the weights are split once per step
 // instead of once per tile.
-template <bool AK, bool BKM, int EPI_LOGW = -1, bool FAST = true, int NP = 3, bool BPS = false>
+// ROWS (split-fp16, K-contiguous A): per-row A maxima (amax.a_rows), a scale per A row; a
+// separate instantiation so that the operand-wide kernels keep their register allocation (one
+// spill reload inside the main loop costs a vmcnt drain per stage).
+template <bool AK, bool BKM, int EPI_LOGW = -1, bool FAST = true, int NP = 3, bool BPS = false,
+          bool ROWS = false>
 __global__ void __launch_bounds__(kXThreads, MVML_X3W_WAVES)  // one workgroup per CU
 gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
@@ -1344,13 +1355,14 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   };
   // NP = 2: operand scales from the |max| bits of A and B (per-row A maxima: amax.a_rows, a
   // shift per A row of the tile in rsh — host: K-contiguous A)
+  static_assert(!ROWS || (NP == 2 && !AK), "per-row A maxima: split-fp16, K-contiguous A");
   int ka = 0, kb = 0;
   if constexpr (NP == 2) {
-    if (!amax.a_rows) ka = amax_shift(*amax.a);
+    if constexpr (!ROWS) ka = amax_shift(*amax.a);
     kb = amax_shift(*amax.b);
   }
   const float s_a = pow2f(ka), s_b = pow2f(kb);
-  __shared__ int rsh[NP == 2 ? XBM : 1];
+  __shared__ int rsh[ROWS ? XBM : 1];
   // KS 16-deep sub-stages per barrier (split-fp16: 2, so a stage carries as many MFMAs as the
   // split-bf16 one); a sub-stage's LDS image is exactly the KS = 1 stage layout
   constexpr int KS = (NP == 2) ? MVML_H2_KS : 1;
@@ -1377,19 +1389,15 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   const int64_t kend = min(K, kbeg + k_split);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
-  // the scales of this thread's staged A pieces (rows (tid >> 2) + 128 i when K-contiguous)
-  float sa_i[OA::NI], sb_i[OB::NI];
-#pragma unroll
-  for (int i = 0; i < OB::NI; ++i) sb_i[i] = s_b;
+  // ROWS: the scales of this thread's staged A pieces (rows (tid >> 2) + 128 i)
+  float sa_i[OA::NI];
 #pragma unroll
   for (int i = 0; i < OA::NI; ++i) sa_i[i] = s_a;
-  if constexpr (NP == 2 && !AK) {
-    if (amax.a_rows) {
+  if constexpr (ROWS) {
 #pragma unroll
-      for (int i = 0; i < OA::NI; ++i) sa_i[i] = pow2f(row_shift(amax, m0 + (tid >> 2) + OA::RS * i, M));
-      // every row's shift for the epilogue (read after the K loop's barriers)
-      if (tid < XBM) rsh[tid] = row_shift(amax, m0 + tid, M);
-    }
+    for (int i = 0; i < OA::NI; ++i) sa_i[i] = pow2f(row_shift(amax, m0 + (tid >> 2) + OA::RS * i, M));
+    // every row's shift for the epilogue (read after the K loop's barriers)
+    if (tid < XBM) rsh[tid] = row_shift(amax, m0 + tid, M);
   }
 
   f32x16 acc[4][2];
@@ -1468,11 +1476,14 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       uint8_t* op = lds + buf * kStage + s * kSub;
-      OA::split_store(op, tid, va[s], sa_i);
+      if constexpr (ROWS)
+        OA::split_store(op, tid, va[s], sa_i);
+      else
+        OA::split_store(op, tid, va[s], s_a);
       if constexpr (BPS)
         OB::store_planes(op + OA::kBytes, tid, vb[s]);
       else
-        OB::split_store(op + OA::kBytes, tid, vb[s], sb_i);
+        OB::split_store(op + OA::kBytes, tid, vb[s], s_b);
     }
   };
 #ifndef MVML_X3W_PRIO
@@ -1630,7 +1641,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     };
     auto stg = [&](auto SET, int buf) {
       OA::split_store(lds + buf * kStage, tid, ra[decltype(SET)::value], sa_i);
-      OB::split_store(lds + buf * kStage + OA::kBytes, tid, rb[decltype(SET)::value], sb_i);
+      OB::split_store(lds + buf * kStage + OA::kBytes, tid, rb[decltype(SET)::value], s_b);
     };
     auto body2 = [&](int64_t t, auto SET, auto STAGE, auto LOAD) {
       const uint8_t* sa = lds + (t & 1) * kStage;
@@ -1719,7 +1730,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   }
   if constexpr (NP == 2) {  // undo the operand scales (exact: powers of two)
     const float ub = pow2f(-kb);
-    if (amax.a_rows) {  // B's scale here, each row's own in the LDS epilogue (rsh)
+    if constexpr (ROWS) {  // B's scale here, each row's own in the LDS epilogue (rsh)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1744,7 +1755,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
                                          act, C, ldc, slab, epi);
   epilogue_lds(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
                    n0 + wn * 64, lane, bias, beta, act, C, ldc, slab, cep,
-                   (NP == 2 && amax.a_rows && ntiles > 0) ? rsh + wm * 128 : nullptr);
+                   (ROWS && ntiles > 0) ? rsh + wm * 128 : nullptr);
 #else
   static_assert(NP != 2, "per-row A maxima need the LDS epilogue");
   tile_epilogue<EPI_LOGW, 4, 2>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta, act, C,
@@ -2455,18 +2466,22 @@ extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float
         BatchStrides{}, AmaxPtrs{amax_a, amax_b, 0, amax_a_rows}, cep);
     return check_launch("gemm_f32_kernel(lstm cell)");
   }
-  if (amax_a && w_planes)  // w_perm from its pre-split planes (mvml_split_f16x2 of w_perm)
+  if (amax_a_rows)  // a scale per A row (Set2Set: per molecule)
+    gemm_x3w_kernel<false, false, -1, true, 2, false, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
+        M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
+        BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, 0, amax_a_rows});
+  else if (amax_a && w_planes)  // w_perm from its pre-split planes (mvml_split_f16x2 of w_perm)
     gemm_x3w_kernel<false, false, -1, true, 2, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, reinterpret_cast<const float*>(w_planes), ldw, nullptr, 0.f, 0, nullptr,
-        N, K, nullptr, av, bv, ProjEpi{}, BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, w_plane, amax_a_rows});
-  else if (amax_a && !amax_a_rows && option(MVML_OPT_GEMM_RING))
+        N, K, nullptr, av, bv, ProjEpi{}, BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, w_plane});
+  else if (amax_a && option(MVML_OPT_GEMM_RING))
     gemm_h2g_kernel<false, false><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, BatchStrides{}, cep,
         AmaxPtrs{amax_a, amax_b});
   else if (amax_a)
     gemm_x3w_kernel<false, false, -1, true, 2><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
-        BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, 0, amax_a_rows});
+        BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b});
   else
     gemm_x3w_kernel<false, false, -1, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
@@ -2554,6 +2569,20 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0) && bst.b % 4 == 0;
   dim3 grid(plan.wide || bf ? x3w_grid_x(tiles, S) : (unsigned)tiles, (unsigned)S, (unsigned)batch);
   const bool ring = option(MVML_OPT_GEMM_RING) != 0 && !amax.a_rows;  // (the ring kernel: one A scale)
+  if (amax.a_rows && plan.wide) {  // per-row A maxima on the 256x256 tile (host: !a_kmajor)
+    if (b_kmajor && x3w_fast(false, true, M, N, K, av, bv))
+      gemm_x3w_kernel<false, true, -1, true, 2, false, true><<<grid, kXThreads, 0, st>>>(
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst, CellEpi{}, amax);
+    else if (b_kmajor)
+      gemm_x3w_kernel<false, true, -1, false, 2, false, true><<<grid, kXThreads, 0, st>>>(
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst, CellEpi{}, amax);
+    else if (x3w_fast(false, false, M, N, K, av, bv))
+      gemm_x3w_kernel<false, false, -1, true, 2, false, true><<<grid, kXThreads, 0, st>>>(
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst, CellEpi{}, amax);
+    else
+      gemm_x3w_kernel<false, false, -1, false, 2, false, true><<<grid, kXThreads, 0, st>>>(
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst, CellEpi{}, amax);
+  } else
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
   do {                                                                                          \
     if (hf && plan.wide && ring && !bps && x3w_fast(AKV, BKV, M, N, K, av, bv))                 \

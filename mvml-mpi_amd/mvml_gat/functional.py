@@ -300,12 +300,16 @@ class GATLayerFunction(torch.autograd.Function):
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()
         attn = torch.empty((E, H), dtype=torch.float32, device=dev)
+        # per-row max |out| for the consumer's per-row split-fp16 GEMMs (next layer, Set2Set)
+        orows = torch.empty(max(N, 1), dtype=torch.int32, device=dev) if (amx is not None and ROW_SCALES) else None
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}", "bytes": agg_fwd_bytes(N, E, H, F, out_cols, C - HF)}
         call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
              ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(_c(bias)), float(slope), int(mode),
-             ptr(out), ptr(attn), slot(amx, 3), st)
+             ptr(out), ptr(attn), slot(amx, 3), ptr(orows), st)
         if amx is not None:  # max |out| for the consumer's split-fp16 GEMMs (next layer, Set2Set)
             fold_amax(out, amx, 3)
+        if orows is not None:
+            fold_rows(out, orows)
         if DEBUG_CAPTURE is not None:
             DEBUG_CAPTURE.setdefault("elr_fwd", []).append(elr.detach().clone())
         ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr)
@@ -336,12 +340,17 @@ class GATLayerFunction(torch.autograd.Function):
         if ctx.amx is not None:
             ctx.amx[2:3].zero_()  # max |gY| of THIS backward (a second one, retain_graph, refolds it)
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_agg_bwd_workspace_size(g.num_edges(), H), dev)
+        # per-row max |gY| for the data-gradient product's per-row scales (not needed by layer 1,
+        # whose input gradient is not formed)
+        gyr = None
+        if ctx.amx is not None and ROW_SCALES and ctx.needs_input_grad[0]:
+            gyr = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}",
                             "bytes": agg_bwd_bytes(N, g.num_edges(), H, F, g_out.shape[1], mode)}
         call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
              ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr),
              ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldg,
-             slot(ctx.amx, 2), wp, wn, st)
+             slot(ctx.amx, 2), ptr(gyr), wp, wn, st)
         amx = ctx.amx  # slot 2 = max |gY|, folded in by mvml_gat_agg_bwd's stores
         if DEBUG_CAPTURE is not None and amx is not None:
             DEBUG_CAPTURE.setdefault("gy_amax", []).append((gY[:, :CE].clone(), amx[2:3].clone()))
@@ -375,7 +384,7 @@ class GATLayerFunction(torch.autograd.Function):
             gX = torch.empty((N, Fin), dtype=torch.float32, device=dev)
             if amx is not None and ROW_SCALES:  # every atom's gradient row at its own scale
                 gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, amax=(None, slot(amx, 1)),
-                     arows=absmax_rows(gY, N, CE, ldg))
+                     arows=gyr if gyr is not None else absmax_rows(gY, N, CE, ldg))
             else:
                 gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, algo=ctx.algo,
                      amax=None if amx is None else (slot(amx, 2), slot(amx, 1)),

@@ -104,7 +104,7 @@ def test_abi_argument_validation_without_gpu():
     rc = L.mvml_gemm_f32(0, 0, -1, 4, 4, None, 4, None, 4, None, 0.0, 0, None, 4, None, 0, None)
     assert rc == 1 and b"negative" in L.mvml_last_error()
     rc = L.mvml_gat_agg_fwd(10, None, 1, None, None, None, 3 * 8 * 2, 3, 8, None, None, 0.2, 0, None, None, None,
-                            None)
+                            None, None)
     assert rc == 1 and b"num_heads" in L.mvml_last_error()
     rc = L.mvml_build_csr(None, None, None, None, 1, 1 << 31, 5, *([None] * 12), None, 0, None)
     assert rc == 1 and b"overflow" in L.mvml_last_error()

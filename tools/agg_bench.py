@@ -56,7 +56,7 @@ def main():
         elr.normal_()
         f = lambda: call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.num_node_groups,
                          ptr(g.in_rowptr), ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(bias), 0.2,
-                         mode, ptr(out), ptr(attn), None, st)
+                         mode, ptr(out), ptr(attn), None, None, st)
         if a.no_fwd:
             f()
             ms = float("nan")
@@ -75,7 +75,7 @@ def main():
         b = lambda: call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups,
                          ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst),
                          ptr(g.out_inslot), ptr(Y), ldy, ptr(elr), ptr(attn), ptr(out), ptr(g_out), H, F,
-                         0.2, mode, ptr(gY), ldg, ptr(gmx), ptr(ws), wsz, st)
+                         0.2, mode, ptr(gY), ldg, ptr(gmx), None, ptr(ws), wsz, st)
         ms = timeit(b)
         by = agg_bwd_bytes(N, E, H, F, oc, mode)
         print(f"  agg_bwd {name:16s} {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
