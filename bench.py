@@ -53,7 +53,8 @@ TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32
          "mvml_gemm_f16x2_bsplit", "mvml_split_f16x2", "mvml_attn_conv_fwd", "mvml_attn_conv_bwd",
          "mvml_bilstm_wide_step_fwd", "mvml_bilstm_wide_step_bwd", "mvml_bilstm_pack_rows",
          "mvml_bilstm_gather_rows", "mvml_bilstm_token_grad", "mvml_bilstm_select_last",
-         "mvml_bilstm_token_grad_packed", "mvml_bilstm_packed_tokens"]
+         "mvml_bilstm_token_grad_packed", "mvml_bilstm_packed_tokens", "mvml_gemm_f16x2_rows",
+         "mvml_absmax_rows_f32", "mvml_segment_max_bits"]
 
 
 def parse(argv=None):
@@ -452,8 +453,11 @@ def run(args):
         opt.step()
 
     nb = len(batches)
+    # the first warm-up step runs the batch with the most edges, so the caching allocator sizes
+    # its blocks for the largest step once (no device malloc inside the timed region)
+    big = max(range(nb), key=lambda j: (batches[j].E, batches[j].N))
     for i in range(args.warmup):
-        step(batches[i % nb])
+        step(batches[big] if i == 0 else batches[i % nb])
     timer_on = not args.no_kernel_timer and not args.dry_run
     if timer_on:
         _lib.timer.enable(TIMED)
@@ -508,6 +512,7 @@ def run(args):
         if os.environ.get("MVML_GEMM_SHAPES") and rank == 0:
             gemm_shape_report(summ.get("mvml_gemm_f32x3", []) + summ.get("mvml_gemm_f32x3_batched", [])
                               + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])
+                              + summ.get("mvml_gemm_f16x2_rows", [])
                               + summ.get("mvml_gemm_f16x2_bsplit", [])
                               + summ.get("mvml_lstm_gates_cell_fwd", [])
                               + summ.get("mvml_gat_proj_fwd", []), args.steps)
@@ -526,7 +531,7 @@ def run(args):
         proj_ev = summ.get("mvml_gat_proj_fwd", [])
         gemm_ev = (summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", [])
                    + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])
-                   + summ.get("mvml_gemm_f16x2_bsplit", [])
+                   + summ.get("mvml_gemm_f16x2_bsplit", []) + summ.get("mvml_gemm_f16x2_rows", [])
                    + summ.get("mvml_gemm_f32x3_batched", []) + summ.get("mvml_lstm_gates_cell_fwd", [])
                    + ([] if args.proj_bf16 else proj_ev))
         bf_ev = summ.get("mvml_gemm_bf16", []) + (proj_ev if args.proj_bf16 else [])
@@ -537,7 +542,8 @@ def run(args):
                 frac=round(extra["roofline_gemm_bf16"]["achieved"] / BF16_MFMA_PEAK_TFS, 4))
         if gemm_ev:
             extra["roofline_gemm"] = roofline_entry(gemm_ev, "mfma")
-            if summ.get("mvml_gemm_f16x2") or summ.get("mvml_gemm_f16x2_amax") or summ.get("mvml_gemm_f16x2_bsplit"):
+            if (summ.get("mvml_gemm_f16x2") or summ.get("mvml_gemm_f16x2_amax") or summ.get("mvml_gemm_f16x2_bsplit")
+                    or summ.get("mvml_gemm_f16x2_rows")):
                 # scaled split-fp16: 3 fp16 MFMA per fp32 multiply-add -> fp32-equivalent peak
                 # 2.5 PF / 3 (the skinny products that fall back to split-bf16 count against it too)
                 extra["roofline_gemm"].update(

@@ -441,7 +441,9 @@ int mvml_conv3_bwd(int64_t B, int C, int O, int W, const float* in, const float*
  * writes P [B, H, 3, 3] (saved softmax) and out [B, 12, dk - 2] (post-ReLU); the backward
  * recomputes the cube from P and pv's v columns and writes g_pv, g_k (as
  * mvml_token_attn_fold_bwd), g_weight, g_bias (as mvml_conv3_bwd; workspace
- * mvml_attn_conv_bwd_workspace_size(B)).  Replaces model.py:66-69's att -> conv round trip. */
+ * mvml_attn_conv_bwd_workspace_size(B)).  Replaces model.py:66-69's att -> conv round trip.
+ * g_pv_rows (may be NULL; zeroed by the caller, 3 B entries): max with the bits of each g_pv
+ * row's |max| (the per-row scales of the data-gradient product that reads g_pv). */
 int mvml_attn_conv_fwd(int64_t B, int H, int dk, const float* pv, int64_t ld, const float* x,
                        int64_t ldx, float scale, const float* weight, const float* bias,
                        float* P, float* out, void* stream);
@@ -449,8 +451,9 @@ size_t mvml_attn_conv_bwd_workspace_size(int64_t B);
 int mvml_attn_conv_bwd(int64_t B, int H, int dk, const float* pv, int64_t ld, const float* x,
                        int64_t ldx, float scale, const float* P, const float* weight,
                        const float* out, const float* g_out, float* g_pv, int64_t ldg,
-                       float* g_k, int64_t ldgk, uint32_t* g_pv_amax, float* g_weight,
-                       float* g_bias, void* workspace, size_t workspace_bytes, void* stream);
+                       float* g_k, int64_t ldgk, uint32_t* g_pv_amax, uint32_t* g_pv_rows,
+                       float* g_weight, float* g_bias, void* workspace, size_t workspace_bytes,
+                       void* stream);
 int mvml_bce_logits(int64_t n, const float* z, const float* y, float* loss_terms, float* g_z,
                     void* stream);
 

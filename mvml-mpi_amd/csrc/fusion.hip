@@ -1087,7 +1087,8 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
                      const float* __restrict__ P, const float* __restrict__ wgt,
                      const float* __restrict__ out, const float* __restrict__ g_out,
                      float* __restrict__ gpv, int64_t ldg, float* __restrict__ gk, int64_t ldgk,
-                     uint32_t* __restrict__ gpv_amax, float* __restrict__ part) {
+                     uint32_t* __restrict__ gpv_amax, float* __restrict__ part,
+                     uint32_t* __restrict__ gpv_rows) {
   constexpr int W = kFuseW, Wo = W - 2, H = kConvC;
   constexpr int64_t HD = (int64_t)H * W;
   constexpr int kCD = kConvC * kConvH / 2;  // cube-gradient rows per thread
@@ -1214,16 +1215,18 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
       load_rows3(s_in + h * NT * kConvLd, kConvLd, lane, g);
       float gs[NT][NT];
       fold_grad_scores(g, v, p, scale, gs);
+      float rmx[NT];  // this wave's part of each token row's |max| (gpv_rows)
 #pragma unroll
       for (int c = 0; c < NT; ++c) {
         float* grow = gpv + (b * NT + c) * ldg + HD + (int64_t)h * W;
+        rmx[c] = 0.f;
 #pragma unroll
         for (int i = 0; i < kDkVpl; ++i) {
           float o = 0.f;
 #pragma unroll
           for (int a = 0; a < NT; ++a) o = fmaf(p[a][c], g[a][i], o);
           grow[lane + 64 * i] = o;
-          gmx = fmaxf(gmx, fabsf(o));
+          rmx[c] = fmaxf(rmx[c], fabsf(o));
         }
       }
       // the keys' gradient partial of head h goes over head h's own cube rows (read above by
@@ -1240,8 +1243,16 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
             ok = fmaf(gs[c][t], q[c][i], ok);
           }
           grow[lane + 64 * i] = oq;
-          gmx = fmaxf(gmx, fabsf(oq));
+          rmx[t] = fmaxf(rmx[t], fabsf(oq));
           s_in[(h * NT + t) * kConvLd + lane + 64 * i] = ok;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        gmx = fmaxf(gmx, rmx[t]);
+        if (gpv_rows) {  // the twelve head waves' parts of the row: an order-free max
+          const float m = wave_max(rmx[t]);
+          if (lane == 0) atomicMax(gpv_rows + b * NT + t, __float_as_uint(m));
         }
       }
     }
@@ -1468,8 +1479,9 @@ extern "C" int mvml_attn_conv_bwd(int64_t B, int H, int dk, const float* pv, int
                                   const float* x, int64_t ldx, float scale, const float* P,
                                   const float* weight, const float* out, const float* g_out,
                                   float* g_pv, int64_t ldg, float* g_k, int64_t ldgk,
-                                  uint32_t* g_pv_amax, float* g_weight, float* g_bias,
-                                  void* workspace, size_t workspace_bytes, void* stream) {
+                                  uint32_t* g_pv_amax, uint32_t* g_pv_rows, float* g_weight,
+                                  float* g_bias, void* workspace, size_t workspace_bytes,
+                                  void* stream) {
   clear_error();
   MVML_REQUIRE(B >= 0 && H == kConvC && dk == 64 * kDkVpl && ld >= 2 * (int64_t)H * dk &&
                    ldx >= dk && ldg >= 2 * (int64_t)H * dk && ldgk >= dk,
@@ -1485,7 +1497,8 @@ extern "C" int mvml_attn_conv_bwd(int64_t B, int H, int dk, const float* pv, int
   const int64_t used = ceil_div(B, per);
   float* part = static_cast<float*>(workspace);
   attn_conv_bwd_kernel<<<(unsigned)used, kFuseThreads, 0, st>>>(
-      B, per, pv, ld, x, ldx, scale, P, weight, out, g_out, g_pv, ldg, g_k, ldgk, g_pv_amax, part);
+      B, per, pv, ld, x, ldx, scale, P, weight, out, g_out, g_pv, ldg, g_k, ldgk, g_pv_amax, part,
+      g_pv_rows);
   int rc = check_launch("attn_conv_bwd_kernel");
   if (rc) return rc;
   partial_sum_kernel<<<(unsigned)ceil_div(kConvWg, 256), 256, 0, st>>>(

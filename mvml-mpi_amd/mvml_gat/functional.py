@@ -256,8 +256,14 @@ class GATLayerFunction(torch.autograd.Function):
             amx = torch.zeros(4, dtype=torch.int32, device=dev)  # [X, Wcat, gY (bwd), out]
             if ROW_SCALES and PROJ_ELR_GEMM:
                 # the projection splits every atom row with its own scale; max |X| (the weight
-                # gradient's A-side scale) is the max of the row maxima (N floats, not N x Fp)
-                xr = row_maxima(Xp, N, Fp, Fp)
+                # gradient's A-side scale) is the max of the row maxima (N floats, not N x Fp).
+                # Layer 1's rows are those of the resident atom features (the pad columns are
+                # zeros): computed once and recorded on the feature tensor itself
+                xr = known_rows(X)
+                if xr is None:
+                    xr = absmax_rows(X, N, Fin, Fin)
+                    if not X.requires_grad:
+                        fold_rows(X, xr)
                 absmax(xr, N, 1, 1, amx, 0)
                 ax = (amx, 0)
             else:
@@ -535,7 +541,6 @@ class Set2SetFunction(torch.autograd.Function):
         # running value bounds every cell seen so far, which is all a scale needs)
         amax_x, amax_w = ctx.amax
         amax_g = torch.zeros(Lr, dtype=torch.int32, device=dev) if amax_x is not None else None
-        grow = torch.empty(max(B, 1), dtype=torch.int32, device=dev) if amax_g is not None else None
         wsb = [None] * Lr  # [W_ih | W_hh] split once for the per-cell data-gradient products
         if amax_g is not None and BSPLIT:
             wsb = [split_planes(Wcat[l], 4 * D, Wcat[l].shape[1], Wcat[l].shape[1], slot(amax_w, l))
@@ -563,13 +568,11 @@ class Set2SetFunction(torch.autograd.Function):
                 ncols = kin + D if t > 0 else (kin if l > 0 else 0)
                 if ncols:
                     out, ldo = (g_qs3[t - 1], 3 * D) if l == 0 else (gxh[l], 2 * D)
-                    if amax_g is not None and ROW_SCALES:  # each molecule's gate gradients at its own scale
-                        gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo,
-                             amax=(None, slot(amax_w, l)), arows=absmax_rows(g_gates, B, 4 * D, 4 * D, grow))
-                    else:
-                        gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo,
-                             amax=None if amax_g is None else (slot(amax_g, l), slot(amax_w, l)),
-                             bsplit=wsb[l])
+                    # (operand-wide scales here: GraphNorm's backward has already mixed each
+                    # 64-molecule group's gradients, so the cells' rows span little)
+                    gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo,
+                         amax=None if amax_g is None else (slot(amax_g, l), slot(amax_w, l)),
+                         bsplit=wsb[l])
         # weight / bias gradients, one product per parameter over all steps:
         #   dW_ih[l] = sum_t g_gates[l,t]^T x_l(t),  dW_hh[l] = sum_{t>=1} g_gates[l,t]^T h_l(t-1)
         # (layer 0's input x_0(t) = q*_{t-1} is zero at t = 0; h_l(-1) = 0)

@@ -167,15 +167,21 @@ class FusionAttnConvFunction(torch.autograd.Function):
             if _F.GEMM_ALGO == "f16x2":  # split-fp16 maxima: gPV (folded by the kernel), Xn, Bcat
                 amx = torch.zeros(3, dtype=torch.int32, device=dev)
             # g_k (the keys' gradient, summed over heads) lands in gXn: the GEMMs add onto it
+            # per-row |gPV| maxima for the data-gradient product (folded by the fused kernel)
+            gpr = None
+            if amx is not None and _F.ROW_SCALES:
+                gpr = torch.zeros(3 * B, dtype=torch.int32, device=dev)
             if fused:
                 wp, wn = _lib.ws_ptr_size(L.mvml_attn_conv_bwd_workspace_size(B), dev)
                 _lib.call_tag[0] = {"bytes": attn_conv_bytes(B, H, D, True)}
                 call("mvml_attn_conv_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
                      ptr(P), ptr(_c(conv_w)), ptr(out), ptr(g_out), ptr(gPV), 2 * HD, ptr(gXn), D,
-                     slot(amx, 0), ptr(g_cw), ptr(g_cb), wp, wn, st)
+                     slot(amx, 0), ptr(gpr), ptr(g_cw), ptr(g_cb), wp, wn, st)
             else:
                 call("mvml_token_attn_fold_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
                      ptr(P), ptr(g_att), ptr(gPV), 2 * HD, ptr(gXn), D, slot(amx, 0), st)
+                if gpr is not None:
+                    _F.absmax_rows(gPV, 3 * B, 2 * HD, 2 * HD, gpr)
             if amx is not None:
                 absmax(Xn, 3 * B, D, D, amx, 1)
                 if _F.DEBUG_CAPTURE is not None:
@@ -192,7 +198,7 @@ class FusionAttnConvFunction(torch.autograd.Function):
             gemm_batched(wq3, G2, D, D, D, 0, 0, D, D, gWk, D, H, D * D, D * D, D * D)
             if amx is not None and _F.ROW_SCALES:  # every token row's gradient at its own scale
                 gemm(gPV, Bcat, 3 * B, D, 2 * HD, 0, 0, 2 * HD, 2 * HD, gXn, D, beta=1.0,
-                     amax=(None, slot(amx, 2)), arows=_F.absmax_rows(gPV, 3 * B, 2 * HD, 2 * HD))
+                     amax=(None, slot(amx, 2)), arows=gpr)
             else:
                 gemm(gPV, Bcat, 3 * B, D, 2 * HD, 0, 0, 2 * HD, 2 * HD, gXn, D, beta=1.0,
                      amax=None if amx is None else (slot(amx, 0), slot(amx, 2)))

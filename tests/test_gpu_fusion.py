@@ -283,9 +283,13 @@ def test_attn_conv_abi_matches_separate_kernels(B):
             call("mvml_attn_conv_fwd", B, H, D, ptr(PV), 2 * H * D, ptr(Xn), D, sc, ptr(w), ptr(bias),
                  ptr(P), ptr(out), st)
             wp, wn = ws_ptr_size(L.mvml_attn_conv_bwd_workspace_size(B), DEV)
+            rows = torch.zeros(3 * B, dtype=torch.int32, device=DEV)
             call("mvml_attn_conv_bwd", B, H, D, ptr(PV), 2 * H * D, ptr(Xn), D, sc, ptr(P), ptr(w),
-                 ptr(out), ptr(gout), ptr(gPV), 2 * H * D, ptr(gk), D, ptr(amx), ptr(gw), ptr(gb),
-                 wp, wn, st)
+                 ptr(out), ptr(gout), ptr(gPV), 2 * H * D, ptr(gk), D, ptr(amx), ptr(rows), ptr(gw),
+                 ptr(gb), wp, wn, st)
+            # the folded per-row maxima equal a pass over the written rows
+            torch.cuda.synchronize()
+            assert torch.equal(rows.view(torch.float32), gPV.abs().amax(1))
         else:
             att = torch.empty(B, H, 3, D, device=DEV)
             call("mvml_token_attn_fold_fwd", B, H, D, ptr(PV), 2 * H * D, ptr(Xn), D, sc, ptr(att),

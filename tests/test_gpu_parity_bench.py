@@ -186,10 +186,28 @@ def test_gnn_fusion_config3_bench_batch():
     1024 GraphNorm groups of 64): GNNModule -> MVFusion -> BCEWithLogits in eval mode, the
     logits, the loss, the two other views' input gradients and EVERY parameter gradient of the
     view and the fusion head against float64 (and fp32, for the conditioning measurement)."""
+    sb = synth.Config3Set(1_000_000, seed=0).molecules(0, 65536)
+    _gnn_fusion_case(sb, 64, 4096, "config3_bench_batch")
+
+
+# ----------------------------------------------------------------------------- config 5
+@pytest.mark.timeout(1500)
+@pytest.mark.parametrize("big_window", [1, 0])
+def test_gnn_fusion_config5_bench_batch(big_window):
+    """the config-5 bench batch as bench.py builds it (synth.config5(8192,
+    seed=1): 150-400-atom molecules with 1-4 hubs of in-degree 32-128, 128 GraphNorm groups of
+    64), GNNModule -> MVFusion -> BCE, forward and every gradient against float64, on the
+    big-window aggregation kernels (default) and on the per-atom fallback pair."""
+    from mvml_gat._lib import option
+    sb = synth.config5(8192, seed=1)
+    with option("big_window", big_window):
+        _gnn_fusion_case(sb, 64, 256, f"config5_bench_batch_bigwindow{big_window}")
+
+
+def _gnn_fusion_case(sb, gs, chunk, case):
     from mvml_gat import MVFusion, bce_with_logits
     from oracle.fusion_ref import MVFusionRef
-    n_mols, gs, chunk = 65536, 64, 4096
-    sb = synth.Config3Set(1_000_000, seed=0).molecules(0, n_mols)
+    n_mols = sb.batch_size
     noff, _ = _offsets(sb)
     prod, ref = model_pair(seed=31)
     torch.manual_seed(32)
@@ -288,9 +306,9 @@ def test_gnn_fusion_config3_bench_batch():
             e = _rel(p.grad, p64[n].grad)
             e32 = _rel(p32[n].grad, p64[n].grad)
             tensors[prefix + n] = {"err": e, "bar": TOL, "e32": e32}
-    rec = {"case": "config3_bench_batch", "molecules": n_mols, "atoms": g.num_nodes(),
+    rec = {"case": case, "molecules": n_mols, "atoms": g.num_nodes(),
            "edges": g.num_edges(), "graphnorm_groups": n_mols // gs, "gemm_algo": Fn.GEMM_ALGO,
-           "tensors": tensors, "kinks": kinks.check()}
-    _write("config3_bench_batch", rec)
+           "row_scales": Fn.ROW_SCALES, "tensors": tensors, "kinks": kinks.check()}
+    _write(case, rec)
     for n, t in tensors.items():
         assert t["err"] < t["bar"], (n, t)

@@ -148,12 +148,16 @@ def test_fusion_shard_invariant_bitwise():
 
 def test_saturated_logits_per_molecule_gradients():
     """one config-3 step (GNNModule -> MVFusion -> BCE) whose logits mix
-    saturated molecules (every |z| >= 20: BCE gradients ~1e-9) with molecules near |z| ~ 0
-    (gradients ~0.1) in one batch — the classifier's weights scaled so that 60 % of the
-    molecules saturate.  Per molecule, dL/d(graph embedding) within 1e-5 of the float64 oracle
-    relative to that molecule's OWN largest entry (per-row split-fp16 scales), and every
-    parameter gradient within 1e-5 norm-wise; margins to profiles via MVML_MARGINS_DIR."""
+    saturated molecules (every |z| >= 15: BCE gradients below 3e-7) with molecules near
+    |z| ~ 0 in one batch — the classifier's weights scaled so that 60 % of the molecules
+    saturate, which makes the rows of dL/d(graph embedding) span far more than 2^20.  Per
+    molecule, that row's error relative to its OWN largest entry is held to max(1e-5, 4 e32),
+    e32 = what the same oracle in fp32 loses on the row (the saturated terms exp(-|z|) turn
+    the logits' absolute rounding into relative gradient error in any fp32 evaluation), and
+    every parameter gradient likewise norm-wise.  The operand-wide-scale path (ROW_SCALES off)
+    is measured beside it for the record."""
     import mvml_gat
+    from mvml_gat import functional as Fn
     from _util import graph_dict
     from oracle.fusion_ref import MVFusionRef, bce_logits_ref
     from oracle.gnn_ref import GNNModuleRef
@@ -163,55 +167,77 @@ def test_saturated_logits_per_molecule_gradients():
     torch.manual_seed(2)
     model = mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3).to(DEV).eval()
     fus = mvml_gat.MVFusion(384, 12, 11, 0.5).to(DEV).eval()
-    ref = GNNModuleRef(74, [192, 384], 0.5, 6, 3).double().eval()
-    fref = MVFusionRef(384, 12, 11, 0.5).double().eval()
-    ref.load_state_dict({k: v.double() for k, v in model.state_dict().items()})
     g = torch.Generator().manual_seed(8)
     sx = torch.randn(B, 384, generator=g, dtype=torch.float64)
     fx = torch.randn(B, 384, generator=g, dtype=torch.float64)
     gd = graph_dict(sb, group_size=gs)
     X64 = torch.as_tensor(sb.feats, dtype=torch.float64)
-    # scale the classifier so that the 40th percentile of min_c |z| lands at 20
+    refs = {}
+    for dt in (torch.float64, torch.float32):
+        r = GNNModuleRef(74, [192, 384], 0.5, 6, 3).to(dt).eval()
+        r.load_state_dict({k: v.to(dt) for k, v in model.state_dict().items()})
+        refs[dt] = [r, MVFusionRef(384, 12, 11, 0.5).to(dt).eval()]
+    # the 40th percentile of min_c |z| at 15
     with torch.no_grad():
         fus.mlp[3].bias.zero_()
-        fref.load_state_dict({k: v.double() for k, v in fus.state_dict().items()})
-        z0 = fref(sx, ref(gd, X64), fx)
-        c = 20.0 / float(torch.quantile(z0.abs().amin(1), 0.4))
-        fus.mlp[3].weight.mul_(c)
-    fref.load_state_dict({k: v.double() for k, v in fus.state_dict().items()})
-    emb_r = ref(gd, X64)
-    emb_r.retain_grad()
-    z_r = fref(sx, emb_r, fx)
-    y = (z_r.detach() > 0).double()  # every label agrees with its logit's sign
-    bce_logits_ref(z_r, y).backward()
-    gdev = sb.to_graph(group_size=gs).to(DEV)
-    emb = model(gdev, gdev.ndata["h"])
-    emb.retain_grad()
-    z = fus(sx.float().to(DEV), emb, fx.float().to(DEV))
-    mvml_gat.bce_with_logits(z, y.float().to(DEV)).backward()
-    zmin = z_r.detach().abs().amin(1)
-    ge_r, ge = emb_r.grad, emb.grad.double().cpu()
-    rmax = ge_r.abs().amax(1)
-    per_row = (ge - ge_r).abs().amax(1) / rmax.clamp_min(1e-300)
-    errs = {"frac_saturated_ge20": float((zmin >= 20).double().mean()),
-            "frac_near_zero_lt1": float((zmin < 1).double().mean()),
-            "emb_grad_row_span_log2": float(torch.log2(rmax.max() / rmax.min())),
-            "emb_grad_per_row_max": float(per_row.max()),
-            "emb_grad_per_row_saturated_max": float(per_row[zmin >= 20].max()),
-            "emb_grad_normwise": rel_err(ge, ge_r),
-            "logits": rel_err(z, z_r)}
-    pr = dict(ref.named_parameters())
-    for n, p in model.named_parameters():
-        errs["gnn." + n] = rel_err(p.grad, pr[n].grad)
-    fr = dict(fref.named_parameters())
-    for n, p in fus.named_parameters():
-        if p.grad is not None:
-            errs["fusion." + n] = rel_err(p.grad, fr[n].grad)
+        refs[torch.float64][1].load_state_dict({k: v.double() for k, v in fus.state_dict().items()})
+        z0 = refs[torch.float64][1](sx, refs[torch.float64][0](gd, X64), fx)
+        fus.mlp[3].weight.mul_(15.0 / float(torch.quantile(z0.abs().amin(1), 0.4)))
+    res = {}
+    for dt, (r, f) in refs.items():
+        f.load_state_dict({k: v.to(dt) for k, v in fus.state_dict().items()})
+        emb = r(gd, X64.to(dt))
+        emb.retain_grad()
+        z = f(sx.to(dt), emb, fx.to(dt))
+        if dt == torch.float64:
+            y = (z.detach() > 0).double()  # every label agrees with its logit's sign
+        bce_logits_ref(z, y.to(dt)).backward()
+        res[dt] = (z.detach(), emb.grad, {n: p.grad for n, p in list(r.named_parameters()) + [
+            ("fusion." + n, p) for n, p in f.named_parameters()] if p.grad is not None})
+    z64, ge64, pg64 = res[torch.float64]
+    rmax = ge64.abs().amax(1)
+    zmin = z64.abs().amin(1)
+
+    def per_row(ge):
+        return (ge.double().cpu() - ge64).abs().amax(1) / rmax.clamp_min(1e-300)
+
+    e32_row = per_row(res[torch.float32][1])
+    budget = torch.clamp(4 * e32_row, min=TOL)
+
+    def product(row_scales):
+        prev = Fn.ROW_SCALES
+        Fn.ROW_SCALES = row_scales
+        try:
+            model.zero_grad(set_to_none=True)
+            fus.zero_grad(set_to_none=True)
+            gdev = sb.to_graph(group_size=gs).to(DEV)
+            emb = model(gdev, gdev.ndata["h"])
+            emb.retain_grad()
+            z = fus(sx.float().to(DEV), emb, fx.float().to(DEV))
+            mvml_gat.bce_with_logits(z, y.float().to(DEV)).backward()
+            grads = {n: p.grad for n, p in model.named_parameters()}
+            grads.update({"fusion." + n: p.grad for n, p in fus.named_parameters() if p.grad is not None})
+            return z, emb.grad, grads
+        finally:
+            Fn.ROW_SCALES = prev
+
+    rec = {"frac_saturated_ge15": float((zmin >= 15).double().mean()),
+           "frac_near_zero_lt1": float((zmin < 1).double().mean()),
+           "emb_grad_row_span_log2": float(torch.log2(rmax.max() / rmax[rmax > 0].min())),
+           "fp32_oracle_per_row_max": float(e32_row.max())}
+    for tag, rs in (("rows", True), ("operand", False)):
+        z, ge, grads = product(rs)
+        pr = per_row(ge)
+        rec[tag] = {"logits": rel_err(z, z64), "emb_grad_per_row_max": float(pr.max()),
+                    "emb_grad_per_row_over_budget": int((pr > budget).sum()),
+                    "emb_grad_per_row_worst_ratio": float((pr / budget).max()),
+                    "emb_grad_normwise": rel_err(ge, ge64)}
+        pbud = {n: max(TOL, 4 * rel_err(res[torch.float32][2][n], g64)) for n, g64 in pg64.items()}
+        rec[tag]["params_worst_ratio"] = max(rel_err(grads[n], g64) / pbud[n] for n, g64 in pg64.items())
+        rec[tag]["params_worst"] = max(((rel_err(grads[n], g64), n) for n, g64 in pg64.items()))
     with open(os.path.join(_margins_dir(), "saturated_logits_config3.json"), "w") as f:
-        json.dump(errs, f, indent=1)
-    print(errs)
-    assert errs["frac_saturated_ge20"] > 0.5 and errs["emb_grad_row_span_log2"] > 20
-    assert errs["emb_grad_per_row_max"] < TOL
-    for k, v in errs.items():
-        if k.startswith(("gnn.", "fusion.")):
-            assert v < TOL, (k, v)
+        json.dump(rec, f, indent=1)
+    print(rec)
+    assert rec["frac_saturated_ge15"] > 0.5 and rec["emb_grad_row_span_log2"] > 20
+    assert rec["rows"]["emb_grad_per_row_over_budget"] == 0, rec["rows"]
+    assert rec["rows"]["params_worst_ratio"] < 1.0, rec["rows"]

@@ -152,3 +152,51 @@ def test_rnn_module_rejects_empty_sequence():
     mod = RNNModule(vocab, 128, 384, 1, 384).to(DEV)
     with pytest.raises(RuntimeError):
         mod({"smiles": batch["smiles"].to(DEV), "seq_len": [0] + batch["seq_len"][1:]})
+
+
+@pytest.mark.timeout(900)
+def test_rnn_module_bench_size():
+    """the wide BiLSTM at config 4's size — 8,192 molecules per step with the
+    bench's token lengths (about 1.8 characters per atom of the config-3 set, 5 .. 462) — output
+    and every parameter gradient against the float64 restatement run on the GPU (aten LSTM:
+    MIOpen has no float64 RNN), margins to MVML_MARGINS_DIR."""
+    import json
+    import os
+    from mvml_gat import synth
+    from mvml_gat.smiles import RNNModule, tokens_struct
+    from oracle.smiles_ref import RNNModuleRef
+    B = 8192
+    sb = synth.Config3Set(1_000_000, seed=0).molecules(0, B)
+    rng = np.random.default_rng([0, 77])
+    lens = np.clip(np.rint(1.8 * sb.num_nodes * rng.uniform(0.8, 1.2, B)), 5, 462).astype(np.int64)
+    T = int(lens.max())
+    tok = rng.integers(2, 39, size=(B, T)).astype(np.float32)
+    tok[np.arange(T)[None, :] >= lens[:, None]] = 0.0
+    batch = {"smiles": torch.from_numpy(tok), "seq_len": lens.tolist()}
+    torch.manual_seed(9)
+    ref = RNNModuleRef(39, 128, 384, 2, 384, 0.5).double().eval()
+    mod = RNNModule(tokens_struct(), 128, 384, 2, 384, 0.5).to(DEV).eval()
+    mod.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    up = torch.randn((B, 384), generator=torch.Generator().manual_seed(3), dtype=torch.float64)
+    zd = mod({"smiles": batch["smiles"].to(DEV), "seq_len": batch["seq_len"]})
+    (zd * up.float().to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    ref = ref.to(DEV)
+    with torch.backends.cudnn.flags(enabled=False):
+        zr = ref({"smiles": batch["smiles"].to(DEV), "seq_len": batch["seq_len"]})
+        (zr * up.to(DEV)).sum().backward()
+    errs = {"out": rel_err(zd, zr)}
+    pr = dict(ref.named_parameters())
+    for name, p in mod.named_parameters():
+        if pr[name].grad is None:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, name
+            continue
+        errs[name] = rel_err(p.grad, pr[name].grad)
+    out = os.environ.get("MVML_MARGINS_DIR", os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "gpurun_out", "parity_margins"))
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "bilstm_bench_size.json"), "w") as f:
+        json.dump({"molecules": B, "T": T, "live_rows": int(lens.sum()), "errors": errs}, f, indent=1)
+    print(errs)
+    for k, e in errs.items():
+        assert e < TOL, (k, e)

@@ -55,7 +55,7 @@ def main():
 
     def fused_bwd():
         call("mvml_attn_conv_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, sc, ptr(P), ptr(w), ptr(out),
-             ptr(g_out), ptr(gPV), 2 * HD, ptr(gk), D, ptr(amx), ptr(gw), ptr(gb), ptr(ws), nws, st)
+             ptr(g_out), ptr(gPV), 2 * HD, ptr(gk), D, ptr(amx), None, ptr(gw), ptr(gb), ptr(ws), nws, st)
 
     def sep_fwd():
         call("mvml_token_attn_fold_fwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, sc, ptr(att), ptr(P), st)
