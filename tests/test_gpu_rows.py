@@ -203,6 +203,9 @@ def test_saturated_logits_per_molecule_gradients():
 
     e32_row = per_row(res[torch.float32][1])
     budget = torch.clamp(4 * e32_row, min=TOL)
+    # rows whose largest gradient is below 2^-100 sit where fp32 itself runs out (BCE's
+    # exp(-|z|) underflows past |z| ~ 88; the GPU flushes denormals): not a scaling question
+    ok = rmax >= 2.0 ** -100
 
     def product(row_scales):
         prev = Fn.ROW_SCALES
@@ -223,14 +226,15 @@ def test_saturated_logits_per_molecule_gradients():
 
     rec = {"frac_saturated_ge15": float((zmin >= 15).double().mean()),
            "frac_near_zero_lt1": float((zmin < 1).double().mean()),
-           "emb_grad_row_span_log2": float(torch.log2(rmax.max() / rmax[rmax > 0].min())),
-           "fp32_oracle_per_row_max": float(e32_row.max())}
+           "emb_grad_row_span_log2": float(torch.log2(rmax[ok].max() / rmax[ok].min())),
+           "rows_checked": int(ok.sum()), "rows_below_fp32_range": int((~ok).sum()),
+           "fp32_oracle_per_row_max": float(e32_row[ok].max())}
     for tag, rs in (("rows", True), ("operand", False)):
         z, ge, grads = product(rs)
         pr = per_row(ge)
-        rec[tag] = {"logits": rel_err(z, z64), "emb_grad_per_row_max": float(pr.max()),
-                    "emb_grad_per_row_over_budget": int((pr > budget).sum()),
-                    "emb_grad_per_row_worst_ratio": float((pr / budget).max()),
+        rec[tag] = {"logits": rel_err(z, z64), "emb_grad_per_row_max": float(pr[ok].max()),
+                    "emb_grad_per_row_over_budget": int((pr[ok] > budget[ok]).sum()),
+                    "emb_grad_per_row_worst_ratio": float((pr[ok] / budget[ok]).max()),
                     "emb_grad_normwise": rel_err(ge, ge64)}
         pbud = {n: max(TOL, 4 * rel_err(res[torch.float32][2][n], g64)) for n, g64 in pg64.items()}
         rec[tag]["params_worst_ratio"] = max(rel_err(grads[n], g64) / pbud[n] for n, g64 in pg64.items())
@@ -239,5 +243,6 @@ def test_saturated_logits_per_molecule_gradients():
         json.dump(rec, f, indent=1)
     print(rec)
     assert rec["frac_saturated_ge15"] > 0.5 and rec["emb_grad_row_span_log2"] > 20
+    assert rec["rows_checked"] >= B // 2
     assert rec["rows"]["emb_grad_per_row_over_budget"] == 0, rec["rows"]
     assert rec["rows"]["params_worst_ratio"] < 1.0, rec["rows"]
