@@ -175,10 +175,19 @@ int mvml_gemm_f16x2_amax(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
  * ~2^17 below it, where the low fp16 plane goes subnormal), and (b) a row of C depends only on
  * its own row of A and on B: the same molecule gives bitwise the same output in any batch. */
 int mvml_gemm_f16x2_rows(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
-                         const float* B, int64_t ldb, int b_kmajor, const uint32_t* amax_a_rows,
-                         const uint32_t* amax_b, const float* bias, float beta, int act,
-                         float* C, int64_t ldc, void* workspace, size_t workspace_bytes,
-                         void* stream);
+                         const float* B, int64_t ldb, int b_kmajor, const float* b_il4,
+                         const uint32_t* amax_a_rows, const uint32_t* amax_b, const float* bias,
+                         float beta, int act, float* C, int64_t ldc, void* workspace,
+                         size_t workspace_bytes, void* stream);
+/* B pre-split once as an interleaved-by-4 image for the split-fp16 GEMMs: every 4 consecutive
+ * values of a row become [4 scaled high fp16 | 4 low fp16] (16 B, the scale from *amax as the
+ * GEMM's own split), written to out with P's own [rows][ld] float indexing, so the image stands
+ * in for B in any layout (K-contiguous or K-major): the 256x256 tiles load a piece with one 16-B
+ * load and skip B's split (b_il4 of mvml_gemm_f16x2_rows; mvml_gemm_f16x2_bsplit with
+ * b_plane = 0; mvml_lstm_gates_cell_fwd with w_plane = 0).  Bitwise the in-kernel split.
+ * cols % 4 == 0, ld % 4 == 0, P and out 16-B aligned. */
+int mvml_split_f16x2_il4(int64_t rows, int64_t cols, const float* P, int64_t ld,
+                         const uint32_t* amax, float* out, void* stream);
 /* out[r] = bits of max_c |P[r*ld + c]|, c < cols (accumulate != 0: max with the current out[r]);
  * one writer per row, no atomics. */
 int mvml_absmax_rows_f32(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32_t* out,
@@ -331,7 +340,8 @@ int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float* A, int64_
                              const uint32_t* amax_a_rows /* NULL, or per-row |A| max bits (M
                                entries; replaces amax_a, see mvml_gemm_f16x2_rows) */,
                              const uint16_t* w_planes, int64_t w_plane /* NULL, or w_perm
-                               pre-split by mvml_split_f16x2 with amax_b */,
+                               pre-split by mvml_split_f16x2 with amax_b; w_plane = 0: the
+                               interleaved image of mvml_split_f16x2_il4 */,
                              void* stream);
 /* Per molecule b: out_bits[b] = max(floor_bits, max_{n in [node_offsets[b], node_offsets[b+1])}
  * in_bits[n]) on non-negative float bits — a molecule's bound from its atoms' row maxima (the

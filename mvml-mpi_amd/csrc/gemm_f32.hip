@@ -1315,7 +1315,7 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
 // ROWS (split-fp16, K-contiguous A): per-row A maxima (amax.a_rows), a scale per A row; a
 // separate instantiation so that the operand-wide kernels keep their register allocation (one
 // spill reload inside the main loop costs a vmcnt drain per stage).
-template <bool AK, bool BKM, int EPI_LOGW = -1, bool FAST = true, int NP = 3, bool BPS = false,
+template <bool AK, bool BKM, int EPI_LOGW = -1, bool FAST = true, int NP = 3, int BPS = 0,
           bool ROWS = false>
 __global__ void __launch_bounds__(kXThreads, MVML_X3W_WAVES)  // one workgroup per CU
 gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
@@ -1341,9 +1341,13 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   using OA = XOp<AK, NP>;
   using OB = XOp<BKM, NP>;
   static_assert(!BPS || (NP == 2 && FAST), "pre-split B: split-fp16 fast path only");
-  // B piece at float-indexed address p: fp32 values, or (BPS) the two planes' 8-B pieces
+  // B piece at float-indexed address p: fp32 values, (BPS 1) the two planes' 8-B pieces, or
+  // (BPS 2) the interleaved image's 16-B piece [4 high | 4 low] (mvml_split_f16x2_il4: the same
+  // float indexing as the fp32 operand, one load per piece like fp32)
   auto ldb4 = [&](const float* p) -> float4 {
-    if constexpr (BPS) {
+    if constexpr (BPS == 2) {
+      return *reinterpret_cast<const float4*>(p);
+    } else if constexpr (BPS == 1) {
       const uint16_t* q = reinterpret_cast<const uint16_t*>(B) + (p - B);
       const uint2 h = *reinterpret_cast<const uint2*>(q);
       const uint2 l = *reinterpret_cast<const uint2*>(q + amax.b_plane);
@@ -1619,7 +1623,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   using L1 = std::integral_constant<int, 1>;
   using L2 = std::integral_constant<int, 2>;
 #if MVML_X3W_PF2
-  if constexpr (FAST && KS == 1 && !BPS) {
+  if constexpr (FAST && KS == 1 && BPS == 0) {
     // Prefetch distance 2: tile k's fp32 values live in register set k % 2 from their load (in
     // body k - 3) to their split (in body k - 1), so a global load has two whole stages to land
     // instead of one (the loads of a stage are issued right after the split that frees the set).
@@ -2248,6 +2252,25 @@ __global__ void __launch_bounds__(256) split_f16x2_il_kernel(int64_t rows, int64
   }
 }
 
+// Interleaved-by-4 pre-split for the 256x256 kernels (BPS 2): every 4-value group of a row
+// becomes [4 scaled high fp16 | 4 low fp16] = 16 B in place of its 16 B of fp32, so the image
+// has the operand's own float indexing (any layout, K-contiguous or K-major) and a staged piece
+// is one 16-B load, stored to the LDS planes as it is (split2h of the kernel's own staging).
+__global__ void __launch_bounds__(256) split_f16x2_il4_kernel(int64_t rows, int64_t cols4,
+                                                              const float* __restrict__ P, int64_t ld,
+                                                              const uint32_t* __restrict__ amax,
+                                                              float* __restrict__ out) {
+  const float sc = pow2f(amax_shift(*amax));
+  const int64_t total = rows * cols4;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t r = e / cols4, c = 4 * (e - r * cols4);
+    uint2 h, l;
+    split2h(*reinterpret_cast<const float4*>(P + r * ld + c), sc, h, l);
+    *reinterpret_cast<float4*>(out + r * ld + c) =
+        make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(l.x), __uint_as_float(l.y));
+  }
+}
+
 int split_il_launch(int64_t rows, int64_t K, const float* P, const uint32_t* amax, float* out,
                     hipStream_t st) {
   const int64_t total = rows * (K / 8);
@@ -2361,18 +2384,33 @@ extern "C" int mvml_gemm_f16x2_amax(int a_kmajor, int b_kmajor, int64_t M, int64
 }
 
 extern "C" int mvml_gemm_f16x2_rows(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
-                                    const float* B, int64_t ldb, int b_kmajor,
+                                    const float* B, int64_t ldb, int b_kmajor, const float* b_il4,
                                     const uint32_t* amax_a_rows, const uint32_t* amax_b,
                                     const float* bias, float beta, int act, float* C, int64_t ldc,
                                     void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
   MVML_REQUIRE(amax_a_rows != nullptr && amax_b != nullptr,
                "gemm_f16x2_rows: amax_a_rows / amax_b are required");
+  MVML_REQUIRE(!b_il4 || ((uintptr_t)b_il4 % 16) == 0, "gemm_f16x2_rows: b_il4 must be 16-B aligned");
   AmaxPtrs am;
   am.b = amax_b;
   am.a_rows = amax_a_rows;
   return gemm_launch(kPrecF16x2, 0, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
-                     workspace, workspace_bytes, stream, 1, BatchStrides{}, am);
+                     workspace, workspace_bytes, stream, 1, BatchStrides{}, am,
+                     reinterpret_cast<const uint16_t*>(b_il4));
+}
+
+extern "C" int mvml_split_f16x2_il4(int64_t rows, int64_t cols, const float* P, int64_t ld,
+                                    const uint32_t* amax, float* out, void* stream) {
+  clear_error();
+  MVML_REQUIRE(rows >= 0 && cols >= 0 && cols % 4 == 0 && ld % 4 == 0 && ld >= cols && amax &&
+                   out && ((uintptr_t)P % 16) == 0 && ((uintptr_t)out % 16) == 0,
+               "split_f16x2_il4: bad shape / alignment");
+  if (rows == 0 || cols == 0) return MVML_OK;
+  const int64_t total = rows * (cols / 4);
+  const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
+  split_f16x2_il4_kernel<<<blocks, 256, 0, as_stream(stream)>>>(rows, cols / 4, P, ld, amax, out);
+  return check_launch("split_f16x2_il4_kernel");
 }
 
 extern "C" int mvml_absmax_rows_f32(int64_t rows, int64_t cols, const float* P, int64_t ld,
@@ -2403,7 +2441,8 @@ extern "C" int mvml_gemm_f16x2_bsplit(int a_kmajor, int b_kmajor, int64_t M, int
                                       int64_t ldc, void* workspace, size_t workspace_bytes,
                                       void* stream) {
   clear_error();
-  MVML_REQUIRE(amax_a && amax_b && b_planes && b_plane > 0 && ((uintptr_t)b_planes % 8) == 0,
+  MVML_REQUIRE(amax_a && amax_b && b_planes && b_plane >= 0 &&
+                   ((uintptr_t)b_planes % (b_plane ? 8 : 16)) == 0,
                "gemm_f16x2_bsplit: maxima and B's planes are required");
   AmaxPtrs am{amax_a, amax_b, b_plane};
   return gemm_launch(kPrecF16x2, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C,
@@ -2466,12 +2505,16 @@ extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float
         BatchStrides{}, AmaxPtrs{amax_a, amax_b, 0, amax_a_rows}, cep);
     return check_launch("gemm_f32_kernel(lstm cell)");
   }
-  if (amax_a_rows)  // a scale per A row (Set2Set: per molecule)
-    gemm_x3w_kernel<false, false, -1, true, 2, false, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
+  if (amax_a_rows && w_planes && w_plane == 0)  // per-row A, w_perm from its il4 image
+    gemm_x3w_kernel<false, false, -1, true, 2, 2, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
+        M, N, K, A, lda, reinterpret_cast<const float*>(w_planes), ldw, nullptr, 0.f, 0, nullptr,
+        N, K, nullptr, av, bv, ProjEpi{}, BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, 0, amax_a_rows});
+  else if (amax_a_rows)  // a scale per A row (Set2Set: per molecule)
+    gemm_x3w_kernel<false, false, -1, true, 2, 0, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
         BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, 0, amax_a_rows});
-  else if (amax_a && w_planes)  // w_perm from its pre-split planes (mvml_split_f16x2 of w_perm)
-    gemm_x3w_kernel<false, false, -1, true, 2, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
+  else if (amax_a && w_planes && w_plane > 0)  // w_perm from its pre-split planes (mvml_split_f16x2)
+    gemm_x3w_kernel<false, false, -1, true, 2, 1><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, reinterpret_cast<const float*>(w_planes), ldw, nullptr, 0.f, 0, nullptr,
         N, K, nullptr, av, bv, ProjEpi{}, BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, w_plane});
   else if (amax_a && option(MVML_OPT_GEMM_RING))
@@ -2569,18 +2612,39 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0) && bst.b % 4 == 0;
   dim3 grid(plan.wide || bf ? x3w_grid_x(tiles, S) : (unsigned)tiles, (unsigned)S, (unsigned)batch);
   const bool ring = option(MVML_OPT_GEMM_RING) != 0 && !amax.a_rows;  // (the ring kernel: one A scale)
+  // B pre-split as an interleaved-by-4 image (bps with b_plane == 0, mvml_split_f16x2_il4) and /
+  // or per-row A maxima, on the 256x256 tile (host: K-contiguous A)
+  const bool il4 = bps && amax.b_plane == 0;
+  const float* Bil = il4 ? reinterpret_cast<const float*>(bps) : B;
+#define MVML_X3W_RB(BKV, BPSV, ROWSV)                                                            \
+  gemm_x3w_kernel<false, BKV, -1, true, 2, BPSV, ROWSV><<<grid, kXThreads, 0, st>>>(             \
+      M, N, K, A, lda, Bil, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst,       \
+      CellEpi{}, amax)
+  if ((amax.a_rows || il4) && plan.wide && !a_kmajor && batch == 1 &&
+      x3w_fast(false, b_kmajor, M, N, K, av, bv)) {
+    if (b_kmajor) {
+      if (il4 && amax.a_rows) MVML_X3W_RB(true, 2, true);
+      else if (il4) MVML_X3W_RB(true, 2, false);
+      else MVML_X3W_RB(true, 0, true);
+    } else {
+      if (il4 && amax.a_rows) MVML_X3W_RB(false, 2, true);
+      else if (il4) MVML_X3W_RB(false, 2, false);
+      else MVML_X3W_RB(false, 0, true);
+    }
+  } else
+#undef MVML_X3W_RB
   if (amax.a_rows && plan.wide) {  // per-row A maxima on the 256x256 tile (host: !a_kmajor)
     if (b_kmajor && x3w_fast(false, true, M, N, K, av, bv))
-      gemm_x3w_kernel<false, true, -1, true, 2, false, true><<<grid, kXThreads, 0, st>>>(
+      gemm_x3w_kernel<false, true, -1, true, 2, 0, true><<<grid, kXThreads, 0, st>>>(
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst, CellEpi{}, amax);
     else if (b_kmajor)
-      gemm_x3w_kernel<false, true, -1, false, 2, false, true><<<grid, kXThreads, 0, st>>>(
+      gemm_x3w_kernel<false, true, -1, false, 2, 0, true><<<grid, kXThreads, 0, st>>>(
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst, CellEpi{}, amax);
     else if (x3w_fast(false, false, M, N, K, av, bv))
-      gemm_x3w_kernel<false, false, -1, true, 2, false, true><<<grid, kXThreads, 0, st>>>(
+      gemm_x3w_kernel<false, false, -1, true, 2, 0, true><<<grid, kXThreads, 0, st>>>(
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst, CellEpi{}, amax);
     else
-      gemm_x3w_kernel<false, false, -1, false, 2, false, true><<<grid, kXThreads, 0, st>>>(
+      gemm_x3w_kernel<false, false, -1, false, 2, 0, true><<<grid, kXThreads, 0, st>>>(
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst, CellEpi{}, amax);
   } else
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
@@ -2589,8 +2653,8 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
       gemm_h2g_kernel<AKV, BKV><<<grid, kXThreads, 0, st>>>(M, N, K, A, lda, B, ldb, bias, beta, \
                                                            act, C, ldc, kc, slab, bst,          \
                                                            CellEpi{}, amax);                    \
-    else if (hf && plan.wide && bps && batch == 1 && x3w_fast(AKV, BKV, M, N, K, av, bv))      \
-      gemm_x3w_kernel<AKV, BKV, -1, true, 2, true><<<grid, kXThreads, 0, st>>>(                 \
+    else if (hf && plan.wide && bps && amax.b_plane && batch == 1 && x3w_fast(AKV, BKV, M, N, K, av, bv)) \
+      gemm_x3w_kernel<AKV, BKV, -1, true, 2, 1><<<grid, kXThreads, 0, st>>>(                 \
           M, N, K, A, lda, reinterpret_cast<const float*>(bps), ldb, bias, beta, act, C, ldc, kc, \
           slab, av, bv, ProjEpi{}, bst, CellEpi{}, amax);                                       \
     else if (hf && plan.wide && x3w_fast(AKV, BKV, M, N, K, av, bv))                            \
@@ -2661,7 +2725,7 @@ int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int
   const bool x3 = prec == kPrecX3 || hf, bf = prec == kPrecBf16;
   const bool wide = bf || (x3 && plan_gemm(kPrecX3, M, N, K).wide);
   AmaxPtrs amx{amax_x, amax_w, w_plane};
-  const bool bps = hf && w_planes && amax_x && amax_w;  // B = Wcat from its pre-split planes
+  const bool bps = hf && w_planes && w_plane > 0 && amax_x && amax_w;  // B = Wcat from its planes
   if (hf && wide && !(amax_x && amax_w)) {  // maxima not supplied: one pass per operand
     MVML_REQUIRE(amax_ws != nullptr, "gat_proj_fwd: split-fp16 needs the maxima workspace");
     int rc = absmax_launch(M, K, A, lda, amax_ws, false, st);
@@ -2678,7 +2742,7 @@ int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int
 #define MVML_PROJ(LW)                                                                          \
   do {                                                                                         \
     if (bps && wide && x3w_fast(false, false, M, N, K, av, bv))                                \
-      gemm_x3w_kernel<false, false, LW, true, 2, true><<<grid, kXThreads, 0, st>>>(            \
+      gemm_x3w_kernel<false, false, LW, true, 2, 1><<<grid, kXThreads, 0, st>>>(            \
           M, N, K, A, lda, reinterpret_cast<const float*>(w_planes), ldb, nullptr, 0.f, 0, C,  \
           ldc, K > 0 ? K : 1, nullptr, av, bv, ProjEpi{vec, cols, part}, BatchStrides{},       \
           CellEpi{}, amx);                                                                     \

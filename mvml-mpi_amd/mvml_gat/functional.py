@@ -155,6 +155,22 @@ PROJ_ELR_GEMM = os.environ.get("MVML_PROJ_ELR_GEMM", "1") != "0"
 BSPLIT = os.environ.get("MVML_BSPLIT", "0") == "1"
 
 
+# Weights split ONCE per step into the interleaved-by-4 fp16 image (mvml_split_f16x2_il4) that
+# the 256x256 split-fp16 tiles load in place of fp32 B: one 16-B load per piece as before and no
+# split VALU for B (bitwise the in-kernel split).  MVML_BSPLIT_IL=0: every tile splits B itself.
+BSPLIT_IL = os.environ.get("MVML_BSPLIT_IL", "1") != "0"
+
+
+def split_il4(W, rows, cols, ld, amax_ptr):
+    """W (fp32 [rows][ld]) as its interleaved split-fp16 image (same shape), or None when off,
+    not the f16x2 algorithm, or not 16-B shaped."""
+    if not BSPLIT_IL or GEMM_ALGO != "f16x2" or cols % 4 or ld % 4 or W.data_ptr() % 16:
+        return None
+    img = torch.empty((rows, ld), dtype=torch.float32, device=W.device)
+    call("mvml_split_f16x2_il4", rows, cols, ptr(W), ld, amax_ptr, ptr(img), _stream(W.device))
+    return img
+
+
 def split_planes(W, rows, cols, ld, amax_ptr):
     """W (fp32, [rows][ld]) split once into its two scaled fp16 planes (mvml_split_f16x2) for
     the split-fp16 GEMMs that read it as B: (planes, elements between the planes); (None, 0)
@@ -167,12 +183,13 @@ def split_planes(W, rows, cols, ld, amax_ptr):
 
 
 def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0, algo=None,
-         amax=None, bsplit=None, arows=None):
+         amax=None, bsplit=None, arows=None, bil4=None):
     """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32 / mvml_gemm_f32x3 /
     mvml_gemm_f16x2).  amax = (pointer to |A| max bits, pointer to |B| max bits) from absmax()
     lets split-fp16 products that share an operand share its max pass.  arows (split-fp16,
     K-contiguous A): per-row |A| max bits (int32 [M]) — every A row gets its own scale
-    (mvml_gemm_f16x2_rows); amax then only needs B's pointer."""
+    (mvml_gemm_f16x2_rows); amax then only needs B's pointer.  bil4: B's interleaved split
+    image (split_il4, made with amax[1])."""
     _lib.call_tag[0] = {"flops": 2 * M * N * K, "shape": (M, N, K, int(a_kmajor), int(b_kmajor))}
     L = _lib.lib()
     dev = C.device
@@ -182,8 +199,13 @@ def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.
     if algo == "f16x2" and arows is not None:
         if a_kmajor or amax is None or amax[1] is None:
             raise ValueError("gemm: per-row A maxima need a K-contiguous A and max |B|")
-        call("mvml_gemm_f16x2_rows", M, N, K, ptr(A), lda, ptr(B), ldb, int(b_kmajor), ptr(arows),
-             amax[1], ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
+        call("mvml_gemm_f16x2_rows", M, N, K, ptr(A), lda, ptr(B), ldb, int(b_kmajor), ptr(bil4),
+             ptr(arows), amax[1], ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
+        return
+    if algo == "f16x2" and amax is not None and bil4 is not None:
+        call("mvml_gemm_f16x2_bsplit", int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda, ptr(B), ldb,
+             ptr(bil4), 0, amax[0], amax[1], ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn,
+             _stream(dev))
         return
     if algo == "f16x2" and amax is not None and bsplit is not None:  # B from its pre-split planes
         call("mvml_gemm_f16x2_bsplit", int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda, ptr(B), ldb,
@@ -252,6 +274,7 @@ class GATLayerFunction(torch.autograd.Function):
         ax = None  # (tensor, slot) of max |X|
         xr = None  # per-row max |X| bits (ROW_SCALES)
         wps = (None, 0)
+        wil = None  # Wcat's interleaved split image (BSPLIT_IL)
         if (algo or GEMM_ALGO) == "f16x2":
             amx = torch.zeros(4, dtype=torch.int32, device=dev)  # [X, Wcat, gY (bwd), out]
             if ROW_SCALES and PROJ_ELR_GEMM:
@@ -274,6 +297,7 @@ class GATLayerFunction(torch.autograd.Function):
             absmax(Wcat, C + 2 * H, Fp, Fp, amx, 1)
             # Wcat split once: the projection's tiles and the backward's dL/dX read the planes
             wps = split_planes(Wcat, C + 2 * H, Fp, Fp, slot(amx, 1))
+            wil = split_il4(Wcat, C + 2 * H, Fp, Fp, slot(amx, 1))
         bf16_elr = (algo or GEMM_ALGO) == "bf16" and PROJ_ELR_GEMM
         if (amx is not None or bf16_elr) and PROJ_ELR_GEMM:
             # el / er as 2H more GEMM columns: X [A_l ; A_r]^T with A_l[h] = sum_f attn_l[h, f]
@@ -286,7 +310,7 @@ class GATLayerFunction(torch.autograd.Function):
             Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
             if xr is not None:
                 gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(None, slot(amx, 1)),
-                     arows=xr)
+                     arows=xr, bil4=wil)
             elif amx is not None:
                 gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(slot(*ax), slot(amx, 1)),
                      bsplit=None if wps[0] is None else wps)
@@ -325,6 +349,7 @@ class GATLayerFunction(torch.autograd.Function):
         ctx.amx = amx
         ctx.ax = ax
         ctx.wps = wps
+        ctx.wil = wil
         return out
 
     @staticmethod
@@ -390,7 +415,7 @@ class GATLayerFunction(torch.autograd.Function):
             gX = torch.empty((N, Fin), dtype=torch.float32, device=dev)
             if amx is not None and ROW_SCALES:  # every atom's gradient row at its own scale
                 gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, amax=(None, slot(amx, 1)),
-                     arows=gyr if gyr is not None else absmax_rows(gY, N, CE, ldg))
+                     arows=gyr if gyr is not None else absmax_rows(gY, N, CE, ldg), bil4=ctx.wil)
             else:
                 gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, algo=ctx.algo,
                      amax=None if amx is None else (slot(amx, 2), slot(amx, 1)),
@@ -465,6 +490,9 @@ class Set2SetFunction(torch.autograd.Function):
             # unfused one Wcat's: the same values per element, so the same products)
             wsp = [split_planes(Wperm[l] if CELL_EPI else Wcat[l], 4 * D, kin[l] + D, kin[l] + D,
                                 slot(amax_w, l)) for l in range(Lr)]
+            if wsp[0][0] is None:  # the interleaved image instead (w_plane = 0)
+                wsp = [(split_il4(Wperm[l] if CELL_EPI else Wcat[l], 4 * D, kin[l] + D, kin[l] + D,
+                                  slot(amax_w, l)), 0) for l in range(Lr)]
         for t in range(T):
             for l in range(Lr):
                 w_ih, w_hh, b_ih, b_hh = W[l]
@@ -488,7 +516,9 @@ class Set2SetFunction(torch.autograd.Function):
                 else:
                     gemm(XH[l][t], Wcat[l], B, 4 * D, K, 0, 0, kin[l] + D, kin[l] + D, gates, 4 * D,
                          amax=None if amax_x is None else (slot(amax_x, 0), slot(amax_w, l)),
-                         bsplit=None if CELL_EPI or wsp[l][0] is None else wsp[l], arows=mrows)
+                         bsplit=None if CELL_EPI or wsp[l][0] is None or wsp[l][1] == 0 else wsp[l],
+                         arows=mrows,
+                         bil4=wsp[l][0] if not CELL_EPI and wsp[l][1] == 0 else None)
                 call("mvml_lstm_cell_fwd", B, D, ptr(gates), ptr(b_ih), ptr(b_hh), ptr(c_prev),
                      ptr(cs[t, l]), ptr(own), kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, st)
             call("mvml_set2set_seg_fwd", B, D, ptr(g.node_offsets), ptr(X), ptr(XH[0][t + 1]), 3 * D,
@@ -542,8 +572,12 @@ class Set2SetFunction(torch.autograd.Function):
         amax_x, amax_w = ctx.amax
         amax_g = torch.zeros(Lr, dtype=torch.int32, device=dev) if amax_x is not None else None
         wsb = [None] * Lr  # [W_ih | W_hh] split once for the per-cell data-gradient products
+        wib = [None] * Lr  # ... as the interleaved image (BSPLIT_IL)
         if amax_g is not None and BSPLIT:
             wsb = [split_planes(Wcat[l], 4 * D, Wcat[l].shape[1], Wcat[l].shape[1], slot(amax_w, l))
+                   for l in range(Lr)]
+        elif amax_g is not None:
+            wib = [split_il4(Wcat[l], 4 * D, Wcat[l].shape[1], Wcat[l].shape[1], slot(amax_w, l))
                    for l in range(Lr)]
         for t in range(T - 1, -1, -1):
             # readout segment backward: dL/dq_t = g_qstar_t[:, :D] + segment term -> g_h
@@ -572,7 +606,7 @@ class Set2SetFunction(torch.autograd.Function):
                     # 64-molecule group's gradients, so the cells' rows span little)
                     gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo,
                          amax=None if amax_g is None else (slot(amax_g, l), slot(amax_w, l)),
-                         bsplit=wsb[l])
+                         bsplit=wsb[l], bil4=wib[l])
         # weight / bias gradients, one product per parameter over all steps:
         #   dW_ih[l] = sum_t g_gates[l,t]^T x_l(t),  dW_hh[l] = sum_{t>=1} g_gates[l,t]^T h_l(t-1)
         # (layer 0's input x_0(t) = q*_{t-1} is zero at t = 0; h_l(-1) = 0)
@@ -652,27 +686,29 @@ def linear_maxima(x, w):
         absmax(x, x.shape[0], x.shape[1], x.shape[1], amx, 0)
         kx = (amx, 0)
     absmax(w, w.shape[0], w.shape[1], w.shape[1], amx, 1)
-    return amx, kx, xr
+    return amx, kx, xr, split_il4(w, w.shape[0], w.shape[1], w.shape[1], slot(amx, 1))
 
 
 def linear_fwd(x, weight, y, M, Nout, K, lm, bias=None, act=0):
     """y = act(x W^T + b): the forward product of a Linear (per-row x scales when lm has them)."""
     if lm is not None and lm[2] is not None:
         gemm(x, weight, M, Nout, K, 0, 0, K, K, y, Nout, bias=bias, act=act, amax=(None, slot(lm[0], 1)),
-             arows=lm[2])
+             arows=lm[2], bil4=lm[3])
     else:
         gemm(x, weight, M, Nout, K, 0, 0, K, K, y, Nout, bias=bias, act=act,
-             amax=None if lm is None else (slot(*lm[1]), slot(lm[0], 1)))
+             amax=None if lm is None else (slot(*lm[1]), slot(lm[0], 1)),
+             bil4=None if lm is None else lm[3])
 
 
 def linear_dx(g, weight, gx, M, Nout, K, lm):
     """gx = g W (the data gradient of a Linear; per-row g scales under ROW_SCALES)."""
     if lm is not None and lm[2] is not None:
         gemm(g, weight, M, K, Nout, 0, 1, Nout, K, gx, K, amax=(None, slot(lm[0], 1)),
-             arows=absmax_rows(g, M, Nout, Nout))
+             arows=absmax_rows(g, M, Nout, Nout), bil4=lm[3])
     else:
         gemm(g, weight, M, K, Nout, 0, 1, Nout, K, gx, K,
-             amax=None if lm is None else (slot(lm[0], 2), slot(lm[0], 1)))
+             amax=None if lm is None else (slot(lm[0], 2), slot(lm[0], 1)),
+             bil4=None if lm is None else lm[3])
 
 
 class LinearReLUFunction(torch.autograd.Function):

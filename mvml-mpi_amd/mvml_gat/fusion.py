@@ -117,7 +117,8 @@ class FusionAttnConvFunction(torch.autograd.Function):
                 bmx = torch.zeros(1, dtype=torch.int32, device=dev)
                 absmax(Bcat, D, 2 * HD, 2 * HD, bmx, 0)
                 gemm(Xn, Bcat, 3 * B, 2 * HD, D, 0, 1, D, 2 * HD, PV, 2 * HD, amax=(None, slot(bmx, 0)),
-                     arows=_F.absmax_rows(Xn, 3 * B, D, D))
+                     arows=_F.absmax_rows(Xn, 3 * B, D, D),
+                     bil4=_F.split_il4(Bcat, D, 2 * HD, 2 * HD, slot(bmx, 0)))
             else:
                 gemm(Xn, Bcat, 3 * B, 2 * HD, D, 0, 1, D, 2 * HD, PV, 2 * HD)
             if fused:
@@ -187,6 +188,7 @@ class FusionAttnConvFunction(torch.autograd.Function):
                 if _F.DEBUG_CAPTURE is not None:
                     _F.DEBUG_CAPTURE["gpv_amax"] = (gPV.clone(), amx[0:1].clone())
                 absmax(Bcat, D, 2 * HD, 2 * HD, amx, 2)
+                bil = _F.split_il4(Bcat, D, 2 * HD, 2 * HD, slot(amx, 2))
             G2 = torch.empty((2 * HD, D), **f32)  # [h D + j][i] = dL/dM_h[i][j]; then dL/dW_v
             gemm(gPV, Xn, 2 * HD, D, 3 * B, 1, 1, 2 * HD, D, G2, D,
                  amax=None if amx is None else (slot(amx, 0), slot(amx, 1)))
@@ -198,7 +200,7 @@ class FusionAttnConvFunction(torch.autograd.Function):
             gemm_batched(wq3, G2, D, D, D, 0, 0, D, D, gWk, D, H, D * D, D * D, D * D)
             if amx is not None and _F.ROW_SCALES:  # every token row's gradient at its own scale
                 gemm(gPV, Bcat, 3 * B, D, 2 * HD, 0, 0, 2 * HD, 2 * HD, gXn, D, beta=1.0,
-                     amax=(None, slot(amx, 2)), arows=gpr)
+                     amax=(None, slot(amx, 2)), arows=gpr, bil4=bil)
             else:
                 gemm(gPV, Bcat, 3 * B, D, 2 * HD, 0, 0, 2 * HD, 2 * HD, gXn, D, beta=1.0,
                      amax=None if amx is None else (slot(amx, 0), slot(amx, 2)))

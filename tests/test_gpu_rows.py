@@ -246,3 +246,59 @@ def test_saturated_logits_per_molecule_gradients():
     assert rec["rows_checked"] >= B // 2
     assert rec["rows"]["emb_grad_per_row_over_budget"] == 0, rec["rows"]
     assert rec["rows"]["params_worst_ratio"] < 1.0, rec["rows"]
+
+
+@pytest.mark.parametrize("rows", [True, False])
+@pytest.mark.parametrize("bk", [0, 1])
+def test_gemm_f16x2_il4_bitwise(rows, bk):
+    """B pre-split once as the interleaved-by-4 image (mvml_split_f16x2_il4) gives bitwise the
+    products of the tiles that split B themselves (per-row and operand-wide A scales, B
+    K-contiguous and K-major; the planner's tile and the forced 256 tile)."""
+    from mvml_gat._lib import option
+    from mvml_gat.functional import absmax, absmax_rows, gemm, slot, split_il4
+    g = torch.Generator().manual_seed(17 + bk)
+    M, N, K = 2000, 448, 768
+    A = (torch.randn(M, K, generator=g) * torch.pow(2.0, torch.randint(-20, 6, (M, 1), generator=g).float())).to(DEV)
+    Bt = torch.randn(N, K, generator=g).to(DEV)
+    Bd = Bt.t().contiguous() if bk else Bt
+    ldb = N if bk else K
+    mx = torch.zeros(2, dtype=torch.int32, device=DEV)
+    absmax(A, M, K, K, mx, 0)
+    absmax(Bd, Bd.shape[0], Bd.shape[1], Bd.shape[1], mx, 1)
+    img = split_il4(Bd, Bd.shape[0], Bd.shape[1], Bd.shape[1], slot(mx, 1))
+    assert img is not None
+    ar = absmax_rows(A, M, K, K) if rows else None
+    for tile in (0, 256):
+        with option("gemm_tile", tile):
+            C0 = torch.empty(M, N, device=DEV)
+            C1 = torch.empty(M, N, device=DEV)
+            am = (None if rows else slot(mx, 0), slot(mx, 1))
+            gemm(A, Bd, M, N, K, 0, bk, K, ldb, C0, N, amax=am, arows=ar)
+            gemm(A, Bd, M, N, K, 0, bk, K, ldb, C1, N, amax=am, arows=ar, bil4=img)
+            assert torch.equal(C0, C1), (tile, (C0 - C1).abs().max().item())
+
+
+def test_gnn_module_il4_bitwise(monkeypatch):
+    """The whole view's forward and every gradient are bitwise the same with the weights'
+    interleaved pre-split (BSPLIT_IL, default) and with the in-kernel split."""
+    import mvml_gat
+    from mvml_gat import functional as Fn
+    sb = _config3_batch(4 * 64, seed=5)
+    torch.manual_seed(3)
+    model = mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3).to(DEV).eval()
+    fus = mvml_gat.MVFusion(384, 12, 11, 0.5).to(DEV).eval()
+    g = sb.to_graph(group_size=64).to(DEV)
+    gen = torch.Generator(device=DEV).manual_seed(1)
+    sx, fx = torch.randn(sb.batch_size, 384, device=DEV, generator=gen), torch.randn(sb.batch_size, 384, device=DEV, generator=gen)
+    y = (torch.rand(sb.batch_size, 11, device=DEV, generator=gen) > 0.8).float()
+    res = []
+    for il in (True, False):
+        monkeypatch.setattr(Fn, "BSPLIT_IL", il)
+        model.zero_grad(set_to_none=True)
+        fus.zero_grad(set_to_none=True)
+        z = fus(sx, model(g, g.ndata["h"]), fx)
+        mvml_gat.bce_with_logits(z, y).backward()
+        res.append([z.detach().clone()] + [p.grad.clone() for p in list(model.parameters()) + list(fus.parameters())
+                                           if p.grad is not None])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
