@@ -61,17 +61,21 @@ def main():
         flops = 2 * M * N * K
         cols = []
         for algo in algos:
-            if algo.startswith("f16x2r"):  # per-row A maxima (mvml_gemm_f16x2_rows)
+            if algo.startswith(("f16x2r", "f16x2i")):  # per-row A maxima (r) / B il4 image (i)
+                rws, il = algo.startswith(("f16x2r", "f16x2ri")), "i" in algo.split("-")[0][5:]
                 if ak:
                     cols.append(f"{algo}      n/a")
                     continue
-                from mvml_gat.functional import absmax, absmax_rows, slot
-                bmx = torch.zeros(1, dtype=torch.int32, device=dev)
-                absmax(Bm, Bm.shape[0], Bm.shape[1], Bm.shape[1], bmx, 0)
-                rows = absmax_rows(A, M, K, K)
+                from mvml_gat.functional import absmax, absmax_rows, slot, split_il4
+                mx = torch.zeros(2, dtype=torch.int32, device=dev)
+                absmax(A, M, K, K, mx, 0)
+                absmax(Bm, Bm.shape[0], Bm.shape[1], Bm.shape[1], mx, 1)
+                rows = absmax_rows(A, M, K, K) if rws else None
+                img = split_il4(Bm, Bm.shape[0], Bm.shape[1], Bm.shape[1], slot(mx, 1)) if il else None
                 with option("gemm_tile", int(algo.split("-")[1]) if "-" in algo else 0):
                     ms, t = tf(lambda: gemm(A, Bm, M, N, K, 0, bk, K, N if bk else K, C, N,
-                                            amax=(None, slot(bmx, 0)), arows=rows), flops)
+                                            amax=(None if rws else slot(mx, 0), slot(mx, 1)), arows=rows,
+                                            bil4=img), flops)
             elif algo == "torch":
                 At = A.t() if ak else A
                 Bt = Bm if bk else Bm.t()
