@@ -6,10 +6,10 @@ tests cover that decomposition on the CPU oracle; here two child processes (rank
 on cuda:0, gloo over the device tensors — RCCL refuses two ranks on one device) run the HIP
 GNNModule + MVFusion on their shards, FlatGradAllReduce sums the gradients and
 EmbeddingAllGather assembles the embeddings.  Rank 0 then runs the whole batch in one process
-and checks: reduced gradients within 1e-5 of the single-process ones (norm-wise, relative to
-the larger of the result and the ranks' partial gradients: the all-reduce re-associates each
-sum, and sums that cancel, e.g. the Set2Set LSTM bias gradients, keep that error relative to
-their terms, not to the small result), the gathered embeddings
+and checks: reduced gradients within max(1e-5, 4 x the difference re-ordering the same batch
+makes) of the single-process ones — the all-reduce re-associates each sum, and sums that cancel
+(layer 2's bias under GraphNorm's mean-free gradient: 3.7e-5) keep that error relative to their
+terms, not to the small result — the gathered embeddings
 BITWISE equal (per-row split-fp16 scales: a molecule's embedding does not depend on its batch),
 and a second step reusing the reducer's cached presence flags.
 """
@@ -52,26 +52,19 @@ _CHILD = textwrap.dedent(r"""
         f = mvml_gat.MVFusion(384, 12, 11, 0.5).to(dev).eval()
         return m, f, list(m.parameters()) + list(f.parameters())
 
-    def step(m, f, a, b, red):
-        sb = gset.molecules(a, b)
+    def step(m, f, a, b, red, sb=None, idx=None):
+        sb = gset.molecules(a, b) if sb is None else sb
+        idx = torch.arange(a, b, device=dev) if idx is None else idx
         g = sb.to_graph(group_size=gs).to(dev)
         emb = m(g, g.ndata["h"])
         # this rank's share of the global mean BCE: the ranks' losses sum to the whole batch's
-        loss = mvml_gat.bce_with_logits(f(sx[a:b], emb, fx[a:b]), y[a:b]) * ((b - a) / total)
+        loss = mvml_gat.bce_with_logits(f(sx[idx], emb, fx[idx]), y[idx]) * (len(idx) / total)
         loss.backward()
         if red is not None:
-            # the largest |partial| each rank contributes to every summed tensor: the scale the
-            # all-reduce's re-association error is measured against (cancelling sums such as
-            # the LSTM bias gradients lose digits relative to the result, not to their terms)
-            loc = torch.stack([p.grad.abs().max() if p.grad is not None else torch.zeros((), device=dev)
-                               for p in params])
-            dist.all_reduce(loc, op=dist.ReduceOp.MAX)
-            part_max.append(loc)
             red()
         return emb.detach()
 
     m, f, params = models()
-    part_max = []
     red = FlatGradAllReduce(params, average=False)
     emb = step(m, f, lo, hi, red)
     full = EmbeddingAllGather()(emb.contiguous())
@@ -86,18 +79,26 @@ _CHILD = textwrap.dedent(r"""
     if rank == 0:
         m1, f1, p1 = models()
         emb1 = step(m1, f1, 0, total, None)
+        # the same whole batch with rank 1's groups first: how far re-ordering the very same
+        # sums moves each gradient (cancelling sums, e.g. the bias of the mean-mode GAT layer
+        # under GraphNorm's mean-free gradient, keep only a few digits of their terms)
+        m2, f2, p2 = models()
+        perm = synth.concat_batches([gset.molecules(hi, total), gset.molecules(0, hi)])
+        step(m2, f2, 0, total, None, sb=perm,
+             idx=torch.cat([torch.arange(hi, total), torch.arange(0, hi)]).to(dev))
         def rel(a, b):
             return ((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30)).item()
         out["emb_bitwise"] = bool(torch.equal(full, emb1))
         out["emb_max_diff"] = float((full - emb1).abs().max())
         assert all((a is None) == (p.grad is None) for a, p in zip(grads, p1))
         names = [n for n, _ in m1.named_parameters()] + ["fusion." + n for n, _ in f1.named_parameters()]
-        errs = [(((a.double() - p.grad.double()).abs().max()
-                  / max(float(part_max[0][i]), float(p.grad.abs().max()), 1e-30)).item(),
-                 rel(a, p.grad), names[i]) for i, (a, p) in enumerate(zip(grads, p1)) if a is not None]
+        # per tensor: the DP error against max(1e-5, 4 x the re-ordering noise)
+        errs = [(rel(a, p.grad) / max(1e-5, 4 * rel(q.grad, p.grad)), rel(a, p.grad),
+                 rel(q.grad, p.grad), names[i])
+                for i, (a, p, q) in enumerate(zip(grads, p1, p2)) if a is not None]
         worst = max(errs)
-        out["grad_rel"], out["grad_rel_result"], out["grad_worst"] = worst
-        out["grad_rel_result_max"] = max(e[1] for e in errs)
+        out["grad_ratio"], out["grad_rel"], out["grad_reorder_rel"], out["grad_worst"] = worst
+        out["grad_rel_max"] = max(e[1] for e in errs)
         out["grad2_equal"] = all((a is None and b is None) or torch.equal(a, b) for a, b in zip(grads, grads2))
         out["grads_none"] = sum(a is None for a in grads)
         out["flags_cached"] = len(red._present)
@@ -144,5 +145,5 @@ def test_two_hip_ranks_match_single_process():
     assert r0["shard"][1] == r1["shard"][0] and r0["shard"][0] == 0 and r1["shard"][1] == 384
     assert 0 < r0["shard"][1] < 384  # both ranks hold molecules
     assert r0["emb_bitwise"], r0
-    assert r0["grad_rel"] < 1e-5, r0
+    assert r0["grad_ratio"] < 1, r0
     assert r0["grad2_equal"] and r0["flags_cached"] == 1, r0
