@@ -17,8 +17,17 @@ from collections import defaultdict
 
 
 def short(name):
-    name = re.sub(r"\(.*$", "", name)  # drop the argument list
-    return name[:110]
+    name = name.replace("(anonymous namespace)::", "").replace("mvml::", "").replace("void ", "")
+    depth, cut = 0, len(name)
+    for i, ch in enumerate(name):  # drop the argument list: the first '(' outside <...>
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            cut = i
+            break
+    return name[:cut][:120]
 
 
 def main():
@@ -27,6 +36,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20, help="divide totals by this many steps")
     ap.add_argument("--match", default="")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--bucket", action="store_true", help="round grids to 2 significant digits")
     a = ap.parse_args()
     files = glob.glob(os.path.join(a.trace, "**", "*kernel_trace.csv"), recursive=True) \
         if os.path.isdir(a.trace) else [a.trace]
@@ -41,6 +51,8 @@ def main():
                 if a.match and a.match not in nm:
                     continue
                 grid = tuple(int(r.get(f"Grid_Size_{c}", 0) or 0) for c in "XYZ")
+                if a.bucket:  # batches of different sizes: bucket the grid to 2 significant digits
+                    grid = tuple(int(float(f"{g:.2g}")) for g in grid)
                 wg = tuple(int(r.get(f"Workgroup_Size_{c}", 0) or 0) for c in "XYZ")
                 key = (short(nm), grid, wg, r.get("LDS_Block_Size", r.get("Group_Segment_Size", "")))
                 tot[key] += d
