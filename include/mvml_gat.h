@@ -179,6 +179,31 @@ int mvml_gemm_f16x2_rows(int64_t M, int64_t N, int64_t K, const float* A, int64_
                          const uint32_t* amax_a_rows, const uint32_t* amax_b, const float* bias,
                          float beta, int act, float* C, int64_t ldc, void* workspace,
                          size_t workspace_bytes, void* stream);
+/* mvml_gemm_f16x2_rows (no beta, no split-K: K is a feature dimension; the 256x256 tile at any
+ * size) with a strided batch and epilogue extras, for the re-associated first GAT layer:
+ *  - product z < batch reads A + z stride_a, B (or b_il4) + z stride_b, amax_a_rows + z
+ *    stride_rows, bias + z stride_bias and writes C + z stride_c;
+ *  - act: 0 none, 1 ReLU, 2 ELU after the bias (x > 0 ? x : expm1(x)), 3 the ELU backward
+ *    through the layer output aux (ld_aux): v *= aux > 0 ? 1 : aux + 1;
+ *  - c_amax (may be NULL): atomicMax of the bits of max |stored value|;
+ *  - c_rows (may be NULL): per-row |max| bits of the stored values, row r of column slot
+ *    col / c_rows_cols (c_rows_cols = 0: one slot) at c_rows[z stride_c_rows + slot
+ *    c_rows_stride + r], by atomicMax (the caller zeroes it; c_rows_cols % 64 == 0).
+ * A, B rows and strides 16-B aligned, K % 4 == 0. */
+int mvml_gemm_f16x2_ex(int64_t M, int64_t N, int64_t K, int64_t batch, const float* A, int64_t lda,
+                       int64_t stride_a, const float* B, int64_t ldb, int b_kmajor,
+                       const float* b_il4, int64_t stride_b, const uint32_t* amax_a_rows,
+                       int64_t stride_rows, const uint32_t* amax_b, const float* bias,
+                       int64_t stride_bias, int act, float* C, int64_t ldc, int64_t stride_c,
+                       const float* aux, int64_t ld_aux, uint32_t* c_amax, uint32_t* c_rows,
+                       int64_t c_rows_stride, int c_rows_cols, int64_t stride_c_rows, void* stream);
+/* Strided-batch split-fp16 GEMM (batch >= 2, no split-K) with operand-wide maxima shared by all
+ * products: C + z stride_c = (A + z stride_a)(B + z stride_b), layouts as mvml_gemm_f32. */
+int mvml_gemm_f16x2_batched(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                            int64_t batch, const float* A, int64_t lda, int64_t stride_a,
+                            const float* B, int64_t ldb, int64_t stride_b, const uint32_t* amax_a,
+                            const uint32_t* amax_b, float* C, int64_t ldc, int64_t stride_c,
+                            void* stream);
 /* B pre-split once as an interleaved-by-4 image for the split-fp16 GEMMs: every 4 consecutive
  * values of a row become [4 scaled high fp16 | 4 low fp16] (16 B, the scale from *amax as the
  * GEMM's own split), written to out with P's own [rows][ld] float indexing, so the image stands
@@ -314,6 +339,34 @@ int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_
                      const float* g_out, int H, int F, float slope, int mode, float* gY,
                      int64_t ldgy, uint32_t* gy_amax, uint32_t* gy_row_amax, void* workspace,
                      size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * The first GATConv (model.py:81, 74 features -> 4 x 192, flatten + ELU) re-associated: the
+ * same GATConv.forward sums in another order,
+ *   rst[v, h] = (sum_e a_e,h X[src_e]) W_h^T + X[v] Wres_h^T + b_h,
+ * so the aggregation runs over the Fp-wide feature rows and no N x (2 H F) projection is formed.
+ * mvml_gat_x_fwd: el / er = X A_l^T, X A_r^T (Alr = [A_l ; A_r] = Wcat's last 2H rows, 2H x Fp)
+ * into elr [N][2H]; the edge softmax (order and arithmetic of mvml_gat_agg_fwd's) into attn
+ * [E][H] (in-CSR slots); axc [N][H][2 Fp] = per head [AX_h | X] with AX_h[v] = sum_e a_e,h
+ * X[src_e]; arows [H][N] = per-row |max| bits of each head block.  The layer output is then
+ * mvml_gemm_f16x2_ex over the H blocks (K = 2 Fp, B = mvml_gat_x_pack_weights' [W_h | Wres_h],
+ * bias + ELU in the epilogue).  H in {1, 2, 4, 8}; Fp % 4 == 0, Fp <= 128 (mvml_gat_x_supported).
+ * mvml_gat_x_bwd, from dax [N][H][Fp] = g_rst_h W_h (g_rst = dL/d rst): g_a_e = <dax_h[dst],
+ * X[src]>, the edge-softmax and LeakyReLU backward (gpre [E][H] = dL/ds_e, in-CSR slots), d er
+ * (in-edges) and d el (out-CSR gather) into gelr [N][2H]; gelr_amax (may be NULL) folds max
+ * |gelr| in by atomicMax.  mvml_gat_elu_bwd: g_rst = g_out ELU'(out) (n floats) with max |g_rst|
+ * folded into *amax. */
+int mvml_gat_x_supported(int H, int Fp);
+int mvml_gat_x_pack_weights(const float* Wcat, int H, int F, int Fp, float* Wb, void* stream);
+int mvml_gat_x_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src, const float* X,
+                   int Fp, const float* Alr, int H, float slope, float* elr, float* attn, float* axc,
+                   uint32_t* arows, void* stream);
+int mvml_gat_x_bwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
+                   const int32_t* out_rowptr, const int32_t* out_inslot, const float* X, int Fp,
+                   const float* elr, const float* attn, int H, float slope, const float* dax,
+                   float* gpre, float* gelr, uint32_t* gelr_amax, void* stream);
+int mvml_gat_elu_bwd(int64_t n, const float* g_out, const float* out, float* g_rst, uint32_t* amax,
+                     void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Set2Set (dgl 0.9.1, model.py:82-84, 92) building blocks.

@@ -384,6 +384,28 @@ struct ProjEpi {
   float* part;       // [cols / W][2][M]: a wave's stores for one (group, side) are 32 rows, contiguous
 };
 
+// Extra epilogue work of the 256x256 split-fp16 tile (mvml_gemm_f16x2_ex):
+//  * act 2: ELU (dgllife GATLayer's flatten activation, x > 0 ? x : expm1(x)) after the bias;
+//    act 3: the ELU backward with the layer output as aux, v *= aux > 0 ? 1 : aux + 1 (torch's
+//    elu_backward on the result) — the layer-2 data gradient leaves as layer 1's g_rst;
+//  * c_amax: unsigned atomicMax of max |stored value| bits (one slot per product);
+//  * c_rows: per-row |max| bits of the stored values, slot (column / rows_cols) of row r at
+//    c_rows[slot * rows_stride + r] (rows_cols = 0: one slot per row), atomicMax so that column
+//    tiles and batch products fold into the same word (host: rows_cols % 64 == 0);
+//  * strided batch: product z adds z * bias_z to bias, z * rows_z to the per-row A maxima and
+//    z * crows_z to c_rows.
+struct EpiX {
+  const float* aux = nullptr;
+  int64_t ld_aux = 0;
+  uint32_t* c_amax = nullptr;
+  uint32_t* c_rows = nullptr;
+  int64_t rows_stride = 0;
+  int rows_cols = 0;
+  int64_t bias_z = 0, rows_z = 0, crows_z = 0;
+};
+__device__ __forceinline__ float elu_epi(float x) { return x > 0.f ? x : expm1f(x); }
+__device__ __forceinline__ float elu_grad_epi(float o) { return o > 0.f ? 1.f : o + 1.f; }
+
 // Epilogue of a wave's FM x FN 32x32 accumulators (rows r0 + 32 i .., columns c0 + 32 j ..):
 // optional GAT logit partials, then bias / beta*C / ReLU, or the raw split-K slab.
 template <int EPI_LOGW, int FM = 2, int FN = 2, bool STORE_C = true>
@@ -468,7 +490,7 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
                                              const float* __restrict__ bias, float beta, int act,
                                              float* __restrict__ C, int64_t ldc,
                                              float* __restrict__ slab, const CellEpi& cep = CellEpi{},
-                                             const int* rs = nullptr);
+                                             const int* rs = nullptr, const EpiX& ex = EpiX{});
 
 // Undo the split-fp16 operand scales of a 128x128 tile's 2 x 2 accumulators (exact: powers of
 // two).  Per-row A maxima: lane li scaled A rows 32 i + li of its wave's 64 (shift ka0 / ka1);
@@ -1128,7 +1150,7 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
                                                  const float* __restrict__ bias, float beta, int act,
                                                  float* __restrict__ C, int64_t ldc,
                                                  float* __restrict__ slab, const CellEpi& cep,
-                                                 const int* rs) {
+                                                 const int* rs, const EpiX& ex) {
   // rs (per-row A maxima): rs[32 i + rr] = the scale shift of row r0 + 32 i + rr, undone here as
   // each row leaves (acc already carries B's)
   const int li = lane & 31, lk = lane >> 5;
@@ -1140,6 +1162,39 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
   // instead of seven dword stores per unit — the cell epilogue was store-issue-bound.  Same
   // arithmetic per unit, so bitwise the per-unit path's results (kept for unaligned operands).
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  // EpiX work (act 2 / 3, folded maxima): its own store path, never with split-K or the cell
+  const bool extra = !slab && cep.D == 0 && (act >= 2 || ex.c_amax || ex.c_rows);
+  const bool fold_rows = extra && ex.c_rows;
+  float am = 0.f;  // |max| of this lane's stored values (c_amax)
+  auto store4x = [&](const float* src, int64_t row, int64_t col, int shift) -> float {
+    float e[4];
+    const float4 t = *reinterpret_cast<const float4*>(src);
+    e[0] = t.x; e[1] = t.y; e[2] = t.z; e[3] = t.w;
+    const float ua = rs ? pow2f(-shift) : 1.f;
+    float* cp = out + row * ld + col;
+    const float* ap = act == 3 ? ex.aux + row * ex.ld_aux + col : nullptr;
+    float m = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (col + u >= N) break;
+      float x = e[u] * ua;
+      if (bias) x += bias[col + u];
+      if (beta != 0.f) x += beta * cp[u];
+      if (act == 1) x = fmaxf(x, 0.f);
+      if (act == 2) x = elu_epi(x);
+      if (act == 3) x *= elu_grad_epi(ap[u]);
+      e[u] = x;
+      m = fmaxf(m, fabsf(x));
+    }
+    if (vec && col + 3 < N) {
+      *reinterpret_cast<float4*>(cp) = make_float4(e[0], e[1], e[2], e[3]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (col + u < N) cp[u] = e[u];
+    }
+    return m;
+  };
   const bool cell4 = cep.D > 0 && cep.D % 4 == 0 && al16(cep.b_ih) && al16(cep.b_hh) &&
                      al16(cep.c_prev) && al16(cep.c_out) && al16(cep.h_out) && al16(cep.h_out2) &&
                      al16(cep.act) && cep.ldh % 4 == 0 && cep.ldh2 % 4 == 0 && al16(cep.gx) &&
@@ -1211,7 +1266,24 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
     for (int q = 0; q < 8; ++q) {
       const int idx = q * 64 + lane, rr = idx >> 4, c4 = (idx & 15) * 4;
       const int64_t row = r0 + 32 * i + rr, col = c0 + c4;
+      if (fold_rows) {  // (uniform) the row's 16 lanes reduce together: no early exit
+        float rm = 0.f;
+        if (row < M && col < N) rm = store4x(wl + rr * kEpiLd + c4, row, col, rs ? rs[32 * i + rr] : 0);
+        am = fmaxf(am, rm);
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) rm = fmaxf(rm, __shfl_xor(rm, o, 64));
+        if ((lane & 15) == 0 && row < M) {
+          const int64_t slot = ex.rows_cols > 0 ? c0 / ex.rows_cols : 0;
+          atomicMax(ex.c_rows + blockIdx.z * ex.crows_z + slot * ex.rows_stride + row,
+                    __float_as_uint(rm));
+        }
+        continue;
+      }
       if (row >= M || col >= N) continue;
+      if (extra) {
+        am = fmaxf(am, store4x(wl + rr * kEpiLd + c4, row, col, rs ? rs[32 * i + rr] : 0));
+        continue;
+      }
       float4 v = *reinterpret_cast<const float4*>(wl + rr * kEpiLd + c4);
       if (rs) {
         const float ua = pow2f(-rs[32 * i + rr]);
@@ -1274,6 +1346,10 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
       }
     }
   }
+  if (extra && ex.c_amax) {  // (uniform) one atomic per wave
+    am = wave_max(am);
+    if (lane == 0) atomicMax(ex.c_amax, __float_as_uint(am));
+  }
 }
 
 #ifndef MVML_X3W_WAVES
@@ -1323,11 +1399,13 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
                 float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
                 float* __restrict__ slab, int a_vec, int b_vec, ProjEpi epi = ProjEpi{},
                 BatchStrides bst = BatchStrides{}, CellEpi cep = CellEpi{},
-                AmaxPtrs amax = AmaxPtrs{}, DualPtrs dual = DualPtrs{}) {
+                AmaxPtrs amax = AmaxPtrs{}, DualPtrs dual = DualPtrs{}, EpiX ex = EpiX{}) {
   if (blockIdx.z) {  // strided batch
     A += blockIdx.z * bst.a;
     B += blockIdx.z * bst.b;
     C += blockIdx.z * bst.c;
+    if (bias) bias += blockIdx.z * ex.bias_z;
+    if (amax.a_rows) amax.a_rows += blockIdx.z * ex.rows_z;
   }
   if (blockIdx.z == 1 && dual.a) {  // the second product of a dual launch
     A = dual.a;
@@ -1759,7 +1837,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
                                          act, C, ldc, slab, epi);
   epilogue_lds(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
                    n0 + wn * 64, lane, bias, beta, act, C, ldc, slab, cep,
-                   (ROWS && ntiles > 0) ? rsh + wm * 128 : nullptr);
+                   (ROWS && ntiles > 0) ? rsh + wm * 128 : nullptr, ex);
 #else
   static_assert(NP != 2, "per-row A maxima need the LDS epilogue");
   tile_epilogue<EPI_LOGW, 4, 2>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta, act, C,
@@ -2398,6 +2476,73 @@ extern "C" int mvml_gemm_f16x2_rows(int64_t M, int64_t N, int64_t K, const float
   return gemm_launch(kPrecF16x2, 0, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc,
                      workspace, workspace_bytes, stream, 1, BatchStrides{}, am,
                      reinterpret_cast<const uint16_t*>(b_il4));
+}
+
+extern "C" int mvml_gemm_f16x2_ex(int64_t M, int64_t N, int64_t K, int64_t batch, const float* A,
+                                  int64_t lda, int64_t stride_a, const float* B, int64_t ldb,
+                                  int b_kmajor, const float* b_il4, int64_t stride_b,
+                                  const uint32_t* amax_a_rows, int64_t stride_rows,
+                                  const uint32_t* amax_b, const float* bias, int64_t stride_bias,
+                                  int act, float* C, int64_t ldc, int64_t stride_c, const float* aux,
+                                  int64_t ld_aux, uint32_t* c_amax, uint32_t* c_rows,
+                                  int64_t c_rows_stride, int c_rows_cols, int64_t stride_c_rows,
+                                  void* stream) {
+  clear_error();
+  MVML_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1 && batch <= 65535, "gemm_f16x2_ex: bad shape");
+  MVML_REQUIRE(amax_a_rows && amax_b, "gemm_f16x2_ex: amax_a_rows / amax_b are required");
+  MVML_REQUIRE(act >= 0 && act <= 3 && (act != 3 || (aux && ld_aux >= N)), "gemm_f16x2_ex: bad act / aux");
+  MVML_REQUIRE(c_rows_cols >= 0 && c_rows_cols % 64 == 0 && (!c_rows || c_rows_stride >= 0),
+               "gemm_f16x2_ex: c_rows_cols must be a multiple of 64");
+  MVML_REQUIRE(lda >= K && ldc >= N && (b_kmajor ? ldb >= N : ldb >= K), "gemm_f16x2_ex: bad leading dims");
+  MVML_REQUIRE(stride_a >= 0 && stride_b >= 0 && stride_c >= 0 && stride_bias >= 0 && stride_rows >= 0 &&
+                   stride_c_rows >= 0, "gemm_f16x2_ex: negative stride");
+  if (M == 0 || N == 0) return MVML_OK;
+  const float* Bp = b_il4 ? b_il4 : B;
+  const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0) && stride_a % 4 == 0;
+  const int bv = (ldb % 4 == 0) && ((uintptr_t)Bp % 16 == 0) && stride_b % 4 == 0;
+  // the 256x256 tile at any size (K is a feature dimension here: no split-K)
+  MVML_REQUIRE(x3w_fast(false, b_kmajor != 0, M, N, K, av, bv),
+               "gemm_f16x2_ex: needs 16-B aligned rows and strides and K %% 4 == 0");
+  const int64_t tiles = ceil_div(M, XBM) * ceil_div(N, XBN);
+  MVML_REQUIRE(tiles < (int64_t(1) << 31), "gemm_f16x2_ex: too many tiles");
+  const dim3 grid(x3w_grid_x(tiles, 1), 1, (unsigned)batch);
+  const BatchStrides bst{stride_a, stride_b, stride_c};
+  AmaxPtrs am;
+  am.b = amax_b;
+  am.a_rows = amax_a_rows;
+  EpiX ex;
+  ex.aux = aux; ex.ld_aux = ld_aux; ex.c_amax = c_amax; ex.c_rows = c_rows;
+  ex.rows_stride = c_rows_stride; ex.rows_cols = c_rows_cols;
+  ex.bias_z = stride_bias; ex.rows_z = stride_rows; ex.crows_z = stride_c_rows;
+  hipStream_t st = as_stream(stream);
+  const int64_t kc = K > 0 ? K : 1;
+#define MVML_X3W_EX(BKV, BPSV)                                                                    \
+  gemm_x3w_kernel<false, BKV, -1, true, 2, BPSV, true><<<grid, kXThreads, 0, st>>>(               \
+      M, N, K, A, lda, Bp, ldb, bias, 0.f, act, C, ldc, kc, nullptr, av, bv, ProjEpi{}, bst,       \
+      CellEpi{}, am, DualPtrs{}, ex)
+  if (b_kmajor) {
+    if (b_il4) MVML_X3W_EX(true, 2);
+    else MVML_X3W_EX(true, 0);
+  } else {
+    if (b_il4) MVML_X3W_EX(false, 2);
+    else MVML_X3W_EX(false, 0);
+  }
+#undef MVML_X3W_EX
+  return check_launch("gemm_x3w_kernel(ex)");
+}
+
+extern "C" int mvml_gemm_f16x2_batched(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                                       int64_t batch, const float* A, int64_t lda, int64_t stride_a,
+                                       const float* B, int64_t ldb, int64_t stride_b,
+                                       const uint32_t* amax_a, const uint32_t* amax_b, float* C,
+                                       int64_t ldc, int64_t stride_c, void* stream) {
+  clear_error();
+  MVML_REQUIRE(batch >= 2 && batch <= 65535 && stride_a >= 0 && stride_b >= 0 && stride_c >= 0,
+               "gemm_f16x2_batched: bad batch / strides");
+  MVML_REQUIRE(amax_a && amax_b, "gemm_f16x2_batched: amax_a / amax_b are required");
+  return gemm_launch(kPrecF16x2, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc,
+                     nullptr, 0, stream, batch, BatchStrides{stride_a, stride_b, stride_c},
+                     AmaxPtrs{amax_a, amax_b});
 }
 
 extern "C" int mvml_split_f16x2_il4(int64_t rows, int64_t cols, const float* P, int64_t ld,

@@ -237,6 +237,40 @@ def colsum(X, M, N, ldx, out, beta=0.0, offset=0, alpha=1.0):
     call("mvml_colsum_f32", M, N, xp, ldx, float(alpha), float(beta), ptr(out), wp, wn, _stream(dev))
 
 
+# The first GATConv (narrow input: Fp = 76 features, flatten heads) re-associated: the edge
+# softmax and aggregation run over the feature rows and one batched GEMM per head forms the
+# output (mvml_gat_x_fwd + mvml_gemm_f16x2_ex, see csrc/gat_x.hip) instead of projecting every
+# atom to 2 H F + 2 H columns and aggregating those.  MVML_GAT_REASSOC=0: the projection path.
+REASSOC_X = os.environ.get("MVML_GAT_REASSOC", "1") != "0"
+
+
+class EluLink:
+    """Fused ELU backward between two GAT layers of one GAT stack (mvml_gat.nn.GAT): the
+    flatten + ELU layer's output records a link; the next layer's forward claims it, and its
+    data-gradient GEMM then multiplies by ELU'(out) in its epilogue (act 3) and folds max |g|,
+    so the first layer receives g_rst itself (no g_out * ELU' pass over N x H F).  The first
+    layer's backward checks that the gradient it receives IS the one the claiming layer wrote."""
+
+    __slots__ = ("claimed", "g_rst", "amax")
+
+    def __init__(self, dev):
+        self.claimed = False
+        self.g_rst = None
+        self.amax = torch.zeros(1, dtype=torch.int32, device=dev)
+
+
+# set by mvml_gat.nn.GAT.forward around its layer loop: links are made and claimed only there,
+# where a flatten + ELU layer's output feeds exactly the next layer
+ELU_LINK = [False]
+
+
+def _elu_link_of(X):
+    rec = getattr(X, "_mvml_elu", None)
+    if rec is None or rec[1] != X._version or rec[2] != (X.data_ptr(), tuple(X.shape), X.stride()):
+        return None
+    return rec[0]
+
+
 class GATLayerFunction(torch.autograd.Function):
     """dgllife GATLayer(GATConv) forward/backward (model.py:79-81): projection GEMM (fc and
     res_fc as one MFMA GEMM) + fused el/er, edge-softmax, aggregation, residual, bias and
@@ -262,6 +296,18 @@ class GATLayerFunction(torch.autograd.Function):
         Xp = X if Fp == Fin else torch.nn.functional.pad(X, (0, Fp - Fin))
         attn_l, attn_r = _c(attn_l), _c(attn_r)
         attn_lr = torch.cat([attn_l.reshape(-1), attn_r.reshape(-1)])
+        ctx.reassoc = False
+        ctx.elu_claim = None
+        if (REASSOC_X and (algo or GEMM_ALGO) == "f16x2" and ROW_SCALES and PROJ_ELR_GEMM
+                and mode in (MODE_FLATTEN_ELU, MODE_FLATTEN) and not X.requires_grad
+                and 2 * Fp <= F and _lib.lib().mvml_gat_x_supported(H, Fp)):
+            return GATLayerFunction._forward_x(ctx, X, Xp, fc_w, res_w, attn_l, attn_r, attn_lr, bias,
+                                               g, H, F, slope, mode, C)
+        link = _elu_link_of(X) if (ELU_LINK[0] and (algo or GEMM_ALGO) == "f16x2" and ROW_SCALES
+                                   and PROJ_ELR_GEMM and X.requires_grad) else None
+        if link is not None and not link.claimed and Fp == Fin:
+            link.claimed = True
+            ctx.elu_claim = link
         # [fc.weight ; res_fc.weight (or its head mean) ; A_l ; A_r]: the projection GEMM uses
         # the first C rows, the backward all C + 2H (the el / er paths, see mvml_gat_agg_bwd)
         Wcat = torch.empty((C + 2 * H, Fp), dtype=torch.float32, device=dev)
@@ -353,7 +399,129 @@ class GATLayerFunction(torch.autograd.Function):
         return out
 
     @staticmethod
+    def _forward_x(ctx, X, Xp, fc_w, res_w, attn_l, attn_r, attn_lr, bias, g, H, F, slope, mode, C):
+        N, Fin = X.shape
+        Fp = Xp.shape[1]
+        dev = X.device
+        HF = H * F
+        st = _stream(dev)
+        Wcat = torch.empty((C + 2 * H, Fp), dtype=torch.float32, device=dev)
+        call("mvml_gat_fold_weights", ptr(_c(fc_w)), ptr(_c(res_w)), ptr(attn_lr), H, F, Fin, Fp, 0,
+             ptr(Wcat), st)
+        # [X, Wcat, axc, out] maxima; X's per-row maxima recorded on the resident feature tensor
+        amx = torch.zeros(4, dtype=torch.int32, device=dev)
+        xr = known_rows(X)
+        if xr is None:
+            xr = absmax_rows(X, N, Fin, Fin)
+            fold_rows(X, xr)
+        absmax(xr, N, 1, 1, amx, 0)
+        absmax(Wcat, C + 2 * H, Fp, Fp, amx, 1)
+        Wb = torch.empty((HF, 2 * Fp), dtype=torch.float32, device=dev)  # [W_h | Wres_h] rows
+        call("mvml_gat_x_pack_weights", ptr(Wcat), H, F, Fp, ptr(Wb), st)
+        wb_il = split_il4(Wb, HF, 2 * Fp, 2 * Fp, slot(amx, 1))
+        wil = split_il4(Wcat, C + 2 * H, Fp, Fp, slot(amx, 1))  # W_h as the backward's B
+        E = g.num_edges()
+        elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
+        attn = torch.empty((E, H), dtype=torch.float32, device=dev)
+        axc = torch.empty((N, H * 2 * Fp), dtype=torch.float32, device=dev)  # per head [AX_h | X]
+        arows = torch.empty(max(H * N, 1), dtype=torch.int32, device=dev)
+        alr = ctypes.c_void_p(ptr(Wcat).value + 4 * C * Fp)  # [A_l ; A_r]: Wcat's last 2H rows
+        _lib.call_tag[0] = {"layer": f"H{H}xF{F}x", "bytes": 4 * (N * Fp + 2 * N * H + (N + 1) + E
+                                                               + 2 * E * H + N * H * 2 * Fp + H * N)}
+        call("mvml_gat_x_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(Xp), Fp, alr, H, float(slope),
+             ptr(elr), ptr(attn), ptr(axc), ptr(arows), st)
+        absmax(arows, H * N, 1, 1, amx, 2)  # max |axc| (the weight gradient's B scale)
+        out = torch.empty((N, HF), dtype=torch.float32, device=dev)
+        orows = torch.zeros(max(N, 1), dtype=torch.int32, device=dev)
+        act = 2 if mode == MODE_FLATTEN_ELU else 0
+        _lib.call_tag[0] = {"flops": 2 * N * HF * 2 * Fp, "shape": (N, F, 2 * Fp, H)}
+        call("mvml_gemm_f16x2_ex", N, F, 2 * Fp, H, ptr(axc), H * 2 * Fp, 2 * Fp, ptr(Wb), 2 * Fp, 0,
+             ptr(wb_il), F * 2 * Fp, ptr(arows), N, slot(amx, 1), ptr(_c(bias)), F, act, ptr(out), HF, F,
+             None, 0, slot(amx, 3), ptr(orows), 0, 0, 0, st)
+        fold_amax(out, amx, 3)
+        fold_rows(out, orows)
+        ctx.reassoc = True
+        ctx.link = None
+        if act == 2 and ELU_LINK[0]:
+            ctx.link = EluLink(dev)
+            out._mvml_elu = (ctx.link, out._version, (out.data_ptr(), tuple(out.shape), out.stride()))
+        if DEBUG_CAPTURE is not None:
+            DEBUG_CAPTURE.setdefault("elr_fwd", []).append(elr.detach().clone())
+        ctx.save_for_backward(Xp, Wcat, axc, attn, elr, out, attn_l, attn_r, attn_lr)
+        ctx.Fin = Fin
+        ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode = g, H, F, slope, mode
+        ctx.amx = amx
+        ctx.wil = wil
+        return out
+
+    @staticmethod
+    def _backward_x(ctx, g_out):
+        Xp, Wcat, axc, attn, elr, out, attn_l, attn_r, attn_lr = ctx.saved_tensors
+        g, H, F, mode = ctx.g, ctx.H, ctx.F, ctx.mode
+        N, Fp = Xp.shape
+        Fin = ctx.Fin
+        dev = Xp.device
+        HF = H * F
+        C = 2 * HF
+        st = _stream(dev)
+        amx = ctx.amx
+        link = ctx.link
+        if link is not None and link.claimed:
+            # the next layer's data-gradient GEMM already applied ELU' and folded max |g_rst|
+            gr = link.g_rst
+            if gr is None or g_out.data_ptr() != gr.data_ptr() or g_out.shape != gr.shape \
+                    or g_out.stride() != gr.stride():
+                raise RuntimeError("GAT ELU link: the gradient reaching the first layer is not the one "
+                                   "the next layer's fused ELU backward wrote (was its output also "
+                                   "consumed elsewhere?)")
+            g_rst, ga = g_out, link.amax
+        else:
+            g_out = _c(g_out)
+            ga = torch.zeros(1, dtype=torch.int32, device=dev)
+            if mode == MODE_FLATTEN_ELU:
+                g_rst = torch.empty((N, HF), dtype=torch.float32, device=dev)
+                call("mvml_gat_elu_bwd", N * HF, ptr(g_out), ptr(out), ptr(g_rst), ptr(ga), st)
+            else:
+                g_rst = g_out
+                absmax(g_rst, N, HF, HF, ga, 0)
+        gp = slot(ga, 0)
+        # dAX_h = g_rst_h W_h: one strided batch over the heads (B = Wcat's rows h F .., K-major)
+        dax = torch.empty((N, H * Fp), dtype=torch.float32, device=dev)
+        _lib.call_tag[0] = {"flops": 2 * N * Fp * F * H, "shape": (N, Fp, F, H)}
+        call("mvml_gemm_f16x2_batched", 0, 1, N, Fp, F, H, ptr(g_rst), HF, F, ptr(Wcat), Fp, F * Fp,
+             gp, slot(amx, 1), ptr(dax), H * Fp, Fp, st)
+        E = g.num_edges()
+        gpre = torch.empty((E, H), dtype=torch.float32, device=dev)
+        gelr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
+        gl = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.call_tag[0] = {"layer": f"H{H}xF{F}x", "bytes": 4 * (N * H * Fp + 2 * E * Fp // 1 + 2 * N * H
+                                                               + 3 * E * H + 2 * (N + 1) + 3 * E)}
+        call("mvml_gat_x_bwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_inslot),
+             ptr(Xp), Fp, ptr(elr), ptr(attn), H, float(ctx.slope), ptr(dax), ptr(gpre), ptr(gelr),
+             ptr(gl), st)
+        # dL/dWcat in the projection path's layout [fc | res_fc | A_l | A_r] rows
+        gW = torch.empty((C + 2 * H, Fp), dtype=torch.float32, device=dev)
+        for h in range(H):  # dL/dW_h = g_rst_h^T AX_h (split-K over atoms)
+            gemm(g_rst[:, h * F:], axc[:, h * 2 * Fp:], F, Fp, N, 1, 1, HF, H * 2 * Fp, gW[h * F:], Fp,
+                 amax=(gp, slot(amx, 2)))
+        gemm(g_rst, Xp, HF, Fp, N, 1, 1, HF, Fp, gW[HF:], Fp, amax=(gp, slot(amx, 0)))  # res_fc
+        gemm(gelr, Xp, 2 * H, Fp, N, 1, 1, 2 * H, Fp, gW[C:], Fp, amax=(slot(gl, 0), slot(amx, 0)))
+        g_fc = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
+        g_res = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
+        call("mvml_gat_unfold_grads", ptr(gW), ptr(attn_lr), H, F, Fin, Fp, 0, ptr(g_fc), ptr(g_res), st)
+        g_alr = torch.empty((2, HF), dtype=torch.float32, device=dev)
+        gemm_batched(gW[C:], Wcat, 2, F, Fp, 0, 0, H * Fp, Fp, g_alr, HF, H, Fp, F * Fp, F)
+        if DEBUG_CAPTURE is not None:
+            DEBUG_CAPTURE.update(elr=elr, gelr=gelr, attn=attn)
+        g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
+        colsum(g_rst, N, HF, HF, g_bias)
+        return (None, g_fc, g_res, g_alr[0].view_as(attn_l), g_alr[1].view_as(attn_r), g_bias,
+                None, None, None, None, None, None)
+
+    @staticmethod
     def backward(ctx, g_out):
+        if ctx.reassoc:
+            return GATLayerFunction._backward_x(ctx, g_out)
         Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr = ctx.saved_tensors
         g, H, F, mode, ldy = ctx.g, ctx.H, ctx.F, ctx.mode, ctx.ldy
         g_out = _c(g_out)
@@ -413,7 +581,17 @@ class GATLayerFunction(torch.autograd.Function):
         gX = None
         if ctx.needs_input_grad[0]:
             gX = torch.empty((N, Fin), dtype=torch.float32, device=dev)
-            if amx is not None and ROW_SCALES:  # every atom's gradient row at its own scale
+            link = ctx.elu_claim
+            if link is not None and amx is not None and ROW_SCALES and ctx.wil is not None:
+                # the previous layer's ELU backward in this product's epilogue: gX leaves as its
+                # g_rst, with max |g_rst| folded for its GEMMs (EluLink)
+                link.amax.zero_()
+                _lib.call_tag[0] = {"flops": 2 * N * Fin * CE, "shape": (N, Fin, CE, 0, 1)}
+                call("mvml_gemm_f16x2_ex", N, Fin, CE, 1, ptr(gY), ldg, 0, ptr(Wcat), Fp, 1, ptr(ctx.wil),
+                     0, ptr(gyr if gyr is not None else absmax_rows(gY, N, CE, ldg)), 0, slot(amx, 1),
+                     None, 0, 3, ptr(gX), Fin, 0, ptr(Xp), Fp, ptr(link.amax), None, 0, 0, 0, st)
+                link.g_rst = gX
+            elif amx is not None and ROW_SCALES:  # every atom's gradient row at its own scale
                 gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, amax=(None, slot(amx, 1)),
                      arows=gyr if gyr is not None else absmax_rows(gY, N, CE, ldg), bil4=ctx.wil)
             else:

@@ -142,8 +142,14 @@ class GAT(nn.Module):
             layer.gat_conv.reset_parameters()
 
     def forward(self, g, feats):
-        for gnn in self.gnn_layers:
-            feats = gnn(g, feats)
+        # inside the stack a flatten + ELU layer's output feeds only the next layer: its ELU
+        # backward may run in that layer's data-gradient GEMM (functional.EluLink)
+        prev, Fn.ELU_LINK[0] = Fn.ELU_LINK[0], True
+        try:
+            for gnn in self.gnn_layers:
+                feats = gnn(g, feats)
+        finally:
+            Fn.ELU_LINK[0] = prev
         return feats
 
 

@@ -149,7 +149,9 @@ def test_gnn_module_config3_graphnorm_groups():
     _module_case(sb, group_size=64, seed=7)
 
 
-def _layer_case(layer, sb, seed=0):
+def _layer_case(layer, sb, seed=0, x_grad=True):
+    """x_grad=False (layer 0, the atom features as GNNModule feeds them): no input gradient, so
+    the re-associated first-layer path runs (functional.REASSOC_X; asserted)."""
     prod, ref = model_pair(seed=seed)
     conv_p = prod.conv.gnn_layers[layer]
     conv_r = ref.conv.gnn_layers[layer].gat_conv
@@ -167,8 +169,10 @@ def _layer_case(layer, sb, seed=0):
     p64 = {k: v.detach().double().requires_grad_() for k, v in params.items()}
     conv_p = conv_p.to(DEV)
     gdev = sb.to_graph().to(DEV)
-    Xp = X.float().to(DEV).requires_grad_()
+    Xp = X.float().to(DEV).requires_grad_(x_grad)
     out_p, elrs = _capture(lambda: conv_p(gdev, Xp))
+    assert out_p.grad_fn.reassoc == (not x_grad and Fn.REASSOC_X and Fn.GEMM_ALGO == "f16x2"
+                                     and Fn.ROW_SCALES and Fn.PROJ_ELR_GEMM)
     br = _branches(gd, elrs)
     _check_kink_flips(gd, br, [X], [p64])
     Xr = X.clone().requires_grad_()
@@ -179,7 +183,8 @@ def _layer_case(layer, sb, seed=0):
     out_r.backward(gout)
     out_p.backward(gout.float().to(DEV))
     assert rel_err(out_p, out_r) < TOL, "forward"
-    assert rel_err(Xp.grad, Xr.grad) < TOL, "dX"
+    if x_grad:
+        assert rel_err(Xp.grad, Xr.grad) < TOL, "dX"
     c = conv_p.gat_conv
     for name, pp in (("fc.weight", c.fc.weight), ("res_fc.weight", c.res_fc.weight),
                      ("attn_l", c.attn_l), ("attn_r", c.attn_r), ("bias", c.bias)):
@@ -196,6 +201,23 @@ def test_gat_layer0_hubs_flatten_elu():
     """Layer 0 (F = 192, flatten + ELU) on hub molecules > 128 atoms: the big-window kernels
     (kind bit 2) with their hub segments, at the production width."""
     _layer_case(0, batch_of_sizes([150, 90, 210], seed=7, hubs=True), seed=2)
+
+
+@pytest.mark.parametrize("case", ["config2", "hubs", "config5", "config5_three", "table_overflow",
+                                  "config3"])
+def test_gat_layer0_reassociated(case):
+    """The first layer as GNNModule runs it (no input gradient): edge softmax + aggregation over
+    the 76-wide feature rows and one batched GEMM per head (mvml_gat_x_fwd, mvml_gemm_f16x2_ex),
+    backward through dAX = g_rst W_h (mvml_gat_x_bwd) — every output and gradient against float64
+    on each graph family the projection path's kernels are tested on (the re-associated kernels
+    have no size classes: one code path for any molecule)."""
+    sb = {"config2": lambda: synth.config2(128, seed=0),
+          "hubs": lambda: batch_of_sizes([150, 90, 210], seed=7, hubs=True),
+          "config5": lambda: synth.config5(2, seed=3),
+          "config5_three": lambda: synth.config5(3, seed=5),
+          "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109),
+          "config3": lambda: synth.config3(192, seed=4)}[case]()
+    _layer_case(0, sb, seed=11, x_grad=False)
 
 
 def test_gat_layer1_config5():
