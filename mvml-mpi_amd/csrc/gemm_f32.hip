@@ -25,6 +25,7 @@
 // variants against fp64) at 6 bf16 MFMAs per 16 k instead of 8 f32 MFMAs at 1/16 the rate.
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "common.h"
@@ -484,7 +485,7 @@ __device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[FM][FN], int64
 }
 
 constexpr int kEpiLd = 68;  // floats per LDS row (64 + 4: the column writes hit distinct banks)
-template <int FM>
+template <int FM, bool EX = false>
 __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* wl, int64_t M,
                                              int64_t N, int64_t r0, int64_t c0, int lane,
                                              const float* __restrict__ bias, float beta, int act,
@@ -1144,7 +1145,93 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 // A wave's FM x 2 accumulator tiles (rows r0 .. r0 + 32 FM, 64 columns) through its 32-row LDS
 // window: FM = 4 in the 256x256 kernels, 2 in the 128x128 one.
+// One float4 of an output row through the EpiX epilogue (bias, beta, act 0-3), stored; returns
+// max |stored value| (columns past N neither stored nor counted).
+__device__ __forceinline__ float epix_store4(const float* src, float* __restrict__ out, int64_t ld,
+                                            int64_t N, int64_t row, int64_t col, float ua,
+                                            const float* __restrict__ bias, float beta, int act,
+                                            const float* __restrict__ aux, int64_t ld_aux, bool vec) {
+  const float4 t = *reinterpret_cast<const float4*>(src);
+  float e0 = t.x * ua, e1 = t.y * ua, e2 = t.z * ua, e3 = t.w * ua;
+  float* cp = out + row * ld + col;
+  const bool full = col + 3 < N;
+  auto fin = [&](float x, int u) __attribute__((always_inline)) -> float {
+    if (bias) x += bias[col + u];
+    if (beta != 0.f) x += beta * cp[u];
+    if (act == 1) x = fmaxf(x, 0.f);
+    if (act == 2) x = elu_epi(x);
+    if (act == 3) x *= elu_grad_epi(aux[row * ld_aux + col + u]);
+    return x;
+  };
+  e0 = fin(e0, 0);
+  if (full || col + 1 < N) e1 = fin(e1, 1);
+  if (full || col + 2 < N) e2 = fin(e2, 2);
+  if (full) e3 = fin(e3, 3);
+  float m = fabsf(e0);
+  if (full && vec) {
+    *reinterpret_cast<float4*>(cp) = make_float4(e0, e1, e2, e3);
+    m = fmaxf(fmaxf(m, fabsf(e1)), fmaxf(fabsf(e2), fabsf(e3)));
+  } else {
+    cp[0] = e0;
+    if (col + 1 < N) { cp[1] = e1; m = fmaxf(m, fabsf(e1)); }
+    if (col + 2 < N) { cp[2] = e2; m = fmaxf(m, fabsf(e2)); }
+    if (col + 3 < N) { cp[3] = e3; m = fmaxf(m, fabsf(e3)); }
+  }
+  return m;
+}
+
+// The EpiX tile pass: the accumulators of each 32-row block through the wave's LDS rows (as
+// epilogue_lds), then stores through epix_store4, per-row maxima (a row's 16 lanes reduce, one
+// atomicMax per row slot) and the tile's |max| (one atomicMax per wave).  The row blocks are
+// unrolled by construction (a fold over the block index) so the accumulators stay in registers;
+// the store loop inside is not unrolled.
+template <int... Is, typename Fn>
+__device__ __forceinline__ void static_for_x(std::integer_sequence<int, Is...>, Fn&& fn) {
+  (fn(std::integral_constant<int, Is>{}), ...);
+}
 template <int FM>
+__device__ __forceinline__ void epix_tile(const f32x16 (&acc)[FM][2], float* wl, int64_t M, int64_t N,
+                                          int64_t r0, int64_t c0, int lane,
+                                          const float* __restrict__ bias, float beta, int act,
+                                          float* __restrict__ out, int64_t ld, bool vec, const int* rs,
+                                          const EpiX& ex) {
+  const int li = lane & 31, lk = lane >> 5;
+  float am = 0.f;
+  static_for_x(std::make_integer_sequence<int, FM>{}, [&](auto I) __attribute__((always_inline)) {
+    constexpr int i = decltype(I)::value;
+    if (i > 0) wave_sync_lds();
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        wl[((r & 3) + 8 * (r >> 2) + 4 * lk) * kEpiLd + 32 * j + li] = acc[i][j][r];
+    wave_sync_lds();
+#pragma nounroll
+    for (int q = 0; q < 8; ++q) {
+      const int idx = q * 64 + lane, rr = idx >> 4, c4 = (idx & 15) * 4;
+      const int64_t row = r0 + 32 * i + rr, col = c0 + c4;
+      float rm = 0.f;
+      if (row < M && col < N)
+        rm = epix_store4(wl + rr * kEpiLd + c4, out, ld, N, row, col, rs ? pow2f(-rs[32 * i + rr]) : 1.f,
+                         bias, beta, act, ex.aux, ex.ld_aux, vec);
+      am = fmaxf(am, rm);
+      if (ex.c_rows) {  // (uniform) the row's 16 lanes reduce together
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) rm = fmaxf(rm, __shfl_xor(rm, o, 64));
+        if ((lane & 15) == 0 && row < M) {
+          const int64_t slot = ex.rows_cols > 0 ? c0 / ex.rows_cols : 0;
+          atomicMax(ex.c_rows + blockIdx.z * ex.crows_z + slot * ex.rows_stride + row, __float_as_uint(rm));
+        }
+      }
+    }
+  });
+  if (ex.c_amax) {  // (uniform) one atomic per wave
+    am = wave_max(am);
+    if (lane == 0) atomicMax(ex.c_amax, __float_as_uint(am));
+  }
+}
+
+template <int FM, bool EX>
 __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* wl, int64_t M,
                                                  int64_t N, int64_t r0, int64_t c0, int lane,
                                                  const float* __restrict__ bias, float beta, int act,
@@ -1162,39 +1249,13 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
   // instead of seven dword stores per unit — the cell epilogue was store-issue-bound.  Same
   // arithmetic per unit, so bitwise the per-unit path's results (kept for unaligned operands).
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  // EpiX work (act 2 / 3, folded maxima): its own store path, never with split-K or the cell
-  const bool extra = !slab && cep.D == 0 && (act >= 2 || ex.c_amax || ex.c_rows);
-  const bool fold_rows = extra && ex.c_rows;
-  float am = 0.f;  // |max| of this lane's stored values (c_amax)
-  auto store4x = [&](const float* src, int64_t row, int64_t col, int shift) -> float {
-    float e[4];
-    const float4 t = *reinterpret_cast<const float4*>(src);
-    e[0] = t.x; e[1] = t.y; e[2] = t.z; e[3] = t.w;
-    const float ua = rs ? pow2f(-shift) : 1.f;
-    float* cp = out + row * ld + col;
-    const float* ap = act == 3 ? ex.aux + row * ex.ld_aux + col : nullptr;
-    float m = 0.f;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (col + u >= N) break;
-      float x = e[u] * ua;
-      if (bias) x += bias[col + u];
-      if (beta != 0.f) x += beta * cp[u];
-      if (act == 1) x = fmaxf(x, 0.f);
-      if (act == 2) x = elu_epi(x);
-      if (act == 3) x *= elu_grad_epi(ap[u]);
-      e[u] = x;
-      m = fmaxf(m, fabsf(x));
+  // EpiX work (act 2 / 3, folded maxima): its own tile pass, never with split-K or the cell
+  if constexpr (EX) {
+    if (!slab && cep.D == 0 && (act >= 2 || ex.c_amax || ex.c_rows)) {
+      epix_tile<FM>(acc, wl, M, N, r0, c0, lane, bias, beta, act, out, ld, vec, rs, ex);
+      return;
     }
-    if (vec && col + 3 < N) {
-      *reinterpret_cast<float4*>(cp) = make_float4(e[0], e[1], e[2], e[3]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (col + u < N) cp[u] = e[u];
-    }
-    return m;
-  };
+  }
   const bool cell4 = cep.D > 0 && cep.D % 4 == 0 && al16(cep.b_ih) && al16(cep.b_hh) &&
                      al16(cep.c_prev) && al16(cep.c_out) && al16(cep.h_out) && al16(cep.h_out2) &&
                      al16(cep.act) && cep.ldh % 4 == 0 && cep.ldh2 % 4 == 0 && al16(cep.gx) &&
@@ -1266,24 +1327,7 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
     for (int q = 0; q < 8; ++q) {
       const int idx = q * 64 + lane, rr = idx >> 4, c4 = (idx & 15) * 4;
       const int64_t row = r0 + 32 * i + rr, col = c0 + c4;
-      if (fold_rows) {  // (uniform) the row's 16 lanes reduce together: no early exit
-        float rm = 0.f;
-        if (row < M && col < N) rm = store4x(wl + rr * kEpiLd + c4, row, col, rs ? rs[32 * i + rr] : 0);
-        am = fmaxf(am, rm);
-#pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) rm = fmaxf(rm, __shfl_xor(rm, o, 64));
-        if ((lane & 15) == 0 && row < M) {
-          const int64_t slot = ex.rows_cols > 0 ? c0 / ex.rows_cols : 0;
-          atomicMax(ex.c_rows + blockIdx.z * ex.crows_z + slot * ex.rows_stride + row,
-                    __float_as_uint(rm));
-        }
-        continue;
-      }
       if (row >= M || col >= N) continue;
-      if (extra) {
-        am = fmaxf(am, store4x(wl + rr * kEpiLd + c4, row, col, rs ? rs[32 * i + rr] : 0));
-        continue;
-      }
       float4 v = *reinterpret_cast<const float4*>(wl + rr * kEpiLd + c4);
       if (rs) {
         const float ua = pow2f(-rs[32 * i + rr]);
@@ -1346,10 +1390,6 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
       }
     }
   }
-  if (extra && ex.c_amax) {  // (uniform) one atomic per wave
-    am = wave_max(am);
-    if (lane == 0) atomicMax(ex.c_amax, __float_as_uint(am));
-  }
 }
 
 #ifndef MVML_X3W_WAVES
@@ -1392,7 +1432,7 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
 // separate instantiation so that the operand-wide kernels keep their register allocation (one
 // spill reload inside the main loop costs a vmcnt drain per stage).
 template <bool AK, bool BKM, int EPI_LOGW = -1, bool FAST = true, int NP = 3, int BPS = 0,
-          bool ROWS = false>
+          bool ROWS = false, bool EX = false>
 __global__ void __launch_bounds__(kXThreads, MVML_X3W_WAVES)  // one workgroup per CU
 gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
@@ -1404,8 +1444,10 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     A += blockIdx.z * bst.a;
     B += blockIdx.z * bst.b;
     C += blockIdx.z * bst.c;
-    if (bias) bias += blockIdx.z * ex.bias_z;
-    if (amax.a_rows) amax.a_rows += blockIdx.z * ex.rows_z;
+    if constexpr (EX) {
+      if (bias) bias += blockIdx.z * ex.bias_z;
+      if (amax.a_rows) amax.a_rows += blockIdx.z * ex.rows_z;
+    }
   }
   if (blockIdx.z == 1 && dual.a) {  // the second product of a dual launch
     A = dual.a;
@@ -1835,9 +1877,9 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   if constexpr (EPI_LOGW >= 0)
     tile_epilogue<EPI_LOGW, 4, 2, false>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta,
                                          act, C, ldc, slab, epi);
-  epilogue_lds(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
-                   n0 + wn * 64, lane, bias, beta, act, C, ldc, slab, cep,
-                   (ROWS && ntiles > 0) ? rsh + wm * 128 : nullptr, ex);
+  epilogue_lds<4, EX>(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
+                      n0 + wn * 64, lane, bias, beta, act, C, ldc, slab, cep,
+                      (ROWS && ntiles > 0) ? rsh + wm * 128 : nullptr, ex);
 #else
   static_assert(NP != 2, "per-row A maxima need the LDS epilogue");
   tile_epilogue<EPI_LOGW, 4, 2>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta, act, C,
@@ -2517,7 +2559,7 @@ extern "C" int mvml_gemm_f16x2_ex(int64_t M, int64_t N, int64_t K, int64_t batch
   hipStream_t st = as_stream(stream);
   const int64_t kc = K > 0 ? K : 1;
 #define MVML_X3W_EX(BKV, BPSV)                                                                    \
-  gemm_x3w_kernel<false, BKV, -1, true, 2, BPSV, true><<<grid, kXThreads, 0, st>>>(               \
+  gemm_x3w_kernel<false, BKV, -1, true, 2, BPSV, true, true><<<grid, kXThreads, 0, st>>>(         \
       M, N, K, A, lda, Bp, ldb, bias, 0.f, act, C, ldc, kc, nullptr, av, bv, ProjEpi{}, bst,       \
       CellEpi{}, am, DualPtrs{}, ex)
   if (b_kmajor) {
