@@ -54,7 +54,9 @@ TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32
          "mvml_bilstm_wide_step_fwd", "mvml_bilstm_wide_step_bwd", "mvml_bilstm_pack_rows",
          "mvml_bilstm_gather_rows", "mvml_bilstm_token_grad", "mvml_bilstm_select_last",
          "mvml_bilstm_token_grad_packed", "mvml_bilstm_packed_tokens", "mvml_gemm_f16x2_rows",
-         "mvml_absmax_rows_f32", "mvml_segment_max_bits"]
+         "mvml_absmax_rows_f32", "mvml_segment_max_bits", "mvml_gat_x_fwd", "mvml_gat_x_bwd",
+         "mvml_gemm_f16x2_ex", "mvml_gemm_f16x2_batched", "mvml_gat_elu_bwd", "mvml_gat_x_pack_weights",
+         "mvml_split_f16x2_il4"]
 
 
 def parse(argv=None):
@@ -514,6 +516,7 @@ def run(args):
                               + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])
                               + summ.get("mvml_gemm_f16x2_rows", [])
                               + summ.get("mvml_gemm_f16x2_bsplit", [])
+                              + summ.get("mvml_gemm_f16x2_ex", []) + summ.get("mvml_gemm_f16x2_batched", [])
                               + summ.get("mvml_lstm_gates_cell_fwd", [])
                               + summ.get("mvml_gat_proj_fwd", []), args.steps)
         if rank == 0:
@@ -533,6 +536,7 @@ def run(args):
                    + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])
                    + summ.get("mvml_gemm_f16x2_bsplit", []) + summ.get("mvml_gemm_f16x2_rows", [])
                    + summ.get("mvml_gemm_f32x3_batched", []) + summ.get("mvml_lstm_gates_cell_fwd", [])
+                   + summ.get("mvml_gemm_f16x2_ex", []) + summ.get("mvml_gemm_f16x2_batched", [])
                    + ([] if args.proj_bf16 else proj_ev))
         bf_ev = summ.get("mvml_gemm_bf16", []) + (proj_ev if args.proj_bf16 else [])
         if bf_ev:
@@ -543,7 +547,7 @@ def run(args):
         if gemm_ev:
             extra["roofline_gemm"] = roofline_entry(gemm_ev, "mfma")
             if (summ.get("mvml_gemm_f16x2") or summ.get("mvml_gemm_f16x2_amax") or summ.get("mvml_gemm_f16x2_bsplit")
-                    or summ.get("mvml_gemm_f16x2_rows")):
+                    or summ.get("mvml_gemm_f16x2_rows") or summ.get("mvml_gemm_f16x2_ex")):
                 # scaled split-fp16: 3 fp16 MFMA per fp32 multiply-add -> fp32-equivalent peak
                 # 2.5 PF / 3 (the skinny products that fall back to split-bf16 count against it too)
                 extra["roofline_gemm"].update(

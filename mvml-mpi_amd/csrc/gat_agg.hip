@@ -1571,6 +1571,199 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
   if (gy_amax) block_amax_commit<kWavesPerBlock * 64>(gmx, gy_amax);
 }
 
+// ---- Head-mean layer backward by SOURCE atom (MVML_OPT_MEAN_SRC) -----------------------------
+// In mean mode g_rst = g_out / H does not depend on the head, so both products of the backward
+//   dZ[u, h, :] = sum_{e: u -> w} a_e,h g_out[w, :] / H          (update_all(u_mul_e, sum) backward)
+//   g_a[e, h]   = <Z[u, h, :], g_out[w, :] / H>                   (the edge-weight gradient)
+// are formed by the wave that owns SOURCE u: its projection row Z[u] (H F floats) is read once,
+// straight from HBM into registers, and only the F-wide g_out rows of its out-neighbours are
+// gathered (from the XCD's L2: xcd_block keeps neighbouring atoms on one XCD) — no LDS window,
+// no chunk barriers, whatever the molecule size.  Lane l owns f-columns 4 (l + 64 j) of every
+// head, so a g_out row is loaded once per edge (not once per head).  dZ walks the out-edges in
+// out-CSR order with the atomwise pass's arithmetic (g_out / H, then fma), so it is bitwise
+// the atomwise dZ; g_a is written per edge (one writer: the edge's source) for the softmax pass.
+// streaming (non-temporal) 16-B load / store: the projection rows read once and the dZ rows
+// written once pass through without displacing the g_out rows the XCD's waves share in L2
+typedef float mvml_f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld4nt(const float* p) {
+  const mvml_f4v v = __builtin_nontemporal_load(reinterpret_cast<const mvml_f4v*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st4nt(float* p, float4 v) {
+  mvml_f4v w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<mvml_f4v*>(p));
+}
+
+template <int H, int NJ>
+__global__ void __launch_bounds__(256)
+gat_mean_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
+                        const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
+                        const float* __restrict__ Y, int64_t ldy, const float* __restrict__ attn,
+                        const float* __restrict__ g_out, int F, float* __restrict__ ga,
+                        float* __restrict__ gY, int64_t ldgy, uint32_t* __restrict__ gy_amax,
+                        uint32_t* __restrict__ gy_rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t u = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  float gmx = 0.f;
+  if (u < N) {  // (no early return: block_amax_commit below has a barrier)
+    const int nf4 = F / 4, HF = H * F;
+    const float hh = (float)H;
+    bool okj[NJ];
+    float4 z[H][NJ], dz[H][NJ];
+    const float* zu = Y + u * ldy;
+    float* gyu = gY + u * ldgy;
+    float rmx = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int fj = lane + 64 * j;
+      okj[j] = fj < nf4;
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        z[h][j] = okj[j] ? ld4nt(zu + h * F + 4 * fj) : f4(0.f);
+        dz[h][j] = f4(0.f);
+      }
+      if (okj[j]) {  // dR[u] = g_out[u] (the head-mean residual's gradient)
+        const float4 go = ld4(g_out + u * F + 4 * fj);
+        st4nt(gyu + HF + 4 * fj, go);
+        rmx = amax4(rmx, go);
+      }
+    }
+    const int ob = out_rowptr[u], oe = out_rowptr[u + 1];
+    for (int base = ob; base < oe; base += 64) {
+      const int cnt = min(64, oe - base);
+      int w_l = 0, s_l = 0;
+      float a_l[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) a_l[h] = 0.f;
+      if (lane < cnt) {
+        w_l = out_dst[base + lane];
+        s_l = out_inslot[base + lane];
+#pragma unroll
+        for (int h = 0; h < H; ++h) a_l[h] = attn[(int64_t)s_l * H + h];
+      }
+#pragma unroll 2
+      for (int j = 0; j < cnt; ++j) {
+        const float* gw = g_out + (int64_t)rl(w_l, j) * F;
+        float a[H], part[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) { a[h] = rl(a_l[h], j); part[h] = 0.f; }
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj) {
+          if (!okj[jj]) continue;
+          float4 g = ld4(gw + 4 * (lane + 64 * jj));
+          g = make_float4(g.x / hh, g.y / hh, g.z / hh, g.w / hh);
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            dz[h][jj] = fma4(a[h], g, dz[h][jj]);
+            part[h] += dot4(z[h][jj], g);
+          }
+        }
+        HeadReduce<H>::template all<false>(part, lane);
+        store_heads<H>(ga + (int64_t)rl(s_l, j) * H, part, lane);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      if (okj[j]) {
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          st4nt(gyu + h * F + 4 * (lane + 64 * j), dz[h][j]);
+          rmx = amax4(rmx, dz[h][j]);
+        }
+      }
+    gmx = wave_max(rmx);
+    if (gy_rows && lane == 0) gy_rows[u] = __float_as_uint(gmx);  // the first writer of the row
+  }
+  if (gy_amax) block_amax_commit<256>(gmx, gy_amax);
+}
+
+// edge_softmax + LeakyReLU backward per destination v (thread per atom, the LDS kernel's
+// arithmetic and edge order): g_a -> g_pre in place, d er[v] -> gY[v, C + H ..]
+template <int H>
+__global__ void __launch_bounds__(256)
+gat_mean_bwd_softmax_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
+                            const float* __restrict__ elr, const float* __restrict__ attn, float slope,
+                            float* __restrict__ gpre, float* __restrict__ gY, int64_t ldgy, int C) {
+  const int64_t v = xcd_block(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
+  if (v >= N) return;
+  const int eb = rowptr[v], ee = rowptr[v + 1];
+  float er[H], dots[H], der[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) { er[h] = elr[v * 2 * H + H + h]; dots[h] = 0.f; der[h] = 0.f; }
+  for (int e = eb; e < ee; ++e)
+#pragma unroll
+    for (int h = 0; h < H; ++h) dots[h] += attn[(int64_t)e * H + h] * gpre[(int64_t)e * H + h];
+  for (int e = eb; e < ee; ++e) {
+    const float* el = elr + (int64_t)in_src[e] * 2 * H;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float g_s = attn[(int64_t)e * H + h] * (gpre[(int64_t)e * H + h] - dots[h]);
+      const float gp = (el[h] + er[h]) > 0.f ? g_s : g_s * slope;
+      gpre[(int64_t)e * H + h] = gp;
+      der[h] += gp;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) gY[v * ldgy + C + H + h] = der[h];
+}
+
+// d el[u] = sum over u's out-edges of g_pre (out-CSR order); the row |max| gains d el / d er.
+template <int H>
+__global__ void __launch_bounds__(256)
+gat_mean_bwd_gel_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
+                        const int32_t* __restrict__ out_inslot, const float* __restrict__ gpre,
+                        float* __restrict__ gY, int64_t ldgy, int C, uint32_t* __restrict__ gy_amax,
+                        uint32_t* __restrict__ gy_rows) {
+  const int64_t u = xcd_block(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
+  float m = 0.f;
+  if (u < N) {
+    float g[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) g[h] = 0.f;
+    for (int o = out_rowptr[u]; o < out_rowptr[u + 1]; ++o) {
+      const float* p = gpre + (int64_t)out_inslot[o] * H;
+#pragma unroll
+      for (int h = 0; h < H; ++h) g[h] += p[h];
+    }
+    float* row = gY + u * ldgy + C;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      row[h] = g[h];
+      m = fmaxf(m, fmaxf(fabsf(g[h]), fabsf(row[H + h])));
+    }
+    if (gy_rows) gy_rows[u] = max(gy_rows[u], __float_as_uint(m));
+  }
+  if (gy_amax) block_amax_commit<256>(m, gy_amax);
+}
+
+template <int H>
+int launch_mean_src(int64_t N, const int32_t* rp, const int32_t* src, const int32_t* orp,
+                    const int32_t* odst, const int32_t* oslot, const float* Y, int64_t ldy,
+                    const float* elr, const float* attn, const float* g_out, int F, float slope,
+                    float* gpre, float* gY, int64_t ldgy, int C, uint32_t* gy_amax, uint32_t* gy_rows,
+                    hipStream_t st) {
+  const int nj = (int)ceil_div(F / 4, 64);
+  const unsigned b4 = (unsigned)ceil_div(N, 4), b256 = (unsigned)ceil_div(N, 256);
+#define MVML_MEAN_SRC(NJ) \
+  gat_mean_bwd_src_kernel<H, NJ><<<b4, 256, 0, st>>>(N, orp, odst, oslot, Y, ldy, attn, g_out, F, gpre, gY, \
+                                                     ldgy, gy_amax, gy_rows)
+  switch (nj) {
+    case 1: MVML_MEAN_SRC(1); break;
+    case 2: MVML_MEAN_SRC(2); break;
+    case 3: MVML_MEAN_SRC(3); break;
+    case 4: MVML_MEAN_SRC(4); break;
+    default: set_error("gat_agg_bwd: mean-src path needs F <= 1024"); return MVML_ERR_INVALID;
+  }
+#undef MVML_MEAN_SRC
+  int rc = check_launch("gat_mean_bwd_src_kernel");
+  if (rc) return rc;
+  gat_mean_bwd_softmax_kernel<H><<<b256, 256, 0, st>>>(N, rp, src, elr, attn, slope, gpre, gY, ldgy, C);
+  rc = check_launch("gat_mean_bwd_softmax_kernel");
+  if (rc) return rc;
+  gat_mean_bwd_gel_kernel<H><<<b256, 256, 0, st>>>(N, orp, oslot, gpre, gY, ldgy, C, gy_amax, gy_rows);
+  return check_launch("gat_mean_bwd_gel_kernel");
+}
+
 template <int H>
 int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, const int32_t* src,
                const float* Y, int64_t ldy, int F, const float* bias, float slope, int mode,
@@ -1613,6 +1806,9 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
                int64_t ldy, const float* elr, const float* attn, const float* out,
                const float* g_out, int F, float slope, int mode, float* gpre, float* gY,
                int64_t ldgy, int C, uint32_t* gy_amax, uint32_t* gy_rows, hipStream_t st) {
+  if (mode == 1 && option(MVML_OPT_MEAN_SRC) && F <= 1024)  // head-mean layer by source atom
+    return launch_mean_src<H>(N, rp, src, orp, odst, oslot, Y, ldy, elr, attn, g_out, F, slope, gpre, gY,
+                              ldgy, C, gy_amax, gy_rows, st);
   if (option(MVML_OPT_BWD_ATOMWISE)) G = 0;  // tests: the per-atom pair over every atom
   if (F % 32 == 0 && G > 0) {  // molecule groups: one pass over Z / g_out / dZ per group
 #ifndef MVML_BWD_CW64

@@ -91,6 +91,9 @@ __global__ void __launch_bounds__(kXThreads) gat_x_elr_kernel(int64_t N, int Fp,
 // Forward: edge softmax per (destination, head) in softmax_pair's order, then
 // AX[v,h] = sum_e a_e,h X[src_e] and the GEMM operand block [AX_h | X] per head, with its per-row
 // |max| bits; attn[e, h] (in-CSR slot order) for the backward.
+// The atom's 16 lanes take its in-edges 16 at a time, one edge per lane (source id and logits
+// loaded in parallel, not walked); the exp sums and the aggregation still run in edge order (each
+// lane reads edge j's value by a shuffle), so the values are softmax_pair's bit for bit.
 template <int H>
 __global__ void __launch_bounds__(kXThreads) gat_x_fwd_kernel(
     int64_t N, int Fp, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
@@ -98,48 +101,91 @@ __global__ void __launch_bounds__(kXThreads) gat_x_fwd_kernel(
     float* __restrict__ axc, uint32_t* __restrict__ arows) {
   const int64_t v = xcd_block(blockIdx.x, gridDim.x) * (kXThreads / kXLanes) + threadIdx.x / kXLanes;
   const int l = threadIdx.x % kXLanes, nc = Fp / 4;
-  if (v >= N) return;
-  float er[H], m[H], sum[H];
+  const int gb = (threadIdx.x & 63) & ~(kXLanes - 1);  // the atom's first lane in the wave
+  if (v >= N) return;  // (whole 16-lane groups: every shuffle below stays inside a live group)
+  float er[H];
   {
     const float* p = elr + v * 2 * H + H;
 #pragma unroll
-    for (int h = 0; h < H; ++h) { er[h] = p[h]; m[h] = -INFINITY; sum[h] = 0.f; }
+    for (int h = 0; h < H; ++h) er[h] = p[h];
   }
   const int eb = rowptr[v], ee = rowptr[v + 1];
-  for (int e = eb; e < ee; ++e) {
-    const float* el = elr + (int64_t)in_src[e] * 2 * H;
+  // logits of one 16-edge chunk, one edge per lane (-inf past the end)
+  auto logits = [&](int base, int& src, float (&s)[H]) {
+    const bool ok = base + l < ee;
+    src = ok ? in_src[base + l] : 0;
+    const float* el = elr + (int64_t)src * 2 * H;
 #pragma unroll
-    for (int h = 0; h < H; ++h) m[h] = fmaxf(m[h], leaky_x(el[h] + er[h], slope));
+    for (int h = 0; h < H; ++h) s[h] = ok ? leaky_x(el[h] + er[h], slope) : -INFINITY;
+  };
+  const bool one = ee - eb <= kXLanes;  // (group-uniform) the first chunk's logits are kept
+  int src0;
+  float s0[H], m[H], sum[H];
+  logits(eb, src0, s0);
+#pragma unroll
+  for (int h = 0; h < H; ++h) { m[h] = s0[h]; sum[h] = 0.f; }
+  for (int base = eb + kXLanes; base < ee; base += kXLanes) {
+    int sr;
+    float s[H];
+    logits(base, sr, s);
+#pragma unroll
+    for (int h = 0; h < H; ++h) m[h] = fmaxf(m[h], s[h]);
   }
-  for (int e = eb; e < ee; ++e) {
-    const float* el = elr + (int64_t)in_src[e] * 2 * H;
 #pragma unroll
-    for (int h = 0; h < H; ++h) sum[h] += expf(leaky_x(el[h] + er[h], slope) - m[h]);
+  for (int h = 0; h < H; ++h) m[h] = max16(m[h]);
+  for (int base = eb; base < ee; base += kXLanes) {
+    int sr;
+    float s[H], x[H];
+    if (one) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) s[h] = s0[h];
+    } else {
+      logits(base, sr, s);
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) x[h] = expf(s[h] - m[h]);  // exp(-inf) = 0 past the end
+    const int cnt = min(kXLanes, ee - base);
+    for (int j = 0; j < cnt; ++j)
+#pragma unroll
+      for (int h = 0; h < H; ++h) sum[h] += __shfl(x[h], gb + j, 64);
   }
   const bool v1 = l + kXLanes < nc;
   float4 acc[H][2];
 #pragma unroll
   for (int h = 0; h < H; ++h) acc[h][0] = acc[h][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int e = eb; e < ee; ++e) {
-    const int64_t u = in_src[e];
-    const float* el = elr + u * 2 * H;
-    float a[H];
+  for (int base = eb; base < ee; base += kXLanes) {
+    int src;
+    float s[H], a[H];
+    if (one) {
+      src = src0;
 #pragma unroll
-    for (int h = 0; h < H; ++h) a[h] = expf(leaky_x(el[h] + er[h], slope) - m[h]) / sum[h];
-    if (l == 0) {
-#pragma unroll
-      for (int h = 0; h < H; ++h) attn[(int64_t)e * H + h] = a[h];
+      for (int h = 0; h < H; ++h) s[h] = s0[h];
+    } else {
+      logits(base, src, s);
     }
-    const float* xr = X + u * Fp;
-    if (l < nc) {
-      const float4 x0 = ld4x(xr + 4 * l);
 #pragma unroll
-      for (int h = 0; h < H; ++h) acc[h][0] = fma4x(a[h], x0, acc[h][0]);
+    for (int h = 0; h < H; ++h) a[h] = expf(s[h] - m[h]) / sum[h];
+    if (base + l < ee) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) attn[(int64_t)(base + l) * H + h] = a[h];
     }
-    if (v1) {
-      const float4 x1 = ld4x(xr + 4 * (l + kXLanes));
+    const int cnt = min(kXLanes, ee - base);
+    for (int j = 0; j < cnt; j += 2) {  // two source rows in flight
+      const int j1 = min(j + 1, cnt - 1);
+      const float* xr0 = X + (int64_t)__shfl(src, gb + j, 64) * Fp;
+      const float* xr1 = X + (int64_t)__shfl(src, gb + j1, 64) * Fp;
+      float aj0[H], aj1[H];
 #pragma unroll
-      for (int h = 0; h < H; ++h) acc[h][1] = fma4x(a[h], x1, acc[h][1]);
+      for (int h = 0; h < H; ++h) { aj0[h] = __shfl(a[h], gb + j, 64); aj1[h] = __shfl(a[h], gb + j1, 64); }
+      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 x00 = l < nc ? ld4x(xr0 + 4 * l) : z4, x01 = v1 ? ld4x(xr0 + 4 * (l + kXLanes)) : z4;
+      const float4 x10 = l < nc ? ld4x(xr1 + 4 * l) : z4, x11 = v1 ? ld4x(xr1 + 4 * (l + kXLanes)) : z4;
+#pragma unroll
+      for (int h = 0; h < H; ++h) { acc[h][0] = fma4x(aj0[h], x00, acc[h][0]); acc[h][1] = fma4x(aj0[h], x01, acc[h][1]); }
+      if (j + 1 < cnt) {
+#pragma unroll
+        for (int h = 0; h < H; ++h) { acc[h][0] = fma4x(aj1[h], x10, acc[h][0]); acc[h][1] = fma4x(aj1[h], x11, acc[h][1]); }
+      }
     }
   }
   const float* xv = X + v * Fp;
@@ -158,8 +204,9 @@ __global__ void __launch_bounds__(kXThreads) gat_x_fwd_kernel(
   }
 }
 
-// Backward, per destination: g_a per in-edge from dAX (pass 1, kept in gpre), then the softmax /
-// LeakyReLU backward (lane 0, edge order): gpre[e] = g_pre, d er[v] -> gelr[v][H ..].
+// Backward, per destination: g_a per in-edge from dAX (a 16-lane dot per edge and head), then the
+// softmax / LeakyReLU backward with one edge per lane: gpre[e] = g_pre, d er[v] -> gelr[v][H ..].
+// Sums over the edges (sum a g_a, d er) run in edge order through shuffles, as the serial walk.
 template <int H>
 __global__ void __launch_bounds__(kXThreads) gat_x_bwd_kernel(
     int64_t N, int Fp, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
@@ -167,6 +214,7 @@ __global__ void __launch_bounds__(kXThreads) gat_x_bwd_kernel(
     float slope, const float* __restrict__ dax, float* __restrict__ gpre, float* __restrict__ gelr) {
   const int64_t v = xcd_block(blockIdx.x, gridDim.x) * (kXThreads / kXLanes) + threadIdx.x / kXLanes;
   const int l = threadIdx.x % kXLanes, nc = Fp / 4;
+  const int gb = (threadIdx.x & 63) & ~(kXLanes - 1);
   if (v >= N) return;
   const bool v0 = l < nc, v1 = l + kXLanes < nc;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -178,42 +226,84 @@ __global__ void __launch_bounds__(kXThreads) gat_x_bwd_kernel(
     d[h][1] = v1 ? ld4x(dr + h * Fp + 4 * (l + kXLanes)) : z4;
   }
   const int eb = rowptr[v], ee = rowptr[v + 1];
-  float S[H];
+  const bool one = ee - eb <= kXLanes;
+  float S[H], er[H];
 #pragma unroll
-  for (int h = 0; h < H; ++h) S[h] = 0.f;
-  for (int e = eb; e < ee; ++e) {
-    const float* xr = X + (int64_t)in_src[e] * Fp;
-    const float4 x0 = v0 ? ld4x(xr + 4 * l) : z4;
-    const float4 x1 = v1 ? ld4x(xr + 4 * (l + kXLanes)) : z4;
-    float ga[H];
+  for (int h = 0; h < H; ++h) { S[h] = 0.f; er[h] = elr[v * 2 * H + H + h]; }
+  float ga0[H], a0[H];  // the first chunk's g_a and attention, one edge per lane
+  int src0 = 0;
+  for (int base = eb; base < ee; base += kXLanes) {
+    const bool ok = base + l < ee;
+    const int src = ok ? in_src[base + l] : 0;
+    float ga[H], a[H];
 #pragma unroll
-    for (int h = 0; h < H; ++h) ga[h] = sum16(dot4x(d[h][0], x0) + dot4x(d[h][1], x1));
-    if (l == 0) {
-      const float* ap = attn + (int64_t)e * H;
+    for (int h = 0; h < H; ++h) { ga[h] = 0.f; a[h] = ok ? attn[(int64_t)(base + l) * H + h] : 0.f; }
+    const int cnt = min(kXLanes, ee - base);
+    for (int j = 0; j < cnt; j += 2) {  // two source rows in flight
+      const int j1 = min(j + 1, cnt - 1);
+      const float* xr0 = X + (int64_t)__shfl(src, gb + j, 64) * Fp;
+      const float* xr1 = X + (int64_t)__shfl(src, gb + j1, 64) * Fp;
+      const float4 x00 = v0 ? ld4x(xr0 + 4 * l) : z4, x01 = v1 ? ld4x(xr0 + 4 * (l + kXLanes)) : z4;
+      const float4 x10 = v0 ? ld4x(xr1 + 4 * l) : z4, x11 = v1 ? ld4x(xr1 + 4 * (l + kXLanes)) : z4;
 #pragma unroll
       for (int h = 0; h < H; ++h) {
-        S[h] += ap[h] * ga[h];
-        gpre[(int64_t)e * H + h] = ga[h];
+        const float t0 = sum16(dot4x(d[h][0], x00) + dot4x(d[h][1], x01));
+        const float t1 = sum16(dot4x(d[h][0], x10) + dot4x(d[h][1], x11));
+        ga[h] = l == j ? t0 : l == j1 ? t1 : ga[h];
       }
     }
-  }
-  if (l != 0) return;
-  float er[H], ger[H];
+    for (int j = 0; j < cnt; ++j)
 #pragma unroll
-  for (int h = 0; h < H; ++h) { er[h] = elr[v * 2 * H + H + h]; ger[h] = 0.f; }
-  for (int e = eb; e < ee; ++e) {
-    const float* el = elr + (int64_t)in_src[e] * 2 * H;
+      for (int h = 0; h < H; ++h) S[h] += __shfl(a[h] * ga[h], gb + j, 64);
+    if (base == eb) {
+      src0 = src;
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-      const float a = attn[(int64_t)e * H + h];
-      const float gs = a * (gpre[(int64_t)e * H + h] - S[h]);
-      const float gp = (el[h] + er[h]) > 0.f ? gs : gs * slope;
-      gpre[(int64_t)e * H + h] = gp;
-      ger[h] += gp;
+      for (int h = 0; h < H; ++h) { ga0[h] = ga[h]; a0[h] = a[h]; }
+    }
+    if (!one && ok) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) gpre[(int64_t)(base + l) * H + h] = ga[h];
     }
   }
+  float ger[H];
 #pragma unroll
-  for (int h = 0; h < H; ++h) gelr[v * 2 * H + H + h] = ger[h];
+  for (int h = 0; h < H; ++h) ger[h] = 0.f;
+  for (int base = eb; base < ee; base += kXLanes) {
+    const bool ok = base + l < ee;
+    int src;
+    float ga[H], a[H];
+    if (one) {
+      src = src0;
+#pragma unroll
+      for (int h = 0; h < H; ++h) { ga[h] = ga0[h]; a[h] = a0[h]; }
+    } else {
+      src = ok ? in_src[base + l] : 0;
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        ga[h] = ok ? gpre[(int64_t)(base + l) * H + h] : 0.f;
+        a[h] = ok ? attn[(int64_t)(base + l) * H + h] : 0.f;
+      }
+    }
+    const float* el = elr + (int64_t)src * 2 * H;
+    float gp[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float gs = a[h] * (ga[h] - S[h]);
+      gp[h] = ok ? ((el[h] + er[h]) > 0.f ? gs : gs * slope) : 0.f;
+    }
+    if (ok) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) gpre[(int64_t)(base + l) * H + h] = gp[h];
+    }
+    const int cnt = min(kXLanes, ee - base);
+    for (int j = 0; j < cnt; ++j)
+#pragma unroll
+      for (int h = 0; h < H; ++h) ger[h] += __shfl(gp[h], gb + j, 64);
+  }
+  if (l == 0) {
+#pragma unroll
+    for (int h = 0; h < H; ++h) gelr[v * 2 * H + H + h] = ger[h];
+  }
 }
 
 // d el[u] = sum over u's out-edges of g_pre (out-CSR order), and the |max| of u's [d el | d er]

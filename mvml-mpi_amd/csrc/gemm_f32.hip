@@ -491,7 +491,8 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
                                              const float* __restrict__ bias, float beta, int act,
                                              float* __restrict__ C, int64_t ldc,
                                              float* __restrict__ slab, const CellEpi& cep = CellEpi{},
-                                             const int* rs = nullptr, const EpiX& ex = EpiX{});
+                                             const int* rs = nullptr, const EpiX& ex = EpiX{},
+                                             uint32_t* s_rm = nullptr);
 
 // Undo the split-fp16 operand scales of a 128x128 tile's 2 x 2 accumulators (exact: powers of
 // two).  Per-row A maxima: lane li scaled A rows 32 i + li of its wave's 64 (shift ka0 / ka1);
@@ -1149,18 +1150,31 @@ __device__ __forceinline__ void wave_sync_lds() {
 // max |stored value| (columns past N neither stored nor counted).
 __device__ __forceinline__ float epix_store4(const float* src, float* __restrict__ out, int64_t ld,
                                             int64_t N, int64_t row, int64_t col, float ua,
-                                            const float* __restrict__ bias, float beta, int act,
+                                            bool hb, const float (&bv)[4], float beta, int act,
                                             const float* __restrict__ aux, int64_t ld_aux, bool vec) {
   const float4 t = *reinterpret_cast<const float4*>(src);
   float e0 = t.x * ua, e1 = t.y * ua, e2 = t.z * ua, e3 = t.w * ua;
   float* cp = out + row * ld + col;
   const bool full = col + 3 < N;
+  // act 3: the four aux values of a full, 16-B aligned piece in one load (ld_aux % 4 == 0 and
+  // aux 16-B aligned: col is a multiple of 4)
+  float ax[4] = {0.f, 0.f, 0.f, 0.f};
+  if (act == 3) {
+    const float* ap = aux + row * ld_aux + col;
+    if (full && vec && (ld_aux & 3) == 0 && ((uintptr_t)aux & 15) == 0) {
+      const float4 a4 = *reinterpret_cast<const float4*>(ap);
+      ax[0] = a4.x; ax[1] = a4.y; ax[2] = a4.z; ax[3] = a4.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ax[u] = col + u < N ? ap[u] : 0.f;
+    }
+  }
   auto fin = [&](float x, int u) __attribute__((always_inline)) -> float {
-    if (bias) x += bias[col + u];
+    if (hb) x += bv[u];
     if (beta != 0.f) x += beta * cp[u];
     if (act == 1) x = fmaxf(x, 0.f);
     if (act == 2) x = elu_epi(x);
-    if (act == 3) x *= elu_grad_epi(aux[row * ld_aux + col + u]);
+    if (act == 3) x *= elu_grad_epi(ax[u]);
     return x;
   };
   e0 = fin(e0, 0);
@@ -1184,7 +1198,10 @@ __device__ __forceinline__ float epix_store4(const float* src, float* __restrict
 // epilogue_lds), then stores through epix_store4, per-row maxima (a row's 16 lanes reduce, one
 // atomicMax per row slot) and the tile's |max| (one atomicMax per wave).  The row blocks are
 // unrolled by construction (a fold over the block index) so the accumulators stay in registers;
-// the store loop inside is not unrolled.
+// the store loop inside is not unrolled.  The bias of the lane's four columns (the same for every
+// row it stores) is loaded once.  s_rm (LDS, the wave's rows of the tile): the per-row maxima
+// are folded there (LDS atomics) and the kernel commits one global atomicMax per row and
+// workgroup after the epilogue, instead of one per row and wave.
 template <int... Is, typename Fn>
 __device__ __forceinline__ void static_for_x(std::integer_sequence<int, Is...>, Fn&& fn) {
   (fn(std::integral_constant<int, Is>{}), ...);
@@ -1194,9 +1211,15 @@ __device__ __forceinline__ void epix_tile(const f32x16 (&acc)[FM][2], float* wl,
                                           int64_t r0, int64_t c0, int lane,
                                           const float* __restrict__ bias, float beta, int act,
                                           float* __restrict__ out, int64_t ld, bool vec, const int* rs,
-                                          const EpiX& ex) {
+                                          const EpiX& ex, uint32_t* s_rm) {
   const int li = lane & 31, lk = lane >> 5;
   float am = 0.f;
+  float bv[4];
+  {
+    const int64_t cb = c0 + (lane & 15) * 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bv[u] = (bias && cb + u < N) ? bias[cb + u] : 0.f;
+  }
   static_for_x(std::make_integer_sequence<int, FM>{}, [&](auto I) __attribute__((always_inline)) {
     constexpr int i = decltype(I)::value;
     if (i > 0) wave_sync_lds();
@@ -1213,14 +1236,18 @@ __device__ __forceinline__ void epix_tile(const f32x16 (&acc)[FM][2], float* wl,
       float rm = 0.f;
       if (row < M && col < N)
         rm = epix_store4(wl + rr * kEpiLd + c4, out, ld, N, row, col, rs ? pow2f(-rs[32 * i + rr]) : 1.f,
-                         bias, beta, act, ex.aux, ex.ld_aux, vec);
+                         bias != nullptr, bv, beta, act, ex.aux, ex.ld_aux, vec);
       am = fmaxf(am, rm);
       if (ex.c_rows) {  // (uniform) the row's 16 lanes reduce together
 #pragma unroll
         for (int o = 8; o >= 1; o >>= 1) rm = fmaxf(rm, __shfl_xor(rm, o, 64));
         if ((lane & 15) == 0 && row < M) {
-          const int64_t slot = ex.rows_cols > 0 ? c0 / ex.rows_cols : 0;
-          atomicMax(ex.c_rows + blockIdx.z * ex.crows_z + slot * ex.rows_stride + row, __float_as_uint(rm));
+          if (s_rm) {
+            atomicMax(s_rm + 32 * i + rr, __float_as_uint(rm));
+          } else {
+            const int64_t slot = ex.rows_cols > 0 ? c0 / ex.rows_cols : 0;
+            atomicMax(ex.c_rows + blockIdx.z * ex.crows_z + slot * ex.rows_stride + row, __float_as_uint(rm));
+          }
         }
       }
     }
@@ -1237,7 +1264,7 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
                                                  const float* __restrict__ bias, float beta, int act,
                                                  float* __restrict__ C, int64_t ldc,
                                                  float* __restrict__ slab, const CellEpi& cep,
-                                                 const int* rs, const EpiX& ex) {
+                                                 const int* rs, const EpiX& ex, uint32_t* s_rm) {
   // rs (per-row A maxima): rs[32 i + rr] = the scale shift of row r0 + 32 i + rr, undone here as
   // each row leaves (acc already carries B's)
   const int li = lane & 31, lk = lane >> 5;
@@ -1252,7 +1279,7 @@ __device__ __forceinline__ void epilogue_lds(const f32x16 (&acc)[FM][2], float* 
   // EpiX work (act 2 / 3, folded maxima): its own tile pass, never with split-K or the cell
   if constexpr (EX) {
     if (!slab && cep.D == 0 && (act >= 2 || ex.c_amax || ex.c_rows)) {
-      epix_tile<FM>(acc, wl, M, N, r0, c0, lane, bias, beta, act, out, ld, vec, rs, ex);
+      epix_tile<FM>(acc, wl, M, N, r0, c0, lane, bias, beta, act, out, ld, vec, rs, ex, s_rm);
       return;
     }
   }
@@ -1487,6 +1514,10 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   }
   const float s_a = pow2f(ka), s_b = pow2f(kb);
   __shared__ int rsh[ROWS ? XBM : 1];
+  // EX: per-row maxima of the tile folded in LDS, committed once per row (rows_cols 0 or whole
+  // tiles: one slot per row of the workgroup)
+  __shared__ uint32_t s_rmax[EX ? XBM : 1];
+  const bool lds_rows = EX && ex.c_rows && !slab && cep.D == 0 && (ex.rows_cols == 0 || ex.rows_cols % XBN == 0);
   // KS 16-deep sub-stages per barrier (split-fp16: 2, so a stage carries as many MFMAs as the
   // split-bf16 one); a sub-stage's LDS image is exactly the KS = 1 stage layout
   constexpr int KS = (NP == 2) ? MVML_H2_KS : 1;
@@ -1522,6 +1553,9 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     for (int i = 0; i < OA::NI; ++i) sa_i[i] = pow2f(row_shift(amax, m0 + (tid >> 2) + OA::RS * i, M));
     // every row's shift for the epilogue (read after the K loop's barriers)
     if (tid < XBM) rsh[tid] = row_shift(amax, m0 + tid, M);
+  }
+  if constexpr (EX) {
+    if (lds_rows && tid < XBM) s_rmax[tid] = 0u;  // (read after the K loop's barriers)
   }
 
   f32x16 acc[4][2];
@@ -1879,7 +1913,16 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
                                          act, C, ldc, slab, epi);
   epilogue_lds<4, EX>(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
                       n0 + wn * 64, lane, bias, beta, act, C, ldc, slab, cep,
-                      (ROWS && ntiles > 0) ? rsh + wm * 128 : nullptr, ex);
+                      (ROWS && ntiles > 0) ? rsh + wm * 128 : nullptr, ex,
+                      lds_rows ? s_rmax + wm * 128 : nullptr);
+  if constexpr (EX) {
+    if (lds_rows) {  // (uniform) one global atomicMax per row of the tile
+      __syncthreads();
+      const int64_t slot = ex.rows_cols > 0 ? n0 / ex.rows_cols : 0;
+      if (tid < XBM && m0 + tid < M && s_rmax[tid] != 0u)
+        atomicMax(ex.c_rows + blockIdx.z * ex.crows_z + slot * ex.rows_stride + m0 + tid, s_rmax[tid]);
+    }
+  }
 #else
   static_assert(NP != 2, "per-row A maxima need the LDS epilogue");
   tile_epilogue<EPI_LOGW, 4, 2>(acc, M, N, m0 + wm * 128, n0 + wn * 64, lane, bias, beta, act, C,

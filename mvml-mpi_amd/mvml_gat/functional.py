@@ -4,6 +4,7 @@ Each Function owns one stage of GNNModule (model.py:89-95) and calls only the C 
 no PyTorch math on the hot path besides allocation (and nn.Dropout, which the reference
 applies with torch's own RNG, model.py:87).
 """
+import contextlib
 import ctypes
 import os
 
@@ -240,8 +241,18 @@ def colsum(X, M, N, ldx, out, beta=0.0, offset=0, alpha=1.0):
 # The first GATConv (narrow input: Fp = 76 features, flatten heads) re-associated: the edge
 # softmax and aggregation run over the feature rows and one batched GEMM per head forms the
 # output (mvml_gat_x_fwd + mvml_gemm_f16x2_ex, see csrc/gat_x.hip) instead of projecting every
-# atom to 2 H F + 2 H columns and aggregating those.  MVML_GAT_REASSOC=0: the projection path.
-REASSOC_X = os.environ.get("MVML_GAT_REASSOC", "1") != "0"
+# atom to 2 H F + 2 H columns and aggregating those.  Off by default (MVML_GAT_REASSOC=1 turns it
+# on): measured slower on configs 3 and 5 (401 k vs 416 k mol/s on config 3; the K = 152 per-head
+# GEMMs and the per-head weight gradients cost more than the projection's Y round trip saves,
+# DESIGN.md "Layer 1 by re-association").
+REASSOC_X = os.environ.get("MVML_GAT_REASSOC", "0") == "1"
+
+# Head-mean layer backward by source atom (csrc/gat_agg.hip gat_mean_bwd_src_kernel) for batches
+# whose atoms sit mostly in molecules past the LDS molecule window (config 5: 150-400 atoms, where
+# it beats the big-window kernel 12.9 vs 18.2 ms); the molecule-window kernel stays faster on
+# drug-sized molecules (6.8 vs 7.3 ms on config 3).  MVML_MEAN_SRC_AUTO=0: never by this rule.
+MEAN_SRC_AUTO = os.environ.get("MVML_MEAN_SRC_AUTO", "1") != "0"
+MEAN_SRC_MIN_ATOMS = 128  # the LDS molecule window (gat_agg.hip kWinL)
 
 
 class EluLink:
@@ -501,10 +512,14 @@ class GATLayerFunction(torch.autograd.Function):
              ptr(gl), st)
         # dL/dWcat in the projection path's layout [fc | res_fc | A_l | A_r] rows
         gW = torch.empty((C + 2 * H, Fp), dtype=torch.float32, device=dev)
-        for h in range(H):  # dL/dW_h = g_rst_h^T AX_h (split-K over atoms)
-            gemm(g_rst[:, h * F:], axc[:, h * 2 * Fp:], F, Fp, N, 1, 1, HF, H * 2 * Fp, gW[h * F:], Fp,
+        # [dL/dW_h | dL/dWres_h] = g_rst_h^T [AX_h | X]: one split-K product per head over its
+        # whole [AX_h | X] block (the res_fc gradient rows come out of the same pass)
+        gWh = torch.empty((H, F, 2 * Fp), dtype=torch.float32, device=dev)
+        for h in range(H):
+            gemm(g_rst[:, h * F:], axc[:, h * 2 * Fp:], F, 2 * Fp, N, 1, 1, HF, H * 2 * Fp, gWh[h], 2 * Fp,
                  amax=(gp, slot(amx, 2)))
-        gemm(g_rst, Xp, HF, Fp, N, 1, 1, HF, Fp, gW[HF:], Fp, amax=(gp, slot(amx, 0)))  # res_fc
+        gW[:HF].view(H, F, Fp).copy_(gWh[:, :, :Fp])
+        gW[HF:C].view(H, F, Fp).copy_(gWh[:, :, Fp:])
         gemm(gelr, Xp, 2 * H, Fp, N, 1, 1, 2 * H, Fp, gW[C:], Fp, amax=(slot(gl, 0), slot(amx, 0)))
         g_fc = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_res = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
@@ -546,13 +561,18 @@ class GATLayerFunction(torch.autograd.Function):
             gyr = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}",
                             "bytes": agg_bwd_bytes(N, g.num_edges(), H, F, g_out.shape[1], mode)}
-        call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
-             ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr),
-             ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldg,
-             slot(ctx.amx, 2), ptr(gyr), wp, wn, st)
+        src_path = (MEAN_SRC_AUTO and mode == MODE_MEAN
+                    and g.large_molecule_fraction(MEAN_SRC_MIN_ATOMS) >= 0.5)
+        with (_lib.option("mean_src", 1) if src_path else contextlib.nullcontext()):
+            call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
+                 ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy,
+                 ptr(elr), ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY),
+                 ldg, slot(ctx.amx, 2), ptr(gyr), wp, wn, st)
         amx = ctx.amx  # slot 2 = max |gY|, folded in by mvml_gat_agg_bwd's stores
         if DEBUG_CAPTURE is not None and amx is not None:
             DEBUG_CAPTURE.setdefault("gy_amax", []).append((gY[:, :CE].clone(), amx[2:3].clone()))
+            if gyr is not None:
+                DEBUG_CAPTURE.setdefault("gy_rows", []).append(gyr.clone())
         # dL/d[Wcat ; A_l ; A_r] = gY^T X  (split-K over atoms)
         gW = torch.empty((CE, Fp), dtype=torch.float32, device=dev)
         gemm(gY, Xp, CE, Fp, N, 1, 1, ldg, Fp, gW, Fp, algo=ctx.algo,

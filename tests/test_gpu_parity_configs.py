@@ -205,7 +205,7 @@ def test_gat_layer0_hubs_flatten_elu():
 
 @pytest.mark.parametrize("case", ["config2", "hubs", "config5", "config5_three", "table_overflow",
                                   "config3"])
-def test_gat_layer0_reassociated(case):
+def test_gat_layer0_reassociated(case, monkeypatch):
     """The first layer as GNNModule runs it (no input gradient): edge softmax + aggregation over
     the 76-wide feature rows and one batched GEMM per head (mvml_gat_x_fwd, mvml_gemm_f16x2_ex),
     backward through dAX = g_rst W_h (mvml_gat_x_bwd) — every output and gradient against float64
@@ -217,35 +217,43 @@ def test_gat_layer0_reassociated(case):
           "config5_three": lambda: synth.config5(3, seed=5),
           "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109),
           "config3": lambda: synth.config3(192, seed=4)}[case]()
+    monkeypatch.setattr(Fn, "REASSOC_X", True)  # (off by default: measured slower)
     _layer_case(0, sb, seed=11, x_grad=False)
 
 
-def test_gat_layer1_config5():
+@pytest.mark.parametrize("auto", [True, False])
+def test_gat_layer1_config5(auto, monkeypatch):
+    """The head-mean layer on config 5: by default its backward takes the source-atom kernel
+    (functional.MEAN_SRC_AUTO, the molecules exceed the LDS window); off, the big window."""
+    monkeypatch.setattr(Fn, "MEAN_SRC_AUTO", auto)
     _layer_case(1, synth.config5(2, seed=3), seed=4)
 
 
 @pytest.mark.parametrize("layer", [0, 1])
-def test_gat_layer_config5_fallback_kernels(layer):
+def test_gat_layer_config5_fallback_kernels(layer, monkeypatch):
     """Option big_window = 0: config-5 groups through the per-atom fallbacks (forward gather
-    with its hub pass, dst / src backward pair) — the path of groups past the big window's caps."""
+    with its hub pass, dst / src backward pair) — the path of groups past the big window's caps
+    (the head-mean layer's source-atom backward, picked for such batches, turned off)."""
+    monkeypatch.setattr(Fn, "MEAN_SRC_AUTO", False)
     with option("big_window", 0):
         _layer_case(layer, synth.config5(2, seed=3), seed=4 + layer)
 
 
 @pytest.mark.parametrize("layer", [0, 1])
-def test_gat_layer_big_window_table_overflow(layer):
+def test_gat_layer_big_window_table_overflow(layer, monkeypatch):
     """A 300-atom molecule with 7 hubs of 109 partners (2428 edges, at the big window's edge
     cap): the backward's staged out-edges (640) and out-edge segments (48) overflow, so the
     last hubs walk their out-edges from global memory on their own lanes."""
     sb = batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109)
     assert int(sb.num_edges[0]) <= 2432
+    monkeypatch.setattr(Fn, "MEAN_SRC_AUTO", False)  # the big-window backward itself
     _layer_case(layer, sb, seed=5 + layer)
 
 
 @pytest.mark.parametrize("layer", [0, 1])
 @pytest.mark.parametrize("case", ["config2", "config5_big", "config5_fallback", "table_overflow",
                                   "atomwise"])
-def test_gat_bwd_fused_gy_max(layer, case):
+def test_gat_bwd_fused_gy_max(layer, case, monkeypatch):
     """mvml_gat_agg_bwd folds max |gY| (the split-fp16 scale of the dL/dW and dL/dX GEMMs) into
     its stores: it must equal the max over every column the GEMMs read, [dZ | dR | d el | d er],
     on every kernel path that writes gY (LDS windows, big windows, the dst / src fallback pair
@@ -258,8 +266,51 @@ def test_gat_bwd_fused_gy_max(layer, case):
           "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109),
           "atomwise": lambda: synth.config3(128, seed=2)}[case]()
     opts = {"config5_fallback": ("big_window", 0), "atomwise": ("bwd_atomwise", 1)}
+    monkeypatch.setattr(Fn, "MEAN_SRC_AUTO", False)  # each kernel path named by the case
     with option(*opts.get(case, ("big_window", 1))):
         _gy_max_case(layer, sb)
+
+
+@pytest.mark.parametrize("case", ["config2", "config5", "hubs", "table_overflow", "config3"])
+def test_gat_layer1_mean_src(case):
+    """Option mean_src = 1: the head-mean layer's aggregation backward by SOURCE atom
+    (gat_mean_bwd_src_kernel: one wave per atom reads its projection row once and gathers the
+    F-wide g_out rows of its out-edges; softmax / d el passes per atom) — forward and every
+    gradient against float64 on each graph family, hubs and the 2,428-edge molecule included."""
+    sb = {"config2": lambda: synth.config2(128, seed=0),
+          "config5": lambda: synth.config5(2, seed=3),
+          "hubs": lambda: batch_of_sizes([150, 90, 210], seed=7, hubs=True),
+          "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109),
+          "config3": lambda: synth.config3(192, seed=4)}[case]()
+    with option("mean_src", 1):
+        _layer_case(1, sb, seed=6)
+
+
+@pytest.mark.parametrize("mean_src", [0, 1])
+@pytest.mark.parametrize("case", ["config2", "config5"])
+def test_gat_bwd_gy_row_maxima(case, mean_src):
+    """The per-row max |gY| the aggregation backward folds into its stores (the dL/dX GEMM's
+    per-row split-fp16 scales) equals each row's max over [dZ | dR | d el | d er]."""
+    if Fn.GEMM_ALGO != "f16x2" or not Fn.ROW_SCALES:
+        pytest.skip("per-row maxima feed the per-row split-fp16 GEMM only")
+    sb = {"config2": lambda: synth.config2(64, seed=0), "config5": lambda: synth.config5(2, seed=3)}[case]()
+    with option("mean_src", mean_src):
+        cap = _gy_max_case(1, sb)
+    (gY, _), = cap["gy_amax"]
+    rows, = cap["gy_rows"]
+    want = gY.abs().max(dim=1).values
+    got = rows.view(torch.float32)[:gY.shape[0]]
+    assert torch.equal(got, want), (got - want).abs().max().item()
+
+
+@pytest.mark.parametrize("case", ["config2", "config5", "table_overflow"])
+def test_gat_bwd_fused_gy_max_mean_src(case):
+    sb = {"config2": lambda: synth.config2(64, seed=0), "config5": lambda: synth.config5(2, seed=3),
+          "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109)}[case]()
+    if Fn.GEMM_ALGO != "f16x2":
+        pytest.skip("the fused max feeds the split-fp16 GEMMs only")
+    with option("mean_src", 1):
+        _gy_max_case(1, sb)
 
 
 def _gy_max_case(layer, sb):
@@ -285,3 +336,4 @@ def _gy_max_case(layer, sb):
     t, i = out._mvml_amax[:2]
     got_o = t[i:i + 1].cpu().view(torch.float32).item()
     assert got_o == out.detach().abs().max().item(), (got_o, out.detach().abs().max().item())
+    return cap
