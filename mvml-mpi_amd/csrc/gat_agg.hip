@@ -1641,25 +1641,39 @@ gat_mean_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
 #pragma unroll
         for (int h = 0; h < H; ++h) a_l[h] = attn[(int64_t)s_l * H + h];
       }
-#pragma unroll 2
-      for (int j = 0; j < cnt; ++j) {
-        const float* gw = g_out + (int64_t)rl(w_l, j) * F;
-        float a[H], part[H];
-#pragma unroll
-        for (int h = 0; h < H; ++h) { a[h] = rl(a_l[h], j); part[h] = 0.f; }
+      // two out-edges per trip: both g_out rows are loaded before either is used
+      for (int j = 0; j < cnt; j += 2) {
+        const int j1 = min(j + 1, cnt - 1);
+        const bool two = j + 1 < cnt;  // (uniform)
+        const float* gw0 = g_out + (int64_t)rl(w_l, j) * F;
+        const float* gw1 = g_out + (int64_t)rl(w_l, j1) * F;
+        float4 g0[NJ], g1[NJ];
 #pragma unroll
         for (int jj = 0; jj < NJ; ++jj) {
-          if (!okj[jj]) continue;
-          float4 g = ld4(gw + 4 * (lane + 64 * jj));
-          g = make_float4(g.x / hh, g.y / hh, g.z / hh, g.w / hh);
+          g0[jj] = okj[jj] ? ld4(gw0 + 4 * (lane + 64 * jj)) : f4(0.f);
+          g1[jj] = okj[jj] ? ld4(gw1 + 4 * (lane + 64 * jj)) : f4(0.f);
+        }
+        float a0[H], a1[H], p0[H], p1[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) { a0[h] = rl(a_l[h], j); a1[h] = rl(a_l[h], j1); p0[h] = 0.f; p1[h] = 0.f; }
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj) {
+          const float4 ga4 = make_float4(g0[jj].x / hh, g0[jj].y / hh, g0[jj].z / hh, g0[jj].w / hh);
+          const float4 gb4 = make_float4(g1[jj].x / hh, g1[jj].y / hh, g1[jj].z / hh, g1[jj].w / hh);
 #pragma unroll
           for (int h = 0; h < H; ++h) {
-            dz[h][jj] = fma4(a[h], g, dz[h][jj]);
-            part[h] += dot4(z[h][jj], g);
+            dz[h][jj] = fma4(a0[h], ga4, dz[h][jj]);
+            p0[h] += dot4(z[h][jj], ga4);
+            if (two) dz[h][jj] = fma4(a1[h], gb4, dz[h][jj]);
+            p1[h] += dot4(z[h][jj], gb4);
           }
         }
-        HeadReduce<H>::template all<false>(part, lane);
-        store_heads<H>(ga + (int64_t)rl(s_l, j) * H, part, lane);
+        HeadReduce<H>::template all<false>(p0, lane);
+        store_heads<H>(ga + (int64_t)rl(s_l, j) * H, p0, lane);
+        if (two) {
+          HeadReduce<H>::template all<false>(p1, lane);
+          store_heads<H>(ga + (int64_t)rl(s_l, j1) * H, p1, lane);
+        }
       }
     }
 #pragma unroll

@@ -24,9 +24,17 @@ ENTRIES = {  # C-ABI entry point -> its kernels (name substrings; "[big]": the b
     "gat_agg_fwd": ["gat_softmax_kernel", "gat_agg_fwd_lds_kernel", "gat_agg_fwd_lds_kernel[big]",
                     "gat_agg_fwd_gather_kernel"],
     "gat_agg_bwd": ["gat_agg_bwd_lds_kernel", "gat_agg_bwd_lds_kernel[big]", "gat_agg_bwd_dst_kernel",
-                    "gat_agg_bwd_src_kernel"],
+                    "gat_agg_bwd_src_kernel", "gat_mean_bwd_src_kernel", "gat_mean_bwd_softmax_kernel",
+                    "gat_mean_bwd_gel_kernel"],
     "set2set_seg_fwd": ["seg_fwd_kernel"],
 }
+# kernels launched exactly once per entry-point call, whichever path the call takes (a call of
+# mvml_gat_agg_bwd launches the molecule-window kernel, or — head-mean layer by source atom —
+# gat_mean_bwd_src_kernel instead): the per-launch traffic is the entry's kernels' total over
+# the number of calls, so layers on different kernel paths average correctly
+ANCHORS = {"gat_agg_fwd": ["gat_agg_fwd_lds_kernel"],
+           "gat_agg_bwd": ["gat_agg_bwd_lds_kernel", "gat_mean_bwd_src_kernel"],
+           "set2set_seg_fwd": ["seg_fwd_kernel"]}
 
 
 def _pattern(name, pat):
@@ -66,8 +74,12 @@ def main():
     write = read_counter(a.write_dir, "WRITE_SIZE")
     out = {}
     for entry, pats in ENTRIES.items():
-        f_kb = sum(sum(fetch[(entry, p)]) / len(fetch[(entry, p)]) for p in pats if fetch.get((entry, p)))
-        w_kb = sum(sum(write[(entry, p)]) / len(write[(entry, p)]) for p in pats if write.get((entry, p)))
+        calls_f = sum(len(fetch.get((entry, p), [])) for p in ANCHORS[entry])
+        calls_w = sum(len(write.get((entry, p), [])) for p in ANCHORS[entry])
+        if not calls_f or not calls_w:
+            continue
+        f_kb = sum(sum(fetch[(entry, p)]) for p in pats if fetch.get((entry, p))) / calls_f
+        w_kb = sum(sum(write[(entry, p)]) for p in pats if write.get((entry, p))) / calls_w
         if not f_kb:
             continue
         out[entry] = {"kernels": {p: {"launches": len(fetch.get((entry, p), [])),
@@ -76,6 +88,7 @@ def main():
                                       "write_size_kb": round(sum(write[(entry, p)]) / len(write[(entry, p)]), 1)
                                       if write.get((entry, p)) else None} for p in pats},
                       "hbm_bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024),
+                      "calls": calls_f,
                       "correction": "read = 2 x FETCH_SIZE (gfx950 16-B/lane reads), write = WRITE_SIZE; "
                                     "averaged over both GAT layers"}
     try:
