@@ -63,10 +63,11 @@ const char* mvml_version(void);
                                    row count, 128 / 256 = forced; 128 also moves
                                    mvml_lstm_gates_cell_fwd to the 128x128 kernel (measured
                                    slower there at 65,536 rows: 0.78 vs 0.70 ms) */
-#define MVML_OPT_MEAN_SRC 7     /* MVML_MEAN_SRC: 1 = head-mean (last) GAT layer's aggregation
-                                   backward by source atom (one wave per atom reads its projection
-                                   row once and gathers the F-wide g_out rows of its out-edges;
-                                   no LDS windows), 0 = molecule / big windows + per-atom pair */
+#define MVML_OPT_MEAN_SRC 7     /* MVML_MEAN_SRC: 1 (default) = head-mean (last) GAT layer's
+                                   aggregation backward by source atom (one wave per atom reads its
+                                   projection row once and gathers the F-wide g_out rows of its
+                                   out-edges; no LDS windows), 0 = molecule / big windows +
+                                   per-atom pair */
 int mvml_set_option(int option, int value);
 int mvml_get_option(int option);
 

@@ -44,7 +44,7 @@ static const bool g_opt_init = [] {
   g_opt[MVML_OPT_GEMM_NSPLIT] = env_int("MVML_GEMM_NSPLIT", 1);
   g_opt[MVML_OPT_GEMM_RING] = env_int("MVML_GEMM_RING", 0);
   g_opt[MVML_OPT_LSTM_TILE] = env_int("MVML_LSTM_TILE", 0);
-  g_opt[MVML_OPT_MEAN_SRC] = env_int("MVML_MEAN_SRC", 0);
+  g_opt[MVML_OPT_MEAN_SRC] = env_int("MVML_MEAN_SRC", 1);
   return true;
 }();
 

@@ -4,7 +4,6 @@ Each Function owns one stage of GNNModule (model.py:89-95) and calls only the C 
 no PyTorch math on the hot path besides allocation (and nn.Dropout, which the reference
 applies with torch's own RNG, model.py:87).
 """
-import contextlib
 import ctypes
 import os
 
@@ -247,12 +246,7 @@ def colsum(X, M, N, ldx, out, beta=0.0, offset=0, alpha=1.0):
 # DESIGN.md "Layer 1 by re-association").
 REASSOC_X = os.environ.get("MVML_GAT_REASSOC", "0") == "1"
 
-# Head-mean layer backward by source atom (csrc/gat_agg.hip gat_mean_bwd_src_kernel) for batches
-# whose atoms sit mostly in molecules past the LDS molecule window (config 5: 150-400 atoms, where
-# it beats the big-window kernel 12.9 vs 18.2 ms); the molecule-window kernel stays faster on
-# drug-sized molecules (6.8 vs 7.3 ms on config 3).  MVML_MEAN_SRC_AUTO=0: never by this rule.
-MEAN_SRC_AUTO = os.environ.get("MVML_MEAN_SRC_AUTO", "1") != "0"
-MEAN_SRC_MIN_ATOMS = 128  # the LDS molecule window (gat_agg.hip kWinL)
+
 
 
 class EluLink:
@@ -561,13 +555,10 @@ class GATLayerFunction(torch.autograd.Function):
             gyr = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}",
                             "bytes": agg_bwd_bytes(N, g.num_edges(), H, F, g_out.shape[1], mode)}
-        src_path = (MEAN_SRC_AUTO and mode == MODE_MEAN
-                    and g.large_molecule_fraction(MEAN_SRC_MIN_ATOMS) >= 0.5)
-        with (_lib.option("mean_src", 1) if src_path else contextlib.nullcontext()):
-            call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
-                 ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy,
-                 ptr(elr), ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY),
-                 ldg, slot(ctx.amx, 2), ptr(gyr), wp, wn, st)
+        call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
+             ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr),
+             ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldg,
+             slot(ctx.amx, 2), ptr(gyr), wp, wn, st)
         amx = ctx.amx  # slot 2 = max |gY|, folded in by mvml_gat_agg_bwd's stores
         if DEBUG_CAPTURE is not None and amx is not None:
             DEBUG_CAPTURE.setdefault("gy_amax", []).append((gY[:, :CE].clone(), amx[2:3].clone()))

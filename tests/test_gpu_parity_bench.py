@@ -193,17 +193,15 @@ def test_gnn_fusion_config3_bench_batch():
 # ----------------------------------------------------------------------------- config 5
 @pytest.mark.timeout(1500)
 @pytest.mark.parametrize("big_window", [1, 0])
-def test_gnn_fusion_config5_bench_batch(big_window, monkeypatch):
+def test_gnn_fusion_config5_bench_batch(big_window):
     """the config-5 bench batch as bench.py builds it (synth.config5(8192,
     seed=1): 150-400-atom molecules with 1-4 hubs of in-degree 32-128, 128 GraphNorm groups of
     64), GNNModule -> MVFusion -> BCE, forward and every gradient against float64, on the
     production kernels (big windows; the head-mean layer's backward by source atom) and on the
     per-atom fallback pair (source-atom backward off)."""
-    from mvml_gat import functional as Fn
     from mvml_gat._lib import option
     sb = synth.config5(8192, seed=1)
-    monkeypatch.setattr(Fn, "MEAN_SRC_AUTO", bool(big_window))
-    with option("big_window", big_window):
+    with option("big_window", big_window), option("mean_src", big_window):
         _gnn_fusion_case(sb, 64, 256, f"config5_bench_batch_bigwindow{big_window}")
 
 

@@ -197,6 +197,15 @@ def test_gat_layer_config2(layer):
     _layer_case(layer, synth.config2(128, seed=0), seed=layer)
 
 
+@pytest.mark.parametrize("case", ["config2", "config3"])
+def test_gat_layer1_molecule_window_backward(case):
+    """Option mean_src = 0: the head-mean layer's backward on the molecule-window LDS kernel (the
+    default path is the source-atom kernel, tested by every other layer-1 case)."""
+    sb = {"config2": lambda: synth.config2(128, seed=0), "config3": lambda: synth.config3(192, seed=4)}[case]()
+    with option("mean_src", 0):
+        _layer_case(1, sb, seed=7)
+
+
 def test_gat_layer0_hubs_flatten_elu():
     """Layer 0 (F = 192, flatten + ELU) on hub molecules > 128 atoms: the big-window kernels
     (kind bit 2) with their hub segments, at the production width."""
@@ -221,12 +230,11 @@ def test_gat_layer0_reassociated(case, monkeypatch):
     _layer_case(0, sb, seed=11, x_grad=False)
 
 
-@pytest.mark.parametrize("auto", [True, False])
-def test_gat_layer1_config5(auto, monkeypatch):
-    """The head-mean layer on config 5: by default its backward takes the source-atom kernel
-    (functional.MEAN_SRC_AUTO, the molecules exceed the LDS window); off, the big window."""
-    monkeypatch.setattr(Fn, "MEAN_SRC_AUTO", auto)
-    _layer_case(1, synth.config5(2, seed=3), seed=4)
+@pytest.mark.parametrize("mean_src", [1, 0])
+def test_gat_layer1_config5(mean_src):
+    """The head-mean layer on config 5: backward by source atom (default) and by big windows."""
+    with option("mean_src", mean_src):
+        _layer_case(1, synth.config5(2, seed=3), seed=4)
 
 
 @pytest.mark.parametrize("layer", [0, 1])
@@ -234,8 +242,7 @@ def test_gat_layer_config5_fallback_kernels(layer, monkeypatch):
     """Option big_window = 0: config-5 groups through the per-atom fallbacks (forward gather
     with its hub pass, dst / src backward pair) — the path of groups past the big window's caps
     (the head-mean layer's source-atom backward, picked for such batches, turned off)."""
-    monkeypatch.setattr(Fn, "MEAN_SRC_AUTO", False)
-    with option("big_window", 0):
+    with option("big_window", 0), option("mean_src", 0):
         _layer_case(layer, synth.config5(2, seed=3), seed=4 + layer)
 
 
@@ -246,8 +253,8 @@ def test_gat_layer_big_window_table_overflow(layer, monkeypatch):
     last hubs walk their out-edges from global memory on their own lanes."""
     sb = batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109)
     assert int(sb.num_edges[0]) <= 2432
-    monkeypatch.setattr(Fn, "MEAN_SRC_AUTO", False)  # the big-window backward itself
-    _layer_case(layer, sb, seed=5 + layer)
+    with option("mean_src", 0):  # the big-window backward itself
+        _layer_case(layer, sb, seed=5 + layer)
 
 
 @pytest.mark.parametrize("layer", [0, 1])
@@ -266,8 +273,7 @@ def test_gat_bwd_fused_gy_max(layer, case, monkeypatch):
           "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109),
           "atomwise": lambda: synth.config3(128, seed=2)}[case]()
     opts = {"config5_fallback": ("big_window", 0), "atomwise": ("bwd_atomwise", 1)}
-    monkeypatch.setattr(Fn, "MEAN_SRC_AUTO", False)  # each kernel path named by the case
-    with option(*opts.get(case, ("big_window", 1))):
+    with option(*opts.get(case, ("big_window", 1))), option("mean_src", 0):  # the named path
         _gy_max_case(layer, sb)
 
 
