@@ -1404,18 +1404,29 @@ gat_agg_bwd_dst_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
     const int u_l = (base + lane < deg) ? in_src[beg + base + lane] : 0;
 #pragma unroll
     for (int h = 0; h < H; ++h) ga_l[h] = 0.f;
-#pragma unroll 4
-    for (int j = 0; j < cnt; ++j) {
-      const float* zu = Y + (int64_t)rl(u_l, j) * ldy;
-      float part[H];
+    for (int j = 0; j < cnt; j += 2) {  // two source rows in flight
+      const int j1 = min(j + 1, cnt - 1);
+      const float* zu0 = Y + (int64_t)rl(u_l, j) * ldy;
+      const float* zu1 = Y + (int64_t)rl(u_l, j1) * ldy;
+      float4 z0[VPL], z1[VPL];
 #pragma unroll
-      for (int h = 0; h < H; ++h) part[h] = 0.f;
+      for (int c = 0; c < VPL; ++c) {
+        z0[c] = okc[c] ? ld4(zu0 + 4 * (lane + 64 * c)) : f4(0.f);
+        z1[c] = okc[c] ? ld4(zu1 + 4 * (lane + 64 * c)) : f4(0.f);
+      }
+      float p0[H], p1[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) { p0[h] = 0.f; p1[h] = 0.f; }
 #pragma unroll
       for (int c = 0; c < VPL; ++c)
-        if (okc[c]) add_at<H>(part, hc[c], dot4(ld4(zu + 4 * (lane + 64 * c)), gr[c]));
-      HeadReduce<H>::template all<false>(part, lane);
+        if (okc[c]) {
+          add_at<H>(p0, hc[c], dot4(z0[c], gr[c]));
+          add_at<H>(p1, hc[c], dot4(z1[c], gr[c]));
+        }
+      HeadReduce<H>::template all<false>(p0, lane);
+      HeadReduce<H>::template all<false>(p1, lane);
 #pragma unroll
-      for (int h = 0; h < H; ++h) ga_l[h] = (lane == j) ? part[h] : ga_l[h];
+      for (int h = 0; h < H; ++h) ga_l[h] = (lane == j) ? p0[h] : (lane == j1) ? p1[h] : ga_l[h];
     }
     const bool valid = base + lane < deg;
     float ag[H];
@@ -1533,19 +1544,27 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
     HeadReduce<H>::template all<false>(gp_l, lane);
 #pragma unroll
     for (int h = 0; h < H; ++h) gel[h] += gp_l[h];
-#pragma unroll 4
-    for (int j = 0; j < cnt; ++j) {
-      const int w = rl(w_l, j);
-      float a[H];
+    for (int j = 0; j < cnt; j += 2) {  // two g_rst rows in flight
+      const int j1 = min(j + 1, cnt - 1);
+      const bool two = j + 1 < cnt;  // (uniform)
+      const int w0 = rl(w_l, j), w1 = rl(w_l, j1);
+      float a0[H], a1[H];
 #pragma unroll
-      for (int h = 0; h < H; ++h) a[h] = rl(a_l[h], j);
-      const float* gw = gY + (int64_t)w * ldgy + HF;  // g_rst row written by the dst pass
+      for (int h = 0; h < H; ++h) { a0[h] = rl(a_l[h], j); a1[h] = rl(a_l[h], j1); }
+      const float* gw0 = gY + (int64_t)w0 * ldgy + HF;  // g_rst rows written by the dst pass
+      const float* gw1 = gY + (int64_t)w1 * ldgy + HF;
+      float4 g0[VPL], g1[VPL];
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) {
+        const int col = 4 * (lane + 64 * c);
+        g0[c] = !okc[c] ? f4(0.f) : (mode == 1) ? grst_of(g_out, out, w0, col, HF, F, H, mode) : ld4(gw0 + col);
+        g1[c] = !okc[c] ? f4(0.f) : (mode == 1) ? grst_of(g_out, out, w1, col, HF, F, H, mode) : ld4(gw1 + col);
+      }
 #pragma unroll
       for (int c = 0; c < VPL; ++c)
         if (okc[c]) {
-          const int col = 4 * (lane + 64 * c);
-          const float4 g = (mode == 1) ? grst_of(g_out, out, w, col, HF, F, H, mode) : ld4(gw + col);
-          gz[c] = fma4(pick<H>(a, hc[c]), g, gz[c]);
+          gz[c] = fma4(pick<H>(a0, hc[c]), g0[c], gz[c]);
+          if (two) gz[c] = fma4(pick<H>(a1, hc[c]), g1[c], gz[c]);
         }
     }
   }
