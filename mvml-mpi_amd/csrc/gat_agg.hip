@@ -1823,8 +1823,14 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
     else if (mode == 1) MVML_AGG_FWD_M(CW, 1);            \
     else MVML_AGG_FWD_M(CW, 2);                           \
   } while (0)
-  if (F % 64 == 0) MVML_AGG_FWD(64);
-  else if (F % 32 == 0) MVML_AGG_FWD(32);
+// Widest column chunk of the forward LDS kernel: 32 (two 512-thread workgroups per CU, so one
+// group's softmax and first loads overlap the other's chunk sweep) measured 3-5 % faster than
+// 64 (one 1024-thread workgroup per CU) on configs 2 and 3 (profiles/r04_fwd_chunk_width.txt).
+#ifndef MVML_FWD_CWMAX
+#define MVML_FWD_CWMAX 32
+#endif
+  if (MVML_FWD_CWMAX >= 64 && F % 64 == 0) MVML_AGG_FWD(64);
+  else if (MVML_FWD_CWMAX >= 32 && F % 32 == 0) MVML_AGG_FWD(32);
   else if (F % 16 == 0) MVML_AGG_FWD(16);
   else if (F % 8 == 0) MVML_AGG_FWD(8);
   else MVML_AGG_FWD(4);
@@ -1845,10 +1851,11 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
   if (option(MVML_OPT_BWD_ATOMWISE)) G = 0;  // tests: the per-atom pair over every atom
   if (F % 32 == 0 && G > 0) {  // molecule groups: one pass over Z / g_out / dZ per group
 #ifndef MVML_BWD_CW64
-#define MVML_BWD_CW64 1
+#define MVML_BWD_CW64 0
 #endif
-    // 64-column chunks (256-B row segments, half the chunks and barriers; one 1024-thread
-    // workgroup per CU) when F allows, else 32-column chunks (two 512-thread workgroups per CU)
+    // 32-column chunks (two 512-thread workgroups per CU); MVML_BWD_CW64=1: 64-column chunks
+    // (256-B row segments, half the chunks and barriers; one 1024-thread workgroup per CU),
+    // measured 1-2 % slower in round 4 (profiles/r04_fwd_chunk_width.txt, second part)
 #define MVML_BWD_LDS(M, CW)                                                                       \
     gat_agg_bwd_lds_kernel<H, M, CW><<<(unsigned)G, 16 * CW, 0, st>>>(groups, G, rp, src, orp, odst, \
                                                                       oslot, Y, ldy, F, elr, attn, \
