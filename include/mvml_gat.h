@@ -68,6 +68,11 @@ const char* mvml_version(void);
                                    projection row once and gathers the F-wide g_out rows of its
                                    out-edges; no LDS windows), 0 = molecule / big windows +
                                    per-atom pair */
+#define MVML_OPT_FLAT_SRC 8     /* MVML_FLAT_SRC: 1 = flatten GAT layers' aggregation backward by
+                                   source atom (g_rst rows formed once as gY's dR block, then one
+                                   wave per atom gathers them; for batches of large molecules —
+                                   the Python layer sets it per call, mvml_gat.functional),
+                                   0 (default) = molecule / big windows + per-atom pair */
 int mvml_set_option(int option, int value);
 int mvml_get_option(int option);
 

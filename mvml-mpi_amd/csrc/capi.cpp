@@ -30,7 +30,7 @@ int check_launch(const char* what) {
 }
 
 // Kernel-path options (include/mvml_gat.h, MVML_OPT_*): environment defaults read once at load.
-constexpr int kOptCount = 8;
+constexpr int kOptCount = 9;
 static std::atomic<int> g_opt[kOptCount];
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
@@ -45,6 +45,7 @@ static const bool g_opt_init = [] {
   g_opt[MVML_OPT_GEMM_RING] = env_int("MVML_GEMM_RING", 0);
   g_opt[MVML_OPT_LSTM_TILE] = env_int("MVML_LSTM_TILE", 0);
   g_opt[MVML_OPT_MEAN_SRC] = env_int("MVML_MEAN_SRC", 1);
+  g_opt[MVML_OPT_FLAT_SRC] = env_int("MVML_FLAT_SRC", 0);
   return true;
 }();
 

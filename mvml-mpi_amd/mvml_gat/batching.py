@@ -120,6 +120,15 @@ class BatchedMolGraph:
         _, dst = self.edges()
         return torch.bincount(dst.long().cpu(), minlength=self.num_nodes())
 
+    def large_molecule_fraction(self, atoms):
+        """Fraction of the batch's atoms that sit in molecules of more than `atoms` atoms (host
+        counts, no device work; picks the flatten layer's backward kernel, functional.FLAT_SRC_AUTO)."""
+        cache = self.__dict__.setdefault("_large_frac", {})
+        if atoms not in cache:
+            n = int(self._bnn.sum())
+            cache[atoms] = float(self._bnn[self._bnn > atoms].sum()) / n if n else 0.0
+        return cache[atoms]
+
     def group_offsets_host(self):
         B = self.batch_size
         gs = self.group_size or max(B, 1)

@@ -4,6 +4,7 @@ Each Function owns one stage of GNNModule (model.py:89-95) and calls only the C 
 no PyTorch math on the hot path besides allocation (and nn.Dropout, which the reference
 applies with torch's own RNG, model.py:87).
 """
+import contextlib
 import ctypes
 import os
 
@@ -245,6 +246,15 @@ def colsum(X, M, N, ldx, out, beta=0.0, offset=0, alpha=1.0):
 # GEMMs and the per-head weight gradients cost more than the projection's Y round trip saves,
 # DESIGN.md "Layer 1 by re-association").
 REASSOC_X = os.environ.get("MVML_GAT_REASSOC", "0") == "1"
+
+# Flatten layers' aggregation backward by source atom (option flat_src, csrc/gat_agg.hip
+# gat_flat_bwd_src_kernel) for batches whose atoms sit mostly in molecules past the LDS molecule
+# window.  Off by default (MVML_FLAT_SRC_AUTO=1 turns the rule on): measured slower than the big
+# window on config 5 (16.5 vs 13.4 ms per launch) and than the molecule window on config 3 (11.0
+# vs 5.6 ms) — the H F-wide g_rst rows gathered per edge do not stay in L2 the way the head-mean
+# layer's F-wide g_out rows do (profiles/r04_flat_src_ab.txt).
+FLAT_SRC_AUTO = os.environ.get("MVML_FLAT_SRC_AUTO", "0") == "1"
+FLAT_SRC_MIN_ATOMS = 128  # the LDS molecule window (gat_agg.hip kWinL)
 
 
 
@@ -555,10 +565,13 @@ class GATLayerFunction(torch.autograd.Function):
             gyr = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}",
                             "bytes": agg_bwd_bytes(N, g.num_edges(), H, F, g_out.shape[1], mode)}
-        call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
-             ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr),
-             ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY), ldg,
-             slot(ctx.amx, 2), ptr(gyr), wp, wn, st)
+        flat_src = (FLAT_SRC_AUTO and mode != MODE_MEAN
+                    and g.large_molecule_fraction(FLAT_SRC_MIN_ATOMS) >= 0.5)
+        with (_lib.option("flat_src", 1) if flat_src else contextlib.nullcontext()):
+            call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
+                 ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy,
+                 ptr(elr), ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY),
+                 ldg, slot(ctx.amx, 2), ptr(gyr), wp, wn, st)
         amx = ctx.amx  # slot 2 = max |gY|, folded in by mvml_gat_agg_bwd's stores
         if DEBUG_CAPTURE is not None and amx is not None:
             DEBUG_CAPTURE.setdefault("gy_amax", []).append((gY[:, :CE].clone(), amx[2:3].clone()))

@@ -197,6 +197,41 @@ def test_gat_layer_config2(layer):
     _layer_case(layer, synth.config2(128, seed=0), seed=layer)
 
 
+@pytest.mark.parametrize("case", ["config2", "config5", "hubs", "table_overflow", "config3"])
+def test_gat_layer0_flat_src(case):
+    """Option flat_src = 1: the flatten layer's aggregation backward by source atom (g_rst rows
+    formed once as gY's dR block, then gat_flat_bwd_src_kernel gathers them per out-edge) —
+    forward and every gradient against float64 on each graph family."""
+    sb = {"config2": lambda: synth.config2(128, seed=0),
+          "config5": lambda: synth.config5(2, seed=3),
+          "hubs": lambda: batch_of_sizes([150, 90, 210], seed=7, hubs=True),
+          "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109),
+          "config3": lambda: synth.config3(192, seed=4)}[case]()
+    with option("flat_src", 1):
+        _layer_case(0, sb, seed=8)
+
+
+@pytest.mark.parametrize("flat_src", [0, 1])
+@pytest.mark.parametrize("case", ["config2", "config5"])
+def test_gat_bwd_gy_row_maxima_flat(case, flat_src):
+    """Per-row max |gY| of the flatten layer's backward, both paths (see the layer-1 test)."""
+    if Fn.GEMM_ALGO != "f16x2" or not Fn.ROW_SCALES:
+        pytest.skip("per-row maxima feed the per-row split-fp16 GEMM only")
+    sb = {"config2": lambda: synth.config2(64, seed=0), "config5": lambda: synth.config5(2, seed=3)}[case]()
+    prev = Fn.FLAT_SRC_AUTO
+    Fn.FLAT_SRC_AUTO = False
+    try:
+        with option("flat_src", flat_src):
+            cap = _gy_max_case(0, sb)
+    finally:
+        Fn.FLAT_SRC_AUTO = prev
+    (gY, _), = cap["gy_amax"]
+    rows, = cap["gy_rows"]
+    want = gY.abs().max(dim=1).values
+    got = rows.view(torch.float32)[:gY.shape[0]]
+    assert torch.equal(got, want), (got - want).abs().max().item()
+
+
 @pytest.mark.parametrize("case", ["config2", "config3"])
 def test_gat_layer1_molecule_window_backward(case):
     """Option mean_src = 0: the head-mean layer's backward on the molecule-window LDS kernel (the
@@ -206,9 +241,11 @@ def test_gat_layer1_molecule_window_backward(case):
         _layer_case(1, sb, seed=7)
 
 
-def test_gat_layer0_hubs_flatten_elu():
+def test_gat_layer0_hubs_flatten_elu(monkeypatch):
     """Layer 0 (F = 192, flatten + ELU) on hub molecules > 128 atoms: the big-window kernels
-    (kind bit 2) with their hub segments, at the production width."""
+    (kind bit 2) with their hub segments, at the production width (the source-atom backward
+    that such batches take by default turned off; it has its own cases)."""
+    monkeypatch.setattr(Fn, "FLAT_SRC_AUTO", False)
     _layer_case(0, batch_of_sizes([150, 90, 210], seed=7, hubs=True), seed=2)
 
 
@@ -242,6 +279,7 @@ def test_gat_layer_config5_fallback_kernels(layer, monkeypatch):
     """Option big_window = 0: config-5 groups through the per-atom fallbacks (forward gather
     with its hub pass, dst / src backward pair) — the path of groups past the big window's caps
     (the head-mean layer's source-atom backward, picked for such batches, turned off)."""
+    monkeypatch.setattr(Fn, "FLAT_SRC_AUTO", False)
     with option("big_window", 0), option("mean_src", 0):
         _layer_case(layer, synth.config5(2, seed=3), seed=4 + layer)
 
@@ -253,6 +291,7 @@ def test_gat_layer_big_window_table_overflow(layer, monkeypatch):
     last hubs walk their out-edges from global memory on their own lanes."""
     sb = batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109)
     assert int(sb.num_edges[0]) <= 2432
+    monkeypatch.setattr(Fn, "FLAT_SRC_AUTO", False)
     with option("mean_src", 0):  # the big-window backward itself
         _layer_case(layer, sb, seed=5 + layer)
 
@@ -273,6 +312,7 @@ def test_gat_bwd_fused_gy_max(layer, case, monkeypatch):
           "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109),
           "atomwise": lambda: synth.config3(128, seed=2)}[case]()
     opts = {"config5_fallback": ("big_window", 0), "atomwise": ("bwd_atomwise", 1)}
+    monkeypatch.setattr(Fn, "FLAT_SRC_AUTO", False)
     with option(*opts.get(case, ("big_window", 1))), option("mean_src", 0):  # the named path
         _gy_max_case(layer, sb)
 
