@@ -362,10 +362,18 @@ def run(args):
         if world > 1:
             dist.init_process_group("gloo", rank=rank, world_size=world)
     else:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        # MVML_BENCH_ONE_DEVICE=1 + MVML_BENCH_BACKEND=gloo: a rehearsal of the N-rank path on a
+        # one-GPU box (every rank on cuda:0; RCCL refuses two ranks per device) — the driver's
+        # N-GPU runs use neither (one rank per GPU over RCCL)
+        one_dev = os.environ.get("MVML_BENCH_ONE_DEVICE") == "1"
+        torch.cuda.set_device(0 if one_dev else local_rank)
+        dev = torch.device("cuda", 0 if one_dev else local_rank)
         if world > 1:
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+            backend = os.environ.get("MVML_BENCH_BACKEND", "nccl")
+            if backend == "nccl":
+                dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+            else:
+                dist.init_process_group(backend, rank=rank, world_size=world)
 
     from mvml_gat.dist import EmbeddingAllGather, FlatGradAllReduce
     from mvml_gat import functional as F
