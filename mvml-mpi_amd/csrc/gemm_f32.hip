@@ -1520,7 +1520,13 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   const bool lds_rows = EX && ex.c_rows && !slab && cep.D == 0 && (ex.rows_cols == 0 || ex.rows_cols % XBN == 0);
   // KS 16-deep sub-stages per barrier (split-fp16: 2, so a stage carries as many MFMAs as the
   // split-bf16 one); a sub-stage's LDS image is exactly the KS = 1 stage layout
-  constexpr int KS = (NP == 2) ? MVML_H2_KS : 1;
+  // (round 4) products whose B comes pre-split (BPS: the il4 weight image) only split A in the
+  // loop: the sched_group_barrier interleave, placed for the split of both operands, measured
+  // slower there than two plain sub-stages per barrier (L2 forward 17.5 -> 16.8 ms, dX 15.7 ->
+  // 15.5, LSTM gates 0.523 -> 0.514; profiles/r04_gemm_schedule_variants.txt), so it is kept
+  // for the in-loop split of both operands only
+  constexpr bool H2SGB = MVML_H2_SGB && BPS == 0;
+  constexpr int KS = (NP == 2) ? (H2SGB ? MVML_H2_KS : 2) : 1;
   constexpr int kSub = OA::kBytes + OB::kBytes;
   constexpr int kStage = KS * kSub;
   // double-buffered stages; the LDS epilogue reuses the space (8 waves x 32 rows x kEpiLd)
@@ -1697,7 +1703,7 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       __syncthreads();
       return;
     }
-    if constexpr (MVML_H2_SGB && decltype(STAGE)::value && NP == 2 && KS == 1) {
+    if constexpr (H2SGB && decltype(STAGE)::value && NP == 2 && KS == 1) {
       // the same interleave for split-fp16 (default): 24 MFMAs carry the 32 split VALU (8 per
       // float4: 2 pk_mul, 2 cvt_pk, 4 fma_mix), 8 LDS plane writes and the 4 global loads —
       // measured +3 / +7 / +3 % on the L2 forward / dX / dW shapes over two sub-stages per
