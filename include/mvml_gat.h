@@ -53,7 +53,8 @@ const char* mvml_version(void);
                                    dst / src kernel pair for every group (default 0) */
 #define MVML_OPT_GEMM_TILE 2    /* MVML_X3_TILE: 0 (default) planned tile, 128 / 256 = forced */
 #define MVML_OPT_GEMM_PERSIST 3 /* MVML_X3W_PERSIST: P > 0 caps a 256x256 launch at P
-                                   workgroups looping over tiles (default 0: one per tile) */
+                                   workgroups looping over tiles (default 256, one per CU;
+                                   0: one workgroup per tile) */
 #define MVML_OPT_GEMM_NSPLIT 4  /* MVML_GEMM_NSPLIT: 1 (default) N = 256 q + r products as two
                                    launches, 0 = one */
 #define MVML_OPT_GEMM_RING 5    /* MVML_GEMM_RING: 1 = split-fp16 256x256 products on the

@@ -40,7 +40,7 @@ static const bool g_opt_init = [] {
   g_opt[MVML_OPT_BIG_WINDOW] = env_int("MVML_BIG_WINDOW", 1);
   g_opt[MVML_OPT_BWD_ATOMWISE] = env_int("MVML_BWD_ATOMWISE", 0);
   g_opt[MVML_OPT_GEMM_TILE] = env_int("MVML_X3_TILE", 0);
-  g_opt[MVML_OPT_GEMM_PERSIST] = env_int("MVML_X3W_PERSIST", 0);
+  g_opt[MVML_OPT_GEMM_PERSIST] = env_int("MVML_X3W_PERSIST", 256);  // one per CU (MI355X)
   g_opt[MVML_OPT_GEMM_NSPLIT] = env_int("MVML_GEMM_NSPLIT", 1);
   g_opt[MVML_OPT_GEMM_RING] = env_int("MVML_GEMM_RING", 0);
   g_opt[MVML_OPT_LSTM_TILE] = env_int("MVML_LSTM_TILE", 0);

@@ -2274,10 +2274,11 @@ int choose_splits(int64_t M, int64_t N, int64_t K) {  // the larger of the two p
 
 int64_t k_chunk(int64_t K, int S) { return ceil_div(ceil_div(K, S), BKT) * BKT; }
 
-// Workgroups of a 256x256 launch: one per tile by default; option MVML_OPT_GEMM_PERSIST = P > 0 caps a
-// launch without split-K at P workgroups that loop over their XCD's tiles (measured neutral at
-// P = 256 / 512 on the step's shapes: the dispatcher already overlaps one tile's C stores with
-// the next tile's start).
+// Workgroups of a 256x256 launch: option MVML_OPT_GEMM_PERSIST = P > 0 (default 256, one per CU)
+// caps a launch without split-K at P workgroups that loop over their XCD's tiles.  Round 2
+// measured it neutral; since the per-row / pre-split-B kernels (round 4) it is 1-9 % faster on
+// every shape of the step (L1 projection 4.73 -> 4.29 ms, L2 forward 16.9 -> 16.3 ms; the step
+// +1 %, profiles/r04_gemm_persist.txt); P = 0 gives one workgroup per tile.
 unsigned x3w_grid_x(int64_t tiles, int S) {
   const int persist = option(MVML_OPT_GEMM_PERSIST);
   if (S > 1 || persist <= 0 || tiles <= persist) return (unsigned)tiles;
