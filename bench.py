@@ -8,7 +8,8 @@ KEGG-like molecules (mvml_gat.synth.Config3Set), sharded over the ranks in whole
 GraphNorm groups (the reference's mini-batches, config.py:21 / main.py:79-81 / model.py:93)
 balanced by edges (mvml_gat.dist.shard_groups), resident in HBM and streamed through steps of
 --mols-per-step molecules per GPU.  Step = one data-parallel training step of model.py:51-72
-restricted to the graph view: GNNModule forward -> MVFusion (shared LayerNorm, 12-head 3-token
+restricted to the graph view: device collation of the step's molecules (dataset.py:52-54:
+dgl.batch + CSR + node-group plan, mvml_build_csr) -> GNNModule forward -> MVFusion (shared LayerNorm, 12-head 3-token
 attention, Conv2d, MLP) -> BCEWithLogits (main.py:91) -> backward -> one flat RCCL all-reduce of
 the gradients (N > 1) -> Adam (main.py:88).  The SMILES and fingerprint view embeddings that
 the fusion also consumes are fixed synthetic tensors (their views are not this workload).
@@ -56,7 +57,7 @@ TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32
          "mvml_bilstm_token_grad_packed", "mvml_bilstm_packed_tokens", "mvml_gemm_f16x2_rows",
          "mvml_absmax_rows_f32", "mvml_segment_max_bits", "mvml_gat_x_fwd", "mvml_gat_x_bwd",
          "mvml_gemm_f16x2_ex", "mvml_gemm_f16x2_batched", "mvml_gat_elu_bwd", "mvml_gat_x_pack_weights",
-         "mvml_split_f16x2_il4"]
+         "mvml_split_f16x2_il4", "mvml_build_csr", "mvml_build_node_groups"]
 
 
 def parse(argv=None):
@@ -69,9 +70,9 @@ def parse(argv=None):
                          "fingerprint MLP + fusion) DP training step on shards of the config-3 set")
     ap.add_argument("--total-mols", type=int, default=1_000_000,
                     help="config 3: size of the ONE global molecule set sharded over the ranks")
-    ap.add_argument("--mols-per-step", type=int, default=65536,
-                    help="molecules per GPU per step (whole GraphNorm groups); config5 / mvp "
-                         "default 8192")
+    ap.add_argument("--mols-per-step", type=int, default=None,
+                    help="molecules per GPU per step (whole GraphNorm groups); default 65536 for "
+                         "config3, 8192 for config5 / mvp")
     ap.add_argument("--group-size", type=int, default=64)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--view-only-steps", type=int, default=3,
@@ -90,6 +91,13 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo plumbing rehearsal with a stand-in model (no measurement)")
     return ap.parse_args(argv)
+
+
+def mols_per_step(args):
+    """The per-GPU step size the workload runs with (explicit, or the workload's default)."""
+    if args.mols_per_step is not None:
+        return args.mols_per_step
+    return 65536 if args.workload == "config3" else 8192
 
 
 def log(*a):
@@ -308,8 +316,7 @@ def build_batches(args, rank, world, dev, with_fusion):
         gset = synth.Config3Set(args.total_mols, seed=args.seed)
         g0, g1 = mdist.shard_groups(gset.group_costs(gs), world, rank)
         lo, hi = g0 * gs, min(g1 * gs, args.total_mols)
-        per = args.mols_per_step if args.mols_per_step != 65536 else 8192
-        per = max(gs, per // gs * gs)
+        per = max(gs, mols_per_step(args) // gs * gs)
         hi = min(hi, lo + 16 * per)  # at most 16 resident steps per rank
         return ([Batch(gset.molecules(m, min(hi, m + per)), m, gs, dev, True, mvp=True)
                  for m in range(lo, hi, per)], (lo, hi))
@@ -317,13 +324,13 @@ def build_batches(args, rank, world, dev, with_fusion):
         gset = synth.Config3Set(args.total_mols, seed=args.seed)
         g0, g1 = mdist.shard_groups(gset.group_costs(gs), world, rank)
         lo, hi = g0 * gs, min(g1 * gs, args.total_mols)
-        per = max(gs, args.mols_per_step // gs * gs)
+        per = max(gs, mols_per_step(args) // gs * gs)
         out = []
         for m in range(lo, hi, per):
             sb = gset.molecules(m, min(hi, m + per))
             out.append(Batch(sb, m, gs, dev, with_fusion))
         return out, (lo, hi)
-    n5 = args.mols_per_step if args.mols_per_step != 65536 else 8192
+    n5 = mols_per_step(args)
     sb = synth.config5(n5, seed=1 + 1000 * args.seed + rank)
     return [Batch(sb, rank * n5, gs, dev, with_fusion)], (rank * n5, (rank + 1) * n5)
 
@@ -399,8 +406,8 @@ def run(args):
         g0, g1 = mdist.shard_groups(gset.group_costs(gs), world, rank)
         lo, hi = g0 * gs, min(g1 * gs, args.total_mols)
         batches = []
-        for m in range(lo, hi, args.mols_per_step):
-            sb = gset.molecules(m, min(hi, m + args.mols_per_step))
+        for m in range(lo, hi, mols_per_step(args)):
+            sb = gset.molecules(m, min(hi, m + mols_per_step(args)))
             b = Batch.__new__(Batch)
             b.g = sb.to_graph(group_size=gs)
             b.feats = torch.as_tensor(sb.feats)
@@ -445,6 +452,10 @@ def run(args):
 
     def step(b, fused=True):
         opt.zero_grad(set_to_none=False)
+        if not args.dry_run:
+            # the collation (dgl.batch + CSR + node-group plan) on the device, every step, as the
+            # reference's DataLoader collates every batch (dataset.py:52-54)
+            b.g.recollate()
         if mvp and fused:
             mvml_gat.bce_with_logits(full(b.smiles, b.g, b.feats, b.fp), b.labels).backward()
             mvp_mod.join_side_stream(dev)
@@ -515,8 +526,7 @@ def run(args):
     value = total_mols / elapsed if elapsed > 0 else 0.0
 
     roofline, extra = None, {}
-    # the per-step molecule count the workload actually used (config 5 / mvp default to 8,192)
-    mps = args.mols_per_step if (args.workload == "config3" or args.mols_per_step != 65536) else 8192
+    mps = mols_per_step(args)  # the per-step molecule count the workload actually used
     wkey = f"{args.workload}/mols_per_step={mps}" + ("/proj_bf16" if args.proj_bf16 else "")
     if timer_on:
         summ = _lib.timer.summary()
@@ -572,6 +582,11 @@ def run(args):
                     "achieved is fp32-equivalent TFLOP/s, peak = dense bf16 MFMA peak / 6")
                 extra["roofline_gemm"]["frac"] = round(extra["roofline_gemm"]["achieved"] / (BF16_MFMA_PEAK_TFS / 6), 4)
         extra["kernel_ms_per_step"] = {k: round(v["ms_per_step"], 3) for k, v in rows.items()}
+        if "mvml_build_csr" in rows:
+            # device collation per step batch (inside the timed step): CSR build + node-group plan
+            extra["batching_ms_per_batch"] = round(sum(rows[k]["ms_per_step"] for k in
+                                                       ("mvml_build_csr", "mvml_build_node_groups")
+                                                       if k in rows), 4)
         # time per step outside every timed entry point: torch-side kernels (Adam, zero_grad,
         # pads / copies), launch gaps and allocator stalls (config 3: one stream, so the
         # entry-point times do not overlap)
@@ -643,7 +658,7 @@ def run(args):
         if args.workload == "config3":
             wl = (f"BASELINE config 3: one global set of {args.total_mols} KEGG-like molecules, "
                   f"sharded in whole {gsz}-molecule GraphNorm groups, streamed through "
-                  f"{args.mols_per_step}-molecule steps per GPU; view + fusion: GNNModule (GAT "
+                  f"{mols_per_step(args)}-molecule steps per GPU; view + fusion: GNNModule (GAT "
                   "[192,384] x4 heads, Set2Set 6x3, GraphNorm, fc) -> MVFusion (12-head 3-token "
                   "attention, Conv2d, MLP) -> BCEWithLogits, fwd+bwd+Adam")
         elif args.workload == "mvp":

@@ -69,11 +69,21 @@ const char* mvml_version(void);
                                    projection row once and gathers the F-wide g_out rows of its
                                    out-edges; no LDS windows), 0 = molecule / big windows +
                                    per-atom pair */
-#define MVML_OPT_FLAT_SRC 8     /* MVML_FLAT_SRC: 1 = flatten GAT layers' aggregation backward by
-                                   source atom (g_rst rows formed once as gY's dR block, then one
-                                   wave per atom gathers them; for batches of large molecules —
-                                   the Python layer sets it per call, mvml_gat.functional),
-                                   0 (default) = molecule / big windows + per-atom pair */
+#define MVML_OPT_FLAT_SRC 8     /* MVML_FLAT_SRC: flatten GAT layers' aggregation backward by
+                                   source atom (one wave per atom gathers its out-neighbours'
+                                   rows): 2 = one pass (g_rst of each gathered row formed in
+                                   registers from g_out / out), 1 = g_rst rows formed first as
+                                   gY's dR block, then gathered; 0 (default) = molecule / big
+                                   windows + per-atom pair.  The Python layer sets it per call
+                                   for batches of large molecules (mvml_gat.functional) */
+#define MVML_OPT_DST_FWD 9      /* MVML_DST_FWD: 1 = aggregation forward by destination wave for
+                                   every atom (edge softmax on the lanes, whole projection rows of
+                                   the in-edges gathered from L2; no LDS windows), 0 (default) =
+                                   molecule / big windows + gather kernel.  The Python layer sets
+                                   it per call for batches of large molecules; 2 = the same
+                                   with the edge softmax as its own launch first */
+#define MVML_OPT_DST_UNR 10     /* MVML_DST_UNR: projection rows in flight per wave of the
+                                   destination-wave forward (0 = the default per width; tuning) */
 int mvml_set_option(int option, int value);
 int mvml_get_option(int option);
 

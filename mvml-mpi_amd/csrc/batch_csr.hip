@@ -7,10 +7,11 @@
 //   in_rowptr[N+1], in_src[E], in_eid[E]       rows = dst, stable in edge id
 //   out_rowptr[N+1], out_dst[E], out_inslot[E]  rows = src, stable in edge id; out_inslot
 //                                               is the in-CSR slot of the same edge
-// Molecules are independent and small, so the CSR is built by ONE workgroup per graph: the
-// per-graph degree histogram lives in LDS (graphs above kLdsNodes atoms fall back to a
-// workspace histogram) and the stable placement walks the edges in 256-edge chunks, ranking
-// equal keys inside a chunk by lane order.  Integer atomics are used only for histogram
+// Molecules are independent and small, so the CSR is built by ONE WAVE per molecule
+// (build_csr_wave_kernel, molecules up to 256 atoms / 1024 edges); larger graphs take ONE
+// workgroup each (build_csr_kernel): the per-graph degree histogram lives in LDS (graphs above
+// kLdsNodes atoms fall back to a workspace histogram) and the stable placement walks the edges
+// in 256-edge chunks, ranking equal keys inside a chunk by lane order.  Integer atomics are used only for histogram
 // counts (order-independent), so the output is deterministic and bit-exact with the oracle
 // (oracle/graph_ref.py: csr_ref).
 #include "common.h"
@@ -23,6 +24,10 @@ constexpr int kScanItems = 4;
 constexpr int kScanTile = kScanThreads * kScanItems;  // 1024 items per block
 constexpr int kCsrThreads = 256;
 constexpr int kLdsNodes = 4096;
+constexpr int kWaveMolAtoms = 256;   // build_csr_wave_kernel: one wave per molecule up to these
+constexpr int kWaveMolEdges = 1024;  // ... sizes (LDS: 6 KB per wave, 4 waves per workgroup)
+constexpr int kBigMolAtoms = 1024;   // build_csr_bigwave_kernel: one wave per molecule up to
+constexpr int kBigMolEdges = 4096;   // ... these sizes (LDS: 24 KB per one-wave workgroup)
 
 template <typename T>
 __device__ T block_exclusive_scan(T v, T* lds_waves /*[kWaves]*/, T* total) {
@@ -176,6 +181,190 @@ __device__ void rows_from_counts(int* cnt, int n, int64_t noff, int64_t eoff,
   if (zero_rows && zeros) atomicAdd(zero_rows, zeros);
 }
 
+// One WAVE per molecule: the wave's degree histograms and the in-slot of every edge live in its
+// own LDS slice, the row starts come from a wave scan, and the stable placement walks the edges
+// 64 at a time in edge order — a lane's rank among the chunk's equal keys is the number of
+// earlier lanes holding its key, found by matching the key bit by bit over ballots (log2(n)
+// steps, no loop over lanes), its slot the row's cursor plus that rank, and the cursors then
+// advance by LDS adds (order-independent).  No block barriers.  Two sizes:
+//  * build_csr_wave_kernel: four molecules per 256-thread workgroup, <= kWaveMolAtoms atoms and
+//    <= kWaveMolEdges edges (every drug-like molecule); larger ones go to a list;
+//  * build_csr_bigwave_kernel: one molecule per 64-thread workgroup, <= kBigMolAtoms atoms and
+//    <= kBigMolEdges edges (config 5's 150-400-atom hub molecules), walking that list; the rest
+//    to a second list for build_csr_kernel (one workgroup per graph, any size).
+// A stable counting sort has one result, so every path gives the same output.
+__device__ __forceinline__ void wave_lds_sync_b() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// exclusive wave scan of cnt[0..n) in place (+ the row starts), returns the zero-count rows
+__device__ __forceinline__ int wave_rows_from_counts(int* cnt, int n, int64_t noff, int64_t eoff,
+                                                     int32_t* __restrict__ rowptr) {
+  const int lane = threadIdx.x & 63;
+  int carry = 0, zeros = 0;
+  for (int b = 0; b < n; b += 64) {
+    const int j = b + lane;
+    const int c = j < n ? cnt[j] : 0;
+    zeros += (j < n && c == 0) ? 1 : 0;
+    int x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (j < n) {
+      cnt[j] = carry + x - c;
+      rowptr[noff + j] = (int32_t)(eoff + carry + x - c);
+    }
+    carry += __shfl(x, 63, 64);
+  }
+  return zeros;
+}
+
+// stable placement of the molecule's edges keyed by key_local (dst: in-CSR, src: out-CSR)
+template <bool IN>
+__device__ __forceinline__ void wave_place_edges(int ne, int n, int64_t eoff, int64_t noff,
+                                                 const int32_t* __restrict__ key_local,
+                                                 const int32_t* __restrict__ val_local, int* cursor,
+                                                 int* s_inslot, int32_t* __restrict__ out_val,
+                                                 int32_t* __restrict__ out_aux) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));  // lanes < this one
+  int nbits = 0;
+  while ((1 << nbits) < n) ++nbits;  // keys are in [0, n)
+  for (int base = 0; base < ne; base += 64) {
+    const int i = base + lane;
+    int k = -1, v = 0;
+    if (i < ne) {
+      k = key_local[eoff + i];
+      v = val_local[eoff + i];
+      if (k < 0 || k >= n || v < 0 || v >= n) k = -1;  // invalid edges are skipped (flagged)
+    }
+    // lanes holding this lane's key: intersect, bit by bit, the ballots that agree with it
+    uint64_t same = __ballot(k >= 0);
+    for (int b = 0; b < nbits; ++b) {
+      const bool bit = ((k >> b) & 1) != 0;
+      const uint64_t on = __ballot(bit);
+      same &= bit ? on : ~on;
+    }
+    const int rank = __popcll(same & below);
+    const int slot = k >= 0 ? cursor[k] + rank : 0;
+    wave_lds_sync_b();  // every lane read its cursor before any advances
+    if (k >= 0) {
+      atomicAdd(&cursor[k], 1);
+      const int64_t gs = eoff + slot;
+      out_val[gs] = v + (int32_t)noff;
+      if (IN) {
+        out_aux[gs] = (int32_t)(eoff + i);  // in_eid
+        s_inslot[i] = (int32_t)gs;          // in-slot of edge eoff + i
+      } else {
+        out_aux[gs] = s_inslot[i];          // out_inslot
+      }
+    }
+    wave_lds_sync_b();
+  }
+}
+
+struct CsrArgs {
+  const int32_t* src_local;
+  const int32_t* dst_local;
+  const int64_t* num_nodes;
+  const int64_t* num_edges;
+  const int64_t* node_off;
+  const int64_t* edge_off;
+  int32_t* src;
+  int32_t* dst;
+  int32_t* node_graph;
+  int32_t* in_rowptr;
+  int32_t* in_src;
+  int32_t* in_eid;
+  int32_t* out_rowptr;
+  int32_t* out_dst;
+  int32_t* out_inslot;
+  int32_t* flags;
+};
+
+// the whole CSR build of molecule g by the calling wave (LDS slices cin / cout [n], slot [ne])
+__device__ __forceinline__ void wave_build_molecule(const CsrArgs& a, int64_t g, int n, int ne, int* cin,
+                                                    int* cout, int* slot) {
+  const int lane = threadIdx.x & 63;
+  const int64_t noff = a.node_off[g], eoff = a.edge_off[g];
+  for (int j = lane; j < n; j += 64) {
+    cin[j] = 0;
+    cout[j] = 0;
+    a.node_graph[noff + j] = (int32_t)g;
+  }
+  wave_lds_sync_b();
+  int bad = 0;
+  for (int i = lane; i < ne; i += 64) {
+    const int s = a.src_local[eoff + i], d = a.dst_local[eoff + i];
+    a.src[eoff + i] = s + (int32_t)noff;
+    a.dst[eoff + i] = d + (int32_t)noff;
+    if (s < 0 || s >= n || d < 0 || d >= n) {
+      ++bad;
+      continue;
+    }
+    atomicAdd(&cin[d], 1);
+    atomicAdd(&cout[s], 1);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o, 64);
+  if (lane == 0 && bad) atomicAdd(&a.flags[1], bad);
+  wave_lds_sync_b();
+  int zeros = wave_rows_from_counts(cin, n, noff, eoff, a.in_rowptr);
+  wave_rows_from_counts(cout, n, noff, eoff, a.out_rowptr);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) zeros += __shfl_xor(zeros, o, 64);
+  if (lane == 0) {
+    if (zeros) atomicAdd(&a.flags[0], zeros);
+    a.in_rowptr[noff + n] = (int32_t)(eoff + ne);  // == the next molecule's first row start
+    a.out_rowptr[noff + n] = (int32_t)(eoff + ne);
+  }
+  wave_lds_sync_b();
+  wave_place_edges<true>(ne, n, eoff, noff, a.dst_local, a.src_local, cin, slot, a.in_src, a.in_eid);
+  wave_place_edges<false>(ne, n, eoff, noff, a.src_local, a.dst_local, cout, slot, a.out_dst, a.out_inslot);
+}
+
+__global__ void __launch_bounds__(256)
+build_csr_wave_kernel(CsrArgs a, int64_t B, int32_t* __restrict__ big_list, int* __restrict__ big_count) {
+  __shared__ int s_cin[4][kWaveMolAtoms];
+  __shared__ int s_cout[4][kWaveMolAtoms];
+  __shared__ int s_slot[4][kWaveMolEdges];
+  const int w = threadIdx.x >> 6;
+  const int64_t g = (int64_t)blockIdx.x * 4 + w;
+  if (g >= B) return;  // (wave-level only: no block barriers below)
+  const int n = (int)a.num_nodes[g];
+  const int ne = (int)a.num_edges[g];
+  if (n > kWaveMolAtoms || ne > kWaveMolEdges) {  // the next size class
+    if ((threadIdx.x & 63) == 0) big_list[atomicAdd(big_count, 1)] = (int32_t)g;
+    return;
+  }
+  wave_build_molecule(a, g, n, ne, s_cin[w], s_cout[w], s_slot[w]);
+}
+
+// persistent over the first list; one wave per workgroup (24 KB of LDS)
+__global__ void __launch_bounds__(64)
+build_csr_bigwave_kernel(CsrArgs a, const int32_t* __restrict__ list, const int* __restrict__ count,
+                         int32_t* __restrict__ huge_list, int* __restrict__ huge_count) {
+  __shared__ int s_cin[kBigMolAtoms];
+  __shared__ int s_cout[kBigMolAtoms];
+  __shared__ int s_slot[kBigMolEdges];
+  const int cnt = *count;
+  for (int li = blockIdx.x; li < cnt; li += gridDim.x) {
+    const int64_t g = list[li];
+    const int n = (int)a.num_nodes[g];
+    const int ne = (int)a.num_edges[g];
+    if (n > kBigMolAtoms || ne > kBigMolEdges) {
+      if (threadIdx.x == 0) huge_list[atomicAdd(huge_count, 1)] = (int32_t)g;
+      continue;
+    }
+    wave_build_molecule(a, g, n, ne, s_cin, s_cout, s_slot);
+    wave_lds_sync_b();  // this molecule's LDS reads are done before the next one's zeroing
+  }
+}
+
 __global__ void __launch_bounds__(kCsrThreads)
 build_csr_kernel(const int32_t* __restrict__ src_local, const int32_t* __restrict__ dst_local,
                  const int64_t* __restrict__ num_nodes, const int64_t* __restrict__ num_edges,
@@ -185,11 +374,15 @@ build_csr_kernel(const int32_t* __restrict__ src_local, const int32_t* __restric
                  int32_t* __restrict__ in_src, int32_t* __restrict__ in_eid,
                  int32_t* __restrict__ out_rowptr, int32_t* __restrict__ out_dst,
                  int32_t* __restrict__ out_inslot, int32_t* __restrict__ flags,
-                 int32_t* __restrict__ inslot_ws, int* __restrict__ big_cnt) {
+                 int32_t* __restrict__ inslot_ws, int* __restrict__ big_cnt,
+                 const int32_t* __restrict__ list, const int* __restrict__ count) {
   __shared__ int cnt_in_l[kLdsNodes];
   __shared__ int cnt_out_l[kLdsNodes];
   __shared__ int chunk_key[kCsrThreads];
-  const int64_t g = blockIdx.x;
+  const int lcount = *count;
+  for (int li = blockIdx.x; li < lcount; li += gridDim.x) {
+  __syncthreads();  // the previous graph's LDS use is done
+  const int64_t g = list[li];
   const int n = (int)num_nodes[g];
   const int ne = (int)num_edges[g];
   const int64_t noff = node_off[g], eoff = edge_off[g];
@@ -232,6 +425,7 @@ build_csr_kernel(const int32_t* __restrict__ src_local, const int32_t* __restric
   // inslot_ws written above by this workgroup; __syncthreads in place_edges orders it.
   place_edges<false>(ne, eoff, noff, src_local, dst_local, cnt_out, chunk_key, out_dst,
                      out_inslot, inslot_ws, n);
+  }
 }
 
 // Node groups: group g starts at the first atom of the molecule that contains atom
@@ -282,45 +476,50 @@ __global__ void node_group_kind_kernel(int64_t G, const int32_t* __restrict__ ro
 }
 
 // The fallback lists in group order (one workgroup: a running exclusive scan over chunks of
-// 1024 groups), so the fallback kernels can hand each XCD a contiguous run of molecules.
+// 1024 groups), so the fallback kernels can hand each XCD a contiguous run of molecules.  The
+// flags are 0 / 1, so a wave's prefix is a popcount of its ballot below the lane; the 16 wave
+// totals go through LDS (two barriers per chunk).
 __global__ void __launch_bounds__(1024) node_group_lists_kernel(int64_t G, int32_t* __restrict__ plan) {
   const int32_t* start = plan;
   const int32_t* kind = plan + G + 1;
   int32_t* count = plan + 2 * G + 1;
-  __shared__ int s_off[2][1024];
-  __shared__ int s_base[2];
-  const int tid = threadIdx.x;
-  if (tid < 2) s_base[tid] = 0;
-  __syncthreads();
+  __shared__ int s_w[2][16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int base0 = 0, base1 = 0;  // running list lengths (uniform)
   for (int64_t c0 = 0; c0 < G; c0 += 1024) {
     const int64_t g = c0 + tid;
-    int f[2] = {0, 0};
+    bool f0 = false, f1 = false;
     if (g < G && start[g + 1] > start[g]) {
-      f[0] = !(kind[g] & 1);
-      f[1] = !(kind[g] & 2);
+      f0 = !(kind[g] & 1);
+      f1 = !(kind[g] & 2);
     }
-    // inclusive Hillis-Steele scan of both flags
-    s_off[0][tid] = f[0];
-    s_off[1][tid] = f[1];
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-      int v0 = 0, v1 = 0;
-      if (tid >= d) { v0 = s_off[0][tid - d]; v1 = s_off[1][tid - d]; }
-      __syncthreads();
-      s_off[0][tid] += v0;
-      s_off[1][tid] += v1;
-      __syncthreads();
-    }
-    if (f[0]) plan[2 * G + 3 + s_base[0] + s_off[0][tid] - 1] = (int32_t)g;
-    if (f[1]) plan[3 * G + 3 + s_base[1] + s_off[1][tid] - 1] = (int32_t)g;
-    __syncthreads();
-    if (tid == 0) {
-      s_base[0] += s_off[0][1023];
-      s_base[1] += s_off[1][1023];
+    const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
+    if (lane == 0) {
+      s_w[0][w] = __popcll(b0);
+      s_w[1][w] = __popcll(b1);
     }
     __syncthreads();
+    int o0 = base0 + __popcll(b0 & below), o1 = base1 + __popcll(b1 & below);
+    int t0 = 0, t1 = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int a0 = s_w[0][k], a1 = s_w[1][k];
+      o0 += k < w ? a0 : 0;
+      o1 += k < w ? a1 : 0;
+      t0 += a0;
+      t1 += a1;
+    }
+    if (f0) plan[2 * G + 3 + o0] = (int32_t)g;
+    if (f1) plan[3 * G + 3 + o1] = (int32_t)g;
+    base0 += t0;
+    base1 += t1;
+    __syncthreads();  // s_w is reused by the next chunk
   }
-  if (tid < 2) count[tid] = s_base[tid];
+  if (tid == 0) {
+    count[0] = base0;
+    count[1] = base1;
+  }
 }
 
 }  // namespace
@@ -332,7 +531,9 @@ extern "C" size_t mvml_build_csr_workspace_size(int64_t num_graphs, int64_t num_
                                                 int64_t num_edges) {
   size_t nt = (size_t)ceil_div(num_graphs > 0 ? num_graphs : 1, kScanTile);
   return carve_size(nt * sizeof(int64_t)) + carve_size((size_t)num_edges * sizeof(int32_t)) +
-         carve_size((size_t)2 * num_nodes * sizeof(int)) + 256;
+         carve_size((size_t)2 * num_nodes * sizeof(int)) +
+         2 * carve_size((size_t)(num_graphs > 0 ? num_graphs : 1) * sizeof(int32_t)) +
+         carve_size(2 * sizeof(int)) + 256;
 }
 
 extern "C" int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local,
@@ -358,7 +559,11 @@ extern "C" int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local
   int64_t* tmp = cv.take<int64_t>((size_t)ceil_div(num_graphs > 0 ? num_graphs : 1, kScanTile));
   int32_t* inslot = cv.take<int32_t>((size_t)num_edges);
   int* big = cv.take<int>((size_t)2 * num_nodes);
+  int32_t* list1 = cv.take<int32_t>((size_t)(num_graphs > 0 ? num_graphs : 1));
+  int32_t* list2 = cv.take<int32_t>((size_t)(num_graphs > 0 ? num_graphs : 1));
+  int* counts = cv.take<int>(2);
   (void)hipMemsetAsync(status_flags, 0, 2 * sizeof(int32_t), st);
+  (void)hipMemsetAsync(counts, 0, 2 * sizeof(int), st);
   int rc = exclusive_scan_i64(batch_num_nodes, num_graphs, node_offsets, tmp, st);
   if (rc) return rc;
   rc = exclusive_scan_i64(batch_num_edges, num_graphs, edge_offsets, tmp, st);
@@ -369,10 +574,21 @@ extern "C" int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local
     return check_launch("build_csr(empty)");
   }
   if (num_graphs > 0) {
-    build_csr_kernel<<<(unsigned)num_graphs, kCsrThreads, 0, st>>>(
+    const CsrArgs a{src_local, dst_local, batch_num_nodes, batch_num_edges, node_offsets, edge_offsets,
+                    src, dst, node_graph, in_rowptr, in_src, in_eid, out_rowptr, out_dst,
+                    out_inslot, status_flags};
+    build_csr_wave_kernel<<<(unsigned)ceil_div(num_graphs, 4), 256, 0, st>>>(a, num_graphs, list1, counts);
+    int rc2 = check_launch("build_csr_wave_kernel");
+    if (rc2) return rc2;
+    // the molecules past the wave kernel's sizes (a device-side list: persistent grids)
+    build_csr_bigwave_kernel<<<(unsigned)std::min<int64_t>(num_graphs, 2048), 64, 0, st>>>(a, list1, counts,
+                                                                                         list2, counts + 1);
+    rc2 = check_launch("build_csr_bigwave_kernel");
+    if (rc2) return rc2;
+    build_csr_kernel<<<(unsigned)std::min<int64_t>(num_graphs, 512), kCsrThreads, 0, st>>>(
         src_local, dst_local, batch_num_nodes, batch_num_edges, node_offsets, edge_offsets,
         num_nodes, num_edges, src, dst, node_graph, in_rowptr, in_src, in_eid, out_rowptr,
-        out_dst, out_inslot, status_flags, inslot, big);
+        out_dst, out_inslot, status_flags, inslot, big, list2, counts + 1);
   }
   return check_launch("build_csr_kernel");
 }

@@ -66,6 +66,17 @@ __device__ __forceinline__ float dot4(float4 a, float4 b) {
 }
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+// streaming (non-temporal) 16-B load / store: rows read or written exactly once pass through
+// without displacing the rows an XCD's waves share in L2
+typedef float mvml_f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld4nt(const float* p) {
+  const mvml_f4v v = __builtin_nontemporal_load(reinterpret_cast<const mvml_f4v*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st4nt(float* p, float4 v) {
+  mvml_f4v w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<mvml_f4v*>(p));
+}
 
 template <int H>
 __device__ __forceinline__ float pick(const float (&a)[H], int h) {
@@ -856,6 +867,246 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
   if (out_amax) block_amax_commit<kAggThreads>(omx, out_amax);
 }
 
+// ---- Forward by destination wave (MVML_OPT_DST_FWD) -------------------------------------------
+// One wave per destination atom v.  xcd_block hands each XCD one contiguous atom range, so the
+// projection rows a destination gathers were just read by its neighbours' waves and come from
+// the XCD's L2 (tree / ring edges), or from the Infinity Cache (a hub's partners); each row
+// crosses HBM about once.  SM (fused softmax): the wave forms v's edge softmax with its lanes on
+// the in-edges (softmax_pair's arithmetic and order: max, then the sum of exp in edge order,
+// a = exp / sum) and writes attn; !SM: gat_softmax_dst_kernel wrote attn before, and the wave
+// reads it (one dependent load less per atom).  Then it gathers the WHOLE Z[src] row of each
+// in-edge into registers, U rows in flight, sums them in edge order starting from 0 (bitwise the
+// LDS / gather kernels' sums), adds residual and bias, applies ELU or the head mean and writes
+// out[v] once.  No LDS, no barriers, no size classes: one code path for every molecule size.
+// Column slots: flatten modes: lane l owns float4 columns c = l + 64 j (j < NJ, 4c < H F);
+// mean mode (H >= 2): the two half-waves own heads [0, H/2) and [H/2, H), lane l the f-float4
+// columns q = (l & 31) + 32 k (k < NJ, 4q < F) of its half's heads (6 slots per lane at
+// H = 4, F = 384, no idle lane), and the halves meet by a cross-half shuffle for the head sum,
+// added in head order (bitwise the LDS kernel's head mean).  H = 1 mean: q = l + 64 k.
+template <int H, int MODE, int NJ, int U, bool SM>
+__global__ void __launch_bounds__(256)
+gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
+                       const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ bias,
+                       const float* __restrict__ elr, float slope, float* __restrict__ attn,
+                       float* __restrict__ out, uint32_t* __restrict__ out_amax,
+                       uint32_t* __restrict__ out_rows) {
+  constexpr bool PAIR = MODE == 1 && H >= 2;
+  constexpr int NH = PAIR ? H / 2 : 1;  // heads per lane (mean mode); 1 register set (flatten)
+  const int lane = threadIdx.x & 63;
+  const int64_t v = xcd_block(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float omx = 0.f;
+  // (a non-persistent grid: the dispatcher hands out blocks in atom order, which keeps an XCD's
+  // waves on one compact window of neighbouring atoms; a persistent walk let them drift apart
+  // and ran 1.3-1.7x slower on config 5)
+  if (v < N) {  // (no early return: block_amax_commit below has a barrier)
+    const int HF = H * F;
+    const int hp = PAIR ? lane >> 5 : 0;       // mean: this lane's half (heads hp H/2 ..)
+    const int ql = PAIR ? (lane & 31) : lane;  // mean: f-float4 base of this lane
+    const float* yv = Y + v * ldy;
+    bool ok[NJ];
+    int hc[NJ];   // flatten: the head of each column slot
+    int cz[NJ];   // float offset of slot j in a projection row (mean: of head hp * NH)
+    float4 res[NJ], acc[NH][NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      if constexpr (MODE == 1) {
+        const int q = ql + (PAIR ? 32 : 64) * j;
+        ok[j] = 4 * q < F;
+        hc[j] = 0;
+        cz[j] = hp * NH * F + 4 * q;
+        // the residual first (its HBM latency overlaps the softmax); the lower half stores out
+        res[j] = (ok[j] && hp == 0) ? ld4nt(yv + HF + 4 * q) : f4(0.f);
+      } else {
+        const int c = lane + 64 * j;
+        ok[j] = 4 * c < HF;
+        hc[j] = ok[j] ? 4 * c / F : 0;
+        cz[j] = 4 * c;
+        res[j] = ok[j] ? ld4nt(yv + HF + 4 * c) : f4(0.f);
+      }
+#pragma unroll
+      for (int h = 0; h < NH; ++h) acc[h][j] = f4(0.f);
+    }
+    const int eb = rowptr[v], deg = rowptr[v + 1] - eb;
+    float er[H], m[H], sum[H], s0[H];
+    int src0 = 0;
+    // logits of the in-edges [eb + base, ...) on the lanes (edge order); -inf past the row
+    auto logits = [&](int base, int& src, float (&s)[H]) {
+      const bool in = base + lane < deg;
+      src = in ? in_src[eb + base + lane] : 0;
+#pragma unroll
+      for (int h = 0; h < H; ++h)
+        s[h] = in ? leaky(elr[(int64_t)src * 2 * H + h] + er[h], slope) : -INFINITY;
+    };
+    if constexpr (SM) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) er[h] = elr[v * 2 * H + H + h];
+      logits(0, src0, s0);
+#pragma unroll
+      for (int h = 0; h < H; ++h) m[h] = s0[h];
+      for (int base = 64; base < deg; base += 64) {  // in-degree > 64 (hubs): more chunks
+        int s_;
+        float s[H];
+        logits(base, s_, s);
+#pragma unroll
+        for (int h = 0; h < H; ++h) m[h] = fmaxf(m[h], s[h]);
+      }
+      HeadReduce<H>::template all<true>(m, lane);
+      // sum of exp in edge order (softmax_pair's order), lane by lane
+#pragma unroll
+      for (int h = 0; h < H; ++h) sum[h] = 0.f;
+      for (int base = 0; base < deg; base += 64) {
+        int s_ = src0;
+        float s[H];
+        if (base == 0) {
+#pragma unroll
+          for (int h = 0; h < H; ++h) s[h] = s0[h];
+        } else {
+          logits(base, s_, s);
+        }
+        float p[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) p[h] = base + lane < deg ? expf(s[h] - m[h]) : 0.f;
+        const int cnt = min(64, deg - base);
+        for (int i = 0; i < cnt; ++i)
+#pragma unroll
+          for (int h = 0; h < H; ++h) sum[h] += rl(p[h], i);
+      }
+    } else {
+      src0 = lane < deg ? in_src[eb + lane] : 0;
+    }
+    // (the attention of) the in-edges and the gather, 64 edges per chunk
+    for (int base = 0; base < deg; base += 64) {
+      const int cnt = min(64, deg - base);
+      int src_l = src0;
+      float a_l[H];
+      if constexpr (SM) {
+        float s[H];
+        if (base == 0) {
+#pragma unroll
+          for (int h = 0; h < H; ++h) s[h] = s0[h];
+        } else {
+          logits(base, src_l, s);
+        }
+#pragma unroll
+        for (int h = 0; h < H; ++h) a_l[h] = lane < cnt ? expf(s[h] - m[h]) / sum[h] : 0.f;
+        if (lane < cnt) {
+          float* ap = attn + (int64_t)(eb + base + lane) * H;
+          if constexpr (H == 4) {
+            st4(ap, make_float4(a_l[0], a_l[1], a_l[2], a_l[3]));
+          } else {
+#pragma unroll
+            for (int h = 0; h < H; ++h) ap[h] = a_l[h];
+          }
+        }
+      } else {
+        if (base > 0) src_l = lane < cnt ? in_src[eb + base + lane] : 0;
+        const float* ap = attn + (int64_t)(eb + base + lane) * H;
+        if constexpr (H == 4) {
+          const float4 a4 = lane < cnt ? ld4(ap) : f4(0.f);
+          a_l[0] = a4.x; a_l[1] = a4.y; a_l[2] = a4.z; a_l[3] = a4.w;
+        } else {
+#pragma unroll
+          for (int h = 0; h < H; ++h) a_l[h] = lane < cnt ? ap[h] : 0.f;
+        }
+      }
+      for (int j0 = 0; j0 < cnt; j0 += U) {
+        float4 z[U][NH][NJ];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = min(j0 + u, cnt - 1);  // past the chunk: a duplicate row, not summed
+          const float* zr = Y + (int64_t)rl(src_l, e) * ldy;
+#pragma unroll
+          for (int h = 0; h < NH; ++h)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) z[u][h][j] = ok[j] ? ld4(zr + cz[j] + h * F) : f4(0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (j0 + u < cnt) {  // (uniform)
+            float a[H];
+#pragma unroll
+            for (int h = 0; h < H; ++h) a[h] = rl(a_l[h], j0 + u);
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
+              // mean: this half's head hp NH + h (a select between the halves' heads)
+              float ah = a[h];
+              if constexpr (PAIR) ah = hp ? a[NH + h] : a[h];
+#pragma unroll
+              for (int j = 0; j < NJ; ++j)
+                acc[h][j] = fma4(MODE == 1 ? ah : pick<H>(a, hc[j]), z[u][h][j], acc[h][j]);
+            }
+          }
+        }
+      }
+    }
+    float rmx = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float4 o;
+      if constexpr (MODE == 1) {  // head mean: heads summed in order (+ bias per head), / H, + R
+        const int q = ql + (PAIR ? 32 : 64) * j;
+        const int qc = ok[j] ? 4 * q : 0;
+        float4 t[NH];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) t[h] = add4(acc[h][j], ld4(bias + (hp * NH + h) * F + qc));
+        float4 tot = t[0];
+#pragma unroll
+        for (int h = 1; h < NH; ++h) tot = add4(tot, t[h]);
+        if constexpr (PAIR) {  // + the upper half's heads, in order
+#pragma unroll
+          for (int h = 0; h < NH; ++h)
+            tot = add4(tot, make_float4(__shfl_xor(t[h].x, 32, 64), __shfl_xor(t[h].y, 32, 64),
+                                        __shfl_xor(t[h].z, 32, 64), __shfl_xor(t[h].w, 32, 64)));
+        }
+        if (!ok[j] || hp != 0) continue;
+        const float invh = (float)H;
+        o = make_float4(tot.x / invh + res[j].x, tot.y / invh + res[j].y, tot.z / invh + res[j].z,
+                        tot.w / invh + res[j].w);
+        st4nt(out + v * F + 4 * q, o);
+      } else {
+        if (!ok[j]) continue;
+        o = add4(add4(acc[0][j], res[j]), ld4(bias + cz[j]));
+        if (MODE == 0) o = make_float4(elu(o.x), elu(o.y), elu(o.z), elu(o.w));
+        st4nt(out + v * HF + cz[j], o);
+      }
+      rmx = amax4(rmx, o);
+    }
+    const float wm = wave_max(rmx);
+    omx = fmaxf(omx, wm);
+    if (out_rows && lane == 0) out_rows[v] = __float_as_uint(wm);
+  }
+  if (out_amax) block_amax_commit<256>(omx, out_amax);
+}
+
+// The edge softmax alone, one thread per (destination, head) (softmax_pair: bitwise the fused
+// kernels' attn), for gat_agg_fwd_dst_kernel<..., SM = false>.
+// *out = max(*out, max_i rows[i]) (bits of non-negative floats): the operand max of a product
+// from the per-row maxima its producer already wrote, instead of one atomicMax per 4-atom block
+// of a wave-per-atom kernel (a single word takes ~90 atomics per us: 440 k of them were most of
+// the forward's 5 ms on config 5).  A few hundred blocks, one atomic each.
+__global__ void __launch_bounds__(256)
+rows_amax_kernel(int64_t n, const uint32_t* __restrict__ rows, uint32_t* __restrict__ out) {
+  uint32_t m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    m = max(m, rows[i]);
+  block_amax_commit<256>(__uint_as_float(m), out);
+}
+
+inline int launch_rows_amax(int64_t n, const uint32_t* rows, uint32_t* out, hipStream_t st) {
+  if (!rows || !out || n <= 0) return MVML_OK;
+  rows_amax_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256 * 16), 512), 256, 0, st>>>(n, rows, out);
+  return check_launch("rows_amax_kernel");
+}
+
+template <int H>
+__global__ void __launch_bounds__(256)
+gat_softmax_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
+                       const float* __restrict__ elr, float slope, float* __restrict__ attn) {
+  const int64_t i = xcd_block(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
+  if (i >= N * H) return;
+  softmax_pair<H>(i / H, (int)(i % H), rowptr, in_src, elr, slope, attn, nullptr, 0);
+}
+
 // --------------------------------------------------------------------------------- backward
 // Backward contract (mvml_gat_agg_bwd): gY[n] = [dZ_agg | dR | d el | d er] where dZ_agg is
 // dL/dZ through update_all(u_mul_e, sum) only; the el / er paths of dL/dZ (d el x attn_l +
@@ -1601,18 +1852,8 @@ gat_agg_bwd_src_kernel(int64_t N, const int32_t* __restrict__ groups, int64_t G,
 // head, so a g_out row is loaded once per edge (not once per head).  dZ walks the out-edges in
 // out-CSR order with the atomwise pass's arithmetic (g_out / H, then fma), so it is bitwise
 // the atomwise dZ; g_a is written per edge (one writer: the edge's source) for the softmax pass.
-// streaming (non-temporal) 16-B load / store: the projection rows read once and the dZ rows
-// written once pass through without displacing the g_out rows the XCD's waves share in L2
-typedef float mvml_f4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 ld4nt(const float* p) {
-  const mvml_f4v v = __builtin_nontemporal_load(reinterpret_cast<const mvml_f4v*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void st4nt(float* p, float4 v) {
-  mvml_f4v w = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(w, reinterpret_cast<mvml_f4v*>(p));
-}
-
+// (ld4nt / st4nt: the projection rows read once and the dZ rows written once pass through
+// without displacing the g_out rows the XCD's waves share in L2)
 template <int H, int NJ>
 __global__ void __launch_bounds__(256)
 gat_mean_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
@@ -1622,7 +1863,7 @@ gat_mean_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
                         float* __restrict__ gY, int64_t ldgy, uint32_t* __restrict__ gy_amax,
                         uint32_t* __restrict__ gy_rows) {
   const int lane = threadIdx.x & 63;
-  const int64_t u = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  const int64_t u = xcd_block(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float gmx = 0.f;
   if (u < N) {  // (no early return: block_amax_commit below has a barrier)
     const int nf4 = F / 4, HF = H * F;
@@ -1704,8 +1945,9 @@ gat_mean_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
           rmx = amax4(rmx, dz[h][j]);
         }
       }
-    gmx = wave_max(rmx);
-    if (gy_rows && lane == 0) gy_rows[u] = __float_as_uint(gmx);  // the first writer of the row
+    const float wm = wave_max(rmx);
+    gmx = fmaxf(gmx, wm);
+    if (gy_rows && lane == 0) gy_rows[u] = __float_as_uint(wm);  // the first writer of the row
   }
   if (gy_amax) block_amax_commit<256>(gmx, gy_amax);
 }
@@ -1882,6 +2124,152 @@ gat_flat_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
   if (gy_amax) block_amax_commit<256>(gmx, gy_amax);
 }
 
+// The flatten layer's backward by source atom in ONE pass (MVML_OPT_FLAT_SRC = 2): no g_rst pass
+// and no re-read of a g_rst block.  The wave of source u forms its own g_rst row once from
+// g_out[u] and out[u] (ELU'(x) = out + 1 below 0, as gat_flat_grst_kernel) and writes it as dR[u];
+// for each out-edge u -> w it gathers the g_out[w] (and out[w]) rows — read by w's own wave and by
+// w's other in-neighbours' waves at about the same time, so from the XCD's L2 — and forms g_rst[w]
+// in registers with the same arithmetic, then dZ[u] += a_e g_rst[w] (out-CSR order) and
+// g_a[e] = <Z[u], g_rst[w]> per head.  Bitwise the two-pass path's gY and g_a.
+template <int H, int NJ, int MODE>
+__global__ void __launch_bounds__(256)
+gat_flat_bwd_src1_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
+                         const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
+                         const float* __restrict__ Y, int64_t ldy, const float* __restrict__ attn,
+                         const float* __restrict__ out, const float* __restrict__ g_out, int F,
+                         float* __restrict__ ga, float* __restrict__ gY, int64_t ldgy,
+                         uint32_t* __restrict__ gy_amax, uint32_t* __restrict__ gy_rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t u = xcd_block(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float gmx = 0.f;
+  if (u < N) {  // (no early return: block_amax_commit below has a barrier)
+    const int HF = H * F;
+    bool okc[NJ];
+    int hc[NJ];
+    float4 z[NJ], dz[NJ];
+    float rmx = 0.f;
+    auto grst = [&](int64_t w, int c) -> float4 {  // g_rst[w, 4 (lane + 64 c) ..]
+      const int col = 4 * (lane + 64 * c);
+      float4 g = ld4(g_out + w * HF + col);
+      if (MODE == 0) {
+        const float4 o = ld4(out + w * HF + col);
+        g.x *= o.x > 0.f ? 1.f : o.x + 1.f;
+        g.y *= o.y > 0.f ? 1.f : o.y + 1.f;
+        g.z *= o.z > 0.f ? 1.f : o.z + 1.f;
+        g.w *= o.w > 0.f ? 1.f : o.w + 1.f;
+      }
+      return g;
+    };
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) {
+      const int col = 4 * (lane + 64 * c);
+      okc[c] = col < HF;
+      hc[c] = okc[c] ? col / F : 0;
+      z[c] = okc[c] ? ld4nt(Y + u * ldy + col) : f4(0.f);
+      dz[c] = f4(0.f);
+      if (okc[c]) {  // dR[u] = g_rst[u]
+        const float4 g = grst(u, c);
+        st4nt(gY + u * ldgy + HF + col, g);
+        rmx = amax4(rmx, g);
+      }
+    }
+    const int ob = out_rowptr[u], oe = out_rowptr[u + 1];
+    for (int base = ob; base < oe; base += 64) {
+      const int cnt = min(64, oe - base);
+      int w_l = 0, s_l = 0;
+      float a_l[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) a_l[h] = 0.f;
+      if (lane < cnt) {
+        w_l = out_dst[base + lane];
+        s_l = out_inslot[base + lane];
+#pragma unroll
+        for (int h = 0; h < H; ++h) a_l[h] = attn[(int64_t)s_l * H + h];
+      }
+      for (int j = 0; j < cnt; j += 2) {  // two out-neighbours' rows in flight
+        const int j1 = min(j + 1, cnt - 1);
+        const bool two = j + 1 < cnt;  // (uniform)
+        const int64_t w0 = rl(w_l, j), w1 = rl(w_l, j1);
+        float4 g0[NJ], g1[NJ];
+#pragma unroll
+        for (int c = 0; c < NJ; ++c) {
+          g0[c] = okc[c] ? grst(w0, c) : f4(0.f);
+          g1[c] = okc[c] ? grst(w1, c) : f4(0.f);
+        }
+        float a0[H], a1[H], p0[H], p1[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) { a0[h] = rl(a_l[h], j); a1[h] = rl(a_l[h], j1); p0[h] = 0.f; p1[h] = 0.f; }
+#pragma unroll
+        for (int c = 0; c < NJ; ++c)
+          if (okc[c]) {
+            dz[c] = fma4(pick<H>(a0, hc[c]), g0[c], dz[c]);
+            if (two) dz[c] = fma4(pick<H>(a1, hc[c]), g1[c], dz[c]);
+            add_at<H>(p0, hc[c], dot4(z[c], g0[c]));
+            add_at<H>(p1, hc[c], dot4(z[c], g1[c]));
+          }
+        HeadReduce<H>::template all<false>(p0, lane);
+        store_heads<H>(ga + (int64_t)rl(s_l, j) * H, p0, lane);
+        if (two) {
+          HeadReduce<H>::template all<false>(p1, lane);
+          store_heads<H>(ga + (int64_t)rl(s_l, j1) * H, p1, lane);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NJ; ++c)
+      if (okc[c]) {
+        st4nt(gY + u * ldgy + 4 * (lane + 64 * c), dz[c]);
+        rmx = amax4(rmx, dz[c]);
+      }
+    const float wm = wave_max(rmx);
+    gmx = fmaxf(gmx, wm);
+    if (gy_rows && lane == 0) gy_rows[u] = __float_as_uint(wm);  // the first writer of the row
+  }
+  if (gy_amax) block_amax_commit<256>(gmx, gy_amax);
+}
+
+template <int H>
+int launch_flat_src1(int64_t N, const int32_t* rp, const int32_t* src, const int32_t* orp,
+                     const int32_t* odst, const int32_t* oslot, const float* Y, int64_t ldy,
+                     const float* elr, const float* attn, const float* out, const float* g_out, int F,
+                     float slope, int mode, float* gpre, float* gY, int64_t ldgy, int C, uint32_t* gy_amax,
+                     uint32_t* gy_rows, hipStream_t st) {
+  const int HF = H * F;
+  const int nj = (int)ceil_div(HF / 4, 64);
+  const unsigned b4 = (unsigned)ceil_div(N, 4), b256 = (unsigned)ceil_div(N, 256);
+  uint32_t* const blk_amax = gy_rows ? nullptr : gy_amax;  // (see launch_mean_src)
+#define MVML_FLAT_SRC1(NJ)                                                                                   \
+  do {                                                                                                       \
+    if (mode == 0)                                                                                           \
+      gat_flat_bwd_src1_kernel<H, NJ, 0><<<b4, 256, 0, st>>>( \
+          N, orp, odst, oslot, Y, ldy, attn, out, g_out, F, gpre, gY, ldgy, blk_amax, gy_rows);               \
+    else                                                                                                     \
+      gat_flat_bwd_src1_kernel<H, NJ, 2><<<b4, 256, 0, st>>>( \
+          N, orp, odst, oslot, Y, ldy, attn, out, g_out, F, gpre, gY, ldgy, blk_amax, gy_rows);               \
+  } while (0)
+  switch (nj) {
+    case 1: MVML_FLAT_SRC1(1); break;
+    case 2: MVML_FLAT_SRC1(2); break;
+    case 3: MVML_FLAT_SRC1(3); break;
+    case 4: MVML_FLAT_SRC1(4); break;
+    case 5: MVML_FLAT_SRC1(5); break;
+    case 6: MVML_FLAT_SRC1(6); break;
+    case 7: MVML_FLAT_SRC1(7); break;
+    case 8: MVML_FLAT_SRC1(8); break;
+    default: set_error("gat_agg_bwd: flat-src path needs H F <= 2048"); return MVML_ERR_INVALID;
+  }
+#undef MVML_FLAT_SRC1
+  int rc = check_launch("gat_flat_bwd_src1_kernel");
+  if (rc) return rc;
+  gat_mean_bwd_softmax_kernel<H><<<b256, 256, 0, st>>>(N, rp, src, elr, attn, slope, gpre, gY, ldgy, C);
+  rc = check_launch("gat_mean_bwd_softmax_kernel");
+  if (rc) return rc;
+  gat_mean_bwd_gel_kernel<H><<<b256, 256, 0, st>>>(N, orp, oslot, gpre, gY, ldgy, C, blk_amax, gy_rows);
+  rc = check_launch("gat_mean_bwd_gel_kernel");
+  if (rc) return rc;
+  return launch_rows_amax(N, gy_rows, gy_amax, st);
+}
+
 template <int H>
 int launch_flat_src(int64_t N, const int32_t* rp, const int32_t* src, const int32_t* orp,
                     const int32_t* odst, const int32_t* oslot, const float* Y, int64_t ldy,
@@ -1926,9 +2314,11 @@ int launch_mean_src(int64_t N, const int32_t* rp, const int32_t* src, const int3
                     hipStream_t st) {
   const int nj = (int)ceil_div(F / 4, 64);
   const unsigned b4 = (unsigned)ceil_div(N, 4), b256 = (unsigned)ceil_div(N, 256);
+  // with per-row maxima requested, max |gY| comes from them at the end (no per-block atomics)
+  uint32_t* const blk_amax = gy_rows ? nullptr : gy_amax;
 #define MVML_MEAN_SRC(NJ) \
-  gat_mean_bwd_src_kernel<H, NJ><<<b4, 256, 0, st>>>(N, orp, odst, oslot, Y, ldy, attn, g_out, F, gpre, gY, \
-                                                     ldgy, gy_amax, gy_rows)
+  gat_mean_bwd_src_kernel<H, NJ><<<b4, 256, 0, st>>>( \
+      N, orp, odst, oslot, Y, ldy, attn, g_out, F, gpre, gY, ldgy, blk_amax, gy_rows)
   switch (nj) {
     case 1: MVML_MEAN_SRC(1); break;
     case 2: MVML_MEAN_SRC(2); break;
@@ -1942,8 +2332,10 @@ int launch_mean_src(int64_t N, const int32_t* rp, const int32_t* src, const int3
   gat_mean_bwd_softmax_kernel<H><<<b256, 256, 0, st>>>(N, rp, src, elr, attn, slope, gpre, gY, ldgy, C);
   rc = check_launch("gat_mean_bwd_softmax_kernel");
   if (rc) return rc;
-  gat_mean_bwd_gel_kernel<H><<<b256, 256, 0, st>>>(N, orp, oslot, gpre, gY, ldgy, C, gy_amax, gy_rows);
-  return check_launch("gat_mean_bwd_gel_kernel");
+  gat_mean_bwd_gel_kernel<H><<<b256, 256, 0, st>>>(N, orp, oslot, gpre, gY, ldgy, C, blk_amax, gy_rows);
+  rc = check_launch("gat_mean_bwd_gel_kernel");
+  if (rc) return rc;
+  return launch_rows_amax(N, gy_rows, gy_amax, st);
 }
 
 template <int H>
@@ -1951,6 +2343,56 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
                const float* Y, int64_t ldy, int F, const float* bias, float slope, int mode,
                float* out, float* attn, const float* elr, uint32_t* out_amax, uint32_t* out_rows,
                hipStream_t st) {
+  if (option(MVML_OPT_DST_FWD) && H * F <= 2048) {  // one wave per destination atom, every atom
+    const unsigned b4 = (unsigned)ceil_div(N, 4);
+    const int HF = H * F;
+    const bool sm = option(MVML_OPT_DST_FWD) == 1;  // 2: the softmax as its own launch first
+    // with per-row maxima requested, max |out| comes from them afterwards (no per-block atomics)
+    uint32_t* const blk_amax = out_rows ? nullptr : out_amax;
+    if (!sm) {
+      gat_softmax_dst_kernel<H><<<(unsigned)ceil_div(N * H, 256), 256, 0, st>>>(N, rp, src, elr, slope, attn);
+      int rc = check_launch("gat_softmax_dst_kernel");
+      if (rc) return rc;
+    }
+#define MVML_DST_FWD(M, NJ, U)                                                                    \
+  do {                                                                                            \
+    if (sm)                                                                                       \
+      gat_agg_fwd_dst_kernel<H, M, NJ, U, true>                                                   \
+          <<<b4, 256, 0, st>>>(   \
+              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);             \
+    else                                                                                          \
+      gat_agg_fwd_dst_kernel<H, M, NJ, U, false>                                                  \
+          <<<b4, 256, 0, st>>>(  \
+              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);             \
+  } while (0)
+    // rows in flight per wave (MVML_OPT_DST_UNR, H = 4 at the GAT widths: tuning A/B)
+    const int unr = option(MVML_OPT_DST_UNR);
+    if (mode == 1) {  // mean: half-waves over the heads, lanes over F / 4
+      const int nj = (int)ceil_div(F / 4, H >= 2 ? 32 : 64);
+      if (nj == 1) MVML_DST_FWD(1, 1, 4);
+      else if (nj == 2) MVML_DST_FWD(1, 2, 2);
+      else if (nj == 3 && H == 4 && unr == 1) MVML_DST_FWD(1, 3, 1);
+      else if (nj == 3 && H == 4 && unr == 3) MVML_DST_FWD(1, 3, 3);
+      else if (nj == 3) MVML_DST_FWD(1, 3, 2);
+      else if (nj <= 4) MVML_DST_FWD(1, 4, 2);
+      else { set_error("gat_agg_fwd: dst path needs F <= %d in mean mode", H >= 2 ? 512 : 1024); return MVML_ERR_INVALID; }
+    } else {
+      const int nj = (int)ceil_div(HF / 4, 64);
+#define MVML_DST_FWD_F(NJ, U) do { if (mode == 0) MVML_DST_FWD(0, NJ, U); else MVML_DST_FWD(2, NJ, U); } while (0)
+      if (nj == 1) MVML_DST_FWD_F(1, 4);
+      else if (nj == 2) MVML_DST_FWD_F(2, 4);
+      else if (nj == 3 && H == 4 && unr == 1) MVML_DST_FWD_F(3, 1);
+      else if (nj == 3 && H == 4 && unr == 4) MVML_DST_FWD_F(3, 4);
+      else if (nj == 3) MVML_DST_FWD_F(3, 2);  // fewer rows in flight, more waves: faster
+      else if (nj == 4) MVML_DST_FWD_F(4, 2);
+      else MVML_DST_FWD_F(8, 2);
+#undef MVML_DST_FWD_F
+    }
+#undef MVML_DST_FWD
+    int rc = check_launch("gat_agg_fwd_dst_kernel");
+    if (rc) return rc;
+    return launch_rows_amax(N, out_rows, out_amax, st);
+  }
   if (G == 0) return MVML_OK;
   const bool big = use_big_window(H, F);
   // the edge_softmax runs inside each kernel for its own groups (no separate softmax launch)
@@ -1997,6 +2439,9 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
   if (mode == 1 && option(MVML_OPT_MEAN_SRC) && F <= 1024)  // head-mean layer by source atom
     return launch_mean_src<H>(N, rp, src, orp, odst, oslot, Y, ldy, elr, attn, g_out, F, slope, gpre, gY,
                               ldgy, C, gy_amax, gy_rows, st);
+  if (mode != 1 && option(MVML_OPT_FLAT_SRC) == 2)  // flatten layer by source atom, one pass
+    return launch_flat_src1<H>(N, rp, src, orp, odst, oslot, Y, ldy, elr, attn, out, g_out, F, slope, mode,
+                               gpre, gY, ldgy, C, gy_amax, gy_rows, st);
   if (mode != 1 && option(MVML_OPT_FLAT_SRC))  // flatten layer by source atom (large molecules)
     return launch_flat_src<H>(N, rp, src, orp, odst, oslot, Y, ldy, elr, attn, out, g_out, F, slope, mode,
                               gpre, gY, ldgy, C, gy_amax, gy_rows, st);

@@ -2280,8 +2280,12 @@ int64_t k_chunk(int64_t K, int S) { return ceil_div(ceil_div(K, S), BKT) * BKT; 
 // every shape of the step (L1 projection 4.73 -> 4.29 ms, L2 forward 16.9 -> 16.3 ms; the step
 // +1 %, profiles/r04_gemm_persist.txt); P = 0 gives one workgroup per tile.
 unsigned x3w_grid_x(int64_t tiles, int S) {
-  const int persist = option(MVML_OPT_GEMM_PERSIST);
-  if (S > 1 || persist <= 0 || tiles <= persist) return (unsigned)tiles;
+  // the persistent kernels give XCD x (the workgroups b % 8 == x) one tile range each, so the
+  // cap is rounded up to a multiple of 8: every XCD gets a workgroup and every range is walked
+  int persist = option(MVML_OPT_GEMM_PERSIST);
+  if (S > 1 || persist <= 0) return (unsigned)tiles;
+  persist = (persist + 7) / 8 * 8;
+  if (tiles <= persist) return (unsigned)tiles;
   return (unsigned)persist;
 }
 

@@ -199,9 +199,32 @@ class BatchedMolGraph:
                   P(d["node_groups"]), _lib.stream_ptr(device))
         d["group_offsets"] = torch.as_tensor(self.group_offsets_host()).to(device)
         d["group_node_offsets"] = None
-        # keep the uploaded inputs alive until the stream has consumed them
-        d["_inputs"] = (bnn, bne, src_l, dst_l)
+        # keep the uploaded inputs: recollate() re-runs the collation from them
+        d["_inputs"] = (bnn, bne, src_l, dst_l, flags)
         self._dev = d
+
+    def recollate(self):
+        """Re-run the device collation (dgl.batch + CSR build + node-group plan) from the
+        resident per-molecule LOCAL edge lists into this batch's index buffers, with no host
+        synchronisation (the id checks ran at the first build).  The reference collates every
+        step on the host (dataset.py:52-54, DataLoader collate_fn); bench.py does it here, inside
+        its timed step.  Same stream as the kernels that read the indices, so it is ordered
+        behind the previous step's readers."""
+        d = self._dev
+        if d is None:
+            raise RuntimeError("recollate() needs a device batch (.to('cuda') first)")
+        bnn, bne, src_l, dst_l, flags = d["_inputs"]
+        B, N, E = self.batch_size, self.num_nodes(), self.num_edges()
+        L = _lib.lib()
+        wp, wn = _lib.ws_ptr_size(L.mvml_build_csr_workspace_size(B, N, E), self.device)
+        P = _lib.ptr
+        st = _lib.stream_ptr(self.device)
+        _lib.call("mvml_build_csr", P(src_l), P(dst_l), P(bnn), P(bne), B, N, E,
+                  P(d["node_offsets"]), P(d["edge_offsets"]), P(d["src"]), P(d["dst"]),
+                  P(d["node_graph"]), P(d["in_rowptr"]), P(d["in_src"]), P(d["in_eid"]),
+                  P(d["out_rowptr"]), P(d["out_dst"]), P(d["out_inslot"]), P(flags), wp, wn, st)
+        _lib.call("mvml_build_node_groups", B, N, P(d["node_offsets"]), P(d["in_rowptr"]),
+                  P(d["node_groups"]), st)
 
     def group_offsets_rows(self):
         """GraphNorm group offsets in molecules (rows of the (B, 2D) readout)."""

@@ -80,11 +80,15 @@ class FlatGradAllReduce:
     so one bucket beats per-tensor collectives).
 
     Parameters whose ``grad`` is None on EVERY rank stay None, as in the single-device
-    reference: torch Adam (main.py:88) skips them, so weight decay does not move the
-    constructed-but-unused LayerNorms (model.py:42, 120).  The buffer carries one presence
-    flag per parameter after the gradients (same collective): a parameter that has a gradient
-    on some rank but not on another gets the sum over the ranks that have one (zeros elsewhere,
-    DDP's convention); one with no gradient anywhere is left None."""
+    reference: torch Adam (main.py:88, weight_decay 1e-4) skips them, so weight decay does not
+    move the constructed-but-unused LayerNorms (model.py:42, 120).  The buffer carries one
+    presence flag per parameter after the gradients (same collective): a parameter that has a
+    gradient on some rank but not on another gets the sum over the ranks that have one (zeros
+    elsewhere, DDP's convention); one with no gradient anywhere is left None.  The reduced flags
+    (P integers) are read back every step: which parameters the OTHER ranks used can change while
+    this rank's own pattern stays the same, and only the reduced flags say so (a cache keyed on
+    the local pattern once left such a parameter None here while another rank stepped it).  The
+    read-back is one small device-to-host copy after the all-reduce."""
 
     def __init__(self, params, average=False, group=None):
         self.params = [p for p in params if p.requires_grad]
@@ -94,7 +98,6 @@ class FlatGradAllReduce:
         self.buf = None
         self.views = None
         self._flags = {}    # local presence pattern -> its flags on the device (built once)
-        self._present = {}  # local presence pattern -> presence over all ranks (read back once)
 
     def _bind(self, dev):
         """One flat buffer; each parameter's gradient becomes a view of its segment, so autograd
@@ -127,11 +130,7 @@ class FlatGradAllReduce:
             fl = self._flags[local] = torch.tensor(local, dtype=self.buf.dtype).to(dev)
         self.buf[self.numel:].copy_(fl)  # device to device: no host round trip per step
         dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group)
-        present = self._present.get(local)
-        if present is None:
-            # read back once per local pattern: the ranks run the same model, so the pattern a
-            # rank sees for a given local pattern does not change between steps
-            present = self._present[local] = tuple((self.buf[self.numel:] > 0).tolist())
+        present = (self.buf[self.numel:] > 0).tolist()  # the GLOBAL pattern of this step
         if self.average:
             self.buf[:self.numel].div_(dist.get_world_size(self.group))
         for p, v, has in zip(self.params, self.views, present):

@@ -247,14 +247,34 @@ def colsum(X, M, N, ldx, out, beta=0.0, offset=0, alpha=1.0):
 # DESIGN.md "Layer 1 by re-association").
 REASSOC_X = os.environ.get("MVML_GAT_REASSOC", "0") == "1"
 
-# Flatten layers' aggregation backward by source atom (option flat_src, csrc/gat_agg.hip
-# gat_flat_bwd_src_kernel) for batches whose atoms sit mostly in molecules past the LDS molecule
-# window.  Off by default (MVML_FLAT_SRC_AUTO=1 turns the rule on): measured slower than the big
-# window on config 5 (16.5 vs 13.4 ms per launch) and than the molecule window on config 3 (11.0
-# vs 5.6 ms) — the H F-wide g_rst rows gathered per edge do not stay in L2 the way the head-mean
-# layer's F-wide g_out rows do (profiles/r04_flat_src_ab.txt).
-FLAT_SRC_AUTO = os.environ.get("MVML_FLAT_SRC_AUTO", "0") == "1"
+# Kernel paths picked per call from the batch's molecule sizes (host counts, no device work):
+# "large" batches have half their atoms or more in molecules past the LDS molecule window
+# (FLAT_SRC_MIN_ATOMS, gat_agg.hip kWinL) — BASELINE config 5.
+#  * Aggregation forward by destination wave (option dst_fwd = 2: the edge softmax as its own
+#    launch, then one wave per atom gathers whole projection rows from L2; csrc/gat_agg.hip
+#    gat_agg_fwd_dst_kernel): flatten layers always, the head-mean layer on large batches
+#    (MVML_DST_FWD_POLICY = auto | all | off).
+#  * Flatten layers' aggregation backward by source atom in one pass (option flat_src = 2,
+#    gat_flat_bwd_src1_kernel) on large batches (MVML_FLAT_SRC_AUTO = 0 turns it off).
+FLAT_SRC_AUTO = os.environ.get("MVML_FLAT_SRC_AUTO", "1") == "1"
 FLAT_SRC_MIN_ATOMS = 128  # the LDS molecule window (gat_agg.hip kWinL)
+DST_FWD_POLICY = os.environ.get("MVML_DST_FWD_POLICY", "auto")
+#  * The ELU link (EluLink, below): the second layer's data-gradient GEMM applies ELU' in its
+#    epilogue, so the first layer's backward gathers g_rst rows only (no `out` rows) — on large
+#    batches, where that backward gathers rows per out-edge (flat_src); on small ones the
+#    epilogue's extra read costs more than the molecule window saves (MVML_ELU_LINK = auto | on
+#    | off).
+ELU_LINK_POLICY = os.environ.get("MVML_ELU_LINK", "auto")
+
+
+def _large_batch(g):
+    return g.large_molecule_fraction(FLAT_SRC_MIN_ATOMS) >= 0.5
+
+
+def _fwd_path(g, mode):
+    """Context manager selecting the aggregation forward kernel path for this call."""
+    dst = DST_FWD_POLICY == "all" or (DST_FWD_POLICY == "auto" and (mode != MODE_MEAN or _large_batch(g)))
+    return _lib.option("dst_fwd", 2) if dst else contextlib.nullcontext()
 
 
 
@@ -320,9 +340,6 @@ class GATLayerFunction(torch.autograd.Function):
                                                g, H, F, slope, mode, C)
         link = _elu_link_of(X) if (ELU_LINK[0] and (algo or GEMM_ALGO) == "f16x2" and ROW_SCALES
                                    and PROJ_ELR_GEMM and X.requires_grad) else None
-        if link is not None and not link.claimed and Fp == Fin:
-            link.claimed = True
-            ctx.elu_claim = link
         # [fc.weight ; res_fc.weight (or its head mean) ; A_l ; A_r]: the projection GEMM uses
         # the first C rows, the backward all C + 2H (the el / er paths, see mvml_gat_agg_bwd)
         Wcat = torch.empty((C + 2 * H, Fp), dtype=torch.float32, device=dev)
@@ -359,6 +376,12 @@ class GATLayerFunction(torch.autograd.Function):
             # Wcat split once: the projection's tiles and the backward's dL/dX read the planes
             wps = split_planes(Wcat, C + 2 * H, Fp, Fp, slot(amx, 1))
             wil = split_il4(Wcat, C + 2 * H, Fp, Fp, slot(amx, 1))
+        # claim the previous layer's ELU link only where the fused data-gradient product will
+        # run (per-row scales and the interleaved weight image: see backward)
+        if (link is not None and not link.claimed and Fp == Fin and amx is not None
+                and wil is not None):
+            link.claimed = True
+            ctx.elu_claim = link
         bf16_elr = (algo or GEMM_ALGO) == "bf16" and PROJ_ELR_GEMM
         if (amx is not None or bf16_elr) and PROJ_ELR_GEMM:
             # el / er as 2H more GEMM columns: X [A_l ; A_r]^T with A_l[h] = sum_f attn_l[h, f]
@@ -394,13 +417,22 @@ class GATLayerFunction(torch.autograd.Function):
         # per-row max |out| for the consumer's per-row split-fp16 GEMMs (next layer, Set2Set)
         orows = torch.empty(max(N, 1), dtype=torch.int32, device=dev) if (amx is not None and ROW_SCALES) else None
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}", "bytes": agg_fwd_bytes(N, E, H, F, out_cols, C - HF)}
-        call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
-             ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(_c(bias)), float(slope), int(mode),
-             ptr(out), ptr(attn), slot(amx, 3), ptr(orows), st)
+        with _fwd_path(g, mode):
+            call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
+                 ptr(g.in_src), ptr(Y), ldy, H, F, ptr(elr), ptr(_c(bias)), float(slope), int(mode),
+                 ptr(out), ptr(attn), slot(amx, 3), ptr(orows), st)
         if amx is not None:  # max |out| for the consumer's split-fp16 GEMMs (next layer, Set2Set)
             fold_amax(out, amx, 3)
         if orows is not None:
             fold_rows(out, orows)
+        # flatten + ELU inside a GAT stack: the next layer's data-gradient GEMM may apply ELU'
+        # in its epilogue (EluLink), so this layer's backward receives g_rst and reads no `out`
+        ctx.link = None
+        if (mode == MODE_FLATTEN_ELU and ELU_LINK[0] and amx is not None and ROW_SCALES
+                and PROJ_ELR_GEMM
+                and (ELU_LINK_POLICY == "on" or (ELU_LINK_POLICY == "auto" and _large_batch(g)))):
+            ctx.link = EluLink(dev)
+            out._mvml_elu = (ctx.link, out._version, (out.data_ptr(), tuple(out.shape), out.stride()))
         if DEBUG_CAPTURE is not None:
             DEBUG_CAPTURE.setdefault("elr_fwd", []).append(elr.detach().clone())
         ctx.save_for_backward(Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr)
@@ -543,6 +575,17 @@ class GATLayerFunction(torch.autograd.Function):
             return GATLayerFunction._backward_x(ctx, g_out)
         Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr = ctx.saved_tensors
         g, H, F, mode, ldy = ctx.g, ctx.H, ctx.F, ctx.mode, ctx.ldy
+        link = ctx.link
+        if link is not None and link.claimed:
+            # the next layer's data-gradient GEMM applied ELU' already: g_out IS g_rst, and the
+            # aggregation backward runs as plain flatten (mode 2: no ELU', no read of `out`)
+            gr = link.g_rst
+            if gr is None or g_out.data_ptr() != gr.data_ptr() or g_out.shape != gr.shape \
+                    or g_out.stride() != gr.stride():
+                raise RuntimeError("GAT ELU link: the gradient reaching the first layer is not the one "
+                                   "the next layer's fused ELU backward wrote (was its output also "
+                                   "consumed elsewhere?)")
+            mode = MODE_FLATTEN
         g_out = _c(g_out)
         N, Fp = Xp.shape
         Fin = ctx.Fin
@@ -560,14 +603,14 @@ class GATLayerFunction(torch.autograd.Function):
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_agg_bwd_workspace_size(g.num_edges(), H), dev)
         # per-row max |gY| for the data-gradient product's per-row scales (not needed by layer 1,
         # whose input gradient is not formed)
+        flat_src = FLAT_SRC_AUTO and mode != MODE_MEAN and _large_batch(g)
         gyr = None
-        if ctx.amx is not None and ROW_SCALES and ctx.needs_input_grad[0]:
+        if ctx.amx is not None and ROW_SCALES and (ctx.needs_input_grad[0] or flat_src):
+            # (the source-atom kernels then form max |gY| from the row maxima: no per-block atomics)
             gyr = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
         _lib.call_tag[0] = {"layer": f"H{H}xF{F}",
                             "bytes": agg_bwd_bytes(N, g.num_edges(), H, F, g_out.shape[1], mode)}
-        flat_src = (FLAT_SRC_AUTO and mode != MODE_MEAN
-                    and g.large_molecule_fraction(FLAT_SRC_MIN_ATOMS) >= 0.5)
-        with (_lib.option("flat_src", 1) if flat_src else contextlib.nullcontext()):
+        with (_lib.option("flat_src", 2) if flat_src else contextlib.nullcontext()):
             call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr),
                  ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy,
                  ptr(elr), ptr(attn), ptr(out), ptr(g_out), H, F, float(ctx.slope), int(mode), ptr(gY),

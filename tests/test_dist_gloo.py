@@ -245,3 +245,45 @@ def test_two_rank_mvp_train_step_keeps_reference_adam_semantics():
     for n, w in want.items():
         d = (torch.as_tensor(got[n]) - w).abs().max().item()
         assert d <= 1e-12 * max(1.0, w.abs().max().item()), (n, d)
+
+
+def _pattern_worker(rank, world, port, out):
+    """Step 1: no rank uses parameter b.  Step 2: only rank 1 does — rank 0's LOCAL pattern is
+    the same in both steps, so only the reduced flags tell it that b now has a gradient."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a = torch.nn.Parameter(torch.ones(3, dtype=torch.float64))
+    b = torch.nn.Parameter(torch.ones(2, dtype=torch.float64))
+    red = FlatGradAllReduce([a, b])
+    seen = []
+    for step in range(2):
+        a.grad = b.grad = None
+        loss = (a * (rank + 1)).sum()
+        if step == 1 and rank == 1:
+            loss = loss + (b * 3).sum()
+        loss.backward()
+        red()
+        seen.append(None if b.grad is None else b.grad.tolist())
+    out.put((rank, seen, a.grad.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_flat_allreduce_follows_other_ranks_presence_changes():
+    """the presence flags must follow the GLOBAL pattern every step (a cache keyed
+    on the local pattern left b None on rank 0 while rank 1 stepped it)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pattern_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (seen, ag)) for r, seen, ag in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in range(2):
+        seen, ag = got[r]
+        assert seen[0] is None, (r, seen)          # nobody used b: stays None (Adam skips it)
+        assert seen[1] == [3.0, 3.0], (r, seen)    # rank 1's gradient, summed, on BOTH ranks
+        assert ag == [3.0, 3.0, 3.0]               # 1 + 2

@@ -11,7 +11,7 @@ makes) of the single-process ones — the all-reduce re-associates each sum, and
 (layer 2's bias under GraphNorm's mean-free gradient: 3.7e-5) keep that error relative to their
 terms, not to the small result — the gathered embeddings
 BITWISE equal (per-row split-fp16 scales: a molecule's embedding does not depend on its batch),
-and a second step reusing the reducer's cached presence flags.
+and a second step through the same reducer (gradients accumulated in its flat buffer).
 """
 import json
 import os
@@ -101,7 +101,6 @@ _CHILD = textwrap.dedent(r"""
         out["grad_rel_max"] = max(e[1] for e in errs)
         out["grad2_equal"] = all((a is None and b is None) or torch.equal(a, b) for a, b in zip(grads, grads2))
         out["grads_none"] = sum(a is None for a in grads)
-        out["flags_cached"] = len(red._present)
     torch.cuda.synchronize()
     dist.barrier()
     dist.destroy_process_group()
@@ -146,4 +145,4 @@ def test_two_hip_ranks_match_single_process():
     assert 0 < r0["shard"][1] < 384  # both ranks hold molecules
     assert r0["emb_bitwise"], r0
     assert r0["grad_ratio"] < 1, r0
-    assert r0["grad2_equal"] and r0["flags_cached"] == 1, r0
+    assert r0["grad2_equal"], r0

@@ -26,6 +26,9 @@ def _to_dev(sb, group_size=None):
     ([11, 23, 80, 5, 1, 40, 23], False),
     ([150, 300, 220], True),
     ([1] * 5, False),
+    # one wave per molecule up to 256 atoms / 1024 edges, a workgroup for the rest, in one batch
+    ([25, 300, 255, 257, 1, 64, 90, 256], True),
+    ([256, 255, 257, 2, 3], False),
 ])
 def test_build_csr_bit_exact(sizes, hubs):
     sb = batch_of_sizes(sizes, seed=3, hubs=hubs)
@@ -78,6 +81,28 @@ def test_build_csr_edge_cases():
     for k in ("in_rowptr", "in_src", "in_eid", "out_rowptr", "out_dst", "out_inslot"):
         np.testing.assert_array_equal(getattr(bg, k).cpu().numpy(), csr[k], err_msg=k)
     assert bg.has_zero_in_degree is True and csr["zero_in_degree"] == 1
+
+
+def test_recollate_reproduces_indices():
+    """BatchedMolGraph.recollate() (bench.py's per-step device collation) rebuilds every index
+    and the node-group plan into the same buffers, bitwise equal to the first build."""
+    sb = batch_of_sizes([11, 23, 80, 5, 1, 40, 23, 130, 64, 300, 150], seed=6, hubs=True)
+    g = _to_dev(sb)
+    keys = ("node_offsets", "edge_offsets", "src", "dst", "node_graph", "in_rowptr", "in_src",
+            "in_eid", "out_rowptr", "out_dst", "out_inslot", "node_groups")
+    first = {k: getattr(g, k).clone() for k in keys}
+    for k in keys:
+        getattr(g, k).fill_(-7)
+    g.recollate()
+    torch.cuda.synchronize()
+    for k in keys[:-1]:
+        assert torch.equal(getattr(g, k), first[k]), k
+    G = g.num_node_groups
+    a, b = first["node_groups"].cpu().numpy(), g.node_groups.cpu().numpy()
+    np.testing.assert_array_equal(a[:2 * G + 3], b[:2 * G + 3])  # starts, kinds, list counts
+    nf, nb = int(a[2 * G + 1]), int(a[2 * G + 2])
+    np.testing.assert_array_equal(a[2 * G + 3:2 * G + 3 + nf], b[2 * G + 3:2 * G + 3 + nf])
+    np.testing.assert_array_equal(a[3 * G + 3:3 * G + 3 + nb], b[3 * G + 3:3 * G + 3 + nb])
 
 
 def test_build_csr_rejects_bad_ids():

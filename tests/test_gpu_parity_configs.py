@@ -211,7 +211,92 @@ def test_gat_layer0_flat_src(case):
         _layer_case(0, sb, seed=8)
 
 
-@pytest.mark.parametrize("flat_src", [0, 1])
+_FAMILIES = {"config2": lambda: synth.config2(128, seed=0),
+             "config5": lambda: synth.config5(2, seed=3),
+             "hubs": lambda: batch_of_sizes([150, 90, 210], seed=7, hubs=True),
+             "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109),
+             "config3": lambda: synth.config3(192, seed=4)}
+
+
+@pytest.mark.parametrize("case", list(_FAMILIES))
+@pytest.mark.parametrize("layer", [0, 1])
+def test_gat_layer_dst_fwd(case, layer):
+    """Option dst_fwd = 1 (aggregation forward by destination wave, every atom; csrc/gat_agg.hip
+    gat_agg_fwd_dst_kernel) with, for the flatten layer, the one-pass source-atom backward
+    (flat_src = 2, gat_flat_bwd_src1_kernel): forward and every gradient against float64 on each
+    graph family (hubs of in-degree past 64: the softmax's multi-chunk path)."""
+    sb = _FAMILIES[case]()
+    with option("dst_fwd", 1), option("flat_src", 2 if layer == 0 else 0):
+        _layer_case(layer, sb, seed=8 + layer)
+
+
+def _agg_outputs(sb, H, F, mode, seed=0):
+    """One aggregation forward + backward through the C ABI on seeded projection rows:
+    (out, attn, gY[:, :C + 2H])."""
+    from mvml_gat._lib import call, lib, ptr, stream_ptr
+    L = lib()
+    g = sb.to_graph().to(DEV)
+    N, E = g.num_nodes(), g.num_edges()
+    gen = torch.Generator(device=DEV).manual_seed(seed)
+    C = L.mvml_gat_proj_cols(H, F, int(mode == 1))
+    ldy = (C + 63) // 64 * 64
+    Y = torch.randn((N, ldy), device=DEV, generator=gen) * 0.3
+    elr = torch.randn((N, 2 * H), device=DEV, generator=gen)
+    bias = torch.randn(H * F, device=DEV, generator=gen) * 0.1
+    oc = F if mode == 1 else H * F
+    out = torch.empty((N, oc), device=DEV)
+    attn = torch.empty((E, H), device=DEV)
+    st = stream_ptr()
+    orow = torch.zeros(N, dtype=torch.int32, device=DEV)
+    omx = torch.zeros(1, dtype=torch.int32, device=DEV)
+    call("mvml_gat_agg_fwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr), ptr(g.in_src),
+         ptr(Y), ldy, H, F, ptr(elr), ptr(bias), 0.2, mode, ptr(out), ptr(attn), ptr(omx), ptr(orow), st)
+    g_out = torch.randn((N, oc), device=DEV, generator=gen)
+    ldg = (C + 2 * H + 63) // 64 * 64
+    gY = torch.zeros((N, ldg), device=DEV)
+    wsz = L.mvml_gat_agg_bwd_workspace_size(E, H)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+    gmx = torch.zeros(1, dtype=torch.int32, device=DEV)
+    grow = torch.zeros(N, dtype=torch.int32, device=DEV)
+    call("mvml_gat_agg_bwd", N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr), ptr(g.in_src),
+         ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), ptr(Y), ldy, ptr(elr), ptr(attn), ptr(out),
+         ptr(g_out), H, F, 0.2, mode, ptr(gY), ldg, ptr(gmx), ptr(grow), ptr(ws), wsz, st)
+    torch.cuda.synchronize()
+    return out, attn, gY[:, :C + 2 * H], omx, orow, gmx, grow
+
+
+@pytest.mark.parametrize("case", ["config2", "config3"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_dst_fwd_bitwise_molecule_windows(case, mode):
+    """Without hubs, the destination-wave forward sums every row in edge order from 0 exactly as
+    the molecule-window / gather kernels do, with the same softmax arithmetic: out, attn and the
+    output maxima are BITWISE equal."""
+    sb = _FAMILIES[case]()
+    F = 192 if mode == 0 else 384
+    with option("dst_fwd", 0):
+        a = _agg_outputs(sb, 4, F, mode)
+    with option("dst_fwd", 1):
+        b = _agg_outputs(sb, 4, F, mode)
+    for i in (0, 1, 3, 4):
+        assert torch.equal(a[i], b[i]), (i, (a[i].double() - b[i].double()).abs().max().item())
+
+
+@pytest.mark.parametrize("case", ["config5", "table_overflow", "config3"])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_flat_src_one_pass_bitwise(case, mode):
+    """flat_src = 2 (g_rst of each gathered row formed in registers) against flat_src = 1 (g_rst
+    rows written as gY's dR block first, then gathered): the same arithmetic in the same order,
+    so gY, max |gY| and the per-row maxima are BITWISE equal."""
+    sb = _FAMILIES[case]()
+    with option("flat_src", 1):
+        a = _agg_outputs(sb, 4, 192, mode)
+    with option("flat_src", 2):
+        b = _agg_outputs(sb, 4, 192, mode)
+    for i in (2, 5, 6):
+        assert torch.equal(a[i], b[i]), (i, (a[i].double() - b[i].double()).abs().max().item())
+
+
+@pytest.mark.parametrize("flat_src", [0, 1, 2])
 @pytest.mark.parametrize("case", ["config2", "config5"])
 def test_gat_bwd_gy_row_maxima_flat(case, flat_src):
     """Per-row max |gY| of the flatten layer's backward, both paths (see the layer-1 test)."""
