@@ -24,8 +24,9 @@ constexpr int kScanItems = 4;
 constexpr int kScanTile = kScanThreads * kScanItems;  // 1024 items per block
 constexpr int kCsrThreads = 256;
 constexpr int kLdsNodes = 4096;
-constexpr int kWaveMolAtoms = 256;   // build_csr_wave_kernel: one wave per molecule up to these
-constexpr int kWaveMolEdges = 1024;  // ... sizes (LDS: 6 KB per wave, 4 waves per workgroup)
+constexpr int kWaveMolAtoms = 128;   // build_csr_wave_kernel: one wave per molecule up to these
+constexpr int kWaveMolEdges = 512;   // ... sizes (LDS: 3 KB per wave, 4 waves per workgroup: 8
+                                     // workgroups per CU; 6 KB slices held occupancy to 6)
 constexpr int kBigMolAtoms = 1024;   // build_csr_bigwave_kernel: one wave per molecule up to
 constexpr int kBigMolEdges = 4096;   // ... these sizes (LDS: 24 KB per one-wave workgroup)
 
@@ -57,64 +58,71 @@ __device__ T block_exclusive_scan(T v, T* lds_waves /*[kWaves]*/, T* total) {
   return res;
 }
 
-__global__ void scan_tile_sums(const int64_t* __restrict__ in, int64_t n, int64_t* __restrict__ sums) {
+// Both offset scans (atoms, edges) in one set of launches: grid y / block index picks the array.
+struct Scan2 {
+  const int64_t* in[2];
+  int64_t* out[2];
+  int64_t* tmp[2];
+};
+__global__ void scan2_tile_sums(Scan2 a, int64_t n) {
+  const int y = blockIdx.y;
   __shared__ int64_t w[kScanThreads / 64 + 1];
-  int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
   int64_t s = 0;
 #pragma unroll
   for (int i = 0; i < kScanItems; ++i)
-    if (base + i < n) s += in[base + i];
+    if (base + i < n) s += a.in[y][base + i];
   int64_t tot;
   block_exclusive_scan<int64_t>(s, w, &tot);
-  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+  if (threadIdx.x == 0) a.tmp[y][blockIdx.x] = tot;
 }
-
-// Single workgroup: exclusive scan of the tile sums in place.
-__global__ void scan_sums_single(int64_t* __restrict__ sums, int64_t nt) {
+__global__ void scan2_sums_single(Scan2 a, int64_t nt) {
+  int64_t* sums = a.tmp[blockIdx.x];
   __shared__ int64_t w[kScanThreads / 64 + 1];
   int64_t carry = 0;
   for (int64_t b = 0; b < nt; b += kScanThreads) {
-    int64_t i = b + threadIdx.x;
-    int64_t v = i < nt ? sums[i] : 0;
+    const int64_t i = b + threadIdx.x;
+    const int64_t v = i < nt ? sums[i] : 0;
     int64_t tot;
-    int64_t ex = block_exclusive_scan<int64_t>(v, w, &tot);
+    const int64_t ex = block_exclusive_scan<int64_t>(v, w, &tot);
     if (i < nt) sums[i] = ex + carry;
     carry += tot;
   }
 }
-
-__global__ void scan_tile_apply(const int64_t* __restrict__ in, int64_t n,
-                                const int64_t* __restrict__ sums, int64_t* __restrict__ out) {
+__global__ void scan2_tile_apply(Scan2 a, int64_t n) {
+  const int y = blockIdx.y;
   __shared__ int64_t w[kScanThreads / 64 + 1];
-  int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
   int64_t v[kScanItems];
   int64_t s = 0;
 #pragma unroll
   for (int i = 0; i < kScanItems; ++i) {
-    v[i] = (base + i < n) ? in[base + i] : 0;
+    v[i] = (base + i < n) ? a.in[y][base + i] : 0;
     s += v[i];
   }
   int64_t tot;
-  int64_t ex = block_exclusive_scan<int64_t>(s, w, &tot) + sums[blockIdx.x];
+  int64_t ex = block_exclusive_scan<int64_t>(s, w, &tot) + a.tmp[y][blockIdx.x];
 #pragma unroll
   for (int i = 0; i < kScanItems; ++i) {
-    if (base + i < n) out[base + i] = ex;
+    if (base + i < n) a.out[y][base + i] = ex;
     ex += v[i];
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == blockDim.x - 1) out[n] = sums[blockIdx.x] + tot;
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == blockDim.x - 1) a.out[y][n] = a.tmp[y][blockIdx.x] + tot;
 }
 
-int exclusive_scan_i64(const int64_t* in, int64_t n, int64_t* out, int64_t* tmp, hipStream_t st) {
+int exclusive_scan2_i64(const Scan2& a, int64_t n, hipStream_t st) {
   if (n == 0) {
-    (void)hipMemsetAsync(out, 0, sizeof(int64_t), st);
-    return check_launch("scan(empty)");
+    (void)hipMemsetAsync(a.out[0], 0, sizeof(int64_t), st);
+    (void)hipMemsetAsync(a.out[1], 0, sizeof(int64_t), st);
+    return check_launch("scan2(empty)");
   }
-  int64_t nt = ceil_div(n, kScanTile);
-  scan_tile_sums<<<(unsigned)nt, kScanThreads, 0, st>>>(in, n, tmp);
-  scan_sums_single<<<1, kScanThreads, 0, st>>>(tmp, nt);
-  scan_tile_apply<<<(unsigned)nt, kScanThreads, 0, st>>>(in, n, tmp, out);
-  return check_launch("exclusive_scan_i64");
+  const int64_t nt = ceil_div(n, kScanTile);
+  scan2_tile_sums<<<dim3((unsigned)nt, 2), kScanThreads, 0, st>>>(a, n);
+  scan2_sums_single<<<2, kScanThreads, 0, st>>>(a, nt);
+  scan2_tile_apply<<<dim3((unsigned)nt, 2), kScanThreads, 0, st>>>(a, n);
+  return check_launch("exclusive_scan2_i64");
 }
+
 
 // Stable placement of one graph's edges into the CSR keyed by `key_local` (dst for the
 // in-CSR, src for the out-CSR).  cursor[] holds each row's next free local slot.
@@ -188,7 +196,7 @@ __device__ void rows_from_counts(int* cnt, int n, int64_t noff, int64_t eoff,
 // steps, no loop over lanes), its slot the row's cursor plus that rank, and the cursors then
 // advance by LDS adds (order-independent).  No block barriers.  Two sizes:
 //  * build_csr_wave_kernel: four molecules per 256-thread workgroup, <= kWaveMolAtoms atoms and
-//    <= kWaveMolEdges edges (every drug-like molecule); larger ones go to a list;
+//    <= kWaveMolEdges edges (every KEGG-like molecule); larger ones go to a list;
 //  * build_csr_bigwave_kernel: one molecule per 64-thread workgroup, <= kBigMolAtoms atoms and
 //    <= kBigMolEdges edges (config 5's 150-400-atom hub molecules), walking that list; the rest
 //    to a second list for build_csr_kernel (one workgroup per graph, any size).
@@ -234,14 +242,24 @@ __device__ __forceinline__ void wave_place_edges(int ne, int n, int64_t eoff, in
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));  // lanes < this one
   int nbits = 0;
   while ((1 << nbits) < n) ++nbits;  // keys are in [0, n)
-  for (int base = 0; base < ne; base += 64) {
+  // the next chunk's keys are loaded before this chunk is placed (one load latency per chunk
+  // hidden: the big molecules walk ~27 chunks per pass)
+  auto load = [&](int base, int& k, int& v) {
     const int i = base + lane;
-    int k = -1, v = 0;
+    k = -1;
+    v = 0;
     if (i < ne) {
       k = key_local[eoff + i];
       v = val_local[eoff + i];
       if (k < 0 || k >= n || v < 0 || v >= n) k = -1;  // invalid edges are skipped (flagged)
     }
+  };
+  int kn, vn;
+  load(0, kn, vn);
+  for (int base = 0; base < ne; base += 64) {
+    const int i = base + lane;
+    const int k = kn, v = vn;
+    if (base + 64 < ne) load(base + 64, kn, vn);
     // lanes holding this lane's key: intersect, bit by bit, the ballots that agree with it
     uint64_t same = __ballot(k >= 0);
     for (int b = 0; b < nbits; ++b) {
@@ -298,6 +316,7 @@ __device__ __forceinline__ void wave_build_molecule(const CsrArgs& a, int64_t g,
   }
   wave_lds_sync_b();
   int bad = 0;
+#pragma unroll 4
   for (int i = lane; i < ne; i += 64) {
     const int s = a.src_local[eoff + i], d = a.dst_local[eoff + i];
     a.src[eoff + i] = s + (int32_t)noff;
@@ -431,36 +450,36 @@ build_csr_kernel(const int32_t* __restrict__ src_local, const int32_t* __restric
 // Node groups: group g starts at the first atom of the molecule that contains atom
 // g * kNodeGroupAtoms (binary search of node_offsets), so every group is a range of whole
 // molecules (possibly empty when a molecule spans several multiples).  group_start[G] = N.
-__global__ void node_groups_kernel(int64_t B, int64_t N, const int64_t* __restrict__ node_offsets,
-                                   int64_t G, int32_t* __restrict__ group_start) {
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g > G) return;
+__device__ __forceinline__ int32_t group_start_of(int64_t g, int64_t B, int64_t N, int64_t G,
+                                                  const int64_t* __restrict__ node_offsets) {
   const int64_t a = g * kNodeGroupAtoms;
-  if (g == G || a >= N) {
-    group_start[g] = (int32_t)N;
-    return;
-  }
+  if (g >= G || a >= N) return (int32_t)N;
   int64_t lo = 0, hi = B;  // last m with node_offsets[m] <= a
   while (hi - lo > 1) {
     const int64_t mid = (lo + hi) / 2;
     if (node_offsets[mid] <= a) lo = mid; else hi = mid;
   }
-  group_start[g] = (int32_t)node_offsets[lo];
+  return (int32_t)node_offsets[lo];
 }
 
-// Group kinds (one wave per group): bit 0 = the forward LDS kernel takes the group (<=
-// kPlanWinAtoms atoms, <= kPlanEdgeCap in-edges, in-degree <= kPlanDegCap everywhere), bit 1 =
-// the backward LDS kernel does (atom and edge caps only), bit 2 = the group fits the big LDS
-// window (<= kPlanBigAtoms atoms, <= kPlanBigEdgeCap in-edges, any in-degree): groups on a
-// fallback list with bit 2 are taken by the big-window kernels.  Non-empty groups without a bit are
-// appended to that direction's fallback list (order irrelevant: groups are independent).
-__global__ void node_group_kind_kernel(int64_t G, const int32_t* __restrict__ rowptr,
+// Group starts and kinds, one wave per group (lanes 0 and 1 find the group's two boundaries).
+// Kind bits: bit 0 = the forward LDS kernel takes the group (<= kPlanWinAtoms atoms, <=
+// kPlanEdgeCap in-edges, in-degree <= kPlanDegCap everywhere), bit 1 = the backward LDS kernel
+// does (atom and edge caps only), bit 2 = the group fits the big LDS window (<= kPlanBigAtoms
+// atoms, <= kPlanBigEdgeCap in-edges, any in-degree): groups on a fallback list with bit 2 are
+// taken by the big-window kernels.  Non-empty groups without a bit are appended to that
+// direction's fallback list.
+__global__ void node_group_kind_kernel(int64_t B, int64_t N, const int64_t* __restrict__ node_offsets,
+                                       int64_t G, const int32_t* __restrict__ rowptr,
                                        int32_t* __restrict__ plan) {
   const int64_t g = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   const int lane = threadIdx.x & 63;
   if (g >= G) return;
   int32_t* kind = plan + G + 1;
-  const int a0 = plan[g], a1 = plan[g + 1];
+  const int32_t bound = lane < 2 ? group_start_of(g + lane, B, N, G, node_offsets) : 0;
+  const int a0 = __shfl(bound, 0, 64), a1 = __shfl(bound, 1, 64);
+  if (lane == 0) plan[g] = a0;
+  if (lane == 1 && g == G - 1) plan[G] = (int32_t)N;
   int dmax = 0;
   for (int v = a0 + lane; v < a1; v += 64) dmax = max(dmax, rowptr[v + 1] - rowptr[v]);
 #pragma unroll
@@ -530,7 +549,7 @@ using namespace mvml;
 extern "C" size_t mvml_build_csr_workspace_size(int64_t num_graphs, int64_t num_nodes,
                                                 int64_t num_edges) {
   size_t nt = (size_t)ceil_div(num_graphs > 0 ? num_graphs : 1, kScanTile);
-  return carve_size(nt * sizeof(int64_t)) + carve_size((size_t)num_edges * sizeof(int32_t)) +
+  return 2 * carve_size(nt * sizeof(int64_t)) + carve_size((size_t)num_edges * sizeof(int32_t)) +
          carve_size((size_t)2 * num_nodes * sizeof(int)) +
          2 * carve_size((size_t)(num_graphs > 0 ? num_graphs : 1) * sizeof(int32_t)) +
          carve_size(2 * sizeof(int)) + 256;
@@ -557,6 +576,7 @@ extern "C" int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local
   hipStream_t st = as_stream(stream);
   Carver cv(workspace, workspace_bytes);
   int64_t* tmp = cv.take<int64_t>((size_t)ceil_div(num_graphs > 0 ? num_graphs : 1, kScanTile));
+  int64_t* tmp2 = cv.take<int64_t>((size_t)ceil_div(num_graphs > 0 ? num_graphs : 1, kScanTile));
   int32_t* inslot = cv.take<int32_t>((size_t)num_edges);
   int* big = cv.take<int>((size_t)2 * num_nodes);
   int32_t* list1 = cv.take<int32_t>((size_t)(num_graphs > 0 ? num_graphs : 1));
@@ -564,9 +584,8 @@ extern "C" int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local
   int* counts = cv.take<int>(2);
   (void)hipMemsetAsync(status_flags, 0, 2 * sizeof(int32_t), st);
   (void)hipMemsetAsync(counts, 0, 2 * sizeof(int), st);
-  int rc = exclusive_scan_i64(batch_num_nodes, num_graphs, node_offsets, tmp, st);
-  if (rc) return rc;
-  rc = exclusive_scan_i64(batch_num_edges, num_graphs, edge_offsets, tmp, st);
+  const Scan2 sc{{batch_num_nodes, batch_num_edges}, {node_offsets, edge_offsets}, {tmp, tmp2}};
+  int rc = exclusive_scan2_i64(sc, num_graphs, st);
   if (rc) return rc;
   if (num_nodes == 0) {
     (void)hipMemsetAsync(in_rowptr, 0, sizeof(int32_t), st);
@@ -613,12 +632,9 @@ extern "C" int mvml_build_node_groups(int64_t num_graphs, int64_t num_nodes,
   MVML_REQUIRE(num_graphs > 0 && node_offsets && in_rowptr && plan, "build_node_groups: null input");
   hipStream_t st = as_stream(stream);
   // fallback counts and lists: node_group_lists_kernel
-  node_groups_kernel<<<(unsigned)ceil_div(G + 1, 256), 256, 0, st>>>(num_graphs, num_nodes,
-                                                                    node_offsets, G, plan);
-  int rc = check_launch("node_groups_kernel");
-  if (rc) return rc;
-  node_group_kind_kernel<<<(unsigned)ceil_div(G, 4), 256, 0, st>>>(G, in_rowptr, plan);
-  rc = check_launch("node_group_kind_kernel");
+  node_group_kind_kernel<<<(unsigned)ceil_div(G, 4), 256, 0, st>>>(num_graphs, num_nodes, node_offsets, G,
+                                                                  in_rowptr, plan);
+  int rc = check_launch("node_group_kind_kernel");
   if (rc) return rc;
   node_group_lists_kernel<<<1, 1024, 0, st>>>(G, plan);
   return check_launch("node_group_lists_kernel");

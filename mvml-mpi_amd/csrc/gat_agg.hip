@@ -61,8 +61,10 @@ __device__ __forceinline__ float4 fma4(float a, float4 z, float4 c) {
 __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
+// explicit roundings: with the device default -ffp-contract=fast the compiler would pick the
+// contraction per call site, so kernels that promise the same dots bitwise could differ
 __device__ __forceinline__ float dot4(float4 a, float4 b) {
-  return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+  return __fmaf_rn(a.w, b.w, __fmaf_rn(a.z, b.z, __fmaf_rn(a.y, b.y, __fmul_rn(a.x, b.x))));
 }
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
@@ -1078,8 +1080,6 @@ gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
   if (out_amax) block_amax_commit<256>(omx, out_amax);
 }
 
-// The edge softmax alone, one thread per (destination, head) (softmax_pair: bitwise the fused
-// kernels' attn), for gat_agg_fwd_dst_kernel<..., SM = false>.
 // *out = max(*out, max_i rows[i]) (bits of non-negative floats): the operand max of a product
 // from the per-row maxima its producer already wrote, instead of one atomicMax per 4-atom block
 // of a wave-per-atom kernel (a single word takes ~90 atomics per us: 440 k of them were most of
@@ -1098,6 +1098,52 @@ inline int launch_rows_amax(int64_t n, const uint32_t* rows, uint32_t* out, hipS
   return check_launch("rows_amax_kernel");
 }
 
+// H = 4: one thread per destination with the four heads as one float4 (el / er rows are 16 B),
+// softmax_pair's per-head arithmetic and edge order, so attn is bitwise the same; the first DC
+// logits stay in registers, later ones are recomputed (L2-resident el rows).
+__global__ void __launch_bounds__(256)
+gat_softmax_dst4_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
+                        const float* __restrict__ elr, float slope, float* __restrict__ attn) {
+  const int64_t v = xcd_block(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
+  if (v >= N) return;
+  const float4 er = ld4(elr + v * 8 + 4);
+  const int eb = rowptr[v], ee = rowptr[v + 1];
+  auto logit = [&](int e) {
+    const float4 el = ld4(elr + (int64_t)in_src[e] * 8);
+    return make_float4(leaky(el.x + er.x, slope), leaky(el.y + er.y, slope), leaky(el.z + er.z, slope),
+                       leaky(el.w + er.w, slope));
+  };
+  constexpr int DC = 6;
+  float4 sc[DC];
+  float4 m = f4(-INFINITY), sum = f4(0.f);
+#pragma unroll
+  for (int t = 0; t < DC; ++t) {
+    sc[t] = (eb + t < ee) ? logit(eb + t) : f4(-INFINITY);
+    m = make_float4(fmaxf(m.x, sc[t].x), fmaxf(m.y, sc[t].y), fmaxf(m.z, sc[t].z), fmaxf(m.w, sc[t].w));
+  }
+  for (int e = eb + DC; e < ee; ++e) {
+    const float4 c = logit(e);
+    m = make_float4(fmaxf(m.x, c.x), fmaxf(m.y, c.y), fmaxf(m.z, c.z), fmaxf(m.w, c.w));
+  }
+  auto ex = [&](float4 c) {
+    return make_float4(expf(c.x - m.x), expf(c.y - m.y), expf(c.z - m.z), expf(c.w - m.w));
+  };
+#pragma unroll
+  for (int t = 0; t < DC; ++t)
+    if (eb + t < ee) sum = add4(sum, ex(sc[t]));
+  for (int e = eb + DC; e < ee; ++e) sum = add4(sum, ex(logit(e)));
+  auto store = [&](int e, float4 c) {
+    const float4 p = ex(c);
+    st4(attn + (int64_t)e * 4, make_float4(p.x / sum.x, p.y / sum.y, p.z / sum.z, p.w / sum.w));
+  };
+#pragma unroll
+  for (int t = 0; t < DC; ++t)
+    if (eb + t < ee) store(eb + t, sc[t]);
+  for (int e = eb + DC; e < ee; ++e) store(e, logit(e));
+}
+
+// The edge softmax alone, one thread per (destination, head) (softmax_pair: bitwise the fused
+// kernels' attn), for gat_agg_fwd_dst_kernel<..., SM = false>.
 template <int H>
 __global__ void __launch_bounds__(256)
 gat_softmax_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
@@ -2131,7 +2177,7 @@ gat_flat_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
 // w's other in-neighbours' waves at about the same time, so from the XCD's L2 — and forms g_rst[w]
 // in registers with the same arithmetic, then dZ[u] += a_e g_rst[w] (out-CSR order) and
 // g_a[e] = <Z[u], g_rst[w]> per head.  Bitwise the two-pass path's gY and g_a.
-template <int H, int NJ, int MODE>
+template <int H, int NJ, int MODE, int U = 2>
 __global__ void __launch_bounds__(256)
 gat_flat_bwd_src1_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
                          const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
@@ -2186,32 +2232,28 @@ gat_flat_bwd_src1_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
 #pragma unroll
         for (int h = 0; h < H; ++h) a_l[h] = attn[(int64_t)s_l * H + h];
       }
-      for (int j = 0; j < cnt; j += 2) {  // two out-neighbours' rows in flight
-        const int j1 = min(j + 1, cnt - 1);
-        const bool two = j + 1 < cnt;  // (uniform)
-        const int64_t w0 = rl(w_l, j), w1 = rl(w_l, j1);
-        float4 g0[NJ], g1[NJ];
+      for (int j = 0; j < cnt; j += U) {  // U out-neighbours' rows in flight
+        float4 g[U][NJ];
 #pragma unroll
-        for (int c = 0; c < NJ; ++c) {
-          g0[c] = okc[c] ? grst(w0, c) : f4(0.f);
-          g1[c] = okc[c] ? grst(w1, c) : f4(0.f);
+        for (int t = 0; t < U; ++t) {
+          const int64_t wt = rl(w_l, min(j + t, cnt - 1));  // past the chunk: a duplicate row, unused
+#pragma unroll
+          for (int c = 0; c < NJ; ++c) g[t][c] = okc[c] ? grst(wt, c) : f4(0.f);
         }
-        float a0[H], a1[H], p0[H], p1[H];
 #pragma unroll
-        for (int h = 0; h < H; ++h) { a0[h] = rl(a_l[h], j); a1[h] = rl(a_l[h], j1); p0[h] = 0.f; p1[h] = 0.f; }
+        for (int t = 0; t < U; ++t) {
+          if (j + t >= cnt) break;  // (uniform)
+          float a[H], pd[H];
 #pragma unroll
-        for (int c = 0; c < NJ; ++c)
-          if (okc[c]) {
-            dz[c] = fma4(pick<H>(a0, hc[c]), g0[c], dz[c]);
-            if (two) dz[c] = fma4(pick<H>(a1, hc[c]), g1[c], dz[c]);
-            add_at<H>(p0, hc[c], dot4(z[c], g0[c]));
-            add_at<H>(p1, hc[c], dot4(z[c], g1[c]));
-          }
-        HeadReduce<H>::template all<false>(p0, lane);
-        store_heads<H>(ga + (int64_t)rl(s_l, j) * H, p0, lane);
-        if (two) {
-          HeadReduce<H>::template all<false>(p1, lane);
-          store_heads<H>(ga + (int64_t)rl(s_l, j1) * H, p1, lane);
+          for (int h = 0; h < H; ++h) { a[h] = rl(a_l[h], j + t); pd[h] = 0.f; }
+#pragma unroll
+          for (int c = 0; c < NJ; ++c)
+            if (okc[c]) {
+              dz[c] = fma4(pick<H>(a, hc[c]), g[t][c], dz[c]);
+              add_at<H>(pd, hc[c], dot4(z[c], g[t][c]));
+            }
+          HeadReduce<H>::template all<false>(pd, lane);
+          store_heads<H>(ga + (int64_t)rl(s_l, j + t) * H, pd, lane);
         }
       }
     }
@@ -2238,13 +2280,20 @@ int launch_flat_src1(int64_t N, const int32_t* rp, const int32_t* src, const int
   const int nj = (int)ceil_div(HF / 4, 64);
   const unsigned b4 = (unsigned)ceil_div(N, 4), b256 = (unsigned)ceil_div(N, 256);
   uint32_t* const blk_amax = gy_rows ? nullptr : gy_amax;  // (see launch_mean_src)
+  const bool u1 = option(MVML_OPT_DST_UNR) != 2;  // one out-neighbour row per trip (2: two)
 #define MVML_FLAT_SRC1(NJ)                                                                                   \
   do {                                                                                                       \
-    if (mode == 0)                                                                                           \
-      gat_flat_bwd_src1_kernel<H, NJ, 0><<<b4, 256, 0, st>>>( \
+    if (mode == 0 && u1)                                                                                     \
+      gat_flat_bwd_src1_kernel<H, NJ, 0, 1><<<b4, 256, 0, st>>>(                                              \
+          N, orp, odst, oslot, Y, ldy, attn, out, g_out, F, gpre, gY, ldgy, blk_amax, gy_rows);               \
+    else if (mode == 0)                                                                                      \
+      gat_flat_bwd_src1_kernel<H, NJ, 0><<<b4, 256, 0, st>>>(                                                 \
+          N, orp, odst, oslot, Y, ldy, attn, out, g_out, F, gpre, gY, ldgy, blk_amax, gy_rows);               \
+    else if (u1)                                                                                             \
+      gat_flat_bwd_src1_kernel<H, NJ, 2, 1><<<b4, 256, 0, st>>>(                                              \
           N, orp, odst, oslot, Y, ldy, attn, out, g_out, F, gpre, gY, ldgy, blk_amax, gy_rows);               \
     else                                                                                                     \
-      gat_flat_bwd_src1_kernel<H, NJ, 2><<<b4, 256, 0, st>>>( \
+      gat_flat_bwd_src1_kernel<H, NJ, 2><<<b4, 256, 0, st>>>(                                                 \
           N, orp, odst, oslot, Y, ldy, attn, out, g_out, F, gpre, gY, ldgy, blk_amax, gy_rows);               \
   } while (0)
   switch (nj) {
@@ -2349,7 +2398,11 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
     const bool sm = option(MVML_OPT_DST_FWD) == 1;  // 2: the softmax as its own launch first
     // with per-row maxima requested, max |out| comes from them afterwards (no per-block atomics)
     uint32_t* const blk_amax = out_rows ? nullptr : out_amax;
-    if (!sm) {
+    if (!sm && H == 4) {
+      gat_softmax_dst4_kernel<<<(unsigned)ceil_div(N, 256), 256, 0, st>>>(N, rp, src, elr, slope, attn);
+      int rc = check_launch("gat_softmax_dst4_kernel");
+      if (rc) return rc;
+    } else if (!sm) {
       gat_softmax_dst_kernel<H><<<(unsigned)ceil_div(N * H, 256), 256, 0, st>>>(N, rp, src, elr, slope, attn);
       int rc = check_launch("gat_softmax_dst_kernel");
       if (rc) return rc;
@@ -2371,9 +2424,9 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
       const int nj = (int)ceil_div(F / 4, H >= 2 ? 32 : 64);
       if (nj == 1) MVML_DST_FWD(1, 1, 4);
       else if (nj == 2) MVML_DST_FWD(1, 2, 2);
-      else if (nj == 3 && H == 4 && unr == 1) MVML_DST_FWD(1, 3, 1);
+      else if (nj == 3 && H == 4 && unr == 2) MVML_DST_FWD(1, 3, 2);
       else if (nj == 3 && H == 4 && unr == 3) MVML_DST_FWD(1, 3, 3);
-      else if (nj == 3) MVML_DST_FWD(1, 3, 2);
+      else if (nj == 3) MVML_DST_FWD(1, 3, 1);  // one row in flight: fewest registers, most waves
       else if (nj <= 4) MVML_DST_FWD(1, 4, 2);
       else { set_error("gat_agg_fwd: dst path needs F <= %d in mean mode", H >= 2 ? 512 : 1024); return MVML_ERR_INVALID; }
     } else {
@@ -2381,9 +2434,9 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
 #define MVML_DST_FWD_F(NJ, U) do { if (mode == 0) MVML_DST_FWD(0, NJ, U); else MVML_DST_FWD(2, NJ, U); } while (0)
       if (nj == 1) MVML_DST_FWD_F(1, 4);
       else if (nj == 2) MVML_DST_FWD_F(2, 4);
-      else if (nj == 3 && H == 4 && unr == 1) MVML_DST_FWD_F(3, 1);
+      else if (nj == 3 && H == 4 && unr == 2) MVML_DST_FWD_F(3, 2);
       else if (nj == 3 && H == 4 && unr == 4) MVML_DST_FWD_F(3, 4);
-      else if (nj == 3) MVML_DST_FWD_F(3, 2);  // fewer rows in flight, more waves: faster
+      else if (nj == 3) MVML_DST_FWD_F(3, 1);  // fewer rows in flight, more waves: faster
       else if (nj == 4) MVML_DST_FWD_F(4, 2);
       else MVML_DST_FWD_F(8, 2);
 #undef MVML_DST_FWD_F

@@ -250,15 +250,18 @@ REASSOC_X = os.environ.get("MVML_GAT_REASSOC", "0") == "1"
 # Kernel paths picked per call from the batch's molecule sizes (host counts, no device work):
 # "large" batches have half their atoms or more in molecules past the LDS molecule window
 # (FLAT_SRC_MIN_ATOMS, gat_agg.hip kWinL) — BASELINE config 5.
-#  * Aggregation forward by destination wave (option dst_fwd = 2: the edge softmax as its own
-#    launch, then one wave per atom gathers whole projection rows from L2; csrc/gat_agg.hip
-#    gat_agg_fwd_dst_kernel): flatten layers always, the head-mean layer on large batches
-#    (MVML_DST_FWD_POLICY = auto | all | off).
+#  * Aggregation forward by destination wave (one wave per atom gathers whole projection rows
+#    from L2; csrc/gat_agg.hip gat_agg_fwd_dst_kernel), every layer (MVML_DST_FWD_POLICY = all |
+#    auto: the head-mean layer on large batches only | off): on small-molecule batches with the
+#    edge softmax as its own launch first (dst_fwd = 2: 2.9 / 3.4 ms against the molecule
+#    window's 3.5 / 3.7 at config 3), on large ones inside the wave (dst_fwd = 1: 4.5 / 6.2 ms
+#    against 5.0 / 6.4 split, config 5) — MVML_DST_FWD_KIND forces one.
 #  * Flatten layers' aggregation backward by source atom in one pass (option flat_src = 2,
 #    gat_flat_bwd_src1_kernel) on large batches (MVML_FLAT_SRC_AUTO = 0 turns it off).
 FLAT_SRC_AUTO = os.environ.get("MVML_FLAT_SRC_AUTO", "1") == "1"
 FLAT_SRC_MIN_ATOMS = 128  # the LDS molecule window (gat_agg.hip kWinL)
-DST_FWD_POLICY = os.environ.get("MVML_DST_FWD_POLICY", "auto")
+DST_FWD_POLICY = os.environ.get("MVML_DST_FWD_POLICY", "all")
+DST_FWD_KIND = int(os.environ.get("MVML_DST_FWD_KIND", "0"))  # 0: by batch (see above)
 #  * The ELU link (EluLink, below): the second layer's data-gradient GEMM applies ELU' in its
 #    epilogue, so the first layer's backward gathers g_rst rows only (no `out` rows) — on large
 #    batches, where that backward gathers rows per out-edge (flat_src); on small ones the
@@ -274,7 +277,9 @@ def _large_batch(g):
 def _fwd_path(g, mode):
     """Context manager selecting the aggregation forward kernel path for this call."""
     dst = DST_FWD_POLICY == "all" or (DST_FWD_POLICY == "auto" and (mode != MODE_MEAN or _large_batch(g)))
-    return _lib.option("dst_fwd", 2) if dst else contextlib.nullcontext()
+    if not dst:
+        return contextlib.nullcontext()
+    return _lib.option("dst_fwd", DST_FWD_KIND or (1 if _large_batch(g) else 2))
 
 
 

@@ -48,6 +48,18 @@ class GATConv(nn.Module):
         self.proj_dtype = None
         self.reset_parameters()
 
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        """Accept both DGL GATConv parameter layouts.  dgl 0.9.1 (README.md pins) keeps an
+        explicit ``bias`` and a bias-free ``res_fc``; later DGL releases fold the bias into the
+        residual Linear (``res_fc.bias``, no ``bias``) when ``res_fc`` projects.  The arithmetic
+        is the same (res_fc(x) + b), so the folded form loads into ``bias`` here."""
+        rb, b = prefix + "res_fc.bias", prefix + "bias"
+        if rb in state_dict and b not in state_dict:
+            state_dict[b] = state_dict.pop(rb)
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                      unexpected_keys, error_msgs)
+
     def reset_parameters(self):
         gain = nn.init.calculate_gain("relu")
         nn.init.xavier_normal_(self.fc.weight, gain=gain)

@@ -138,6 +138,33 @@ def test_state_dict_layout_matches_reference():
                         "conv.gnn_layers.0.gat_conv.res_fc.weight"]
 
 
+@pytest.mark.parametrize("which", ["gnn", "mvp"])
+def test_state_dict_accepts_folded_residual_bias(which):
+    """both DGL GATConv layouts load with strict=True — the explicit
+    ``gat_conv.bias`` (dgl 0.9.1, what state_dict() writes) and the later releases' bias folded
+    into the projecting residual (``gat_conv.res_fc.bias``, no ``bias``); the arithmetic is the
+    same, so the folded tensor becomes ``bias``."""
+    from mvml_gat.mvp import MVP
+    torch.manual_seed(0)
+    make = (lambda: mvml_gat.GNNModule(74, [192, 384], 0.5, 6, 3)) if which == "gnn" else \
+        (lambda: MVP(11, 74, [192, 384], 6, 3, 128, 384, 2, 512, 12, 0.5))
+    src, dst = make(), make()
+    for p in src.parameters():
+        p.data.uniform_(-1, 1)
+    sd = src.state_dict()
+    folded = {}
+    for k, v in sd.items():
+        if k.endswith("gat_conv.bias"):
+            folded[k[:-len("bias")] + "res_fc.bias"] = v.clone()
+        else:
+            folded[k] = v.clone()
+    assert not any(k.endswith("gat_conv.bias") for k in folded)
+    dst.load_state_dict(folded, strict=True)
+    for (k, a), (k2, b) in zip(src.state_dict().items(), dst.state_dict().items()):
+        assert k == k2 and torch.equal(a, b), k
+    dst.load_state_dict(sd, strict=True)  # and the explicit layout still loads
+
+
 # ------------------------------------------------------------------ fusion head / node groups
 def test_fusion_state_dict_matches_reference_layout():
     """MVFusion carries MVP's fusion parameters under MVP's names and shapes (model.py:23-45)."""

@@ -124,7 +124,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mols", type=int, default=65536)
     ap.add_argument("--config", default="3")
-    ap.add_argument("--layers", default="01", help="which layers: 0 = L1 flatten+ELU, 1 = L2 mean")
+    ap.add_argument("--layers", default="01", help="which layers: 0 = L1 flatten+ELU, 1 = L2 mean, "
+                    "2 = L1 flatten without ELU (the ELU-link backward)")
     ap.add_argument("--no-bwd", action="store_true")
     ap.add_argument("--no-fwd", action="store_true", help="time only the backward (forward runs once)")
     ap.add_argument("--ab", default="", help="option sets to compare on one box, e.g. "
@@ -137,7 +138,9 @@ def main():
     L = _lib.lib()
     st = _lib.stream_ptr()
     print(f"config{a.config}: {a.mols} molecules, N={N}, E={E}")
-    layers = ((4, 192, 0, "L1 flatten+ELU"), (4, 384, 1, "L2 mean"))
+    # "2": layer 1 as the GNN runs it on large batches with the ELU link (mode 2: the next
+    # layer's GEMM applied ELU', so the backward reads no `out`)
+    layers = ((4, 192, 0, "L1 flatten+ELU"), (4, 384, 1, "L2 mean"), (4, 192, 2, "L1 flatten (link)"))
     if "x" in a.layers:
         bench_x(a, g, N, E, st)
     for (H, F, mode, name) in [layers[int(i)] for i in a.layers if i != "x"]:

@@ -22,12 +22,12 @@ case "$step" in
   prof)    # rocprofv3 kernel stats of a command: tools/gpu_r5.sh prof <tag> <python args...>
     tag=$1; shift
     export TMPDIR=/tmp
-    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run -- python3 "$@" \
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python3 "$@" \
       > gpurun_out/prof_$tag.log 2>&1; rc=$?; tail -3 gpurun_out/prof_$tag.log; exit $rc ;;
   pmc)     # one PMC pass: tools/gpu_r5.sh pmc <tag> "<counters>" <python args...>
     tag=$1; ctr=$2; shift 2
     export TMPDIR=/tmp
-    timeout -s KILL 120 rocprofv3 --pmc $ctr -d gpurun_out/pmc_$tag -o run -- python3 "$@" \
+    timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc_$tag -o run -- python3 "$@" \
       > gpurun_out/pmc_$tag.log 2>&1; rc=$?; tail -3 gpurun_out/pmc_$tag.log; exit $rc ;;
   *) echo "unknown step $step"; exit 2 ;;
 esac
