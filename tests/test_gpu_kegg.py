@@ -81,3 +81,48 @@ def test_kegg_config1_labels_identical():
           f"test metrics (acc, prec, rec, f1) {np.mean(res_d, 0)}")
     assert worst < TOL
     assert np.array_equal(np.mean(res_d, 0), np.mean(res_r, 0))
+
+
+def test_kegg_config1_whole_mvp_real_fingerprints():
+    """The whole MVP model in eval mode (model.py:13-75) on the 420 test-split molecules with the
+    three real view inputs: SMILES tokens (utils.py:55-96 restated), graphs (featurize) and the
+    2,513-value fingerprints of dataset.py:37-45 (mvml_gat.fingerprints; RDKit agreement
+    unpinned): logits within 1e-5 of the float64 oracle and predicted labels identical."""
+    from mvml_gat.featurize import MolDataSet, collate
+    from mvml_gat.fingerprints import FP_SIZE, fingerprints
+    from mvml_gat.mvp import MVP
+    from mvml_gat.smiles import collate_smiles, tokens_struct
+    from oracle.fusion_ref import MVPRef
+    from oracle.graph_ref import batch_ref
+
+    ds = MolDataSet(os.path.join(HERE, "golden", "kegg_test_split.csv"))
+    fps = torch.as_tensor(fingerprints(ds.smiles))
+    assert fps.shape == (len(ds), FP_SIZE) and fps[:, :167].sum() > 0 and fps[:, 1489:].sum() > 0
+    torch.manual_seed(0)
+    mod = MVP(11, 74, [192, 384], 6, 3, 128, 384, 2, 512, 12, 0.5)
+    randomize_(mod.gnn, 0)
+    ref = MVPRef().double().eval()
+    ref.load_state_dict({k: v.double() for k, v in mod.state_dict().items()})
+    mod = mod.to(DEV).eval()
+    tok = tokens_struct()
+    worst = 0.0
+    with torch.no_grad():
+        for s in range(0, len(ds), 64):
+            idx = list(range(s, min(s + 64, len(ds))))
+            samples = [ds[i] for i in idx]
+            bg, y = collate(samples)
+            sm = collate_smiles([ds.smiles[i] for i in idx], tok)
+            g = bg.to(DEV)
+            zd = mod({"smiles": sm["smiles"].to(DEV), "seq_len": sm["seq_len"]}, g, g.ndata["h"].to(DEV),
+                     fps[idx].to(DEV)).double().cpu()
+            gr = [m for m, _ in samples]
+            gd = batch_ref(np.array([m.num_nodes() for m in gr]), np.concatenate([m.src for m in gr]),
+                           np.concatenate([m.dst for m in gr]), np.array([m.num_edges() for m in gr]))
+            x = torch.cat([m.ndata["h"] for m in gr]).double()
+            zr = ref(sm, gd, x, fps[idx].double())
+            worst = max(worst, rel_err(zd, zr))
+            pd_, _ = _metrics(y.numpy(), zd.numpy())
+            pr_, _ = _metrics(y.numpy(), zr.numpy())
+            assert np.array_equal(pd_, pr_), f"labels differ in batch {s // 64}"
+    print(f"config1 whole MVP: logits rel_err {worst:.2e}")
+    assert worst < TOL

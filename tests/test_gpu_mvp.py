@@ -2,8 +2,9 @@
 (main.py:24-36): RNNModule + GNNModule + FPNModule (fp_2_dim = 512, config.py:16) + fusion head
 + BCEWithLogits + Adam (lr 1e-3, wd 1e-4, main.py:88) — against the composed float64 oracle
 (oracle/fusion_ref.py MVPRef) on one 64-molecule KEGG batch (the first test-split batch,
-data_index.txt order, featurised by mvml_gat.featurize; fingerprints are seeded 0/1 bits since
-RDKit is absent here).
+data_index.txt order, featurised by mvml_gat.featurize; fingerprints from
+mvml_gat.fingerprints, the restated MACCS / ErG / PubChem / Morgan of dataset.py:37-45 —
+RDKit agreement unpinned, tests/test_fingerprints.py).
 
 Bars: logits / loss within 1e-5 of float64; every parameter gradient within 1e-5 or 4x the
 fp32 oracle's own error where conditioning makes fp32 lose that much (see
@@ -39,7 +40,8 @@ def _kegg_batch(n=64, seed=0):
                    np.concatenate([m.dst for m in gr]), np.array([m.num_edges() for m in gr]))
     x = torch.cat([m.ndata["h"] for m in gr]).double()
     smiles = collate_smiles(ds.smiles[:n], tokens_struct())
-    fp = (torch.rand(n, 2513, generator=torch.Generator().manual_seed(seed)) < 0.1).double()
+    from mvml_gat.fingerprints import fingerprints
+    fp = torch.as_tensor(fingerprints(ds.smiles[:n])).double()  # dataset.py:37-45 (restated)
     return bg, gd, x, smiles, fp, y.double()
 
 
