@@ -21,12 +21,15 @@ of RDKit's sanitisation that the 74 atom features depend on:
 Host-side data preparation (the reference runs it per item on the CPU as well); everything it
 produces is plain integer/float arrays that ``batching.bigraph_from_bonds`` turns into a graph.
 
-Differences from the reference that are known and deliberate:
-* atoms keep SMILES parse order; dgllife renumbers them by RDKit's canonical ranking
-  (``canonical_atom_order=True``).  The view is permutation-invariant per molecule (GAT is
-  equivariant, Set2Set / GraphNorm invariant — KAT 4 in tests/test_oracle_kat.py), so this only
-  changes floating-point summation order;
-* agreement with RDKit itself is **unpinned** (RDKit cannot be run here); the restatement is
+* canonical atom order (dgllife's ``canonical_atom_order=True``): RDKit's canonical ranking
+  restated (``canonical_ranks``) and applied as dgllife applies it.
+
+Known differences from the reference:
+* agreement with RDKit itself is **unpinned** (including the canonical ranks: tie-breaking
+  details of RDKit's implementation cannot be checked; the view is permutation-invariant per
+  molecule — GAT equivariant, Set2Set / GraphNorm invariant, KAT 4 in tests/test_oracle_kat.py —
+  so a different canonical order only changes floating-point summation order);
+* the rest of the agreement with RDKit is **unpinned** (RDKit cannot be run here); the restatement is
   pinned by hand-derived known answers in tests/test_featurize.py.
 """
 import numpy as np
@@ -682,14 +685,63 @@ def atom_features(m):
     return f
 
 
-def smiles_to_bigraph(smiles, add_self_loop=True):
+def canonical_ranks(m):
+    """Chem.CanonicalRankAtoms (RDKit's canonicalisation, Schneider, Sayle & Landrum, J. Chem. Inf.
+    Model. 2015, restated; parity with RDKit unpinned): atoms are partitioned by the base
+    invariants RDKit compares first (degree, atomic number, isotope, total H, formal charge);
+    partitions are refined by each atom's sorted (neighbour rank, bond order) list until stable;
+    a partition still tied after refinement (symmetry) is split by giving its lowest-index atom
+    the lower rank, then refinement resumes.  Returns rank[old atom] in 0 .. n-1."""
+    n = m.num_atoms
+    if n == 0:
+        return []
+    code = {1: 1, 2: 2, 3: 3, AROM: 12}
+
+    def dense(keys):
+        order = sorted(range(n), key=lambda i: (keys[i], i))
+        rk, r = [0] * n, 0
+        for t, i in enumerate(order):
+            if t and keys[i] != keys[order[t - 1]]:
+                r = t
+            rk[i] = r
+        return rk
+
+    ranks = dense([(m.degree(i), m.z(i), 0, m.total_h(i), m.charge[i]) for i in range(n)])
+    while True:
+        while True:  # refine by neighbourhoods
+            keys = [(ranks[i], tuple(sorted((ranks[j], code[m.bonds[k][2]]) for (j, k) in m.nbrs(i))))
+                    for i in range(n)]
+            new = dense(keys)
+            if len(set(new)) == len(set(ranks)):
+                ranks = new
+                break
+            ranks = new
+        if len(set(ranks)) == n:
+            return ranks
+        # break the first tie: the lowest-index atom of the lowest tied rank goes first
+        tied = min(r for r in set(ranks) if ranks.count(r) > 1)
+        first = min(i for i in range(n) if ranks[i] == tied)
+        ranks = dense([(ranks[i], 0 if i == first else 1) for i in range(n)])
+
+
+def smiles_to_bigraph(smiles, add_self_loop=True, canonical_atom_order=True):
     """mol_to_bigraph(Chem.MolFromSmiles(s), add_self_loop=True,
     node_featurizer=CanonicalAtomFeaturizer('h')) (dataset.py:33-35): a MolGraph whose edges
-    are (u_i->v_i),(v_i->u_i) per bond in bond order, then self-loops; ndata['h'] f32[n,74]."""
+    are (u_i->v_i),(v_i->u_i) per bond in bond order, then self-loops; ndata['h'] f32[n,74].
+    canonical_atom_order (dgllife's default, True): the atoms renumbered as dgllife does,
+    ``RenumberAtoms(mol, CanonicalRankAtoms(mol))`` — new atom k is old atom rank[k] — with the
+    bonds in their original order and orientation (RDKit RenumberAtoms)."""
     from .batching import bigraph_from_bonds
     m = mol_from_smiles(smiles)
+    feats = atom_features(m)
     bonds = np.array([(a, b) for (a, b, _) in m.bonds], dtype=np.int32).reshape(-1, 2)
-    return bigraph_from_bonds(m.num_atoms, bonds, atom_features(m), add_self_loop=add_self_loop)
+    if canonical_atom_order and m.num_atoms:
+        new_order = np.asarray(canonical_ranks(m), dtype=np.int64)  # new atom k <- old new_order[k]
+        inv = np.empty_like(new_order)
+        inv[new_order] = np.arange(len(new_order))
+        feats = feats[new_order]
+        bonds = inv[bonds].astype(np.int32).reshape(-1, 2)
+    return bigraph_from_bonds(m.num_atoms, bonds, feats, add_self_loop=add_self_loop)
 
 
 class MolDataSet:

@@ -79,7 +79,7 @@ def test_aromaticity(smi, n_arom):
 
 def test_feature_layout_and_bigraph():
     """74-d layout of CanonicalAtomFeaturizer and mol_to_bigraph edge order (a1)."""
-    g = fz.smiles_to_bigraph("CC(=O)[O-]")
+    g = fz.smiles_to_bigraph("CC(=O)[O-]", canonical_atom_order=False)
     f = g.ndata["h"].numpy()
     assert f.shape == (4, fz.FEAT_SIZE)
     assert f[0, 0] == 1 and f[2, 2] == 1                  # C, O one-hot
@@ -117,3 +117,50 @@ def test_kegg_test_split_fixture():
         nb = (g.num_edges() - g.num_nodes()) // 2
         assert np.all(src[0:2 * nb:2] == dst[1:2 * nb:2])  # rev(e) = e ^ 1
     assert 10_000 < n_atoms < 14_000                      # ~11.7k atoms
+
+
+def test_canonical_ranks_ethanol_and_dgllife_renumbering():
+    """CCO: base invariants (degree, Z, isotope, total H, charge) already separate the atoms —
+    C0 (1, 6, 0, 3, 0) < O2 (1, 8, 0, 1, 0) < C1 (2, 6, 0, 2, 0) — so the ranks are [0, 2, 1].
+    dgllife passes the rank list to RenumberAtoms as newOrder (mol_to_graph,
+    canonical_atom_order=True): new atom k is old atom rank[k], bonds keep order and
+    orientation: bond (0, 1) -> (0, 2), bond (1, 2) -> (2, 1)."""
+    m = fz.mol_from_smiles("CCO")
+    assert fz.canonical_ranks(m) == [0, 2, 1]
+    g = fz.smiles_to_bigraph("CCO", add_self_loop=False)
+    src, dst = g.edges()
+    assert list(src) == [0, 2, 2, 1] and list(dst) == [2, 0, 1, 2]
+    f = g.ndata["h"].numpy()
+    assert f[0, 0] == 1 and f[1, 2] == 1 and f[2, 0] == 1           # C, O, C
+    assert f[0, 69 + 3] == 1 and f[2, 69 + 2] == 1                 # CH3 first, CH2 last
+
+
+@pytest.mark.parametrize("a,b", [
+    ("OCC(N)C", "CC(N)CO"),
+    ("CC(=O)Oc1ccccc1C(=O)O", "OC(=O)c1ccccc1OC(C)=O"),          # aspirin, two writings
+])
+def test_canonical_ranks_are_writing_independent(a, b):
+    """The ranks themselves are canonical: an atom's rank does not depend on how the SMILES was
+    written (matched through each writing's rank-sorted feature rows and neighbour ranks)."""
+    def signature(smi):
+        m = fz.mol_from_smiles(smi)
+        r = fz.canonical_ranks(m)
+        f = fz.atom_features(m)
+        by_rank = sorted(range(m.num_atoms), key=lambda i: r[i])
+        return [(tuple(f[i]), tuple(sorted(r[j] for (j, _) in m.nbrs(i)))) for i in by_rank]
+    assert signature(a) == signature(b)
+
+
+@pytest.mark.parametrize("smi", ["c1ccccc1", "C1CCCCC1", "CC(C)(C)C", "OC(=O)CC(O)(CC(=O)O)C(=O)O"])
+def test_canonical_ranks_symmetric(smi):
+    """Symmetric molecules: ties broken to a permutation of 0..n-1; the ranked graph is the
+    molecule (same degree sequence, bigraph invariants kept)."""
+    m = fz.mol_from_smiles(smi)
+    r = fz.canonical_ranks(m)
+    assert sorted(r) == list(range(m.num_atoms))
+    g = fz.smiles_to_bigraph(smi)
+    src, dst = g.edges()
+    nb = (g.num_edges() - g.num_nodes()) // 2
+    assert np.all(src[0:2 * nb:2] == dst[1:2 * nb:2])
+    deg = np.bincount(dst[:2 * nb], minlength=g.num_nodes())
+    assert sorted(deg.tolist()) == sorted(m.degree(i) for i in range(m.num_atoms))
