@@ -2496,6 +2496,217 @@ int colsum_splits(int64_t M, int64_t N) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 4096));
 }
 
+// ---- small-K split-fp16 product: the layer-1 projection as the memory kernel it is ---------
+// C[M][N] = A[M][K] B[N][K]^T for K <= 80 (the atom features: K = 76 against the 1544 rows of
+// layer 1's Wcat) writes N / K ~ 20 output bytes per input byte: HBM-bound on the C stores, and
+// the 256x256 tile (five 16-deep stages, then an LDS epilogue that cannot overlap the next
+// tile's loads) reached 0.34 of HBM on it.  Here a WAVE owns 64 output columns: it loads the
+// split-fp16 planes of its 64 B rows into registers ONCE (B's il4 image, or fp32 split in place
+// -- bitwise the same planes), then walks chunk_blocks blocks of 16 A rows: A's fragments come
+// straight from global memory (the next block's in flight behind the current block's MFMAs),
+// are split with the row's own scale (split2h, as the tiles do) and multiplied as C^T = B A^T
+// on v_mfma_f32_16x16x32_f16 (the K tail on 16x16x16) — transposed so that each lane's four
+// accumulators are FOUR CONSECUTIVE COLUMNS OF ONE ROW: the C tile leaves as float4 stores
+// straight from the accumulators (16 rows x 64 B per instruction), no LDS, no barrier.  The
+// three products per k-step keep the tiles' order (l_b h_a, h_b l_a, h_b h_a); the scales are
+// undone as there (B's, then the row's).  Waves are numbered XCD-major (xcd_block), slab
+// fastest: the ~25 waves sharing a block of A rows run together on one XCD and read the rows
+// from its L2.  Same values as the tiles to fp32-GEMM accuracy (the MFMA shape changes the
+// summation order, so not bitwise).
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSkMaxK = 80;
+
+template <int KS16, bool IL4, bool NT>
+__global__ void __launch_bounds__(256)
+gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int64_t lda,
+                   const float* __restrict__ B, int64_t ldb, const uint32_t* __restrict__ a_rows,
+                   const uint32_t* __restrict__ amax_b, const float* __restrict__ bias, int act,
+                   float* __restrict__ C, int64_t ldc, int n_slabs, int chunk_blocks) {
+  constexpr int N32 = KS16 / 2, T16 = KS16 % 2, NW = N32 > 0 ? N32 : 1;
+  const int lane = threadIdx.x & 63, li = lane & 15, lq = lane >> 4;
+  const int64_t w = xcd_block(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int slab = (int)(w % n_slabs);
+  const int64_t nrb = (M + 15) >> 4;
+  const int64_t rb0 = (w / n_slabs) * chunk_blocks;
+  if (rb0 >= nrb) return;
+  const int64_t rb1 = min(nrb, rb0 + (int64_t)chunk_blocks);
+  const int kb = amax_shift(*amax_b);
+  const float s_b = pow2f(kb), u_b = pow2f(-kb);
+  // this lane's B rows (output columns c0 + 16 g + li) for the MFMA's A side: k = 32 s + 8 lq
+  // + 0..7 (x32 steps), 32 N32 + 4 lq + 0..3 (x16 tail); k >= K reads as zero
+  f16x8 bh[4][NW], bl[4][NW];
+  f16x4 th[4], tl[4];
+  auto piece = [&](const float* row, int k, uint2& h, uint2& l) {  // B[row][k .. k + 3] as planes
+    const float4 v = *reinterpret_cast<const float4*>(row + min(k, K - 4));
+    if constexpr (IL4) {
+      h = make_uint2(__float_as_uint(v.x), __float_as_uint(v.y));
+      l = make_uint2(__float_as_uint(v.z), __float_as_uint(v.w));
+    } else {
+      split2h(v, s_b, h, l);
+    }
+    if (k >= K) h = l = make_uint2(0u, 0u);
+  };
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int64_t col = (int64_t)slab * 64 + 16 * g + li;
+    const float* row = B + min(col, N - 1) * ldb;
+#pragma unroll
+    for (int s = 0; s < N32; ++s) {
+      uint2 h0, l0, h1, l1;
+      piece(row, 32 * s + 8 * lq, h0, l0);
+      piece(row, 32 * s + 8 * lq + 4, h1, l1);
+      const u32x4 hv = {h0.x, h0.y, h1.x, h1.y}, lv = {l0.x, l0.y, l1.x, l1.y};
+      bh[g][s] = __builtin_bit_cast(f16x8, hv);
+      bl[g][s] = __builtin_bit_cast(f16x8, lv);
+    }
+    if constexpr (T16) {
+      uint2 h, l;
+      piece(row, 32 * N32 + 4 * lq, h, l);
+      th[g] = __builtin_bit_cast(f16x4, h);
+      tl[g] = __builtin_bit_cast(f16x4, l);
+    }
+  }
+  float bv[4][4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t col = (int64_t)slab * 64 + 16 * g + 4 * lq + u;
+      bv[g][u] = (bias && col < N) ? bias[col] : 0.f;
+    }
+  // A fragments of one 16-row block: row 16 rb + li, k as B's; KS16 float4 per lane
+  auto load_a = [&](int64_t rb, float4 (&x)[KS16], uint32_t& rbits) {
+    const int64_t r = min(rb * 16 + li, M - 1);
+    const float* p = A + r * lda;
+#pragma unroll
+    for (int s = 0; s < N32; ++s) {
+      x[2 * s] = *reinterpret_cast<const float4*>(p + min(32 * s + 8 * lq, K - 4));
+      x[2 * s + 1] = *reinterpret_cast<const float4*>(p + min(32 * s + 8 * lq + 4, K - 4));
+    }
+    if constexpr (T16) x[KS16 - 1] = *reinterpret_cast<const float4*>(p + min(32 * N32 + 4 * lq, K - 4));
+    rbits = a_rows[r];
+  };
+  float4 xn[KS16];
+  uint32_t rn;
+  load_a(rb0, xn, rn);
+  for (int64_t rb = rb0; rb < rb1; ++rb) {
+    float4 x[KS16];
+#pragma unroll
+    for (int i = 0; i < KS16; ++i) x[i] = xn[i];
+    const int ka = amax_shift(rn);
+    if (rb + 1 < rb1) load_a(rb + 1, xn, rn);
+    const float s_a = pow2f(ka);
+    f16x8 ah[NW], al[NW];
+    f16x4 ath, atl;
+#pragma unroll
+    for (int s = 0; s < N32; ++s) {
+      uint2 h0, l0, h1, l1;
+      split2h(x[2 * s], s_a, h0, l0);
+      split2h(x[2 * s + 1], s_a, h1, l1);
+      if (32 * s + 8 * lq >= K) h0 = l0 = make_uint2(0u, 0u);
+      if (32 * s + 8 * lq + 4 >= K) h1 = l1 = make_uint2(0u, 0u);
+      const u32x4 hv = {h0.x, h0.y, h1.x, h1.y}, lv = {l0.x, l0.y, l1.x, l1.y};
+      ah[s] = __builtin_bit_cast(f16x8, hv);
+      al[s] = __builtin_bit_cast(f16x8, lv);
+    }
+    if constexpr (T16) {
+      uint2 h, l;
+      split2h(x[KS16 - 1], s_a, h, l);
+      if (32 * N32 + 4 * lq >= K) h = l = make_uint2(0u, 0u);
+      ath = __builtin_bit_cast(f16x4, h);
+      atl = __builtin_bit_cast(f16x4, l);
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < N32; ++s) {
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[g][s], ah[s], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[g][s], al[s], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[g][s], ah[s], acc[g], 0, 0, 0);
+      }
+      if constexpr (T16) {
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(tl[g], ath, acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[g], atl, acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[g], ath, acc[g], 0, 0, 0);
+      }
+    }
+    const int64_t row = rb * 16 + li;
+    const float u_a = pow2f(-ka);
+    if (row < M) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int64_t col = (int64_t)slab * 64 + 16 * g + 4 * lq;
+        if (col >= N) continue;
+        float4 o;
+        o.x = acc[g][0] * u_b * u_a + bv[g][0];
+        o.y = acc[g][1] * u_b * u_a + bv[g][1];
+        o.z = acc[g][2] * u_b * u_a + bv[g][2];
+        o.w = acc[g][3] * u_b * u_a + bv[g][3];
+        if (act == 1) {
+          o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+        }
+        if constexpr (NT) {
+          const f32x4 ov = {o.x, o.y, o.z, o.w};
+          __builtin_nontemporal_store(ov, reinterpret_cast<f32x4*>(C + row * ldc + col));
+        } else {
+          *reinterpret_cast<float4*>(C + row * ldc + col) = o;
+        }
+      }
+    }
+  }
+}
+
+// Host: the shapes the small-K kernel takes (per-row A scales, K-contiguous B, K <= 80, every
+// row and pointer 16-B aligned, N % 4 == 0, no beta, act 0 / 1).
+bool smallk_fits(int b_kmajor, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                 const float* Bp, int64_t ldb, float beta, int act, const float* C, int64_t ldc) {
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  return option(MVML_OPT_SMALLK) != 0 && !b_kmajor && M > 0 && K >= 4 && K <= kSkMaxK && K % 4 == 0 &&
+         N % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 && al(A) && al(Bp) && al(C) &&
+         beta == 0.f && (act == 0 || act == 1);
+}
+
+int smallk_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
+                  int64_t ldb, bool il4, const uint32_t* a_rows, const uint32_t* amax_b,
+                  const float* bias, int act, float* C, int64_t ldc, hipStream_t st) {
+  const int n_slabs = (int)ceil_div(N, 64);
+  const int64_t nrb = ceil_div(M, 16);
+  // ~32 row blocks (512 rows) per wave: the B slab's one load is 1/30 of what the wave stores;
+  // fewer on small launches so that >= 4096 waves fill the chip
+  const int64_t cb = std::max<int64_t>(1, std::min<int64_t>(32, nrb * n_slabs / 4096));
+  const int64_t waves = ceil_div(nrb, cb) * n_slabs;
+  const int64_t blocks = ceil_div(waves, 4);
+  if (blocks >= (int64_t(1) << 31)) {
+    set_error("gemm small-K: too many blocks");
+    return MVML_ERR_INVALID;
+  }
+  const bool nt = option(MVML_OPT_SMALLK) != 2;
+  const int ks = (int)ceil_div(K, 16);
+#define MVML_SK(KS, IL, NTV)                                                                      \
+  gemm_smallk_kernel<KS, IL, NTV><<<(unsigned)blocks, 256, 0, st>>>(M, N, (int)K, A, lda, B, ldb,  \
+                                                                      a_rows, amax_b, bias, act, C, \
+                                                                      ldc, n_slabs, (int)cb)
+#define MVML_SK_KS(IL, NTV)                 \
+  switch (ks) {                             \
+    case 1: MVML_SK(1, IL, NTV); break;     \
+    case 2: MVML_SK(2, IL, NTV); break;     \
+    case 3: MVML_SK(3, IL, NTV); break;     \
+    case 4: MVML_SK(4, IL, NTV); break;     \
+    default: MVML_SK(5, IL, NTV); break;    \
+  }
+  if (il4) {
+    if (nt) { MVML_SK_KS(true, true) } else { MVML_SK_KS(true, false) }
+  } else {
+    if (nt) { MVML_SK_KS(false, true) } else { MVML_SK_KS(false, false) }
+  }
+#undef MVML_SK_KS
+#undef MVML_SK
+  return check_launch("gemm_smallk_kernel");
+}
+
 }  // namespace
 }  // namespace mvml
 
@@ -2566,6 +2777,13 @@ extern "C" int mvml_gemm_f16x2_rows(int64_t M, int64_t N, int64_t K, const float
   MVML_REQUIRE(amax_a_rows != nullptr && amax_b != nullptr,
                "gemm_f16x2_rows: amax_a_rows / amax_b are required");
   MVML_REQUIRE(!b_il4 || ((uintptr_t)b_il4 % 16) == 0, "gemm_f16x2_rows: b_il4 must be 16-B aligned");
+  MVML_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f16x2_rows: negative shape");
+  if (M == 0 || N == 0) return MVML_OK;
+  // small K (layer 1: the atom features): the wave-per-64-columns memory kernel
+  if (smallk_fits(b_kmajor, M, N, K, A, lda, b_il4 ? b_il4 : B, ldb, beta, act, C, ldc) && ldc >= N &&
+      lda >= K && ldb >= K)
+    return smallk_launch(M, N, K, A, lda, b_il4 ? b_il4 : B, ldb, b_il4 != nullptr, amax_a_rows, amax_b,
+                         bias, act, C, ldc, as_stream(stream));
   AmaxPtrs am;
   am.b = amax_b;
   am.a_rows = amax_a_rows;
