@@ -85,7 +85,7 @@ const char* mvml_version(void);
 #define MVML_OPT_DST_UNR 10     /* MVML_DST_UNR: projection rows in flight per wave of the
                                    destination-wave forward (0 = the default per width; tuning) */
 #define MVML_OPT_SMALLK 11      /* MVML_SMALLK: 1 (default) mvml_gemm_f16x2_rows products with
-                                   K <= 80 (layer 1's projection) on the wave-per-64-columns
+                                   K <= 96 (layer 1's projection) on the wave-per-64-columns
                                    memory kernel (non-temporal stores; 2 = plain stores);
                                    0 = the 256x256 tile */
 int mvml_set_option(int option, int value);

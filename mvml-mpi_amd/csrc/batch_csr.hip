@@ -285,6 +285,50 @@ __device__ __forceinline__ void wave_place_edges(int ne, int n, int64_t eoff, in
   }
 }
 
+// The same placement from registers: the wave kernel's molecules have <= kWaveMolEdges edges,
+// so the lane's <= NCH (src, dst) pairs loaded once for the counts are kept and both passes
+// place them without reloading (two dependent global round trips fewer per molecule).
+template <bool IN, int NCH>
+__device__ __forceinline__ void wave_place_edges_reg(int ne, int n, int64_t eoff, int64_t noff,
+                                                     const int (&sv)[NCH], const int (&dv)[NCH], int* cursor,
+                                                     int* s_inslot, int32_t* __restrict__ out_val,
+                                                     int32_t* __restrict__ out_aux) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int nbits = 0;
+  while ((1 << nbits) < n) ++nbits;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int base = 64 * c;
+    if (base >= ne) break;
+    const int i = base + lane;
+    int k = IN ? dv[c] : sv[c];
+    const int v = IN ? sv[c] : dv[c];
+    if (i >= ne || k < 0 || k >= n || v < 0 || v >= n) k = -1;
+    uint64_t same = __ballot(k >= 0);
+    for (int b = 0; b < nbits; ++b) {
+      const bool bit = ((k >> b) & 1) != 0;
+      const uint64_t on = __ballot(bit);
+      same &= bit ? on : ~on;
+    }
+    const int rank = __popcll(same & below);
+    const int slot = k >= 0 ? cursor[k] + rank : 0;
+    wave_lds_sync_b();
+    if (k >= 0) {
+      atomicAdd(&cursor[k], 1);
+      const int64_t gs = eoff + slot;
+      out_val[gs] = v + (int32_t)noff;
+      if (IN) {
+        out_aux[gs] = (int32_t)(eoff + i);
+        s_inslot[i] = (int32_t)gs;
+      } else {
+        out_aux[gs] = s_inslot[i];
+      }
+    }
+    wave_lds_sync_b();
+  }
+}
+
 struct CsrArgs {
   const int32_t* src_local;
   const int32_t* dst_local;
@@ -304,11 +348,22 @@ struct CsrArgs {
   int32_t* flags;
 };
 
-// the whole CSR build of molecule g by the calling wave (LDS slices cin / cout [n], slot [ne])
-__device__ __forceinline__ void wave_build_molecule(const CsrArgs& a, int64_t g, int n, int ne, int* cin,
-                                                    int* cout, int* slot) {
+// the whole CSR build of molecule g by the calling wave (LDS slices cin / cout [n], slot [ne]);
+// NCH > 0 (ne <= 64 NCH): the edges stay in registers between the count and the two placements
+template <int NCH = 0>
+__device__ __forceinline__ void wave_build_molecule(const CsrArgs& a, int64_t g, int n, int ne, int64_t noff,
+                                                    int64_t eoff, int* cin, int* cout, int* slot) {
   const int lane = threadIdx.x & 63;
-  const int64_t noff = a.node_off[g], eoff = a.edge_off[g];
+  constexpr int NR = NCH > 0 ? NCH : 1;
+  int sv[NR], dv[NR];
+  if constexpr (NCH > 0) {  // issue every edge load first
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int i = 64 * c + lane;
+      sv[c] = i < ne ? a.src_local[eoff + i] : -1;
+      dv[c] = i < ne ? a.dst_local[eoff + i] : -1;
+    }
+  }
   for (int j = lane; j < n; j += 64) {
     cin[j] = 0;
     cout[j] = 0;
@@ -316,17 +371,23 @@ __device__ __forceinline__ void wave_build_molecule(const CsrArgs& a, int64_t g,
   }
   wave_lds_sync_b();
   int bad = 0;
-#pragma unroll 4
-  for (int i = lane; i < ne; i += 64) {
-    const int s = a.src_local[eoff + i], d = a.dst_local[eoff + i];
+  auto count_edge = [&](int i, int s, int d) {
     a.src[eoff + i] = s + (int32_t)noff;
     a.dst[eoff + i] = d + (int32_t)noff;
     if (s < 0 || s >= n || d < 0 || d >= n) {
       ++bad;
-      continue;
+      return;
     }
     atomicAdd(&cin[d], 1);
     atomicAdd(&cout[s], 1);
+  };
+  if constexpr (NCH > 0) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      if (64 * c + lane < ne) count_edge(64 * c + lane, sv[c], dv[c]);
+  } else {
+#pragma unroll 4
+    for (int i = lane; i < ne; i += 64) count_edge(i, a.src_local[eoff + i], a.dst_local[eoff + i]);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o, 64);
@@ -342,8 +403,13 @@ __device__ __forceinline__ void wave_build_molecule(const CsrArgs& a, int64_t g,
     a.out_rowptr[noff + n] = (int32_t)(eoff + ne);
   }
   wave_lds_sync_b();
-  wave_place_edges<true>(ne, n, eoff, noff, a.dst_local, a.src_local, cin, slot, a.in_src, a.in_eid);
-  wave_place_edges<false>(ne, n, eoff, noff, a.src_local, a.dst_local, cout, slot, a.out_dst, a.out_inslot);
+  if constexpr (NCH > 0) {
+    wave_place_edges_reg<true>(ne, n, eoff, noff, sv, dv, cin, slot, a.in_src, a.in_eid);
+    wave_place_edges_reg<false>(ne, n, eoff, noff, sv, dv, cout, slot, a.out_dst, a.out_inslot);
+  } else {
+    wave_place_edges<true>(ne, n, eoff, noff, a.dst_local, a.src_local, cin, slot, a.in_src, a.in_eid);
+    wave_place_edges<false>(ne, n, eoff, noff, a.src_local, a.dst_local, cout, slot, a.out_dst, a.out_inslot);
+  }
 }
 
 __global__ void __launch_bounds__(256)
@@ -354,13 +420,15 @@ build_csr_wave_kernel(CsrArgs a, int64_t B, int32_t* __restrict__ big_list, int*
   const int w = threadIdx.x >> 6;
   const int64_t g = (int64_t)blockIdx.x * 4 + w;
   if (g >= B) return;  // (wave-level only: no block barriers below)
+  // sizes and offsets in one round trip (the offsets are the scan's, already written)
   const int n = (int)a.num_nodes[g];
   const int ne = (int)a.num_edges[g];
+  const int64_t noff = a.node_off[g], eoff = a.edge_off[g];
   if (n > kWaveMolAtoms || ne > kWaveMolEdges) {  // the next size class
     if ((threadIdx.x & 63) == 0) big_list[atomicAdd(big_count, 1)] = (int32_t)g;
     return;
   }
-  wave_build_molecule(a, g, n, ne, s_cin[w], s_cout[w], s_slot[w]);
+  wave_build_molecule<kWaveMolEdges / 64>(a, g, n, ne, noff, eoff, s_cin[w], s_cout[w], s_slot[w]);
 }
 
 // persistent over the first list; one wave per workgroup (24 KB of LDS)
@@ -379,7 +447,7 @@ build_csr_bigwave_kernel(CsrArgs a, const int32_t* __restrict__ list, const int*
       if (threadIdx.x == 0) huge_list[atomicAdd(huge_count, 1)] = (int32_t)g;
       continue;
     }
-    wave_build_molecule(a, g, n, ne, s_cin, s_cout, s_slot);
+    wave_build_molecule(a, g, n, ne, a.node_off[g], a.edge_off[g], s_cin, s_cout, s_slot);
     wave_lds_sync_b();  // this molecule's LDS reads are done before the next one's zeroing
   }
 }
@@ -448,38 +516,34 @@ build_csr_kernel(const int32_t* __restrict__ src_local, const int32_t* __restric
 }
 
 // Node groups: group g starts at the first atom of the molecule that contains atom
-// g * kNodeGroupAtoms (binary search of node_offsets), so every group is a range of whole
-// molecules (possibly empty when a molecule spans several multiples).  group_start[G] = N.
-__device__ __forceinline__ int32_t group_start_of(int64_t g, int64_t B, int64_t N, int64_t G,
-                                                  const int64_t* __restrict__ node_offsets) {
-  const int64_t a = g * kNodeGroupAtoms;
-  if (g >= G || a >= N) return (int32_t)N;
-  int64_t lo = 0, hi = B;  // last m with node_offsets[m] <= a
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) / 2;
-    if (node_offsets[mid] <= a) lo = mid; else hi = mid;
-  }
-  return (int32_t)node_offsets[lo];
+// g * kNodeGroupAtoms, so every group is a range of whole molecules (possibly empty when a
+// molecule spans several multiples).  group_start[G] = N.  One thread per MOLECULE writes the
+// starts of the groups whose first multiple it contains (every multiple of kNodeGroupAtoms
+// below N lies in exactly one molecule, so each start is written once) — no per-group binary
+// search over node_offsets (16 dependent loads per group: ~30 us per 65,536-molecule batch).
+__global__ void node_group_start_kernel(int64_t B, int64_t N, const int64_t* __restrict__ node_offsets,
+                                        int64_t G, int32_t* __restrict__ plan) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m == 0) plan[G] = (int32_t)N;
+  if (m >= B) return;
+  const int64_t a = node_offsets[m], b = m + 1 < B ? node_offsets[m + 1] : N;
+  for (int64_t g = (a + kNodeGroupAtoms - 1) / kNodeGroupAtoms; g * kNodeGroupAtoms < b; ++g)
+    plan[g] = (int32_t)a;
 }
 
-// Group starts and kinds, one wave per group (lanes 0 and 1 find the group's two boundaries).
-// Kind bits: bit 0 = the forward LDS kernel takes the group (<= kPlanWinAtoms atoms, <=
-// kPlanEdgeCap in-edges, in-degree <= kPlanDegCap everywhere), bit 1 = the backward LDS kernel
-// does (atom and edge caps only), bit 2 = the group fits the big LDS window (<= kPlanBigAtoms
-// atoms, <= kPlanBigEdgeCap in-edges, any in-degree): groups on a fallback list with bit 2 are
-// taken by the big-window kernels.  Non-empty groups without a bit are appended to that
-// direction's fallback list.
-__global__ void node_group_kind_kernel(int64_t B, int64_t N, const int64_t* __restrict__ node_offsets,
-                                       int64_t G, const int32_t* __restrict__ rowptr,
+// Group kinds, one wave per group.  Kind bits: bit 0 = the forward LDS kernel takes the group
+// (<= kPlanWinAtoms atoms, <= kPlanEdgeCap in-edges, in-degree <= kPlanDegCap everywhere),
+// bit 1 = the backward LDS kernel does (atom and edge caps only), bit 2 = the group fits the big
+// LDS window (<= kPlanBigAtoms atoms, <= kPlanBigEdgeCap in-edges, any in-degree): groups on a
+// fallback list with bit 2 are taken by the big-window kernels.  Non-empty groups without a bit
+// are appended to that direction's fallback list.
+__global__ void node_group_kind_kernel(int64_t G, const int32_t* __restrict__ rowptr,
                                        int32_t* __restrict__ plan) {
   const int64_t g = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   const int lane = threadIdx.x & 63;
   if (g >= G) return;
   int32_t* kind = plan + G + 1;
-  const int32_t bound = lane < 2 ? group_start_of(g + lane, B, N, G, node_offsets) : 0;
-  const int a0 = __shfl(bound, 0, 64), a1 = __shfl(bound, 1, 64);
-  if (lane == 0) plan[g] = a0;
-  if (lane == 1 && g == G - 1) plan[G] = (int32_t)N;
+  const int a0 = plan[g], a1 = plan[g + 1];
   int dmax = 0;
   for (int v = a0 + lane; v < a1; v += 64) dmax = max(dmax, rowptr[v + 1] - rowptr[v]);
 #pragma unroll
@@ -494,50 +558,67 @@ __global__ void node_group_kind_kernel(int64_t B, int64_t N, const int64_t* __re
   kind[g] = k;
 }
 
-// The fallback lists in group order (one workgroup: a running exclusive scan over chunks of
-// 1024 groups), so the fallback kernels can hand each XCD a contiguous run of molecules.  The
-// flags are 0 / 1, so a wave's prefix is a popcount of its ballot below the lane; the 16 wave
-// totals go through LDS (two barriers per chunk).
+// The fallback lists in group order, one workgroup: thread t owns the contiguous groups
+// [t R, (t + 1) R), R = ceil(G / 1024) — it counts its flags (independent loads, no load
+// latency per 1024-group chunk behind two barriers: ~35 us per batch before), the counts are
+// exclusive-scanned across the workgroup (shuffles within a wave, the 16 wave totals through
+// LDS), and a second pass over the same groups writes the entries in group order.
+__device__ __forceinline__ void group_flags(const int32_t* start, const int32_t* kind, int64_t g, bool& f0,
+                                            bool& f1) {
+  f0 = f1 = false;
+  if (start[g + 1] > start[g]) {
+    const int k = kind[g];
+    f0 = (k & 1) == 0;
+    f1 = (k & 2) == 0;
+  }
+}
 __global__ void __launch_bounds__(1024) node_group_lists_kernel(int64_t G, int32_t* __restrict__ plan) {
   const int32_t* start = plan;
   const int32_t* kind = plan + G + 1;
   int32_t* count = plan + 2 * G + 1;
   __shared__ int s_w[2][16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  int base0 = 0, base1 = 0;  // running list lengths (uniform)
-  for (int64_t c0 = 0; c0 < G; c0 += 1024) {
-    const int64_t g = c0 + tid;
-    bool f0 = false, f1 = false;
-    if (g < G && start[g + 1] > start[g]) {
-      f0 = !(kind[g] & 1);
-      f1 = !(kind[g] & 2);
-    }
-    const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
-    if (lane == 0) {
-      s_w[0][w] = __popcll(b0);
-      s_w[1][w] = __popcll(b1);
-    }
-    __syncthreads();
-    int o0 = base0 + __popcll(b0 & below), o1 = base1 + __popcll(b1 & below);
-    int t0 = 0, t1 = 0;
+  const int64_t R = (G + 1023) / 1024, g0 = min(G, tid * R), g1 = min(G, g0 + R);
+  int c0 = 0, c1 = 0;
+  for (int64_t g = g0; g < g1; ++g) {
+    bool f0, f1;
+    group_flags(start, kind, g, f0, f1);
+    c0 += f0;
+    c1 += f1;
+  }
+  int i0 = c0, i1 = c1;  // inclusive wave scans
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int a0 = s_w[0][k], a1 = s_w[1][k];
-      o0 += k < w ? a0 : 0;
-      o1 += k < w ? a1 : 0;
-      t0 += a0;
-      t1 += a1;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u0 = __shfl_up(i0, o, 64), u1 = __shfl_up(i1, o, 64);
+    if (lane >= o) {
+      i0 += u0;
+      i1 += u1;
     }
-    if (f0) plan[2 * G + 3 + o0] = (int32_t)g;
-    if (f1) plan[3 * G + 3 + o1] = (int32_t)g;
-    base0 += t0;
-    base1 += t1;
-    __syncthreads();  // s_w is reused by the next chunk
+  }
+  if (lane == 63) {
+    s_w[0][w] = i0;
+    s_w[1][w] = i1;
+  }
+  __syncthreads();
+  int o0 = i0 - c0, o1 = i1 - c1, t0 = 0, t1 = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    o0 += k < w ? s_w[0][k] : 0;
+    o1 += k < w ? s_w[1][k] : 0;
+    t0 += s_w[0][k];
+    t1 += s_w[1][k];
+  }
+  if (c0 | c1) {
+    for (int64_t g = g0; g < g1; ++g) {
+      bool f0, f1;
+      group_flags(start, kind, g, f0, f1);
+      if (f0) plan[2 * G + 3 + o0++] = (int32_t)g;
+      if (f1) plan[3 * G + 3 + o1++] = (int32_t)g;
+    }
   }
   if (tid == 0) {
-    count[0] = base0;
-    count[1] = base1;
+    count[0] = t0;
+    count[1] = t1;
   }
 }
 
@@ -631,10 +712,13 @@ extern "C" int mvml_build_node_groups(int64_t num_graphs, int64_t num_nodes,
   if (G == 0) return MVML_OK;
   MVML_REQUIRE(num_graphs > 0 && node_offsets && in_rowptr && plan, "build_node_groups: null input");
   hipStream_t st = as_stream(stream);
+  node_group_start_kernel<<<(unsigned)ceil_div(num_graphs, 256), 256, 0, st>>>(num_graphs, num_nodes,
+                                                                              node_offsets, G, plan);
+  int rc = check_launch("node_group_start_kernel");
+  if (rc) return rc;
   // fallback counts and lists: node_group_lists_kernel
-  node_group_kind_kernel<<<(unsigned)ceil_div(G, 4), 256, 0, st>>>(num_graphs, num_nodes, node_offsets, G,
-                                                                  in_rowptr, plan);
-  int rc = check_launch("node_group_kind_kernel");
+  node_group_kind_kernel<<<(unsigned)ceil_div(G, 4), 256, 0, st>>>(G, in_rowptr, plan);
+  rc = check_launch("node_group_kind_kernel");
   if (rc) return rc;
   node_group_lists_kernel<<<1, 1024, 0, st>>>(G, plan);
   return check_launch("node_group_lists_kernel");

@@ -2497,7 +2497,7 @@ int colsum_splits(int64_t M, int64_t N) {
 }
 
 // ---- small-K split-fp16 product: the layer-1 projection as the memory kernel it is ---------
-// C[M][N] = A[M][K] B[N][K]^T for K <= 80 (the atom features: K = 76 against the 1544 rows of
+// C[M][N] = A[M][K] B[N][K]^T for K <= 96 (the atom features: K = 76 against the 1544 rows of
 // layer 1's Wcat) writes N / K ~ 20 output bytes per input byte: HBM-bound on the C stores, and
 // the 256x256 tile (five 16-deep stages, then an LDS epilogue that cannot overlap the next
 // tile's loads) reached 0.34 of HBM on it.  Here a WAVE owns 64 output columns: it loads the
@@ -2505,9 +2505,10 @@ int colsum_splits(int64_t M, int64_t N) {
 // -- bitwise the same planes), then walks chunk_blocks blocks of 16 A rows: A's fragments come
 // straight from global memory (the next block's in flight behind the current block's MFMAs),
 // are split with the row's own scale (split2h, as the tiles do) and multiplied as C^T = B A^T
-// on v_mfma_f32_16x16x32_f16 (the K tail on 16x16x16) — transposed so that each lane's four
-// accumulators are FOUR CONSECUTIVE COLUMNS OF ONE ROW: the C tile leaves as float4 stores
-// straight from the accumulators (16 rows x 64 B per instruction), no LDS, no barrier.  The
+// on v_mfma_f32_16x16x32_f16 (K <= 16: 16x16x16) — transposed so that each lane's four
+// accumulators are FOUR CONSECUTIVE COLUMNS OF ONE ROW; a wave-private LDS slice turns the
+// 16 x 64 block into 4-row x 256-B float4 stores (measured: float4 stores straight from the
+// accumulators, 16 rows x 64 B per instruction, ran at the tile's 2.7 TB/s), no block barrier.  The
 // three products per k-step keep the tiles' order (l_b h_a, h_b l_a, h_b h_a); the scales are
 // undone as there (B's, then the row's).  Waves are numbered XCD-major (xcd_block), slab
 // fastest: the ~25 waves sharing a block of A rows run together on one XCD and read the rows
@@ -2515,15 +2516,21 @@ int colsum_splits(int64_t M, int64_t N) {
 // summation order, so not bitwise).
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kSkMaxK = 80;
+constexpr int kSkMaxK = 96;
+constexpr int kSkPitch = 68;  // floats per row of a wave's 16 x 64 LDS staging slice (+4: rows 4 banks apart)
 
+// KS16: 1 = one 16-deep step on 16x16x16 (K <= 16); else ceil(K / 32) steps of 16x16x32, the
+// last zero-padded past K.  (A 16x16x16 tail behind 16x16x32 steps on the same accumulators
+// came out wrong in the first two of each lane's four results at K = 76 / 80 — a missing
+// MFMA-to-MFMA wait between the two pass counts — so the kernel never mixes the two shapes.)
 template <int KS16, bool IL4, bool NT>
 __global__ void __launch_bounds__(256)
 gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int64_t lda,
                    const float* __restrict__ B, int64_t ldb, const uint32_t* __restrict__ a_rows,
                    const uint32_t* __restrict__ amax_b, const float* __restrict__ bias, int act,
                    float* __restrict__ C, int64_t ldc, int n_slabs, int chunk_blocks) {
-  constexpr int N32 = KS16 / 2, T16 = KS16 % 2, NW = N32 > 0 ? N32 : 1;
+  constexpr int N32 = KS16 == 1 ? 0 : (KS16 + 1) / 2, T16 = KS16 == 1 ? 1 : 0, NW = N32 > 0 ? N32 : 1;
+  constexpr int NX = 2 * N32 + T16;  // A float4 per lane and row block
   const int lane = threadIdx.x & 63, li = lane & 15, lq = lane >> 4;
   const int64_t w = xcd_block(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int slab = (int)(w % n_slabs);
@@ -2576,7 +2583,7 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
       bv[g][u] = (bias && col < N) ? bias[col] : 0.f;
     }
   // A fragments of one 16-row block: row 16 rb + li, k as B's; KS16 float4 per lane
-  auto load_a = [&](int64_t rb, float4 (&x)[KS16], uint32_t& rbits) {
+  auto load_a = [&](int64_t rb, float4 (&x)[NX], uint32_t& rbits) {
     const int64_t r = min(rb * 16 + li, M - 1);
     const float* p = A + r * lda;
 #pragma unroll
@@ -2584,16 +2591,18 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
       x[2 * s] = *reinterpret_cast<const float4*>(p + min(32 * s + 8 * lq, K - 4));
       x[2 * s + 1] = *reinterpret_cast<const float4*>(p + min(32 * s + 8 * lq + 4, K - 4));
     }
-    if constexpr (T16) x[KS16 - 1] = *reinterpret_cast<const float4*>(p + min(32 * N32 + 4 * lq, K - 4));
+    if constexpr (T16) x[NX - 1] = *reinterpret_cast<const float4*>(p + min(32 * N32 + 4 * lq, K - 4));
     rbits = a_rows[r];
   };
-  float4 xn[KS16];
+  __shared__ __attribute__((aligned(16))) float s_c[4][16 * kSkPitch];
+  float* wl = s_c[threadIdx.x >> 6];
+  float4 xn[NX];
   uint32_t rn;
   load_a(rb0, xn, rn);
   for (int64_t rb = rb0; rb < rb1; ++rb) {
-    float4 x[KS16];
+    float4 x[NX];
 #pragma unroll
-    for (int i = 0; i < KS16; ++i) x[i] = xn[i];
+    for (int i = 0; i < NX; ++i) x[i] = xn[i];
     const int ka = amax_shift(rn);
     if (rb + 1 < rb1) load_a(rb + 1, xn, rn);
     const float s_a = pow2f(ka);
@@ -2612,7 +2621,7 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
     }
     if constexpr (T16) {
       uint2 h, l;
-      split2h(x[KS16 - 1], s_a, h, l);
+      split2h(x[NX - 1], s_a, h, l);
       if (32 * N32 + 4 * lq >= K) h = l = make_uint2(0u, 0u);
       ath = __builtin_bit_cast(f16x4, h);
       atl = __builtin_bit_cast(f16x4, l);
@@ -2633,21 +2642,29 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[g], ath, acc[g], 0, 0, 0);
       }
     }
-    const int64_t row = rb * 16 + li;
+    // the 16 x 64 block leaves through the wave's LDS slice: each lane's 4 x float4 (row li,
+    // columns 16 g + 4 lq) in, then 4 rows x 256 contiguous bytes per store instruction out
+    // (straight from the accumulators a store instruction would write 16 rows x 64 B)
     const float u_a = pow2f(-ka);
-    if (row < M) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int64_t col = (int64_t)slab * 64 + 16 * g + 4 * lq;
-        if (col >= N) continue;
-        float4 o;
-        o.x = acc[g][0] * u_b * u_a + bv[g][0];
-        o.y = acc[g][1] * u_b * u_a + bv[g][1];
-        o.z = acc[g][2] * u_b * u_a + bv[g][2];
-        o.w = acc[g][3] * u_b * u_a + bv[g][3];
-        if (act == 1) {
-          o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
-        }
+    for (int g = 0; g < 4; ++g) {
+      float4 o;
+      o.x = acc[g][0] * u_b * u_a + bv[g][0];
+      o.y = acc[g][1] * u_b * u_a + bv[g][1];
+      o.z = acc[g][2] * u_b * u_a + bv[g][2];
+      o.w = acc[g][3] * u_b * u_a + bv[g][3];
+      if (act == 1) {
+        o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+      }
+      *reinterpret_cast<float4*>(wl + li * kSkPitch + 16 * g + 4 * lq) = o;
+    }
+    wave_sync_lds();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int rr = 4 * t + (lane >> 4), c4 = 4 * (lane & 15);
+      const float4 o = *reinterpret_cast<const float4*>(wl + rr * kSkPitch + c4);
+      const int64_t row = rb * 16 + rr, col = (int64_t)slab * 64 + c4;
+      if (row < M && col < N) {
         if constexpr (NT) {
           const f32x4 ov = {o.x, o.y, o.z, o.w};
           __builtin_nontemporal_store(ov, reinterpret_cast<f32x4*>(C + row * ldc + col));
@@ -2656,10 +2673,11 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
         }
       }
     }
+    wave_sync_lds();  // the reads are done before the next block's writes
   }
 }
 
-// Host: the shapes the small-K kernel takes (per-row A scales, K-contiguous B, K <= 80, every
+// Host: the shapes the small-K kernel takes (per-row A scales, K-contiguous B, K <= 96, every
 // row and pointer 16-B aligned, N % 4 == 0, no beta, act 0 / 1).
 bool smallk_fits(int b_kmajor, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                  const float* Bp, int64_t ldb, float beta, int act, const float* C, int64_t ldc) {
@@ -2684,7 +2702,7 @@ int smallk_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, 
     return MVML_ERR_INVALID;
   }
   const bool nt = option(MVML_OPT_SMALLK) != 2;
-  const int ks = (int)ceil_div(K, 16);
+  const int ks = K <= 16 ? 1 : (int)ceil_div(K, 32) * 2;  // 1, 2, 4, 6: the k-step plans above
 #define MVML_SK(KS, IL, NTV)                                                                      \
   gemm_smallk_kernel<KS, IL, NTV><<<(unsigned)blocks, 256, 0, st>>>(M, N, (int)K, A, lda, B, ldb,  \
                                                                       a_rows, amax_b, bias, act, C, \
@@ -2693,9 +2711,8 @@ int smallk_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, 
   switch (ks) {                             \
     case 1: MVML_SK(1, IL, NTV); break;     \
     case 2: MVML_SK(2, IL, NTV); break;     \
-    case 3: MVML_SK(3, IL, NTV); break;     \
     case 4: MVML_SK(4, IL, NTV); break;     \
-    default: MVML_SK(5, IL, NTV); break;    \
+    default: MVML_SK(6, IL, NTV); break;    \
   }
   if (il4) {
     if (nt) { MVML_SK_KS(true, true) } else { MVML_SK_KS(true, false) }

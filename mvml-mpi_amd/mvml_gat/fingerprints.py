@@ -841,3 +841,16 @@ def fingerprints(smiles_list):
     """float32[len, 2513] (the fps_t tensor collate builds, dataset.py:56)."""
     return np.stack([fingerprint(s) for s in smiles_list]) if smiles_list else \
         np.zeros((0, FP_SIZE), dtype=np.float32)
+
+
+def kegg_pool():
+    """float32[420, 2513]: the fingerprints of the 420 KEGG test-split molecules
+    (tests/golden/kegg_test_split.csv) as computed by fingerprints() and stored bit-packed in
+    data/kegg_fp_pool.npz (tools/make_fp_pool.py) — real bit vectors for workloads whose
+    molecules are synthetic (bench.py --workload mvp cycles them)."""
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "kegg_fp_pool.npz")
+    with np.load(path, allow_pickle=False) as z:
+        bits = np.unpackbits(z["bits"], axis=1, count=int(z["nbits"])).astype(np.float32)
+        erg = z["erg"].astype(np.float32)
+    return np.concatenate([bits[:, :MACCS_BITS], erg, bits[:, MACCS_BITS:]], axis=1)

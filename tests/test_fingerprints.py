@@ -90,3 +90,18 @@ def test_fingerprint_layout():
     v = fp.fingerprints(["CNO", "c1ccncc1"])
     assert v.shape == (2, 2513) and v.dtype == np.float32
     assert np.array_equal(v[0, :167], fp.maccs_keys(fz.mol_from_smiles("CNO")))
+
+
+def test_kegg_pool_matches_fingerprints():
+    """The packed pool bench.py's MVP workload reads holds exactly what fingerprints() computes
+    for those molecules (a sample of rows recomputed here)."""
+    import csv
+    import os
+    from mvml_gat.fingerprints import FP_SIZE, fingerprints, kegg_pool
+    pool = kegg_pool()
+    assert pool.shape == (420, FP_SIZE) and pool.dtype == np.float32
+    here = os.path.dirname(os.path.abspath(__file__))
+    with open(os.path.join(here, "golden", "kegg_test_split.csv"), newline="") as f:
+        smiles = [r["smiles"] for r in csv.DictReader(f)]
+    idx = [0, 1, 57, 200, 419]
+    assert np.array_equal(pool[idx], fingerprints([smiles[i] for i in idx]))

@@ -1,6 +1,5 @@
 #!/bin/bash
-# small-K projection: tests + micro-bench + kernel trace
 set -o pipefail
 cd "$(dirname "$0")/.."
-tools/gpu_r5.sh tests sk tests/test_gpu_smallk.py && \
+tools/gpu_r5.sh tests sk tests/test_gpu_smallk.py || exit 1
 timeout -k 10 300 python -u tools/smallk_bench.py > gpurun_out/smallk_bench.txt 2>&1; rc=$?; cat gpurun_out/smallk_bench.txt; exit $rc
