@@ -43,6 +43,7 @@ METRIC = "molecules/sec GAT-view fwd+bwd at 1/2/4/8 GPU; % HBM peak on aggregati
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 FP32_MFMA_PEAK_TFS = 157.3  # f32-input MFMA = f32 vector peak (same table)
 BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA peak (same table; the 5 PF figure is 2:1 sparse)
+SMALLK_MAX_K = 96  # mvml_gemm_f16x2_rows products at K <= this run gemm_smallk_kernel (option smallk)
 TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32x3", "mvml_gemm_bf16", "mvml_gat_proj_fwd", "mvml_set2set_seg_fwd",
          "mvml_set2set_seg_bwd", "mvml_lstm_cell_fwd", "mvml_lstm_cell_bwd", "mvml_set2set_gx",
          "mvml_graphnorm_fwd", "mvml_graphnorm_bwd", "mvml_colsum_f32", "mvml_gat_fold_weights",
@@ -565,9 +566,19 @@ def run(args):
             extra["roofline_agg_bwd"] = roofline_entry(summ["mvml_gat_agg_bwd"], "hbm",
                                                        load_traffic(wkey, "gat_agg_bwd"))
         proj_ev = summ.get("mvml_gat_proj_fwd", [])
+        # the small-K per-row products (K <= 96: layer 1's projection on the wave-per-64-column
+        # memory kernel, gemm_smallk_kernel) are an HBM roofline of their own, not MFMA work
+        rows_ev = summ.get("mvml_gemm_f16x2_rows", [])
+        sk_ev = [e for e in rows_ev if (e[1] or {}).get("shape", (0, 0, 1 << 30))[2] <= SMALLK_MAX_K]
+        rows_ev = [e for e in rows_ev if e not in sk_ev]
+        if sk_ev:
+            extra["roofline_proj_l1"] = roofline_entry(sk_ev, "hbm")
+            extra["roofline_proj_l1"]["kernel"] = (
+                "mvml_gemm_f16x2_rows at K <= 96 (layer-1 projection X[N, 76] Wcat[1544, 76]^T, "
+                "gemm_smallk_kernel); bytes = A, B and C once")
         gemm_ev = (summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", [])
                    + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])
-                   + summ.get("mvml_gemm_f16x2_bsplit", []) + summ.get("mvml_gemm_f16x2_rows", [])
+                   + summ.get("mvml_gemm_f16x2_bsplit", []) + rows_ev
                    + summ.get("mvml_gemm_f32x3_batched", []) + summ.get("mvml_lstm_gates_cell_fwd", [])
                    + summ.get("mvml_gemm_f16x2_ex", []) + summ.get("mvml_gemm_f16x2_batched", [])
                    + ([] if args.proj_bf16 else proj_ev))

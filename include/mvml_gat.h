@@ -71,9 +71,9 @@ const char* mvml_version(void);
                                    per-atom pair */
 #define MVML_OPT_FLAT_SRC 8     /* MVML_FLAT_SRC: flatten GAT layers' aggregation backward by
                                    source atom (one wave per atom gathers its out-neighbours'
-                                   rows): 2 = one pass (g_rst of each gathered row formed in
-                                   registers from g_out / out), 1 = g_rst rows formed first as
-                                   gY's dR block, then gathered; 0 (default) = molecule / big
+                                   rows; g_rst of each gathered row formed in registers from
+                                   g_out / out): 1 or 2 (the same one-pass kernel since round
+                                   5); 0 (default) = molecule / big
                                    windows + per-atom pair.  The Python layer sets it per call
                                    for batches of large molecules (mvml_gat.functional) */
 #define MVML_OPT_DST_FWD 9      /* MVML_DST_FWD: 1 = aggregation forward by destination wave for
@@ -86,7 +86,8 @@ const char* mvml_version(void);
                                    destination-wave forward (0 = the default per width; tuning) */
 #define MVML_OPT_SMALLK 11      /* MVML_SMALLK: 1 (default) mvml_gemm_f16x2_rows products with
                                    K <= 96 (layer 1's projection) on the wave-per-64-columns
-                                   memory kernel (non-temporal stores; 2 = plain stores);
+                                   memory kernel (non-temporal stores; 2 = plain stores;
+                                   3 .. 6: timing variants, tools/smallk_bench.py);
                                    0 = the 256x256 tile */
 int mvml_set_option(int option, int value);
 int mvml_get_option(int option);

@@ -63,9 +63,12 @@ struct Scan2 {
   const int64_t* in[2];
   int64_t* out[2];
   int64_t* tmp[2];
+  int32_t* zero[2] = {nullptr, nullptr};  // two words each, zeroed by the first kernel (the
+                                          // CSR build's status flags and list counts: no memsets)
 };
 __global__ void scan2_tile_sums(Scan2 a, int64_t n) {
   const int y = blockIdx.y;
+  if (blockIdx.x == 0 && threadIdx.x < 2 && a.zero[y]) a.zero[y][threadIdx.x] = 0;
   __shared__ int64_t w[kScanThreads / 64 + 1];
   const int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
   int64_t s = 0;
@@ -559,17 +562,36 @@ __global__ void node_group_kind_kernel(int64_t G, const int32_t* __restrict__ ro
 }
 
 // The fallback lists in group order, one workgroup: thread t owns the contiguous groups
-// [t R, (t + 1) R), R = ceil(G / 1024) — it counts its flags (independent loads, no load
-// latency per 1024-group chunk behind two barriers: ~35 us per batch before), the counts are
-// exclusive-scanned across the workgroup (shuffles within a wave, the 16 wave totals through
-// LDS), and a second pass over the same groups writes the entries in group order.
-__device__ __forceinline__ void group_flags(const int32_t* start, const int32_t* kind, int64_t g, bool& f0,
-                                            bool& f1) {
-  f0 = f1 = false;
-  if (start[g + 1] > start[g]) {
-    const int k = kind[g];
-    f0 = (k & 1) == 0;
-    f1 = (k & 2) == 0;
+// [t R, (t + 1) R), R = ceil(G / 1024).  Its starts and kinds are read 8 groups per round with
+// every load independent (a loop with the kind load behind the emptiness test paid two load
+// latencies per group: ~30 us per 65,536-molecule batch), the flags kept as bit masks (R <= 64;
+// larger plans re-read them in a second pass), the counts exclusive-scanned across the
+// workgroup (shuffles within a wave, the 16 wave totals through LDS) and the entries written
+// in group order.
+constexpr int kListUnroll = 8;
+__device__ __forceinline__ void group_flag_masks(const int32_t* __restrict__ start, const int32_t* __restrict__ kind,
+                                                 int64_t G, int64_t g0, int64_t g1, uint64_t& m0, uint64_t& m1,
+                                                 int& c0, int& c1) {
+  m0 = m1 = 0;
+  c0 = c1 = 0;
+  for (int64_t base = g0; base < g1; base += kListUnroll) {
+    int32_t sv[kListUnroll + 1], kv[kListUnroll];
+#pragma unroll
+    for (int u = 0; u <= kListUnroll; ++u) sv[u] = start[min(base + u, G)];
+#pragma unroll
+    for (int u = 0; u < kListUnroll; ++u) kv[u] = kind[min(base + u, G - 1)];
+#pragma unroll
+    for (int u = 0; u < kListUnroll; ++u) {
+      const bool live = base + u < g1 && sv[u + 1] > sv[u];
+      const bool f0 = live && (kv[u] & 1) == 0, f1 = live && (kv[u] & 2) == 0;
+      c0 += f0;
+      c1 += f1;
+      const int sh = (int)(base + u - g0);
+      if (sh < 64) {
+        m0 |= (uint64_t)f0 << sh;
+        m1 |= (uint64_t)f1 << sh;
+      }
+    }
   }
 }
 __global__ void __launch_bounds__(1024) node_group_lists_kernel(int64_t G, int32_t* __restrict__ plan) {
@@ -579,13 +601,9 @@ __global__ void __launch_bounds__(1024) node_group_lists_kernel(int64_t G, int32
   __shared__ int s_w[2][16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t R = (G + 1023) / 1024, g0 = min(G, tid * R), g1 = min(G, g0 + R);
-  int c0 = 0, c1 = 0;
-  for (int64_t g = g0; g < g1; ++g) {
-    bool f0, f1;
-    group_flags(start, kind, g, f0, f1);
-    c0 += f0;
-    c1 += f1;
-  }
+  uint64_t m0, m1;
+  int c0, c1;
+  group_flag_masks(start, kind, G, g0, g1, m0, m1, c0, c1);
   int i0 = c0, i1 = c1;  // inclusive wave scans
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -608,13 +626,13 @@ __global__ void __launch_bounds__(1024) node_group_lists_kernel(int64_t G, int32
     t0 += s_w[0][k];
     t1 += s_w[1][k];
   }
-  if (c0 | c1) {
-    for (int64_t g = g0; g < g1; ++g) {
-      bool f0, f1;
-      group_flags(start, kind, g, f0, f1);
-      if (f0) plan[2 * G + 3 + o0++] = (int32_t)g;
-      if (f1) plan[3 * G + 3 + o1++] = (int32_t)g;
+  for (int64_t cb = g0; cb < g1 && (c0 | c1); cb += 64) {  // 64 groups per mask
+    if (cb > g0) {  // (R > 64 only) the next 64 groups' flags again
+      int d0, d1;
+      group_flag_masks(start, kind, G, cb, min(g1, cb + 64), m0, m1, d0, d1);
     }
+    for (uint64_t m = m0; m; m &= m - 1) plan[2 * G + 3 + o0++] = (int32_t)(cb + __builtin_ctzll(m));
+    for (uint64_t m = m1; m; m &= m - 1) plan[3 * G + 3 + o1++] = (int32_t)(cb + __builtin_ctzll(m));
   }
   if (tid == 0) {
     count[0] = t0;
@@ -663,9 +681,9 @@ extern "C" int mvml_build_csr(const int32_t* src_local, const int32_t* dst_local
   int32_t* list1 = cv.take<int32_t>((size_t)(num_graphs > 0 ? num_graphs : 1));
   int32_t* list2 = cv.take<int32_t>((size_t)(num_graphs > 0 ? num_graphs : 1));
   int* counts = cv.take<int>(2);
-  (void)hipMemsetAsync(status_flags, 0, 2 * sizeof(int32_t), st);
-  (void)hipMemsetAsync(counts, 0, 2 * sizeof(int), st);
-  const Scan2 sc{{batch_num_nodes, batch_num_edges}, {node_offsets, edge_offsets}, {tmp, tmp2}};
+  if (num_graphs == 0) (void)hipMemsetAsync(status_flags, 0, 2 * sizeof(int32_t), st);
+  const Scan2 sc{{batch_num_nodes, batch_num_edges}, {node_offsets, edge_offsets}, {tmp, tmp2},
+                 {status_flags, reinterpret_cast<int32_t*>(counts)}};
   int rc = exclusive_scan2_i64(sc, num_graphs, st);
   if (rc) return rc;
   if (num_nodes == 0) {

@@ -2059,124 +2059,13 @@ gat_mean_bwd_gel_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
 
 // ---- Flatten layer backward by source atom (MVML_OPT_FLAT_SRC), for large molecules ----------
 // The flatten layer's g_rst (= g_out x ELU'(out)) is per head, so the source-owned form needs
-// g_rst rows of the out-neighbours: pass 1 forms every row's g_rst once and writes it as gY's dR
-// block (the backward writes that block anyway); pass 2 is the source-atom kernel over H F-wide
-// rows: the wave of source u reads Z[u] once and gathers the g_rst rows of its out-edges (from
-// the XCD's L2), forming dZ[u] (out-CSR order, the per-atom pass's arithmetic) and g_a per edge.
-// The softmax and d el passes are the head-mean path's.  Used where the molecule windows do not
-// hold the molecules (config 5), where it replaces the big window's 96 chunk barriers.
-__global__ void __launch_bounds__(256)
-gat_flat_grst_kernel(int64_t N, int HF, const float* __restrict__ g_out, const float* __restrict__ out,
-                     int mode, float* __restrict__ gY, int64_t ldgy, uint32_t* __restrict__ gy_amax,
-                     uint32_t* __restrict__ gy_rows) {
-  const int lane = threadIdx.x & 63;
-  const int64_t v = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-  float m = 0.f;
-  if (v < N) {
-    for (int c4 = lane; 4 * c4 < HF; c4 += 64) {
-      float4 g = ld4(g_out + v * HF + 4 * c4);
-      if (mode == 0) {  // ELU'(x) = 1 (x > 0) else out + 1 (torch elu_backward on the result)
-        const float4 o = ld4(out + v * HF + 4 * c4);
-        g.x *= o.x > 0.f ? 1.f : o.x + 1.f;
-        g.y *= o.y > 0.f ? 1.f : o.y + 1.f;
-        g.z *= o.z > 0.f ? 1.f : o.z + 1.f;
-        g.w *= o.w > 0.f ? 1.f : o.w + 1.f;
-      }
-      st4(gY + v * ldgy + HF + 4 * c4, g);
-      m = amax4(m, g);
-    }
-    m = wave_max(m);
-    if (gy_rows && lane == 0) gy_rows[v] = __float_as_uint(m);  // the first writer of the row
-  }
-  if (gy_amax) block_amax_commit<256>(m, gy_amax);
-}
-
-template <int H, int NJ>
-__global__ void __launch_bounds__(256)
-gat_flat_bwd_src_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
-                        const int32_t* __restrict__ out_dst, const int32_t* __restrict__ out_inslot,
-                        const float* __restrict__ Y, int64_t ldy, const float* __restrict__ attn, int F,
-                        float* __restrict__ ga, float* __restrict__ gY, int64_t ldgy,
-                        uint32_t* __restrict__ gy_amax, uint32_t* __restrict__ gy_rows) {
-  const int lane = threadIdx.x & 63;
-  const int64_t u = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-  float gmx = 0.f;
-  if (u < N) {  // (no early return: block_amax_commit below has a barrier)
-    const int HF = H * F;
-    bool okc[NJ];
-    int hc[NJ];
-    float4 z[NJ], dz[NJ];
-#pragma unroll
-    for (int c = 0; c < NJ; ++c) {
-      const int col = 4 * (lane + 64 * c);
-      okc[c] = col < HF;
-      hc[c] = okc[c] ? col / F : 0;
-      z[c] = okc[c] ? ld4nt(Y + u * ldy + col) : f4(0.f);
-      dz[c] = f4(0.f);
-    }
-    const int ob = out_rowptr[u], oe = out_rowptr[u + 1];
-    for (int base = ob; base < oe; base += 64) {
-      const int cnt = min(64, oe - base);
-      int w_l = 0, s_l = 0;
-      float a_l[H];
-#pragma unroll
-      for (int h = 0; h < H; ++h) a_l[h] = 0.f;
-      if (lane < cnt) {
-        w_l = out_dst[base + lane];
-        s_l = out_inslot[base + lane];
-#pragma unroll
-        for (int h = 0; h < H; ++h) a_l[h] = attn[(int64_t)s_l * H + h];
-      }
-      for (int j = 0; j < cnt; j += 2) {  // two g_rst rows in flight
-        const int j1 = min(j + 1, cnt - 1);
-        const bool two = j + 1 < cnt;  // (uniform)
-        const float* g0p = gY + (int64_t)rl(w_l, j) * ldgy + HF;
-        const float* g1p = gY + (int64_t)rl(w_l, j1) * ldgy + HF;
-        float4 g0[NJ], g1[NJ];
-#pragma unroll
-        for (int c = 0; c < NJ; ++c) {
-          g0[c] = okc[c] ? ld4(g0p + 4 * (lane + 64 * c)) : f4(0.f);
-          g1[c] = okc[c] ? ld4(g1p + 4 * (lane + 64 * c)) : f4(0.f);
-        }
-        float a0[H], a1[H], p0[H], p1[H];
-#pragma unroll
-        for (int h = 0; h < H; ++h) { a0[h] = rl(a_l[h], j); a1[h] = rl(a_l[h], j1); p0[h] = 0.f; p1[h] = 0.f; }
-#pragma unroll
-        for (int c = 0; c < NJ; ++c)
-          if (okc[c]) {
-            dz[c] = fma4(pick<H>(a0, hc[c]), g0[c], dz[c]);
-            if (two) dz[c] = fma4(pick<H>(a1, hc[c]), g1[c], dz[c]);
-            add_at<H>(p0, hc[c], dot4(z[c], g0[c]));
-            add_at<H>(p1, hc[c], dot4(z[c], g1[c]));
-          }
-        HeadReduce<H>::template all<false>(p0, lane);
-        store_heads<H>(ga + (int64_t)rl(s_l, j) * H, p0, lane);
-        if (two) {
-          HeadReduce<H>::template all<false>(p1, lane);
-          store_heads<H>(ga + (int64_t)rl(s_l, j1) * H, p1, lane);
-        }
-      }
-    }
-    float rmx = 0.f;
-#pragma unroll
-    for (int c = 0; c < NJ; ++c)
-      if (okc[c]) {
-        st4nt(gY + u * ldgy + 4 * (lane + 64 * c), dz[c]);
-        rmx = amax4(rmx, dz[c]);
-      }
-    gmx = wave_max(rmx);
-    if (gy_rows && lane == 0) gy_rows[u] = max(gy_rows[u], __float_as_uint(gmx));
-  }
-  if (gy_amax) block_amax_commit<256>(gmx, gy_amax);
-}
-
-// The flatten layer's backward by source atom in ONE pass (MVML_OPT_FLAT_SRC = 2): no g_rst pass
-// and no re-read of a g_rst block.  The wave of source u forms its own g_rst row once from
-// g_out[u] and out[u] (ELU'(x) = out + 1 below 0, as gat_flat_grst_kernel) and writes it as dR[u];
+// the g_rst rows of the out-neighbours.  One pass: the wave of source u forms its own g_rst row
+// once from g_out[u] and out[u] (ELU'(x) = out + 1 below 0) and writes it as dR[u];
 // for each out-edge u -> w it gathers the g_out[w] (and out[w]) rows — read by w's own wave and by
 // w's other in-neighbours' waves at about the same time, so from the XCD's L2 — and forms g_rst[w]
 // in registers with the same arithmetic, then dZ[u] += a_e g_rst[w] (out-CSR order) and
-// g_a[e] = <Z[u], g_rst[w]> per head.  Bitwise the two-pass path's gY and g_a.
+// g_a[e] = <Z[u], g_rst[w]> per head.  (Round 4 had a two-pass form — every g_rst row written
+// first, then gathered — with the same bits; measured slower, deleted in round 5.)
 template <int H, int NJ, int MODE, int U = 2>
 __global__ void __launch_bounds__(256)
 gat_flat_bwd_src1_kernel(int64_t N, const int32_t* __restrict__ out_rowptr,
@@ -2320,42 +2209,6 @@ int launch_flat_src1(int64_t N, const int32_t* rp, const int32_t* src, const int
 }
 
 template <int H>
-int launch_flat_src(int64_t N, const int32_t* rp, const int32_t* src, const int32_t* orp,
-                    const int32_t* odst, const int32_t* oslot, const float* Y, int64_t ldy,
-                    const float* elr, const float* attn, const float* out, const float* g_out, int F,
-                    float slope, int mode, float* gpre, float* gY, int64_t ldgy, int C, uint32_t* gy_amax,
-                    uint32_t* gy_rows, hipStream_t st) {
-  const int HF = H * F;
-  const int nj = (int)ceil_div(HF / 4, 64);
-  const unsigned b4 = (unsigned)ceil_div(N, 4), b256 = (unsigned)ceil_div(N, 256);
-  gat_flat_grst_kernel<<<b4, 256, 0, st>>>(N, HF, g_out, out, mode, gY, ldgy, gy_amax, gy_rows);
-  int rc = check_launch("gat_flat_grst_kernel");
-  if (rc) return rc;
-#define MVML_FLAT_SRC(NJ) \
-  gat_flat_bwd_src_kernel<H, NJ><<<b4, 256, 0, st>>>(N, orp, odst, oslot, Y, ldy, attn, F, gpre, gY, ldgy, \
-                                                     gy_amax, gy_rows)
-  switch (nj) {
-    case 1: MVML_FLAT_SRC(1); break;
-    case 2: MVML_FLAT_SRC(2); break;
-    case 3: MVML_FLAT_SRC(3); break;
-    case 4: MVML_FLAT_SRC(4); break;
-    case 5: MVML_FLAT_SRC(5); break;
-    case 6: MVML_FLAT_SRC(6); break;
-    case 7: MVML_FLAT_SRC(7); break;
-    case 8: MVML_FLAT_SRC(8); break;
-    default: set_error("gat_agg_bwd: flat-src path needs H F <= 2048"); return MVML_ERR_INVALID;
-  }
-#undef MVML_FLAT_SRC
-  rc = check_launch("gat_flat_bwd_src_kernel");
-  if (rc) return rc;
-  gat_mean_bwd_softmax_kernel<H><<<b256, 256, 0, st>>>(N, rp, src, elr, attn, slope, gpre, gY, ldgy, C);
-  rc = check_launch("gat_mean_bwd_softmax_kernel");
-  if (rc) return rc;
-  gat_mean_bwd_gel_kernel<H><<<b256, 256, 0, st>>>(N, orp, oslot, gpre, gY, ldgy, C, gy_amax, gy_rows);
-  return check_launch("gat_mean_bwd_gel_kernel");
-}
-
-template <int H>
 int launch_mean_src(int64_t N, const int32_t* rp, const int32_t* src, const int32_t* orp,
                     const int32_t* odst, const int32_t* oslot, const float* Y, int64_t ldy,
                     const float* elr, const float* attn, const float* g_out, int F, float slope,
@@ -2492,12 +2345,11 @@ int launch_bwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
   if (mode == 1 && option(MVML_OPT_MEAN_SRC) && F <= 1024)  // head-mean layer by source atom
     return launch_mean_src<H>(N, rp, src, orp, odst, oslot, Y, ldy, elr, attn, g_out, F, slope, gpre, gY,
                               ldgy, C, gy_amax, gy_rows, st);
-  if (mode != 1 && option(MVML_OPT_FLAT_SRC) == 2)  // flatten layer by source atom, one pass
+  // flatten layer by source atom, one pass (round 5; the round-4 two-pass form — g_rst rows
+  // written first, then gathered — computed the same bits and was measured slower: deleted)
+  if (mode != 1 && option(MVML_OPT_FLAT_SRC))
     return launch_flat_src1<H>(N, rp, src, orp, odst, oslot, Y, ldy, elr, attn, out, g_out, F, slope, mode,
                                gpre, gY, ldgy, C, gy_amax, gy_rows, st);
-  if (mode != 1 && option(MVML_OPT_FLAT_SRC))  // flatten layer by source atom (large molecules)
-    return launch_flat_src<H>(N, rp, src, orp, odst, oslot, Y, ldy, elr, attn, out, g_out, F, slope, mode,
-                              gpre, gY, ldgy, C, gy_amax, gy_rows, st);
   if (option(MVML_OPT_BWD_ATOMWISE)) G = 0;  // tests: the per-atom pair over every atom
   if (F % 32 == 0 && G > 0) {  // molecule groups: one pass over Z / g_out / dZ per group
 #ifndef MVML_BWD_CW64

@@ -2517,20 +2517,25 @@ int colsum_splits(int64_t M, int64_t N) {
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kSkMaxK = 96;
-constexpr int kSkPitch = 68;  // floats per row of a wave's 16 x 64 LDS staging slice (+4: rows 4 banks apart)
 
-// KS16: 1 = one 16-deep step on 16x16x16 (K <= 16); else ceil(K / 32) steps of 16x16x32, the
-// last zero-padded past K.  (A 16x16x16 tail behind 16x16x32 steps on the same accumulators
-// came out wrong in the first two of each lane's four results at K = 76 / 80 — a missing
-// MFMA-to-MFMA wait between the two pass counts — so the kernel never mixes the two shapes.)
-template <int KS16, bool IL4, bool NT>
-__global__ void __launch_bounds__(256)
+// KS16 = ceil(K / 16): KS16 / 2 steps of 16x16x32 and, for odd KS16, a 16-deep tail on
+// 16x16x16, each zero-padded past K.  The tail accumulates into its OWN registers, added once at
+// the end: behind 16x16x32 steps on the same accumulators it came out wrong in the first two of
+// each lane's four results (K = 76 / 80, a missing MFMA-to-MFMA wait between the two pass
+// counts).  Skipping the 16 padding k of a 96-deep plan saves 1/6 of the MFMA time at K = 76.
+// A rows with an all-zero low plane (fp16-exact values: layer 1's 0/1 atom features) skip the
+// h_b l_a products — per 16-row block, wave-uniform (a ballot); adding exact zeros is all they
+// would do.
+// ABL (timing ablations, option smallk 5 / 6; wrong results): 1 = no MFMAs, 2 = no C stores
+template <int KS16, bool IL4, bool NT, int ABL = 0, int NG = 4>
+__global__ void __launch_bounds__(256, 2)  // two waves per SIMD: <= 256 registers per lane
 gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int64_t lda,
                    const float* __restrict__ B, int64_t ldb, const uint32_t* __restrict__ a_rows,
                    const uint32_t* __restrict__ amax_b, const float* __restrict__ bias, int act,
                    float* __restrict__ C, int64_t ldc, int n_slabs, int chunk_blocks) {
-  constexpr int N32 = KS16 == 1 ? 0 : (KS16 + 1) / 2, T16 = KS16 == 1 ? 1 : 0, NW = N32 > 0 ? N32 : 1;
+  constexpr int N32 = KS16 / 2, T16 = KS16 % 2, NW = N32 > 0 ? N32 : 1;
   constexpr int NX = 2 * N32 + T16;  // A float4 per lane and row block
+  constexpr int SW = 16 * NG, PITCH = SW + 4;  // slab width (columns per wave); LDS row pitch
   const int lane = threadIdx.x & 63, li = lane & 15, lq = lane >> 4;
   const int64_t w = xcd_block(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int slab = (int)(w % n_slabs);
@@ -2542,8 +2547,8 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
   const float s_b = pow2f(kb), u_b = pow2f(-kb);
   // this lane's B rows (output columns c0 + 16 g + li) for the MFMA's A side: k = 32 s + 8 lq
   // + 0..7 (x32 steps), 32 N32 + 4 lq + 0..3 (x16 tail); k >= K reads as zero
-  f16x8 bh[4][NW], bl[4][NW];
-  f16x4 th[4], tl[4];
+  f16x8 bh[NG][NW], bl[NG][NW];
+  f16x4 th[NG], tl[NG];
   auto piece = [&](const float* row, int k, uint2& h, uint2& l) {  // B[row][k .. k + 3] as planes
     const float4 v = *reinterpret_cast<const float4*>(row + min(k, K - 4));
     if constexpr (IL4) {
@@ -2555,8 +2560,8 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
     if (k >= K) h = l = make_uint2(0u, 0u);
   };
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int64_t col = (int64_t)slab * 64 + 16 * g + li;
+  for (int g = 0; g < NG; ++g) {
+    const int64_t col = (int64_t)slab * SW + 16 * g + li;
     const float* row = B + min(col, N - 1) * ldb;
 #pragma unroll
     for (int s = 0; s < N32; ++s) {
@@ -2574,12 +2579,12 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
       tl[g] = __builtin_bit_cast(f16x4, l);
     }
   }
-  float bv[4][4];
+  float bv[NG][4];
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
+  for (int g = 0; g < NG; ++g)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int64_t col = (int64_t)slab * 64 + 16 * g + 4 * lq + u;
+      const int64_t col = (int64_t)slab * SW + 16 * g + 4 * lq + u;
       bv[g][u] = (bias && col < N) ? bias[col] : 0.f;
     }
   // A fragments of one 16-row block: row 16 rb + li, k as B's; KS16 float4 per lane
@@ -2594,17 +2599,16 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
     if constexpr (T16) x[NX - 1] = *reinterpret_cast<const float4*>(p + min(32 * N32 + 4 * lq, K - 4));
     rbits = a_rows[r];
   };
-  __shared__ __attribute__((aligned(16))) float s_c[4][16 * kSkPitch];
+  __shared__ __attribute__((aligned(16))) float s_c[4][16 * PITCH];
   float* wl = s_c[threadIdx.x >> 6];
-  float4 xn[NX];
-  uint32_t rn;
-  load_a(rb0, xn, rn);
-  for (int64_t rb = rb0; rb < rb1; ++rb) {
+  // two register sets, prefetch distance 2: a block's A rows are requested two blocks before
+  // they are split (the first of the ~25 waves reading a row block pays the HBM miss)
+  auto block = [&](int64_t rb, float4 (&xn)[NX], uint32_t& rn) {
     float4 x[NX];
 #pragma unroll
     for (int i = 0; i < NX; ++i) x[i] = xn[i];
     const int ka = amax_shift(rn);
-    if (rb + 1 < rb1) load_a(rb + 1, xn, rn);
+    if (rb + 2 < rb1) load_a(rb + 2, xn, rn);
     const float s_a = pow2f(ka);
     f16x8 ah[NW], al[NW];
     f16x4 ath, atl;
@@ -2626,28 +2630,62 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
       ath = __builtin_bit_cast(f16x4, h);
       atl = __builtin_bit_cast(f16x4, l);
     }
-    f32x4 acc[4];
+    // any non-zero word in the block's A low plane (wave-uniform)
+    uint32_t lo_bits = 0;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < N32; ++s) {
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[g][s], ah[s], acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[g][s], al[s], acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[g][s], ah[s], acc[g], 0, 0, 0);
-      }
-      if constexpr (T16) {
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(tl[g], ath, acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[g], atl, acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[g], ath, acc[g], 0, 0, 0);
-      }
+    for (int s = 0; s < N32; ++s) {
+      const u32x4 q = __builtin_bit_cast(u32x4, al[s]);
+      lo_bits |= q[0] | q[1] | q[2] | q[3];
     }
+    if constexpr (T16) {
+      const uint2 q = __builtin_bit_cast(uint2, atl);
+      lo_bits |= q.x | q.y;
+    }
+    const bool a_lo = __ballot(lo_bits != 0) != 0;
+    f32x4 acc[NG];
+    auto products = [&](auto ALO) {
+      constexpr bool kLo = decltype(ALO)::value;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (ABL == 1) {
+#pragma unroll
+          for (int s = 0; s < N32; ++s) {
+            acc[g][0] += (float)ah[s][g] * (float)bh[g][s][0];
+            acc[g][1] += (float)al[s][g] * (float)bl[g][s][1];
+          }
+          continue;
+        }
+#pragma unroll
+        for (int s = 0; s < N32; ++s) {
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[g][s], ah[s], acc[g], 0, 0, 0);
+          if constexpr (kLo) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[g][s], al[s], acc[g], 0, 0, 0);
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[g][s], ah[s], acc[g], 0, 0, 0);
+        }
+      }
+      if constexpr (T16 && ABL != 1) {
+        f32x4 tac[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          tac[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+          tac[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(tl[g], ath, tac[g], 0, 0, 0);
+          if constexpr (kLo) tac[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[g], atl, tac[g], 0, 0, 0);
+          tac[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[g], ath, tac[g], 0, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) acc[g] = N32 > 0 ? acc[g] + tac[g] : tac[g];
+      }
+    };
+    if (a_lo)
+      products(std::true_type{});
+    else
+      products(std::false_type{});
     // the 16 x 64 block leaves through the wave's LDS slice: each lane's 4 x float4 (row li,
     // columns 16 g + 4 lq) in, then 4 rows x 256 contiguous bytes per store instruction out
     // (straight from the accumulators a store instruction would write 16 rows x 64 B)
     const float u_a = pow2f(-ka);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < NG; ++g) {
       float4 o;
       o.x = acc[g][0] * u_b * u_a + bv[g][0];
       o.y = acc[g][1] * u_b * u_a + bv[g][1];
@@ -2656,15 +2694,15 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
       if (act == 1) {
         o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
       }
-      *reinterpret_cast<float4*>(wl + li * kSkPitch + 16 * g + 4 * lq) = o;
+      *reinterpret_cast<float4*>(wl + li * PITCH + 16 * g + 4 * lq) = o;
     }
     wave_sync_lds();
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int rr = 4 * t + (lane >> 4), c4 = 4 * (lane & 15);
-      const float4 o = *reinterpret_cast<const float4*>(wl + rr * kSkPitch + c4);
-      const int64_t row = rb * 16 + rr, col = (int64_t)slab * 64 + c4;
-      if (row < M && col < N) {
+    for (int t = 0; t < NG; ++t) {  // 64 / (4 NG) rows of SW floats per store instruction
+      const int rr = (16 / NG) * t + lane / (4 * NG), c4 = 4 * (lane % (4 * NG));
+      const float4 o = *reinterpret_cast<const float4*>(wl + rr * PITCH + c4);
+      const int64_t row = rb * 16 + rr, col = (int64_t)slab * SW + c4;
+      if (row < M && col < N && (ABL != 2 || __float_as_uint(o.x) == 0x7fc00123u)) {
         if constexpr (NT) {
           const f32x4 ov = {o.x, o.y, o.z, o.w};
           __builtin_nontemporal_store(ov, reinterpret_cast<f32x4*>(C + row * ldc + col));
@@ -2674,6 +2712,16 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
       }
     }
     wave_sync_lds();  // the reads are done before the next block's writes
+  };
+  float4 xa[NX], xb[NX];
+  uint32_t ra = 0, rbits = 0;
+  load_a(rb0, xa, ra);
+  if (rb0 + 1 < rb1) load_a(rb0 + 1, xb, rbits);
+  // (measured: issuing block rb + 1's MFMAs before block rb's epilogue, two accumulator sets,
+  // was ~5 % slower relative to the tile on the same box)
+  for (int64_t rb = rb0; rb < rb1; rb += 2) {
+    block(rb, xa, ra);
+    if (rb + 1 < rb1) block(rb + 1, xb, rbits);
   }
 }
 
@@ -2690,19 +2738,23 @@ bool smallk_fits(int b_kmajor, int64_t M, int64_t N, int64_t K, const float* A, 
 int smallk_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
                   int64_t ldb, bool il4, const uint32_t* a_rows, const uint32_t* amax_b,
                   const float* bias, int act, float* C, int64_t ldc, hipStream_t st) {
+  // 64 columns per wave (NG = 4).  Measured: 32-column slabs (NG = 2, 152 VGPRs, three waves
+  // per SIMD) 3.38 vs 2.87 ms at config 3 — twice the A reads cost more than the occupancy buys
   const int n_slabs = (int)ceil_div(N, 64);
   const int64_t nrb = ceil_div(M, 16);
   // ~32 row blocks (512 rows) per wave: the B slab's one load is 1/30 of what the wave stores;
   // fewer on small launches so that >= 4096 waves fill the chip
-  const int64_t cb = std::max<int64_t>(1, std::min<int64_t>(32, nrb * n_slabs / 4096));
+  const int sko = option(MVML_OPT_SMALLK);
+  const int64_t cap = sko == 3 ? 8 : (sko == 4 ? 128 : 32);  // (3 / 4: chunk-size variants)
+  const int64_t cb = std::max<int64_t>(1, std::min<int64_t>(cap, nrb * n_slabs / 4096));
   const int64_t waves = ceil_div(nrb, cb) * n_slabs;
   const int64_t blocks = ceil_div(waves, 4);
   if (blocks >= (int64_t(1) << 31)) {
     set_error("gemm small-K: too many blocks");
     return MVML_ERR_INVALID;
   }
-  const bool nt = option(MVML_OPT_SMALLK) != 2;
-  const int ks = K <= 16 ? 1 : (int)ceil_div(K, 32) * 2;  // 1, 2, 4, 6: the k-step plans above
+  const bool nt = option(MVML_OPT_SMALLK) != 2;  // (3 .. 6: timing variants)
+  const int ks = (int)ceil_div(K, 16);  // 1 .. 6: the k-step plans above
 #define MVML_SK(KS, IL, NTV)                                                                      \
   gemm_smallk_kernel<KS, IL, NTV><<<(unsigned)blocks, 256, 0, st>>>(M, N, (int)K, A, lda, B, ldb,  \
                                                                       a_rows, amax_b, bias, act, C, \
@@ -2711,8 +2763,20 @@ int smallk_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, 
   switch (ks) {                             \
     case 1: MVML_SK(1, IL, NTV); break;     \
     case 2: MVML_SK(2, IL, NTV); break;     \
+    case 3: MVML_SK(3, IL, NTV); break;     \
     case 4: MVML_SK(4, IL, NTV); break;     \
+    case 5: MVML_SK(5, IL, NTV); break;     \
     default: MVML_SK(6, IL, NTV); break;    \
+  }
+  const int opt = option(MVML_OPT_SMALLK);
+  if ((opt == 5 || opt == 6) && ks == 5 && il4) {
+    if (opt == 5)
+      gemm_smallk_kernel<5, true, true, 1><<<(unsigned)blocks, 256, 0, st>>>(
+          M, N, (int)K, A, lda, B, ldb, a_rows, amax_b, bias, act, C, ldc, n_slabs, (int)cb);
+    else
+      gemm_smallk_kernel<5, true, true, 2><<<(unsigned)blocks, 256, 0, st>>>(
+          M, N, (int)K, A, lda, B, ldb, a_rows, amax_b, bias, act, C, ldc, n_slabs, (int)cb);
+    return check_launch("gemm_smallk_kernel(ablation)");
   }
   if (il4) {
     if (nt) { MVML_SK_KS(true, true) } else { MVML_SK_KS(true, false) }

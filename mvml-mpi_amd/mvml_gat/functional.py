@@ -191,7 +191,10 @@ def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.
     K-contiguous A): per-row |A| max bits (int32 [M]) — every A row gets its own scale
     (mvml_gemm_f16x2_rows); amax then only needs B's pointer.  bil4: B's interleaved split
     image (split_il4, made with amax[1])."""
-    _lib.call_tag[0] = {"flops": 2 * M * N * K, "shape": (M, N, K, int(a_kmajor), int(b_kmajor))}
+    # bytes: what the product must move at least (A, B and C once) — the small-K products
+    # (layer 1's projection) are reported against HBM with it (bench.py roofline_proj_l1)
+    _lib.call_tag[0] = {"flops": 2 * M * N * K, "shape": (M, N, K, int(a_kmajor), int(b_kmajor)),
+                        "bytes": 4 * (M * N + M * K + N * K)}
     L = _lib.lib()
     dev = C.device
     wsz = L.mvml_gemm_workspace_size(M, N, K)

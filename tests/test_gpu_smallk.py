@@ -112,3 +112,22 @@ def test_smallk_pitch_bias_relu():
     assert float(d.max()) < TOL
     C0 = _run(A, B, M, N, K, bias=bias, act=1, ldc=ldc, smallk=0).cpu()
     assert float(((C[:, :N] - C0[:, :N]).abs().max(1).values.double() / den).max()) < 2e-6
+
+
+@pytest.mark.parametrize("shape", [(4099, 1544, 76), (1000, 68, 76), (77, 100, 44), (300, 60, 80), (40, 12, 16)])
+def test_smallk_zero_low_plane(shape):
+    """0 / 1 rows (layer 1's atom features: fp16-exact, so the low plane is zero and the kernel
+    skips the h_b l_a products for the block) mixed with random rows in some 16-row blocks:
+    every row within 1e-5 of float64 and agreeing with the tile path."""
+    M, N, K = shape
+    g = torch.Generator().manual_seed(21 + K)
+    A = (torch.rand(M, K, generator=g) < 0.15).float()
+    mixed = torch.arange(M) % 97 == 5  # a few random rows: their blocks take the full product
+    A[mixed] = torch.randn(int(mixed.sum()), K, generator=g)
+    B = torch.randn(N, K, generator=g).float()
+    ref = A.double() @ B.double().t()
+    C = _run(A, B, M, N, K).double().cpu()
+    den = ref.abs().max(1).values.clamp_min(1e-30)
+    assert float(((C - ref).abs().max(1).values / den).max()) < TOL
+    C0 = _run(A, B, M, N, K, smallk=0).double().cpu()
+    assert float(((C - C0).abs().max(1).values / den).max()) < 2e-6

@@ -1,6 +1,9 @@
 """Layer-1 projection on the config-3 shape (M = atoms of a 65,536-molecule batch, N = 1544 Wcat
-rows, K = 76): the small-K memory kernel (option smallk 1 = non-temporal stores, 2 = plain) against
-the 256x256 tile (smallk 0), interleaved in one process; HIP events on torch's current stream.
+rows, K = 76): the small-K memory kernel (option smallk 1 = non-temporal stores, the default;
+2 = plain stores; 3 / 4 = 8 / 128 row blocks per wave instead of 32; 5 / 6 = timing ablations
+without the MFMAs / without the C stores — wrong results) against the 256x256 tile (smallk 0),
+interleaved in one process; HIP events on torch's current stream.  Default X: 0/1 values like
+the atom features (the kernel skips the products of A's zero low plane); --random: Gaussian.
 Algorithmic bytes: read X, its row maxima and the il4 weight image once, write Y once.
 
     python tools/smallk_bench.py [--m 1753156] [--n 1544] [--k 76] [--iters 10]
@@ -23,12 +26,14 @@ def main():
     ap.add_argument("--n", type=int, default=1544)
     ap.add_argument("--k", type=int, default=76)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--kinds", default="1,2,0")
+    ap.add_argument("--kinds", default="1,2,3,4,5,6,0")
+    ap.add_argument("--random", action="store_true")
     a = ap.parse_args()
     M, N, K = a.m, a.n, a.k
     dev = "cuda"
     st = stream_ptr()
-    X = torch.randn(M, K, device=dev)
+    # 0 / 1 values like the atom features (--random: Gaussian rows, no zero low plane)
+    X = torch.randn(M, K, device=dev) if a.random else (torch.rand(M, K, device=dev) < 0.15).float()
     W = torch.randn(N, K, device=dev) * 0.05
     ldc = _row_pitch(N)
     Y = torch.empty(M, ldc, device=dev)
@@ -51,7 +56,7 @@ def main():
         run(kd)
         torch.cuda.synchronize()
         outs[kd] = Y[:, :N].clone()
-    ref = outs[kinds[-1]].double()
+    ref = outs[0 if 0 in outs else kinds[-1]].double()
     times = {kd: [] for kd in kinds}
     for _ in range(a.iters):
         for kd in kinds:
