@@ -84,9 +84,6 @@ const char* mvml_version(void);
                                    with the edge softmax as its own launch first */
 #define MVML_OPT_DST_UNR 10     /* MVML_DST_UNR: projection rows in flight per wave of the
                                    destination-wave forward (0 = the default per width; tuning) */
-#define MVML_OPT_DST_PARTS 12   /* MVML_DST_PARTS: P > 1 = the destination-wave forward as P
-                                   launches over 1 / P of the columns each (smaller L2 working
-                                   set on large molecules; bitwise the same outputs); 1 default */
 #define MVML_OPT_SMALLK 11      /* MVML_SMALLK: 1 (default) mvml_gemm_f16x2_rows products with
                                    K <= 96 (layer 1's projection) on the wave-per-64-columns
                                    memory kernel (non-temporal stores; 2 = plain stores;

@@ -56,7 +56,7 @@ unsigned resident_blocks(const void* kernel, int threads, int64_t need) {
 }
 
 // Kernel-path options (include/mvml_gat.h, MVML_OPT_*): environment defaults read once at load.
-constexpr int kOptCount = 13;
+constexpr int kOptCount = 12;
 static std::atomic<int> g_opt[kOptCount];
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
@@ -75,7 +75,6 @@ static const bool g_opt_init = [] {
   g_opt[MVML_OPT_DST_FWD] = env_int("MVML_DST_FWD", 0);
   g_opt[MVML_OPT_DST_UNR] = env_int("MVML_DST_UNR", 0);
   g_opt[MVML_OPT_SMALLK] = env_int("MVML_SMALLK", 1);
-  g_opt[MVML_OPT_DST_PARTS] = env_int("MVML_DST_PARTS", 1);
   return true;
 }();
 

@@ -891,10 +891,7 @@ gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
                        const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ bias,
                        const float* __restrict__ elr, float slope, float* __restrict__ attn,
                        float* __restrict__ out, uint32_t* __restrict__ out_amax,
-                       uint32_t* __restrict__ out_rows, int p_off = 0, int p_w = 1 << 30,
-                       int rows_acc = 0) {
-  // column part (launch_fwd's dst_parts): float4 columns [p_off, p_off + p_w) of each head
-  // (mean) or of the row (flatten); rows_acc: fold this part's row maxima into out_rows
+                       uint32_t* __restrict__ out_rows) {
   constexpr bool PAIR = MODE == 1 && H >= 2;
   constexpr int NH = PAIR ? H / 2 : 1;  // heads per lane (mean mode); 1 register set (flatten)
   const int lane = threadIdx.x & 63;
@@ -915,15 +912,15 @@ gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       if constexpr (MODE == 1) {
-        const int q = ql + (PAIR ? 32 : 64) * j + p_off;
-        ok[j] = 4 * q < F && q - p_off < p_w;
+        const int q = ql + (PAIR ? 32 : 64) * j;
+        ok[j] = 4 * q < F;
         hc[j] = 0;
         cz[j] = hp * NH * F + 4 * q;
         // the residual first (its HBM latency overlaps the softmax); the lower half stores out
         res[j] = (ok[j] && hp == 0) ? ld4nt(yv + HF + 4 * q) : f4(0.f);
       } else {
-        const int c = lane + 64 * j + p_off;
-        ok[j] = 4 * c < HF && c - p_off < p_w;
+        const int c = lane + 64 * j;
+        ok[j] = 4 * c < HF;
         hc[j] = ok[j] ? 4 * c / F : 0;
         cz[j] = 4 * c;
         res[j] = ok[j] ? ld4nt(yv + HF + 4 * c) : f4(0.f);
@@ -1049,7 +1046,7 @@ gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
     for (int j = 0; j < NJ; ++j) {
       float4 o;
       if constexpr (MODE == 1) {  // head mean: heads summed in order (+ bias per head), / H, + R
-        const int q = ql + (PAIR ? 32 : 64) * j + p_off;
+        const int q = ql + (PAIR ? 32 : 64) * j;
         const int qc = ok[j] ? 4 * q : 0;
         float4 t[NH];
 #pragma unroll
@@ -1078,7 +1075,7 @@ gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
     }
     const float wm = wave_max(rmx);
     omx = fmaxf(omx, wm);
-    if (out_rows && lane == 0) out_rows[v] = rows_acc ? max(out_rows[v], __float_as_uint(wm)) : __float_as_uint(wm);
+    if (out_rows && lane == 0) out_rows[v] = __float_as_uint(wm);
   }
   if (out_amax) block_amax_commit<256>(omx, out_amax);
 }
@@ -2263,33 +2260,21 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
       int rc = check_launch("gat_softmax_dst_kernel");
       if (rc) return rc;
     }
-    // column parts (MVML_OPT_DST_PARTS = P > 1): P launches, each over every atom but 1 / P of
-    // the columns (mean: of every head), so an XCD's working set of projection rows shrinks P
-    // times (config 5's molecules: ~1 MB of rows per molecule against a 4 MB L2).  Part 0 forms
-    // the softmax (and attn), the others read attn; the arithmetic per column is unchanged, so
-    // the outputs are bitwise the one-launch ones.
-    const int wq = mode == 1 ? F / 4 : HF / 4;  // float4 columns per head (mean) / per row
-    const int parts = std::max(1, std::min(option(MVML_OPT_DST_PARTS), 8));
-    const int pw = (int)ceil_div(wq, parts);
-    int p_off = 0, rows_acc = 0;
-    bool sm_p = sm;
 #define MVML_DST_FWD(M, NJ, U)                                                                    \
   do {                                                                                            \
-    if (sm_p)                                                                                     \
+    if (sm)                                                                                       \
       gat_agg_fwd_dst_kernel<H, M, NJ, U, true>                                                   \
           <<<b4, 256, 0, st>>>(   \
-              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows, p_off, pw, rows_acc); \
+              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);             \
     else                                                                                          \
       gat_agg_fwd_dst_kernel<H, M, NJ, U, false>                                                  \
           <<<b4, 256, 0, st>>>(  \
-              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows, p_off, pw, rows_acc); \
+              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);             \
   } while (0)
     // rows in flight per wave (MVML_OPT_DST_UNR, H = 4 at the GAT widths: tuning A/B)
     const int unr = option(MVML_OPT_DST_UNR);
-    for (int part = 0; part < parts; ++part, p_off += pw, rows_acc = 1, sm_p = false) {
-    if (p_off >= wq) break;
     if (mode == 1) {  // mean: half-waves over the heads, lanes over F / 4
-      const int nj = (int)ceil_div(pw, H >= 2 ? 32 : 64);
+      const int nj = (int)ceil_div(F / 4, H >= 2 ? 32 : 64);
       if (nj == 1) MVML_DST_FWD(1, 1, 4);
       else if (nj == 2) MVML_DST_FWD(1, 2, 2);
       else if (nj == 3 && H == 4 && unr == 2) MVML_DST_FWD(1, 3, 2);
@@ -2298,7 +2283,7 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
       else if (nj <= 4) MVML_DST_FWD(1, 4, 2);
       else { set_error("gat_agg_fwd: dst path needs F <= %d in mean mode", H >= 2 ? 512 : 1024); return MVML_ERR_INVALID; }
     } else {
-      const int nj = (int)ceil_div(pw, 64);
+      const int nj = (int)ceil_div(HF / 4, 64);
 #define MVML_DST_FWD_F(NJ, U) do { if (mode == 0) MVML_DST_FWD(0, NJ, U); else MVML_DST_FWD(2, NJ, U); } while (0)
       if (nj == 1) MVML_DST_FWD_F(1, 4);
       else if (nj == 2) MVML_DST_FWD_F(2, 4);
@@ -2309,10 +2294,9 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
       else MVML_DST_FWD_F(8, 2);
 #undef MVML_DST_FWD_F
     }
+#undef MVML_DST_FWD
     int rc = check_launch("gat_agg_fwd_dst_kernel");
     if (rc) return rc;
-    }
-#undef MVML_DST_FWD
     return launch_rows_amax(N, out_rows, out_amax, st);
   }
   if (G == 0) return MVML_OK;

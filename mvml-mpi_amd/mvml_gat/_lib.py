@@ -151,7 +151,7 @@ def call(name, *args):
 # C ABI; the environment variables only seed the defaults when the library loads.
 OPTIONS = {"big_window": 0, "bwd_atomwise": 1, "gemm_tile": 2, "gemm_persist": 3, "gemm_nsplit": 4,
            "gemm_ring": 5, "lstm_tile": 6, "mean_src": 7, "flat_src": 8, "dst_fwd": 9,
-           "dst_unr": 10, "smallk": 11, "dst_parts": 12}
+           "dst_unr": 10, "smallk": 11}
 
 
 class option:

@@ -453,21 +453,3 @@ def _gy_max_case(layer, sb):
     got_o = t[i:i + 1].cpu().view(torch.float32).item()
     assert got_o == out.detach().abs().max().item(), (got_o, out.detach().abs().max().item())
     return cap
-
-
-@pytest.mark.parametrize("case", ["config5", "hubs", "config3"])
-@pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("parts", [2, 3])
-def test_dst_fwd_column_parts_bitwise(case, mode, parts):
-    """The destination-wave forward as `parts` launches over a slice of the columns each
-    (option dst_parts; part 0 forms the softmax, the rest read attn): out, attn, max |out| and
-    the per-row maxima BITWISE equal to the one-launch forward, fused and split softmax."""
-    sb = _FAMILIES[case]()
-    F = 192 if mode == 0 else 384
-    for kind in (1, 2):
-        with option("dst_fwd", kind), option("dst_parts", 1):
-            a = _agg_outputs(sb, 4, F, mode)
-        with option("dst_fwd", kind), option("dst_parts", parts):
-            b = _agg_outputs(sb, 4, F, mode)
-        for i in (0, 1, 3, 4):
-            assert torch.equal(a[i], b[i]), (kind, i, (a[i].double() - b[i].double()).abs().max().item())
