@@ -566,13 +566,14 @@ def run(args):
             extra["roofline_agg_bwd"] = roofline_entry(summ["mvml_gat_agg_bwd"], "hbm",
                                                        load_traffic(wkey, "gat_agg_bwd"))
         proj_ev = summ.get("mvml_gat_proj_fwd", [])
-        # the small-K per-row products (K <= 96: layer 1's projection on the wave-per-64-column
-        # memory kernel, gemm_smallk_kernel) are an HBM roofline of their own, not MFMA work
+        # the GAT projection at small K (K <= 96: layer 1's, on the wave-per-64-column memory
+        # kernel gemm_smallk_kernel) is an HBM roofline of its own, not MFMA work
         rows_ev = summ.get("mvml_gemm_f16x2_rows", [])
-        sk_ev = [e for e in rows_ev if (e[1] or {}).get("shape", (0, 0, 1 << 30))[2] <= SMALLK_MAX_K]
+        sk_ev = [e for e in rows_ev if (e[1] or {}).get("role") == "gat_proj"
+                 and e[1].get("shape", (0, 0, 1 << 30))[2] <= SMALLK_MAX_K]
         rows_ev = [e for e in rows_ev if e not in sk_ev]
         if sk_ev:
-            extra["roofline_proj_l1"] = roofline_entry(sk_ev, "hbm")
+            extra["roofline_proj_l1"] = roofline_entry(sk_ev, "hbm", load_traffic(wkey, "gemm_smallk"))
             extra["roofline_proj_l1"]["kernel"] = (
                 "mvml_gemm_f16x2_rows at K <= 96 (layer-1 projection X[N, 76] Wcat[1544, 76]^T, "
                 "gemm_smallk_kernel); bytes = A, B and C once")

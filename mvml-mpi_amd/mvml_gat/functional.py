@@ -184,7 +184,7 @@ def split_planes(W, rows, cols, ld, amax_ptr):
 
 
 def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0, algo=None,
-         amax=None, bsplit=None, arows=None, bil4=None):
+         amax=None, bsplit=None, arows=None, bil4=None, role=None):
     """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32 / mvml_gemm_f32x3 /
     mvml_gemm_f16x2).  amax = (pointer to |A| max bits, pointer to |B| max bits) from absmax()
     lets split-fp16 products that share an operand share its max pass.  arows (split-fp16,
@@ -194,7 +194,7 @@ def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.
     # bytes: what the product must move at least (A, B and C once) — the small-K products
     # (layer 1's projection) are reported against HBM with it (bench.py roofline_proj_l1)
     _lib.call_tag[0] = {"flops": 2 * M * N * K, "shape": (M, N, K, int(a_kmajor), int(b_kmajor)),
-                        "bytes": 4 * (M * N + M * K + N * K)}
+                        "bytes": 4 * (M * N + M * K + N * K), "role": role}
     L = _lib.lib()
     dev = C.device
     wsz = L.mvml_gemm_workspace_size(M, N, K)
@@ -402,7 +402,7 @@ class GATLayerFunction(torch.autograd.Function):
             Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
             if xr is not None:
                 gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(None, slot(amx, 1)),
-                     arows=xr, bil4=wil)
+                     arows=xr, bil4=wil, role="gat_proj")
             elif amx is not None:
                 gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(slot(*ax), slot(amx, 1)),
                      bsplit=None if wps[0] is None else wps)

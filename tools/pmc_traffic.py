@@ -22,19 +22,26 @@ from collections import defaultdict
 ENTRIES = {  # C-ABI entry point -> its kernels (name substrings; "[big]": the big-window
     # instantiation, template argument BIG = true, launched beside the molecule-window one)
     "gat_agg_fwd": ["gat_softmax_kernel", "gat_agg_fwd_lds_kernel", "gat_agg_fwd_lds_kernel[big]",
-                    "gat_agg_fwd_gather_kernel"],
+                    "gat_agg_fwd_gather_kernel",
+                    # round 5: the destination-wave forward (and its split-softmax launch)
+                    "gat_agg_fwd_dst_kernel", "gat_softmax_dst4_kernel", "gat_softmax_dst_kernel"],
     "gat_agg_bwd": ["gat_agg_bwd_lds_kernel", "gat_agg_bwd_lds_kernel[big]", "gat_agg_bwd_dst_kernel",
                     "gat_agg_bwd_src_kernel", "gat_mean_bwd_src_kernel", "gat_mean_bwd_softmax_kernel",
-                    "gat_mean_bwd_gel_kernel"],
+                    "gat_mean_bwd_gel_kernel",
+                    # round 5: the flatten layer's one-pass source-atom backward
+                    "gat_flat_bwd_src1_kernel"],
     "set2set_seg_fwd": ["seg_fwd_kernel"],
+    # round 5: the small-K GAT projection (layer 1)
+    "gemm_smallk": ["gemm_smallk_kernel"],
 }
 # kernels launched exactly once per entry-point call, whichever path the call takes (a call of
 # mvml_gat_agg_bwd launches the molecule-window kernel, or — head-mean layer by source atom —
 # gat_mean_bwd_src_kernel instead): the per-launch traffic is the entry's kernels' total over
 # the number of calls, so layers on different kernel paths average correctly
-ANCHORS = {"gat_agg_fwd": ["gat_agg_fwd_lds_kernel"],
-           "gat_agg_bwd": ["gat_agg_bwd_lds_kernel", "gat_mean_bwd_src_kernel"],
-           "set2set_seg_fwd": ["seg_fwd_kernel"]}
+ANCHORS = {"gat_agg_fwd": ["gat_agg_fwd_lds_kernel", "gat_agg_fwd_dst_kernel"],
+           "gat_agg_bwd": ["gat_agg_bwd_lds_kernel", "gat_mean_bwd_src_kernel", "gat_flat_bwd_src1_kernel"],
+           "set2set_seg_fwd": ["seg_fwd_kernel"],
+           "gemm_smallk": ["gemm_smallk_kernel"]}
 
 
 def _pattern(name, pat):
