@@ -87,7 +87,7 @@ const char* mvml_version(void);
 #define MVML_OPT_SMALLK 11      /* MVML_SMALLK: 1 (default) mvml_gemm_f16x2_rows products with
                                    K <= 96 (layer 1's projection) on the wave-per-64-columns
                                    memory kernel (non-temporal stores; 2 = plain stores;
-                                   3 .. 6: timing variants, tools/smallk_bench.py);
+                                   3 .. 6, 10: timing variants, tools/smallk_bench.py);
                                    0 = the 256x256 tile */
 int mvml_set_option(int option, int value);
 int mvml_get_option(int option);

@@ -2527,8 +2527,13 @@ constexpr int kSkMaxK = 96;
 // h_b l_a products — per 16-row block, wave-uniform (a ballot); adding exact zeros is all they
 // would do.
 // ABL (timing ablations, option smallk 5 / 6; wrong results): 1 = no MFMAs, 2 = no C stores
-template <int KS16, bool IL4, bool NT, int ABL = 0, int NG = 4>
-__global__ void __launch_bounds__(256, 2)  // two waves per SIMD: <= 256 registers per lane
+// WL (default): the workgroup's four waves share ONE 64-column slab (four consecutive row
+// chunks) and its B planes live in LDS (filled once, one group per wave), read per block as
+// fragments — no B registers (162 VGPRs instead of 230), so three waves fit per SIMD and the
+// store stream overlaps more matrix work: 3.26 -> 2.75 ms at config 3 on one box.  WL = false
+// (B fragments in registers, every wave its own slab) stays as option smallk 10.
+template <int KS16, bool IL4, bool NT, int ABL = 0, int NG = 4, bool WL = false>
+__global__ void __launch_bounds__(256, WL ? 3 : 2)  // two (three) waves per SIMD
 gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int64_t lda,
                    const float* __restrict__ B, int64_t ldb, const uint32_t* __restrict__ a_rows,
                    const uint32_t* __restrict__ amax_b, const float* __restrict__ bias, int act,
@@ -2537,18 +2542,23 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
   constexpr int NX = 2 * N32 + T16;  // A float4 per lane and row block
   constexpr int SW = 16 * NG, PITCH = SW + 4;  // slab width (columns per wave); LDS row pitch
   const int lane = threadIdx.x & 63, li = lane & 15, lq = lane >> 4;
-  const int64_t w = xcd_block(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int slab = (int)(w % n_slabs);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+  const int64_t w = lb * 4 + wid;
+  const int slab = (int)(WL ? lb % n_slabs : w % n_slabs);
   const int64_t nrb = (M + 15) >> 4;
-  const int64_t rb0 = (w / n_slabs) * chunk_blocks;
-  if (rb0 >= nrb) return;
+  const int64_t rb0 = (WL ? (lb / n_slabs) * 4 + wid : w / n_slabs) * chunk_blocks;
+  if (!WL && rb0 >= nrb) return;
   const int64_t rb1 = min(nrb, rb0 + (int64_t)chunk_blocks);
   const int kb = amax_shift(*amax_b);
   const float s_b = pow2f(kb), u_b = pow2f(-kb);
   // this lane's B rows (output columns c0 + 16 g + li) for the MFMA's A side: k = 32 s + 8 lq
   // + 0..7 (x32 steps), 32 N32 + 4 lq + 0..3 (x16 tail); k >= K reads as zero
-  f16x8 bh[NG][NW], bl[NG][NW];
-  f16x4 th[NG], tl[NG];
+  constexpr int RG = WL ? 1 : NG;  // register copies of the B fragments (WL: none)
+  f16x8 bh[RG][NW], bl[RG][NW];
+  f16x4 th[RG], tl[RG];
+  __shared__ u32x4 s_wh[WL ? NG : 1][WL ? NW : 1][WL ? 64 : 1], s_wl[WL ? NG : 1][WL ? NW : 1][WL ? 64 : 1];
+  __shared__ uint2 s_th[WL ? NG : 1][WL ? 64 : 1], s_tl[WL ? NG : 1][WL ? 64 : 1];
   auto piece = [&](const float* row, int k, uint2& h, uint2& l) {  // B[row][k .. k + 3] as planes
     const float4 v = *reinterpret_cast<const float4*>(row + min(k, K - 4));
     if constexpr (IL4) {
@@ -2559,6 +2569,28 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
     }
     if (k >= K) h = l = make_uint2(0u, 0u);
   };
+  if constexpr (WL) {  // wave wid fills group wid's planes (NG == 4 waves), then one barrier
+    static_assert(NG == 4, "one group per wave");
+    const int g = wid;
+    const int64_t col = (int64_t)slab * SW + 16 * g + li;
+    const float* row = B + min(col, N - 1) * ldb;
+#pragma unroll
+    for (int s = 0; s < N32; ++s) {
+      uint2 h0, l0, h1, l1;
+      piece(row, 32 * s + 8 * lq, h0, l0);
+      piece(row, 32 * s + 8 * lq + 4, h1, l1);
+      s_wh[g][s][lane] = u32x4{h0.x, h0.y, h1.x, h1.y};
+      s_wl[g][s][lane] = u32x4{l0.x, l0.y, l1.x, l1.y};
+    }
+    if constexpr (T16) {
+      uint2 h, l;
+      piece(row, 32 * N32 + 4 * lq, h, l);
+      s_th[g][lane] = h;
+      s_tl[g][lane] = l;
+    }
+    __syncthreads();
+    if (rb0 >= nrb) return;
+  } else {
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int64_t col = (int64_t)slab * SW + 16 * g + li;
@@ -2579,6 +2611,20 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
       tl[g] = __builtin_bit_cast(f16x4, l);
     }
   }
+  }
+  // the B fragments of group g (registers, or the LDS image)
+  auto fbh = [&](int g, int s) -> f16x8 {
+    if constexpr (WL) return __builtin_bit_cast(f16x8, s_wh[g][s][lane]); else return bh[g][s];
+  };
+  auto fbl = [&](int g, int s) -> f16x8 {
+    if constexpr (WL) return __builtin_bit_cast(f16x8, s_wl[g][s][lane]); else return bl[g][s];
+  };
+  auto fth = [&](int g) -> f16x4 {
+    if constexpr (WL) return __builtin_bit_cast(f16x4, s_th[g][lane]); else return th[g];
+  };
+  auto ftl = [&](int g) -> f16x4 {
+    if constexpr (WL) return __builtin_bit_cast(f16x4, s_tl[g][lane]); else return tl[g];
+  };
   float bv[NG][4];
 #pragma unroll
   for (int g = 0; g < NG; ++g)
@@ -2651,16 +2697,17 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
         if constexpr (ABL == 1) {
 #pragma unroll
           for (int s = 0; s < N32; ++s) {
-            acc[g][0] += (float)ah[s][g] * (float)bh[g][s][0];
-            acc[g][1] += (float)al[s][g] * (float)bl[g][s][1];
+            acc[g][0] += (float)ah[s][g] * (float)fbh(g, s)[0];
+            acc[g][1] += (float)al[s][g] * (float)fbl(g, s)[1];
           }
           continue;
         }
 #pragma unroll
         for (int s = 0; s < N32; ++s) {
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[g][s], ah[s], acc[g], 0, 0, 0);
-          if constexpr (kLo) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[g][s], al[s], acc[g], 0, 0, 0);
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[g][s], ah[s], acc[g], 0, 0, 0);
+          const f16x8 bhv = fbh(g, s), blv = fbl(g, s);
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(blv, ah[s], acc[g], 0, 0, 0);
+          if constexpr (kLo) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bhv, al[s], acc[g], 0, 0, 0);
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bhv, ah[s], acc[g], 0, 0, 0);
         }
       }
       if constexpr (T16 && ABL != 1) {
@@ -2668,9 +2715,10 @@ gemm_smallk_kernel(int64_t M, int64_t N, int K, const float* __restrict__ A, int
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
           tac[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-          tac[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(tl[g], ath, tac[g], 0, 0, 0);
-          if constexpr (kLo) tac[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[g], atl, tac[g], 0, 0, 0);
-          tac[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[g], ath, tac[g], 0, 0, 0);
+          const f16x4 thv = fth(g), tlv = ftl(g);
+          tac[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(tlv, ath, tac[g], 0, 0, 0);
+          if constexpr (kLo) tac[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(thv, atl, tac[g], 0, 0, 0);
+          tac[g] = __builtin_amdgcn_mfma_f32_16x16x16f16(thv, ath, tac[g], 0, 0, 0);
         }
 #pragma unroll
         for (int g = 0; g < NG; ++g) acc[g] = N32 > 0 ? acc[g] + tac[g] : tac[g];
@@ -2755,10 +2803,11 @@ int smallk_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, 
   }
   const bool nt = option(MVML_OPT_SMALLK) != 2;  // (3 .. 6: timing variants)
   const int ks = (int)ceil_div(K, 16);  // 1 .. 6: the k-step plans above
+  // WL: a workgroup = four row chunks of one slab
+  const int64_t wl_blocks = ceil_div(ceil_div(nrb, cb), 4) * n_slabs;
 #define MVML_SK(KS, IL, NTV)                                                                      \
-  gemm_smallk_kernel<KS, IL, NTV><<<(unsigned)blocks, 256, 0, st>>>(M, N, (int)K, A, lda, B, ldb,  \
-                                                                      a_rows, amax_b, bias, act, C, \
-                                                                      ldc, n_slabs, (int)cb)
+  gemm_smallk_kernel<KS, IL, NTV, 0, 4, true><<<(unsigned)wl_blocks, 256, 0, st>>>(              \
+      M, N, (int)K, A, lda, B, ldb, a_rows, amax_b, bias, act, C, ldc, n_slabs, (int)cb)
 #define MVML_SK_KS(IL, NTV)                 \
   switch (ks) {                             \
     case 1: MVML_SK(1, IL, NTV); break;     \
@@ -2769,12 +2818,17 @@ int smallk_launch(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, 
     default: MVML_SK(6, IL, NTV); break;    \
   }
   const int opt = option(MVML_OPT_SMALLK);
+  if (opt == 10 && ks == 5 && il4) {  // (10: B fragments in registers — the round-5 first build)
+    gemm_smallk_kernel<5, true, true, 0, 4, false><<<(unsigned)blocks, 256, 0, st>>>(
+        M, N, (int)K, A, lda, B, ldb, a_rows, amax_b, bias, act, C, ldc, n_slabs, (int)cb);
+    return check_launch("gemm_smallk_kernel(B in registers)");
+  }
   if ((opt == 5 || opt == 6) && ks == 5 && il4) {
     if (opt == 5)
-      gemm_smallk_kernel<5, true, true, 1><<<(unsigned)blocks, 256, 0, st>>>(
+      gemm_smallk_kernel<5, true, true, 1, 4, true><<<(unsigned)wl_blocks, 256, 0, st>>>(
           M, N, (int)K, A, lda, B, ldb, a_rows, amax_b, bias, act, C, ldc, n_slabs, (int)cb);
     else
-      gemm_smallk_kernel<5, true, true, 2><<<(unsigned)blocks, 256, 0, st>>>(
+      gemm_smallk_kernel<5, true, true, 2, 4, true><<<(unsigned)wl_blocks, 256, 0, st>>>(
           M, N, (int)K, A, lda, B, ldb, a_rows, amax_b, bias, act, C, ldc, n_slabs, (int)cb);
     return check_launch("gemm_smallk_kernel(ablation)");
   }

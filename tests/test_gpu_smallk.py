@@ -131,3 +131,12 @@ def test_smallk_zero_low_plane(shape):
     assert float(((C - ref).abs().max(1).values / den).max()) < TOL
     C0 = _run(A, B, M, N, K, smallk=0).double().cpu()
     assert float(((C - C0).abs().max(1).values / den).max()) < 2e-6
+
+
+@pytest.mark.parametrize("shape", [(4099, 1544, 76), (1000, 68, 76), (40, 12, 76)])
+def test_smallk_b_in_lds_bitwise(shape):
+    """The default kernel (B planes in LDS, a workgroup per slab) against the register-B build
+    (option smallk 10): the same fragments and products, so bitwise equal outputs."""
+    M, N, K = shape
+    A, B = _inputs(M, N, K, 17)
+    assert torch.equal(_run(A, B, M, N, K, smallk=1), _run(A, B, M, N, K, smallk=10))

@@ -1,9 +1,6 @@
 #!/bin/bash
-# PMC traffic (FETCH_SIZE / WRITE_SIZE passes) of the config-3 and config-5 bench batches
 set -o pipefail
 cd "$(dirname "$0")/.."
-WORKLOAD=config3 bash tools/pmc_bench.sh pmc3 > gpurun_out/pmc3.txt 2>&1 || { tail -30 gpurun_out/pmc3.txt; exit 1; }
-cp gpurun_out/pmc3/pmc_traffic.json profiles/pmc_traffic.json
-WORKLOAD=config5 bash tools/pmc_bench.sh pmc5 > gpurun_out/pmc5.txt 2>&1 || { tail -30 gpurun_out/pmc5.txt; exit 1; }
-cp gpurun_out/pmc5/pmc_traffic.json gpurun_out/pmc_traffic_new.json
-tail -40 gpurun_out/pmc5.txt
+tools/gpu_r5.sh tests sk tests/test_gpu_smallk.py tests/test_gpu_rows.py tests/test_gpu_parity.py -k "smallk or il4 or shard or gnn or gat" || exit 1
+timeout -k 10 300 python -u tools/smallk_bench.py > gpurun_out/smallk_bench.txt 2>&1; rc=$?; cat gpurun_out/smallk_bench.txt; [ $rc = 0 ] || exit $rc
+tools/gpu_r5.sh bench c3g --steps 16 --warmup 2 --no-cpu-baseline --no-inference
