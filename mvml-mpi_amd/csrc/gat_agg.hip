@@ -885,8 +885,10 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
 // columns q = (l & 31) + 32 k (k < NJ, 4q < F) of its half's heads (6 slots per lane at
 // H = 4, F = 384, no idle lane), and the halves meet by a cross-half shuffle for the head sum,
 // added in head order (bitwise the LDS kernel's head mean).  H = 1 mean: q = l + 64 k.
-template <int H, int MODE, int NJ, int U, bool SM>
-__global__ void __launch_bounds__(256)
+// LR (late residual): the residual row is loaded after the gather instead of before the softmax
+// (12 fewer VGPRs live across the gather loop in mean mode: five waves per SIMD instead of four)
+template <int H, int MODE, int NJ, int U, bool SM, bool LR = false>
+__global__ void __launch_bounds__(256, LR ? 5 : 1)
 gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
                        const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ bias,
                        const float* __restrict__ elr, float slope, float* __restrict__ attn,
@@ -917,7 +919,7 @@ gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
         hc[j] = 0;
         cz[j] = hp * NH * F + 4 * q;
         // the residual first (its HBM latency overlaps the softmax); the lower half stores out
-        res[j] = (ok[j] && hp == 0) ? ld4nt(yv + HF + 4 * q) : f4(0.f);
+        if constexpr (!LR) res[j] = (ok[j] && hp == 0) ? ld4nt(yv + HF + 4 * q) : f4(0.f);
       } else {
         const int c = lane + 64 * j;
         ok[j] = 4 * c < HF;
@@ -1042,6 +1044,13 @@ gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
       }
     }
     float rmx = 0.f;
+    if constexpr (LR && MODE == 1) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int q = ql + (PAIR ? 32 : 64) * j;
+        res[j] = (ok[j] && hp == 0) ? ld4nt(yv + HF + 4 * q) : f4(0.f);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       float4 o;
@@ -2279,6 +2288,18 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
       else if (nj == 2) MVML_DST_FWD(1, 2, 2);
       else if (nj == 3 && H == 4 && unr == 2) MVML_DST_FWD(1, 3, 2);
       else if (nj == 3 && H == 4 && unr == 3) MVML_DST_FWD(1, 3, 3);
+      else if (nj == 3 && unr == 6) MVML_DST_FWD(1, 3, 1);  // (6: the residual loaded first)
+      else if (nj == 3 && H == 4) {
+        // one row in flight, the residual loaded after the gather: 90 VGPRs, five waves per SIMD
+        // (residual first: 104, four) — config 5 layer 2 6.35 -> 6.08 ms, config 3 3.66 -> 3.60
+        // (profiles/r05_agg_late_residual_config*.txt)
+        if (sm)
+          gat_agg_fwd_dst_kernel<H, 1, 3, 1, true, true><<<b4, 256, 0, st>>>(
+              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);
+        else
+          gat_agg_fwd_dst_kernel<H, 1, 3, 1, false, true><<<b4, 256, 0, st>>>(
+              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);
+      }
       else if (nj == 3) MVML_DST_FWD(1, 3, 1);  // one row in flight: fewest registers, most waves
       else if (nj <= 4) MVML_DST_FWD(1, 4, 2);
       else { set_error("gat_agg_fwd: dst path needs F <= %d in mean mode", H >= 2 ? 512 : 1024); return MVML_ERR_INVALID; }

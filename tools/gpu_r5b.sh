@@ -1,6 +1,5 @@
 #!/bin/bash
 set -o pipefail
 cd "$(dirname "$0")/.."
-tools/gpu_r5.sh tests sk tests/test_gpu_smallk.py tests/test_gpu_rows.py tests/test_gpu_parity.py -k "smallk or il4 or shard or gnn or gat" || exit 1
-timeout -k 10 300 python -u tools/smallk_bench.py > gpurun_out/smallk_bench.txt 2>&1; rc=$?; cat gpurun_out/smallk_bench.txt; [ $rc = 0 ] || exit $rc
-tools/gpu_r5.sh bench c3g --steps 16 --warmup 2 --no-cpu-baseline --no-inference
+tools/gpu_r5.sh agg c5lr --config 5 --mols 8192 --layers 1 --no-bwd --ab "dst_fwd=1;dst_fwd=1,dst_unr=5;dst_fwd=2;dst_fwd=2,dst_unr=5" || exit 1
+tools/gpu_r5.sh agg c3lr --config 3 --mols 65536 --layers 1 --no-bwd --ab "dst_fwd=2;dst_fwd=2,dst_unr=5;dst_fwd=1;dst_fwd=1,dst_unr=5"
