@@ -887,8 +887,10 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
 // added in head order (bitwise the LDS kernel's head mean).  H = 1 mean: q = l + 64 k.
 // LR (late residual): the residual row is loaded after the gather instead of before the softmax
 // (12 fewer VGPRs live across the gather loop in mean mode: five waves per SIMD instead of four)
+// (measured: the head-mean form held to six waves per SIMD spills 17 VGPRs with the fused softmax
+// and ran 6.1 -> 7.6-8.1 ms on config 5; even without it)
 template <int H, int MODE, int NJ, int U, bool SM, bool LR = false>
-__global__ void __launch_bounds__(256, LR ? 5 : 1)
+__global__ void __launch_bounds__(256, LR ? (MODE == 1 ? 5 : 8) : 1)
 gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ in_src,
                        const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ bias,
                        const float* __restrict__ elr, float slope, float* __restrict__ attn,
@@ -925,7 +927,7 @@ gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
         ok[j] = 4 * c < HF;
         hc[j] = ok[j] ? 4 * c / F : 0;
         cz[j] = 4 * c;
-        res[j] = ok[j] ? ld4nt(yv + HF + 4 * c) : f4(0.f);
+        if constexpr (!LR) res[j] = ok[j] ? ld4nt(yv + HF + 4 * c) : f4(0.f);
       }
 #pragma unroll
       for (int h = 0; h < NH; ++h) acc[h][j] = f4(0.f);
@@ -1044,11 +1046,15 @@ gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
       }
     }
     float rmx = 0.f;
-    if constexpr (LR && MODE == 1) {
+    if constexpr (LR) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int q = ql + (PAIR ? 32 : 64) * j;
-        res[j] = (ok[j] && hp == 0) ? ld4nt(yv + HF + 4 * q) : f4(0.f);
+        if constexpr (MODE == 1) {
+          const int q = ql + (PAIR ? 32 : 64) * j;
+          res[j] = (ok[j] && hp == 0) ? ld4nt(yv + HF + 4 * q) : f4(0.f);
+        } else {
+          res[j] = ok[j] ? ld4nt(yv + HF + 4 * (lane + 64 * j)) : f4(0.f);
+        }
       }
     }
 #pragma unroll
@@ -2310,6 +2316,22 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
       else if (nj == 2) MVML_DST_FWD_F(2, 4);
       else if (nj == 3 && H == 4 && unr == 2) MVML_DST_FWD_F(3, 2);
       else if (nj == 3 && H == 4 && unr == 4) MVML_DST_FWD_F(3, 4);
+      else if (nj == 3 && H == 4 && (unr == 5 || (unr == 0 && sm))) {
+        // late residual (60 VGPRs, eight waves per SIMD instead of six): with the fused softmax
+        // (large molecules) config-5 layer 1 4.90 -> 4.41 ms; the split-softmax form (small
+        // molecules) measured even (profiles/r05_agg_late_residual_flatten_config*.txt)
+#define MVML_DST_FWD_LR(M)                                                                        \
+  do {                                                                                            \
+    if (sm)                                                                                       \
+      gat_agg_fwd_dst_kernel<H, M, 3, 1, true, true><<<b4, 256, 0, st>>>(                         \
+          N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);                 \
+    else                                                                                          \
+      gat_agg_fwd_dst_kernel<H, M, 3, 1, false, true><<<b4, 256, 0, st>>>(                        \
+          N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);                 \
+  } while (0)
+        if (mode == 0) MVML_DST_FWD_LR(0); else MVML_DST_FWD_LR(2);
+#undef MVML_DST_FWD_LR
+      }
       else if (nj == 3) MVML_DST_FWD_F(3, 1);  // fewer rows in flight, more waves: faster
       else if (nj == 4) MVML_DST_FWD_F(4, 2);
       else MVML_DST_FWD_F(8, 2);
