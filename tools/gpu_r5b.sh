@@ -1,5 +1,8 @@
 #!/bin/bash
+# PMC traffic (FETCH_SIZE / WRITE_SIZE passes) of the config-3 and config-5 bench batches
 set -o pipefail
 cd "$(dirname "$0")/.."
-tools/gpu_r5.sh agg c5o6 --config 5 --mols 8192 --layers 1 --no-bwd --ab "dst_fwd=1;dst_fwd=1,dst_unr=7;dst_fwd=1;dst_fwd=1,dst_unr=7" || exit 1
-tools/gpu_r5.sh agg c3o6 --config 3 --mols 65536 --layers 1 --no-bwd --ab "dst_fwd=2;dst_fwd=2,dst_unr=7;dst_fwd=2;dst_fwd=2,dst_unr=7"
+WORKLOAD=config3 bash tools/pmc_bench.sh pmc3 > gpurun_out/pmc3.txt 2>&1 || { tail -30 gpurun_out/pmc3.txt; exit 1; }
+cp gpurun_out/pmc3/pmc_traffic.json profiles/pmc_traffic.json
+WORKLOAD=config5 bash tools/pmc_bench.sh pmc5 > gpurun_out/pmc5.txt 2>&1 || { tail -30 gpurun_out/pmc5.txt; exit 1; }
+cp gpurun_out/pmc5/pmc_traffic.json gpurun_out/pmc_traffic_new.json
