@@ -461,7 +461,10 @@ def run(args):
                                    proj_dtype=torch.bfloat16 if args.proj_bf16 else None).to(dev).train()
         fusion = mvml_gat.MVFusion(384, 12, 11, 0.5).to(dev).train()
         params = list(model.parameters()) + list(fusion.parameters())
-    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-4)
+    # main.py:88's Adam (lr 1e-3, weight decay 1e-4) as torch's single-kernel (fused) update on the
+    # device (MVML_BENCH_ADAM=foreach: the multi-tensor form)
+    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-4,
+                           **({"fused": True} if os.environ.get("MVML_BENCH_ADAM", "fused") == "fused" else {}))
     reducer = FlatGradAllReduce(params, average=True)
 
     def step(b, fused=True):
