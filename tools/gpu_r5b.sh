@@ -1,5 +1,4 @@
 #!/bin/bash
 set -o pipefail
 cd "$(dirname "$0")/.."
-MVML_BENCH_ADAM=foreach tools/gpu_r5.sh bench adf --steps 16 --warmup 2 --no-cpu-baseline --no-inference || exit 1
-tools/gpu_r5.sh bench adu --steps 16 --warmup 2 --no-cpu-baseline --no-inference
+tools/gpu_r5.sh agg c5rs --config 5 --mols 8192 --layers 1 --no-bwd --ab "dst_fwd=1;dst_fwd=1,dst_unr=8;dst_fwd=1;dst_fwd=1,dst_unr=8"
