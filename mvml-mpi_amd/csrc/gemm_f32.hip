@@ -2462,8 +2462,10 @@ int absmax_launch(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32
   if (rows <= 0 || cols <= 0) return MVML_OK;
   const int vec = (cols % 4 == 0) && (ld % 4 == 0) && ((uintptr_t)P % 16 == 0);
   const int64_t cx = ceil_div(vec ? cols / 4 : cols, 256);
-  // ~16 K workgroups of 256 threads in flight at most (4 rows each): HBM-rate for big operands
-  const int64_t ry = std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, 4), ceil_div(8192, cx)));
+  // ~1 K workgroups (each ends with ONE atomicMax on the single output word: a word takes ~90
+  // atomics per us, so the round-4 8 K workgroups spent ~90 us of a 150 us pass on them); each
+  // thread walks its column down rows 4 at a time, enough loads in flight for HBM rate
+  const int64_t ry = std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, 4), ceil_div(1024, cx)));
   absmax_kernel<<<dim3((unsigned)cx, (unsigned)ry), 256, 0, st>>>(rows, cols, P, ld, vec, out);
   return check_launch("absmax_kernel");
 }

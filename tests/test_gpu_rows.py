@@ -345,3 +345,21 @@ def test_gnn_module_il4_bitwise(monkeypatch):
                                            if p.grad is not None])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_absmax_matches_torch():
+    """mvml_absmax_f32 (one atomicMax per workgroup, ~1 K workgroups) equals torch's max |x| bit
+    for bit on tall, wide, unaligned and tiny operands, and accumulates into a prior value."""
+    from mvml_gat.functional import absmax
+    g = torch.Generator().manual_seed(3)
+    for rows, cols, ld in ((1, 1, 1), (65536, 768, 768), (1753, 76, 76), (300000, 5, 7), (17, 9000, 9001),
+                           (4096, 1928, 1984)):
+        X = torch.randn(rows, ld, generator=g).to(DEV)
+        X[rows // 2, cols - 1] = -7.5e3  # the max sits in one place, negative
+        out = torch.zeros(2, dtype=torch.int32, device=DEV)
+        absmax(X, rows, cols, ld, out, 1)
+        want = X[:, :cols].abs().max()
+        assert out[1].view(torch.float32) == want, (rows, cols, ld)
+        out[0] = torch.tensor(1e5, dtype=torch.float32).view(torch.int32)
+        absmax(X, rows, cols, ld, out, 0, accumulate=True)
+        assert out[0].view(torch.float32).item() == 1e5

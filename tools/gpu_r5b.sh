@@ -1,4 +1,5 @@
 #!/bin/bash
 set -o pipefail
 cd "$(dirname "$0")/.."
-tools/gpu_r5.sh agg c5rs --config 5 --mols 8192 --layers 1 --no-bwd --ab "dst_fwd=1;dst_fwd=1,dst_unr=8;dst_fwd=1;dst_fwd=1,dst_unr=8"
+tools/gpu_r5.sh tests am tests/test_gpu_rows.py tests/test_gpu_parity.py tests/test_gpu_mvp.py -k "absmax or gnn or mvp or gemm" || exit 1
+tools/gpu_r5.sh bench am --steps 16 --warmup 2 --no-cpu-baseline --no-inference
