@@ -56,8 +56,8 @@ TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32
          "mvml_bilstm_wide_step_fwd", "mvml_bilstm_wide_step_bwd", "mvml_bilstm_pack_rows",
          "mvml_bilstm_gather_rows", "mvml_bilstm_token_grad", "mvml_bilstm_select_last",
          "mvml_bilstm_token_grad_packed", "mvml_bilstm_packed_tokens", "mvml_gemm_f16x2_rows",
-         "mvml_absmax_rows_f32", "mvml_segment_max_bits", "mvml_gat_x_fwd", "mvml_gat_x_bwd",
-         "mvml_gemm_f16x2_ex", "mvml_gemm_f16x2_batched", "mvml_gat_elu_bwd", "mvml_gat_x_pack_weights",
+         "mvml_absmax_rows_f32", "mvml_segment_max_bits",
+         "mvml_gemm_f16x2_ex", "mvml_gemm_f16x2_batched",
          "mvml_split_f16x2_il4", "mvml_build_csr", "mvml_build_node_groups"]
 
 
@@ -461,11 +461,19 @@ def run(args):
                                    proj_dtype=torch.bfloat16 if args.proj_bf16 else None).to(dev).train()
         fusion = mvml_gat.MVFusion(384, 12, 11, 0.5).to(dev).train()
         params = list(model.parameters()) + list(fusion.parameters())
-    # main.py:88's Adam (lr 1e-3, weight decay 1e-4) as torch's single-kernel (fused) update on the
-    # device (MVML_BENCH_ADAM=foreach: the multi-tensor form)
-    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-4,
-                           **({"fused": True} if os.environ.get("MVML_BENCH_ADAM", "fused") == "fused" else {}))
-    reducer = FlatGradAllReduce(params, average=True)
+    # main.py:88's Adam (lr 1e-3, weight decay 1e-4): by default mvml_gat.FlatAdam — the gradient
+    # gather, the ONE all-reduce of [gradients | presence flags] and the update as HIP kernels
+    # over flat buffers, no host synchronisation (MVML_BENCH_ADAM=fused / foreach: torch's Adam
+    # behind FlatGradAllReduce, which reads the reduced presence flags back every step)
+    adam_kind = "torch" if args.dry_run else os.environ.get("MVML_BENCH_ADAM", "flat")
+    if adam_kind == "flat":
+        from mvml_gat.optim import FlatAdam
+        opt = FlatAdam(params, lr=1e-3, weight_decay=1e-4, average=True)
+        reducer = lambda: None  # noqa: E731  (the all-reduce is inside FlatAdam.step)
+    else:
+        opt = torch.optim.Adam(params, lr=1e-3, weight_decay=1e-4,
+                               **({"fused": True} if adam_kind == "fused" else {}))
+        reducer = FlatGradAllReduce(params, average=True)
 
     def step(b, fused=True):
         opt.zero_grad(set_to_none=False)
@@ -499,6 +507,8 @@ def run(args):
     timer_on = not args.no_kernel_timer and not args.dry_run
     if timer_on:
         _lib.timer.enable(TIMED)
+    if adam_kind == "flat":
+        opt.allreduce_events = []  # the timed steps' all-reduces only
     barrier()
     sync()
     mem0 = alloc_stats(args)
@@ -543,6 +553,15 @@ def run(args):
     value = total_mols / elapsed if elapsed > 0 else 0.0
 
     roofline, extra = None, {}
+    if adam_kind == "flat" and world > 1:
+        # HIP events around each timed step's one all-reduce of [gradients | presence flags]
+        ar = opt.allreduce_ms()
+        extra["allreduce_ms"] = {"rank0": round(ar, 4), "max_over_ranks": round(reduce_max(ar), 4),
+                                 "bytes": int(opt.gbuf.numel() * 4),
+                                 "what": "mean per-step duration of the gradient all-reduce (HIP events on "
+                                         "the step's stream), this rank and the slowest rank"}
+    extra["optimizer"] = ("FlatAdam (mvml_grad_gather + one all-reduce + mvml_adam_flat)" if adam_kind == "flat"
+                          else f"torch.optim.Adam ({adam_kind}) + FlatGradAllReduce")
     mps = mols_per_step(args)  # the per-step molecule count the workload actually used
     wkey = f"{args.workload}/mols_per_step={mps}" + ("/proj_bf16" if args.proj_bf16 else "")
     if timer_on:
@@ -554,6 +573,7 @@ def run(args):
                               + summ.get("mvml_gemm_f16x2_rows", [])
                               + summ.get("mvml_gemm_f16x2_bsplit", [])
                               + summ.get("mvml_gemm_f16x2_ex", []) + summ.get("mvml_gemm_f16x2_batched", [])
+                              + summ.get("mvml_gemm_f16x2_planes", [])
                               + summ.get("mvml_lstm_gates_cell_fwd", [])
                               + summ.get("mvml_gat_proj_fwd", []), args.steps)
         if rank == 0:
@@ -572,8 +592,8 @@ def run(args):
         # the GAT projection at small K (K <= 96: layer 1's, on the wave-per-64-column memory
         # kernel gemm_smallk_kernel) is an HBM roofline of its own, not MFMA work
         rows_ev = summ.get("mvml_gemm_f16x2_rows", [])
-        sk_ev = [e for e in rows_ev if (e[1] or {}).get("role") == "gat_proj"
-                 and e[1].get("shape", (0, 0, 1 << 30))[2] <= SMALLK_MAX_K]
+        # (the path the library actually took, not the shape: mvml_gemm_rows_smallk)
+        sk_ev = [e for e in rows_ev if (e[1] or {}).get("role") == "gat_proj" and e[1].get("path") == "smallk"]
         rows_ev = [e for e in rows_ev if e not in sk_ev]
         if sk_ev:
             extra["roofline_proj_l1"] = roofline_entry(sk_ev, "hbm", load_traffic(wkey, "gemm_smallk"))
@@ -585,6 +605,7 @@ def run(args):
                    + summ.get("mvml_gemm_f16x2_bsplit", []) + rows_ev
                    + summ.get("mvml_gemm_f32x3_batched", []) + summ.get("mvml_lstm_gates_cell_fwd", [])
                    + summ.get("mvml_gemm_f16x2_ex", []) + summ.get("mvml_gemm_f16x2_batched", [])
+                   + summ.get("mvml_gemm_f16x2_planes", [])
                    + ([] if args.proj_bf16 else proj_ev))
         bf_ev = summ.get("mvml_gemm_bf16", []) + (proj_ev if args.proj_bf16 else [])
         if bf_ev:

@@ -205,8 +205,15 @@ int mvml_gemm_f16x2_rows(int64_t M, int64_t N, int64_t K, const float* A, int64_
                          const uint32_t* amax_a_rows, const uint32_t* amax_b, const float* bias,
                          float beta, int act, float* C, int64_t ldc, void* workspace,
                          size_t workspace_bytes, void* stream);
+/* 1 if mvml_gemm_f16x2_rows with these arguments (b = b_il4 if given, else B) runs on the
+ * small-K memory kernel under the current options, else 0 (the 256x256 tile): how a caller
+ * or a timer tells which roofline a product belongs to (no device work). */
+int mvml_gemm_rows_smallk(int b_kmajor, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                          const float* B, int64_t ldb, float beta, int act, const float* C,
+                          int64_t ldc);
 /* mvml_gemm_f16x2_rows (no beta, no split-K: K is a feature dimension; the 256x256 tile at any
- * size) with a strided batch and epilogue extras, for the re-associated first GAT layer:
+ * size) with a strided batch and epilogue extras (the ELU link: layer 2's data gradient leaves
+ * as layer 1's g_rst through act 3):
  *  - product z < batch reads A + z stride_a, B (or b_il4) + z stride_b, amax_a_rows + z
  *    stride_rows, bias + z stride_bias and writes C + z stride_c;
  *  - act: 0 none, 1 ReLU, 2 ELU after the bias (x > 0 ? x : expm1(x)), 3 the ELU backward
@@ -239,6 +246,27 @@ int mvml_gemm_f16x2_batched(int a_kmajor, int b_kmajor, int64_t M, int64_t N, in
  * cols % 4 == 0, ld % 4 == 0, P and out 16-B aligned. */
 int mvml_split_f16x2_il4(int64_t rows, int64_t cols, const float* P, int64_t ld,
                          const uint32_t* amax, float* out, void* stream);
+/* The "il8" split-fp16 image of an fp32 operand for mvml_gemm_f16x2_planes (round 6): out is
+ * [rows][ld_out] floats; per 8-value k group g < ld_out / 8 of row r it holds the 8 scaled high
+ * fp16 halves of x[r][8g .. 8g+7], then the 8 low halves (the GEMM's own split: scale from
+ * *amax, or from amax_rows[r] — exactly one of the two), k >= K as zeros.  x[r][k] is
+ * P[r*ld + k] (kmajor = 0) or P[k*ld + r] (kmajor = 1: the image of the transpose).
+ * ld_out >= K rounded up to 32, ld_out % 8 == 0, out 16-B aligned. */
+int mvml_split_f16x2_il8(int64_t rows, int64_t K, const float* P, int64_t ld, int kmajor,
+                         const uint32_t* amax, const uint32_t* amax_rows, float* out,
+                         int64_t ld_out, void* stream);
+/* C[M][N] = act(A B^T + bias + beta C) at fp32 accuracy (scaled split-fp16, three fp16 MFMAs
+ * per product; the 256x256 tile with both operands staged by LDS-DMA, round 6), B given as its
+ * il8 image b_image ([N][ldb], ldb >= K rounded up to 32, made with amax_b).  A is fp32
+ * [M][lda] (K % 4 == 0; its scale from *amax_a, or per row from amax_a_rows — exactly one) or,
+ * with a_image != 0, its il8 image made with the same maxima (lda >= K rounded up to 32).
+ * act 0 / 1 (ReLU); rows 16-B aligned.  The mvml_gemm_f16x2_rows / _amax product of the same
+ * operands to fp32 accuracy (a different MFMA order: not bitwise). */
+int mvml_gemm_f16x2_planes(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                           int a_image, const uint32_t* amax_a, const uint32_t* amax_a_rows,
+                           const float* b_image, int64_t ldb, const uint32_t* amax_b,
+                           const float* bias, float beta, int act, float* C, int64_t ldc,
+                           void* stream);
 /* out[r] = bits of max_c |P[r*ld + c]|, c < cols (accumulate != 0: max with the current out[r]);
  * one writer per row, no atomics. */
 int mvml_absmax_rows_f32(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32_t* out,
@@ -365,34 +393,28 @@ int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_
                      const float* g_out, int H, int F, float slope, int mode, float* gY,
                      int64_t ldgy, uint32_t* gy_amax, uint32_t* gy_row_amax, void* workspace,
                      size_t workspace_bytes, void* stream);
-
-/* ---------------------------------------------------------------------------------------
- * The first GATConv (model.py:81, 74 features -> 4 x 192, flatten + ELU) re-associated: the
- * same GATConv.forward sums in another order,
- *   rst[v, h] = (sum_e a_e,h X[src_e]) W_h^T + X[v] Wres_h^T + b_h,
- * so the aggregation runs over the Fp-wide feature rows and no N x (2 H F) projection is formed.
- * mvml_gat_x_fwd: el / er = X A_l^T, X A_r^T (Alr = [A_l ; A_r] = Wcat's last 2H rows, 2H x Fp)
- * into elr [N][2H]; the edge softmax (order and arithmetic of mvml_gat_agg_fwd's) into attn
- * [E][H] (in-CSR slots); axc [N][H][2 Fp] = per head [AX_h | X] with AX_h[v] = sum_e a_e,h
- * X[src_e]; arows [H][N] = per-row |max| bits of each head block.  The layer output is then
- * mvml_gemm_f16x2_ex over the H blocks (K = 2 Fp, B = mvml_gat_x_pack_weights' [W_h | Wres_h],
- * bias + ELU in the epilogue).  H in {1, 2, 4, 8}; Fp % 4 == 0, Fp <= 128 (mvml_gat_x_supported).
- * mvml_gat_x_bwd, from dax [N][H][Fp] = g_rst_h W_h (g_rst = dL/d rst): g_a_e = <dax_h[dst],
- * X[src]>, the edge-softmax and LeakyReLU backward (gpre [E][H] = dL/ds_e, in-CSR slots), d er
- * (in-edges) and d el (out-CSR gather) into gelr [N][2H]; gelr_amax (may be NULL) folds max
- * |gelr| in by atomicMax.  mvml_gat_elu_bwd: g_rst = g_out ELU'(out) (n floats) with max |g_rst|
- * folded into *amax. */
-int mvml_gat_x_supported(int H, int Fp);
-int mvml_gat_x_pack_weights(const float* Wcat, int H, int F, int Fp, float* Wb, void* stream);
-int mvml_gat_x_fwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src, const float* X,
-                   int Fp, const float* Alr, int H, float slope, float* elr, float* attn, float* axc,
-                   uint32_t* arows, void* stream);
-int mvml_gat_x_bwd(int64_t num_nodes, const int32_t* in_rowptr, const int32_t* in_src,
-                   const int32_t* out_rowptr, const int32_t* out_inslot, const float* X, int Fp,
-                   const float* elr, const float* attn, int H, float slope, const float* dax,
-                   float* gpre, float* gelr, uint32_t* gelr_amax, void* stream);
-int mvml_gat_elu_bwd(int64_t n, const float* g_out, const float* out, float* g_rst, uint32_t* amax,
-                     void* stream);
+/* A GATConv's whole backward in one call (SURVEY §8(b)'s proj_bwd; the autograd of dgl GATConv /
+ * dgllife GATLayer, model.py:81, 91): from the forward's X ([N][Fp], Fp = Fin rounded up to 4,
+ * zero-padded), Wcat and attn_lr (mvml_gat_fold_weights' inputs / output), Y (ldy), elr, attn, out
+ * and g_out = dL/d out, it writes g_X ([N][Fin]; NULL: not formed), g_fc and g_res ([H F][Fin]:
+ * fc.weight's and res_fc.weight's layouts), g_attn ([2][H F]: attn_l's then attn_r's) and g_bias
+ * ([H F]).  mean = 0: flatten + ELU layer (aggregation mode 0), 1: head mean (mode 1).
+ * The same launches, in the same order, as mvml_gat.functional.GATLayerFunction.backward (so
+ * bitwise its results): mvml_gat_agg_bwd, the split-K weight-gradient product
+ * (mvml_gemm_f16x2_amax), mvml_gat_unfold_grads, the attention-vector product
+ * (mvml_gemm_f32x3_batched), mvml_colsum_f32 and the per-row-scaled data-gradient product
+ * (mvml_gemm_f16x2_rows, Wcat as its interleaved image), every operand maximum and scratch
+ * buffer inside `workspace` (mvml_gat_layer_bwd_workspace_size bytes). */
+size_t mvml_gat_layer_bwd_workspace_size(int64_t num_nodes, int64_t num_edges, int H, int F, int Fin,
+                                         int mean);
+int mvml_gat_layer_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
+                       const int32_t* in_rowptr, const int32_t* in_src, const int32_t* out_rowptr,
+                       const int32_t* out_dst, const int32_t* out_inslot, int64_t num_edges, int H,
+                       int F, int Fin, int mean, float slope, const float* X, const float* Wcat,
+                       const float* attn_lr, const float* Y, int64_t ldy, const float* elr,
+                       const float* attn, const float* out, const float* g_out, float* g_X,
+                       float* g_fc, float* g_res, float* g_attn, float* g_bias, void* workspace,
+                       size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Set2Set (dgl 0.9.1, model.py:82-84, 92) building blocks.
@@ -430,15 +452,17 @@ int mvml_segment_max_bits(int64_t B, const int64_t* node_offsets, const uint32_t
 int mvml_lstm_cell_fwd(int64_t B, int D, const float* gates_pre, const float* b_ih,
                        const float* b_hh, const float* c_prev, float* c_out, float* h_out,
                        int64_t ldh, float* act_out, float* h_out2, int64_t ldh2, void* stream);
-/* g_h [B,D] (ld ldgh), g_c [B,D] (carry from t+1, may be NULL) -> g_gates [B,4D] (pre-act),
+/* g_h [B,D] (ld ldgh) + g_h2 [B,D] (ld ldgh2; may be NULL: a second consumer's dL/dh, summed
+ * in the kernel), g_c [B,D] (carry from t+1, may be NULL) -> g_gates [B,4D] (pre-act),
  * g_c_prev [B,D] (may be NULL).  gg_amax (may be NULL): *gg_amax = max(*gg_amax, bits of
  * max |g_gates|) — the split-fp16 operand max of the GEMMs that read g_gates.  gb_part (may be
  * NULL): [R][4D] partial column sums of g_gates, R = mvml_lstm_cell_bwd_part_rows(B, D) (the
  * bias gradient is their column sum, over every step's partial). */
 int64_t mvml_lstm_cell_bwd_part_rows(int64_t B, int D);
 int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const float* c, const float* c_prev,
-                       const float* g_h, int64_t ldgh, const float* g_c, float* g_gates,
-                       float* g_c_prev, uint32_t* gg_amax, float* gb_part, void* stream);
+                       const float* g_h, int64_t ldgh, const float* g_h2, int64_t ldgh2,
+                       const float* g_c, float* g_gates, float* g_c_prev, uint32_t* gg_amax,
+                       float* gb_part, void* stream);
 /* Readout segment pass (one wavefront per molecule): e_n = <x_n, q_g>, alpha = softmax over
  * the molecule's atoms (softmax_nodes), r_g = sum_n alpha_n x_n (sum_nodes).  Writes r into
  * qstar[:, D:2D] (ld ldq, q itself already sits in qstar[:, 0:D]) and lse[g] for backward. */
@@ -664,6 +688,28 @@ int mvml_bilstm_wide_bwd(int64_t T, int64_t B, int D, const int32_t* batch_sizes
                          const float* c0, const float* c1, float* carry, float* gg0, float* gg1,
                          uint32_t* gg_amax, const uint32_t* amax, int gg_packed, void* workspace,
                          size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Optimizer step on flat buffers: main.py:88's torch.optim.Adam(params, lr, weight_decay)
+ * (amsgrad off, L2 decay into the gradient) over every parameter at once, with "this
+ * parameter has a gradient" kept on the device (torch skips parameters whose .grad is None;
+ * across ranks, one whose all-reduced flag is 0).  Parameters occupy [param_off[i],
+ * param_off[i] + n_i) of the flat buffers; a static chunk table (chunk c covers
+ * [chunk_beg[c], chunk_end[c]) of parameter chunk_param[c]) gives one workgroup per chunk.
+ * ------------------------------------------------------------------------------------- */
+/* flat[param_off[i] ..] = the gradient at src[i] (a device pointer, 0 = none: zeros), and
+ * flat[numel + i] = 1.0 / 0.0 (the presence flag) for i < P. */
+int mvml_grad_gather(int64_t nchunks, const int32_t* chunk_param, const int64_t* chunk_beg,
+                     const int64_t* chunk_end, const int64_t* param_off, const uint64_t* src, int P,
+                     float* flat, int64_t numel, void* stream);
+/* For every parameter i with flags[i] > 0: step = steps[i] + 1, g = grad * grad_scale (+
+ * weight_decay param), exp_avg += (1 - beta1)(g - exp_avg), exp_avg_sq = beta2 exp_avg_sq +
+ * (1 - beta2) g^2, param -= lr / (1 - beta1^step) * exp_avg / (sqrt(exp_avg_sq) /
+ * sqrt(1 - beta2^step) + eps) (torch's Adam); then steps[i] += 1.  Others are untouched. */
+int mvml_adam_flat(int64_t nchunks, const int32_t* chunk_param, const int64_t* chunk_beg,
+                   const int64_t* chunk_end, const float* flags, int32_t* steps, int P, float* param,
+                   const float* grad, float* exp_avg, float* exp_avg_sq, float lr, float beta1,
+                   float beta2, float eps, float weight_decay, float grad_scale, void* stream);
 
 #ifdef __cplusplus
 }

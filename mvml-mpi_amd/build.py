@@ -35,7 +35,7 @@ def _stale(obj, deps):
 def compile_one(src):
     path = os.path.join(CSRC, src)
     obj = os.path.join(OBJ, src + ".o")
-    deps = [path, os.path.join(CSRC, "common.h"), HEADER]
+    deps = [path, HEADER] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     if not _stale(obj, deps):
         return obj
     cmd = [HIPCC, *FLAGS, "-c", path, "-o", obj]

@@ -4,8 +4,6 @@
 #include <stdlib.h>
 
 #include <atomic>
-#include <mutex>
-#include <unordered_map>
 
 #include "common.h"
 
@@ -29,30 +27,6 @@ int check_launch(const char* what) {
     return MVML_ERR_LAUNCH;
   }
   return MVML_OK;
-}
-
-unsigned resident_blocks(const void* kernel, int threads, int64_t need) {
-  static std::mutex mu;
-  static std::unordered_map<const void*, int> per_cu;
-  static int cus = 0;
-  int n = 0;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    if (cus == 0) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-        cus = 256;  // MI355X
-    }
-    auto it = per_cu.find(kernel);
-    if (it == per_cu.end()) {
-      int b = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, threads, 0) != hipSuccess || b <= 0) b = 1;
-      it = per_cu.emplace(kernel, b).first;
-    }
-    n = it->second * cus;
-  }
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, n));
 }
 
 // Kernel-path options (include/mvml_gat.h, MVML_OPT_*): environment defaults read once at load.

@@ -41,15 +41,6 @@ struct GroupPlan {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Workgroups of `kernel` (`threads` each) resident on the whole device at once (CUs x the
-// occupancy calculator's blocks per CU; cached per kernel), capped at `need`: the grid of a
-// persistent kernel whose blocks each walk many work items and commit block-wide results once.
-unsigned resident_blocks(const void* kernel, int threads, int64_t need);
-template <typename K>
-unsigned resident_blocks(K* kernel, int threads, int64_t need) {
-  return resident_blocks(reinterpret_cast<const void*>(kernel), threads, need);
-}
-
 // Check the launch we just enqueued; never synchronises.
 int check_launch(const char* what);
 // Current value of a kernel-path option (MVML_OPT_*, capi.cpp).

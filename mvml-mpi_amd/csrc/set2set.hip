@@ -60,6 +60,7 @@ __global__ void lstm_cell_fwd_kernel(int64_t B, int D, const float* __restrict__
 __global__ void lstm_cell_bwd_kernel(int64_t B, int D, const float* __restrict__ act,
                                      const float* __restrict__ c, const float* __restrict__ c_prev,
                                      const float* __restrict__ g_h, int64_t ldgh,
+                                     const float* __restrict__ g_h2, int64_t ldgh2,
                                      const float* __restrict__ g_c, float* __restrict__ g_gates,
                                      float* __restrict__ g_c_prev, uint32_t* __restrict__ gg_amax,
                                      float* __restrict__ gb_part) {
@@ -72,7 +73,9 @@ __global__ void lstm_cell_bwd_kernel(int64_t B, int D, const float* __restrict__
     const int d = (int)(e - b * D);
     const float* a = act + b * 4 * D;
     const float i = a[d], f = a[D + d], gt = a[2 * D + d], o = a[3 * D + d];
-    const float gh = g_h[b * ldgh + d];
+    // dL/dh from its two consumers (the next layer's input, the next step's recurrence): the
+    // sum autograd would form with a separate add, formed here
+    const float gh = g_h2 ? g_h[b * ldgh + d] + g_h2[b * ldgh2 + d] : g_h[b * ldgh + d];
     const float tc = tanhf(c[e]);
     const float gc = (g_c ? g_c[e] : 0.f) + gh * o * (1.f - tc * tc);
     const float cp = c_prev ? c_prev[e] : 0.f;
@@ -390,17 +393,18 @@ extern "C" int64_t mvml_lstm_cell_bwd_part_rows(int64_t B, int D) {
 
 extern "C" int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const float* c,
                                   const float* c_prev, const float* g_h, int64_t ldgh,
+                                  const float* g_h2, int64_t ldgh2,
                                   const float* g_c, float* g_gates, float* g_c_prev,
                                   uint32_t* gg_amax, float* gb_part, void* stream) {
   clear_error();
-  MVML_REQUIRE(B >= 0 && D > 0 && ldgh >= D, "lstm_cell_bwd: bad shape");
+  MVML_REQUIRE(B >= 0 && D > 0 && ldgh >= D && (!g_h2 || ldgh2 >= D), "lstm_cell_bwd: bad shape");
   if (B == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
   if (gb_part) {  // grid * 256 = R D: every thread keeps one unit (see the kernel)
     const int64_t R = cell_bwd_part_rows(B, D);
     lstm_cell_bwd_kernel<<<(unsigned)(R * D / 256), 256, 0, st>>>(B, D, act, c, c_prev, g_h, ldgh,
-                                                                  g_c, g_gates, g_c_prev, gg_amax,
-                                                                  gb_part);
+                                                                  g_h2, ldgh2, g_c, g_gates, g_c_prev,
+                                                                  gg_amax, gb_part);
     return check_launch("lstm_cell_bwd_kernel");
   }
   // with gg_amax, one atomicMax per workgroup on a single word: a short kernel whose thousands
@@ -409,8 +413,8 @@ extern "C" int mvml_lstm_cell_bwd(int64_t B, int D, const float* act, const floa
   const unsigned grid = gg_amax ? (unsigned)std::min<int64_t>(
                                       grid_for(B * D), std::max<int64_t>(256, ceil_div(B * D, 4096)))
                                 : grid_for(B * D);
-  lstm_cell_bwd_kernel<<<grid, 256, 0, st>>>(B, D, act, c, c_prev, g_h, ldgh, g_c, g_gates,
-                                             g_c_prev, gg_amax, nullptr);
+  lstm_cell_bwd_kernel<<<grid, 256, 0, st>>>(B, D, act, c, c_prev, g_h, ldgh, g_h2, ldgh2, g_c,
+                                             g_gates, g_c_prev, gg_amax, nullptr);
   return check_launch("lstm_cell_bwd_kernel");
 }
 

@@ -149,13 +149,6 @@ def slot(t, i):
 # or mvml_gat_proj_fwd's logit-partial epilogue over the Z tile (False)
 PROJ_ELR_GEMM = os.environ.get("MVML_PROJ_ELR_GEMM", "1") != "0"
 
-# MVML_BSPLIT=1: weights split once per step into fp16 planes that the split-fp16 GEMMs read
-# as B (mvml_split_f16x2 / mvml_gemm_f16x2_bsplit).  Off by default: A/B on one box, config-3
-# step 165.0 ms without vs 167.9 ms with — two 8-B plane loads per piece cost more than the
-# split VALU they save (the no-split ablation bound was ~5 % per GEMM); correct either way.
-BSPLIT = os.environ.get("MVML_BSPLIT", "0") == "1"
-
-
 # Weights split ONCE per step into the interleaved-by-4 fp16 image (mvml_split_f16x2_il4) that
 # the 256x256 split-fp16 tiles load in place of fp32 B: one 16-B load per piece as before and no
 # split VALU for B (bitwise the in-kernel split).  MVML_BSPLIT_IL=0: every tile splits B itself.
@@ -172,19 +165,32 @@ def split_il4(W, rows, cols, ld, amax_ptr):
     return img
 
 
-def split_planes(W, rows, cols, ld, amax_ptr):
-    """W (fp32, [rows][ld]) split once into its two scaled fp16 planes (mvml_split_f16x2) for
-    the split-fp16 GEMMs that read it as B: (planes, elements between the planes); (None, 0)
-    with MVML_BSPLIT=0."""
-    if not BSPLIT:
-        return None, 0
-    planes = torch.empty(2 * rows * ld, dtype=torch.int16, device=W.device)
-    call("mvml_split_f16x2", rows, cols, ptr(W), ld, amax_ptr, ptr(planes), _stream(W.device))
-    return planes, rows * ld
+def split_il8(P, rows, K, ld, kmajor=0, amax_ptr=None, rows_max=None, out=None):
+    """P's il8 split-fp16 image (mvml_split_f16x2_il8) for mvml_gemm_f16x2_planes: fp32
+    [rows][K rounded up to 32]; x[r][k] = P[r, k] (kmajor 0) or P[k, r] (kmajor 1: the image of
+    P^T); scale from amax_ptr (operand-wide) or rows_max (per row, int32 [rows])."""
+    kp = (K + 31) // 32 * 32
+    if out is None:
+        out = torch.empty((max(rows, 1), kp), dtype=torch.float32, device=P.device)
+    call("mvml_split_f16x2_il8", rows, K, ptr(P), ld, int(kmajor), amax_ptr, ptr(rows_max), ptr(out), kp,
+         _stream(P.device))
+    return out
+
+
+def gemm_planes(A, M, N, K, lda, bimg, ldb, C, ldc, amax_b, amax_a=None, arows=None, a_image=False,
+                bias=None, beta=0.0, act=0, role=None):
+    """C[M,N] = act(A B^T + bias + beta C) with B given as its il8 image (split_il8, made with
+    amax_b) and A fp32 (or, a_image, its il8 image made with the same maxima): the LDS-DMA
+    split-fp16 tile (mvml_gemm_f16x2_planes).  amax_a: pointer to max |A| bits, or arows: per-row
+    |A| max bits (int32 [M])."""
+    _lib.call_tag[0] = {"flops": 2 * M * N * K, "shape": (M, N, K, 0, 0),
+                        "bytes": 4 * (M * N + M * K + N * K), "role": role}
+    call("mvml_gemm_f16x2_planes", M, N, K, ptr(A), lda, int(a_image), amax_a, ptr(arows), ptr(bimg), ldb,
+         amax_b, ptr(bias), float(beta), int(act), ptr(C), ldc, _stream(C.device))
 
 
 def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.0, act=0, algo=None,
-         amax=None, bsplit=None, arows=None, bil4=None, role=None):
+         amax=None, arows=None, bil4=None, role=None):
     """C[M,N] = act(A*B + bias + beta*C) on MFMA (see mvml_gemm_f32 / mvml_gemm_f32x3 /
     mvml_gemm_f16x2).  amax = (pointer to |A| max bits, pointer to |B| max bits) from absmax()
     lets split-fp16 products that share an operand share its max pass.  arows (split-fp16,
@@ -203,6 +209,12 @@ def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.
     if algo == "f16x2" and arows is not None:
         if a_kmajor or amax is None or amax[1] is None:
             raise ValueError("gemm: per-row A maxima need a K-contiguous A and max |B|")
+        # which kernel runs (the small-K memory kernel or the tile): bench.py files the timing
+        # under the matching roofline
+        fn = getattr(L, "mvml_gemm_rows_smallk", None)  # (absent from older libraries of A/B runs)
+        sk = fn(int(b_kmajor), M, N, K, ptr(A), lda, ptr(bil4 if bil4 is not None else B), ldb, float(beta),
+                int(act), ptr(C), ldc) if fn is not None else 0
+        _lib.call_tag[0]["path"] = "smallk" if sk else "tile"
         call("mvml_gemm_f16x2_rows", M, N, K, ptr(A), lda, ptr(B), ldb, int(b_kmajor), ptr(bil4),
              ptr(arows), amax[1], ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn, _stream(dev))
         return
@@ -210,11 +222,6 @@ def gemm(A, B, M, N, K, a_kmajor, b_kmajor, lda, ldb, C, ldc, bias=None, beta=0.
         call("mvml_gemm_f16x2_bsplit", int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda, ptr(B), ldb,
              ptr(bil4), 0, amax[0], amax[1], ptr(bias), float(beta), int(act), ptr(C), ldc, wp, wn,
              _stream(dev))
-        return
-    if algo == "f16x2" and amax is not None and bsplit is not None:  # B from its pre-split planes
-        call("mvml_gemm_f16x2_bsplit", int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda, ptr(B), ldb,
-             ptr(bsplit[0]), bsplit[1], amax[0], amax[1], ptr(bias), float(beta), int(act), ptr(C), ldc,
-             wp, wn, _stream(dev))
         return
     if algo == "f16x2" and amax is not None:
         call("mvml_gemm_f16x2_amax", int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), lda, ptr(B), ldb,
@@ -240,15 +247,6 @@ def colsum(X, M, N, ldx, out, beta=0.0, offset=0, alpha=1.0):
     xp = ctypes.c_void_p(ptr(X).value + 4 * offset)
     call("mvml_colsum_f32", M, N, xp, ldx, float(alpha), float(beta), ptr(out), wp, wn, _stream(dev))
 
-
-# The first GATConv (narrow input: Fp = 76 features, flatten heads) re-associated: the edge
-# softmax and aggregation run over the feature rows and one batched GEMM per head forms the
-# output (mvml_gat_x_fwd + mvml_gemm_f16x2_ex, see csrc/gat_x.hip) instead of projecting every
-# atom to 2 H F + 2 H columns and aggregating those.  Off by default (MVML_GAT_REASSOC=1 turns it
-# on): measured slower on configs 3 and 5 (401 k vs 416 k mol/s on config 3; the K = 152 per-head
-# GEMMs and the per-head weight gradients cost more than the projection's Y round trip saves,
-# DESIGN.md "Layer 1 by re-association").
-REASSOC_X = os.environ.get("MVML_GAT_REASSOC", "0") == "1"
 
 # Kernel paths picked per call from the batch's molecule sizes (host counts, no device work):
 # "large" batches have half their atoms or more in molecules past the LDS molecule window
@@ -339,13 +337,7 @@ class GATLayerFunction(torch.autograd.Function):
         Xp = X if Fp == Fin else torch.nn.functional.pad(X, (0, Fp - Fin))
         attn_l, attn_r = _c(attn_l), _c(attn_r)
         attn_lr = torch.cat([attn_l.reshape(-1), attn_r.reshape(-1)])
-        ctx.reassoc = False
         ctx.elu_claim = None
-        if (REASSOC_X and (algo or GEMM_ALGO) == "f16x2" and ROW_SCALES and PROJ_ELR_GEMM
-                and mode in (MODE_FLATTEN_ELU, MODE_FLATTEN) and not X.requires_grad
-                and 2 * Fp <= F and _lib.lib().mvml_gat_x_supported(H, Fp)):
-            return GATLayerFunction._forward_x(ctx, X, Xp, fc_w, res_w, attn_l, attn_r, attn_lr, bias,
-                                               g, H, F, slope, mode, C)
         link = _elu_link_of(X) if (ELU_LINK[0] and (algo or GEMM_ALGO) == "f16x2" and ROW_SCALES
                                    and PROJ_ELR_GEMM and X.requires_grad) else None
         # [fc.weight ; res_fc.weight (or its head mean) ; A_l ; A_r]: the projection GEMM uses
@@ -359,7 +351,6 @@ class GATLayerFunction(torch.autograd.Function):
         amx = None
         ax = None  # (tensor, slot) of max |X|
         xr = None  # per-row max |X| bits (ROW_SCALES)
-        wps = (None, 0)
         wil = None  # Wcat's interleaved split image (BSPLIT_IL)
         if (algo or GEMM_ALGO) == "f16x2":
             amx = torch.zeros(4, dtype=torch.int32, device=dev)  # [X, Wcat, gY (bwd), out]
@@ -381,8 +372,7 @@ class GATLayerFunction(torch.autograd.Function):
                 absmax(Xp, N, Fp, Fp, amx, 0)
                 ax = (amx, 0)
             absmax(Wcat, C + 2 * H, Fp, Fp, amx, 1)
-            # Wcat split once: the projection's tiles and the backward's dL/dX read the planes
-            wps = split_planes(Wcat, C + 2 * H, Fp, Fp, slot(amx, 1))
+            # Wcat split once: the projection's tiles and the backward's dL/dX read the image
             wil = split_il4(Wcat, C + 2 * H, Fp, Fp, slot(amx, 1))
         # claim the previous layer's ELU link only where the fused data-gradient product will
         # run (per-row scales and the interleaved weight image: see backward)
@@ -404,8 +394,7 @@ class GATLayerFunction(torch.autograd.Function):
                 gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(None, slot(amx, 1)),
                      arows=xr, bil4=wil, role="gat_proj")
             elif amx is not None:
-                gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(slot(*ax), slot(amx, 1)),
-                     bsplit=None if wps[0] is None else wps)
+                gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(slot(*ax), slot(amx, 1)))
             else:
                 gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, algo="bf16")
             elr = Y[:, C:C + 2 * H].contiguous()
@@ -417,7 +406,7 @@ class GATLayerFunction(torch.autograd.Function):
             _lib.call_tag[0] = {"flops": 2 * N * C * Fp}
             call("mvml_gat_proj_fwd", N, ptr(Xp), Fp, Fp, ptr(Wcat), Fp, ptr(attn_lr), H, F, mean_res,
                  _GEMM_ENTRY[algo or GEMM_ALGO][1], ptr(Y), ldy, ptr(elr),
-                 None if ax is None else slot(*ax), slot(amx, 1), ptr(wps[0]), wps[1], wp, wn, st)
+                 None if ax is None else slot(*ax), slot(amx, 1), None, 0, wp, wn, st)
         out_cols = F if mode == MODE_MEAN else HF
         out = torch.empty((N, out_cols), dtype=torch.float32, device=dev)
         E = g.num_edges()
@@ -449,138 +438,11 @@ class GATLayerFunction(torch.autograd.Function):
         ctx.algo = algo
         ctx.amx = amx
         ctx.ax = ax
-        ctx.wps = wps
         ctx.wil = wil
         return out
-
-    @staticmethod
-    def _forward_x(ctx, X, Xp, fc_w, res_w, attn_l, attn_r, attn_lr, bias, g, H, F, slope, mode, C):
-        N, Fin = X.shape
-        Fp = Xp.shape[1]
-        dev = X.device
-        HF = H * F
-        st = _stream(dev)
-        Wcat = torch.empty((C + 2 * H, Fp), dtype=torch.float32, device=dev)
-        call("mvml_gat_fold_weights", ptr(_c(fc_w)), ptr(_c(res_w)), ptr(attn_lr), H, F, Fin, Fp, 0,
-             ptr(Wcat), st)
-        # [X, Wcat, axc, out] maxima; X's per-row maxima recorded on the resident feature tensor
-        amx = torch.zeros(4, dtype=torch.int32, device=dev)
-        xr = known_rows(X)
-        if xr is None:
-            xr = absmax_rows(X, N, Fin, Fin)
-            fold_rows(X, xr)
-        absmax(xr, N, 1, 1, amx, 0)
-        absmax(Wcat, C + 2 * H, Fp, Fp, amx, 1)
-        Wb = torch.empty((HF, 2 * Fp), dtype=torch.float32, device=dev)  # [W_h | Wres_h] rows
-        call("mvml_gat_x_pack_weights", ptr(Wcat), H, F, Fp, ptr(Wb), st)
-        wb_il = split_il4(Wb, HF, 2 * Fp, 2 * Fp, slot(amx, 1))
-        wil = split_il4(Wcat, C + 2 * H, Fp, Fp, slot(amx, 1))  # W_h as the backward's B
-        E = g.num_edges()
-        elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
-        attn = torch.empty((E, H), dtype=torch.float32, device=dev)
-        axc = torch.empty((N, H * 2 * Fp), dtype=torch.float32, device=dev)  # per head [AX_h | X]
-        arows = torch.empty(max(H * N, 1), dtype=torch.int32, device=dev)
-        alr = ctypes.c_void_p(ptr(Wcat).value + 4 * C * Fp)  # [A_l ; A_r]: Wcat's last 2H rows
-        _lib.call_tag[0] = {"layer": f"H{H}xF{F}x", "bytes": 4 * (N * Fp + 2 * N * H + (N + 1) + E
-                                                               + 2 * E * H + N * H * 2 * Fp + H * N)}
-        call("mvml_gat_x_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(Xp), Fp, alr, H, float(slope),
-             ptr(elr), ptr(attn), ptr(axc), ptr(arows), st)
-        absmax(arows, H * N, 1, 1, amx, 2)  # max |axc| (the weight gradient's B scale)
-        out = torch.empty((N, HF), dtype=torch.float32, device=dev)
-        orows = torch.zeros(max(N, 1), dtype=torch.int32, device=dev)
-        act = 2 if mode == MODE_FLATTEN_ELU else 0
-        _lib.call_tag[0] = {"flops": 2 * N * HF * 2 * Fp, "shape": (N, F, 2 * Fp, H)}
-        call("mvml_gemm_f16x2_ex", N, F, 2 * Fp, H, ptr(axc), H * 2 * Fp, 2 * Fp, ptr(Wb), 2 * Fp, 0,
-             ptr(wb_il), F * 2 * Fp, ptr(arows), N, slot(amx, 1), ptr(_c(bias)), F, act, ptr(out), HF, F,
-             None, 0, slot(amx, 3), ptr(orows), 0, 0, 0, st)
-        fold_amax(out, amx, 3)
-        fold_rows(out, orows)
-        ctx.reassoc = True
-        ctx.link = None
-        if act == 2 and ELU_LINK[0]:
-            ctx.link = EluLink(dev)
-            out._mvml_elu = (ctx.link, out._version, (out.data_ptr(), tuple(out.shape), out.stride()))
-        if DEBUG_CAPTURE is not None:
-            DEBUG_CAPTURE.setdefault("elr_fwd", []).append(elr.detach().clone())
-        ctx.save_for_backward(Xp, Wcat, axc, attn, elr, out, attn_l, attn_r, attn_lr)
-        ctx.Fin = Fin
-        ctx.g, ctx.H, ctx.F, ctx.slope, ctx.mode = g, H, F, slope, mode
-        ctx.amx = amx
-        ctx.wil = wil
-        return out
-
-    @staticmethod
-    def _backward_x(ctx, g_out):
-        Xp, Wcat, axc, attn, elr, out, attn_l, attn_r, attn_lr = ctx.saved_tensors
-        g, H, F, mode = ctx.g, ctx.H, ctx.F, ctx.mode
-        N, Fp = Xp.shape
-        Fin = ctx.Fin
-        dev = Xp.device
-        HF = H * F
-        C = 2 * HF
-        st = _stream(dev)
-        amx = ctx.amx
-        link = ctx.link
-        if link is not None and link.claimed:
-            # the next layer's data-gradient GEMM already applied ELU' and folded max |g_rst|
-            gr = link.g_rst
-            if gr is None or g_out.data_ptr() != gr.data_ptr() or g_out.shape != gr.shape \
-                    or g_out.stride() != gr.stride():
-                raise RuntimeError("GAT ELU link: the gradient reaching the first layer is not the one "
-                                   "the next layer's fused ELU backward wrote (was its output also "
-                                   "consumed elsewhere?)")
-            g_rst, ga = g_out, link.amax
-        else:
-            g_out = _c(g_out)
-            ga = torch.zeros(1, dtype=torch.int32, device=dev)
-            if mode == MODE_FLATTEN_ELU:
-                g_rst = torch.empty((N, HF), dtype=torch.float32, device=dev)
-                call("mvml_gat_elu_bwd", N * HF, ptr(g_out), ptr(out), ptr(g_rst), ptr(ga), st)
-            else:
-                g_rst = g_out
-                absmax(g_rst, N, HF, HF, ga, 0)
-        gp = slot(ga, 0)
-        # dAX_h = g_rst_h W_h: one strided batch over the heads (B = Wcat's rows h F .., K-major)
-        dax = torch.empty((N, H * Fp), dtype=torch.float32, device=dev)
-        _lib.call_tag[0] = {"flops": 2 * N * Fp * F * H, "shape": (N, Fp, F, H)}
-        call("mvml_gemm_f16x2_batched", 0, 1, N, Fp, F, H, ptr(g_rst), HF, F, ptr(Wcat), Fp, F * Fp,
-             gp, slot(amx, 1), ptr(dax), H * Fp, Fp, st)
-        E = g.num_edges()
-        gpre = torch.empty((E, H), dtype=torch.float32, device=dev)
-        gelr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
-        gl = torch.zeros(1, dtype=torch.int32, device=dev)
-        _lib.call_tag[0] = {"layer": f"H{H}xF{F}x", "bytes": 4 * (N * H * Fp + 2 * E * Fp // 1 + 2 * N * H
-                                                               + 3 * E * H + 2 * (N + 1) + 3 * E)}
-        call("mvml_gat_x_bwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(g.out_rowptr), ptr(g.out_inslot),
-             ptr(Xp), Fp, ptr(elr), ptr(attn), H, float(ctx.slope), ptr(dax), ptr(gpre), ptr(gelr),
-             ptr(gl), st)
-        # dL/dWcat in the projection path's layout [fc | res_fc | A_l | A_r] rows
-        gW = torch.empty((C + 2 * H, Fp), dtype=torch.float32, device=dev)
-        # [dL/dW_h | dL/dWres_h] = g_rst_h^T [AX_h | X]: one split-K product per head over its
-        # whole [AX_h | X] block (the res_fc gradient rows come out of the same pass)
-        gWh = torch.empty((H, F, 2 * Fp), dtype=torch.float32, device=dev)
-        for h in range(H):
-            gemm(g_rst[:, h * F:], axc[:, h * 2 * Fp:], F, 2 * Fp, N, 1, 1, HF, H * 2 * Fp, gWh[h], 2 * Fp,
-                 amax=(gp, slot(amx, 2)))
-        gW[:HF].view(H, F, Fp).copy_(gWh[:, :, :Fp])
-        gW[HF:C].view(H, F, Fp).copy_(gWh[:, :, Fp:])
-        gemm(gelr, Xp, 2 * H, Fp, N, 1, 1, 2 * H, Fp, gW[C:], Fp, amax=(slot(gl, 0), slot(amx, 0)))
-        g_fc = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
-        g_res = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
-        call("mvml_gat_unfold_grads", ptr(gW), ptr(attn_lr), H, F, Fin, Fp, 0, ptr(g_fc), ptr(g_res), st)
-        g_alr = torch.empty((2, HF), dtype=torch.float32, device=dev)
-        gemm_batched(gW[C:], Wcat, 2, F, Fp, 0, 0, H * Fp, Fp, g_alr, HF, H, Fp, F * Fp, F)
-        if DEBUG_CAPTURE is not None:
-            DEBUG_CAPTURE.update(elr=elr, gelr=gelr, attn=attn)
-        g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
-        colsum(g_rst, N, HF, HF, g_bias)
-        return (None, g_fc, g_res, g_alr[0].view_as(attn_l), g_alr[1].view_as(attn_r), g_bias,
-                None, None, None, None, None, None)
 
     @staticmethod
     def backward(ctx, g_out):
-        if ctx.reassoc:
-            return GATLayerFunction._backward_x(ctx, g_out)
         Xp, Wcat, Y, attn, elr, out, attn_l, attn_r, attn_lr = ctx.saved_tensors
         g, H, F, mode, ldy = ctx.g, ctx.H, ctx.F, ctx.mode, ctx.ldy
         link = ctx.link
@@ -671,8 +533,7 @@ class GATLayerFunction(torch.autograd.Function):
                      arows=gyr if gyr is not None else absmax_rows(gY, N, CE, ldg), bil4=ctx.wil)
             else:
                 gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, algo=ctx.algo,
-                     amax=None if amx is None else (slot(amx, 2), slot(amx, 1)),
-                     bsplit=None if ctx.wps[0] is None else ctx.wps)
+                     amax=None if amx is None else (slot(amx, 2), slot(amx, 1)))
         return gX, g_fc, g_res, g_al, g_ar, g_bias, None, None, None, None, None, None
 
 
@@ -739,13 +600,11 @@ class Set2SetFunction(torch.autograd.Function):
             amax_w = torch.empty(Lr, dtype=torch.int32, device=dev)
             for l in range(Lr):
                 absmax(Wcat[l], 4 * D, kin[l] + D, kin[l] + D, amax_w, l)  # = Wperm's max
-            # the gates' weights split once per forward (the fused path reads Wperm's planes, the
-            # unfused one Wcat's: the same values per element, so the same products)
-            wsp = [split_planes(Wperm[l] if CELL_EPI else Wcat[l], 4 * D, kin[l] + D, kin[l] + D,
-                                slot(amax_w, l)) for l in range(Lr)]
-            if wsp[0][0] is None:  # the interleaved image instead (w_plane = 0)
-                wsp = [(split_il4(Wperm[l] if CELL_EPI else Wcat[l], 4 * D, kin[l] + D, kin[l] + D,
-                                  slot(amax_w, l)), 0) for l in range(Lr)]
+            # the gates' weights split once per forward into the interleaved image (the fused path
+            # reads Wperm's, the unfused one Wcat's: the same values per element, so the same
+            # products; w_plane = 0)
+            wsp = [(split_il4(Wperm[l] if CELL_EPI else Wcat[l], 4 * D, kin[l] + D, kin[l] + D,
+                              slot(amax_w, l)), 0) for l in range(Lr)]
         for t in range(T):
             for l in range(Lr):
                 w_ih, w_hh, b_ih, b_hh = W[l]
@@ -769,7 +628,6 @@ class Set2SetFunction(torch.autograd.Function):
                 else:
                     gemm(XH[l][t], Wcat[l], B, 4 * D, K, 0, 0, kin[l] + D, kin[l] + D, gates, 4 * D,
                          amax=None if amax_x is None else (slot(amax_x, 0), slot(amax_w, l)),
-                         bsplit=None if CELL_EPI or wsp[l][0] is None or wsp[l][1] == 0 else wsp[l],
                          arows=mrows,
                          bil4=wsp[l][0] if not CELL_EPI and wsp[l][1] == 0 else None)
                 call("mvml_lstm_cell_fwd", B, D, ptr(gates), ptr(b_ih), ptr(b_hh), ptr(c_prev),
@@ -824,12 +682,8 @@ class Set2SetFunction(torch.autograd.Function):
         # running value bounds every cell seen so far, which is all a scale needs)
         amax_x, amax_w = ctx.amax
         amax_g = torch.zeros(Lr, dtype=torch.int32, device=dev) if amax_x is not None else None
-        wsb = [None] * Lr  # [W_ih | W_hh] split once for the per-cell data-gradient products
-        wib = [None] * Lr  # ... as the interleaved image (BSPLIT_IL)
-        if amax_g is not None and BSPLIT:
-            wsb = [split_planes(Wcat[l], 4 * D, Wcat[l].shape[1], Wcat[l].shape[1], slot(amax_w, l))
-                   for l in range(Lr)]
-        elif amax_g is not None:
+        wib = [None] * Lr  # [W_ih | W_hh] split once (interleaved image) for the per-cell data-gradient products
+        if amax_g is not None:
             wib = [split_il4(Wcat[l], 4 * D, Wcat[l].shape[1], Wcat[l].shape[1], slot(amax_w, l))
                    for l in range(Lr)]
         for t in range(T - 1, -1, -1):
@@ -842,11 +696,13 @@ class Set2SetFunction(torch.autograd.Function):
                     gh, ldgh = g_h, D
                 else:
                     gh, ldgh = gxh[l + 1][:, :D], 2 * D  # dL/dh_l(t) from layer l+1's input
-                if t < T - 1:  # dL/dh_l(t) through the recurrence at step t+1
-                    gh.add_(g_qs3[t][:, 2 * D:] if l == 0 else gxh[l][:, D:])
+                gh2, ldgh2 = None, 0
+                if t < T - 1:  # + dL/dh_l(t) through the recurrence at step t+1 (summed in the kernel)
+                    gh2, ldgh2 = (g_qs3[t][:, 2 * D:], 3 * D) if l == 0 else (gxh[l][:, D:], 2 * D)
                 c_prev = cs[t - 1, l] if t > 0 else None
                 g_gates = g_gates_all[l, t]
                 call("mvml_lstm_cell_bwd", B, D, ptr(acts[t, l]), ptr(cs[t, l]), ptr(c_prev), ptr(gh), ldgh,
+                     ptr(gh2), ldgh2,
                      ptr(g_c[l]) if t < T - 1 else None, ptr(g_gates), ptr(g_c_new), slot(amax_g, l),
                      ptr(gb_part[l, t]), st)
                 g_c[l], g_c_new = g_c_new, g_c[l]
@@ -859,7 +715,7 @@ class Set2SetFunction(torch.autograd.Function):
                     # 64-molecule group's gradients, so the cells' rows span little)
                     gemm(g_gates, Wcat[l], B, ncols, 4 * D, 0, 1, 4 * D, kin + D, out, ldo,
                          amax=None if amax_g is None else (slot(amax_g, l), slot(amax_w, l)),
-                         bsplit=wsb[l], bil4=wib[l])
+                         bil4=wib[l])
         # weight / bias gradients, one product per parameter over all steps:
         #   dW_ih[l] = sum_t g_gates[l,t]^T x_l(t),  dW_hh[l] = sum_{t>=1} g_gates[l,t]^T h_l(t-1)
         # (layer 0's input x_0(t) = q*_{t-1} is zero at t = 0; h_l(-1) = 0)

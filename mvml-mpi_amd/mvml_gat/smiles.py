@@ -298,7 +298,7 @@ class BiLSTMLayerFunction(torch.autograd.Function):
                     c_prev = c[tp] if 0 <= tp < T else None
                     g_c = carry[k % 2] if nxt is not None else None
                     call("mvml_lstm_cell_bwd", bs, H, ptr(act[t]), ptr(c[t]), ptr(c_prev),
-                         ptr(g[t, :, d * H:]), 2 * H, ptr(g_c), ptr(gg[t]), ptr(carry[(k + 1) % 2]),
+                         ptr(g[t, :, d * H:]), 2 * H, None, 0, ptr(g_c), ptr(gg[t]), ptr(carry[(k + 1) % 2]),
                          slot(amg, d), None, st)
                     nxt, k = t, k + 1
         # weight / input gradients: GEMMs over every position — on the wide path over the live

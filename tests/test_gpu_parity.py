@@ -208,21 +208,6 @@ def test_gemm_f16x2_scales(sa, sb):
         _lib.call("mvml_gemm_f16x2_amax", 0, 0, M, N, K, ptr(Ad), K, ptr(Bd), K, slot(amx, 0),
                   slot(amx, 1), None, 0.0, 0, ptr(C2), N, wp, wn, _stream(C2.device))
     assert torch.equal(C, C2)
-    # B split once into planes (mvml_split_f16x2 + mvml_gemm_f16x2_bsplit): the same values
-    # per element as the tiles' own split, so the same products, bit for bit
-    from mvml_gat.functional import split_planes
-    import mvml_gat.functional as Fn
-    old = Fn.BSPLIT
-    Fn.BSPLIT = True
-    try:
-        planes = split_planes(Bd, N, K, K, slot(amx, 1))
-    finally:
-        Fn.BSPLIT = old
-    C3 = torch.zeros(M, N, device=DEV)
-    with _x3_tile("f16x2-256") as a:
-        gemm(Ad, Bd, M, N, K, 0, 0, K, K, C3, N, algo=a, amax=(slot(amx, 0), slot(amx, 1)),
-             bsplit=planes)
-    assert torch.equal(C, C3)
 
 
 @pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 0), (1, 1)])

@@ -150,8 +150,7 @@ def test_gnn_module_config3_graphnorm_groups():
 
 
 def _layer_case(layer, sb, seed=0, x_grad=True):
-    """x_grad=False (layer 0, the atom features as GNNModule feeds them): no input gradient, so
-    the re-associated first-layer path runs (functional.REASSOC_X; asserted)."""
+    """x_grad=False: layer 0 as GNNModule runs it, on the atom features (no input gradient)."""
     prod, ref = model_pair(seed=seed)
     conv_p = prod.conv.gnn_layers[layer]
     conv_r = ref.conv.gnn_layers[layer].gat_conv
@@ -171,8 +170,6 @@ def _layer_case(layer, sb, seed=0, x_grad=True):
     gdev = sb.to_graph().to(DEV)
     Xp = X.float().to(DEV).requires_grad_(x_grad)
     out_p, elrs = _capture(lambda: conv_p(gdev, Xp))
-    assert out_p.grad_fn.reassoc == (not x_grad and Fn.REASSOC_X and Fn.GEMM_ALGO == "f16x2"
-                                     and Fn.ROW_SCALES and Fn.PROJ_ELR_GEMM)
     br = _branches(gd, elrs)
     _check_kink_flips(gd, br, [X], [p64])
     Xr = X.clone().requires_grad_()
@@ -218,15 +215,21 @@ _FAMILIES = {"config2": lambda: synth.config2(128, seed=0),
              "config3": lambda: synth.config3(192, seed=4)}
 
 
+@pytest.mark.parametrize("kind", [1, 2])
 @pytest.mark.parametrize("case", list(_FAMILIES))
 @pytest.mark.parametrize("layer", [0, 1])
-def test_gat_layer_dst_fwd(case, layer):
-    """Option dst_fwd = 1 (aggregation forward by destination wave, every atom; csrc/gat_agg.hip
-    gat_agg_fwd_dst_kernel) with, for the flatten layer, the one-pass source-atom backward
-    (flat_src = 2, gat_flat_bwd_src1_kernel): forward and every gradient against float64 on each
-    graph family (hubs of in-degree past 64: the softmax's multi-chunk path)."""
+def test_gat_layer_dst_fwd(case, layer, kind, monkeypatch):
+    """The aggregation forward by destination wave (csrc/gat_agg.hip gat_agg_fwd_dst_kernel),
+    FORCED to each kind through the layer (GATLayerFunction picks the kind per call from the
+    batch, functional._fwd_path, so the option alone is overridden): kind 1 fuses the edge
+    softmax, kind 2 runs it first as its own launch (gat_softmax_dst4_kernel).  With, for the
+    flatten layer, the one-pass source-atom backward (flat_src = 2): forward and every gradient
+    against float64 on each graph family (hubs of in-degree past 64: the softmax's multi-chunk
+    path and the logit recomputation past the cached in-edges)."""
+    monkeypatch.setattr(Fn, "DST_FWD_POLICY", "all")
+    monkeypatch.setattr(Fn, "DST_FWD_KIND", kind)
     sb = _FAMILIES[case]()
-    with option("dst_fwd", 1), option("flat_src", 2 if layer == 0 else 0):
+    with option("flat_src", 2 if layer == 0 else 0):
         _layer_case(layer, sb, seed=8 + layer)
 
 
@@ -275,7 +278,25 @@ def test_dst_fwd_bitwise_molecule_windows(case, mode):
     F = 192 if mode == 0 else 384
     with option("dst_fwd", 0):
         a = _agg_outputs(sb, 4, F, mode)
+    for kind in (1, 2):  # softmax fused / softmax as its own launch first
+        with option("dst_fwd", kind):
+            b = _agg_outputs(sb, 4, F, mode)
+        for i in (0, 1, 3, 4):
+            assert torch.equal(a[i], b[i]), (kind, i, (a[i].double() - b[i].double()).abs().max().item())
+
+
+@pytest.mark.parametrize("case", ["hubs", "table_overflow", "config5"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_dst_fwd_kinds_bitwise_hubs(case, mode):
+    """On hub molecules (in-degrees past the 6 cached in-edges and past 64: the softmax kernel's
+    logit recomputation and the gather kernel's SM = false path over long rows) the two
+    destination-wave kinds give BITWISE the same out, attn and output maxima: the softmax as its
+    own launch (kind 2) follows the fused softmax's (kind 1) arithmetic and edge order."""
+    sb = _FAMILIES[case]()
+    F = 192 if mode == 0 else 384
     with option("dst_fwd", 1):
+        a = _agg_outputs(sb, 4, F, mode)
+    with option("dst_fwd", 2):
         b = _agg_outputs(sb, 4, F, mode)
     for i in (0, 1, 3, 4):
         assert torch.equal(a[i], b[i]), (i, (a[i].double() - b[i].double()).abs().max().item())
@@ -321,19 +342,15 @@ def test_gat_layer0_hubs_flatten_elu(monkeypatch):
 
 @pytest.mark.parametrize("case", ["config2", "hubs", "config5", "config5_three", "table_overflow",
                                   "config3"])
-def test_gat_layer0_reassociated(case, monkeypatch):
-    """The first layer as GNNModule runs it (no input gradient): edge softmax + aggregation over
-    the 76-wide feature rows and one batched GEMM per head (mvml_gat_x_fwd, mvml_gemm_f16x2_ex),
-    backward through dAX = g_rst W_h (mvml_gat_x_bwd) — every output and gradient against float64
-    on each graph family the projection path's kernels are tested on (the re-associated kernels
-    have no size classes: one code path for any molecule)."""
+def test_gat_layer0_no_input_grad(case):
+    """The first layer as GNNModule runs it (no input gradient: the dX product is skipped) —
+    every output and gradient against float64 on each graph family."""
     sb = {"config2": lambda: synth.config2(128, seed=0),
           "hubs": lambda: batch_of_sizes([150, 90, 210], seed=7, hubs=True),
           "config5": lambda: synth.config5(2, seed=3),
           "config5_three": lambda: synth.config5(3, seed=5),
           "table_overflow": lambda: batch_of_sizes([300, 40], seed=9, hubs=True, n_hubs=7, partners=109),
           "config3": lambda: synth.config3(192, seed=4)}[case]()
-    monkeypatch.setattr(Fn, "REASSOC_X", True)  # (off by default: measured slower)
     _layer_case(0, sb, seed=11, x_grad=False)
 
 

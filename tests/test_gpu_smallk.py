@@ -1,8 +1,8 @@
 """Small-K split-fp16 products (gemm_smallk_kernel behind mvml_gemm_f16x2_rows):
 layer 1's projection X [N_atoms, 76] x Wcat [1544, 76]^T as a wave-per-64-columns memory kernel.
 
-Checks, on ragged shapes (M, N not multiples of the 16-row block / 64-column slab; K = 4 .. 80,
-every k-step count 1 .. 5 incl. the 16-deep tail) with rows spread over 2^-28 .. 2^12:
+Checks, on ragged shapes (M, N not multiples of the 16-row block / 64-column slab; K = 4 .. 96,
+every k-step count 1 .. 6 incl. the 16-deep tail) with rows spread over 2^-28 .. 2^12:
   * every row within 1e-5 of the float64 product relative to its own max (the tiles' bar);
   * the 256x256 tile path (option smallk = 0) agrees to fp32-GEMM accuracy (not bitwise: the
     MFMA shape changes the summation order);
@@ -21,7 +21,9 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 TOL = 1e-5
 SHAPES = [(1, 4, 4), (17, 8, 12), (1000, 68, 76), (4099, 1544, 76), (300, 60, 80), (2000, 200, 16),
-          (513, 64, 32), (77, 100, 44), (130, 1548, 64), (40, 12, 48)]
+          (513, 64, 32), (77, 100, 44), (130, 1548, 64), (40, 12, 48),
+          # K 84 .. 96: the KS16 = 6 plan (three 16x16x32 steps, no 16-deep tail)
+          (1000, 200, 84), (333, 1544, 92), (2048, 64, 96)]
 
 
 def _inputs(M, N, K, seed):

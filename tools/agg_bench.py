@@ -27,56 +27,6 @@ def timeit(fn, it=10):
     return s.elapsed_time(e) / it
 
 
-def bench_x(a, g, N, E, st, H=4, F=192, Fin=74):
-    """The re-associated first layer (csrc/gat_x.hip): mvml_gat_x_fwd (el / er + edge softmax +
-    aggregation over the 76-wide feature rows) alone, then the whole layer forward (and
-    forward + backward) through mvml_gat.nn.GATLayer as GNNModule runs it."""
-    from mvml_gat import nn as mnn
-    from mvml_gat import functional as Fn
-    Fp = (Fin + 3) // 4 * 4
-    X = torch.nn.functional.pad(torch.rand((N, Fin), device="cuda"), (0, Fp - Fin))
-    alr = torch.randn((2 * H, Fp), device="cuda") * 0.1
-    elr = torch.empty((N, 2 * H), device="cuda")
-    attn = torch.empty((E, H), device="cuda")
-    axc = torch.empty((N, H * 2 * Fp), device="cuda")
-    arows = torch.empty(H * N, dtype=torch.int32, device="cuda")
-    f = lambda: call("mvml_gat_x_fwd", N, ptr(g.in_rowptr), ptr(g.in_src), ptr(X), Fp, ptr(alr), H, 0.2,
-                     ptr(elr), ptr(attn), ptr(axc), ptr(arows), st)
-    ms = timeit(f)
-    by = 4 * (N * Fp + 2 * N * H + (N + 1) + E + 2 * E * H + N * H * 2 * Fp + H * N)
-    print(f"  gat_x_fwd L1 (re-assoc) {ms:7.3f} ms  {by / 1e9:6.2f} GB  {by / ms / 1e6:7.1f} GB/s")
-    del X, alr, elr, attn, axc, arows
-    torch.manual_seed(0)
-    layer = mnn.GATLayer(Fin, F, H, 0.0, 0.0, 0.2, True, "flatten", torch.nn.functional.elu).cuda()
-    X = torch.rand((N, Fin), device="cuda")
-    with torch.no_grad():
-        ms = timeit(lambda: layer(g, X))
-    print(f"  layer L1 fwd (re-assoc={int(Fn.REASSOC_X)}) {ms:7.3f} ms  (GATConv forward: softmax, "
-          f"aggregation, per-head GEMM + bias + ELU)")
-    gout = torch.randn((N, H * F), device="cuda")
-    def fb():
-        layer.zero_grad(set_to_none=True)
-        layer(g, X).backward(gout)
-    ms = timeit(fb)
-    print(f"  layer L1 fwd+bwd (re-assoc={int(Fn.REASSOC_X)}) {ms:7.3f} ms")
-    del X, gout, layer
-    # the backward's dAX_h = g_rst_h W_h product alone, per GEMM tile plan
-    from mvml_gat._lib import option
-    from mvml_gat.functional import absmax, slot
-    g_rst = torch.randn((N, H * F), device="cuda")
-    W = torch.randn((H * F, Fp), device="cuda") * 0.1
-    dax = torch.empty((N, H * Fp), device="cuda")
-    mx = torch.zeros(2, dtype=torch.int32, device="cuda")
-    absmax(g_rst, N, H * F, H * F, mx, 0)
-    absmax(W, H * F, Fp, Fp, mx, 1)
-    for tile in (0, 128, 256):
-        with option("gemm_tile", tile):
-            ms = timeit(lambda: call("mvml_gemm_f16x2_batched", 0, 1, N, Fp, F, H, ptr(g_rst), H * F, F, ptr(W),
-                                     Fp, F * Fp, slot(mx, 0), slot(mx, 1), ptr(dax), H * Fp, Fp, st))
-        print(f"  dAX batched GEMM (N={N}, {Fp}, {F}) x {H}, tile {tile}: {ms:7.3f} ms")
-    del g_rst, W, dax
-
-
 def bench_layer(a, g, N, E, st, L, H, F, mode, name):
     """One layer's aggregation forward (and backward) on seeded inputs; returns (out, attn, gY)."""
     torch.manual_seed(0)
@@ -141,9 +91,7 @@ def main():
     # "2": layer 1 as the GNN runs it on large batches with the ELU link (mode 2: the next
     # layer's GEMM applied ELU', so the backward reads no `out`)
     layers = ((4, 192, 0, "L1 flatten+ELU"), (4, 384, 1, "L2 mean"), (4, 192, 2, "L1 flatten (link)"))
-    if "x" in a.layers:
-        bench_x(a, g, N, E, st)
-    for (H, F, mode, name) in [layers[int(i)] for i in a.layers if i != "x"]:
+    for (H, F, mode, name) in [layers[int(i)] for i in a.layers]:
         ref = None
         for opts in sets:
             with contextlib.ExitStack() as es:
