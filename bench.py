@@ -52,7 +52,7 @@ TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32
          "mvml_token_attn_fold_bwd", "mvml_gemm_f32x3_batched", "mvml_conv3_fwd", "mvml_conv3_bwd",
          "mvml_bce_logits", "mvml_gat_attn_grad", "mvml_bilstm_seq_fwd", "mvml_bilstm_seq_bwd", "mvml_bilstm_wide_fwd", "mvml_bilstm_wide_bwd",
          "mvml_lstm_gates_cell_fwd", "mvml_gemm_f16x2", "mvml_gemm_f16x2_amax", "mvml_absmax_f32",
-         "mvml_gemm_f16x2_bsplit", "mvml_split_f16x2", "mvml_attn_conv_fwd", "mvml_attn_conv_bwd",
+         "mvml_gemm_f16x2_bsplit", "mvml_attn_conv_fwd", "mvml_attn_conv_bwd",
          "mvml_bilstm_wide_step_fwd", "mvml_bilstm_wide_step_bwd", "mvml_bilstm_pack_rows",
          "mvml_bilstm_gather_rows", "mvml_bilstm_token_grad", "mvml_bilstm_select_last",
          "mvml_bilstm_token_grad_packed", "mvml_bilstm_packed_tokens", "mvml_gemm_f16x2_rows",

@@ -271,15 +271,10 @@ int mvml_gemm_f16x2_planes(int64_t M, int64_t N, int64_t K, const float* A, int6
  * one writer per row, no atomics. */
 int mvml_absmax_rows_f32(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32_t* out,
                          int accumulate, void* stream);
-/* Split an fp32 matrix once into the two scaled fp16 planes the split-fp16 GEMM stages
- * (hi at planes, lo at planes + rows * ld, both [rows][ld]; scale from *amax, as the GEMM's own
- * split): a weight operand read by many tiles / products is then split once per step.
- * cols % 4 == 0, ld % 4 == 0, P 16-B and planes 8-B aligned. */
-int mvml_split_f16x2(int64_t rows, int64_t cols, const float* P, int64_t ld, const uint32_t* amax,
-                     uint16_t* planes, void* stream);
-/* mvml_gemm_f16x2_amax with B also given as its pre-split planes (b_plane elements apart, the
- * same [.][ldb] indexing as B, split with *amax_b): the 256x256 tiles read the planes; plans
- * that do not use that kernel read the fp32 B. */
+/* mvml_gemm_f16x2_amax with B also given as its interleaved split image (b_planes, from
+ * mvml_split_f16x2_il4 with *amax_b, the same [.][ldb] indexing as B; b_plane must be 0 — the
+ * two-plane layout was removed in round 6): the 256x256 tiles read the image; plans that do not
+ * use that kernel read the fp32 B. */
 int mvml_gemm_f16x2_bsplit(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                            const float* A, int64_t lda, const float* B, int64_t ldb,
                            const uint16_t* b_planes, int64_t b_plane, const uint32_t* amax_a,
@@ -332,8 +327,8 @@ int mvml_gat_unfold_grads(const float* gWcat, const float* attn_lr, int H, int F
  * of the fp32 Z tile and summed per head in fixed order — no second pass over Z.
  * attn_lr: [2, H*F] = [attn_l | attn_r]; elr: [N, 2H] = [el | er].  F % 32 == 0.
  * algo MVML_GEMM_F16X2: amax_x / amax_w = bits of max |X| / max |Wcat| (mvml_absmax_f32), or
- * both NULL (computed here); w_planes (may be NULL, needs both maxima): Wcat split once by
- * mvml_split_f16x2 with amax_w (w_plane elements between its planes), read instead of Wcat.
+ * both NULL (computed here); w_planes must be NULL (w_plane ignored: the two-plane weight image
+ * was removed in round 6).
  * workspace: mvml_gat_proj_fwd_workspace_size(N, H, F) bytes. */
 size_t mvml_gat_proj_fwd_workspace_size(int64_t num_nodes, int H, int F);
 int mvml_gat_proj_fwd(int64_t num_nodes, const float* X, int64_t ldx, int64_t K,
@@ -440,9 +435,9 @@ int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float* A, int64_
                                split-bf16; else split-fp16 with these |A|, |w_perm| max bits */,
                              const uint32_t* amax_a_rows /* NULL, or per-row |A| max bits (M
                                entries; replaces amax_a, see mvml_gemm_f16x2_rows) */,
-                             const uint16_t* w_planes, int64_t w_plane /* NULL, or w_perm
-                               pre-split by mvml_split_f16x2 with amax_b; w_plane = 0: the
-                               interleaved image of mvml_split_f16x2_il4 */,
+                             const uint16_t* w_planes, int64_t w_plane /* NULL, or w_perm's
+                               interleaved image (mvml_split_f16x2_il4 with amax_b; w_plane
+                               must be 0) */,
                              void* stream);
 /* Per molecule b: out_bits[b] = max(floor_bits, max_{n in [node_offsets[b], node_offsets[b+1])}
  * in_bits[n]) on non-negative float bits — a molecule's bound from its atoms' row maxima (the

@@ -1045,10 +1045,10 @@ struct XOp {
 // stage guarded.
 // NP = 3: fp32-accurate split-bf16 (six MFMAs per fragment pair); NP = 1: bf16 operands
 // (one MFMA per pair, fp32 accumulate) — the bf16 projection of BASELINE config 4.
-// BPS (split-fp16, FAST only): B points at the two fp16 planes of a pre-split operand
-// (mvml_split_f16x2, amax.b_plane elements apart) instead of fp32 values: a B piece is loaded
-// as two 8-B plane reads and stored to LDS unsplit — the weights are split once per step
-// instead of once per tile.
+// BPS = 2 (split-fp16, FAST only): B points at the interleaved split image of the operand
+// (mvml_split_f16x2_il4: [4 high | 4 low] fp16 per 16-B piece) instead of fp32 values: a B
+// piece is one 16-B load stored to the LDS planes unsplit — the weights are split once per
+// step instead of once per tile.
 // ROWS (split-fp16, K-contiguous A): per-row A maxima (amax.a_rows), a scale per A row; a
 // separate instantiation so that the operand-wide kernels keep their register allocation (one
 // spill reload inside the main loop costs a vmcnt drain per stage).
@@ -1082,18 +1082,12 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   using OA = XOp<AK, NP>;
   using OB = XOp<BKM, NP>;
   static_assert(!BPS || (NP == 2 && FAST), "pre-split B: split-fp16 fast path only");
-  // B piece at float-indexed address p: fp32 values, (BPS 1) the two planes' 8-B pieces, or
+  // B piece at float-indexed address p: fp32 values, or
   // (BPS 2) the interleaved image's 16-B piece [4 high | 4 low] (mvml_split_f16x2_il4: the same
   // float indexing as the fp32 operand, one load per piece like fp32)
   auto ldb4 = [&](const float* p) -> float4 {
     if constexpr (BPS == 2) {
       return *reinterpret_cast<const float4*>(p);
-    } else if constexpr (BPS == 1) {
-      const uint16_t* q = reinterpret_cast<const uint16_t*>(B) + (p - B);
-      const uint2 h = *reinterpret_cast<const uint2*>(q);
-      const uint2 l = *reinterpret_cast<const uint2*>(q + amax.b_plane);
-      return make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(l.x),
-                         __uint_as_float(l.y));
     } else {
       return *reinterpret_cast<const float4*>(p);
     }
@@ -1531,265 +1525,6 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   }  // tile loop
 }
 
-// ---- split-fp16 GEMM with an LDS-DMA ring (round 3) -------------------------------------
-// gemm_x3w_kernel<NP = 2> stages its operands through registers (load -> split -> two fp16
-// planes -> LDS) one 16-deep stage ahead, so every stage starts with a vmcnt(0) on loads issued
-// one stage (~4 K cycles) earlier: at 1-2 us of loaded HBM latency its matrix pipe idled about
-// two thirds of the time (SQ_VALU_MFMA_BUSY_CYCLES = 32 x MFMAs, 0.35 of the SIMD cycles on the
-// L2 dX shape, profiles/r03_pmc_gemm_*).  A second stage of registers does not fit (PF2 spills
-// ~500 VGPRs).  This kernel moves the fp32 tiles global -> LDS with global_load_lds_dwordx4
-// (no registers), kGBuf = 4 stages deep (three in flight behind the one being read), and every
-// wave splits its OWN fragments after reading them from LDS: the same bytes cross LDS (fp32 =
-// two fp16 planes), the split VALU triples (each A value is split by the 4 waves sharing its
-// rows, each B value by 2) but runs beside the MFMAs, and the load latency is covered by three
-// stages.  Same tile (256 x 256, 8 waves of 128 x 64), same split (split2h), same MFMA order
-// per k-step (l_a h_b, h_a l_b, h_a h_b) and the same k order as gemm_x3w_kernel<NP = 2>, so
-// the results are bit-identical to it.
-//   * K-contiguous operand (rows x k): stage image [256 rows][16 fp32] (64-B rows), the 16-B
-//     chunk index XOR-swizzled by (row >> 2) & 3 through the glds SOURCE address (the LDS side
-//     of a glds is lane-linear); a lane's fragment (row, 8 k) is two ds_read_b128, conflict-free.
-//   * K-major operand (k x rows, rows contiguous): image [16 k][256 fp32] with a 1040-B k-row
-//     pitch (k-rows 8 apart land 32 banks apart); a fragment is eight ds_read_b32.
-// Fragment reads are inline asm (the compiler would otherwise wait vmcnt(0) — draining the
-// ring — before every ds_read of LDS a glds writes); waits are explicit: vmcnt(4 x stages
-// still allowed in flight), lgkmcnt(0), then a raw s_barrier.  A K tail (the last stage, when
-// (kend - kbeg) % 16 != 0) is filled synchronously with zero-filled register loads.
-constexpr int kGBuf = 4;
-constexpr int kGKPitch = 1040;
-
-template <bool KMAJ>
-struct GOp {
-  static constexpr int kBytes = KMAJ ? XBK * kGKPitch : 256 * 64;
-  __device__ static __forceinline__ int swz(int row) { return (row >> 2) & 3; }
-
-  // This thread's two 1-KB pieces of a stage (wave w: pieces 2w, 2w + 1) by LDS-DMA.
-  __device__ static __forceinline__ void issue(const float* __restrict__ P, int64_t ld, int64_t r0,
-                                               int64_t rows, int64_t k0, uint8_t* op, int wid,
-                                               int lane) {
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int inst = 2 * wid + it;
-      const float* src;
-      uint8_t* dst;
-      if (!KMAJ) {
-        const int row = 16 * inst + (lane >> 2);
-        const int gc = (lane & 3) ^ swz(row);
-        src = P + min(r0 + row, rows - 1) * ld + k0 + 4 * gc;  // rows past the edge: never stored
-        dst = op + inst * 1024;
-      } else {  // rows % 4 == 0 (host): a piece past the edge re-reads the last in-range piece
-        src = P + (k0 + inst) * ld + min(r0 + 4 * lane, rows - 4);
-        dst = op + inst * kGKPitch;
-      }
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-    }
-  }
-
-  // The same two pieces through registers, zero outside rows / [k0, kend) (the K tail).
-  __device__ static __forceinline__ void fill_guarded(const float* __restrict__ P, int64_t ld,
-                                                      int64_t r0, int64_t rows, int64_t k0,
-                                                      int64_t kend, uint8_t* op, int wid,
-                                                      int lane) {
-    float4 v[2];
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int inst = 2 * wid + it;
-      float e[4] = {0.f, 0.f, 0.f, 0.f};
-      if (!KMAJ) {
-        const int row = 16 * inst + (lane >> 2);
-        const int64_t gr = r0 + row, gk = k0 + 4 * ((lane & 3) ^ swz(row));
-        if (gr < rows)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (gk + j < kend) e[j] = P[gr * ld + gk + j];
-      } else {
-        const int64_t gk = k0 + inst, gr = r0 + 4 * lane;
-        if (gk < kend)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (gr + j < rows) e[j] = P[gk * ld + gr + j];
-      }
-      v[it] = make_float4(e[0], e[1], e[2], e[3]);
-    }
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int inst = 2 * wid + it;
-      *reinterpret_cast<float4*>(op + (KMAJ ? inst * kGKPitch : inst * 1024) + lane * 16) = v[it];
-    }
-  }
-
-  // LDS byte offsets (within a stage image) of this lane's fragment of rows R0 .. R0 + 31:
-  // the lane's row R0 + (lane & 31), k = 8 (lane >> 5) + [0, 4) (lo) and + [4, 8) (hi; used
-  // by the K-contiguous image only).
-  __device__ static __forceinline__ uint32_t frag_off(int R0, int lane, int half = 0) {
-    const int row = R0 + (lane & 31), j = lane >> 5;
-    if (!KMAJ) return row * 64 + 16 * ((2 * j + half) ^ swz(row));
-    return (8 * j) * kGKPitch + 4 * row;
-  }
-
-  // Inline-asm fragment read (lo = k 0..3, hi = k 4..7 of the lane's 8) at stage-relative
-  // addresses a_lo / a_hi (a_hi: K-contiguous only); the caller waits lgkmcnt(0) and places a
-  // sched_barrier before using the values.
-  __device__ static __forceinline__ void frag_asm(uint32_t addr, uint32_t a_hi, float4& lo,
-                                                  float4& hi) {
-    if (!KMAJ) {
-      asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(addr) : "memory");
-      asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(a_hi) : "memory");
-    } else {
-      asm volatile(
-          "ds_read_b32 %0, %8\n\t"
-          "ds_read_b32 %1, %8 offset:1040\n\t"
-          "ds_read_b32 %2, %8 offset:2080\n\t"
-          "ds_read_b32 %3, %8 offset:3120\n\t"
-          "ds_read_b32 %4, %8 offset:4160\n\t"
-          "ds_read_b32 %5, %8 offset:5200\n\t"
-          "ds_read_b32 %6, %8 offset:6240\n\t"
-          "ds_read_b32 %7, %8 offset:7280"
-          : "=&v"(lo.x), "=&v"(lo.y), "=&v"(lo.z), "=&v"(lo.w), "=&v"(hi.x), "=&v"(hi.y),
-            "=&v"(hi.z), "=&v"(hi.w)
-          : "v"(addr)
-          : "memory");
-    }
-  }
-};
-static_assert(kGKPitch == 1040, "frag_asm's ds_read_b32 offsets assume the 1040-B k-row pitch");
-
-// (lo, hi) = one lane's 8 fp32 values -> its high / low fp16 MFMA operands (split2h)
-__device__ __forceinline__ void split_frag(const float4& lo, const float4& hi, float s,
-                                           f16x8& h, f16x8& l) {
-  uint2 h0, l0, h1, l1;
-  split2h(lo, s, h0, l0);
-  split2h(hi, s, h1, l1);
-  const u32x4 hv = {h0.x, h0.y, h1.x, h1.y}, lv = {l0.x, l0.y, l1.x, l1.y};
-  h = __builtin_bit_cast(f16x8, hv);
-  l = __builtin_bit_cast(f16x8, lv);
-}
-
-template <bool AK, bool BKM>
-__global__ void __launch_bounds__(kXThreads, 2)  // one workgroup per CU
-gemm_h2g_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
-                const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
-                float beta, int act, float* __restrict__ C, int64_t ldc, int64_t k_split,
-                float* __restrict__ slab, BatchStrides bst, CellEpi cep, AmaxPtrs amax) {
-  if (blockIdx.z) {  // strided batch
-    A += blockIdx.z * bst.a;
-    B += blockIdx.z * bst.b;
-    C += blockIdx.z * bst.c;
-  }
-  using OA = GOp<AK>;
-  using OB = GOp<BKM>;
-  constexpr int kStage = OA::kBytes + OB::kBytes;
-  constexpr int kRing = kGBuf * kStage;
-  constexpr int kEpiBytes = 8 * 32 * kEpiLd * 4;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing > kEpiBytes ? kRing : kEpiBytes];
-  const uint32_t lds_b = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds;
-  const int ka = amax_shift(*amax.a), kb = amax_shift(*amax.b);
-  const float s_a = pow2f(ka), s_b = pow2f(kb);
-  const int64_t tiles_n = ceil_div(N, XBN);
-  const int64_t n_tiles = ceil_div(M, XBM) * tiles_n;
-  const unsigned xq = n_tiles / 8, xr = n_tiles % 8, bx = blockIdx.x % 8;
-  const int64_t t_beg = (bx < xr) ? bx * (xq + 1) : xr * (xq + 1) + (bx - xr) * xq;
-  const int64_t t_end = t_beg + xq + (bx < xr ? 1 : 0);
-  const unsigned bq = gridDim.x / 8, br = gridDim.x % 8;
-  const int64_t t_step = bq + (bx < br ? 1 : 0);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
-  // this lane's fragment offsets inside a stage image: A rows wm 128 + 32 i, B rows wn 64 + 32 j
-  const uint32_t offa = OA::frag_off(wm * 128, lane), offa1 = OA::frag_off(wm * 128, lane, 1);
-  const uint32_t offb = OA::kBytes + OB::frag_off(wn * 64, lane);
-  const uint32_t offb1 = OA::kBytes + OB::frag_off(wn * 64, lane, 1);
-  constexpr uint32_t kFragA = AK ? 32 * 4 : 32 * 64;  // bytes between A fragments i and i + 1
-  constexpr uint32_t kFragB = BKM ? 32 * 4 : 32 * 64;
-  for (int64_t tile = t_beg + blockIdx.x / 8; tile < t_end; tile += t_step) {
-    if (tile != t_beg + blockIdx.x / 8) __syncthreads();  // the previous tile's epilogue LDS reads
-    const int64_t m0 = (tile / tiles_n) * XBM, n0 = (tile % tiles_n) * XBN;
-    const int64_t kbeg = (int64_t)blockIdx.y * k_split;
-    const int64_t kend = min(K, kbeg + k_split);
-    const int64_t nst = kend > kbeg ? ceil_div(kend - kbeg, XBK) : 0;
-    const bool tail = ((kend - kbeg) % XBK) != 0;  // the last stage is partial
-    f32x16 acc[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    auto fill = [&](int64_t t) {  // stage t into ring slot t % kGBuf
-      uint8_t* op = lds + (t % kGBuf) * kStage;
-      const int64_t k0 = kbeg + t * XBK;
-      if (tail && t == nst - 1) {
-        OA::fill_guarded(A, lda, m0, M, k0, kend, op, wid, lane);
-        OB::fill_guarded(B, ldb, n0, N, k0, kend, op + OA::kBytes, wid, lane);
-      } else {
-        OA::issue(A, lda, m0, M, k0, op, wid, lane);
-        OB::issue(B, ldb, n0, N, k0, op + OA::kBytes, wid, lane);
-      }
-    };
-    // LDS-DMA stages among t + 1, t + 2 (4 pieces each): what may stay in flight at stage t
-    auto dma_after = [&](int64_t t) {
-      int n = 0;
-#pragma unroll
-      for (int d = 1; d <= 2; ++d)
-        if (t + d < nst && !(tail && t + d == nst - 1)) ++n;
-      return n;
-    };
-#pragma unroll
-    for (int d = 0; d < kGBuf - 1; ++d)
-      if (d < nst) fill(d);
-    for (int64_t t = 0; t < nst; ++t) {
-      const int n = dma_after(t);
-      if (n == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (t + kGBuf - 1 < nst) fill(t + kGBuf - 1);  // into the slot every wave finished reading
-      const uint32_t sb = lds_b + (uint32_t)((t % kGBuf) * kStage);
-      float4 bf[2][2], af[2][2];
-      OB::frag_asm(sb + offb, sb + offb1, bf[0][0], bf[0][1]);
-      OB::frag_asm(sb + offb + kFragB, sb + offb1 + kFragB, bf[1][0], bf[1][1]);
-      OA::frag_asm(sb + offa, sb + offa1, af[0][0], af[0][1]);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      f16x8 bh[2], bl[2], ah, al;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) split_frag(bf[j][0], bf[j][1], s_b, bh[j], bl[j]);
-      split_frag(af[0][0], af[0][1], s_a, ah, al);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (i < 3)
-          OA::frag_asm(sb + offa + (i + 1) * kFragA, sb + offa1 + (i + 1) * kFragA,
-                       af[(i + 1) & 1][0], af[(i + 1) & 1][1]);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {  // mfma_np<2>'s order
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[j], acc[i][j], 0, 0, 0);
-        }
-        if (i < 3) {  // the MFMAs above issue before the wait (pinned on both sides)
-          __builtin_amdgcn_sched_barrier(0);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-          split_frag(af[(i + 1) & 1][0], af[(i + 1) & 1][1], s_a, ah, al);
-        }
-      }
-    }
-    {  // undo the operand scales (exact: powers of two)
-      const float ua = pow2f(-ka), ub = pow2f(-kb);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ua * ub;
-    }
-    // every wave is past its last ring read (and no LDS-DMA is in flight) before the ring
-    // turns into the epilogue's staging tiles
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    epilogue_lds(acc, reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd, M, N, m0 + wm * 128,
-                     n0 + wn * 64, lane, bias, beta, act, C, ldc, slab, cep);
-  }
-}
-
 // Host check for gemm_x3w_kernel<FAST = true>: aligned rows; a K-major operand's row count
 // % 4 == 0 (its clamped float4 never straddles the edge); K % 4 == 0 when an operand is
 // K-contiguous (the K tail's clamped float4 stays inside the row).
@@ -1979,23 +1714,6 @@ __global__ void __launch_bounds__(256) absmax_rows_kernel(int64_t rows, int64_t 
       if (accumulate) b = max(b, out[row]);
       out[row] = b;
     }
-  }
-}
-
-// Split an fp32 operand once into its two scaled fp16 planes (hi at planes, lo at planes +
-// rows * ld; the same [rows][ld] layout): exactly split2h of the GEMM's own staging.
-__global__ void __launch_bounds__(256) split_f16x2_kernel(int64_t rows, int64_t cols4,
-                                                          const float* __restrict__ P, int64_t ld,
-                                                          const uint32_t* __restrict__ amax,
-                                                          uint16_t* __restrict__ planes) {
-  const float sc = pow2f(amax_shift(*amax));
-  const int64_t total = rows * cols4, lo = rows * ld;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int64_t r = e / cols4, c = 4 * (e - r * cols4);
-    uint2 h, l;
-    split2h(*reinterpret_cast<const float4*>(P + r * ld + c), sc, h, l);
-    *reinterpret_cast<uint2*>(planes + r * ld + c) = h;
-    *reinterpret_cast<uint2*>(planes + lo + r * ld + c) = l;
   }
 }
 
@@ -2617,19 +2335,6 @@ extern "C" int mvml_absmax_rows_f32(int64_t rows, int64_t cols, const float* P, 
   return absmax_rows_launch(rows, cols, P, ld, out, accumulate != 0, as_stream(stream));
 }
 
-extern "C" int mvml_split_f16x2(int64_t rows, int64_t cols, const float* P, int64_t ld,
-                                const uint32_t* amax, uint16_t* planes, void* stream) {
-  clear_error();
-  MVML_REQUIRE(rows >= 0 && cols >= 0 && cols % 4 == 0 && ld % 4 == 0 && ld >= cols && amax &&
-                   planes && ((uintptr_t)P % 16) == 0 && ((uintptr_t)planes % 8) == 0,
-               "split_f16x2: bad shape / alignment");
-  if (rows == 0 || cols == 0) return MVML_OK;
-  const int64_t total = rows * (cols / 4);
-  const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
-  split_f16x2_kernel<<<blocks, 256, 0, as_stream(stream)>>>(rows, cols / 4, P, ld, amax, planes);
-  return check_launch("split_f16x2_kernel");
-}
-
 extern "C" int mvml_gemm_f16x2_bsplit(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                                       const float* A, int64_t lda, const float* B, int64_t ldb,
                                       const uint16_t* b_planes, int64_t b_plane,
@@ -2638,8 +2343,7 @@ extern "C" int mvml_gemm_f16x2_bsplit(int a_kmajor, int b_kmajor, int64_t M, int
                                       int64_t ldc, void* workspace, size_t workspace_bytes,
                                       void* stream) {
   clear_error();
-  MVML_REQUIRE(amax_a && amax_b && b_planes && b_plane >= 0 &&
-                   ((uintptr_t)b_planes % (b_plane ? 8 : 16)) == 0,
+  MVML_REQUIRE(amax_a && amax_b && b_planes && b_plane == 0 && ((uintptr_t)b_planes % 16) == 0,
                "gemm_f16x2_bsplit: maxima and B's planes are required");
   AmaxPtrs am{amax_a, amax_b, b_plane};
   return gemm_launch(kPrecF16x2, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, bias, beta, act, C,
@@ -2702,7 +2406,8 @@ extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float
         BatchStrides{}, AmaxPtrs{amax_a, amax_b, 0, amax_a_rows}, cep);
     return check_launch("gemm_f32_kernel(lstm cell)");
   }
-  if (amax_a_rows && w_planes && w_plane == 0)  // per-row A, w_perm from its il4 image
+  MVML_REQUIRE(!w_planes || w_plane == 0, "lstm_gates_cell_fwd: w_planes must be the il4 image (w_plane 0)");
+  if (amax_a_rows && w_planes)  // per-row A, w_perm from its il4 image
     gemm_x3w_kernel<false, false, -1, true, 2, 2, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, reinterpret_cast<const float*>(w_planes), ldw, nullptr, 0.f, 0, nullptr,
         N, K, nullptr, av, bv, ProjEpi{}, BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, 0, amax_a_rows});
@@ -2710,14 +2415,6 @@ extern "C" int mvml_lstm_gates_cell_fwd(int64_t M, int D, int64_t K, const float
     gemm_x3w_kernel<false, false, -1, true, 2, 0, true><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
         BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, 0, amax_a_rows});
-  else if (amax_a && w_planes && w_plane > 0)  // w_perm from its pre-split planes (mvml_split_f16x2)
-    gemm_x3w_kernel<false, false, -1, true, 2, 1><<<grid, kXThreads, 0, as_stream(stream)>>>(
-        M, N, K, A, lda, reinterpret_cast<const float*>(w_planes), ldw, nullptr, 0.f, 0, nullptr,
-        N, K, nullptr, av, bv, ProjEpi{}, BatchStrides{}, cep, AmaxPtrs{amax_a, amax_b, w_plane});
-  else if (amax_a && option(MVML_OPT_GEMM_RING))
-    gemm_h2g_kernel<false, false><<<grid, kXThreads, 0, as_stream(stream)>>>(
-        M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, BatchStrides{}, cep,
-        AmaxPtrs{amax_a, amax_b});
   else if (amax_a)
     gemm_x3w_kernel<false, false, -1, true, 2><<<grid, kXThreads, 0, as_stream(stream)>>>(
         M, N, K, A, lda, w_perm, ldw, nullptr, 0.f, 0, nullptr, N, K, nullptr, av, bv, ProjEpi{},
@@ -2808,7 +2505,6 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   const int av = (lda % 4 == 0) && ((uintptr_t)A % 16 == 0) && bst.a % 4 == 0;
   const int bv = (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0) && bst.b % 4 == 0;
   dim3 grid(plan.wide || bf ? x3w_grid_x(tiles, S) : (unsigned)tiles, (unsigned)S, (unsigned)batch);
-  const bool ring = option(MVML_OPT_GEMM_RING) != 0 && !amax.a_rows;  // (the ring kernel: one A scale)
   // B pre-split as an interleaved-by-4 image (bps with b_plane == 0, mvml_split_f16x2_il4) and /
   // or per-row A maxima, on the 256x256 tile (host: K-contiguous A)
   const bool il4 = bps && amax.b_plane == 0;
@@ -2846,15 +2542,7 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
   } else
 #define MVML_GEMM_LAUNCH(AKV, BKV)                                                              \
   do {                                                                                          \
-    if (hf && plan.wide && ring && !bps && x3w_fast(AKV, BKV, M, N, K, av, bv))                 \
-      gemm_h2g_kernel<AKV, BKV><<<grid, kXThreads, 0, st>>>(M, N, K, A, lda, B, ldb, bias, beta, \
-                                                           act, C, ldc, kc, slab, bst,          \
-                                                           CellEpi{}, amax);                    \
-    else if (hf && plan.wide && bps && amax.b_plane && batch == 1 && x3w_fast(AKV, BKV, M, N, K, av, bv)) \
-      gemm_x3w_kernel<AKV, BKV, -1, true, 2, 1><<<grid, kXThreads, 0, st>>>(                 \
-          M, N, K, A, lda, reinterpret_cast<const float*>(bps), ldb, bias, beta, act, C, ldc, kc, \
-          slab, av, bv, ProjEpi{}, bst, CellEpi{}, amax);                                       \
-    else if (hf && plan.wide && x3w_fast(AKV, BKV, M, N, K, av, bv))                            \
+    if (hf && plan.wide && x3w_fast(AKV, BKV, M, N, K, av, bv))                                 \
       gemm_x3w_kernel<AKV, BKV, -1, true, 2><<<grid, kXThreads, 0, st>>>(                       \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst,   \
           CellEpi{}, amax);                                                                     \
@@ -2922,7 +2610,7 @@ int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int
   const bool x3 = prec == kPrecX3 || hf, bf = prec == kPrecBf16;
   const bool wide = bf || (x3 && plan_gemm(kPrecX3, M, N, K).wide);
   AmaxPtrs amx{amax_x, amax_w, w_plane};
-  const bool bps = hf && w_planes && w_plane > 0 && amax_x && amax_w;  // B = Wcat from its planes
+  MVML_REQUIRE(!w_planes, "gat_proj_fwd: w_planes must be NULL (the two-plane weight image was removed)");
   if (hf && wide && !(amax_x && amax_w)) {  // maxima not supplied: one pass per operand
     MVML_REQUIRE(amax_ws != nullptr, "gat_proj_fwd: split-fp16 needs the maxima workspace");
     int rc = absmax_launch(M, K, A, lda, amax_ws, false, st);
@@ -2938,12 +2626,7 @@ int gemm_proj_epi(int prec, int64_t M, int64_t N, int64_t K, const float* A, int
   dim3 grid(wide ? x3w_grid_x(tiles, 1) : (unsigned)tiles, 1);
 #define MVML_PROJ(LW)                                                                          \
   do {                                                                                         \
-    if (bps && wide && x3w_fast(false, false, M, N, K, av, bv))                                \
-      gemm_x3w_kernel<false, false, LW, true, 2, 1><<<grid, kXThreads, 0, st>>>(            \
-          M, N, K, A, lda, reinterpret_cast<const float*>(w_planes), ldb, nullptr, 0.f, 0, C,  \
-          ldc, K > 0 ? K : 1, nullptr, av, bv, ProjEpi{vec, cols, part}, BatchStrides{},       \
-          CellEpi{}, amx);                                                                     \
-    else if (hf && wide && x3w_fast(false, false, M, N, K, av, bv))                            \
+    if (hf && wide && x3w_fast(false, false, M, N, K, av, bv))                                 \
       gemm_x3w_kernel<false, false, LW, true, 2><<<grid, kXThreads, 0, st>>>(                  \
           M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, K > 0 ? K : 1, nullptr, av, bv,    \
           ProjEpi{vec, cols, part}, BatchStrides{}, CellEpi{}, amx);                       \

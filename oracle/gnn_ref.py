@@ -91,8 +91,74 @@ def gatconv_ref(src, dst, X, fc_w, res_w, attn_l, attn_r, bias, num_heads, out_f
     return rst
 
 
-def gat_layer_ref(src, dst, X, p, num_heads, out_feats, agg_mode, activation, branch=None):
-    """dgllife GATLayer.forward: gat_conv -> flatten(1) | mean(1) -> activation."""
+def _bf16_round(x):
+    """x rounded to bf16 (round-to-nearest-even, via fp32 as the product sees its fp32 operands),
+    carried in x's dtype."""
+    return x.to(torch.float32).to(torch.bfloat16).to(x.dtype)
+
+
+class _ProjBF16(torch.autograd.Function):
+    """Y = bf16(X) bf16(Wcat)^T, with the backward's two products on bf16-rounded operands too:
+    dX = bf16(gY) bf16(Wcat), dWcat = bf16(gY)^T bf16(X) — exactly the rounding points of the
+    bf16 projection (mvml_gemm_bf16 on X, Wcat and gY; mvml_gat.functional GATLayerFunction with
+    algo 'bf16'), every other operation in the input dtype (float64: the bf16-EMULATED oracle)."""
+
+    @staticmethod
+    def forward(ctx, X, Wcat):
+        ctx.save_for_backward(X, Wcat)
+        return _bf16_round(X) @ _bf16_round(Wcat).t()
+
+    @staticmethod
+    def backward(ctx, gY):
+        X, Wcat = ctx.saved_tensors
+        g = _bf16_round(gY)
+        return g @ _bf16_round(Wcat), g.t() @ _bf16_round(X)
+
+
+def gat_layer_bf16_ref(src, dst, X, p, num_heads, out_feats, agg_mode, activation, branch=None):
+    """The bf16-projection path's GATConv in ITS association (mvml_gat_fold_weights): one
+    product Y = X Wcat^T with Wcat = [fc.weight ; res_fc.weight (head mean in the 'mean' layer) ;
+    A_l ; A_r], A_l[h] = sum_f attn_l[h, f] fc.weight[h F + f] (el = X A_l^T is (Z * attn_l).sum
+    re-associated), so el / er and the residual see the same bf16 rounding as Z; then dgl's
+    edge softmax and u_mul_e sum exactly as gatconv_ref.  Same function as gat_layer_ref up to
+    the re-association and the bf16 rounding of _ProjBF16."""
+    src = _as_long(src, X.device)
+    dst = _as_long(dst, X.device)
+    n = X.shape[0]
+    H, Fo = num_heads, out_feats
+    fc_w, res_w = p["fc.weight"], p["res_fc.weight"]
+    mean = agg_mode == "mean"
+    Wfc = fc_w.view(H, Fo, -1)
+    A_l = (p["attn_l"].view(H, Fo, 1) * Wfc).sum(1)
+    A_r = (p["attn_r"].view(H, Fo, 1) * Wfc).sum(1)
+    R_w = res_w.view(H, Fo, -1).mean(0) if mean else res_w
+    Wcat = torch.cat([fc_w, R_w, A_l, A_r], 0)
+    Y = _ProjBF16.apply(X, Wcat)
+    HF = H * Fo
+    RC = Fo if mean else HF
+    Z = Y[:, :HF].view(n, H, Fo)
+    R = Y[:, HF:HF + RC]
+    el, er = Y[:, HF + RC:HF + RC + H], Y[:, HF + RC + H:HF + RC + 2 * H]
+    s = el[src] + er[dst]
+    e = F.leaky_relu(s, 0.2) if branch is None else leaky_relu_branch(s, 0.2, branch)
+    a = edge_softmax_ref(e, dst, n)
+    agg = torch.zeros((n, H, Fo), dtype=X.dtype, device=X.device).index_add(0, dst, a.unsqueeze(-1) * Z[src])
+    bias = p["bias"].view(H, Fo)
+    if mean:
+        out = agg.mean(1) + R + bias.mean(0)
+    else:
+        out = (agg + R.view(n, H, Fo) + bias).flatten(1)
+    if activation is not None:
+        out = activation(out)
+    return out
+
+
+def gat_layer_ref(src, dst, X, p, num_heads, out_feats, agg_mode, activation, branch=None,
+                  proj=None):
+    """dgllife GATLayer.forward: gat_conv -> flatten(1) | mean(1) -> activation.  proj='bf16':
+    the bf16-emulated projection (gat_layer_bf16_ref)."""
+    if proj == "bf16":
+        return gat_layer_bf16_ref(src, dst, X, p, num_heads, out_feats, agg_mode, activation, branch)
     rst = gatconv_ref(src, dst, X, p["fc.weight"], p["res_fc.weight"], p["attn_l"],
                       p["attn_r"], p["bias"], num_heads, out_feats, branch=branch)
     out = rst.flatten(1) if agg_mode == "flatten" else rst.mean(1)
@@ -101,7 +167,7 @@ def gat_layer_ref(src, dst, X, p, num_heads, out_feats, agg_mode, activation, br
     return out
 
 
-def gat_ref(src, dst, X, layer_params, hidden_feats, num_heads=None, branches=None):
+def gat_ref(src, dst, X, layer_params, hidden_feats, num_heads=None, branches=None, proj=None):
     L = len(hidden_feats)
     num_heads = num_heads or [4] * L
     h = X
@@ -109,7 +175,7 @@ def gat_ref(src, dst, X, layer_params, hidden_feats, num_heads=None, branches=No
         last = i == L - 1
         h = gat_layer_ref(src, dst, h, layer_params[i], num_heads[i], hidden_feats[i],
                           "mean" if last else "flatten", None if last else F.elu,
-                          branch=None if branches is None else branches[i])
+                          branch=None if branches is None else branches[i], proj=proj)
     return h
 
 
@@ -210,8 +276,9 @@ class GNNModuleRef(nn.Module):
     """
 
     def __init__(self, in_feats=74, hidden_feats=None, dropout=0.5, num_step_set2set=6,
-                 num_layer_set2set=3):
+                 num_layer_set2set=3, proj=None):
         super().__init__()
+        self.proj = proj  # None: exact; 'bf16': the bf16-emulated GAT projections
         hidden_feats = list(hidden_feats or [192, 384])
         self.hidden_feats = hidden_feats
         self.conv = _GATParams(in_feats, hidden_feats)
@@ -232,7 +299,7 @@ class GNNModuleRef(nn.Module):
         """branches: optional per-GAT-layer bool (E, H) LeakyReLU sides (leaky_relu_branch);
         fc_branch: optional bool (B, out) side of the fc ReLU (relu_branch)."""
         node_x = gat_ref(graph["src"], graph["dst"], atom_feats, self.layer_params(),
-                         self.hidden_feats, branches=branches)
+                         self.hidden_feats, branches=branches, proj=self.proj)
         graph_x = set2set_ref(graph["node_offsets"], node_x, self.readout.lstm,
                               self.readout.n_iters)
         out = graphnorm_ref(graph_x, self.norm.weight, self.norm.bias, self.norm.mean_scale,

@@ -63,15 +63,16 @@ def test_persist_rows(il4):
 
 
 def test_persist_amax_and_bsplit():
-    """mvml_gemm_f16x2_amax (operand-wide scales) and mvml_gemm_f16x2_bsplit (B from its planes)."""
+    """mvml_gemm_f16x2_amax (operand-wide scales) and mvml_gemm_f16x2_bsplit (B from its
+    interleaved split image)."""
     A, B = _inputs(2)
     A, B = A[0], B[0]
     st = stream_ptr()
     mx = torch.zeros(2, dtype=torch.int32, device=DEV)
     absmax(A, M, K, K, mx, 0)
     absmax(B, N, K, K, mx, 1)
-    planes = torch.empty(2 * N * K, dtype=torch.int16, device=DEV)
-    call("mvml_split_f16x2", N, K, ptr(B), K, slot(mx, 1), ptr(planes), st)
+    img = torch.empty_like(B)
+    call("mvml_split_f16x2_il4", N, K, ptr(B), K, slot(mx, 1), ptr(img), st)
     wp, wn = ws_ptr_size(lib().mvml_gemm_workspace_size(M, N, K), DEV)
 
     def fn():
@@ -79,7 +80,7 @@ def test_persist_amax_and_bsplit():
         C2 = torch.full((M, N), float("nan"), device=DEV)
         call("mvml_gemm_f16x2_amax", 0, 0, M, N, K, ptr(A), K, ptr(B), K, slot(mx, 0), slot(mx, 1), None,
              0.0, 0, ptr(C1), N, wp, wn, st)
-        call("mvml_gemm_f16x2_bsplit", 0, 0, M, N, K, ptr(A), K, ptr(B), K, ptr(planes), N * K,
+        call("mvml_gemm_f16x2_bsplit", 0, 0, M, N, K, ptr(A), K, ptr(B), K, ptr(img), 0,
              slot(mx, 0), slot(mx, 1), None, 0.0, 0, ptr(C2), N, wp, wn, st)
         return [C1, C2]
     _run(fn)

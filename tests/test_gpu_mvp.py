@@ -140,13 +140,17 @@ def test_mvp_train_step_bf16_projection():
     operands (proj_dtype=torch.bfloat16, fp32 accumulate) against the float64 oracle of the fp32
     reference semantics: logits and loss within north_star's bf16 bar 2e-2; gradients held
     norm-wise (Frobenius) and by direction as test_gpu_bf16.py does (a bf16-perturbed
-    pre-activation that crosses a kink flips single gradient entries by O(1)); one Adam step."""
+    pre-activation that crosses a kink flips single gradient entries by O(1)) against the
+    bf16-EMULATED float64 oracle (test_gpu_bf16.check_emulated); one Adam step."""
     from mvml_gat import bce_with_logits
     from mvml_gat.mvp import MVP
-    from oracle.fusion_ref import bce_logits_ref
-    from test_gpu_bf16 import TOL_BF16, grad_ok
+    from oracle.fusion_ref import MVPRef, bce_logits_ref
+    from test_gpu_bf16 import EMU_FRO, TOL_BF16, check_emulated
     bg, gd, x, smiles, fp, y = _kegg_batch()
     _, ref64, _ = _models()
+    emu = MVPRef().double().eval()
+    emu.load_state_dict(ref64.state_dict())
+    emu.gnn.proj = "bf16"
     mod = MVP(11, 74, [192, 384], 6, 3, 128, 384, 2, 512, 12, 0.5, proj_dtype=torch.bfloat16)
     mod.load_state_dict({k: v.float() for k, v in ref64.state_dict().items()})
     mod = mod.to(DEV).eval()
@@ -160,21 +164,16 @@ def test_mvp_train_step_bf16_projection():
     z_r = ref64(smiles, gd, x, fp)
     loss_r = bce_logits_ref(z_r, y)
     loss_r.backward()
+    z_e = emu(smiles, gd, x, fp)
+    bce_logits_ref(z_e, y).backward()
     e_z = rel_err(z_d, z_r)
     assert 1e-7 < e_z < TOL_BF16, e_z
+    assert rel_err(z_d, z_e) < EMU_FRO
     assert abs(loss_d.item() - loss_r.item()) / abs(loss_r.item()) < TOL_BF16
-    p64 = dict(ref64.named_parameters())
-    worst = {}
-    for n, p in mod.named_parameters():
-        if p64[n].grad is None:
-            assert p.grad is None or float(p.grad.abs().max()) == 0.0, n
-            continue
-        a, b = p.grad.double().cpu().flatten(), p64[n].grad.flatten()
-        fro = ((a - b).norm() / b.norm()).item()
-        cos = (a @ b / (a.norm() * b.norm())).item()
-        worst[n] = (round(fro, 4), round(cos, 5))
-    print(f"MVP bf16 projection: logits {e_z:.2e}; worst grads", sorted(worst.items(), key=lambda kv: -kv[1][0])[:3])
-    bad = {n: v for n, v in worst.items() if not grad_ok(n, *v)}
+    rows, bad = check_emulated(mod.named_parameters(), dict(emu.named_parameters()),
+                               dict(ref64.named_parameters()))
+    print(f"MVP bf16 projection: logits {e_z:.2e}; worst grads (vs emulated, vs exact, emulated vs "
+          "exact)", sorted(rows.items(), key=lambda kv: -kv[1][0])[:4])
     assert not bad, bad
     opt.step()
     assert all(torch.isfinite(p).all() for p in mod.parameters())

@@ -63,8 +63,11 @@ def test_flat_adam_matches_torch():
         step_i, m, v = fopt.state_of(b)
         assert step_i == n, (i, step_i, n)
         if n:
-            assert torch.allclose(m, st["exp_avg"], rtol=1e-5, atol=1e-12), i
-            assert torch.allclose(v, st["exp_avg_sq"], rtol=1e-5, atol=1e-20), i
+            # (exp_avg's small entries are differences g - m: fp32 rounding relative to the
+            # tensor's scale, not to each entry)
+            em, ev = st["exp_avg"], st["exp_avg_sq"]
+            assert torch.allclose(m, em, rtol=1e-5, atol=1e-6 * float(em.abs().max())), i
+            assert torch.allclose(v, ev, rtol=1e-5, atol=1e-6 * float(ev.abs().max())), i
     # the never-used parameter is bitwise untouched
     assert torch.equal(mine[3].detach().cpu(), _params(0)[3].detach())
 

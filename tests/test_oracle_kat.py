@@ -201,3 +201,38 @@ def test_fusion_identical_views_give_uniform_attention():
     assert torch.allclose(att, v.unsqueeze(2).expand(4, 2, 3, 8))
     out = m.conv(att).view(4, -1)
     assert torch.allclose(m.mlp(out), m(x, x, x))
+
+
+@pytest.mark.parametrize("agg", ["flatten", "mean"])
+def test_bf16_emulated_layer_is_the_exact_layer_without_rounding(agg, monkeypatch):
+    """The bf16-emulated GATConv (gnn_ref.gat_layer_bf16_ref: the folded projection [fc ; res_fc
+    (head mean) ; A_l ; A_r] in one product) with its bf16 rounding turned off is the exact
+    layer up to float64 re-association — forward and every gradient; with the rounding on it
+    differs by bf16's own error (far above float64, far below the 2e-2 output bar)."""
+    from _util import batch_of_sizes, graph_dict
+    sb = batch_of_sizes([25, 11, 40, 23], seed=5)
+    gd = graph_dict(sb)
+    torch.manual_seed(3)
+    Fin, Fo, H = (74, 192, 4) if agg == "flatten" else (768, 384, 4)
+    X = torch.randn(int(sb.num_nodes.sum()), Fin, **D64) if agg == "mean" else torch.as_tensor(sb.feats, **D64)
+    p = {"fc.weight": torch.randn(H * Fo, Fin, **D64) * 0.1, "res_fc.weight": torch.randn(H * Fo, Fin, **D64) * 0.1,
+         "attn_l": torch.randn(1, H, Fo, **D64) * 0.1, "attn_r": torch.randn(1, H, Fo, **D64) * 0.1,
+         "bias": torch.randn(H * Fo, **D64) * 0.1}
+    act = F.elu if agg == "flatten" else None
+    gout = torch.randn(X.shape[0], H * Fo if agg == "flatten" else Fo, **D64)
+
+    def run(fn):
+        q = {k: v.clone().requires_grad_() for k, v in p.items()}
+        out = fn(gd["src"], gd["dst"], X, q, H, Fo, agg, act)
+        out.backward(gout)
+        return out.detach(), {k: v.grad for k, v in q.items()}
+
+    exact, g_exact = run(gnn_ref.gat_layer_ref)
+    monkeypatch.setattr(gnn_ref, "_bf16_round", lambda x: x)
+    folded, g_folded = run(gnn_ref.gat_layer_bf16_ref)
+    assert rel_err(folded, exact) < 1e-12
+    for k in p:
+        assert rel_err(g_folded[k], g_exact[k]) < 1e-11, k
+    monkeypatch.undo()
+    emu, _ = run(gnn_ref.gat_layer_bf16_ref)
+    assert 1e-5 < rel_err(emu, exact) < 2e-2

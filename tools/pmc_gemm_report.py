@@ -59,9 +59,10 @@ def main():
         v = c.get(k)
         return sum(v) / len(v) if v else float("nan")
 
-    print("kernel <AK, BKM, EPI, FAST, NP, BPS, ROWS, EX>  (x3w/x3s/f32 as in csrc/gemm_f32.hip)")
+    print("kernel <AK, BKM, EPI, FAST, NP, BPS, ROWS, EX>  (x3w/x3s/f32 as in csrc/gemm_f32.hip;")
+    print("  planes <APS, ROWS, EX, CELL, BK, ABL> as in csrc/gemm_planes.hip); clk_GHz = GRBM_GUI_ACTIVE / 8 / duration")
     hdr = ("calls", "avg_us", "step%", "mfma_busy", "issue", "parked", "stalled", "lds_stall",
-           "lds_conf", "valu/mfma")
+           "lds_conf", "valu/mfma", "clk_GHz")
     print(f"{'kernel':58s} " + " ".join(f"{h:>9s}" for h in hdr))
     rows = []
     for k, c in per.items():
@@ -79,7 +80,8 @@ def main():
             avg(c, "SQ_WAIT_INST_ANY") / wave,
             avg(c, "SQ_WAIT_INST_LDS") / wave,
             avg(c, "SQ_LDS_BANK_CONFLICT") / avg(c, "SQ_LDS_IDX_ACTIVE"),
-            avg(c, "SQ_INSTS_VALU") / avg(c, "SQ_INSTS_MFMA"))))
+            avg(c, "SQ_INSTS_VALU") / avg(c, "SQ_INSTS_MFMA"),
+            cyc / (st[1] * 1e3) if st[1] == st[1] else float("nan"))))
     for _, k, v in sorted(rows, reverse=True):
         if v[0] < a.min_calls:
             continue
