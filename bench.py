@@ -475,6 +475,8 @@ def run(args):
                                **({"fused": True} if adam_kind == "fused" else {}))
         reducer = FlatGradAllReduce(params, average=True)
 
+    one = torch.ones((), device=dev)  # dL/dL, made once (backward() would fill one every step)
+
     def step(b, fused=True):
         opt.zero_grad(set_to_none=False)
         if not args.dry_run:
@@ -482,7 +484,7 @@ def run(args):
             # reference's DataLoader collates every batch (dataset.py:52-54)
             b.g.recollate()
         if mvp and fused:
-            mvml_gat.bce_with_logits(full(b.smiles, b.g, b.feats, b.fp), b.labels).backward()
+            mvml_gat.bce_with_logits(full(b.smiles, b.g, b.feats, b.fp), b.labels).backward(one)
             mvp_mod.join_side_stream(dev)
             reducer()
             opt.step()
@@ -492,7 +494,7 @@ def run(args):
             torch.nn.functional.binary_cross_entropy_with_logits(
                 model.fuse(b.smiles_x, out, b.fp_x), b.labels).backward()
         elif fused:
-            mvml_gat.bce_with_logits(fusion(b.smiles_x, out, b.fp_x), b.labels).backward()
+            mvml_gat.bce_with_logits(fusion(b.smiles_x, out, b.fp_x), b.labels).backward(one)
         else:
             out.backward(b.upstream)
         reducer()

@@ -399,7 +399,9 @@ int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_
  * (mvml_gemm_f16x2_amax), mvml_gat_unfold_grads, the attention-vector product
  * (mvml_gemm_f32x3_batched), mvml_colsum_f32 and the per-row-scaled data-gradient product
  * (mvml_gemm_f16x2_rows, Wcat as its interleaved image), every operand maximum and scratch
- * buffer inside `workspace` (mvml_gat_layer_bwd_workspace_size bytes). */
+ * buffer inside `workspace` (mvml_gat_layer_bwd_workspace_size bytes).  The aggregation
+ * backward's kernel choice follows the process options (mvml_set_option) as for
+ * mvml_gat_agg_bwd: the Python layer sets "flat_src" for large-molecule batches. */
 size_t mvml_gat_layer_bwd_workspace_size(int64_t num_nodes, int64_t num_edges, int H, int F, int Fin,
                                          int mean);
 int mvml_gat_layer_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
@@ -416,7 +418,8 @@ int mvml_gat_layer_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t nu
  * LSTM cell (torch.nn.LSTM gate order i,f,g,o): gates_pre[B, 4D] = x W_ih^T + h W_hh^T (by
  * mvml_gemm_f32), then
  *   c = sigmoid(f)*c_prev + sigmoid(i)*tanh(g);  h = sigmoid(o)*tanh(c)
- * act_out[B,4D] saves the activated gates for the backward.  c_prev may be NULL (zeros).
+ * act_out[B,4D] saves the activated gates for the backward.  c_prev may be NULL (zeros), and
+ * so may gates_pre (zero pre-activations: the bias alone).
  * h is written with leading dimension ldh, and again to h_out2 (ld ldh2) when h_out2 is not
  * NULL: the cell's output is both its own recurrent input and the next layer's input, each
  * stored inside a combined [x | h_prev] GEMM operand row.
@@ -496,9 +499,35 @@ int mvml_graphnorm_bwd(int64_t G, int D, const int64_t* group_offsets, const flo
                        float* g_mean_scale, void* workspace, size_t workspace_bytes,
                        void* stream);
 
-/* Small elementwise helpers.  ReLU backward (threshold_backward on the output):
- * g_x = g_y * (y > 0). */
-int mvml_relu_bwd(int64_t n, const float* y, const float* g_y, float* g_x, void* stream);
+/* Small elementwise helpers.  ReLU backward (threshold_backward on the output), times the
+ * Dropout scale when a Dropout followed the ReLU (scale = 1 / (1 - p), 1 without one):
+ * g_x = g_y * scale * (y > 0).  y is the DROPPED output: a dropped element reads 0, so its
+ * gradient is 0 without a stored mask (nn.Dropout's backward is g * mask * scale). */
+int mvml_relu_bwd(int64_t n, const float* y, const float* g_y, float* g_x, float scale, void* stream);
+/* nn.Dropout(p) in training mode (model.py:87, 36, 46; torch's fused_dropout): y = x * keep /
+ * (1 - p), x == y allowed; element i kept iff a 32-bit counter-based hash of (seed, i) is at
+ * least round(p 2^32).  The mask is a function of (seed, i) only: nothing is stored, and after
+ * a ReLU the backward is mvml_relu_bwd's scaled form with scale = (float)(1 / (1 - p)), the
+ * float this kernel multiplies by.  0 <= p < 1. */
+int mvml_dropout_fwd(int64_t n, const float* x, float* y, double p, int64_t seed, void* stream);
+/* dst[r][0:cols) = src[r][0:cols) for r < rows (row pitches lds, ldd): a narrow column slice
+ * of a wide row-pitched matrix into a dense one (the projection output's 2H logit columns);
+ * lds = 0 replicates src's one row into every dst row. */
+int mvml_copy_cols(int64_t rows, int cols, const float* src, int64_t lds, float* dst, int64_t ldd,
+                   void* stream);
+/* Zero `rows` rows of row_bytes bytes at a pitch of pitch_bytes (hipMemsetAsync, or
+ * hipMemset2DAsync when pitch_bytes > row_bytes): the zero initial states and accumulators. */
+int mvml_fill_zero(void* p, int64_t rows, int64_t row_bytes, int64_t pitch_bytes, void* stream);
+/* Set2Set's LSTM weights in the gates products' layouts (nn.LSTM w_ih [4D][kin], w_hh [4D][D]):
+ * wcat [4D][kin + D] = [w_ih | w_hh]; wperm (may be NULL) the same rows interleaved for the
+ * cell epilogue (row 4 j + q = wcat row q D + j, see mvml_lstm_gates_cell_fwd). */
+int mvml_lstm_pack_weights(int D, int kin, const float* w_ih, const float* w_hh, float* wcat,
+                           float* wperm, void* stream);
+/* dst[c][r] = src[r][c] (row pitches lds, ldd). */
+int mvml_transpose(int64_t rows, int64_t cols, const float* src, int64_t lds, float* dst, int64_t ldd,
+                   void* stream);
+/* y[i] = x[i] * s[0], s a device scalar (x == y allowed). */
+int mvml_scale_by(int64_t n, const float* x, const float* s, float* y, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Multi-view attention fusion head (MVP, model.py:28-48, 57-71), the consumer
@@ -551,15 +580,19 @@ int mvml_conv3_bwd(int64_t B, int C, int O, int W, const float* in, const float*
  * mvml_token_attn_fold_bwd), g_weight, g_bias (as mvml_conv3_bwd; workspace
  * mvml_attn_conv_bwd_workspace_size(B)).  Replaces model.py:66-69's att -> conv round trip.
  * g_pv_rows (may be NULL; zeroed by the caller, 3 B entries): max with the bits of each g_pv
- * row's |max| (the per-row scales of the data-gradient product that reads g_pv). */
+ * row's |max| (the per-row scales of the data-gradient product that reads g_pv).  g_scale:
+ * the Dropout after the ReLU (model.py:36) — out is then the dropped output and the ReLU
+ * gradient is g_out * g_scale where out > 0 (1: no Dropout).  The forward applies that Dropout
+ * in its store when drop_p > 0 (mask of mvml_dropout_fwd for (drop_seed, element index of out);
+ * g_scale = (float)(1 / (1 - drop_p))). */
 int mvml_attn_conv_fwd(int64_t B, int H, int dk, const float* pv, int64_t ld, const float* x,
                        int64_t ldx, float scale, const float* weight, const float* bias,
-                       float* P, float* out, void* stream);
+                       float* P, float* out, double drop_p, int64_t drop_seed, void* stream);
 size_t mvml_attn_conv_bwd_workspace_size(int64_t B);
 int mvml_attn_conv_bwd(int64_t B, int H, int dk, const float* pv, int64_t ld, const float* x,
                        int64_t ldx, float scale, const float* P, const float* weight,
-                       const float* out, const float* g_out, float* g_pv, int64_t ldg,
-                       float* g_k, int64_t ldgk, uint32_t* g_pv_amax, uint32_t* g_pv_rows,
+                       const float* out, const float* g_out, float g_scale, float* g_pv,
+                       int64_t ldg, float* g_k, int64_t ldgk, uint32_t* g_pv_amax, uint32_t* g_pv_rows,
                        float* g_weight, float* g_bias, void* workspace, size_t workspace_bytes,
                        void* stream);
 int mvml_bce_logits(int64_t n, const float* z, const float* y, float* loss_terms, float* g_z,
@@ -703,8 +736,8 @@ int mvml_grad_gather(int64_t nchunks, const int32_t* chunk_param, const int64_t*
  * sqrt(1 - beta2^step) + eps) (torch's Adam); then steps[i] += 1.  Others are untouched. */
 int mvml_adam_flat(int64_t nchunks, const int32_t* chunk_param, const int64_t* chunk_beg,
                    const int64_t* chunk_end, const float* flags, int32_t* steps, int P, float* param,
-                   const float* grad, float* exp_avg, float* exp_avg_sq, float lr, float beta1,
-                   float beta2, float eps, float weight_decay, float grad_scale, void* stream);
+                   const float* grad, float* exp_avg, float* exp_avg_sq, double lr, double beta1,
+                   double beta2, double eps, double weight_decay, float grad_scale, void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,7 @@
 //     Weight gradients: per-workgroup partials over a run of molecules, summed in fixed order
 //     by a second kernel (deterministic, no atomics).
 #include "common.h"
+#include "dropout.h"
 
 namespace mvml {
 namespace {
@@ -938,7 +939,8 @@ __global__ void __launch_bounds__(kFuseThreads, 3)  // one workgroup per CU
 attn_conv_fwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv, int64_t ld,
                      const float* __restrict__ x, int64_t ldx, float scale,
                      const float* __restrict__ wgt, const float* __restrict__ bias,
-                     float* __restrict__ P, float* __restrict__ out) {
+                     float* __restrict__ P, float* __restrict__ out, uint32_t drop_thr,
+                     float drop_scale, uint64_t drop_seed) {
   constexpr int W = kFuseW, Wo = W - 2, H = kConvC;
   constexpr int64_t HD = (int64_t)H * W;
   __shared__ float s_in[kFuseCube];
@@ -998,7 +1000,13 @@ attn_conv_fwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int o = 4 * lk + r;
-        if (o < kConvO && xx < Wo) ob[o * Wo + xx] = fmaxf(acc[ct][r] + bo[r], 0.f);
+        if (o < kConvO && xx < Wo) {
+          float y = fmaxf(acc[ct][r] + bo[r], 0.f);
+          if (drop_thr)  // the Dropout after the ReLU (model.py:36), mvml_dropout_fwd's mask
+            y = dropout_u32(drop_seed, b * (int64_t)(kConvO * Wo) + o * Wo + xx) >= drop_thr ? y * drop_scale
+                                                                                               : 0.f;
+          ob[o * Wo + xx] = y;
+        }
       }
     }
   }
@@ -1085,7 +1093,7 @@ __global__ void __launch_bounds__(kFuseThreads, 3)  // one workgroup per CU
 attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv, int64_t ld,
                      const float* __restrict__ x, int64_t ldx, float scale,
                      const float* __restrict__ P, const float* __restrict__ wgt,
-                     const float* __restrict__ out, const float* __restrict__ g_out,
+                     const float* __restrict__ out, const float* __restrict__ g_out, float g_scale,
                      float* __restrict__ gpv, int64_t ldg, float* __restrict__ gk, int64_t ldgk,
                      uint32_t* __restrict__ gpv_amax, float* __restrict__ part,
                      uint32_t* __restrict__ gpv_rows) {
@@ -1132,7 +1140,8 @@ attn_conv_bwd_kernel(int64_t B, int64_t per_block, const float* __restrict__ pv,
     // (A) molecule b's staging landed (this wave's pieces; the barrier: everyone's); then
     // g_pre = g_out (out > 0) in place
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    for (int e = tid; e < kConvO * Wo; e += kFuseThreads) s_gp[e] = s_o[e] > 0.f ? s_gp[e] : 0.f;
+    for (int e = tid; e < kConvO * Wo; e += kFuseThreads)
+      s_gp[e] = s_o[e] > 0.f ? (g_scale == 1.f ? s_gp[e] : s_gp[e] * g_scale) : 0.f;
     // (B) the cube rows of head h
     {
       float p[NT][NT], v[NT][kDkVpl];
@@ -1460,14 +1469,17 @@ static int64_t fused_blocks(int64_t B) { return std::min<int64_t>(B, 256); }  //
 
 extern "C" int mvml_attn_conv_fwd(int64_t B, int H, int dk, const float* pv, int64_t ld,
                                   const float* x, int64_t ldx, float scale, const float* weight,
-                                  const float* bias, float* P, float* out, void* stream) {
+                                  const float* bias, float* P, float* out, double drop_p,
+                                  int64_t drop_seed, void* stream) {
   clear_error();
   MVML_REQUIRE(B >= 0 && H == kConvC && dk == 64 * kDkVpl && ld >= 2 * (int64_t)H * dk && ldx >= dk,
                "attn_conv_fwd: H must be %d, dk %d, ld >= 2*H*dk, ldx >= dk", kConvC, 64 * kDkVpl);
+  MVML_REQUIRE(drop_p >= 0.0 && drop_p < 1.0, "attn_conv_fwd: dropout p must be in [0, 1)");
   if (B == 0) return MVML_OK;
   const int64_t nblk = fused_blocks(B), per = ceil_div(B, nblk);
   attn_conv_fwd_kernel<<<(unsigned)ceil_div(B, per), kFuseThreads, 0, as_stream(stream)>>>(
-      B, per, pv, ld, x, ldx, scale, weight, bias, P, out);
+      B, per, pv, ld, x, ldx, scale, weight, bias, P, out, drop_p > 0.0 ? dropout_threshold(drop_p) : 0u,
+      dropout_scale(drop_p), (uint64_t)drop_seed);
   return check_launch("attn_conv_fwd_kernel");
 }
 
@@ -1478,7 +1490,7 @@ extern "C" size_t mvml_attn_conv_bwd_workspace_size(int64_t B) {
 extern "C" int mvml_attn_conv_bwd(int64_t B, int H, int dk, const float* pv, int64_t ld,
                                   const float* x, int64_t ldx, float scale, const float* P,
                                   const float* weight, const float* out, const float* g_out,
-                                  float* g_pv, int64_t ldg, float* g_k, int64_t ldgk,
+                                  float g_scale, float* g_pv, int64_t ldg, float* g_k, int64_t ldgk,
                                   uint32_t* g_pv_amax, uint32_t* g_pv_rows, float* g_weight,
                                   float* g_bias, void* workspace, size_t workspace_bytes,
                                   void* stream) {
@@ -1497,8 +1509,8 @@ extern "C" int mvml_attn_conv_bwd(int64_t B, int H, int dk, const float* pv, int
   const int64_t used = ceil_div(B, per);
   float* part = static_cast<float*>(workspace);
   attn_conv_bwd_kernel<<<(unsigned)used, kFuseThreads, 0, st>>>(
-      B, per, pv, ld, x, ldx, scale, P, weight, out, g_out, g_pv, ldg, g_k, ldgk, g_pv_amax, part,
-      g_pv_rows);
+      B, per, pv, ld, x, ldx, scale, P, weight, out, g_out, g_scale, g_pv, ldg, g_k, ldgk, g_pv_amax,
+      part, g_pv_rows);
   int rc = check_launch("attn_conv_bwd_kernel");
   if (rc) return rc;
   partial_sum_kernel<<<(unsigned)ceil_div(kConvWg, 256), 256, 0, st>>>(

@@ -41,19 +41,21 @@ __global__ void __launch_bounds__(kOptThreads)
 adam_flat_kernel(const int32_t* __restrict__ chunk_param, const int64_t* __restrict__ chunk_beg,
                  const int64_t* __restrict__ chunk_end, const float* __restrict__ flags,
                  const int32_t* __restrict__ steps, float* __restrict__ param, const float* __restrict__ grad,
-                 float* __restrict__ m, float* __restrict__ v, float lr, float beta1, float beta2,
+                 float* __restrict__ m, float* __restrict__ v, double lr, double beta1, double beta2,
                  float eps, float weight_decay, float grad_scale) {
   const int c = blockIdx.x;
   const int i = chunk_param[c];
   if (!(flags[i] > 0.f)) return;  // no rank produced a gradient: torch skips the parameter
   const int64_t b = chunk_beg[c], e = chunk_end[c];
   const int step = steps[i] + 1;
-  // torch (non-capturable Adam): bias corrections on the host in double, then float math
-  const double bc1 = 1.0 - pow((double)beta1, (double)step);
-  const double bc2 = 1.0 - pow((double)beta2, (double)step);
-  const float step_size = (float)((double)lr / bc1);
+  // torch (non-capturable Adam): the hyper-parameters are Python doubles, the bias corrections
+  // and 1 - beta are formed in double and only then rounded to the tensor's float (1 - 0.999f
+  // in float would be 1.3e-5 off 0.001, a systematic offset of exp_avg_sq)
+  const double bc1 = 1.0 - pow(beta1, (double)step);
+  const double bc2 = 1.0 - pow(beta2, (double)step);
+  const float step_size = (float)(lr / bc1);
   const float bc2_sqrt = (float)sqrt(bc2);
-  const float w1 = 1.f - beta1, w2 = 1.f - beta2;
+  const float w1 = (float)(1.0 - beta1), w2 = (float)(1.0 - beta2), b2 = (float)beta2;
   for (int64_t k = b + threadIdx.x; k < e; k += kOptThreads) {
     float g = grad[k];
     if (grad_scale != 1.f) g *= grad_scale;
@@ -61,7 +63,7 @@ adam_flat_kernel(const int32_t* __restrict__ chunk_param, const int64_t* __restr
     if (weight_decay != 0.f) g = g + weight_decay * p;  // grad.add(param, alpha=weight_decay)
     float mk = m[k];
     mk = mk + w1 * (g - mk);                            // exp_avg.lerp_(grad, 1 - beta1)
-    const float vk = v[k] * beta2 + w2 * g * g;         // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+    const float vk = v[k] * b2 + w2 * g * g;             // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
     const float denom = sqrtf(vk) / bc2_sqrt + eps;
     p = p - step_size * (mk / denom);                   // param.addcdiv_(exp_avg, denom, -step_size)
     m[k] = mk;
@@ -95,18 +97,19 @@ extern "C" int mvml_grad_gather(int64_t nchunks, const int32_t* chunk_param, con
 extern "C" int mvml_adam_flat(int64_t nchunks, const int32_t* chunk_param, const int64_t* chunk_beg,
                               const int64_t* chunk_end, const float* flags, int32_t* steps, int P,
                               float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                              float lr, float beta1, float beta2, float eps, float weight_decay,
+                              double lr, double beta1, double beta2, double eps, double weight_decay,
                               float grad_scale, void* stream) {
   clear_error();
   MVML_REQUIRE(nchunks >= 0 && nchunks < (int64_t(1) << 31) && P >= 0 && flags && steps,
                "adam_flat: bad arguments");
-  MVML_REQUIRE(beta1 >= 0.f && beta1 < 1.f && beta2 >= 0.f && beta2 < 1.f && eps >= 0.f && lr >= 0.f,
+  MVML_REQUIRE(beta1 >= 0.0 && beta1 < 1.0 && beta2 >= 0.0 && beta2 < 1.0 && eps >= 0.0 && lr >= 0.0,
                "adam_flat: bad hyper-parameters");
   if (nchunks == 0 || P == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
   adam_flat_kernel<<<(unsigned)nchunks, kOptThreads, 0, st>>>(chunk_param, chunk_beg, chunk_end, flags, steps,
                                                               param, grad, exp_avg, exp_avg_sq, lr, beta1,
-                                                              beta2, eps, weight_decay, grad_scale);
+                                                              beta2, (float)eps, (float)weight_decay,
+                                                              grad_scale);
   int rc = check_launch("adam_flat_kernel");
   if (rc) return rc;
   adam_steps_kernel<<<(unsigned)ceil_div(P, 256), 256, 0, st>>>(P, flags, steps);

@@ -30,11 +30,13 @@ __global__ void lstm_cell_fwd_kernel(int64_t B, int D, const float* __restrict__
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = e / D;
     const int d = (int)(e - b * D);
-    const float* g = gp + b * 4 * D;
-    const float gi = g[d] + b_ih[d] + b_hh[d];
-    const float gf = g[D + d] + b_ih[D + d] + b_hh[D + d];
-    const float gg = g[2 * D + d] + b_ih[2 * D + d] + b_hh[2 * D + d];
-    const float go = g[3 * D + d] + b_ih[3 * D + d] + b_hh[3 * D + d];
+    // gp NULL: the pre-activations are zero (Set2Set's first cell: q*_{-1} = 0, h(-1) = 0);
+    // 0 + b_ih + b_hh rounds as the zero-filled buffer did
+    const float* g = gp ? gp + b * 4 * D : nullptr;
+    const float gi = (g ? g[d] : 0.f) + b_ih[d] + b_hh[d];
+    const float gf = (g ? g[D + d] : 0.f) + b_ih[D + d] + b_hh[D + d];
+    const float gg = (g ? g[2 * D + d] : 0.f) + b_ih[2 * D + d] + b_hh[2 * D + d];
+    const float go = (g ? g[3 * D + d] : 0.f) + b_ih[3 * D + d] + b_hh[3 * D + d];
     const float i = sigm(gi), f = sigm(gf), gt = tanhf(gg), o = sigm(go);
     const float cp = c_prev ? c_prev[e] : 0.f;
     // explicit rounding (no contraction choice left to the compiler): the split-fp16 GEMM's

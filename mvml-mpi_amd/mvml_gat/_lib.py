@@ -21,6 +21,7 @@ _CTYPE = {
     "int": ctypes.c_int,
     "uint32_t": ctypes.c_uint32,
     "float": ctypes.c_float,
+    "double": ctypes.c_double,
     "size_t": ctypes.c_size_t,
     "void": None,
 }

@@ -65,6 +65,21 @@ def bigraph_from_bonds(num_atoms, bonds, node_feats=None, add_self_loop=True):
     return MolGraph(num_atoms, src, dst, ndata)
 
 
+def pad_columns(v, device, mult=4):
+    """v on `device`; a 2-D float32 tensor whose width is not a multiple of `mult` (the 74 atom
+    features) is stored as the column view [:, :F] of a zero-padded [N, round_up(F, mult)]
+    buffer, recorded on the view (functional.zero_padded), so the GAT layer's 16-B-aligned
+    GEMM operand is the buffer itself — no pad copy per step.  The data are unchanged."""
+    if not (v.dim() == 2 and v.dtype == torch.float32 and v.shape[1] % mult and torch.device(device).type == "cuda"):
+        return v.to(device, non_blocking=True)
+    n, f = v.shape
+    buf = torch.zeros((n, (f + mult - 1) // mult * mult), dtype=torch.float32, device=device)
+    out = buf[:, :f]
+    out.copy_(v, non_blocking=True)
+    out._mvml_padded = (buf, out._version, (out.data_ptr(), tuple(out.shape), out.stride()))
+    return out
+
+
 class BatchedMolGraph:
     """A batch of molecule graphs (dgl.batch result) with device-built CSR indices.
 
@@ -151,6 +166,8 @@ class BatchedMolGraph:
 
     # ---- device build ----
     def to(self, device):
+        """Move the batch to `device`; on a GPU, build the device index arrays (CSR, node
+        groups) and store 2-D float node features with rows padded to 16 B (pad_columns)."""
         device = torch.device(device)
         if device.type != "cuda":
             self.device = device
@@ -159,7 +176,7 @@ class BatchedMolGraph:
         with torch.cuda.device(device):
             self._build_device(device)
         self.device = device
-        self.ndata = {k: v.to(device, non_blocking=True) for k, v in self.ndata.items()}
+        self.ndata = {k: pad_columns(v, device) for k, v in self.ndata.items()}
         return self
 
     def _build_device(self, device):

@@ -8,6 +8,7 @@ import contextlib
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -29,6 +30,49 @@ def _c(t):
 
 def _stream(dev):
     return _lib.stream_ptr(dev)
+
+
+_UNIT_SEGMENT = {}
+
+
+def _unit_segment(dev):
+    """int64 [0, 1] on `dev` (made once): the offsets of one one-element segment."""
+    t = _UNIT_SEGMENT.get(str(dev))
+    if t is None:
+        t = _UNIT_SEGMENT[str(dev)] = torch.tensor([0, 1], dtype=torch.int64, device=dev)
+    return t
+
+
+def zeros(shape, dtype=torch.float32, device=None):
+    """torch.zeros through mvml_fill_zero (hipMemsetAsync): no framework fill kernel in the step."""
+    t = torch.empty(shape, dtype=dtype, device=device)
+    zero_(t)
+    return t
+
+
+def zero_(t):
+    """Zero a contiguous tensor, or a 2-D row-pitched one (unit column stride), in place."""
+    es = t.element_size()
+    if t.is_contiguous():
+        n = t.numel() * es
+        call("mvml_fill_zero", ptr(t), 1, n, n, _stream(t.device))
+    else:
+        if t.dim() != 2 or t.stride(1) != 1:
+            raise ValueError("zero_: contiguous or 2-D row-pitched tensors only")
+        call("mvml_fill_zero", ptr(t), t.shape[0], t.shape[1] * es, t.stride(0) * es, _stream(t.device))
+    return t
+
+
+def copy2d(dst, src):
+    """dst[:] = src for float32 2-D views with unit column stride (1-D: one row); a src row
+    stride of 0 (an expanded row) replicates it (mvml_copy_cols)."""
+    d2 = dst.view(1, -1) if dst.dim() == 1 else dst
+    s2 = src.reshape(1, -1) if src.dim() == 1 else src
+    if d2.shape != s2.shape or d2.stride(1) != 1 or (s2.shape[1] > 1 and s2.stride(1) != 1):
+        raise ValueError("copy2d: matching 2-D views with unit column stride")
+    call("mvml_copy_cols", d2.shape[0], d2.shape[1], ptr(s2), s2.stride(0) if s2.shape[0] > 1 else s2.shape[1],
+         ptr(d2), d2.stride(0) if d2.shape[0] > 1 else d2.shape[1], _stream(dst.device))
+    return dst
 
 
 # Diagnostics hook (tools/diag_golden.py, the parity tests' kink-branch capture): when a dict,
@@ -106,6 +150,15 @@ def known_rows(X):
     if rec is None or rec[1] != X._version or rec[2] != (X.data_ptr(), tuple(X.shape), X.stride()):
         return None
     return rec[0]
+
+
+def zero_padded(X, Fp):
+    """The zero-padded [N, Fp] buffer X is the [:, :F] view of (batching.pad_columns: the
+    batch's resident atom features), if unchanged since recorded, else None."""
+    rec = getattr(X, "_mvml_padded", None)
+    if rec is None or rec[1] != X._version or rec[2] != (X.data_ptr(), tuple(X.shape), X.stride()):
+        return None
+    return rec[0] if rec[0].shape[1] == Fp else None
 
 
 def fold_rows(out, rows):
@@ -297,7 +350,7 @@ class EluLink:
     def __init__(self, dev):
         self.claimed = False
         self.g_rst = None
-        self.amax = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.amax = zeros(1, dtype=torch.int32, device=dev)
 
 
 # set by mvml_gat.nn.GAT.forward around its layer loop: links are made and claimed only there,
@@ -321,7 +374,10 @@ class GATLayerFunction(torch.autograd.Function):
     def forward(ctx, X, fc_w, res_w, attn_l, attn_r, bias, g, H, F, slope, mode, algo=None):
         for t, n in ((X, "feat"), (fc_w, "fc.weight"), (res_w, "res_fc.weight")):
             _check_cuda_f32(t, n)
-        X = _c(X)
+        # the batch's atom features may already sit in a zero-padded 16-B-row buffer
+        Xpad = zero_padded(X, _round4(X.shape[1])) if X.dim() == 2 else None
+        if Xpad is None:
+            X = _c(X)
         N, Fin = X.shape
         dev = X.device
         HF = H * F
@@ -334,9 +390,15 @@ class GATLayerFunction(torch.autograd.Function):
         # measured 1.02e-5 from float64 on config 3 — the bias sums cancel and the split-fp16
         # representation error shows — so the bias keeps its exact fp32 column sum.)
         Fp = _round4(Fin)
-        Xp = X if Fp == Fin else torch.nn.functional.pad(X, (0, Fp - Fin))
+        if Xpad is not None:
+            Xp = Xpad
+        else:
+            Xp = X if Fp == Fin else torch.nn.functional.pad(X, (0, Fp - Fin))
         attn_l, attn_r = _c(attn_l), _c(attn_r)
-        attn_lr = torch.cat([attn_l.reshape(-1), attn_r.reshape(-1)])
+        HFa = attn_l.numel()
+        attn_lr = torch.empty(2 * HFa, dtype=torch.float32, device=X.device)
+        copy2d(attn_lr[:HFa], attn_l.reshape(-1))
+        copy2d(attn_lr[HFa:], attn_r.reshape(-1))
         ctx.elu_claim = None
         link = _elu_link_of(X) if (ELU_LINK[0] and (algo or GEMM_ALGO) == "f16x2" and ROW_SCALES
                                    and PROJ_ELR_GEMM and X.requires_grad) else None
@@ -353,7 +415,7 @@ class GATLayerFunction(torch.autograd.Function):
         xr = None  # per-row max |X| bits (ROW_SCALES)
         wil = None  # Wcat's interleaved split image (BSPLIT_IL)
         if (algo or GEMM_ALGO) == "f16x2":
-            amx = torch.zeros(4, dtype=torch.int32, device=dev)  # [X, Wcat, gY (bwd), out]
+            amx = zeros(4, dtype=torch.int32, device=dev)  # [X, Wcat, gY (bwd), out]
             if ROW_SCALES and PROJ_ELR_GEMM:
                 # the projection splits every atom row with its own scale; max |X| (the weight
                 # gradient's A-side scale) is the max of the row maxima (N floats, not N x Fp).
@@ -361,7 +423,7 @@ class GATLayerFunction(torch.autograd.Function):
                 # zeros): computed once and recorded on the feature tensor itself
                 xr = known_rows(X)
                 if xr is None:
-                    xr = absmax_rows(X, N, Fin, Fin)
+                    xr = absmax_rows(Xp, N, Fin, Fp)
                     if not X.requires_grad:
                         fold_rows(X, xr)
                 absmax(xr, N, 1, 1, amx, 0)
@@ -397,7 +459,10 @@ class GATLayerFunction(torch.autograd.Function):
                 gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, amax=(slot(*ax), slot(amx, 1)))
             else:
                 gemm(Xp, Wcat, N, C + 2 * H, Fp, 0, 0, Fp, Fp, Y, ldy, algo="bf16")
-            elr = Y[:, C:C + 2 * H].contiguous()
+            # (a native slice copy: torch's strided copy splits into 32-bit-indexable pieces,
+            # 8 launches for a 1.75 M-atom batch)
+            elr = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
+            call("mvml_copy_cols", N, 2 * H, ptr(Y[:, C:]), ldy, ptr(elr), 2 * H, st)
         else:
             ldy = _row_pitch(C)
             Y = torch.empty((N, ldy), dtype=torch.float32, device=dev)
@@ -469,7 +534,7 @@ class GATLayerFunction(torch.autograd.Function):
         st = _stream(dev)
         gY = torch.empty((N, ldg), dtype=torch.float32, device=dev)
         if ctx.amx is not None:
-            ctx.amx[2:3].zero_()  # max |gY| of THIS backward (a second one, retain_graph, refolds it)
+            zero_(ctx.amx[2:3])  # max |gY| of THIS backward (a second one, retain_graph, refolds it)
         wp, wn = _lib.ws_ptr_size(L.mvml_gat_agg_bwd_workspace_size(g.num_edges(), H), dev)
         # per-row max |gY| for the data-gradient product's per-row scales (not needed by layer 1,
         # whose input gradient is not formed)
@@ -512,7 +577,7 @@ class GATLayerFunction(torch.autograd.Function):
         g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
         if mean_res:  # every head's bias sees g_out / H: one column sum, replicated over heads
             colsum(gY, N, F, ldg, g_bias, offset=HF, alpha=1.0 / H)
-            g_bias.view(H, F)[1:].copy_(g_bias[:F].expand(H - 1, F))
+            copy2d(g_bias.view(H, F)[1:], g_bias[:F].view(1, F).expand(H - 1, F))
         else:
             colsum(gY, N, HF, ldg, g_bias, offset=HF)
         gX = None
@@ -522,7 +587,7 @@ class GATLayerFunction(torch.autograd.Function):
             if link is not None and amx is not None and ROW_SCALES and ctx.wil is not None:
                 # the previous layer's ELU backward in this product's epilogue: gX leaves as its
                 # g_rst, with max |g_rst| folded for its GEMMs (EluLink)
-                link.amax.zero_()
+                zero_(link.amax)
                 _lib.call_tag[0] = {"flops": 2 * N * Fin * CE, "shape": (N, Fin, CE, 0, 1)}
                 call("mvml_gemm_f16x2_ex", N, Fin, CE, 1, ptr(gY), ldg, 0, ptr(Wcat), Fp, 1, ptr(ctx.wil),
                      0, ptr(gyr if gyr is not None else absmax_rows(gY, N, CE, ldg)), 0, slot(amx, 1),
@@ -564,14 +629,16 @@ class Set2SetFunction(torch.autograd.Function):
         # (XH[l+1][t][:, :D], or q_t = XH[0][t+1][:, :D] for the top layer).
         kin = [2 * D] + [D] * (Lr - 1)
         XH = [torch.empty((T + 1, B, kin[l] + D), **f32) for l in range(Lr)]
-        XH[0][0].zero_()
+        zero_(XH[0][0])
         for l in range(1, Lr):
-            XH[l][0, :, D:].zero_()
-        Wcat = [torch.cat([w[0], w[1]], dim=1).contiguous() for w in W]
+            zero_(XH[l][0, :, D:])
         L = _lib.lib()
-        # interleaved rows for the cell epilogue: row 4 j + q = row q D + j (unit j's i, f, g, o)
-        Wperm = [Wcat[l].view(4, D, kin[l] + D).transpose(0, 1).reshape(4 * D, kin[l] + D).contiguous()
-                 if CELL_EPI else None for l in range(Lr)]
+        # [W_ih | W_hh] and (cell epilogue) its interleaved rows: row 4 j + q = row q D + j (unit
+        # j's i, f, g, o), both from one mvml_lstm_pack_weights launch per layer
+        Wcat = [torch.empty((4 * D, kin[l] + D), **f32) for l in range(Lr)]
+        Wperm = [torch.empty((4 * D, kin[l] + D), **f32) if CELL_EPI else None for l in range(Lr)]
+        for l in range(Lr):
+            call("mvml_lstm_pack_weights", D, kin[l], ptr(W[l][0]), ptr(W[l][1]), ptr(Wcat[l]), ptr(Wperm[l]), st)
         acts = torch.empty((T, Lr, B, 4 * D), **f32)
         cs = torch.empty((T, Lr, B, D), **f32)
         lse = torch.empty((T, B), **f32)
@@ -585,11 +652,12 @@ class Set2SetFunction(torch.autograd.Function):
             # (a convex combination: |r| <= max |X|), so max(1, max |X|) bounds every cell's A
             # (an upper bound is all the scale needs) — one pass instead of one per cell
             kx = known_amax(X)  # folded by the last GAT layer's aggregation
-            if kx is not None:  # max(1, max |X|) on the float bits (non-negative: int order)
-                amax_x = torch.clamp_min(kx[0][kx[1]:kx[1] + 1], 0x3F800000)
-            else:
-                amax_x = torch.full((1,), 0x3F800000, dtype=torch.int32, device=dev)  # 1.0f
-                absmax(X, N, D, D, amax_x, 0, accumulate=True)
+            if kx is None:
+                kx = (zeros(1, dtype=torch.int32, device=dev), 0)
+                absmax(X, N, D, D, kx[0], 0, accumulate=True)
+            # max(1, max |X|) on the float bits (non-negative: int order), one "segment" [0, 1)
+            amax_x = torch.empty(1, dtype=torch.int32, device=dev)
+            call("mvml_segment_max_bits", 1, ptr(_unit_segment(dev)), slot(*kx), 0x3F800000, ptr(amax_x), st)
             if ROW_SCALES:
                 # per molecule: max(1, max |X| over its atoms) bounds every entry of its cell rows
                 # [x | h] (h = o tanh c, the readout a convex combination of its own atoms' rows),
@@ -623,21 +691,22 @@ class Set2SetFunction(torch.autograd.Function):
                          kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, pa, pw, ptr(mrows),
                          ptr(wsp[l][0]), wsp[l][1], st)
                     continue
+                gp = gates
                 if t == 0 and l == 0:
-                    gates.zero_()  # q*_{-1} = 0 and h_0(-1) = 0
+                    gp = None  # q*_{-1} = 0 and h_0(-1) = 0: zero pre-activations, the bias alone
                 else:
                     gemm(XH[l][t], Wcat[l], B, 4 * D, K, 0, 0, kin[l] + D, kin[l] + D, gates, 4 * D,
                          amax=None if amax_x is None else (slot(amax_x, 0), slot(amax_w, l)),
                          arows=mrows,
                          bil4=wsp[l][0] if not CELL_EPI and wsp[l][1] == 0 else None)
-                call("mvml_lstm_cell_fwd", B, D, ptr(gates), ptr(b_ih), ptr(b_hh), ptr(c_prev),
+                call("mvml_lstm_cell_fwd", B, D, ptr(gp), ptr(b_ih), ptr(b_hh), ptr(c_prev),
                      ptr(cs[t, l]), ptr(own), kin[l] + D, ptr(acts[t, l]), ptr(nxt), ldn, st)
             call("mvml_set2set_seg_fwd", B, D, ptr(g.node_offsets), ptr(X), ptr(XH[0][t + 1]), 3 * D,
                  ptr(lse[t]), st)
         ctx.save_for_backward(X, acts, cs, lse, *XH, *[p for w in W for p in w])
         ctx.g, ctx.T, ctx.Lr = g, T, Lr
         ctx.amax = (amax_x, amax_w)
-        return XH[0][T][:, :2 * D].clone()
+        return copy2d(torch.empty((B, 2 * D), **f32), XH[0][T][:, :2 * D])
 
     @staticmethod
     def backward(ctx, g_out):
@@ -656,21 +725,24 @@ class Set2SetFunction(torch.autograd.Function):
         # g_qs3[t-1] = [dL/dq*_{t-1} (2D) | dL/dh_0(t-1) (D)], for layers l > 0 in gxh[l] =
         # [dL/dh_{l-1}(t) | dL/dh_l(t-1)].  N = kin + D fills whole 256-column GEMM tiles
         # (768 / 1152) where two products of N = 384 would each waste a quarter of theirs.
-        Wcat = [torch.cat([w[0], w[1]], dim=1).contiguous() for w in W]
+        kins = [2 * D] + [D] * (Lr - 1)
+        Wcat = [torch.empty((4 * D, kins[l] + D), **f32) for l in range(Lr)]
+        for l in range(Lr):
+            call("mvml_lstm_pack_weights", D, kins[l], ptr(W[l][0]), ptr(W[l][1]), ptr(Wcat[l]), None, st)
         g_qs3 = torch.empty((T, B, 3 * D), **f32)
         g_qstars = g_qs3[:, :, :2 * D]
-        g_qstars[T - 1].copy_(g_out)
+        copy2d(g_qstars[T - 1], _c(g_out))
         alphas = torch.empty((T, N), **f32)
         g_es = torch.empty((T, N), **f32)
-        gW_ih = [torch.zeros_like(w[0]) for w in W]
-        gW_hh = [torch.zeros_like(w[1]) for w in W]
-        gb = [torch.zeros_like(w[2]) for w in W]
+        gW_ih = [torch.empty_like(w[0]) for w in W]  # written below (one product per layer)
+        gW_hh = [torch.empty_like(w[1]) for w in W]
+        gb = [torch.empty_like(w[2]) for w in W]
         # every step's gate gradients are kept so that each weight gradient is ONE GEMM over
         # all T*B rows after the recurrence (K = 393k instead of 6 launches of 65k)
         g_gates_all = torch.empty((Lr, T, B, 4 * D), **f32)
         g_h = torch.empty((B, D), **f32)
         gxh = [None] + [torch.empty((B, 2 * D), **f32) for _ in range(1, Lr)]
-        g_c = [torch.zeros((B, D), **f32) for _ in range(Lr)]
+        g_c = [torch.empty((B, D), **f32) for _ in range(Lr)]  # first read at t = T - 2 (None before)
         g_c_new = torch.empty((B, D), **f32)
         # LSTM bias gradients: every cell backward leaves [R, 4D] partial column sums of its
         # gate gradients (mvml_lstm_cell_bwd's gb_part); one column sum over the T R partial rows
@@ -681,7 +753,7 @@ class Set2SetFunction(torch.autograd.Function):
         # running |max| of each layer's gate gradients, folded in by mvml_lstm_cell_bwd (the
         # running value bounds every cell seen so far, which is all a scale needs)
         amax_x, amax_w = ctx.amax
-        amax_g = torch.zeros(Lr, dtype=torch.int32, device=dev) if amax_x is not None else None
+        amax_g = zeros(Lr, dtype=torch.int32, device=dev) if amax_x is not None else None
         wib = [None] * Lr  # [W_ih | W_hh] split once (interleaved image) for the per-cell data-gradient products
         if amax_g is not None:
             wib = [split_il4(Wcat[l], 4 * D, Wcat[l].shape[1], Wcat[l].shape[1], slot(amax_w, l))
@@ -731,15 +803,15 @@ class Set2SetFunction(torch.autograd.Function):
                 gWcat = torch.empty((4 * D, ldx), **f32)
                 gemm(G[t0:], XH[l][t0:T], 4 * D, ldx, (T - t0) * B, 1, 1, 4 * D, ldx, gWcat, ldx,
                      amax=None if amax_g is None else (slot(amax_g, l), slot(amax_x, 0)))
-                gW_ih[l].copy_(gWcat[:, :kin])
-                gW_hh[l].copy_(gWcat[:, kin:])
+                copy2d(gW_ih[l], gWcat[:, :kin])
+                copy2d(gW_hh[l], gWcat[:, kin:])
             colsum(gb_part[l], T * R, 4 * D, 4 * D, gb[l])
         gX = torch.empty((N, D), **f32)
         call("mvml_set2set_gx", N, D, T, ptr(g.node_graph), ptr(g.node_offsets), B, ptr(qs), 3 * D, B * 3 * D,
              ptr(g_qs3), 3 * D, B * 3 * D, ptr(alphas), ptr(g_es), ptr(gX), st)
         grads = []
         for l in range(Lr):
-            grads += [gW_ih[l], gW_hh[l], gb[l], gb[l].clone()]
+            grads += [gW_ih[l], gW_hh[l], gb[l], copy2d(torch.empty_like(gb[l]), gb[l])]
         return (gX, None, None, None, *grads)
 
 
@@ -783,7 +855,7 @@ def linear_maxima(x, w):
     x's per-row maxima for the forward product; None for the other algorithms."""
     if GEMM_ALGO != "f16x2":
         return None
-    amx = torch.zeros(3, dtype=torch.int32, device=x.device)
+    amx = zeros(3, dtype=torch.int32, device=x.device)
     xr = None
     if ROW_SCALES:
         xr = row_maxima(x, x.shape[0], x.shape[1], x.shape[1])
@@ -820,12 +892,35 @@ def linear_dx(g, weight, gx, M, Nout, K, lm):
              bil4=None if lm is None else lm[3])
 
 
+def dropout_seed():
+    """A seed for mvml_dropout_fwd from torch's default (CPU) generator: reproducible under
+    torch.manual_seed like nn.Dropout's draws, and no device round trip."""
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+
+
+def dropout_p(module):
+    """The probability an nn.Dropout module applies now (0 in eval mode)."""
+    return float(module.p) if module.training and module.p > 0 else 0.0
+
+
+def relu_dropout_(y, p):
+    """nn.Dropout(p) in place on a ReLU output y (mvml_dropout_fwd); returns the backward's
+    scale 1 / (1 - p) (1.0 for p == 0: nothing launched)."""
+    if p <= 0.0:
+        return 1.0
+    if p >= 1.0:
+        raise ValueError("dropout probability must be < 1 on the HIP path")
+    call("mvml_dropout_fwd", y.numel(), ptr(y), ptr(y), float(p), dropout_seed(), _stream(y.device))
+    return float(np.float32(1.0 / (1.0 - p)))  # the float the kernel multiplied by
+
+
 class LinearReLUFunction(torch.autograd.Function):
     """nn.Linear + nn.ReLU of GNNModule.fc (model.py:86-87) as one MFMA GEMM with a bias+ReLU
-    epilogue."""
+    epilogue, and the nn.Dropout(p) that follows it (model.py:87; p = 0: none) applied in place
+    on the ReLU output: the backward then needs no mask (mvml_relu_bwd's scaled form)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, p=0.0):
         _check_cuda_f32(x, "x")
         x = _c(x)
         M, K = x.shape
@@ -835,7 +930,8 @@ class LinearReLUFunction(torch.autograd.Function):
         lm = ctx.lm = linear_maxima(x, weight)
         linear_fwd(x, weight, y, M, Nout, K, lm, bias=_c(bias), act=1)
         if DEBUG_CAPTURE is not None:  # the ReLU sides the product took (parity tests)
-            DEBUG_CAPTURE.setdefault("relu_out", []).append(y.detach())
+            DEBUG_CAPTURE.setdefault("relu_out", []).append(y.detach().clone())
+        ctx.scale = relu_dropout_(y, p)
         ctx.save_for_backward(x, weight, y)
         return y
 
@@ -847,7 +943,7 @@ class LinearReLUFunction(torch.autograd.Function):
         Nout = weight.shape[0]
         dev = x.device
         g_pre = torch.empty_like(y)
-        call("mvml_relu_bwd", y.numel(), ptr(y), ptr(g_y), ptr(g_pre), _stream(dev))
+        call("mvml_relu_bwd", y.numel(), ptr(y), ptr(g_y), ptr(g_pre), float(ctx.scale), _stream(dev))
         lm = ctx.lm
         if lm is not None:
             absmax(g_pre, M, Nout, Nout, lm[0], 2)
@@ -860,4 +956,4 @@ class LinearReLUFunction(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
             linear_dx(g_pre, weight, gx, M, Nout, K, lm)
-        return gx, gw, gb
+        return gx, gw, gb, None

@@ -12,6 +12,7 @@ of model.py:72.  Parameter names / shapes equal MVP's, so ``MVP.state_dict()`` e
 import math
 import os
 
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -85,7 +86,7 @@ class FusionAttnConvFunction(torch.autograd.Function):
     + ReLU.  Returns (B, nh * (dim - 2)) like ``self.conv(att).view(B, -1)`` before Dropout."""
 
     @staticmethod
-    def forward(ctx, smiles_x, graph_x, fp_x, ln_w, ln_b, wq, wk, wv, conv_w, conv_b, eps):
+    def forward(ctx, smiles_x, graph_x, fp_x, ln_w, ln_b, wq, wk, wv, conv_w, conv_b, eps, p=0.0):
         for t, n in ((smiles_x, "smiles_x"), (graph_x, "graph_x"), (fp_x, "fp_x")):
             _check_cuda_f32(t, n)
         B, D = graph_x.shape
@@ -93,12 +94,16 @@ class FusionAttnConvFunction(torch.autograd.Function):
         dev = graph_x.device
         st = _stream(dev)
         f32 = dict(dtype=torch.float32, device=dev)
-        X = torch.stack([_c(smiles_x), _c(graph_x), _c(fp_x)], dim=1).reshape(3 * B, D)  # row 3b+t
+        # the shared LayerNorm, one launch per view, each writing its rows 3b+t of Xn (no stacked
+        # copy of the three embeddings; the backward returns each view's gradient contiguous)
+        views = [_c(smiles_x), _c(graph_x), _c(fp_x)]
         Xn = torch.empty((3 * B, D), **f32)
-        mean = torch.empty((3 * B,), **f32)
-        rstd = torch.empty((3 * B,), **f32)
-        call("mvml_layernorm_fwd", 3 * B, D, ptr(X), D, ptr(_c(ln_w)), ptr(_c(ln_b)), float(eps),
-             ptr(Xn), D, ptr(mean), ptr(rstd), st)
+        Xn3 = Xn.view(B, 3, D)
+        mean = torch.empty((3, B), **f32)
+        rstd = torch.empty((3, B), **f32)
+        for t, xt in enumerate(views):
+            call("mvml_layernorm_fwd", B, D, ptr(xt), D, ptr(_c(ln_w)), ptr(_c(ln_b)), float(eps),
+                 ptr(Xn3[:, t]), 3 * D, ptr(mean[t]), ptr(rstd[t]), st)
         P = torch.empty((B, H, 3, 3), **f32)
         scale = 1.0 / math.sqrt(D)
         HD = H * D
@@ -111,10 +116,11 @@ class FusionAttnConvFunction(torch.autograd.Function):
             # Bcat [D, 2 H D] = [M_1 .. M_H | W_v^T]: M_h[i][j] = sum_o Wq_h[o][i] Wk_h[o][j]
             Bcat = torch.empty((D, 2 * HD), **f32)
             gemm_batched(wq3, wk3, D, D, D, 1, 1, D, D, Bcat, 2 * HD, H, D * D, D * D, D)
-            Bcat[:, HD:].copy_(_c(wv).t())  # parameter layout (7 MB), not a product
+            # W_v^T into Bcat's right half: parameter layout (7 MB), not a product
+            call("mvml_transpose", HD, D, ptr(_c(wv)), D, ptr(Bcat[:, HD:]), 2 * HD, st)
             PV = torch.empty((3 * B, 2 * HD), **f32)  # rows 3b+t: [x M_1 .. x M_H | x W_v^T]
             if _F.GEMM_ALGO == "f16x2" and _F.ROW_SCALES:  # every token row at its own scale
-                bmx = torch.zeros(1, dtype=torch.int32, device=dev)
+                bmx = _F.zeros(1, dtype=torch.int32, device=dev)
                 absmax(Bcat, D, 2 * HD, 2 * HD, bmx, 0)
                 gemm(Xn, Bcat, 3 * B, 2 * HD, D, 0, 1, D, 2 * HD, PV, 2 * HD, amax=(None, slot(bmx, 0)),
                      arows=_F.absmax_rows(Xn, 3 * B, D, D),
@@ -122,9 +128,16 @@ class FusionAttnConvFunction(torch.autograd.Function):
             else:
                 gemm(Xn, Bcat, 3 * B, 2 * HD, D, 0, 1, D, 2 * HD, PV, 2 * HD)
             if fused:
+                # the Dropout after the ReLU (model.py:36) in the kernel's store (the parity tests'
+                # ReLU-side capture needs the undropped output: then it runs separately below)
+                fp = p if (p > 0.0 and _F.DEBUG_CAPTURE is None) else 0.0
                 _lib.call_tag[0] = {"bytes": attn_conv_bytes(B, H, D, False)}
                 call("mvml_attn_conv_fwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
-                     ptr(_c(conv_w)), ptr(_c(conv_b)), ptr(P), ptr(out), st)
+                     ptr(_c(conv_w)), ptr(_c(conv_b)), ptr(P), ptr(out), float(fp),
+                     _F.dropout_seed() if fp > 0.0 else 0, st)
+                if fp > 0.0:
+                    p = 0.0
+                    ctx.g_scale = float(np.float32(1.0 / (1.0 - fp)))
             else:
                 call("mvml_token_attn_fold_fwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
                      ptr(att), ptr(P), st)
@@ -138,16 +151,21 @@ class FusionAttnConvFunction(torch.autograd.Function):
         if not fused:
             call("mvml_conv3_fwd", B, H, H, D, ptr(att), ptr(_c(conv_w)), ptr(_c(conv_b)), ptr(out), st)
         if _F.DEBUG_CAPTURE is not None:  # the ReLU sides the product took (parity tests)
-            _F.DEBUG_CAPTURE["conv_out"] = out.detach()
-        ctx.save_for_backward(X, Xn, mean, rstd, ln_w, wq, wk, wv, *saved, P, att, out, conv_w)
+            _F.DEBUG_CAPTURE["conv_out"] = out.detach().clone()
+        # the Dropout after the ReLU (model.py:36), in place where the kernel did not apply it:
+        # the backward needs no mask either way
+        if p > 0.0 or not hasattr(ctx, "g_scale"):
+            ctx.g_scale = _F.relu_dropout_(out, p)
+        ctx.save_for_backward(*views, Xn, mean, rstd, ln_w, wq, wk, wv, *saved, P, att, out, conv_w)
         ctx.dims = (B, D, H, scale, fold, fused)
         return out.view(B, H * (D - 2))
 
     @staticmethod
     def backward(ctx, g_out):
-        X, Xn, mean, rstd, ln_w, wq, wk, wv, S0, S1, P, att, out, conv_w = ctx.saved_tensors
+        x0, x1, x2, Xn, mean, rstd, ln_w, wq, wk, wv, S0, S1, P, att, out, conv_w = ctx.saved_tensors
+        views = (x0, x1, x2)
         B, D, H, scale, fold, fused = ctx.dims
-        dev = X.device
+        dev = x0.device
         st = _stream(dev)
         f32 = dict(dtype=torch.float32, device=dev)
         L = _lib.lib()
@@ -166,17 +184,18 @@ class FusionAttnConvFunction(torch.autograd.Function):
             gPV = torch.empty((3 * B, 2 * HD), **f32)
             amx = None
             if _F.GEMM_ALGO == "f16x2":  # split-fp16 maxima: gPV (folded by the kernel), Xn, Bcat
-                amx = torch.zeros(3, dtype=torch.int32, device=dev)
+                amx = _F.zeros(3, dtype=torch.int32, device=dev)
             # g_k (the keys' gradient, summed over heads) lands in gXn: the GEMMs add onto it
             # per-row |gPV| maxima for the data-gradient product (folded by the fused kernel)
             gpr = None
             if amx is not None and _F.ROW_SCALES:
-                gpr = torch.zeros(3 * B, dtype=torch.int32, device=dev)
+                gpr = _F.zeros(3 * B, dtype=torch.int32, device=dev)
             if fused:
                 wp, wn = _lib.ws_ptr_size(L.mvml_attn_conv_bwd_workspace_size(B), dev)
                 _lib.call_tag[0] = {"bytes": attn_conv_bytes(B, H, D, True)}
                 call("mvml_attn_conv_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
-                     ptr(P), ptr(_c(conv_w)), ptr(out), ptr(g_out), ptr(gPV), 2 * HD, ptr(gXn), D,
+                     ptr(P), ptr(_c(conv_w)), ptr(out), ptr(g_out), float(ctx.g_scale), ptr(gPV), 2 * HD,
+                     ptr(gXn), D,
                      slot(amx, 0), ptr(gpr), ptr(g_cw), ptr(g_cb), wp, wn, st)
             else:
                 call("mvml_token_attn_fold_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, float(scale),
@@ -214,16 +233,18 @@ class FusionAttnConvFunction(torch.autograd.Function):
             gemm(gQKV, Xn, 3 * HD, D, 3 * B, 1, 1, 3 * HD, D, gW, D)
             gemm(gQKV, Wqkv, 3 * B, D, 3 * HD, 0, 1, 3 * HD, D, gXn, D)
             g_wq, g_wk, g_wv = gW[:HD], gW[HD:2 * HD], gW[2 * HD:]
-        gX = torch.empty((3 * B, D), **f32)
-        gyxh = torch.empty((3 * B, D), **f32)
-        call("mvml_layernorm_bwd", 3 * B, D, ptr(X), D, ptr(_c(ln_w)), ptr(mean), ptr(rstd), ptr(gXn), D,
-             ptr(gX), D, ptr(gyxh), st)
+        gXn3 = gXn.view(B, 3, D)
+        gyxh = torch.empty((3, B, D), **f32)
+        gX = []
+        for t, xt in enumerate(views):
+            gX.append(torch.empty((B, D), **f32))
+            call("mvml_layernorm_bwd", B, D, ptr(xt), D, ptr(_c(ln_w)), ptr(mean[t]), ptr(rstd[t]),
+                 ptr(gXn3[:, t]), 3 * D, ptr(gX[t]), D, ptr(gyxh[t]), st)
         g_lnw = torch.empty((D,), **f32)
         g_lnb = torch.empty((D,), **f32)
         colsum(gyxh, 3 * B, D, D, g_lnw)
         colsum(gXn, 3 * B, D, D, g_lnb)
-        gX = gX.view(B, 3, D)
-        return (gX[:, 0], gX[:, 1], gX[:, 2], g_lnw, g_lnb, g_wq, g_wk, g_wv, g_cw, g_cb, None)
+        return (gX[0], gX[1], gX[2], g_lnw, g_lnb, g_wq, g_wk, g_wv, g_cw, g_cb, None, None)
 
 
 class BCEWithLogitsFunction(torch.autograd.Function):
@@ -235,14 +256,19 @@ class BCEWithLogitsFunction(torch.autograd.Function):
         z, y = _c(logits), _c(labels.float())
         terms = torch.empty_like(z)
         gz = torch.empty_like(z)
-        call("mvml_bce_logits", z.numel(), ptr(z), ptr(y), ptr(terms), ptr(gz), _stream(z.device))
+        n = z.numel()
+        call("mvml_bce_logits", n, ptr(z), ptr(y), ptr(terms), ptr(gz), _stream(z.device))
         ctx.save_for_backward(gz)
-        return terms.sum() / z.numel()
+        loss = torch.empty((1,), dtype=torch.float32, device=z.device)
+        colsum(terms, n, 1, 1, loss, alpha=1.0 / n)  # the mean, one native column sum
+        return loss.view(())
 
     @staticmethod
     def backward(ctx, g):
         (gz,) = ctx.saved_tensors
-        return gz * g, None
+        out = torch.empty_like(gz)
+        call("mvml_scale_by", gz.numel(), ptr(gz), ptr(_c(g)), ptr(out), _stream(gz.device))
+        return out, None
 
 
 def bce_with_logits(logits, labels):
@@ -277,19 +303,19 @@ class MVFusion(nn.Module):
         out = FusionAttnConvFunction.apply(smiles_x, graph_x, fp_x, ln.weight, ln.bias,
                                            self.linear_q.weight, self.linear_k.weight,
                                            self.linear_v.weight, self.conv[0].weight,
-                                           self.conv[0].bias, ln.eps)
-        out = self.conv[2](out)
-        out = LinearReLUFunction.apply(out, self.mlp[0].weight, self.mlp[0].bias)
-        out = self.mlp[2](out)
+                                           self.conv[0].bias, ln.eps, _F.dropout_p(self.conv[2]))
+        # conv = Conv2d -> ReLU -> Dropout, mlp = Linear -> ReLU -> Dropout -> Linear: each
+        # Dropout in place on its ReLU output (mvml_dropout_fwd; the backward needs no mask)
+        out = LinearReLUFunction.apply(out, self.mlp[0].weight, self.mlp[0].bias, _F.dropout_p(self.mlp[2]))
         return LinearFunction.apply(out, self.mlp[3].weight, self.mlp[3].bias)
 
 
 class FPNModule(nn.Module):
     """The fingerprint view's MLP, model.py:138-155, on the HIP GEMMs:
     fc1 (2513 -> fp_2_dim) -> Dropout -> ReLU -> fc2 (-> out_feats), parameter names as in the
-    reference.  fc1 + ReLU run as one GEMM with a bias+ReLU epilogue and the Dropout follows:
-    ReLU(mask * z / (1-p)) == mask * ReLU(z) / (1-p) exactly, and the mask is drawn for the same
-    shape, so this equals the reference order.  The 2513-bit fingerprints themselves (MACCS,
+    reference.  fc1 + ReLU run as one GEMM with a bias+ReLU epilogue and the Dropout follows,
+    in place: ReLU(mask * z / (1-p)) == mask * ReLU(z) / (1-p) exactly, and the mask is drawn
+    for the same shape, so this equals the reference order.  The 2513-bit fingerprints themselves (MACCS,
     ErG, PubChem, Morgan; dataset.py:37-45) need RDKit and are out of scope."""
 
     def __init__(self, fp_2_dim, out_feats, dropout=0.2):
@@ -304,6 +330,5 @@ class FPNModule(nn.Module):
         self.dropout = nn.Dropout(p=self.dropout_fpn)
 
     def forward(self, fp):
-        h = LinearReLUFunction.apply(fp, self.fc1.weight, self.fc1.bias)
-        h = self.dropout(h)
+        h = LinearReLUFunction.apply(fp, self.fc1.weight, self.fc1.bias, _F.dropout_p(self.dropout))
         return LinearFunction.apply(h, self.fc2.weight, self.fc2.bias)

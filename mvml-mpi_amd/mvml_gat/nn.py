@@ -254,5 +254,5 @@ class GNNModule(nn.Module):
         node_x = self.conv(graphs, atom_feats)
         graph_x = self.readout(graphs, node_x)
         out = self.norm(graph_x, group_offsets=graphs.group_offsets_rows())
-        out = Fn.LinearReLUFunction.apply(out, self.fc[0].weight, self.fc[0].bias)
-        return self.fc[2](out)
+        # fc = Linear -> ReLU -> Dropout (model.py:86-87): the Dropout in place on the ReLU output
+        return Fn.LinearReLUFunction.apply(out, self.fc[0].weight, self.fc[0].bias, Fn.dropout_p(self.fc[2]))

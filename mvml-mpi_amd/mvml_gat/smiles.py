@@ -26,6 +26,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from . import functional as _F
 from ._lib import call, lib, ptr, workspace
 from .functional import LinearReLUFunction, _c, _check_cuda_f32, _stream, absmax, colsum, gemm, slot
 
@@ -474,5 +475,4 @@ class RNNModule(nn.Module):
             if l + 1 < self.num_layers and self.training and self.rnn.dropout > 0:
                 x = nn.functional.dropout(x, self.rnn.dropout, True)  # nn.LSTM inter-layer dropout
         fea = SelectLastFunction.apply(x, pk)
-        out = LinearReLUFunction.apply(fea, self.fc[0].weight, self.fc[0].bias)
-        return self.fc[2](out)
+        return LinearReLUFunction.apply(fea, self.fc[0].weight, self.fc[0].bias, _F.dropout_p(self.fc[2]))

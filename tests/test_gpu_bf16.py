@@ -8,9 +8,10 @@
   reference semantics);
 * gradients against the bf16-EMULATED float64 oracle (oracle/gnn_ref.py, proj='bf16': the
   projection operands X, Wcat and gY rounded to bf16 exactly where the product rounds them,
-  everything else float64): within EMU_FRO norm-wise on every parameter, and each gradient's
-  error against the exact float64 oracle at most EMU_RATIO x the emulated oracle's own (the
-  error of bf16 itself, not of the kernels)."""
+  everything else float64): each gradient's distance to the emulated oracle's at most EMU_REL
+  (a tenth) of the bf16 error itself, and its error against the exact float64 oracle at most
+  EMU_RATIO x the emulated oracle's own (the error of bf16, not of the kernels); the output
+  within EMU_FRO of the emulated oracle's."""
 import pytest
 import torch
 
@@ -21,9 +22,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 TOL_EXACT = 1e-5
 TOL_BF16 = 2e-2
-# gradients vs the bf16-emulated oracle: what is left is fp32 accumulation and the rare
-# element whose fp32 and float64 values round to different bf16 neighbours
+# vs the bf16-emulated oracle what is left is fp32 accumulation and the rare element whose
+# fp32 and float64 values round to different bf16 neighbours (in the gradients such flips
+# compound through the layers: measured <= 2.3% of the bf16 error, config2 x 96)
 EMU_FRO = 1e-4
+EMU_REL = 0.1
 # error vs exact float64 <= EMU_RATIO x the emulated oracle's own error (+ EMU_FLOOR)
 EMU_RATIO, EMU_FLOOR = 1.2, 1e-5
 
@@ -35,7 +38,8 @@ def _fro(a, b):
 
 def check_emulated(prod_named, emu_named, exact_named):
     """{name: (vs emulated, vs exact, emulated vs exact)} and the failures: each gradient within
-    EMU_FRO of the emulated oracle's and no more than EMU_RATIO x its error vs float64."""
+    EMU_REL x (emulated vs exact) of the emulated oracle's and no more than EMU_RATIO x its
+    error vs float64."""
     rows, bad = {}, {}
     for n, p in prod_named:
         ge, gx = emu_named[n].grad, exact_named[n].grad
@@ -44,7 +48,7 @@ def check_emulated(prod_named, emu_named, exact_named):
             continue
         r = (_fro(p.grad, ge), _fro(p.grad, gx), _fro(ge, gx))
         rows[n] = tuple(round(v, 7) for v in r)
-        if not (r[0] < EMU_FRO and r[1] <= EMU_RATIO * r[2] + EMU_FLOOR):
+        if not (r[0] <= EMU_REL * r[2] + EMU_FLOOR and r[1] <= EMU_RATIO * r[2] + EMU_FLOOR):
             bad[n] = rows[n]
     return rows, bad
 

@@ -281,11 +281,11 @@ def test_attn_conv_abi_matches_separate_kernels(B):
         amx = torch.zeros(1, dtype=torch.int32, device=DEV)
         if fused:
             call("mvml_attn_conv_fwd", B, H, D, ptr(PV), 2 * H * D, ptr(Xn), D, sc, ptr(w), ptr(bias),
-                 ptr(P), ptr(out), st)
+                 ptr(P), ptr(out), 0.0, 0, st)
             wp, wn = ws_ptr_size(L.mvml_attn_conv_bwd_workspace_size(B), DEV)
             rows = torch.zeros(3 * B, dtype=torch.int32, device=DEV)
             call("mvml_attn_conv_bwd", B, H, D, ptr(PV), 2 * H * D, ptr(Xn), D, sc, ptr(P), ptr(w),
-                 ptr(out), ptr(gout), ptr(gPV), 2 * H * D, ptr(gk), D, ptr(amx), ptr(rows), ptr(gw),
+                 ptr(out), ptr(gout), 1.0, ptr(gPV), 2 * H * D, ptr(gk), D, ptr(amx), ptr(rows), ptr(gw),
                  ptr(gb), wp, wn, st)
             # the folded per-row maxima equal a pass over the written rows
             torch.cuda.synchronize()

@@ -8,8 +8,11 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+import contextlib
+
+from mvml_gat import functional as Fn
 from mvml_gat import synth
-from mvml_gat._lib import lib, ptr, stream_ptr
+from mvml_gat._lib import lib, option, ptr, stream_ptr
 from mvml_gat.nn import GATLayer
 
 pytestmark = pytest.mark.gpu
@@ -48,11 +51,15 @@ def test_gat_layer_bwd_one_call_bitwise(layer, case):
     g_res = torch.empty((HF, Fin), device=DEV)
     g_attn = torch.empty((2, HF), device=DEV)
     g_bias = torch.empty((HF,), device=DEV)
-    rc = L.mvml_gat_layer_bwd(N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr), ptr(g.in_src),
-                              ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), E, H, Fo, Fin, layer,
-                              ctypes.c_float(0.2), ptr(Xp), ptr(Wcat), ptr(attn_lr), ptr(Y), Y.stride(0),
-                              ptr(elr), ptr(attn), ptr(outs), ptr(gout.contiguous()), ptr(g_X), ptr(g_fc),
-                              ptr(g_res), ptr(g_attn), ptr(g_bias), ptr(ws), ws.numel(), stream_ptr())
+    # the aggregation backward's kernel choice is a process option (mvml_set_option), as for
+    # mvml_gat_agg_bwd: set it the way the Python layer did for this batch
+    flat_src = Fn.FLAT_SRC_AUTO and layer == 0 and Fn._large_batch(g)
+    with option("flat_src", 2) if flat_src else contextlib.nullcontext():
+        rc = L.mvml_gat_layer_bwd(N, ptr(g.node_groups), g.num_node_groups, ptr(g.in_rowptr), ptr(g.in_src),
+                                  ptr(g.out_rowptr), ptr(g.out_dst), ptr(g.out_inslot), E, H, Fo, Fin, layer,
+                                  ctypes.c_float(0.2), ptr(Xp), ptr(Wcat), ptr(attn_lr), ptr(Y), Y.stride(0),
+                                  ptr(elr), ptr(attn), ptr(outs), ptr(gout.contiguous()), ptr(g_X), ptr(g_fc),
+                                  ptr(g_res), ptr(g_attn), ptr(g_bias), ptr(ws), ws.numel(), stream_ptr())
     assert rc == 0, L.mvml_last_error().decode()
     torch.cuda.synchronize()
     conv = m.gat_conv

@@ -51,11 +51,11 @@ def main():
 
     def fused_fwd():
         call("mvml_attn_conv_fwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, sc, ptr(w), ptr(b), ptr(P),
-             ptr(out), st)
+             ptr(out), 0.0, 0, st)
 
     def fused_bwd():
         call("mvml_attn_conv_bwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, sc, ptr(P), ptr(w), ptr(out),
-             ptr(g_out), ptr(gPV), 2 * HD, ptr(gk), D, ptr(amx), None, ptr(gw), ptr(gb), ptr(ws), nws, st)
+             ptr(g_out), 1.0, ptr(gPV), 2 * HD, ptr(gk), D, ptr(amx), None, ptr(gw), ptr(gb), ptr(ws), nws, st)
 
     def sep_fwd():
         call("mvml_token_attn_fold_fwd", B, H, D, ptr(PV), 2 * HD, ptr(Xn), D, sc, ptr(att), ptr(P), st)
