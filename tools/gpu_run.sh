@@ -9,6 +9,7 @@
 #   config5 | mvp | mvpbf16   the other bench workloads      -> gpurun_out/TAG_<pass>.json
 #   ab[:V,V..]     bench.py (20 steps) of each tree back to back on one box: variants/<V> (the
 #                  round-4 / round-5 trees with their own libraries) or . (this tree); default r04,r05,.
+#   dp2            bench.py --gpus 2, both ranks on cuda:0 over gloo -> gpurun_out/TAG_dp2.json
 #   planes[:IDX]   tools/planes_bench.py (IDX: shape indices) -> gpurun_out/TAG_planes.txt
 #   pmc[:WL]       tools/pmc_bench.sh: PMC HBM traffic of the bench workload WL (config3 | config5)
 # Every GPU step runs under its own time limit; the first failing step ends the call.
@@ -55,6 +56,10 @@ for P in "$@"; do
           --no-inference) > ${O}_ab_$VN.json 2> ${O}_ab_$VN.err; rc=$?
         cat ${O}_ab_$VN.json; [ $rc = 0 ] || exit $rc
       done ;;
+    dp2)  # the 2-rank DP path rehearsed on the one GPU (gloo; RCCL refuses two ranks per device)
+      MVML_BENCH_ONE_DEVICE=1 MVML_BENCH_BACKEND=gloo timeout -k 10 600 python -u bench.py --gpus 2 --steps 6 \
+        --warmup 2 --no-cpu-baseline --no-inference > ${O}_dp2.json 2> ${O}_dp2.err; rc=$?
+      cat ${O}_dp2.json; [ $rc = 0 ] || exit $rc ;;
     planes)
       timeout -k 10 600 python -u tools/planes_bench.py $ARG > ${O}_planes.txt 2>&1; rc=$?
       cat ${O}_planes.txt; [ $rc = 0 ] || exit $rc ;;
