@@ -602,8 +602,18 @@ def run(args):
             extra["roofline_proj_l1"]["kernel"] = (
                 "mvml_gemm_f16x2_rows at K <= 96 (layer-1 projection X[N, 76] Wcat[1544, 76]^T, "
                 "gemm_smallk_kernel); bytes = A, B and C once")
+        # layer 1's weight gradient (N = 76 columns: gY^T X over every atom, split-K) streams the
+        # N x 1544 gradient rows once at 36 flop per byte: an HBM roofline of its own too
+        amax_ev = summ.get("mvml_gemm_f16x2_amax", [])
+        dw_ev = [e for e in amax_ev if (e[1] or {}).get("role") == "gat_dw" and e[1]["shape"][1] <= 96]
+        amax_ev = [e for e in amax_ev if e not in dw_ev]
+        if dw_ev:
+            extra["roofline_dw_l1"] = roofline_entry(dw_ev, "hbm", load_traffic(wkey, "gemm_dw_l1"))
+            extra["roofline_dw_l1"]["kernel"] = (
+                "mvml_gemm_f16x2_amax for the layer-1 weight gradient gY[N, 1544]^T X[N, 76] (split-K "
+                "gemm_f32_kernel + splitk_reduce_kernel); bytes = gY's 1544 columns, X and dW once")
         gemm_ev = (summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", [])
-                   + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])
+                   + summ.get("mvml_gemm_f16x2", []) + amax_ev
                    + summ.get("mvml_gemm_f16x2_bsplit", []) + rows_ev
                    + summ.get("mvml_gemm_f32x3_batched", []) + summ.get("mvml_lstm_gates_cell_fwd", [])
                    + summ.get("mvml_gemm_f16x2_ex", []) + summ.get("mvml_gemm_f16x2_batched", [])

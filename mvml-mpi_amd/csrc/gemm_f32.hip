@@ -302,8 +302,10 @@ __device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[FM][FN], int64
                                               int64_t r0, int64_t c0, int lane,
                                               const float* __restrict__ bias, float beta, int act,
                                               float* __restrict__ C, int64_t ldc,
-                                              float* __restrict__ slab, const ProjEpi& epi) {
+                                              float* __restrict__ slab, const ProjEpi& epi,
+                                              int64_t split = -1) {
   const int li = lane & 31, lk = lane >> 5;
+  if (split < 0) split = blockIdx.y;  // the split-K slab's block: the grid's y unless remapped
   // Epilogue. C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
   if constexpr (EPI_LOGW >= 0) {
     constexpr int W = 1 << EPI_LOGW, NV = 32 >> EPI_LOGW;
@@ -360,7 +362,7 @@ __device__ __forceinline__ void tile_epilogue(const f32x16 (&acc)[FM][FN], int64
         if (row >= M) continue;
         float v = acc[i][j][r];
         if (slab) {
-          slab[((int64_t)blockIdx.y * M + row) * N + col] = v;
+          slab[(split * M + row) * N + col] = v;
         } else {
           v += bcol;
           float* cp = C + row * ldc + col;
@@ -437,12 +439,25 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   __shared__ __attribute__((aligned(16))) float lds[2 * 2 * kTileFloats];
 
   // XCD-aware tile order: each XCD walks a contiguous range of tiles, N fastest, so the
-  // workgroups sharing an A row-panel share one L2.
+  // workgroups sharing an A row-panel share one L2.  Split-K grids (S % 8 == 0, no batch):
+  // every tile of one K split runs on ONE XCD, back to back (XCD x takes splits x, x + 8, ...),
+  // so the K chunk of the operand all the tiles share (the skinny weight gradients' B, e.g.
+  // the layer-1 atom features under every 128-row tile of the 1544 gradient rows) is read from
+  // HBM once into that XCD's L2 instead of once per XCD.
   const int64_t tiles_n = ceil_div(N, BN);
-  const int64_t tile = xcd_block(blockIdx.x, gridDim.x);
+  int64_t tile, split;
+  if (gridDim.y > 1 && gridDim.y % 8 == 0 && gridDim.z == 1) {
+    const int64_t L = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;  // dispatch order; XCD = L % 8
+    const int64_t j = L / 8;
+    split = L % 8 + 8 * (j / gridDim.x);
+    tile = j % gridDim.x;
+  } else {
+    tile = xcd_block(blockIdx.x, gridDim.x);
+    split = blockIdx.y;
+  }
   const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
   if (m0 >= M) return;  // a dual launch's shorter product (grid sized for the longer one)
-  const int64_t kbeg = (int64_t)blockIdx.y * k_split;
+  const int64_t kbeg = split * k_split;
   const int64_t kend = min(K, kbeg + k_split);
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -627,7 +642,7 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     }
   }
   tile_epilogue<EPI_LOGW>(acc, M, N, m0 + wm * 64, n0 + wn * 64, lane, bias, beta, act, C, ldc,
-                          slab, epi);
+                          slab, epi, split);
 }
 
 // ---- split-bf16 GEMM with the split done once per workgroup, at staging -------------------

@@ -558,7 +558,7 @@ class GATLayerFunction(torch.autograd.Function):
         # dL/d[Wcat ; A_l ; A_r] = gY^T X  (split-K over atoms)
         gW = torch.empty((CE, Fp), dtype=torch.float32, device=dev)
         gemm(gY, Xp, CE, Fp, N, 1, 1, ldg, Fp, gW, Fp, algo=ctx.algo,
-             amax=None if amx is None else (slot(amx, 2), slot(*ctx.ax)))
+             amax=None if amx is None else (slot(amx, 2), slot(*ctx.ax)), role="gat_dw")
         g_fc = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_res = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         call("mvml_gat_unfold_grads", ptr(gW), ptr(attn_lr), H, F, Fin, Fp, mean_res, ptr(g_fc),
