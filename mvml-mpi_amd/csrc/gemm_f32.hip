@@ -439,18 +439,19 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   __shared__ __attribute__((aligned(16))) float lds[2 * 2 * kTileFloats];
 
   // XCD-aware tile order: each XCD walks a contiguous range of tiles, N fastest, so the
-  // workgroups sharing an A row-panel share one L2.  Split-K grids (S % 8 == 0, no batch):
-  // every tile of one K split runs on ONE XCD, back to back (XCD x takes splits x, x + 8, ...),
-  // so the K chunk of the operand all the tiles share (the skinny weight gradients' B, e.g.
-  // the layer-1 atom features under every 128-row tile of the 1544 gradient rows) is read from
-  // HBM once into that XCD's L2 instead of once per XCD.
+  // workgroups sharing an A row-panel share one L2.  Split-K grids (no batch): the (split,
+  // tile) pairs in split-major order, each XCD a contiguous range of them (xcd_block over the
+  // dispatch order, XCD = L % 8), so the tiles of one K split run on one XCD back to back and
+  // the K chunk of the operand they all read (the skinny weight gradients' B, e.g. the layer-1
+  // atom features under every 128-row tile of the 1544 gradient rows) is fetched from HBM once
+  // into that XCD's L2 instead of once per XCD (a split straddling two XCDs: twice).
   const int64_t tiles_n = ceil_div(N, BN);
   int64_t tile, split;
-  if (gridDim.y > 1 && gridDim.y % 8 == 0 && gridDim.z == 1) {
-    const int64_t L = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;  // dispatch order; XCD = L % 8
-    const int64_t j = L / 8;
-    split = L % 8 + 8 * (j / gridDim.x);
-    tile = j % gridDim.x;
+  if (gridDim.y > 1 && gridDim.z == 1) {
+    const unsigned L = blockIdx.x + blockIdx.y * gridDim.x;
+    const int64_t pair = xcd_block(L, gridDim.x * gridDim.y);
+    split = pair / gridDim.x;
+    tile = pair % gridDim.x;
   } else {
     tile = xcd_block(blockIdx.x, gridDim.x);
     split = blockIdx.y;
@@ -1145,11 +1146,29 @@ gemm_x3w_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   const int64_t t_beg = (bx < xr) ? bx * (xq + 1) : xr * (xq + 1) + (bx - xr) * xq;
   const int64_t t_end = t_beg + xq + (bx < xr ? 1 : 0);
   const unsigned bq = gridDim.x / 8, br = gridDim.x % 8;
-  const int64_t t_step = bq + (bx < br ? 1 : 0);  // blocks on this XCD
-  for (int64_t tile = t_beg + blockIdx.x / 8; tile < t_end; tile += t_step) {
-  if (tile != t_beg + blockIdx.x / 8) __syncthreads();  // the previous tile's epilogue LDS reads
+  int64_t t_first = t_beg + blockIdx.x / 8, t_stop = t_end;
+  int64_t t_step = bq + (bx < br ? 1 : 0);  // blocks on this XCD
+  // Split-K grids (one workgroup per (tile, split), never persistent): the pairs in split-major
+  // order, each XCD a contiguous range (xcd_block over the dispatch order), so all tiles of a K
+  // split run on one XCD together and its K chunk of both operands streams from HBM once into
+  // that L2 (tile-major, every XCD re-read all of the operand its tiles do not own: the layer-2
+  // weight gradient's 5.4 GB of X eight times).  The slab pointer is shifted so the epilogue's
+  // blockIdx.y-indexed store lands in this pair's split.
+  int64_t split = blockIdx.y;
+  if (gridDim.y > 1) {
+    const unsigned L = blockIdx.x + blockIdx.y * gridDim.x;
+    const int64_t pair = xcd_block(L, gridDim.x * gridDim.y);
+    split = pair / gridDim.x;
+    t_first = pair % gridDim.x;
+    t_stop = t_first + 1;
+    t_step = 1;
+    if (t_first >= n_tiles) return;
+    if (slab) slab += (split - (int64_t)blockIdx.y) * M * N;
+  }
+  for (int64_t tile = t_first; tile < t_stop; tile += t_step) {
+  if (tile != t_first) __syncthreads();  // the previous tile's epilogue LDS reads
   const int64_t m0 = (tile / tiles_n) * XBM, n0 = (tile % tiles_n) * XBN;
-  const int64_t kbeg = (int64_t)blockIdx.y * k_split;
+  const int64_t kbeg = split * k_split;
   const int64_t kend = min(K, kbeg + k_split);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
