@@ -321,6 +321,209 @@ gemm_planes_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
   }
 }
 
+// Ping-pong form (PP, BK = 16, 4-slot ring): the 8 waves are two groups of four — waves 0-3
+// (rows 0-127 of the tile) and 4-7 (rows 128-255), one wave of each on every SIMD — that run the
+// same stage loop one phase apart, separated by workgroup barriers:
+//   phase 2t:     group 0 reads stage t's fragments (and splits A) | group 1 runs stage t-1's MFMAs
+//   phase 2t + 1: group 0 runs stage t's MFMAs                   | group 1 reads stage t
+// so each SIMD's matrix core is fed by one group while the other group's LDS reads, A split and
+// DMA issue run beside it (the one-group loop above alternates the whole CU between an LDS phase
+// and an MFMA phase: its ablations add the two up).  Stage s is DMA'd at phase 2(s - 3) by every
+// wave (its slot was last read by group 1 in phase 2s - 7), and every wave waits for its own
+// pieces of stage t + 1 at the end of phase 2t + 1, before the barrier that opens group 0's read.
+template <bool APS, bool ROWS, int ABL = 0>
+__global__ void __launch_bounds__(kPThreads, 2)
+gemm_planes_pp_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
+                      const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
+                      float beta, int act, float* __restrict__ C, int64_t ldc, AmaxPtrs amax) {
+  constexpr int BK = 16;
+  using G = PGeo<BK>;
+  static_assert(G::RING == 4 && G::SUB == 1, "ping-pong: four 16-deep slots");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[G::RING_BYTES + kPBM * 4];
+  int* rsh = reinterpret_cast<int*>(lds + G::RING_BYTES);
+  const uint32_t lds_b = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wid >> 2;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int li = lane & 31, lk = lane >> 5;
+  const int kb = amax_shift(*amax.b);
+  const int ka = ROWS ? 0 : amax_shift(*amax.a);
+  const int sw = G::swz(li);
+  const uint32_t o0 = li * G::RB + 16 * ((2 * lk) ^ sw), o1 = li * G::RB + 16 * ((2 * lk + 1) ^ sw);
+  const uint32_t oa = wm * 64 * G::RB, ob = G::OP + wn * 128 * G::RB;
+  const int64_t nst = ceil_div(K, BK);
+  const int64_t kmax_a = APS ? nst * BK - 4 : K - 4, kmax_b = nst * BK - 4;
+  const int64_t tiles_n = ceil_div(N, kPBN);
+  const int64_t n_tiles = ceil_div(M, kPBM) * tiles_n;
+  const unsigned xq = n_tiles / 8, xr = n_tiles % 8, bx = blockIdx.x % 8;
+  const int64_t t_beg = (bx < xr) ? bx * (xq + 1) : xr * (xq + 1) + (bx - xr) * xq;
+  const int64_t t_end = t_beg + xq + (bx < xr ? 1 : 0);
+  const unsigned bq = gridDim.x / 8, br = gridDim.x % 8;
+  const int64_t t_step = bq + (bx < br ? 1 : 0);
+  constexpr int R = 32 * G::RB;  // one 32-row block of a stage image
+  for (int64_t tile = t_beg + blockIdx.x / 8; tile < t_end; tile += t_step) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int64_t m0 = (tile / tiles_n) * kPBM, n0 = (tile % tiles_n) * kPBN;
+    uint32_t rb_t = 0, rb_0 = 0, rb_1 = 0;
+    if constexpr (ROWS) {
+      if (tid < kPBM) rb_t = p_ld_u32(amax.a_rows + min(m0 + tid, M - 1));
+      if constexpr (!APS) {
+        rb_0 = p_ld_u32(amax.a_rows + min(m0 + wm * 64 + li, M - 1));
+        rb_1 = p_ld_u32(amax.a_rows + min(m0 + wm * 64 + 32 + li, M - 1));
+      }
+    }
+    auto issue = [&](int64_t t) {
+      if (t >= nst) return;
+      uint8_t* st = lds + (t % G::RING) * G::STAGE;
+      p_issue<BK>(A, lda, m0, M, t * BK, kmax_a, st, wid, lane);
+      p_issue<BK>(B, ldb, n0, N, t * BK, kmax_b, st + G::OP, wid, lane);
+    };
+    // this wave's pieces of stage t have landed (stages after it, up to two, may still fly)
+    auto wait_own = [&](int64_t t) {
+      const int64_t ahead = min<int64_t>(nst - 1 - t, 2);
+      if (ahead >= 2) p_vmcnt<2 * G::DPS>();
+      else if (ahead == 1) p_vmcnt<G::DPS>();
+      else p_vmcnt<0>();
+    };
+    issue(0);
+    issue(1);
+    issue(2);
+    wait_own(0);  // (and the row maxima, issued before)
+    asm volatile("" : "+v"(rb_t), "+v"(rb_0), "+v"(rb_1));
+    float s_a0 = pow2f(ka), s_a1 = s_a0;
+    if constexpr (ROWS) {
+      if (tid < kPBM) rsh[tid] = amax_shift(rb_t);
+      if constexpr (!APS) {
+        s_a0 = pow2f(amax_shift(rb_0));
+        s_a1 = pow2f(amax_shift(rb_1));
+      }
+    }
+    f32x16 acc[2][2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[h][i][j][r] = 0.f;
+    u32x4 bh[4], bl[4];
+    f16x8 ah[2], al[2];
+    auto a_ops = [&](const u32x4& c0, const u32x4& c1, float s, bool tl, int64_t k0, f16x8& h8, f16x8& l8) {
+      if constexpr (APS) {
+        h8 = __builtin_bit_cast(f16x8, c0);
+        l8 = __builtin_bit_cast(f16x8, c1);
+      } else {
+        float4 lo = __builtin_bit_cast(float4, c0), hi = __builtin_bit_cast(float4, c1);
+        if (tl) {
+          if (k0 + 8 * lk >= K) lo = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (k0 + 8 * lk + 4 >= K) hi = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        bf16x8 h, l;
+        split2h8(lo, hi, s, h, l);
+        h8 = __builtin_bit_cast(f16x8, h);
+        l8 = __builtin_bit_cast(f16x8, l);
+      }
+    };
+    // READ phase: every fragment of stage t into registers, A split
+    auto read = [&](int64_t t) {
+      const uint32_t sb = lds_b + (uint32_t)(t % G::RING) * G::STAGE;
+      const uint32_t vb0 = sb + ob + o0, vb1 = sb + ob + o1, va0 = sb + oa + o0, va1 = sb + oa + o1;
+      u32x4 a[4];
+      p_rd<0>(bh[0], vb0);
+      p_rd<0>(bl[0], vb1);
+      p_rd<R>(bh[1], vb0);
+      p_rd<R>(bl[1], vb1);
+      p_rd<2 * R>(bh[2], vb0);
+      p_rd<2 * R>(bl[2], vb1);
+      p_rd<3 * R>(bh[3], vb0);
+      p_rd<3 * R>(bl[3], vb1);
+      p_rd<0>(a[0], va0);
+      p_rd<0>(a[1], va1);
+      p_rd<R>(a[2], va0);
+      p_rd<R>(a[3], va1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const bool tl = !APS && t == nst - 1 && (K % BK) != 0;
+      a_ops(a[0], a[1], s_a0, tl, t * BK, ah[0], al[0]);
+      a_ops(a[2], a[3], s_a1, tl, t * BK, ah[1], al[1]);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // MFMA phase: the 24 products of the fragments read
+    auto mfma = [&]() {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          f32x16 c = acc[jj >> 1][i][jj & 1];
+          if constexpr (ABL == 2) {
+            asm volatile("" ::"v"(ah[i]), "v"(al[i]), "v"(bh[jj]), "v"(bl[jj]));
+          } else {
+            const f16x8 bhv = __builtin_bit_cast(f16x8, bh[jj]), blv = __builtin_bit_cast(f16x8, bl[jj]);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bhv, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], blv, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bhv, c, 0, 0, 0);
+          }
+          acc[jj >> 1][i][jj & 1] = c;
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = [] { asm volatile("s_barrier" ::: "memory"); };
+    bar();  // every wave's stage 0 has landed
+    if (grp == 0) {
+      for (int64_t t = 0; t < nst; ++t) {
+        issue(t + 3);  // phase 2t: stage t + 3 into the slot group 1 left at the last barrier
+        read(t);
+        bar();
+        mfma();  // phase 2t + 1
+        if (t + 1 < nst) wait_own(t + 1);
+        bar();
+      }
+      bar();  // group 1's last MFMA phase
+    } else {
+      issue(3);  // phase 0
+      bar();
+      for (int64_t t = 0; t < nst; ++t) {
+        read(t);  // phase 2t + 1
+        if (t + 1 < nst) wait_own(t + 1);
+        bar();
+        issue(t + 4);  // phase 2t + 2
+        mfma();
+        bar();
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    {
+      const float u = ROWS ? pow2f(-kb) : pow2f(-kb) * pow2f(-ka);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[h][i][j][r] = acc[h][i][j][r] * u;
+    }
+    if constexpr (ABL == 1) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[h][i][j]));
+      continue;
+    }
+    float* wl = reinterpret_cast<float*>(lds) + wid * 32 * kEpiLd;
+    const int* rs = ROWS ? rsh + wm * 64 : nullptr;
+    epilogue_lds<2, false>(acc[0], wl, M, N, m0 + wm * 64, n0 + wn * 128, lane, bias, beta, act, C, ldc,
+                           nullptr, CellEpi{}, rs);
+    wave_sync_lds();
+    epilogue_lds<2, false>(acc[1], wl, M, N, m0 + wm * 64, n0 + wn * 128 + 64, lane, bias, beta, act, C,
+                           ldc, nullptr, CellEpi{}, rs);
+  }
+}
+
 // il8 image of a K-contiguous ([rows][ld]) or K-major ([K][ld], kmajor) fp32 operand: out[r]
 // holds, per 8-value k group g < ld_out / 8, the 8 scaled high halves of x[r][8g .. 8g+7] then
 // the 8 low halves (split2h8 with the operand's scale, or the row's own with amax_rows); k >= K
@@ -410,14 +613,36 @@ extern "C" int mvml_gemm_f16x2_planes(int64_t M, int64_t N, int64_t K, const flo
   am.b = amax_b;
   am.a_rows = amax_a_rows;
   hipStream_t st = as_stream(stream);
-  static const int abl = [] {  // timing ablations (tools/planes_bench.py)
-    const char* e = getenv("MVML_PLANES_ABL");
-    return e ? atoi(e) : 0;
-  }();
-  static const int bk = [] {  // stage depth 16 / 32 (experiments)
-    const char* e = getenv("MVML_PLANES_BK");
-    return e ? atoi(e) : 32;
-  }();
+  // experiment switches, read per call (tools/planes_bench.py, tests/test_gpu_planes.py):
+  // MVML_PLANES_ABL timing ablations (1 no epilogue, 2 no MFMAs: wrong results),
+  // MVML_PLANES_BK stage depth 16 / 32, MVML_PLANES_PP ping-pong wave groups (BK 16)
+  auto env_int = [](const char* k, int d) {
+    const char* e = getenv(k);
+    return e ? atoi(e) : d;
+  };
+  const int abl = env_int("MVML_PLANES_ABL", 0);
+  const int bk = env_int("MVML_PLANES_BK", 32);
+  const int pp = env_int("MVML_PLANES_PP", 0);
+  if (pp) {
+#define MVML_PP(APSV, ROWSV)                                                                           \
+  do {                                                                                                 \
+    if (abl == 1) gemm_planes_pp_kernel<APSV, ROWSV, 1><<<grid, kPThreads, 0, st>>>(                   \
+        M, N, K, A, lda, b_image, ldb, bias, beta, act, C, ldc, am);                                   \
+    else if (abl == 2) gemm_planes_pp_kernel<APSV, ROWSV, 2><<<grid, kPThreads, 0, st>>>(              \
+        M, N, K, A, lda, b_image, ldb, bias, beta, act, C, ldc, am);                                   \
+    else gemm_planes_pp_kernel<APSV, ROWSV, 0><<<grid, kPThreads, 0, st>>>(                            \
+        M, N, K, A, lda, b_image, ldb, bias, beta, act, C, ldc, am);                                   \
+  } while (0)
+    if (a_image) {
+      if (amax_a_rows) MVML_PP(true, true);
+      else MVML_PP(true, false);
+    } else {
+      if (amax_a_rows) MVML_PP(false, true);
+      else MVML_PP(false, false);
+    }
+#undef MVML_PP
+    return check_launch("gemm_planes_pp_kernel");
+  }
 #define MVML_PL4(APSV, ROWSV, BKV, ABLV)                                                             \
   gemm_planes_kernel<APSV, ROWSV, false, false, BKV, ABLV><<<grid, kPThreads, 0, st>>>(               \
       M, N, K, A, lda, b_image, ldb, bias, beta, act, C, ldc, am, CellEpi{}, EpiX{})
