@@ -524,6 +524,153 @@ gemm_planes_pp_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__
   }
 }
 
+// 16x16x32 form (M16, BK = 32, experiment): the same staging and stage images as BK = 32, the
+// products on v_mfma_f32_16x16x32_f16 (lane l: A row l & 15, k 8 (l >> 4) .. + 7; C rows
+// 4 (l >> 4) + r, column l & 15), 4 x 8 blocks of 16 x 16 per wave.  The point of the shape:
+// under load the chip holds a higher clock on 16x16x32 than on 32x32x16 MFMA streams of equal
+// cycles (MI355X_MICROARCH.md, DVFS (7): 1.12-1.15 x the FLOP/s).  Direct epilogue (per-row and
+// operand scales, bias, beta, ReLU; 64-B row pieces).  The k order inside an MFMA differs from
+// the 32x32x16 tile's, so results agree to rounding, not bitwise.
+template <bool APS, bool ROWS>
+__global__ void __launch_bounds__(kPThreads, 2)
+gemm_planes16_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
+                     const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
+                     float beta, int act, float* __restrict__ C, int64_t ldc, AmaxPtrs amax) {
+  constexpr int BK = 32;
+  using G = PGeo<BK>;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[G::RING_BYTES];
+  const uint32_t lds_b = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int kb = amax_shift(*amax.b);
+  const int ka = ROWS ? 0 : amax_shift(*amax.a);
+  // lane's two 16-B chunks (k group lg: chunks 2 lg, 2 lg + 1) of row lr of a 16-row block; the
+  // stage images are swizzled per row as for BK = 32 (chunk ^ ((row >> 1) & 7)); blocks of 16
+  // rows keep (row >> 1) & 7 of rows 16 b + lr equal to that of lr
+  const int sw = G::swz(lr);
+  const uint32_t o0 = lr * G::RB + 16 * ((2 * lg) ^ sw), o1 = lr * G::RB + 16 * ((2 * lg + 1) ^ sw);
+  const uint32_t oa = wm * 64 * G::RB, ob = G::OP + wn * 128 * G::RB;
+  const int64_t nst = ceil_div(K, BK);
+  const int64_t kmax_a = APS ? nst * BK - 4 : K - 4, kmax_b = nst * BK - 4;
+  const bool tail = !APS && (K % BK) != 0;
+  const int64_t tiles_n = ceil_div(N, kPBN);
+  const int64_t n_tiles = ceil_div(M, kPBM) * tiles_n;
+  const unsigned xq = n_tiles / 8, xr = n_tiles % 8, bx = blockIdx.x % 8;
+  const int64_t t_beg = (bx < xr) ? bx * (xq + 1) : xr * (xq + 1) + (bx - xr) * xq;
+  const int64_t t_end = t_beg + xq + (bx < xr ? 1 : 0);
+  const unsigned bq = gridDim.x / 8, br = gridDim.x % 8;
+  const int64_t t_step = bq + (bx < br ? 1 : 0);
+  constexpr int R16 = 16 * G::RB;  // one 16-row block of a stage image
+  for (int64_t tile = t_beg + blockIdx.x / 8; tile < t_end; tile += t_step) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int64_t m0 = (tile / tiles_n) * kPBM, n0 = (tile % tiles_n) * kPBN;
+    uint32_t rbv[4] = {0u, 0u, 0u, 0u};  // this lane's A rows 16 i + lr (split scales)
+    if constexpr (ROWS) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rbv[i] = p_ld_u32(amax.a_rows + min(m0 + wm * 64 + 16 * i + lr, M - 1));
+    }
+    auto issue = [&](int64_t t) {
+      uint8_t* st = lds + (t % G::RING) * G::STAGE;
+      p_issue<BK>(A, lda, m0, M, t * BK, kmax_a, st, wid, lane);
+      p_issue<BK>(B, ldb, n0, N, t * BK, kmax_b, st + G::OP, wid, lane);
+    };
+    issue(0);
+    p_vmcnt<0>();  // stage 0 and the row maxima
+    asm volatile("" : "+v"(rbv[0]), "+v"(rbv[1]), "+v"(rbv[2]), "+v"(rbv[3]));
+    float sa[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sa[i] = ROWS ? pow2f(amax_shift(rbv[i])) : pow2f(ka);
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto stage = [&](int64_t t, bool tl) {
+      const uint32_t sb = lds_b + (uint32_t)(t % G::RING) * G::STAGE;
+      // A's four 16-row blocks first (split once), then B in two halves of four 16-column
+      // blocks (32 VGPRs of B fragments live instead of 64)
+      f16x8 ah[4], al[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        u32x4 c0, c1;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(c0) : "v"(sb + oa + o0 + i * R16) : "memory");
+        asm volatile("ds_read_b128 %0, %1" : "=v"(c1) : "v"(sb + oa + o1 + i * R16) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (APS) {
+          ah[i] = __builtin_bit_cast(f16x8, c0);
+          al[i] = __builtin_bit_cast(f16x8, c1);
+        } else {
+          float4 lo = __builtin_bit_cast(float4, c0), hi = __builtin_bit_cast(float4, c1);
+          if (tl) {
+            if (t * BK + 8 * lg >= K) lo = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (t * BK + 8 * lg + 4 >= K) hi = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+          bf16x8 h, l;
+          split2h8(lo, hi, sa[i], h, l);
+          ah[i] = __builtin_bit_cast(f16x8, h);
+          al[i] = __builtin_bit_cast(f16x8, l);
+        }
+      }
+#pragma unroll
+      for (int jh = 0; jh < 2; ++jh) {
+        u32x4 bh[4], bl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t vb0 = sb + ob + o0 + (4 * jh + j) * R16, vb1 = sb + ob + o1 + (4 * jh + j) * R16;
+          asm volatile("ds_read_b128 %0, %1" : "=v"(bh[j]) : "v"(vb0) : "memory");
+          asm volatile("ds_read_b128 %0, %1" : "=v"(bl[j]) : "v"(vb1) : "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f16x8 bhv = __builtin_bit_cast(f16x8, bh[j]), blv = __builtin_bit_cast(f16x8, bl[j]);
+            f32x4 c = acc[i][4 * jh + j];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bhv, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], blv, c, 0, 0, 0);
+            acc[i][4 * jh + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bhv, c, 0, 0, 0);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    for (int64_t t = 0; t < nst; ++t) {
+      // stage t landed for this wave; after the barrier, for every wave, and stage t - 1's slot
+      // is free: stage t + 1 goes into it
+      p_vmcnt<0>();
+      asm volatile("s_barrier" ::: "memory");
+      if (t + 1 < nst) issue(t + 1);
+      stage(t, tail && t == nst - 1);
+    }
+    // direct epilogue: lane's rows 16 i + 4 lg + r, column 16 j + lr of the wave's 64 x 128
+    const float ub = pow2f(-kb) * (ROWS ? 1.f : pow2f(-ka));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 64 + 16 * i + 4 * lg + r;
+        if (row >= M) continue;
+        float us = ub;
+        if constexpr (ROWS) us *= pow2f(-amax_shift(amax.a_rows[row]));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int64_t col = n0 + wn * 128 + 16 * j + lr;
+          if (col >= N) continue;
+          float v = acc[i][j][r] * us;
+          if (bias) v += bias[col];
+          float* cp = C + row * ldc + col;
+          if (beta != 0.f) v += beta * (*cp);
+          if (act == 1) v = fmaxf(v, 0.f);
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
 // il8 image of a K-contiguous ([rows][ld]) or K-major ([K][ld], kmajor) fp32 operand: out[r]
 // holds, per 8-value k group g < ld_out / 8, the 8 scaled high halves of x[r][8g .. 8g+7] then
 // the 8 low halves (split2h8 with the operand's scale, or the row's own with amax_rows); k >= K
@@ -623,6 +770,16 @@ extern "C" int mvml_gemm_f16x2_planes(int64_t M, int64_t N, int64_t K, const flo
   const int abl = env_int("MVML_PLANES_ABL", 0);
   const int bk = env_int("MVML_PLANES_BK", 32);
   const int pp = env_int("MVML_PLANES_PP", 0);
+  if (env_int("MVML_PLANES_M16", 0)) {
+    if (a_image) {
+      if (amax_a_rows) gemm_planes16_kernel<true, true><<<grid, kPThreads, 0, st>>>(M, N, K, A, lda, b_image, ldb, bias, beta, act, C, ldc, am);
+      else gemm_planes16_kernel<true, false><<<grid, kPThreads, 0, st>>>(M, N, K, A, lda, b_image, ldb, bias, beta, act, C, ldc, am);
+    } else {
+      if (amax_a_rows) gemm_planes16_kernel<false, true><<<grid, kPThreads, 0, st>>>(M, N, K, A, lda, b_image, ldb, bias, beta, act, C, ldc, am);
+      else gemm_planes16_kernel<false, false><<<grid, kPThreads, 0, st>>>(M, N, K, A, lda, b_image, ldb, bias, beta, act, C, ldc, am);
+    }
+    return check_launch("gemm_planes16_kernel");
+  }
   if (pp) {
 #define MVML_PP(APSV, ROWSV)                                                                           \
   do {                                                                                                 \
