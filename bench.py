@@ -295,9 +295,6 @@ class Batch:
     def __init__(self, sb, first_mol, group_size, dev, with_fusion, mvp=False):
         self.g = sb.to_graph(group_size=group_size).to(dev)
         self.feats = self.g.ndata["h"]
-        if os.environ.get("MVML_DST_ORDER") == "1":  # experiment: each molecule's hubs first
-            from mvml_gat.batching import hub_first_order
-            self.g.dst_order = hub_first_order(self.g)
         self.B, self.N, self.E = self.g.batch_size, self.g.num_nodes(), self.g.num_edges()
         if with_fusion:
             gen = torch.Generator(device=dev).manual_seed(1234 + first_mol)

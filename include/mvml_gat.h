@@ -380,11 +380,6 @@ int mvml_gat_agg_fwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_
  * operand max of the two GEMMs that read gY; the caller zeroes it).  gy_row_amax (may be NULL):
  * gy_row_amax[n] = bits of max_c |gY[n, c]|, c < C + 2H, for every atom (the per-row scales of the
  * data-gradient product, mvml_gemm_f16x2_rows; no float atomics).  workspace: [E, H]. */
-/* The order in which the destination-wave forward (MVML_OPT_DST_FWD) takes the atoms: order[i]
- * is the atom of wave i (a permutation of [0, N) of the next mvml_gat_agg_fwd calls' batch, on
- * the device), NULL = atom order (the default).  Process-global like the options; results do
- * not depend on it (each atom's output is computed the same way). */
-int mvml_set_dst_order(const int32_t* order);
 size_t mvml_gat_agg_bwd_workspace_size(int64_t num_edges, int H);
 int mvml_gat_agg_bwd(int64_t num_nodes, const int32_t* node_groups, int64_t num_groups,
                      const int32_t* in_rowptr, const int32_t* in_src, const int32_t* out_rowptr,

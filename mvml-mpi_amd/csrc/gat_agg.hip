@@ -869,9 +869,6 @@ gat_agg_fwd_gather_kernel(const int32_t* __restrict__ plan, int64_t G, const int
   if (out_amax) block_amax_commit<kAggThreads>(omx, out_amax);
 }
 
-// mvml_set_dst_order's wave-to-atom map for the destination-wave forward (NULL: atom order)
-const int32_t* g_dst_order = nullptr;
-
 // ---- Forward by destination wave (MVML_OPT_DST_FWD) -------------------------------------------
 // One wave per destination atom v.  xcd_block hands each XCD one contiguous atom range, so the
 // projection rows a destination gathers were just read by its neighbours' waves and come from
@@ -898,13 +895,11 @@ gat_agg_fwd_dst_kernel(int64_t N, const int32_t* __restrict__ rowptr, const int3
                        const float* __restrict__ Y, int64_t ldy, int F, const float* __restrict__ bias,
                        const float* __restrict__ elr, float slope, float* __restrict__ attn,
                        float* __restrict__ out, uint32_t* __restrict__ out_amax,
-                       uint32_t* __restrict__ out_rows, const int32_t* __restrict__ order) {
+                       uint32_t* __restrict__ out_rows) {
   constexpr bool PAIR = MODE == 1 && H >= 2;
   constexpr int NH = PAIR ? H / 2 : 1;  // heads per lane (mean mode); 1 register set (flatten)
   const int lane = threadIdx.x & 63;
-  const int64_t vi = xcd_block(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // (mvml_set_dst_order: the waves take the atoms in that order; the default is atom order)
-  const int64_t v = (order && vi < N) ? (int64_t)__builtin_amdgcn_readfirstlane(order[vi]) : vi;
+  const int64_t v = xcd_block(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float omx = 0.f;
   // (a non-persistent grid: the dispatcher hands out blocks in atom order, which keeps an XCD's
   // waves on one compact window of neighbouring atoms; a persistent walk let them drift apart
@@ -2285,11 +2280,11 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
     if (sm)                                                                                       \
       gat_agg_fwd_dst_kernel<H, M, NJ, U, true>                                                   \
           <<<b4, 256, 0, st>>>(   \
-              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows, g_dst_order);             \
+              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);             \
     else                                                                                          \
       gat_agg_fwd_dst_kernel<H, M, NJ, U, false>                                                  \
           <<<b4, 256, 0, st>>>(  \
-              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows, g_dst_order);             \
+              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);             \
   } while (0)
     // rows in flight per wave (MVML_OPT_DST_UNR, H = 4 at the GAT widths: tuning A/B)
     const int unr = option(MVML_OPT_DST_UNR);
@@ -2306,10 +2301,10 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
         // (profiles/r05_agg_late_residual_config*.txt)
         if (sm)
           gat_agg_fwd_dst_kernel<H, 1, 3, 1, true, true><<<b4, 256, 0, st>>>(
-              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows, g_dst_order);
+              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);
         else
           gat_agg_fwd_dst_kernel<H, 1, 3, 1, false, true><<<b4, 256, 0, st>>>(
-              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows, g_dst_order);
+              N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);
       }
       else if (nj == 3) MVML_DST_FWD(1, 3, 1);  // one row in flight: fewest registers, most waves
       else if (nj <= 4) MVML_DST_FWD(1, 4, 2);
@@ -2329,10 +2324,10 @@ int launch_fwd(int64_t N, const int32_t* groups, int64_t G, const int32_t* rp, c
   do {                                                                                            \
     if (sm)                                                                                       \
       gat_agg_fwd_dst_kernel<H, M, 3, 1, true, true><<<b4, 256, 0, st>>>(                         \
-          N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows, g_dst_order);                 \
+          N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);                 \
     else                                                                                          \
       gat_agg_fwd_dst_kernel<H, M, 3, 1, false, true><<<b4, 256, 0, st>>>(                        \
-          N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows, g_dst_order);                 \
+          N, rp, src, Y, ldy, F, bias, elr, slope, attn, out, blk_amax, out_rows);                 \
   } while (0)
         if (mode == 0) MVML_DST_FWD_LR(0); else MVML_DST_FWD_LR(2);
 #undef MVML_DST_FWD_LR
@@ -2755,9 +2750,4 @@ extern "C" int mvml_gat_unfold_grads(const float* gWcat, const float* attn_lr, i
   const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
   unfold_w_kernel<<<blocks, 256, 0, st>>>(gWcat, attn_lr, H, F, Fin, ldg, mean_residual, g_fc_w, g_res_fc_w);
   return check_launch("unfold_w_kernel");
-}
-
-extern "C" int mvml_set_dst_order(const int32_t* order) {
-  g_dst_order = order;
-  return MVML_OK;
 }

@@ -271,15 +271,3 @@ def from_arrays(batch_num_nodes, batch_num_edges, src_local, dst_local, node_fea
     ndata = {} if node_feats is None else {"h": torch.as_tensor(node_feats)}
     return BatchedMolGraph(batch_num_nodes, batch_num_edges, src_local, dst_local, ndata,
                            group_size=group_size)
-
-
-def hub_first_order(g, min_degree=16):
-    """A wave-to-atom order for the destination-wave forward (mvml_set_dst_order): each
-    molecule's atoms of in-degree >= min_degree (the hubs) first, then the rest, both in atom
-    order — the hub's wave then loads its partners' projection rows just before their own waves
-    read them.  torch ops on the device (made once per batch, not per step)."""
-    rp = g.in_rowptr.long()
-    deg = rp[1:] - rp[:-1]
-    mol = g.node_graph.long()
-    key = mol * 2 + (deg < min_degree).long()
-    return torch.sort(key, stable=True).indices.to(torch.int32)

@@ -333,25 +333,7 @@ def _fwd_path(g, mode):
     dst = DST_FWD_POLICY == "all" or (DST_FWD_POLICY == "auto" and (mode != MODE_MEAN or _large_batch(g)))
     if not dst:
         return contextlib.nullcontext()
-    order = getattr(g, "dst_order", None) if DST_ORDER else None
-    if order is None:
-        return _lib.option("dst_fwd", DST_FWD_KIND or (1 if _large_batch(g) else 2))
-    return _dst_order_ctx(g, order)
-
-
-@contextlib.contextmanager
-def _dst_order_ctx(g, order):
-    with _lib.option("dst_fwd", DST_FWD_KIND or (1 if _large_batch(g) else 2)):
-        _lib.lib().mvml_set_dst_order(ptr(order))
-        try:
-            yield
-        finally:
-            _lib.lib().mvml_set_dst_order(None)
-
-
-# Destination-wave forward in a wave-to-atom order the graph carries (g.dst_order, e.g.
-# batching.hub_first_order: each molecule's hubs first) — experiment (MVML_DST_ORDER=1)
-DST_ORDER = os.environ.get("MVML_DST_ORDER", "0") == "1"
+    return _lib.option("dst_fwd", DST_FWD_KIND or (1 if _large_batch(g) else 2))
 
 
 
