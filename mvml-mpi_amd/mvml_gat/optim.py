@@ -32,20 +32,28 @@ def _stream(dev):
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
-class FlatAdam:
+class FlatAdam(torch.optim.Optimizer):
     """torch.optim.Adam(params, lr, betas, eps, weight_decay) (amsgrad off, L2 decay) on flat
     buffers; ``group``: the process group whose ranks' gradients are averaged (None: the default
-    group when torch.distributed is initialised with more than one rank)."""
+    group when torch.distributed is initialised with more than one rank).  A torch Optimizer with
+    one parameter group, so main.py's uses work unchanged: ``optimizer.param_groups[0]["lr"]``
+    (main.py:23) and ``torch.optim.lr_scheduler.ExponentialLR(optimizer, gamma)`` (main.py:89)
+    — every step reads the group's current lr, betas, eps and weight_decay; ``state_dict()`` is
+    torch Adam's layout (per-parameter step / exp_avg / exp_avg_sq)."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, group=None,
                  average=True):
-        self.params = [p for p in params if p.requires_grad]
+        params = list(params)
+        if params and isinstance(params[0], dict):
+            raise ValueError("FlatAdam: one parameter group (main.py:88 passes model.parameters())")
+        super().__init__([p for p in params if p.requires_grad],
+                         dict(lr=float(lr), betas=tuple(betas), eps=float(eps), weight_decay=float(weight_decay)))
+        self.params = list(self.param_groups[0]["params"])
         if not self.params:
             raise ValueError("FlatAdam: no parameters")
         dev = self.params[0].device
         if dev.type != "cuda" or any(p.device != dev or p.dtype != torch.float32 for p in self.params):
             raise ValueError("FlatAdam: fp32 parameters on one GPU")
-        self.lr, self.betas, self.eps, self.weight_decay = float(lr), betas, float(eps), float(weight_decay)
         self.group, self.average = group, average
         P = len(self.params)
         sizes = [p.numel() for p in self.params]
@@ -126,11 +134,12 @@ class FlatAdam:
             e2.record()
             self.allreduce_events.append((s, e2))
         scale = 1.0 / world if (self.average and world > 1) else 1.0
-        b1, b2 = self.betas
+        hp = self.param_groups[0]  # (an lr scheduler may have changed it since the last step)
+        b1, b2 = hp["betas"]
         call("mvml_adam_flat", self.nchunks, ptr(self.chunk_param), ptr(self.chunk_beg), ptr(self.chunk_end),
              ptr(self.gbuf[self.numel:]), ptr(self.steps), P, ptr(self.pbuf), ptr(self.gbuf),
-             ptr(self.exp_avg), ptr(self.exp_avg_sq), self.lr, float(b1), float(b2), self.eps,
-             self.weight_decay, float(scale), st)
+             ptr(self.exp_avg), ptr(self.exp_avg_sq), float(hp["lr"]), float(b1), float(b2), float(hp["eps"]),
+             float(hp["weight_decay"]), float(scale), st)
 
     def allreduce_ms(self, reset=True):
         """Mean duration of the recorded all-reduces (HIP events; synchronises), or None."""
@@ -141,6 +150,40 @@ class FlatAdam:
         if reset:
             self.allreduce_events = []
         return float(np.mean(ms))
+
+    def state_dict(self):
+        """torch.optim.Adam's layout: {"state": {index: {"step", "exp_avg", "exp_avg_sq"}},
+        "param_groups": [...]} (parameters never stepped have no entry, as in torch)."""
+        steps = self.steps.cpu().tolist()
+        state = {}
+        for i, p in enumerate(self.params):
+            if steps[i] > 0:
+                _, m, v = self.state_of(p)
+                state[i] = {"step": torch.tensor(float(steps[i])), "exp_avg": m.clone(),
+                            "exp_avg_sq": v.clone()}
+        groups = [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]
+        groups[0]["params"] = list(range(len(self.params)))
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, sd):
+        g = sd["param_groups"][0]
+        if len(sd["param_groups"]) != 1 or len(g["params"]) != len(self.params):
+            raise ValueError("FlatAdam.load_state_dict: one group with this optimizer's parameters")
+        for k, v in g.items():
+            if k != "params":
+                self.param_groups[0][k] = v
+        steps = [0] * len(self.params)
+        with torch.no_grad():
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            for i, p in enumerate(self.params):
+                st = sd["state"].get(i, sd["state"].get(str(i)))
+                if st:
+                    steps[i] = int(float(st["step"]))
+                    _, m, v = self.state_of(p)
+                    m.copy_(st["exp_avg"].reshape(m.shape))
+                    v.copy_(st["exp_avg_sq"].reshape(v.shape))
+        self.steps.copy_(torch.tensor(steps, dtype=torch.int32))
 
     def state_of(self, p):
         """(step, exp_avg, exp_avg_sq) of parameter p, shaped like it (tests)."""

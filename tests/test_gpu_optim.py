@@ -156,3 +156,57 @@ def test_flat_adam_two_ranks_device_presence(tmp_path):
         assert torch.allclose(torch.tensor(r["b"]), b.detach(), rtol=1e-6), r
         assert r["c"] == [1.0, 1.0], r
     assert res[0]["a"] == res[1]["a"] and res[0]["b"] == res[1]["b"]
+
+
+def test_flat_adam_with_exponential_lr_and_state_dict():
+    """main.py:88-89 unchanged: ExponentialLR(FlatAdam, 0.95) moves the lr each epoch exactly as
+    it moves torch Adam's (param_groups[0]["lr"], main.py:23), and state_dict() is torch Adam's
+    layout: loading torch's state into a fresh FlatAdam continues identically."""
+    ref = _params(5)
+    mine = [torch.nn.Parameter(p.detach().clone().to(DEV)) for p in ref]
+    ref = [torch.nn.Parameter(p.detach().clone().to(DEV)) for p in ref]
+    topt = torch.optim.Adam(ref, lr=1e-2, weight_decay=1e-4, foreach=False)
+    fopt = FlatAdam(mine, lr=1e-2, weight_decay=1e-4)
+    tsch = torch.optim.lr_scheduler.ExponentialLR(topt, gamma=0.95)
+    fsch = torch.optim.lr_scheduler.ExponentialLR(fopt, gamma=0.95)
+    g = torch.Generator().manual_seed(7)
+    for epoch in range(3):
+        for step in range(2):
+            topt.zero_grad()
+            fopt.zero_grad()
+            for i, (a, b) in enumerate(zip(ref, mine)):
+                if i == 3:
+                    continue
+                gr = torch.randn(a.shape, generator=g).to(DEV)
+                a.grad, b.grad = gr.clone(), gr.clone()
+            topt.step()
+            fopt.step()
+        tsch.step()
+        fsch.step()
+        assert fopt.param_groups[0]["lr"] == topt.param_groups[0]["lr"]
+    torch.cuda.synchronize()
+    for a, b in zip(ref, mine):
+        d = (a.detach() - b.detach()).abs().max().item()
+        assert d <= 2e-6 * max(a.detach().abs().max().item(), 1e-3), d
+    # torch's state into a fresh FlatAdam over copies of torch's parameters: one more step each
+    sd = topt.state_dict()
+    steps0 = {i: float(st["step"]) for i, st in sd["state"].items()}  # (sd holds torch's live tensors)
+    mine2 = [torch.nn.Parameter(a.detach().clone()) for a in ref]
+    f2 = FlatAdam(mine2, lr=1.0)
+    f2.load_state_dict(sd)
+    assert f2.param_groups[0]["lr"] == topt.param_groups[0]["lr"]
+    for a, b in zip(ref, mine2):
+        a.grad = torch.ones_like(a)
+        b.grad = torch.ones_like(b)
+    ref[3].grad = None
+    mine2[3].grad = None
+    topt.step()
+    f2.step()
+    torch.cuda.synchronize()
+    for a, b in zip(ref, mine2):
+        d = (a.detach() - b.detach()).abs().max().item()
+        assert d <= 2e-6 * max(a.detach().abs().max().item(), 1e-3), d
+    out = f2.state_dict()
+    assert sorted(out["state"]) == sorted(sd["state"])
+    for i, n in steps0.items():
+        assert float(out["state"][i]["step"]) == n + 1
