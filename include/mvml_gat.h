@@ -57,8 +57,8 @@ const char* mvml_version(void);
                                    0: one workgroup per tile) */
 #define MVML_OPT_GEMM_NSPLIT 4  /* MVML_GEMM_NSPLIT: 1 (default) N = 256 q + r products as two
                                    launches, 0 = one */
-#define MVML_OPT_GEMM_RING 5    /* MVML_GEMM_RING: 1 = split-fp16 256x256 products on the
-                                   LDS-DMA ring kernel, 0 (default) = the register-staged one */
+#define MVML_OPT_GEMM_RING 5    /* (rounds 3-5: the LDS-DMA ring kernel; removed in round 6 —
+                                   the option is accepted and ignored) */
 #define MVML_OPT_LSTM_TILE 6    /* MVML_LSTM_TILE: tile of the wide BiLSTM step products
                                    (mvml_bilstm_wide_step_*): 0 (default) planned from the live
                                    row count, 128 / 256 = forced; 128 also moves

@@ -213,12 +213,11 @@ def test_gemm_f16x2_scales(sa, sb):
 @pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(1000, 1928, 768), (257, 300, 74), (4100, 768, 1928),
                                    (512, 384, 65536 + 17), (6144, 520, 40), (300, 260, 16)])
-def test_gemm_f16x2_ring_bitwise(ak, bk, M, N, K):
-    """The LDS-DMA ring kernel (gemm_h2g_kernel, option gemm_ring = 1, the default) against the
-    register-staged split-fp16 kernel (gemm_ring = 0): same split, same MFMA order, same k order,
-    so C is bit-identical — K tails (K % 16 != 0), ragged M / N edges, split-K, the N = 256 q + r
-    split, bias / beta / ReLU epilogue — and within the fp32 bar of float64."""
-    from mvml_gat._lib import option
+def test_gemm_f16x2_256_layouts(ak, bk, M, N, K):
+    """The split-fp16 256x256 tile on every operand layout — K tails (K % 16 != 0), ragged M / N
+    edges, split-K, the N = 256 q + r split, bias / beta / ReLU epilogue — within the fp32 bar
+    of float64.  (Rounds 3-5 ran it against the LDS-DMA ring kernel too; the ring was removed in
+    round 6.)"""
     from mvml_gat.functional import gemm
     g = torch.Generator().manual_seed(M + 3 * N + 7 * K + ak + 2 * bk)
     A = torch.randn(M, K, generator=g, dtype=torch.float64)
@@ -227,15 +226,11 @@ def test_gemm_f16x2_ring_bitwise(ak, bk, M, N, K):
     C0 = torch.randn(M, N, generator=g, dtype=torch.float64)
     Ad = (A.t() if ak else A).contiguous().float().to(DEV)
     Bd = (B if bk else B.t()).contiguous().float().to(DEV)
-    out = {}
-    for ring in (1, 0):
-        C = C0.float().to(DEV)
-        with option("gemm_ring", ring), _x3_tile("f16x2-256") as a:
-            gemm(Ad, Bd, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N,
-                 bias=bias.float().to(DEV), beta=0.5, act=1, algo=a)
-        out[ring] = C
-    assert torch.equal(out[1], out[0])
-    assert rel_err(out[1], torch.relu(A @ B + bias + 0.5 * C0)) < TOL
+    C = C0.float().to(DEV)
+    with _x3_tile("f16x2-256") as a:
+        gemm(Ad, Bd, M, N, K, ak, bk, M if ak else K, N if bk else K, C, N,
+             bias=bias.float().to(DEV), beta=0.5, act=1, algo=a)
+    assert rel_err(C, torch.relu(A @ B + bias + 0.5 * C0)) < TOL
 
 
 @pytest.mark.parametrize("ak,bk", [(1, 1), (0, 1), (0, 0), (1, 0)])
@@ -363,19 +358,16 @@ def test_set2set_parity():
         assert rel_err(p.grad, p2.grad) < TOL, n
 
 
-@pytest.mark.parametrize("ring,tile", [(1, 0), (0, 0), (0, 128)])
-def test_set2set_cell_epilogue_bitwise(ring, tile):
+@pytest.mark.parametrize("tile", [0, 128])
+def test_set2set_cell_epilogue_bitwise(tile):
     """Set2Set at a width where the gates GEMM takes the 256x256 plan (16,384 molecules): the
     fused gates + LSTM-cell epilogue (mvml_lstm_gates_cell_fwd) equals the GEMM + cell kernel
     path bit for bit (same MFMA accumulation per element, same cell arithmetic), forward and
-    backward, on either split-fp16 kernel (ring: the LDS-DMA ring one, the default) and on the
-    128x128 one (tile = 128: option lstm_tile); the unfused path is the one pinned to the
-    float64 oracle above."""
+    backward, on the 256x256 split-fp16 kernel and on the 128x128 one (tile = 128: option
+    lstm_tile); the unfused path is the one pinned to the float64 oracle above."""
     import mvml_gat.functional as fn
     from mvml_gat import _lib
     from mvml_gat._lib import option
-    opt = option("gemm_ring", ring)
-    opt.__enter__()
     opt_t = option("lstm_tile", tile)
     opt_t.__enter__()
     from mvml_gat.nn import Set2Set
@@ -399,7 +391,6 @@ def test_set2set_cell_epilogue_bitwise(ring, tile):
         finally:
             fn.CELL_EPI = old
     opt_t.__exit__(None, None, None)
-    opt.__exit__(None, None, None)
     for a, b in zip(*res):
         assert torch.equal(a, b)
 
