@@ -46,6 +46,7 @@ class FlatAdam(torch.optim.Optimizer):
         params = list(params)
         if params and isinstance(params[0], dict):
             raise ValueError("FlatAdam: one parameter group (main.py:88 passes model.parameters())")
+        self._flat_ready = False
         super().__init__([p for p in params if p.requires_grad],
                          dict(lr=float(lr), betas=tuple(betas), eps=float(eps), weight_decay=float(weight_decay)))
         self.params = list(self.param_groups[0]["params"])
@@ -89,6 +90,12 @@ class FlatAdam(torch.optim.Optimizer):
         self._turn = 0
         self._dev_tab = torch.zeros(P, dtype=torch.int64, device=dev)
         self.allreduce_events = []  # (start, end) HIP events around each step's all-reduce
+        self._flat_ready = True
+
+    def add_param_group(self, param_group):
+        if self._flat_ready:  # (the flat buffers are laid out once, at construction)
+            raise NotImplementedError("FlatAdam: one parameter group, fixed at construction")
+        super().add_param_group(param_group)
 
     def zero_grad(self, set_to_none=True):
         """Gradients back to None (the reference's optimizer.zero_grad()); set_to_none=False is
@@ -101,8 +108,18 @@ class FlatAdam(torch.optim.Optimizer):
             return dist.get_world_size(self.group)
         return 1
 
+    def step(self, closure=None):
+        """One Adam step over every parameter (torch's Optimizer.step contract: an optional
+        closure re-evaluates the loss, which is returned)."""
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self._step()
+        return loss
+
     @torch.no_grad()
-    def step(self):
+    def _step(self):
         dev = self.pbuf.device
         st = _stream(dev)
         P = len(self.params)
