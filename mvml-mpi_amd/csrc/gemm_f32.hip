@@ -1722,6 +1722,43 @@ __global__ void __launch_bounds__(256) absmax_kernel(int64_t rows, int64_t cols,
   }
 }
 
+// |max| of a contiguous run of n floats (a matrix with ld == cols, or one row): grid-stride over
+// float4s (vec) or floats, 4 loads in flight per thread, one atomicMax per workgroup.  The
+// column-parallel absmax_kernel leaves all but `cols` lanes of a workgroup idle, which for the
+// GAT layers' max-of-row-maxima (N x 1) was 1 live lane in 256: ~0.4 ms per 1.75 M atoms.
+__global__ void __launch_bounds__(256) absmax_flat_kernel(int64_t n, const float* __restrict__ P,
+                                                          int vec, uint32_t* __restrict__ out) {
+  float m[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (vec) {
+    const int64_t n4 = n / 4;
+    const float4* P4 = reinterpret_cast<const float4*>(P);
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = P4[i + u * stride];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        m[u] = fmaxf(m[u], fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+    }
+    for (; i < n4; i += stride) {
+      const float4 v = P4[i];
+      m[0] = fmaxf(m[0], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+  } else {
+    for (; i < n; i += stride) m[0] = fmaxf(m[0], fabsf(P[i]));
+  }
+  float v = wave_max(fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3])));
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    v = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(out, __float_as_uint(v));
+  }
+}
+
 // Per-row |max| bits: a group of 2^lg lanes per row (float4 columns when vec), butterfly max;
 // one writer per row (accumulate: max with the stored bits), so no atomics.
 __global__ void __launch_bounds__(256) absmax_rows_kernel(int64_t rows, int64_t cols,
@@ -1806,6 +1843,14 @@ int absmax_launch(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32
     return MVML_ERR_LAUNCH;
   }
   if (rows <= 0 || cols <= 0) return MVML_OK;
+  if ((ld == cols || rows == 1) && cols < 1024) {  // contiguous and narrow: flat pass
+    const int64_t n = rows * cols;
+    const int fvec = (n % 4 == 0) && ((uintptr_t)P % 16 == 0);
+    const unsigned blocks =
+        (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(fvec ? n / 4 : n, 256 * 4), 1024));
+    absmax_flat_kernel<<<blocks, 256, 0, st>>>(n, P, fvec, out);
+    return check_launch("absmax_flat_kernel");
+  }
   const int vec = (cols % 4 == 0) && (ld % 4 == 0) && ((uintptr_t)P % 16 == 0);
   const int64_t cx = ceil_div(vec ? cols / 4 : cols, 256);
   // ~1 K workgroups (each ends with ONE atomicMax on the single output word: a word takes ~90

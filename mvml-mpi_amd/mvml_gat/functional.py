@@ -423,7 +423,9 @@ class GATLayerFunction(torch.autograd.Function):
                 # zeros): computed once and recorded on the feature tensor itself
                 xr = known_rows(X)
                 if xr is None:
-                    xr = absmax_rows(Xp, N, Fin, Fp)
+                    # Xp's pad columns are zeros: the whole padded row (float4 loads) has the
+                    # same |max| as its Fin features
+                    xr = absmax_rows(Xp, N, Fp, Fp)
                     if not X.requires_grad:
                         fold_rows(X, xr)
                 absmax(xr, N, 1, 1, amx, 0)

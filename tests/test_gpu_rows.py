@@ -352,8 +352,10 @@ def test_absmax_matches_torch():
     for bit on tall, wide, unaligned and tiny operands, and accumulates into a prior value."""
     from mvml_gat.functional import absmax
     g = torch.Generator().manual_seed(3)
+    # (N, 1, 1) etc.: contiguous narrow operands take the flat pass (the GAT layers' max of
+    # per-row maxima), float4 when the count is a multiple of 4, scalar otherwise
     for rows, cols, ld in ((1, 1, 1), (65536, 768, 768), (1753, 76, 76), (300000, 5, 7), (17, 9000, 9001),
-                           (4096, 1928, 1984)):
+                           (4096, 1928, 1984), (1750000, 1, 1), (1750001, 1, 1), (1, 333, 333), (10, 7, 7)):
         X = torch.randn(rows, ld, generator=g).to(DEV)
         X[rows // 2, cols - 1] = -7.5e3  # the max sits in one place, negative
         out = torch.zeros(2, dtype=torch.int32, device=DEV)
@@ -363,3 +365,9 @@ def test_absmax_matches_torch():
         out[0] = torch.tensor(1e5, dtype=torch.float32).view(torch.int32)
         absmax(X, rows, cols, ld, out, 0, accumulate=True)
         assert out[0].view(torch.float32).item() == 1e5
+    # flat pass from a non-16-B-aligned start (offset 1): scalar loads, same bits
+    X = torch.randn(4001, generator=g).to(DEV)
+    X[2000] = 9.25e2
+    out = torch.zeros(1, dtype=torch.int32, device=DEV)
+    absmax(X, 4000, 1, 1, out, 0, offset=1)
+    assert out[0].view(torch.float32) == X[1:].abs().max()
