@@ -1669,19 +1669,30 @@ __global__ void colsum_partial_kernel(int64_t M, int64_t N, const float* __restr
   part[(int64_t)blockIdx.y * N + col] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
-__global__ void colsum_final_kernel(int64_t N, int S, const float* __restrict__ part, float alpha,
-                                    float beta, float* __restrict__ out) {
-  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= N) return;
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 loads in flight, fixed order
-  int z = 0;
-  for (; z + 8 <= S; z += 8) {
+// out[col] = beta out[col] + alpha sum_z part[z][col]: a workgroup per 16 columns, 16 stripes of
+// the S partials per column (four accumulators each, loads in flight), a fixed-order LDS tree —
+// deterministic.  (A thread per column walking all S ~ 1024 partials took 20-70 us.)
+__global__ void __launch_bounds__(256) colsum_final_kernel(int64_t N, int S, const float* __restrict__ part,
+                                                           float alpha, float beta, float* __restrict__ out) {
+  const int c = threadIdx.x & 15, stripe = threadIdx.x >> 4;
+  const int64_t col = (int64_t)blockIdx.x * 16 + c;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (col < N) {
+    int z = stripe;
+    for (; z + 48 < S; z += 64) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] += part[(int64_t)(z + j) * N + col];
+      for (int u = 0; u < 4; ++u) a[u] += part[(int64_t)(z + 16 * u) * N + col];
+    }
+    for (; z < S; z += 16) a[0] += part[(int64_t)z * N + col];
   }
-  for (; z < S; ++z) s[0] += part[(int64_t)z * N + col];
-  const float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-  out[col] = (beta != 0.f ? beta * out[col] : 0.f) + alpha * t;
+  __shared__ float red[16][17];
+  red[stripe][c] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  for (int h = 8; h > 0; h >>= 1) {
+    if (stripe < h) red[stripe][c] += red[stripe + h][c];
+    __syncthreads();
+  }
+  if (stripe == 0 && col < N) out[col] = (beta != 0.f ? beta * out[col] : 0.f) + alpha * red[0][c];
 }
 
 // |max| of a stored rows x cols fp32 matrix (row pitch ld) folded into *out as float bits:
@@ -2769,7 +2780,7 @@ extern "C" int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx
   float* part = static_cast<float*>(workspace);
   dim3 g1((unsigned)ceil_div(N, 256), (unsigned)S);
   colsum_partial_kernel<<<g1, 256, 0, st>>>(M, N, X, ldx, rows_per, part);
-  colsum_final_kernel<<<(unsigned)ceil_div(N, 256), 256, 0, st>>>(N, S, part, alpha, beta, out);
+  colsum_final_kernel<<<(unsigned)ceil_div(N, 16), 256, 0, st>>>(N, S, part, alpha, beta, out);
   return check_launch("colsum");
 }
 

@@ -90,16 +90,37 @@ __global__ void graphnorm_bwd_kernel(int D, const int64_t* __restrict__ off, con
   part[(2 * G + g) * D + col] = pms;
 }
 
-__global__ void graphnorm_param_reduce(int D, int64_t G, const double* __restrict__ part,
-                                       float* __restrict__ gw, float* __restrict__ gb,
-                                       float* __restrict__ gms) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+// Sum of the G group partials of one parameter gradient: a workgroup per 16 columns, 16 group
+// stripes per column (g = stripe, stripe + 16, ...; four independent accumulators so the loads
+// stay in flight), then a fixed-order tree over the stripes in LDS — deterministic.  (One thread
+// per column walking all G groups took 0.36 ms for G = 1024, D = 768: latency, not bytes.)
+__global__ void __launch_bounds__(256) graphnorm_param_reduce(int D, int64_t G, const double* __restrict__ part,
+                                                              float* __restrict__ gw, float* __restrict__ gb,
+                                                              float* __restrict__ gms) {
+  const int c = threadIdx.x & 15, stripe = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + c;
   const int which = blockIdx.y;
-  if (col >= D) return;
-  double s = 0.0;
-  for (int64_t g = 0; g < G; ++g) s += part[((int64_t)which * G + g) * D + col];
-  float* dst = which == 0 ? gw : (which == 1 ? gb : gms);
-  if (dst) dst[col] = (float)s;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  if (col < D) {
+    const double* p = part + (int64_t)which * G * D + col;
+    int64_t g = stripe;
+    for (; g + 48 < G; g += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += p[(g + 16 * u) * D];
+    }
+    for (; g < G; g += 16) a[0] += p[g * D];
+  }
+  __shared__ double red[16][17];
+  red[stripe][c] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  for (int h = 8; h > 0; h >>= 1) {
+    if (stripe < h) red[stripe][c] += red[stripe + h][c];
+    __syncthreads();
+  }
+  if (stripe == 0 && col < D) {
+    float* dst = which == 0 ? gw : (which == 1 ? gb : gms);
+    if (dst) dst[col] = (float)red[0][c];
+  }
 }
 
 __global__ void relu_bwd_kernel(int64_t n, const float* __restrict__ y, const float* __restrict__ gy,
@@ -188,6 +209,17 @@ __global__ void scale_by_kernel(int64_t n, const float* __restrict__ x, const fl
     y[i] = x[i] * a;
 }
 
+// Zero a pitched block of rows with 16-B vector stores (row_bytes, pitch and base 16-B aligned):
+// the runtime's 2-D memset ran at ~0.8 TB/s on Set2Set's [B, D] recurrent-state slices
+__global__ void fill_zero_2d_kernel(int64_t rows, int64_t row_vecs, int64_t pitch_vecs, float4* __restrict__ p) {
+  const int64_t total = rows * row_vecs;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / row_vecs;
+    p[r * pitch_vecs + (i - r * row_vecs)] = z;
+  }
+}
+
 }  // namespace
 }  // namespace mvml
 
@@ -228,7 +260,7 @@ extern "C" int mvml_graphnorm_bwd(int64_t G, int D, const int64_t* group_offsets
                                              part, G);
   int rc = check_launch("graphnorm_bwd_kernel");
   if (rc) return rc;
-  dim3 g2((unsigned)ceil_div(D, 256), 3);
+  dim3 g2((unsigned)ceil_div(D, 16), 3);
   graphnorm_param_reduce<<<g2, 256, 0, st>>>(D, G, part, g_weight, g_bias, g_mean_scale);
   return check_launch("graphnorm_param_reduce");
 }
@@ -279,6 +311,12 @@ extern "C" int mvml_fill_zero(void* p, int64_t rows, int64_t row_bytes, int64_t 
                "fill_zero: bad shape");
   if (rows == 0 || row_bytes == 0) return MVML_OK;
   hipStream_t st = as_stream(stream);
+  if (pitch_bytes != row_bytes && row_bytes % 16 == 0 && pitch_bytes % 16 == 0 && (uintptr_t)p % 16 == 0) {
+    const int64_t total = rows * (row_bytes / 16);
+    fill_zero_2d_kernel<<<(unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(total, 256), 8192)), 256, 0, st>>>(
+        rows, row_bytes / 16, pitch_bytes / 16, static_cast<float4*>(p));
+    return check_launch("fill_zero_2d_kernel");
+  }
   const hipError_t e = (pitch_bytes == row_bytes)
                            ? hipMemsetAsync(p, 0, (size_t)(rows * row_bytes), st)
                            : hipMemset2DAsync(p, (size_t)pitch_bytes, 0, (size_t)row_bytes, (size_t)rows, st);

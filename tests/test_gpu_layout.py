@@ -47,6 +47,14 @@ def test_fill_zero_contiguous_and_pitched():
     ref[:, 32:] = 0
     Fn.zero_(big[:, 32:])
     assert torch.equal(big, ref)
+    # the vector-store kernel (aligned pitched slices, Set2Set's recurrent-state columns at the
+    # bench's size: more rows than one grid sweep) and the runtime's 2-D memset (unaligned start)
+    for rows, cols, c0 in ((65536, 1152, 384), (50, 96, 33), (9, 8, 4)):
+        big = torch.randn(rows, cols, device=DEV)
+        ref = big.clone()
+        ref[:, c0:] = 0
+        Fn.zero_(big[:, c0:])
+        assert torch.equal(big, ref), (rows, cols, c0)
     z = Fn.zeros((3, 1000), dtype=torch.int32, device=DEV)
     assert z.dtype == torch.int32 and torch.count_nonzero(z) == 0
 

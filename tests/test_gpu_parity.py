@@ -287,6 +287,12 @@ def test_colsum():
     out = torch.ones(37, dtype=torch.float32, device=DEV)
     colsum(X.float().to(DEV), 5000, 37, 37, out, beta=1.0)
     assert rel_err(out, X.sum(0) + 1) < TOL
+    # tall: ~1 K row partials per column (the final pass's 16 stripes x 4 accumulators), a
+    # column count that is not a multiple of 16, alpha scaling
+    X = torch.randn(200003, 517, dtype=torch.float64)
+    out = torch.empty(517, dtype=torch.float32, device=DEV)
+    colsum(X.float().to(DEV), 200003, 517, 517, out, alpha=0.5)
+    assert rel_err(out, 0.5 * X.sum(0)) < TOL
 
 
 # ------------------------------------------------------------------ GAT layers
@@ -415,6 +421,33 @@ def test_graphnorm_parity():
     yp.backward(gy.float().to(DEV))
     assert rel_err(yp, yr) < TOL
     assert rel_err(xp.grad, xr.grad) < TOL
+    for a, r in ((gn.weight, w), (gn.bias, b), (gn.mean_scale, ms)):
+        assert rel_err(a.grad, r.grad) < TOL
+
+
+@pytest.mark.parametrize("G,D", [(1000, 100), (37, 768), (1, 20)])
+def test_graphnorm_param_reduce_many_groups(G, D):
+    """The parameter gradients' reduction over G group partials (16 stripes per column, a fixed
+    tree) at group counts around its stripe / unroll boundaries and a column count that is not a
+    multiple of 16, against float64."""
+    from mvml_gat.nn import GraphNorm
+    gen = torch.Generator().manual_seed(G + D)
+    sizes = torch.randint(1, 6, (G,), generator=gen)
+    offs = [0] + torch.cumsum(sizes, 0).tolist()
+    x = torch.randn(offs[-1], D, dtype=torch.float64, generator=gen) * 2 + 0.5
+    gn = GraphNorm(D)
+    with torch.no_grad():
+        gn.weight.add_(torch.randn(D, generator=gen) * 0.1)
+        gn.mean_scale.add_(torch.randn(D, generator=gen) * 0.1)
+    w, b, ms = (p.detach().double().requires_grad_() for p in (gn.weight, gn.bias, gn.mean_scale))
+    xr = x.clone().requires_grad_()
+    yr = gnn_ref.graphnorm_ref(xr, w, b, ms, 1e-5, offs)
+    gy = torch.randn(yr.shape, dtype=torch.float64, generator=gen)
+    yr.backward(gy)
+    gn = gn.to(DEV)
+    xp = x.float().to(DEV).requires_grad_()
+    yp = gn(xp, group_offsets=torch.tensor(offs, device=DEV))
+    yp.backward(gy.float().to(DEV))
     for a, r in ((gn.weight, w), (gn.bias, b), (gn.mean_scale, ms)):
         assert rel_err(a.grad, r.grad) < TOL
 
