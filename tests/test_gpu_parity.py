@@ -425,14 +425,17 @@ def test_graphnorm_parity():
         assert rel_err(a.grad, r.grad) < TOL
 
 
-@pytest.mark.parametrize("G,D", [(1000, 100), (37, 768), (1, 20)])
-def test_graphnorm_param_reduce_many_groups(G, D):
+@pytest.mark.parametrize("G,D,big", [(1000, 100, False), (37, 768, False), (1, 20, False), (6, 300, True)])
+def test_graphnorm_param_reduce_many_groups(G, D, big):
     """The parameter gradients' reduction over G group partials (16 stripes per column, a fixed
     tree) at group counts around its stripe / unroll boundaries and a column count that is not a
-    multiple of 16, against float64."""
+    multiple of 16, against float64.  big: groups of 63-130 rows, on both sides of the kernels'
+    64-row register path (longer groups re-read their rows)."""
     from mvml_gat.nn import GraphNorm
     gen = torch.Generator().manual_seed(G + D)
-    sizes = torch.randint(1, 6, (G,), generator=gen)
+    sizes = torch.randint(63, 131, (G,), generator=gen) if big else torch.randint(1, 6, (G,), generator=gen)
+    if big:
+        sizes[:3] = torch.tensor([64, 65, 63])
     offs = [0] + torch.cumsum(sizes, 0).tolist()
     x = torch.randn(offs[-1], D, dtype=torch.float64, generator=gen) * 2 + 0.5
     gn = GraphNorm(D)
@@ -448,6 +451,8 @@ def test_graphnorm_param_reduce_many_groups(G, D):
     xp = x.float().to(DEV).requires_grad_()
     yp = gn(xp, group_offsets=torch.tensor(offs, device=DEV))
     yp.backward(gy.float().to(DEV))
+    assert rel_err(yp, yr) < TOL
+    assert rel_err(xp.grad, xr.grad) < TOL
     for a, r in ((gn.weight, w), (gn.bias, b), (gn.mean_scale, ms)):
         assert rel_err(a.grad, r.grad) < TOL
 
