@@ -1854,7 +1854,7 @@ int absmax_launch(int64_t rows, int64_t cols, const float* P, int64_t ld, uint32
     return MVML_ERR_LAUNCH;
   }
   if (rows <= 0 || cols <= 0) return MVML_OK;
-  if ((ld == cols || rows == 1) && cols < 1024) {  // contiguous and narrow: flat pass
+  if (ld == cols || rows == 1) {  // contiguous: one flat pass (also bounds the atomics at ~1 K)
     const int64_t n = rows * cols;
     const int fvec = (n % 4 == 0) && ((uintptr_t)P % 16 == 0);
     const unsigned blocks =
