@@ -51,7 +51,8 @@ TIMED = ["mvml_gat_agg_fwd", "mvml_gat_agg_bwd", "mvml_gemm_f32", "mvml_gemm_f32
          "mvml_token_attn_fwd", "mvml_token_attn_bwd", "mvml_token_attn_fold_fwd",
          "mvml_token_attn_fold_bwd", "mvml_gemm_f32x3_batched", "mvml_conv3_fwd", "mvml_conv3_bwd",
          "mvml_bce_logits", "mvml_gat_attn_grad", "mvml_bilstm_seq_fwd", "mvml_bilstm_seq_bwd", "mvml_bilstm_wide_fwd", "mvml_bilstm_wide_bwd",
-         "mvml_lstm_gates_cell_fwd", "mvml_gemm_f16x2", "mvml_gemm_f16x2_amax", "mvml_absmax_f32",
+         "mvml_lstm_gates_cell_fwd", "mvml_gemm_f16x2", "mvml_gemm_f16x2_amax", "mvml_gemm_f16x2_amax_colsum",
+         "mvml_absmax_f32",
          "mvml_gemm_f16x2_bsplit", "mvml_attn_conv_fwd", "mvml_attn_conv_bwd",
          "mvml_bilstm_wide_step_fwd", "mvml_bilstm_wide_step_bwd", "mvml_bilstm_pack_rows",
          "mvml_bilstm_gather_rows", "mvml_bilstm_token_grad", "mvml_bilstm_select_last",
@@ -572,6 +573,7 @@ def run(args):
         if os.environ.get("MVML_GEMM_SHAPES") and rank == 0:
             gemm_shape_report(summ.get("mvml_gemm_f32x3", []) + summ.get("mvml_gemm_f32x3_batched", [])
                               + summ.get("mvml_gemm_f16x2", []) + summ.get("mvml_gemm_f16x2_amax", [])
+                              + summ.get("mvml_gemm_f16x2_amax_colsum", [])
                               + summ.get("mvml_gemm_f16x2_rows", [])
                               + summ.get("mvml_gemm_f16x2_bsplit", [])
                               + summ.get("mvml_gemm_f16x2_ex", []) + summ.get("mvml_gemm_f16x2_batched", [])
@@ -604,14 +606,16 @@ def run(args):
                 "gemm_smallk_kernel); bytes = A, B and C once")
         # layer 1's weight gradient (N = 76 columns: gY^T X over every atom, split-K) streams the
         # N x 1544 gradient rows once at 36 flop per byte: an HBM roofline of its own too
-        amax_ev = summ.get("mvml_gemm_f16x2_amax", [])
+        # (mvml_gemm_f16x2_amax_colsum: the same product with the bias column sums from its reads)
+        amax_ev = summ.get("mvml_gemm_f16x2_amax", []) + summ.get("mvml_gemm_f16x2_amax_colsum", [])
         dw_ev = [e for e in amax_ev if (e[1] or {}).get("role") == "gat_dw" and e[1]["shape"][1] <= 96]
         amax_ev = [e for e in amax_ev if e not in dw_ev]
         if dw_ev:
             extra["roofline_dw_l1"] = roofline_entry(dw_ev, "hbm", load_traffic(wkey, "gemm_dw_l1"))
             extra["roofline_dw_l1"]["kernel"] = (
-                "mvml_gemm_f16x2_amax for the layer-1 weight gradient gY[N, 1544]^T X[N, 76] (split-K "
-                "gemm_f32_kernel + splitk_reduce_kernel); bytes = gY's 1544 columns, X and dW once")
+                "mvml_gemm_f16x2_amax_colsum for the layer-1 weight gradient gY[N, 1544]^T X[N, 76] and "
+                "the bias column sums from the same reads (split-K gemm_f32_kernel + splitk_reduce_kernel "
+                "+ the row sums' final pass); bytes = gY's 1544 columns, X and dW once")
         gemm_ev = (summ.get("mvml_gemm_f32", []) + summ.get("mvml_gemm_f32x3", [])
                    + summ.get("mvml_gemm_f16x2", []) + amax_ev
                    + summ.get("mvml_gemm_f16x2_bsplit", []) + rows_ev
@@ -627,7 +631,8 @@ def run(args):
                 frac=round(extra["roofline_gemm_bf16"]["achieved"] / BF16_MFMA_PEAK_TFS, 4))
         if gemm_ev:
             extra["roofline_gemm"] = roofline_entry(gemm_ev, "mfma")
-            if (summ.get("mvml_gemm_f16x2") or summ.get("mvml_gemm_f16x2_amax") or summ.get("mvml_gemm_f16x2_bsplit")
+            if (summ.get("mvml_gemm_f16x2") or summ.get("mvml_gemm_f16x2_amax")
+                    or summ.get("mvml_gemm_f16x2_amax_colsum") or summ.get("mvml_gemm_f16x2_bsplit")
                     or summ.get("mvml_gemm_f16x2_rows") or summ.get("mvml_gemm_f16x2_ex")):
                 # scaled split-fp16: 3 fp16 MFMA per fp32 multiply-add -> fp32-equivalent peak
                 # 2.5 PF / 3 (the skinny products that fall back to split-bf16 count against it too)

@@ -294,6 +294,20 @@ int mvml_absmax_f32(int64_t rows, int64_t cols, const float* P, int64_t ld, uint
 size_t mvml_colsum_workspace_size(int64_t M, int64_t N);
 int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx, float alpha, float beta,
                     float* out, void* workspace, size_t workspace_bytes, void* stream);
+/* A weight gradient and the bias gradient of the same output gradient in one call (round 6):
+ *   C[M][N]    = A^T B^T, A [K][lda] and B [K][ldb] both k-major (mvml_gemm_f16x2_amax(1, 1, ...))
+ *   sum_out[c] = alpha * sum_k A[k][sum_off + c], c < sum_n (mvml_colsum_f32 over those columns)
+ * For a GATConv (autograd of gatconv.py's fc / res_fc / bias, model.py:79-81) A = gY, B = X:
+ * dL/dWcat and, over gY's residual columns, dL/dbias.  When mvml_gemm_colsum_fused(M, N, K)
+ * (the skinny 128x128 plan: layer 1, N = 76 atom features) the column sums come out of the
+ * fragments the product reads (fp32 adds, fixed order: deterministic, not the order of
+ * mvml_colsum_f32); otherwise the product then mvml_colsum_f32, bitwise the two calls. */
+int mvml_gemm_colsum_fused(int64_t M, int64_t N, int64_t K);
+size_t mvml_gemm_colsum_workspace_size(int64_t M, int64_t N, int64_t K, int64_t sum_n);
+int mvml_gemm_f16x2_amax_colsum(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
+                                int64_t ldb, const uint32_t* amax_a, const uint32_t* amax_b, float* C,
+                                int64_t ldc, int64_t sum_off, int64_t sum_n, float alpha, float* sum_out,
+                                void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * GATConv projection (dgl 0.9.1 GATConv.fc and res_fc, gatconv.py forward, homogeneous-graph

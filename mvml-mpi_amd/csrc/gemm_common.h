@@ -78,6 +78,9 @@ struct AmaxPtrs {
   const uint32_t* b = nullptr;
   int64_t b_plane = 0;  // BPS: elements from B's high fp16 plane to its low plane
   const uint32_t* a_rows = nullptr;
+  // gemm_f32_kernel<..., RS = true> (k-major A): fp32 sums over k of every op(A) row, as
+  // [2 S][M] partials (split s, wave column half h -> row 2 s + h); mvml_gemm_f16x2_amax_colsum
+  float* a_rowsum = nullptr;
 };
 
 // Scale shift of A row `row` (clamped into range: clamped rows feed outputs never stored).

@@ -408,7 +408,17 @@ __device__ __forceinline__ void unscale_rows(f32x16 (&acc)[2][2], bool per_row, 
 // kernel's NP = 2), the skinny products' plan when the algorithm is f16x2.
 // BPS (H2, K-contiguous B only): B is the interleaved pre-split of the operand
 // (split_f16x2_il_kernel), so the B fragments need no split.
-template <bool AK, bool BKM, int EPI_LOGW = -1, bool X3 = false, bool H2 = false, bool BPS = false>
+__device__ __forceinline__ float hsum8(const float4& a, const float4& b) {
+  return ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+}
+
+// RS (split-fp16, k-major A): the fp32 A fragments the waves read anyway are also summed over k
+// per A row (a weight gradient's A = gY^T: the bias gradient's column sums of gY come out of
+// the product's own reads).  Waves of column half wn sum 16-k step wn of every 32-k stage, the
+// two k halves of a row (lanes l, l + 32) are added once at the end, and every workgroup of the
+// first N tile writes its rows' partials to amax.a_rowsum[2 split + wn][row].
+template <bool AK, bool BKM, int EPI_LOGW = -1, bool X3 = false, bool H2 = false, bool BPS = false,
+          bool RS = false>
 __global__ void __launch_bounds__(kThreads, 2)
 gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
                 const float* __restrict__ B, int64_t ldb, const float* __restrict__ bias,
@@ -418,6 +428,7 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
                 CellEpi cep = CellEpi{}, DualPtrs dual = DualPtrs{}) {
   static_assert(!H2 || X3, "split-fp16 is a split product");
   static_assert(!BPS || (H2 && !BKM), "pre-split B: split-fp16, K-contiguous B");
+  static_assert(!RS || (H2 && AK), "row sums: split-fp16, k-major A");
   if (blockIdx.z) {  // strided batch
     A += blockIdx.z * bst.a;
     B += blockIdx.z * bst.b;
@@ -464,6 +475,8 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int li = lane & 31, lk = lane >> 5;
+  const bool rs_on = RS && amax.a_rowsum && gridDim.z == 1 && (tile % tiles_n) == 0;
+  float rs0 = 0.f, rs1 = 0.f;  // RS: this lane's k-half sums of A rows ra0 / ra1
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -546,6 +559,17 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (RS) {
+        if (rs_on) {  // wave-uniform: column half wn takes 16-k step wn
+          if (wn == 0) {
+            rs0 += hsum8(f[0][0][0], f[0][0][1]);
+            rs1 += hsum8(f[0][1][0], f[0][1][1]);
+          } else {
+            rs0 += hsum8(f[1][0][0], f[1][0][1]);
+            rs1 += hsum8(f[1][1][0], f[1][1][1]);
+          }
+        }
+      }
 #pragma unroll
       for (int T = 0; T < 2; ++T) {
         split2h8(f[T][0][0], f[T][0][1], s_a0, pa[0][0], pa[0][1]);
@@ -633,6 +657,18 @@ gemm_f32_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A, in
     }
   }
 
+  if constexpr (RS) {
+    if (rs_on) {
+      rs0 += __shfl_xor(rs0, 32, 64);  // + the other k half of the same rows
+      rs1 += __shfl_xor(rs1, 32, 64);
+      if (lk == 0) {
+        float* dst = amax.a_rowsum + (split * 2 + wn) * M;
+        const int64_t r = m0 + wm * 64 + li;
+        if (r < M) dst[r] = rs0;
+        if (r + 32 < M) dst[r + 32] = rs1;
+      }
+    }
+  }
   if constexpr (H2) unscale_rows(acc, amax.a_rows != nullptr, ka, ka0, ka1, kb, lane);
   if constexpr (H2 && EPI_LOGW < 0) {
     if (cep.D > 0) {  // LSTM cell epilogue through LDS (host: N = 4 D, no split-K)
@@ -1669,11 +1705,12 @@ __global__ void colsum_partial_kernel(int64_t M, int64_t N, const float* __restr
   part[(int64_t)blockIdx.y * N + col] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
-// out[col] = beta out[col] + alpha sum_z part[z][col]: a workgroup per 16 columns, 16 stripes of
+// out[col] = beta out[col] + alpha sum_z part[z ld + col]: a workgroup per 16 columns, 16 stripes of
 // the S partials per column (four accumulators each, loads in flight), a fixed-order LDS tree —
 // deterministic.  (A thread per column walking all S ~ 1024 partials took 20-70 us.)
 __global__ void __launch_bounds__(256) colsum_final_kernel(int64_t N, int S, const float* __restrict__ part,
-                                                           float alpha, float beta, float* __restrict__ out) {
+                                                           int64_t ld, float alpha, float beta,
+                                                           float* __restrict__ out) {
   const int c = threadIdx.x & 15, stripe = threadIdx.x >> 4;
   const int64_t col = (int64_t)blockIdx.x * 16 + c;
   float a[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1681,9 +1718,9 @@ __global__ void __launch_bounds__(256) colsum_final_kernel(int64_t N, int S, con
     int z = stripe;
     for (; z + 48 < S; z += 64) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] += part[(int64_t)(z + 16 * u) * N + col];
+      for (int u = 0; u < 4; ++u) a[u] += part[(int64_t)(z + 16 * u) * ld + col];
     }
-    for (; z < S; z += 16) a[0] += part[(int64_t)z * N + col];
+    for (; z < S; z += 16) a[0] += part[(int64_t)z * ld + col];
   }
   __shared__ float red[16][17];
   red[stripe][c] = (a[0] + a[1]) + (a[2] + a[3]);
@@ -2652,6 +2689,10 @@ int gemm_launch(int prec, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
     else if (plan.wide)                                                                         \
       gemm_x3w_kernel<AKV, BKV, -1, false><<<grid, kXThreads, 0, st>>>(                         \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst);  \
+    else if (hf && AKV && BKV && amax.a_rowsum) /* + A's row sums (host: AKV) */               \
+      gemm_f32_kernel<AKV, BKV, -1, true, true, false, AKV><<<grid, kThreads, 0, st>>>(         \
+          M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst,   \
+          amax);                                                                                \
     else if (hf && AKV && BKV) /* skinny, both k-major: split-fp16 fragment split */           \
       gemm_f32_kernel<AKV, BKV, -1, true, true><<<grid, kThreads, 0, st>>>(                     \
           M, N, K, A, lda, B, ldb, bias, beta, act, C, ldc, kc, slab, av, bv, ProjEpi{}, bst,   \
@@ -2780,8 +2821,64 @@ extern "C" int mvml_colsum_f32(int64_t M, int64_t N, const float* X, int64_t ldx
   float* part = static_cast<float*>(workspace);
   dim3 g1((unsigned)ceil_div(N, 256), (unsigned)S);
   colsum_partial_kernel<<<g1, 256, 0, st>>>(M, N, X, ldx, rows_per, part);
-  colsum_final_kernel<<<(unsigned)ceil_div(N, 16), 256, 0, st>>>(N, S, part, alpha, beta, out);
+  colsum_final_kernel<<<(unsigned)ceil_div(N, 16), 256, 0, st>>>(N, S, part, N, alpha, beta, out);
   return check_launch("colsum");
+}
+
+// ---- weight gradient + bias gradient from one read of the gradient ------------------------
+// C[M][N] = A^T B^T with both operands k-major (A = gY [K][lda]: a layer's weight gradient,
+// K = atoms) and sum_out[c] = alpha sum_k A[k][sum_off + c] (its bias gradient, the column sums
+// of gY).  Skinny products (the 128x128 split-fp16 plan: layer 1, N = 76) form the row sums
+// from the fragments the product reads anyway (gemm_f32_kernel RS); other plans run the
+// product and then mvml_colsum_f32 on the summed columns — the sequence this entry replaces.
+namespace {
+bool colsum_fused(int64_t M, int64_t N, int64_t K) {
+  return M > 0 && N > 0 && K > 0 && N <= XBN && !plan_gemm(kPrecF16x2, M, N, K).wide;
+}
+}  // namespace
+
+extern "C" int mvml_gemm_colsum_fused(int64_t M, int64_t N, int64_t K) { return colsum_fused(M, N, K) ? 1 : 0; }
+
+extern "C" size_t mvml_gemm_colsum_workspace_size(int64_t M, int64_t N, int64_t K, int64_t sum_n) {
+  const size_t parts = carve_size((size_t)2 * choose_splits(M, N, K) * std::max<int64_t>(M, 1) * sizeof(float));
+  return carve_size(mvml_gemm_workspace_size(M, N, K)) +
+         std::max(parts, mvml_colsum_workspace_size(K, std::max<int64_t>(sum_n, 1)));
+}
+
+extern "C" int mvml_gemm_f16x2_amax_colsum(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                                           const float* B, int64_t ldb, const uint32_t* amax_a,
+                                           const uint32_t* amax_b, float* C, int64_t ldc, int64_t sum_off,
+                                           int64_t sum_n, float alpha, float* sum_out, void* workspace,
+                                           size_t workspace_bytes, void* stream) {
+  clear_error();
+  MVML_REQUIRE(amax_a != nullptr && amax_b != nullptr, "gemm_f16x2_amax_colsum: amax_a / amax_b are required");
+  MVML_REQUIRE(M >= 0 && N >= 0 && K >= 0 && sum_off >= 0 && sum_n >= 0 && sum_off + sum_n <= M &&
+                   (sum_n == 0 || sum_out),
+               "gemm_f16x2_amax_colsum: bad shape");
+  if (!workspace || workspace_bytes < mvml_gemm_colsum_workspace_size(M, N, K, sum_n)) {
+    set_error("gemm_f16x2_amax_colsum: workspace too small (need %zu)",
+              mvml_gemm_colsum_workspace_size(M, N, K, sum_n));
+    return MVML_ERR_WORKSPACE;
+  }
+  const size_t gws = carve_size(mvml_gemm_workspace_size(M, N, K));
+  float* extra = reinterpret_cast<float*>(static_cast<uint8_t*>(workspace) + gws);
+  const size_t extra_bytes = workspace_bytes - gws;
+  hipStream_t st = as_stream(stream);
+  if (colsum_fused(M, N, K)) {
+    AmaxPtrs am{amax_a, amax_b};
+    am.a_rowsum = extra;
+    int rc = gemm_launch(kPrecF16x2, 1, 1, M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, workspace, gws,
+                         stream, 1, BatchStrides{}, am);
+    if (rc || sum_n == 0) return rc;
+    const int parts = 2 * plan_gemm(kPrecF16x2, M, N, K).S;
+    colsum_final_kernel<<<(unsigned)ceil_div(sum_n, 16), 256, 0, st>>>(sum_n, parts, extra + sum_off, M, alpha,
+                                                                       0.f, sum_out);
+    return check_launch("colsum_final_kernel(gemm row sums)");
+  }
+  int rc = gemm_launch(kPrecF16x2, 1, 1, M, N, K, A, lda, B, ldb, nullptr, 0.f, 0, C, ldc, workspace, gws, stream,
+                       1, BatchStrides{}, AmaxPtrs{amax_a, amax_b});
+  if (rc || sum_n == 0) return rc;
+  return mvml_colsum_f32(K, sum_n, A + sum_off, lda, alpha, 0.f, sum_out, extra, extra_bytes, stream);
 }
 
 // ---- wide-batch BiLSTM steps (MVP's RNNModule at B > 512; BASELINE config 4) ---------------

@@ -17,7 +17,7 @@ int64_t row_pitch(int64_t c) { return (c + 63) / 64 * 64; }  // functional._row_
 
 struct LayerBwdPlan {
   int64_t Fp, C, CE, ldg, outc;
-  size_t gy, gyr, amx, gW, wil, agg, gemm, colsum, total;
+  size_t gy, gyr, amx, gW, wil, agg, gemm, total;
 };
 
 LayerBwdPlan layer_bwd_plan(int64_t N, int64_t E, int H, int F, int Fin, int mean) {
@@ -39,8 +39,8 @@ LayerBwdPlan layer_bwd_plan(int64_t N, int64_t E, int H, int F, int Fin, int mea
   p.gW = take((size_t)p.CE * p.Fp * sizeof(float));
   p.wil = take((size_t)p.CE * p.Fp * sizeof(float));
   p.agg = take(mvml_gat_agg_bwd_workspace_size(E, H));
-  p.gemm = take(std::max(mvml_gemm_workspace_size(p.CE, p.Fp, N), mvml_gemm_workspace_size(N, Fin, p.CE)));
-  p.colsum = take(mvml_colsum_workspace_size(N, (int64_t)H * F));
+  p.gemm = take(std::max(mvml_gemm_colsum_workspace_size(p.CE, p.Fp, N, (int64_t)H * F),
+                         mvml_gemm_workspace_size(N, Fin, p.CE)));
   p.total = off;
   return p;
 }
@@ -101,26 +101,24 @@ extern "C" int mvml_gat_layer_bwd(int64_t N, const int32_t* node_groups, int64_t
                             ldy, elr, attn, out, g_out, H, F, slope, mode, gY, p.ldg, amx + 2,
                             g_X ? gyr : nullptr, ws + p.agg, mvml_gat_agg_bwd_workspace_size(num_edges, H),
                             stream));
-  // dL/d[Wcat ; A_l ; A_r] = gY^T X (split-K over atoms), unfolded into fc / res_fc
-  const size_t gws = std::max(mvml_gemm_workspace_size(p.CE, p.Fp, N), mvml_gemm_workspace_size(N, Fin, p.CE));
-  MVML_TRY(mvml_gemm_f16x2_amax(1, 1, p.CE, p.Fp, N, gY, p.ldg, X, p.Fp, amx + 2, amx + 0, nullptr, 0.f, 0, gW,
-                                p.Fp, ws + p.gemm, gws, stream));
+  // dL/d[Wcat ; A_l ; A_r] = gY^T X (split-K over atoms), unfolded into fc / res_fc; with it the
+  // bias gradient: column sums of g_rst = gY's residual columns (mean: g_out / H, the same for
+  // every head)
+  const size_t gws = std::max(mvml_gemm_colsum_workspace_size(p.CE, p.Fp, N, HF),
+                              mvml_gemm_workspace_size(N, Fin, p.CE));
+  MVML_TRY(mvml_gemm_f16x2_amax_colsum(p.CE, p.Fp, N, gY, p.ldg, X, p.Fp, amx + 2, amx + 0, gW, p.Fp, HF,
+                                       mean ? F : HF, mean ? 1.f / H : 1.f, g_bias, ws + p.gemm, gws, stream));
   MVML_TRY(mvml_gat_unfold_grads(gW, attn_lr, H, F, Fin, (int)p.Fp, mean ? 1 : 0, g_fc, g_res, stream));
   // attention vectors, re-associated: per head, rows [G_l ; G_r] of gW times its F rows of Wcat
   MVML_TRY(mvml_gemm_f32x3_batched(0, 0, 2, F, p.Fp, H, gW + p.C * p.Fp, (int64_t)H * p.Fp, p.Fp, Wcat, p.Fp,
                                    (int64_t)F * p.Fp, nullptr, 0.f, 0, g_attn, HF, F, stream));
-  // bias: column sums of g_rst (mean: g_out / H, the same for every head)
-  const size_t cws = mvml_colsum_workspace_size(N, HF);
   if (mean) {
-    MVML_TRY(mvml_colsum_f32(N, F, gY + HF, p.ldg, 1.f / H, 0.f, g_bias, ws + p.colsum, cws, stream));
     for (int h = 1; h < H; ++h)
       if (hipMemcpyAsync(g_bias + (int64_t)h * F, g_bias, F * sizeof(float), hipMemcpyDeviceToDevice, st) !=
           hipSuccess) {
         set_error("gat_layer_bwd: hipMemcpyAsync failed");
         return MVML_ERR_LAUNCH;
       }
-  } else {
-    MVML_TRY(mvml_colsum_f32(N, HF, gY + HF, p.ldg, 1.f, 0.f, g_bias, ws + p.colsum, cws, stream));
   }
   // dL/dX = gY Wcat, every atom's row at its own scale, Wcat from its interleaved image
   if (g_X) {

@@ -557,10 +557,24 @@ class GATLayerFunction(torch.autograd.Function):
             DEBUG_CAPTURE.setdefault("gy_amax", []).append((gY[:, :CE].clone(), amx[2:3].clone()))
             if gyr is not None:
                 DEBUG_CAPTURE.setdefault("gy_rows", []).append(gyr.clone())
-        # dL/d[Wcat ; A_l ; A_r] = gY^T X  (split-K over atoms)
+        # dL/d[Wcat ; A_l ; A_r] = gY^T X  (split-K over atoms); the bias gradient is the column
+        # sums of gY's residual columns (g_rst; mean: g_out / H for every head), formed with it
+        # where the product's own reads can (mvml_gemm_f16x2_amax_colsum: layer 1)
         gW = torch.empty((CE, Fp), dtype=torch.float32, device=dev)
-        gemm(gY, Xp, CE, Fp, N, 1, 1, ldg, Fp, gW, Fp, algo=ctx.algo,
-             amax=None if amx is None else (slot(amx, 2), slot(*ctx.ax)), role="gat_dw")
+        g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
+        bias_done = False
+        if amx is not None and (ctx.algo or GEMM_ALGO) == "f16x2" and COLSUM_FUSED and \
+                L.mvml_gemm_colsum_fused(CE, Fp, N):
+            sum_n = F if mean_res else HF
+            _lib.call_tag[0] = {"flops": 2 * CE * Fp * N, "shape": (CE, Fp, N, 1, 1),
+                                "bytes": 4 * (CE * Fp + CE * N + Fp * N), "role": "gat_dw"}
+            wp, wn = _lib.ws_ptr_size(L.mvml_gemm_colsum_workspace_size(CE, Fp, N, sum_n), dev)
+            call("mvml_gemm_f16x2_amax_colsum", CE, Fp, N, ptr(gY), ldg, ptr(Xp), Fp, slot(amx, 2),
+                 slot(*ctx.ax), ptr(gW), Fp, HF, sum_n, 1.0 / H if mean_res else 1.0, ptr(g_bias), wp, wn, st)
+            bias_done = True
+        else:
+            gemm(gY, Xp, CE, Fp, N, 1, 1, ldg, Fp, gW, Fp, algo=ctx.algo,
+                 amax=None if amx is None else (slot(amx, 2), slot(*ctx.ax)), role="gat_dw")
         g_fc = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         g_res = torch.empty((HF, Fin), dtype=torch.float32, device=dev)
         call("mvml_gat_unfold_grads", ptr(gW), ptr(attn_lr), H, F, Fin, Fp, mean_res, ptr(g_fc),
@@ -576,11 +590,11 @@ class GATLayerFunction(torch.autograd.Function):
         g_ar = g_alr[1].view_as(attn_r)
         if DEBUG_CAPTURE is not None:
             DEBUG_CAPTURE.update(elr=elr, gelr=gelr, attn=attn)
-        g_bias = torch.empty((HF,), dtype=torch.float32, device=dev)
         if mean_res:  # every head's bias sees g_out / H: one column sum, replicated over heads
-            colsum(gY, N, F, ldg, g_bias, offset=HF, alpha=1.0 / H)
+            if not bias_done:
+                colsum(gY, N, F, ldg, g_bias, offset=HF, alpha=1.0 / H)
             copy2d(g_bias.view(H, F)[1:], g_bias[:F].view(1, F).expand(H - 1, F))
-        else:
+        elif not bias_done:
             colsum(gY, N, HF, ldg, g_bias, offset=HF)
         gX = None
         if ctx.needs_input_grad[0]:
@@ -602,6 +616,11 @@ class GATLayerFunction(torch.autograd.Function):
                 gemm(gY, Wcat, N, Fin, CE, 0, 1, ldg, Fp, gX, Fin, algo=ctx.algo,
                      amax=None if amx is None else (slot(amx, 2), slot(amx, 1)))
         return gX, g_fc, g_res, g_al, g_ar, g_bias, None, None, None, None, None, None
+
+
+# GAT layer weight + bias gradients from one read of gY where the product's plan allows
+# (mvml_gemm_f16x2_amax_colsum); MVML_COLSUM_FUSED=0: the product, then a column-sum pass
+COLSUM_FUSED = os.environ.get("MVML_COLSUM_FUSED", "1") != "0"
 
 
 # Set2Set's gates GEMM + LSTM cell as one launch (mvml_lstm_gates_cell_fwd: the cell in the
